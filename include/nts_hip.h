@@ -1,0 +1,225 @@
+/*
+ * nts_hip.h — C-ABI of the MI355X (gfx950) sampled-GNN hot path.
+ *
+ * This is the drop-in boundary: a plain-C interface (raw device pointers,
+ * sizes, status codes; no torch types) that replaces the hot subset of the
+ * reference's `Cuda_Stream` device layer (cuda/ntsCUDA.hpp:177-595) and its
+ * NCCL wrapper (cuda/ntsCUDA.hpp:132-175).  Every entry point below names
+ * the reference interface it replaces (file:line in AiX-im/Sample-based-GNN).
+ *
+ * Conventions
+ *  - Vertex ids are uint32 (VertexId, dep/gemini/type.hpp:29; cuda/cuda_type.h:21).
+ *  - Global CSC offsets are uint64 (the reference uses uint32 and overflows
+ *    past 2^32 edges); per-batch sampled offsets are uint32.
+ *  - Values are fp32 (ValueType, dep/gemini/type.hpp:31).
+ *  - Sizes that are only known on the device (e_size, src_size of a sampled
+ *    layer) are passed as device scalars plus a host-side capacity; kernels
+ *    read the live size and never touch entries past it.  No entry point
+ *    synchronises with the host.
+ *  - All work is enqueued on the context's stream (async); buffers are owned
+ *    by the caller.  Return value 0 = success; on failure the message is
+ *    available from nts_hip_last_error() (thread-local).  The reference
+ *    aborts instead (CHECK_CUDA_RESULT, cuda/ntsCUDAGraphOP.cu:21-28); the
+ *    C++ host layer reproduces abort-on-error by throwing.
+ *  - A context is re-entrant per stream and holds no global mutable state
+ *    (unlike Cuda_Stream::total_*, cuda/ntsCUDAGraphOP.cu:64-66).
+ */
+#ifndef NTS_HIP_H
+#define NTS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NTS_HIP_ABI_VERSION 1
+
+/* status codes */
+#define NTS_OK 0
+#define NTS_ERR_INVALID 1
+#define NTS_ERR_HIP 2
+#define NTS_ERR_OOM 3
+#define NTS_ERR_UNSUPPORTED 4
+#define NTS_ERR_RCCL 5
+
+/* Random stream used by the sampler.
+ *  PHILOX          : counter-based Philox4x32-10 keyed by (seed), counter
+ *                    (word block, dst id, layer, batch_seq) — every dst is
+ *                    independent, fully parallel (the fast default).
+ *  MT19937_LEMIRE  : the reference's stream, bit-exact: one
+ *                    `static thread_local std::mt19937 generator(seed)`
+ *                    consumed sequentially by std::uniform_int_distribution
+ *                    (core/ntsFastSampler.hpp:200-205) in libstdc++ >= 11 form
+ *                    (Lemire nearly-divisionless, uniform_int_dist.h:246-263).
+ *  MT19937_DIV     : same stream, libstdc++ <= 10 form (2-division rejection).
+ * The MT modes consume one generator shared by all layers/batches of a
+ * context, exactly like the reference's thread_local generator. */
+#define NTS_RNG_PHILOX 0
+#define NTS_RNG_MT19937_LEMIRE 1
+#define NTS_RNG_MT19937_DIV 2
+
+/* Edge weights, mirrors `enum class WeightType{Sum, Mean, None}`
+ * (core/ntsFastSampler.hpp:27) with the CPU sampler's formulas
+ * (core/ntsFastSampler.hpp:1111-1119, nts_norm_degree core/ntsBaseOp.hpp:652-657). */
+#define NTS_WEIGHT_SUM 0
+#define NTS_WEIGHT_MEAN 1
+#define NTS_WEIGHT_NONE 2
+
+typedef struct nts_hip_ctx nts_hip_ctx;
+typedef struct nts_hip_comm nts_hip_comm;
+
+/* Replicated global graph resident in HBM (FullyRepGraph, core/FullyRepGraph.hpp:682-798
+ * + Graph degrees core/graph.hpp:1157-1186,1420-1425,4525-4530). */
+typedef struct {
+  uint64_t n_vertices;
+  uint64_t n_edges;
+  const uint64_t *column_offset; /* [V+1] CSC keyed by dst                         */
+  const uint32_t *row_indices;   /* [E] src ids, file order within each dst        */
+  const uint32_t *in_degree;     /* [V] in_degree_for_backward  (clamped >= 1)     */
+  const uint32_t *out_degree;    /* [V] out_degree_for_backward (clamped >= 1)     */
+} nts_graph_dev;
+
+/* One sampled layer (sampCSC, core/coocsc.hpp:417-460), device side.
+ * Inputs: destination + v_size.  Everything else is written by
+ * nts_hip_sample_layer.  CSR arrays may be NULL (no transpose built). */
+typedef struct {
+  uint32_t v_cap, e_cap, s_cap;    /* host capacities of the arrays below       */
+  const uint32_t *destination;     /* [v_cap] global dst ids (input)           */
+  const uint32_t *v_size;          /* device scalar: live dst count (input)    */
+  uint32_t *column_offset;         /* [v_cap+1] local CSC offsets              */
+  uint32_t *row_indices;           /* [e_cap] local src ids                    */
+  uint32_t *sample_ans;            /* [e_cap] global src ids (sample_ans)      */
+  uint32_t *edge_dst;              /* [e_cap] local dst of each edge (COO)     */
+  uint32_t *source;                /* [s_cap] global src ids, ascending        */
+  float *edge_weight_forward;      /* [e_cap] CSC order (NULL iff WEIGHT_NONE) */
+  uint32_t *row_offset;            /* [s_cap+1] CSR offsets, or NULL           */
+  uint32_t *column_indices;        /* [e_cap] CSR local dst ids, or NULL       */
+  float *edge_weight_backward;     /* [e_cap] CSR order, or NULL               */
+  uint32_t *sizes;                 /* device [4]: v_size, e_size, src_size,
+                                      overflow flag (nonzero = a capacity was
+                                      exceeded and the layer is truncated)     */
+} nts_sampcsc_dev;
+
+/* ---- context ------------------------------------------------------------ */
+int nts_hip_abi_version(void);
+const char *nts_hip_last_error(void);
+/* Replaces `new Cuda_Stream()` (cuda/ntsCUDAGraphOP.cu:201-212).  stream may be
+ * NULL (a non-blocking stream is created and owned).  seed feeds PHILOX and
+ * the MT19937 generator (reference: 2000, core/ntsFastSampler.hpp:202). */
+int nts_hip_ctx_create(nts_hip_ctx **ctx, int device, void *stream, uint64_t seed);
+int nts_hip_ctx_destroy(nts_hip_ctx *ctx);
+/* Cuda_Stream::setNewStream (cuda/ntsCUDA.hpp:188). */
+int nts_hip_ctx_set_stream(nts_hip_ctx *ctx, void *stream);
+void *nts_hip_ctx_get_stream(nts_hip_ctx *ctx);
+/* Pre-size the scratch arena so no allocation happens inside the hot loop
+ * (keeps every call graph-capturable).  n_vertices: |V| of the graph;
+ * max_items: largest e_cap / v_cap that will be passed. */
+int nts_hip_ctx_reserve(nts_hip_ctx *ctx, uint64_t n_vertices, uint64_t max_items);
+/* Re-seed the MT19937 state (std::mt19937(seed)).  Enqueued on the stream. */
+int nts_hip_rng_seed(nts_hip_ctx *ctx, uint64_t seed);
+/* Copy the MT19937 state (624 words + position) to host; synchronises. */
+int nts_hip_rng_state(nts_hip_ctx *ctx, uint32_t *host_state625);
+
+/* ---- graph preprocessing ----------------------------------------------- */
+/* Degrees from an edge list, clamped to >= 1:
+ * Graph::load_directed (core/graph.hpp:1157-1186 out, :1420-1425 in) +
+ * generate_backward_structure clamp (core/graph.hpp:4525-4530). */
+int nts_hip_degrees(nts_hip_ctx *ctx, const uint32_t *src, const uint32_t *dst,
+                    uint64_t n_edges, uint64_t n_vertices, uint32_t *out_degree,
+                    uint32_t *in_degree);
+/* Global CSC keyed by dst, src ids in edge-list (file) order within each dst:
+ * FullyRepGraph::ReadRepGraphFromRawFile (core/FullyRepGraph.hpp:724-798). */
+int nts_hip_build_csc(nts_hip_ctx *ctx, const uint32_t *src, const uint32_t *dst,
+                      uint64_t n_edges, uint64_t n_vertices, uint64_t *column_offset,
+                      uint32_t *row_indices);
+
+/* ---- sampler ------------------------------------------------------------ */
+/* One hop of FastSampler::sample_fast / sample_gpu_fast
+ * (core/ntsFastSampler.hpp:962-1140, :648-709):
+ *   num_d = min(deg(d), fanout) (fanout < 0: all), draw num_d distinct
+ *   neighbour positions by rejection (deg > fanout) or take all in CSC order,
+ *   frontier = distinct sampled ids in ascending global order (source),
+ *   row_indices relabelled to local ids, CSR transpose (csc_to_csr,
+ *   core/coocsc.hpp:82-111, stable = ascending dst) and edge weights
+ *   (WeightCompute, core/coocsc.hpp:301-324).  Replaces
+ *   sample_processing_get_co_gpu + sample_processing_traverse_gpu +
+ *   sample_processing_update_ri_gpu + GetWeight (cuda/ntsCUDAGraphOP.cu:1246-1700).
+ * batch_seq/layer key the PHILOX stream; MT modes ignore them. */
+int nts_hip_sample_layer(nts_hip_ctx *ctx, const nts_graph_dev *graph, int fanout,
+                         int layer, uint64_t batch_seq, int rng_mode, int weight_type,
+                         nts_sampcsc_dev *out);
+
+/* ---- feature / label movement ------------------------------------------- */
+/* out[i,:] = table[index[i],:] for i < *n (n == NULL: n_cap rows).
+ * Replaces zero_copy_feature_move_gpu (cuda/ntsCUDAGraphOP.cu:1711-1729) and
+ * nts::op::get_feature (core/ntsMiniBatchGraphOp.hpp:45-60); the table is
+ * HBM-resident instead of pinned host memory; 64-bit row offsets. */
+int nts_hip_gather_rows(nts_hip_ctx *ctx, const float *table, uint64_t ld_table,
+                        const uint32_t *index, const uint32_t *n, uint32_t n_cap,
+                        uint32_t feature_size, float *out, uint64_t ld_out);
+/* out[i] = labels[index[i]]: global_copy_label_move_gpu (cuda/ntsCUDAGraphOP.cu,
+ * kernel cuda/ntsCUDATransferKernel.cuh:203-212) / get_label (core/ntsMiniBatchGraphOp.hpp:36-43). */
+int nts_hip_gather_labels(nts_hip_ctx *ctx, const int64_t *labels, const uint32_t *index,
+                          const uint32_t *n, uint32_t n_cap, int64_t *out);
+
+/* ---- sampled aggregation ------------------------------------------------ */
+/* Y[d,:] = sum_{e in [co[d],co[d+1])} w[e] * X[row(e),:], summed in CSC edge
+ * order as (x*w)+acc with no FMA contraction — the exact arithmetic of
+ * MiniBatchFuseOp::forward / nts_comp (core/ntsMiniBatchGraphOp.hpp:153-182,
+ * core/ntsBaseOp.hpp:546-562).  row(e) = row_indices[e], or
+ * x_row_map[row_indices[e]] when x_row_map != NULL (fused feature gather:
+ * X is then the global feature table and x_row_map the layer's `source`).
+ * Every row d < *v is written (no pre-zeroing needed).  Replaces
+ * Gather_By_Dst_From_Src(_Spmm) (cuda/ntsCUDAGraphOP.cu:340-373,425-587). */
+int nts_hip_spmm_csc_fwd(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                         const uint32_t *row_indices, const float *weight,
+                         const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
+                         const uint32_t *x_row_map, uint32_t feature_size, float *y,
+                         uint64_t ldy);
+/* G_in[s,:] = sum_{j in [ro[s],ro[s+1])} w_b[j] * G_out[ci[j],:] (ascending dst
+ * order, deterministic, atomic-free).  Replaces Gather_By_Src_From_Dst_Spmm
+ * (cuda/ntsCUDAGraphOP.cu:901-1042) and MiniBatchFuseOp::backward
+ * (core/ntsMiniBatchGraphOp.hpp:214-268). */
+int nts_hip_spmm_csr_bwd(nts_hip_ctx *ctx, const uint32_t *row_offset,
+                         const uint32_t *column_indices, const float *weight_backward,
+                         const uint32_t *s, uint32_t s_cap, const float *g_out,
+                         uint64_t ld_gout, uint32_t feature_size, float *g_in,
+                         uint64_t ld_gin);
+/* G_in[row_indices[e],:] += w[e] * G_out[d,:] with float atomics over the CSC
+ * (g_in must be zeroed by the caller; summation order is not deterministic).
+ * Replaces Push_From_Dst_To_Src_Spmm (cuda/ntsCUDAGraphOP.cu:621-770). */
+int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                                const uint32_t *row_indices, const float *weight,
+                                const uint32_t *v, uint32_t v_cap, const float *g_out,
+                                uint64_t ld_gout, uint32_t feature_size, float *g_in,
+                                uint64_t ld_gin);
+
+/* ---- optimiser ---------------------------------------------------------- */
+/* Fused Adam step on one parameter (n elements), element-wise identical to
+ *  bias_correction != 0: Parameter::learnC2C_with_decay_Adam (core/NtsScheduler.hpp:863-880)
+ *  bias_correction == 0: Parameter::learn_local_with_decay_Adam (core/NtsScheduler.hpp:937-945)
+ * beta1_t/beta2_t are the running powers kept by Parameter::next(). */
+int nts_hip_adam(nts_hip_ctx *ctx, float *w, const float *grad, float *m, float *v,
+                 uint64_t n, float alpha, float beta1, float beta2, float epsilon,
+                 float weight_decay, float beta1_t, float beta2_t, int bias_correction);
+
+/* ---- RCCL over xGMI (replaces NCCL_Communicator, cuda/ntsCUDA.hpp:132-175,
+ *      cuda/ntsCUDAGraphOP.cu:173-200) --------------------------------------- */
+int nts_hip_comm_unique_id(uint8_t out_id[128]);
+/* One communicator per process/GPU (ncclCommInitRank) instead of the
+ * reference's single-process ncclCommInitAll clique. */
+int nts_hip_comm_init(nts_hip_comm **comm, int nranks, int rank, const uint8_t id[128],
+                      int device);
+int nts_hip_comm_destroy(nts_hip_comm *comm);
+/* In-place float SUM all-reduce (NCCL_Communicator::AllReduce, cuda/ntsCUDAGraphOP.cu:180-186). */
+int nts_hip_allreduce_sum_f32(nts_hip_comm *comm, float *buf, uint64_t count, void *stream);
+/* In-place broadcast from root (NCCL_Communicator::Bcast, cuda/ntsCUDAGraphOP.cu:188-193). */
+int nts_hip_broadcast_f32(nts_hip_comm *comm, float *buf, uint64_t count, int root,
+                          void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NTS_HIP_H */

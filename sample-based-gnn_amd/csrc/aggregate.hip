@@ -1,0 +1,386 @@
+// Sampled aggregation (CSC gather SpMM, CSR transpose gather, atomic scatter),
+// row/label gathers and the fused Adam step.
+//
+// The aggregation is HBM-bound (~2 flop/B).  Layout: X/Y row-major
+// fp32 [rows, ld]; one wave-group (LPD lanes) per destination row, each lane
+// owning NCH vectors of VEC floats of the row; neighbour rows are fetched 4
+// edges ahead so every lane keeps 4*NCH independent loads in flight.  The sum
+// runs in CSC edge order as acc + x*w with contraction disabled: bit-identical
+// to the reference's MiniBatchFuseOp/nts_comp (core/ntsBaseOp.hpp:546-562,
+// `_mm256_add_ps(_mm256_mul_ps(source,w),destination)`) for the same sampCSC.
+#include "common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace nts_hip {
+
+template <int VEC>
+struct VT;
+template <>
+struct VT<1> {
+  using T = float;
+  __device__ static __forceinline__ T zero() { return 0.f; }
+  __device__ static __forceinline__ T madd(T a, T x, float w) { return a + x * w; }
+  __device__ static __forceinline__ T scale(T x, float w) { return x * w; }
+};
+template <>
+struct VT<2> {
+  using T = float2;
+  __device__ static __forceinline__ T zero() { return make_float2(0.f, 0.f); }
+  __device__ static __forceinline__ T madd(T a, T x, float w) {
+    return make_float2(a.x + x.x * w, a.y + x.y * w);
+  }
+  __device__ static __forceinline__ T scale(T x, float w) { return make_float2(x.x * w, x.y * w); }
+};
+template <>
+struct VT<4> {
+  using T = float4;
+  __device__ static __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ static __forceinline__ T madd(T a, T x, float w) {
+    return make_float4(a.x + x.x * w, a.y + x.y * w, a.z + x.z * w, a.w + x.w * w);
+  }
+  __device__ static __forceinline__ T scale(T x, float w) {
+    return make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
+  }
+};
+
+constexpr int kAggThreads = 256;
+constexpr int kUnroll = 4;
+
+// y[d, :] = sum_{e in [off[d], off[d+1])} w[e] * x[row(e), :]
+// row(e) = MAP ? map[idx[e]] : idx[e];  w == nullptr -> weight 1.
+template <int VEC, int LPD, int NCH, bool MAP>
+__global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
+    const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
+    const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t nv,
+    float* __restrict__ y, uint64_t ldy) {
+  using V = VT<VEC>;
+  using T = typename V::T;
+  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  constexpr int GPB = kAggThreads / LPD;
+  const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
+  for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
+    const uint32_t beg = off[d], end = off[d + 1];
+    T* yrow = reinterpret_cast<T*>(y + (uint64_t)d * ldy);
+    for (uint32_t c0 = 0; c0 < nv; c0 += LPD * NCH) {
+      T acc[NCH];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
+      uint32_t e = beg;
+      for (; e + kUnroll <= end; e += kUnroll) {
+        uint32_t r[kUnroll];
+        float ww[kUnroll];
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) {
+          r[j] = idx[e + j];
+          ww[j] = w ? w[e + j] : 1.0f;
+        }
+        if (MAP) {
+#pragma unroll
+          for (int j = 0; j < kUnroll; ++j) r[j] = map[r[j]];
+        }
+        T xv[kUnroll][NCH];
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) {
+          const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r[j] * ldx);
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            const uint32_t col = c0 + sl + c * LPD;
+            xv[j][c] = (col < nv) ? xrow[col] : V::zero();
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j)
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
+      }
+      for (; e < end; ++e) {
+        uint32_t r = idx[e];
+        const float we = w ? w[e] : 1.0f;
+        if (MAP) r = map[r];
+        const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r * ldx);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = c0 + sl + c * LPD;
+          if (col < nv) acc[c] = V::madd(acc[c], xrow[col], we);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const uint32_t col = c0 + sl + c * LPD;
+        if (col < nv) yrow[col] = acc[c];
+      }
+    }
+  }
+}
+
+// g_in[idx[e], :] += w[e] * g_out[d, :]   (float atomics, order not deterministic)
+template <int VEC, int LPD>
+__global__ __launch_bounds__(kAggThreads) void k_spmm_scatter_atomic(
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
+    const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
+    const float* __restrict__ g, uint64_t ldg, uint32_t nv, float* __restrict__ gin,
+    uint64_t ldgi) {
+  using V = VT<VEC>;
+  using T = typename V::T;
+  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  constexpr int GPB = kAggThreads / LPD;
+  const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
+  for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
+    const uint32_t beg = off[d], end = off[d + 1];
+    const T* grow = reinterpret_cast<const T*>(g + (uint64_t)d * ldg);
+    for (uint32_t col = sl; col < nv; col += LPD) {
+      const T gv = grow[col];
+      for (uint32_t e = beg; e < end; ++e) {
+        const float we = w ? w[e] : 1.0f;
+        const T v = V::scale(gv, we);
+        float* dst = gin + (uint64_t)idx[e] * ldgi + (uint64_t)col * VEC;
+        const float* vs = reinterpret_cast<const float*>(&v);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) unsafeAtomicAdd(dst + k, vs[k]);
+      }
+    }
+  }
+}
+
+template <int VEC, int LPD>
+__global__ __launch_bounds__(kAggThreads) void k_gather_rows(const float* __restrict__ table,
+                                                            uint64_t ldt,
+                                                            const uint32_t* __restrict__ index,
+                                                            const uint32_t* n_dev, uint32_t n_cap,
+                                                            uint32_t nv, float* __restrict__ out,
+                                                            uint64_t ldo) {
+  using T = typename VT<VEC>::T;
+  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  constexpr int GPB = kAggThreads / LPD;
+  const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
+  for (uint32_t i = blockIdx.x * GPB + grp; i < n; i += gridDim.x * GPB) {
+    const T* src = reinterpret_cast<const T*>(table + (uint64_t)index[i] * ldt);
+    T* dst = reinterpret_cast<T*>(out + (uint64_t)i * ldo);
+    for (uint32_t c = sl; c < nv; c += LPD) dst[c] = src[c];
+  }
+}
+
+__global__ void k_gather_labels(const int64_t* __restrict__ labels,
+                                const uint32_t* __restrict__ index, const uint32_t* n_dev,
+                                uint32_t n_cap, int64_t* __restrict__ out) {
+  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    out[i] = labels[index[i]];
+}
+
+// Adam, element-wise in the exact operation order of the reference's torch
+// expressions (core/NtsScheduler.hpp:863-880 and :937-945).
+__global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float* __restrict__ M,
+                       float* __restrict__ Vv, uint64_t n, float alpha, float beta1, float beta2,
+                       float eps, float wd, float beta1_t, float beta2_t, int bias_correction) {
+  const float omb1 = 1.0f - beta1, omb2 = 1.0f - beta2;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const float w = W[i];
+    if (bias_correction) {
+      // W_g = W_gradient + weight_decay * S
+      const float wg = G[i] + wd * w;
+      const float m = beta1 * M[i] + omb1 * wg;
+      const float v = beta2 * Vv[i] + omb2 * (wg * wg);
+      M[i] = m;
+      Vv[i] = v;
+      const float mt = m / (1.0f - beta1_t);
+      const float vt = v / (1.0f - beta2_t);
+      W[i] = w - (alpha * mt) / (sqrtf(vt) + eps);
+    } else {
+      // W_g = W * weight_decay + W.grad();  V = b2*V + (1-b2)*W_g*W_g
+      const float wg = w * wd + G[i];
+      const float m = beta1 * M[i] + omb1 * wg;
+      const float v = beta2 * Vv[i] + (omb2 * wg) * wg;
+      M[i] = m;
+      Vv[i] = v;
+      W[i] = w - (alpha * m) / (sqrtf(v) + eps);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dispatch
+// ---------------------------------------------------------------------------
+static int pick_vec(uint32_t F, uint64_t ld1, uint64_t ld2, const void* p1, const void* p2) {
+  auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p % a) == 0; };
+  if (F % 4 == 0 && ld1 % 4 == 0 && ld2 % 4 == 0 && al(p1, 16) && al(p2, 16)) return 4;
+  if (F % 2 == 0 && ld1 % 2 == 0 && ld2 % 2 == 0 && al(p1, 8) && al(p2, 8)) return 2;
+  return 1;
+}
+
+struct Shape {
+  int lpd, nch;
+};
+static Shape pick_shape(uint32_t nv) {
+  if (nv <= 8) return {8, 1};
+  if (nv <= 16) return {16, 1};
+  if (nv <= 32) return {32, 1};
+  if (nv <= 64) return {64, 1};
+  uint32_t nch = (nv + 63) / 64;
+  return {64, (int)std::min<uint32_t>(nch, 8)};
+}
+
+template <int VEC, bool MAP>
+static int launch_gather_vec(hipStream_t st, uint32_t grid, Shape s, const uint32_t* off,
+                             const uint32_t* idx, const float* w, const uint32_t* n_dev,
+                             uint32_t n_cap, const float* x, uint64_t ldx, const uint32_t* map,
+                             uint32_t nv, float* y, uint64_t ldy) {
+#define NTS_G(LPD, NCH)                                                                    \
+  hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP>), dim3(grid), dim3(kAggThreads), 0, \
+                     st, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy)
+  if (s.lpd == 8) NTS_G(8, 1);
+  else if (s.lpd == 16) NTS_G(16, 1);
+  else if (s.lpd == 32) NTS_G(32, 1);
+  else switch (s.nch) {
+      case 1: NTS_G(64, 1); break;
+      case 2: NTS_G(64, 2); break;
+      case 3: NTS_G(64, 3); break;
+      case 4: NTS_G(64, 4); break;
+      case 5: NTS_G(64, 5); break;
+      case 6: NTS_G(64, 6); break;
+      case 7: NTS_G(64, 7); break;
+      default: NTS_G(64, 8); break;
+    }
+#undef NTS_G
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+template <bool MAP>
+static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
+                         const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
+                         uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy) {
+  const int vec = pick_vec(F, ldx, ldy, x, y);
+  const uint32_t nv = F / vec;
+  const Shape s = pick_shape(nv);
+  const uint32_t gpb = kAggThreads / s.lpd;
+  // enough waves to saturate HBM: 256 CUs x 16 waves, grid-stride beyond
+  const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), 4096u));
+  if (vec == 4)
+    return launch_gather_vec<4, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
+  if (vec == 2)
+    return launch_gather_vec<2, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
+  return launch_gather_vec<1, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
+}
+
+}  // namespace nts_hip
+
+using namespace nts_hip;
+
+extern "C" {
+
+int nts_hip_spmm_csc_fwd(nts_hip_ctx* ctx, const uint32_t* column_offset,
+                         const uint32_t* row_indices, const float* weight, const uint32_t* v,
+                         uint32_t v_cap, const float* x, uint64_t ldx,
+                         const uint32_t* x_row_map, uint32_t feature_size, float* y,
+                         uint64_t ldy) {
+  NTS_CHECK_ARG(ctx && column_offset && row_indices && x && y, "NULL argument");
+  NTS_CHECK_ARG(ldx >= feature_size && ldy >= feature_size, "leading dimension < feature_size");
+  if (v_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  if (x_row_map)
+    return launch_gather<true>(ctx->stream, column_offset, row_indices, weight, v, v_cap, x, ldx,
+                               x_row_map, feature_size, y, ldy);
+  return launch_gather<false>(ctx->stream, column_offset, row_indices, weight, v, v_cap, x, ldx,
+                              nullptr, feature_size, y, ldy);
+}
+
+int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
+                         const uint32_t* column_indices, const float* weight_backward,
+                         const uint32_t* s, uint32_t s_cap, const float* g_out, uint64_t ld_gout,
+                         uint32_t feature_size, float* g_in, uint64_t ld_gin) {
+  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && g_in, "NULL argument");
+  NTS_CHECK_ARG(ld_gout >= feature_size && ld_gin >= feature_size,
+                "leading dimension < feature_size");
+  if (s_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  return launch_gather<false>(ctx->stream, row_offset, column_indices, weight_backward, s, s_cap,
+                              g_out, ld_gout, nullptr, feature_size, g_in, ld_gin);
+}
+
+int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx* ctx, const uint32_t* column_offset,
+                                const uint32_t* row_indices, const float* weight,
+                                const uint32_t* v, uint32_t v_cap, const float* g_out,
+                                uint64_t ld_gout, uint32_t feature_size, float* g_in,
+                                uint64_t ld_gin) {
+  NTS_CHECK_ARG(ctx && column_offset && row_indices && g_out && g_in, "NULL argument");
+  NTS_CHECK_ARG(ld_gout >= feature_size && ld_gin >= feature_size,
+                "leading dimension < feature_size");
+  if (v_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const int vec = pick_vec(feature_size, ld_gout, ld_gin, g_out, g_in);
+  const uint32_t nv = feature_size / vec;
+  const int lpd = nv <= 16 ? 16 : (nv <= 32 ? 32 : 64);
+  const uint32_t grid = std::max(1u, std::min(ceil_div(v_cap, kAggThreads / lpd), 4096u));
+#define NTS_S(VEC, LPD)                                                                    \
+  hipLaunchKernelGGL((k_spmm_scatter_atomic<VEC, LPD>), dim3(grid), dim3(kAggThreads), 0,   \
+                     ctx->stream, column_offset, row_indices, weight, v, v_cap, g_out, ld_gout, \
+                     nv, g_in, ld_gin)
+  if (vec == 4) {
+    if (lpd == 16) NTS_S(4, 16); else if (lpd == 32) NTS_S(4, 32); else NTS_S(4, 64);
+  } else if (vec == 2) {
+    if (lpd == 16) NTS_S(2, 16); else if (lpd == 32) NTS_S(2, 32); else NTS_S(2, 64);
+  } else {
+    if (lpd == 16) NTS_S(1, 16); else if (lpd == 32) NTS_S(1, 32); else NTS_S(1, 64);
+  }
+#undef NTS_S
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+int nts_hip_gather_rows(nts_hip_ctx* ctx, const float* table, uint64_t ld_table,
+                        const uint32_t* index, const uint32_t* n, uint32_t n_cap,
+                        uint32_t feature_size, float* out, uint64_t ld_out) {
+  NTS_CHECK_ARG(ctx && table && index && out, "NULL argument");
+  NTS_CHECK_ARG(ld_table >= feature_size && ld_out >= feature_size,
+                "leading dimension < feature_size");
+  if (n_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const int vec = pick_vec(feature_size, ld_table, ld_out, table, out);
+  const uint32_t nv = feature_size / vec;
+  const int lpd = nv <= 16 ? 16 : (nv <= 32 ? 32 : 64);
+  const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, kAggThreads / lpd), 4096u));
+#define NTS_R(VEC, LPD)                                                                      \
+  hipLaunchKernelGGL((k_gather_rows<VEC, LPD>), dim3(grid), dim3(kAggThreads), 0, ctx->stream, \
+                     table, ld_table, index, n, n_cap, nv, out, ld_out)
+  if (vec == 4) {
+    if (lpd == 16) NTS_R(4, 16); else if (lpd == 32) NTS_R(4, 32); else NTS_R(4, 64);
+  } else if (vec == 2) {
+    if (lpd == 16) NTS_R(2, 16); else if (lpd == 32) NTS_R(2, 32); else NTS_R(2, 64);
+  } else {
+    if (lpd == 16) NTS_R(1, 16); else if (lpd == 32) NTS_R(1, 32); else NTS_R(1, 64);
+  }
+#undef NTS_R
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+int nts_hip_gather_labels(nts_hip_ctx* ctx, const int64_t* labels, const uint32_t* index,
+                          const uint32_t* n, uint32_t n_cap, int64_t* out) {
+  NTS_CHECK_ARG(ctx && labels && index && out, "NULL argument");
+  if (n_cap == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, 256), kMaxGrid));
+  hipLaunchKernelGGL(k_gather_labels, dim3(grid), dim3(256), 0, ctx->stream, labels, index, n,
+                     n_cap, out);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+int nts_hip_adam(nts_hip_ctx* ctx, float* w, const float* grad, float* m, float* v, uint64_t n,
+                 float alpha, float beta1, float beta2, float epsilon, float weight_decay,
+                 float beta1_t, float beta2_t, int bias_correction) {
+  NTS_CHECK_ARG(ctx && w && grad && m && v, "NULL argument");
+  if (n == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const uint32_t grid = std::max(1u, std::min(ceil_div(n, 256), kMaxGrid));
+  hipLaunchKernelGGL(k_adam, dim3(grid), dim3(256), 0, ctx->stream, w, grad, m, v, n, alpha,
+                     beta1, beta2, epsilon, weight_decay, beta1_t, beta2_t, bias_correction);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+}  // extern "C"

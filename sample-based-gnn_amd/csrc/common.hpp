@@ -1,0 +1,104 @@
+// Internal helpers shared by the HIP translation units of libnts_hip.so.
+// Not part of the C-ABI (see include/nts_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "nts_hip.h"
+
+namespace nts_hip {
+
+// ---- error plumbing (thread-local message, status codes) -----------------
+void set_error(const char* fmt, ...);
+
+#define NTS_HIP_TRY(expr)                                                        \
+  do {                                                                           \
+    hipError_t _e = (expr);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      ::nts_hip::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #expr,    \
+                           hipGetErrorString(_e));                               \
+      return NTS_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+#define NTS_CHECK_ARG(cond, msg)                                                 \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      ::nts_hip::set_error("%s: invalid argument: %s", __func__, msg);          \
+      return NTS_ERR_INVALID;                                                    \
+    }                                                                            \
+  } while (0)
+
+#define NTS_LAUNCH_CHECK()                                                       \
+  do {                                                                           \
+    hipError_t _e = hipGetLastError();                                           \
+    if (_e != hipSuccess) {                                                      \
+      ::nts_hip::set_error("%s:%d: kernel launch failed: %s", __FILE__, __LINE__, \
+                           hipGetErrorString(_e));                               \
+      return NTS_ERR_HIP;                                                        \
+    }                                                                            \
+  } while (0)
+
+#define NTS_RET(expr)                                                            \
+  do {                                                                           \
+    int _r = (expr);                                                             \
+    if (_r != NTS_OK) return _r;                                                 \
+  } while (0)
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+inline uint32_t ceil_log2(uint64_t x) {
+  uint32_t b = 0;
+  while ((uint64_t(1) << b) < x) ++b;
+  return b;
+}
+
+// Memory-bound grid cap: 256 CUs x 8 blocks of 256 threads (guide G11).
+constexpr uint32_t kMaxGrid = 2048;
+
+}  // namespace nts_hip
+
+// ---- context ---------------------------------------------------------------
+struct nts_hip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  uint64_t seed = 2000;
+  // Scratch arena (grown by nts_hip_ctx_reserve / on demand).
+  uint8_t* marks = nullptr;        // [V] frontier byte map
+  uint32_t* src_index = nullptr;   // [V] global -> local id of the current layer
+  uint64_t v_cap = 0;
+  void* scratch = nullptr;         // scans / radix sort temporaries
+  size_t scratch_bytes = 0;
+  uint32_t* mt_state = nullptr;    // 624 words + position (device)
+};
+
+namespace nts_hip {
+// Ensure scratch capacity (may allocate: call nts_hip_ctx_reserve up front
+// to keep the hot loop allocation-free).
+int ensure_vertices(nts_hip_ctx* ctx, uint64_t n_vertices);
+int ensure_scratch(nts_hip_ctx* ctx, size_t bytes);
+
+// Exclusive scan of n items (n = *n_dev, or n_cap when n_dev == nullptr):
+// out[i] = sum(in[0..i)) for i in [0, n]; out must hold n_cap+1 entries.
+// In-place (in == out) is allowed.  tmp must hold scan_tmp_elems(n_cap).
+template <typename T>
+int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T* tmp,
+                   hipStream_t stream);
+template <typename T>
+size_t scan_tmp_elems(uint64_t n_cap);
+
+// Stable LSD radix sort of (key, value) pairs on the low `bits` key bits.
+// n = *n_dev (or n_cap).  vals_in == nullptr means values = 0..n-1.
+// Result lands in keys_out/vals_out.  tmp: radix_tmp_bytes(n_cap).
+int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
+                     uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap,
+                     uint32_t bits, void* tmp, hipStream_t stream);
+size_t radix_tmp_bytes(uint64_t n_cap);
+}  // namespace nts_hip

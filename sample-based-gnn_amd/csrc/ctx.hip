@@ -1,0 +1,152 @@
+// Context, error plumbing and scratch arena of libnts_hip.so.
+// Replaces the reference's Cuda_Stream object lifetime (cuda/ntsCUDAGraphOP.cu:201-212)
+// and its per-subgraph GPU arena (core/FullyRepGraph.hpp:113-121).
+#include <cstdarg>
+#include <vector>
+
+#include "common.hpp"
+
+namespace nts_hip {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int ensure_vertices(nts_hip_ctx* ctx, uint64_t n_vertices) {
+  if (n_vertices <= ctx->v_cap) return NTS_OK;
+  if (ctx->marks) NTS_HIP_TRY(hipFree(ctx->marks));
+  if (ctx->src_index) NTS_HIP_TRY(hipFree(ctx->src_index));
+  ctx->marks = nullptr;
+  ctx->src_index = nullptr;
+  // marks are scanned 16 bytes per lane: pad to a multiple of 4096.
+  uint64_t padded = (n_vertices + 4095) / 4096 * 4096;
+  NTS_HIP_TRY(hipMalloc(&ctx->marks, padded));
+  NTS_HIP_TRY(hipMemset(ctx->marks, 0, padded));
+  NTS_HIP_TRY(hipMalloc(&ctx->src_index, n_vertices * sizeof(uint32_t)));
+  ctx->v_cap = n_vertices;
+  return NTS_OK;
+}
+
+int ensure_scratch(nts_hip_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return NTS_OK;
+  // Growing the arena must not race with in-flight kernels using it.
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (ctx->scratch) NTS_HIP_TRY(hipFree(ctx->scratch));
+  ctx->scratch = nullptr;
+  size_t b = bytes + bytes / 4;
+  NTS_HIP_TRY(hipMalloc(&ctx->scratch, b));
+  ctx->scratch_bytes = b;
+  return NTS_OK;
+}
+
+// std::mt19937 seeding (init_genrand): sequential, done on the host.
+static void mt_seed_host(uint64_t seed, uint32_t* st) {
+  st[0] = (uint32_t)seed;
+  for (int i = 1; i < 624; ++i)
+    st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
+  st[624] = 624;  // position: next call twists
+}
+
+}  // namespace nts_hip
+
+using namespace nts_hip;
+
+extern "C" {
+
+int nts_hip_abi_version(void) { return NTS_HIP_ABI_VERSION; }
+
+const char* nts_hip_last_error(void) { return g_err; }
+
+int nts_hip_ctx_create(nts_hip_ctx** out, int device, void* stream, uint64_t seed) {
+  NTS_CHECK_ARG(out != nullptr, "out is NULL");
+  *out = nullptr;
+  NTS_HIP_TRY(hipSetDevice(device));
+  nts_hip_ctx* ctx = new nts_hip_ctx();
+  ctx->device = device;
+  ctx->seed = seed;
+  if (stream) {
+    ctx->stream = (hipStream_t)stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      set_error("hipStreamCreateWithFlags: %s", hipGetErrorString(e));
+      delete ctx;
+      return NTS_ERR_HIP;
+    }
+    ctx->own_stream = true;
+  }
+  hipError_t e = hipMalloc(&ctx->mt_state, 625 * sizeof(uint32_t));
+  if (e != hipSuccess) {
+    set_error("hipMalloc(mt_state): %s", hipGetErrorString(e));
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return NTS_ERR_HIP;
+  }
+  *out = ctx;
+  return nts_hip_rng_seed(ctx, seed);
+}
+
+int nts_hip_ctx_destroy(nts_hip_ctx* ctx) {
+  if (!ctx) return NTS_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->marks) (void)hipFree(ctx->marks);
+  if (ctx->src_index) (void)hipFree(ctx->src_index);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->mt_state) (void)hipFree(ctx->mt_state);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return NTS_OK;
+}
+
+int nts_hip_ctx_set_stream(nts_hip_ctx* ctx, void* stream) {
+  NTS_CHECK_ARG(ctx && stream, "ctx/stream is NULL");
+  if (ctx->own_stream) {
+    NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    NTS_HIP_TRY(hipStreamDestroy(ctx->stream));
+    ctx->own_stream = false;
+  }
+  ctx->stream = (hipStream_t)stream;
+  return NTS_OK;
+}
+
+void* nts_hip_ctx_get_stream(nts_hip_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int nts_hip_ctx_reserve(nts_hip_ctx* ctx, uint64_t n_vertices, uint64_t max_items) {
+  NTS_CHECK_ARG(ctx, "ctx is NULL");
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  NTS_RET(ensure_vertices(ctx, n_vertices));
+  uint64_t items = max_items > n_vertices ? max_items : n_vertices;
+  size_t need = radix_tmp_bytes(items);
+  size_t s64 = scan_tmp_elems<uint64_t>(items + 1) * sizeof(uint64_t) + 256;
+  if (s64 > need) need = s64;
+  return ensure_scratch(ctx, need);
+}
+
+int nts_hip_rng_seed(nts_hip_ctx* ctx, uint64_t seed) {
+  NTS_CHECK_ARG(ctx, "ctx is NULL");
+  std::vector<uint32_t> st(625);
+  mt_seed_host(seed, st.data());
+  ctx->seed = seed;
+  // Synchronous copy from pageable memory is safe w.r.t. the host vector's
+  // lifetime; order it after prior work on the stream first.
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  NTS_HIP_TRY(hipMemcpy(ctx->mt_state, st.data(), 625 * sizeof(uint32_t),
+                        hipMemcpyHostToDevice));
+  return NTS_OK;
+}
+
+int nts_hip_rng_state(nts_hip_ctx* ctx, uint32_t* host_state625) {
+  NTS_CHECK_ARG(ctx && host_state625, "NULL argument");
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  NTS_HIP_TRY(hipMemcpy(host_state625, ctx->mt_state, 625 * sizeof(uint32_t),
+                        hipMemcpyDeviceToHost));
+  return NTS_OK;
+}
+
+}  // extern "C"

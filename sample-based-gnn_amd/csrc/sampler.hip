@@ -1,0 +1,569 @@
+// Multi-hop neighbour sampler, one hop per call, entirely on the device.
+//
+// Reference semantics (CPU FastSampler::sample_fast, core/ntsFastSampler.hpp:962-1140):
+//   per dst d:  num = min(deg(d), fanout)  (fanout < 0 -> deg)      init_co_only (FullyRepGraph.hpp:530-539)
+//               deg > fanout : draw uniform positions in [0,deg) by rejection until
+//                              `num` distinct ones (unordered_map, :1026-1038)
+//               else         : take every neighbour in CSC order (:1040-1048)
+//   frontier  : bitmap of sampled ids scanned in ascending order -> `source`,
+//               src_index (:1064-1083); row_indices relabelled (:1085-1099)
+//   csc_to_csr (core/coocsc.hpp:82-111), WeightCompute (core/coocsc.hpp:301-324)
+//
+// MI355X design:
+//   * one wave per destination; the copy path is a coalesced 64-lane stride,
+//     the rejection path draws up to 64 candidates per round and resolves
+//     "first `num` distinct in draw order" with ballots (no hash map),
+//   * PHILOX mode: every dst owns an independent counter-based stream -> fully
+//     parallel and deterministic; MT19937 modes replay the reference's single
+//     sequential generator with one wave (bit-exact neighbour sets),
+//   * frontier dedup = byte map + popcount scan over V/4096 tiles: ascending
+//     `source` without the reference GPU path's O(V) atomics (stage3,
+//     cuda/ntsCUDATransferKernel.cuh:1107-1125) and without host round trips,
+//   * CSR transpose = stable radix sort of (local src, edge id) -> identical to
+//     the reference's serial fill order (ascending dst), atomic-free.
+#include "common.hpp"
+
+namespace nts_hip {
+
+constexpr int kSelThreads = 256;
+constexpr int kSelWaves = kSelThreads / kWave;
+constexpr int kSetCap = 1024;  // max fanout of the rejection path
+
+// ---------------------------------------------------------------------------
+// random words
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += W0;
+    k.y += W1;
+  }
+  return c;
+}
+
+// Word `idx` of the PHILOX stream of (dst, layer, batch_seq).
+__device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint32_t dst, uint32_t layer,
+                                                uint64_t batch_seq, uint32_t idx) {
+  uint4 c = make_uint4(idx >> 2, dst, layer, (uint32_t)batch_seq);
+  uint2 k = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32) ^ (uint32_t)(batch_seq >> 32));
+  uint4 r = philox4x32_10(c, k);
+  uint32_t j = idx & 3u;
+  return j == 0 ? r.x : (j == 1 ? r.y : (j == 2 ? r.z : r.w));
+}
+
+// uniform_int_distribution<int>(0, range-1) acceptance test for one 32-bit word.
+// Lemire (libstdc++ >= 11, uniform_int_dist.h:246-263): a word is rejected iff
+// low32(x*range) < (-range) % range; accepted words yield high32(x*range).
+// DIV (libstdc++ <= 10): scaling = 0xFFFFFFFF/range, reject x >= range*scaling,
+// value = x / scaling.
+struct Draw {
+  uint32_t range, thr, scaling, past;
+  bool lemire;
+  __device__ __forceinline__ void init(uint32_t r, bool lem) {
+    range = r;
+    lemire = lem;
+    thr = (0u - r) % r;
+    scaling = 0xFFFFFFFFu / r;
+    past = r * scaling;
+  }
+  __device__ __forceinline__ bool apply(uint32_t x, uint32_t& v) const {
+    if (lemire) {
+      uint64_t m = (uint64_t)x * range;
+      v = (uint32_t)(m >> 32);
+      return (uint32_t)m >= thr;
+    }
+    v = x / scaling;
+    return x < past;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// per-layer kernels
+// ---------------------------------------------------------------------------
+__global__ void k_count(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
+                        const uint32_t* v_in, uint32_t v_cap, int fanout,
+                        uint32_t* __restrict__ co, uint32_t* sizes) {
+  const uint32_t v_req = *v_in;
+  const uint32_t v = min(v_req, v_cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    sizes[0] = v;
+    sizes[3] = (v_req > v_cap) ? 1u : 0u;
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < v; i += gridDim.x * blockDim.x) {
+    uint32_t d = dst[i];
+    uint32_t deg = (uint32_t)(goff[d + 1] - goff[d]);
+    co[i] = (fanout < 0) ? deg : min(deg, (uint32_t)fanout);
+  }
+}
+
+__global__ void k_finish_count(const uint32_t* co, uint32_t e_cap, uint32_t* sizes) {
+  uint32_t e = co[sizes[0]];
+  sizes[1] = min(e, e_cap);
+  if (e > e_cap) sizes[3] = 1u;
+}
+
+struct SelectArgs {
+  const uint64_t* goff;
+  const uint32_t* grows;
+  const uint32_t* dst;
+  const uint32_t* co;
+  const uint32_t* sizes;
+  uint32_t* ans;
+  uint32_t* edst;
+  uint8_t* marks;
+  uint32_t e_cap;
+  int fanout;
+  uint32_t layer;
+  uint64_t batch_seq;
+  uint64_t seed;
+};
+
+// Copy path: all neighbours of dst i in CSC order (coalesced stride).
+__device__ __forceinline__ void copy_all(const SelectArgs& a, uint32_t i, uint64_t beg,
+                                         uint32_t deg, uint32_t c, int lane) {
+  for (uint32_t k = lane; k < deg; k += kWave) {
+    uint32_t g = a.grows[beg + k];
+    a.ans[c + k] = g;
+    a.edst[c + k] = i;
+    a.marks[g] = 1;
+  }
+}
+
+// Rejection path: the first `need` distinct accepted draws, in draw order.
+// `word(j)` returns the j-th word of this dst's stream.  Returns words consumed.
+template <typename WordFn>
+__device__ __forceinline__ uint32_t select_distinct(const SelectArgs& a, uint32_t i,
+                                                    uint64_t beg, uint32_t deg, uint32_t need,
+                                                    uint32_t c, int lane, uint32_t* set,
+                                                    const Draw& dr, WordFn word) {
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t count = 0, consumed = 0;
+  while (count < need) {
+    const uint32_t remaining = need - count;
+    // round width: fewer candidates when few are missing (cheaper dedup)
+    const int R = remaining <= 12 ? 16 : (remaining <= 28 ? 32 : 64);
+    uint32_t val = 0;
+    bool ok = false;
+    if (lane < R) ok = dr.apply(word(consumed + lane), val);
+    bool dup = false;
+    for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);  // LDS broadcast reads
+    const uint64_t okmask = __ballot(ok);
+    for (int j = 0; j < R; ++j) {
+      uint32_t vj = __shfl(val, j, kWave);
+      dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
+    }
+    const bool isnew = ok && !dup;
+    const uint64_t newmask = __ballot(isnew);
+    const uint32_t nnew = __popcll(newmask);
+    uint64_t take = newmask;
+    if (nnew >= remaining) {
+      // keep the first `remaining` new lanes; the stream is consumed up to the last one
+      uint64_t m = newmask;
+      for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+      const int last = __ffsll((long long)m) - 1;
+      take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
+      consumed += (uint32_t)last + 1u;
+    } else {
+      consumed += (uint32_t)R;
+    }
+    if ((take >> lane) & 1ull) {
+      const uint32_t slot = count + (uint32_t)__popcll(take & lt_mask);
+      set[slot] = val;
+      const uint32_t pos = c + slot;
+      const uint32_t g = a.grows[beg + val];
+      a.ans[pos] = g;
+      a.edst[pos] = i;
+      a.marks[g] = 1;
+    }
+    count += (uint32_t)__popcll(take);
+    __builtin_amdgcn_wave_barrier();
+  }
+  return consumed;
+}
+
+// PHILOX: one wave per destination, grid-stride.
+__global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
+  __shared__ uint32_t sets[kSelWaves][kSetCap];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t v = a.sizes[0];
+  uint32_t* set = sets[w];
+  const uint32_t nw = gridDim.x * kSelWaves;
+  for (uint32_t i = blockIdx.x * kSelWaves + w; i < v; i += nw) {
+    const uint32_t d = a.dst[i];
+    const uint64_t beg = a.goff[d];
+    const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
+    const uint32_t c = a.co[i];
+    const uint32_t n = a.co[i + 1] - c;
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged in k_finish_count)
+    if (n == deg) {
+      copy_all(a, i, beg, deg, c, lane);
+    } else if (n > 0) {
+      Draw dr;
+      dr.init(deg, true);
+      const uint64_t seed = a.seed;
+      const uint32_t layer = a.layer;
+      const uint64_t bs = a.batch_seq;
+      select_distinct(a, i, beg, deg, n, c, lane, set, dr, [&](uint32_t j) {
+        return philox_word(seed, d, layer, bs, j);
+      });
+    }
+  }
+}
+
+// ---- MT19937 (reference stream) -------------------------------------------
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+// nxt = twist(cur), libstdc++ _M_gen_rand order, 64 lanes, chunk by chunk
+// (each chunk only depends on earlier chunks since m - n = -227 < -64).
+__device__ __forceinline__ void mt_twist(const uint32_t* cur, uint32_t* nxt, int lane) {
+  const uint32_t U = 0x80000000u, L = 0x7fffffffu, A = 0x9908b0dfu;
+  for (int base = 0; base < 624; base += kWave) {
+    const int k = base + lane;
+    if (k < 624) {
+      uint32_t x1 = (k < 623) ? cur[k + 1] : nxt[0];
+      uint32_t y = (cur[k] & U) | (x1 & L);
+      uint32_t src = (k < 227) ? cur[k + 397] : nxt[k - 227];
+      nxt[k] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    __syncthreads();
+  }
+}
+
+// One wave replays the reference's sequential generator over all dsts in order.
+// blk[cur] is the current 624-word block (std::mt19937::_M_x) and q0 the read
+// position in it (_M_p); blk[cur^1] is the next block, twisted on demand.
+__global__ __launch_bounds__(kWave) void k_select_mt(SelectArgs a, uint32_t* mt_state,
+                                                     int lemire) {
+  __shared__ uint32_t blk[2][624];
+  __shared__ uint32_t set[kSetCap];
+  const int lane = threadIdx.x;
+  for (int k = lane; k < 624; k += kWave) blk[0][k] = mt_state[k];
+  uint32_t q0 = mt_state[624];
+  int cur = 0;
+  bool have_next = false;
+  __syncthreads();
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t v = a.sizes[0];
+  for (uint32_t i = 0; i < v; ++i) {
+    const uint32_t d = a.dst[i];
+    const uint64_t beg = a.goff[d];
+    const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
+    const uint32_t c = a.co[i];
+    const uint32_t n = a.co[i + 1] - c;
+    if (c + n > a.e_cap) continue;
+    if (n == deg) {  // deg <= fanout: no draws (core/ntsFastSampler.hpp:1040-1048)
+      copy_all(a, i, beg, deg, c, lane);
+      continue;
+    }
+    if (n == 0) continue;
+    Draw dr;
+    dr.init(deg, lemire != 0);
+    uint32_t count = 0;
+    while (count < n) {
+      if (q0 + kWave > 624 && !have_next) {
+        mt_twist(blk[cur], blk[cur ^ 1], lane);
+        have_next = true;
+      }
+      if (q0 >= 624) {  // window slides: next block becomes current
+        cur ^= 1;
+        q0 -= 624;
+        have_next = false;
+        continue;
+      }
+      const uint32_t remaining = n - count;
+      const int R = remaining <= 12 ? 16 : (remaining <= 28 ? 32 : 64);
+      uint32_t val = 0;
+      bool ok = false;
+      if (lane < R) {
+        const uint32_t q = q0 + lane;
+        const uint32_t x = q < 624 ? mt_temper(blk[cur][q]) : mt_temper(blk[cur ^ 1][q - 624]);
+        ok = dr.apply(x, val);
+      }
+      bool dup = false;
+      for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
+      const uint64_t okmask = __ballot(ok);
+      for (int j = 0; j < R; ++j) {
+        uint32_t vj = __shfl(val, j, kWave);
+        dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
+      }
+      const bool isnew = ok && !dup;
+      const uint64_t newmask = __ballot(isnew);
+      const uint32_t nnew = __popcll(newmask);
+      uint64_t take = newmask;
+      if (nnew >= remaining) {
+        uint64_t m = newmask;
+        for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+        const int last = __ffsll((long long)m) - 1;
+        take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
+        q0 += (uint32_t)last + 1u;
+      } else {
+        q0 += (uint32_t)R;
+      }
+      if ((take >> lane) & 1ull) {
+        const uint32_t slot = count + (uint32_t)__popcll(take & lt_mask);
+        set[slot] = val;
+        const uint32_t pos = c + slot;
+        const uint32_t g = a.grows[beg + val];
+        a.ans[pos] = g;
+        a.edst[pos] = i;
+        a.marks[g] = 1;
+      }
+      count += (uint32_t)__popcll(take);
+      __syncthreads();
+    }
+  }
+  if (q0 >= 624 && have_next) {
+    cur ^= 1;
+    q0 -= 624;
+  }
+  __syncthreads();
+  // persist generator state: std::mt19937 keeps (_M_x = current block, _M_p)
+  for (int k = lane; k < 624; k += kWave) mt_state[k] = blk[cur][k];
+  if (lane == 0) mt_state[624] = q0;
+}
+
+// ---- frontier compaction --------------------------------------------------
+constexpr int kMarkThreads = 256;
+constexpr int kMarkTile = kMarkThreads * 16;  // 4096 vertices per block
+
+__device__ __forceinline__ uint32_t count16(uint4 m) {
+  // marks are 0/1 bytes -> popcount of each word counts set bytes
+  return __popc(m.x) + __popc(m.y) + __popc(m.z) + __popc(m.w);
+}
+
+__global__ __launch_bounds__(kMarkThreads) void k_mark_count(const uint8_t* __restrict__ marks,
+                                                             uint32_t* blk) {
+  const uint4 m = reinterpret_cast<const uint4*>(marks)[(uint64_t)blockIdx.x * kMarkThreads +
+                                                        threadIdx.x];
+  uint32_t c = count16(m);
+  // wave reduce + block reduce
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, kWave);
+  __shared__ uint32_t ws[kMarkThreads / kWave];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int i = 0; i < kMarkThreads / kWave; ++i) s += ws[i];
+    blk[blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(kMarkThreads) void k_mark_write(
+    const uint8_t* __restrict__ marks, const uint32_t* __restrict__ blk_off, uint32_t nblk,
+    uint64_t n_vertices, uint32_t s_cap, uint32_t* __restrict__ source,
+    uint32_t* __restrict__ src_index, uint32_t* sizes) {
+  const uint64_t tid = (uint64_t)blockIdx.x * kMarkThreads + threadIdx.x;
+  const uint4 m = reinterpret_cast<const uint4*>(marks)[tid];
+  const uint32_t c = count16(m);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    uint32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  __shared__ uint32_t ws[kMarkThreads / kWave];
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t off = blk_off[blockIdx.x];
+  for (int i = 0; i < w; ++i) off += ws[i];
+  uint32_t pos = off + inc - c;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t s = blk_off[nblk];
+    sizes[2] = min(s, s_cap);
+    if (s > s_cap) atomicOr(&sizes[3], 2u);
+  }
+  if (c == 0) return;
+  const uint32_t words[4] = {m.x, m.y, m.z, m.w};
+  const uint64_t v0 = tid * 16;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if ((words[q] >> (8 * b)) & 0xffu) {
+        const uint64_t vtx = v0 + q * 4 + b;
+        if (vtx < n_vertices && pos < s_cap) {
+          source[pos] = (uint32_t)vtx;
+          src_index[vtx] = pos;
+        }
+        ++pos;
+      }
+    }
+  }
+}
+
+// ---- relabel + weights ------------------------------------------------------
+__device__ __forceinline__ float norm_degree(uint32_t out_src, uint32_t in_dst) {
+  // 1 / ((float)std::sqrt(out) * (float)std::sqrt(in)), nts_norm_degree
+  // (core/ntsBaseOp.hpp:652-657): std::sqrt of an integer is the double sqrt.
+  const float a = (float)sqrt((double)out_src);
+  const float b = (float)sqrt((double)in_dst);
+  return 1.0f / (a * b);
+}
+
+__global__ void k_relabel(const uint32_t* __restrict__ ans, const uint32_t* __restrict__ edst,
+                          const uint32_t* __restrict__ dst, const uint32_t* __restrict__ src_index,
+                          const uint32_t* __restrict__ out_deg, const uint32_t* __restrict__ in_deg,
+                          const uint32_t* sizes, int weight_type, uint32_t* __restrict__ ri,
+                          float* __restrict__ wf) {
+  const uint32_t e = sizes[1];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x) {
+    const uint32_t g = ans[k];
+    ri[k] = src_index[g];
+    if (weight_type != NTS_WEIGHT_NONE) {
+      const uint32_t dg = dst[edst[k]];
+      const uint32_t ind = in_deg[dg];
+      float w = norm_degree(out_deg[g], ind);
+      if (weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
+      wf[k] = w;
+    }
+  }
+}
+
+// ---- CSR from sorted (local src, edge id) ----------------------------------
+__global__ void k_csr_finalize(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ seid,
+                               const uint32_t* __restrict__ edst, const float* __restrict__ wf,
+                               const uint32_t* sizes, uint32_t* __restrict__ ro,
+                               uint32_t* __restrict__ ci, float* __restrict__ wb) {
+  const uint32_t e = sizes[1];
+  const uint32_t s = sizes[2];
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < e; j += gridDim.x * blockDim.x) {
+    const uint32_t key = skey[j];
+    const uint32_t eid = seid[j];
+    ci[j] = edst[eid];
+    if (wb) wb[j] = wf ? wf[eid] : 0.0f;
+    if (j == 0 || skey[j - 1] != key) {
+      // rows between the previous key and this one are empty (cannot happen for
+      // a frontier built from the edges, kept for robustness)
+      const uint32_t prev = (j == 0) ? 0u : skey[j - 1] + 1u;
+      for (uint32_t r = prev; r <= key; ++r) ro[r] = j;
+    }
+    if (j == e - 1)
+      for (uint32_t r = key + 1; r <= s; ++r) ro[r] = e;
+  }
+  if (e == 0 && blockIdx.x == 0 && threadIdx.x == 0)
+    for (uint32_t r = 0; r <= s; ++r) ro[r] = 0;
+}
+
+}  // namespace nts_hip
+
+using namespace nts_hip;
+
+extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, int fanout,
+                                    int layer, uint64_t batch_seq, int rng_mode,
+                                    int weight_type, nts_sampcsc_dev* o) {
+  NTS_CHECK_ARG(ctx && g && o, "NULL argument");
+  NTS_CHECK_ARG(g->column_offset && g->row_indices, "graph not on device");
+  NTS_CHECK_ARG(o->destination && o->v_size && o->column_offset && o->row_indices &&
+                    o->sample_ans && o->edge_dst && o->source && o->sizes,
+                "missing sampCSC buffer");
+  NTS_CHECK_ARG(weight_type == NTS_WEIGHT_NONE || (o->edge_weight_forward && g->in_degree &&
+                                                   g->out_degree),
+                "weights requested without buffers/degrees");
+  NTS_CHECK_ARG(rng_mode >= NTS_RNG_PHILOX && rng_mode <= NTS_RNG_MT19937_DIV, "rng_mode");
+  NTS_CHECK_ARG(fanout <= kSetCap, "fanout above the rejection-path capacity (1024)");
+  NTS_CHECK_ARG(g->n_vertices <= 0xFFFFFFFFull, "vertex count exceeds uint32 ids");
+  const bool csr = o->row_offset != nullptr;
+  NTS_CHECK_ARG(!csr || o->column_indices, "CSR requested without column_indices");
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const uint64_t V = g->n_vertices;
+  NTS_RET(ensure_vertices(ctx, V));
+  const uint32_t nblk_marks = ceil_div(V, kMarkTile);
+
+  // scratch layout (u32 words)
+  auto al = [](uint64_t x) { return (x + 63) / 64 * 64; };
+  const uint64_t scan_co = al(scan_tmp_elems<uint32_t>(o->v_cap) + 1);
+  const uint64_t blk = al(nblk_marks + 1);
+  const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
+  const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
+  const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
+  const size_t need =
+      (scan_co + blk + scan_blk + sort_k + sort_v) * sizeof(uint32_t) + sort_tmp + 256;
+  NTS_RET(ensure_scratch(ctx, need));
+  uint32_t* w0 = (uint32_t*)ctx->scratch;
+  uint32_t* t_scan_co = w0;
+  uint32_t* t_blk = t_scan_co + scan_co;
+  uint32_t* t_scan_blk = t_blk + blk;
+  uint32_t* t_skey = t_scan_blk + scan_blk;
+  uint32_t* t_seid = t_skey + sort_k;
+  void* t_sort = (void*)(t_seid + sort_v);
+
+  const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
+  const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
+
+  // 1) per-dst counts -> column_offset, e_size
+  hipLaunchKernelGGL(k_count, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
+                     o->v_size, o->v_cap, fanout, o->column_offset, o->sizes);
+  NTS_LAUNCH_CHECK();
+  NTS_RET(scan_exclusive<uint32_t>(o->column_offset, o->column_offset, o->sizes, o->v_cap,
+                                   t_scan_co, st));
+  hipLaunchKernelGGL(k_finish_count, dim3(1), dim3(1), 0, st, o->column_offset, o->e_cap,
+                     o->sizes);
+  NTS_LAUNCH_CHECK();
+
+  // 2) selection (marks the frontier)
+  // clear the whole scanned range (V rounded up to the 4096-vertex tile): the
+  // arena may be larger than this graph and hold marks of a previous one
+  NTS_HIP_TRY(hipMemsetAsync(ctx->marks, 0, (size_t)nblk_marks * kMarkTile, st));
+  SelectArgs a;
+  a.goff = g->column_offset;
+  a.grows = g->row_indices;
+  a.dst = o->destination;
+  a.co = o->column_offset;
+  a.sizes = o->sizes;
+  a.ans = o->sample_ans;
+  a.edst = o->edge_dst;
+  a.marks = ctx->marks;
+  a.e_cap = o->e_cap;
+  a.fanout = fanout;
+  a.layer = (uint32_t)layer;
+  a.batch_seq = batch_seq;
+  a.seed = ctx->seed;
+  if (rng_mode == NTS_RNG_PHILOX) {
+    const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves), 4096u));
+    hipLaunchKernelGGL(k_select_philox, dim3(gs), dim3(kSelThreads), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_select_mt, dim3(1), dim3(kWave), 0, st, a, ctx->mt_state,
+                       rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0);
+  }
+  NTS_LAUNCH_CHECK();
+
+  // 3) frontier: ascending compaction of the byte map
+  hipLaunchKernelGGL(k_mark_count, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
+                     t_blk);
+  NTS_LAUNCH_CHECK();
+  NTS_RET(scan_exclusive<uint32_t>(t_blk, t_blk, nullptr, nblk_marks, t_scan_blk, st));
+  hipLaunchKernelGGL(k_mark_write, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
+                     t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index, o->sizes);
+  NTS_LAUNCH_CHECK();
+
+  // 4) relabel to local ids + forward weights
+  hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, o->sample_ans, o->edge_dst,
+                     o->destination, ctx->src_index, g->out_degree, g->in_degree, o->sizes,
+                     weight_type, o->row_indices, o->edge_weight_forward);
+  NTS_LAUNCH_CHECK();
+
+  // 5) CSR transpose (stable in edge order = ascending local dst)
+  if (csr) {
+    NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
+                             ceil_log2((uint64_t)o->s_cap + 1), t_sort, st));
+    hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
+                       weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
+                       o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward);
+    NTS_LAUNCH_CHECK();
+  }
+  return NTS_OK;
+}

@@ -1,0 +1,142 @@
+"""Reference on-disk formats and the config parser.
+
+* Edge file: raw binary array of {uint32 src; uint32 dst} (EdgeUnit<Empty>,
+  core/graph.hpp:1139-1140), |E| = bytes / 8.
+* Feature file: text, one line per vertex `id f_1 ... f_F`
+  (GNNDatum::readFeature_Label_Mask, core/ntsDataloador.hpp:999-1064).
+* Label file: `id label`; mask file: `id train|val|eval|test`; unlisted
+  vertices keep the memset(…,1) pattern (core/ntsDataloador.hpp:191) = 0x01010101.
+* FEATURE_FILE:random (core/ntsDataloador.hpp:835-861): all-ones features,
+  rand() % C labels, masks 65/10/25 % by vertex id.
+* Config: KEY:VALUE lines, `#` comments (InputInfo::readFromCfgFile,
+  core/GraphSegment.cpp:222-347).
+"""
+from __future__ import annotations
+
+import io
+import pathlib
+import zipfile
+from dataclasses import dataclass, field
+
+import numpy as np
+
+MASK_TRAIN, MASK_VAL, MASK_TEST, MASK_OTHER = 0, 1, 2, 3
+MASK_UNLISTED = 0x01010101
+
+
+def read_edge_file(path) -> tuple[np.ndarray, np.ndarray]:
+    e = np.fromfile(path, dtype=np.uint32)
+    if e.size % 2:
+        raise ValueError(f"{path}: size is not a multiple of 8 bytes")
+    e = e.reshape(-1, 2)
+    return np.ascontiguousarray(e[:, 0]), np.ascontiguousarray(e[:, 1])
+
+
+def write_edge_file(path, src: np.ndarray, dst: np.ndarray) -> None:
+    e = np.empty((src.size, 2), np.uint32)
+    e[:, 0] = src
+    e[:, 1] = dst
+    e.tofile(path)
+
+
+def _text(path) -> str:
+    p = pathlib.Path(path)
+    if p.suffix == ".zip":
+        with zipfile.ZipFile(p) as z:
+            name = z.namelist()[0]
+            return z.read(name).decode()
+    return p.read_text()
+
+
+def read_feature_label_mask(feature_path, label_path, mask_path, n_vertices: int, n_features: int):
+    """readFeature_Label_Mask (core/ntsDataloador.hpp:999-1064) for one partition covering all ids."""
+    feats = np.zeros((n_vertices, n_features), np.float32)
+    labels = np.zeros(n_vertices, np.int64)
+    masks = np.full(n_vertices, MASK_UNLISTED, np.int32)
+    ftab = np.loadtxt(io.StringIO(_text(feature_path)), dtype=np.float64, ndmin=2)
+    ids = ftab[:, 0].astype(np.int64)
+    feats[ids] = ftab[:, 1:1 + n_features].astype(np.float32)
+    ltab = np.loadtxt(io.StringIO(_text(label_path)), dtype=np.int64, ndmin=2)
+    # labels/masks are read line-by-line alongside the feature lines
+    labels[ids] = ltab[: ids.size, 1]
+    kinds = {"train": MASK_TRAIN, "eval": MASK_VAL, "val": MASK_VAL, "test": MASK_TEST}
+    mlines = _text(mask_path).split()
+    mids = np.array(mlines[0::2], np.int64)
+    mvals = np.array([kinds.get(s, MASK_OTHER) for s in mlines[1::2]], np.int32)
+    masks[ids] = mvals[: ids.size]
+    del mids
+    return feats, labels, masks
+
+
+def random_generate(n_vertices: int, n_features: int, n_classes: int, seed: int = 1,
+                    train_rate=0.65, val_rate=0.10):
+    """GNNDatum::random_generate: all-ones features, uniform labels, masks by id."""
+    feats = np.ones((n_vertices, n_features), np.float32)
+    rng = np.random.default_rng(seed)
+    labels = rng.integers(0, n_classes, n_vertices).astype(np.int64)
+    max_train = int(n_vertices * train_rate)
+    max_val = int(n_vertices * val_rate + max_train)
+    masks = np.full(n_vertices, MASK_TEST, np.int32)
+    masks[:max_train] = MASK_TRAIN
+    masks[max_train:max_val] = MASK_VAL
+    return feats, labels, masks
+
+
+@dataclass
+class InputInfo:
+    """InputInfo (core/GraphSegment.h:156-244) — the cfg keys of Appendix C."""
+    algorithm: str = ""
+    vertices: int = 0
+    epochs: int = 0
+    layer_string: str = ""
+    fanout_string: str = ""
+    edge_file: str = ""
+    feature_file: str = ""
+    label_file: str = ""
+    mask_file: str = ""
+    learn_rate: float = 0.0
+    weight_decay: float = 0.0
+    decay_rate: float = 0.0
+    decay_epoch: float = 0.0
+    drop_rate: float = 0.0
+    batch_size: int = 0
+    pipeline_num: int = 1
+    cache_rate: float = 0.1
+    up_degree: bool = False
+    gpu_num: int = 1
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def layers(self) -> list[int]:
+        return [int(x) for x in self.layer_string.split("-") if x]
+
+    @property
+    def fanout(self) -> list[int]:
+        return [int(x) for x in self.fanout_string.split("-") if x]
+
+    @classmethod
+    def from_cfg(cls, path) -> "InputInfo":
+        info = cls()
+        keymap = {
+            "ALGORITHM": ("algorithm", str), "VERTICES": ("vertices", int), "EPOCHS": ("epochs", int),
+            "LAYERS": ("layer_string", str), "FANOUT": ("fanout_string", str),
+            "EDGE_FILE": ("edge_file", str), "FEATURE_FILE": ("feature_file", str),
+            "LABEL_FILE": ("label_file", str), "MASK_FILE": ("mask_file", str),
+            "LEARN_RATE": ("learn_rate", float), "WEIGHT_DECAY": ("weight_decay", float),
+            "DECAY_RATE": ("decay_rate", float), "DECAY_EPOCH": ("decay_epoch", float),
+            "DROP_RATE": ("drop_rate", float), "BATCH_SIZE": ("batch_size", int),
+            "PIPELINE_NUM": ("pipeline_num", int), "CACHE_RATE": ("cache_rate", float),
+            "UP_DEGREE": ("up_degree", lambda s: bool(int(s))), "GPU_NUM": ("gpu_num", int),
+        }
+        for raw in pathlib.Path(path).read_text().splitlines():
+            line = raw.strip()
+            if not line or line.startswith("#") or ":" not in line:
+                continue
+            k, v = line.split(":", 1)
+            k, v = k.strip(), v.strip()
+            if k in keymap:
+                name, conv = keymap[k]
+                setattr(info, name, conv(v))
+            else:
+                info.extra[k] = v
+        return info

@@ -1,0 +1,188 @@
+"""Thin Python handle over the C-ABI (one `nts_hip_ctx` per stream).
+
+Used by the kernel-level parity tests and by the data-preparation helpers;
+the training path itself runs in the C++ host layer (nts/host).  All methods
+take torch tensors already resident on the GPU and enqueue work on the
+context's stream; nothing here falls back to the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _abi
+from ._abi import check, ptr
+
+
+def _u32(n, device):
+    return torch.empty(int(n), dtype=torch.int32, device=device)
+
+
+class HipContext:
+    """Owns an nts_hip_ctx bound to a torch stream (Cuda_Stream equivalent)."""
+
+    def __init__(self, device: int = 0, stream: torch.cuda.Stream | None = None, seed: int = 2000):
+        self.lib = _abi.lib()
+        self.device = device
+        self.stream = stream if stream is not None else torch.cuda.current_stream(device)
+        h = C.c_void_p()
+        check(self.lib.nts_hip_ctx_create(C.byref(h), device, C.c_void_p(self.stream.cuda_stream), seed))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.nts_hip_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- context -------------------------------------------------------------
+    def reserve(self, n_vertices: int, max_items: int):
+        check(self.lib.nts_hip_ctx_reserve(self.h, n_vertices, max_items))
+
+    def rng_seed(self, seed: int):
+        check(self.lib.nts_hip_rng_seed(self.h, seed))
+
+    def rng_state(self) -> torch.Tensor:
+        out = torch.empty(625, dtype=torch.int32)
+        check(self.lib.nts_hip_rng_state(self.h, C.c_void_p(out.data_ptr())))
+        return out
+
+    # ---- graph ---------------------------------------------------------------
+    def degrees(self, src: torch.Tensor, dst: torch.Tensor, V: int):
+        out_deg = _u32(V, src.device)
+        in_deg = _u32(V, src.device)
+        check(self.lib.nts_hip_degrees(self.h, ptr(src), ptr(dst), src.numel(), V,
+                                       ptr(out_deg), ptr(in_deg)))
+        return out_deg, in_deg
+
+    def build_csc(self, src: torch.Tensor, dst: torch.Tensor, V: int):
+        col = torch.empty(V + 1, dtype=torch.int64, device=src.device)
+        rows = _u32(src.numel(), src.device)
+        check(self.lib.nts_hip_build_csc(self.h, ptr(src), ptr(dst), src.numel(), V,
+                                         ptr(col), ptr(rows)))
+        return col, rows
+
+    # ---- sampler -------------------------------------------------------------
+    def sample_layer(self, graph: "DeviceGraph", lay: "LayerBuffers", fanout: int, layer: int,
+                     batch_seq: int, rng_mode: int, weight_type: int):
+        g = graph.as_struct()
+        o = lay.as_struct()
+        check(self.lib.nts_hip_sample_layer(self.h, C.byref(g), fanout, layer, batch_seq,
+                                            rng_mode, weight_type, C.byref(o)))
+
+    # ---- movement / aggregation ------------------------------------------------
+    def gather_rows(self, table, index, n_dev, n_cap, out):
+        F = table.shape[1]
+        check(self.lib.nts_hip_gather_rows(self.h, ptr(table), table.stride(0), ptr(index),
+                                           ptr(n_dev), n_cap, F, ptr(out), out.stride(0)))
+
+    def gather_labels(self, labels, index, n_dev, n_cap, out):
+        check(self.lib.nts_hip_gather_labels(self.h, ptr(labels), ptr(index), ptr(n_dev),
+                                             n_cap, ptr(out)))
+
+    def spmm_csc_fwd(self, co, ri, w, v_dev, v_cap, x, y, row_map=None):
+        F = x.shape[1]
+        check(self.lib.nts_hip_spmm_csc_fwd(self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev), v_cap,
+                                            ptr(x), x.stride(0), ptr(row_map), F, ptr(y),
+                                            y.stride(0)))
+
+    def spmm_csr_bwd(self, ro, ci, wb, s_dev, s_cap, g_out, g_in):
+        F = g_out.shape[1]
+        check(self.lib.nts_hip_spmm_csr_bwd(self.h, ptr(ro), ptr(ci), ptr(wb), ptr(s_dev), s_cap,
+                                            ptr(g_out), g_out.stride(0), F, ptr(g_in),
+                                            g_in.stride(0)))
+
+    def spmm_csc_bwd_atomic(self, co, ri, w, v_dev, v_cap, g_out, g_in):
+        F = g_out.shape[1]
+        check(self.lib.nts_hip_spmm_csc_bwd_atomic(self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev),
+                                                   v_cap, ptr(g_out), g_out.stride(0), F,
+                                                   ptr(g_in), g_in.stride(0)))
+
+    def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
+        check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,
+                                    beta1, beta2, eps, wd, beta1_t, beta2_t, int(bias_correction)))
+
+
+@dataclass
+class DeviceGraph:
+    """FullyRepGraph + degrees resident in HBM."""
+    n_vertices: int
+    n_edges: int
+    column_offset: torch.Tensor  # int64 [V+1]
+    row_indices: torch.Tensor    # int32 [E]
+    in_degree: torch.Tensor      # int32 [V]
+    out_degree: torch.Tensor     # int32 [V]
+
+    def as_struct(self) -> _abi.GraphDev:
+        return _abi.GraphDev(self.n_vertices, self.n_edges, ptr(self.column_offset),
+                             ptr(self.row_indices), ptr(self.in_degree), ptr(self.out_degree))
+
+
+@dataclass
+class LayerBuffers:
+    """Device arrays of one sampCSC (capacity-sized)."""
+    v_cap: int
+    e_cap: int
+    s_cap: int
+    destination: torch.Tensor
+    v_size: torch.Tensor
+    device: torch.device
+    csr: bool = True
+    weights: bool = True
+    t: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        d = self.device
+        self.t["column_offset"] = _u32(self.v_cap + 1, d)
+        self.t["row_indices"] = _u32(max(self.e_cap, 1), d)
+        self.t["sample_ans"] = _u32(max(self.e_cap, 1), d)
+        self.t["edge_dst"] = _u32(max(self.e_cap, 1), d)
+        self.t["source"] = _u32(max(self.s_cap, 1), d)
+        self.t["sizes"] = torch.zeros(4, dtype=torch.int32, device=d)
+        self.t["edge_weight_forward"] = (torch.empty(max(self.e_cap, 1), dtype=torch.float32, device=d)
+                                         if self.weights else None)
+        if self.csr:
+            self.t["row_offset"] = _u32(self.s_cap + 1, d)
+            self.t["column_indices"] = _u32(max(self.e_cap, 1), d)
+            self.t["edge_weight_backward"] = (torch.empty(max(self.e_cap, 1), dtype=torch.float32, device=d)
+                                              if self.weights else None)
+        else:
+            self.t["row_offset"] = self.t["column_indices"] = self.t["edge_weight_backward"] = None
+
+    def __getattr__(self, k):
+        t = self.__dict__.get("t")
+        if t is not None and k in t:
+            return t[k]
+        raise AttributeError(k)
+
+    def as_struct(self) -> _abi.SampCSCDev:
+        t = self.t
+        return _abi.SampCSCDev(
+            self.v_cap, self.e_cap, self.s_cap, ptr(self.destination), ptr(self.v_size),
+            ptr(t["column_offset"]), ptr(t["row_indices"]), ptr(t["sample_ans"]), ptr(t["edge_dst"]),
+            ptr(t["source"]), ptr(t["edge_weight_forward"]), ptr(t["row_offset"]),
+            ptr(t["column_indices"]), ptr(t["edge_weight_backward"]), ptr(t["sizes"]))
+
+    def sizes_host(self):
+        s = self.t["sizes"].cpu().tolist()
+        return s[0], s[1], s[2], s[3]
+
+
+def layer_caps(batch: int, fanouts, n_vertices: int, n_edges: int):
+    """Upper bounds (v_cap, e_cap, s_cap) per layer: v_0 = B, e_l <= v_l * f_l
+    (or the edge count for fanout -1), s_l <= min(e_l, V), v_{l+1} = s_l."""
+    caps = []
+    v = batch
+    for f in fanouts:
+        e = n_edges if f < 0 else min(v * f, n_edges)
+        s = min(e, n_vertices)
+        caps.append((v, e, s))
+        v = s
+    return caps
