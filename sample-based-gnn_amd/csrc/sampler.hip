@@ -466,7 +466,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                                     int weight_type, nts_sampcsc_dev* o) {
   NTS_CHECK_ARG(ctx && g && o, "NULL argument");
   NTS_CHECK_ARG(g->column_offset && g->row_indices, "graph not on device");
-  NTS_CHECK_ARG(o->destination && o->v_size && o->column_offset && o->row_indices &&
+  NTS_CHECK_ARG((o->destination || o->v_cap == 0) && o->v_size && o->column_offset &&
+                    o->row_indices &&
                     o->sample_ans && o->edge_dst && o->source && o->sizes,
                 "missing sampCSC buffer");
   NTS_CHECK_ARG(weight_type == NTS_WEIGHT_NONE || (o->edge_weight_forward && g->in_degree &&

@@ -1,0 +1,479 @@
+// C++ host layer: streams, graph, sampler, graph ops, autodiff context,
+// parameters and the RCCL communicator.  See nts_host.hpp for the reference
+// classes each of these mirrors.
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+#include "nts_host.hpp"
+
+namespace nts {
+
+void hip_check(int rc, const char* what) {
+  if (rc != NTS_OK)
+    throw std::runtime_error(std::string(what) + ": nts_hip error " + std::to_string(rc) + ": " +
+                             nts_hip_last_error());
+}
+
+static void hip_rt(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---------------------------------------------------------------------------
+NtsStream::NtsStream(int device, void* stream, uint64_t seed) : device_(device) {
+  if (!stream) stream = (void*)c10::hip::getCurrentHIPStream(device).stream();
+  hip_check(nts_hip_ctx_create(&ctx_, device, stream, seed), "nts_hip_ctx_create");
+}
+NtsStream::~NtsStream() { nts_hip_ctx_destroy(ctx_); }
+void NtsStream::setNewStream(void* stream) {
+  hip_check(nts_hip_ctx_set_stream(ctx_, stream), "setNewStream");
+}
+void* NtsStream::stream() const { return nts_hip_ctx_get_stream(ctx_); }
+void NtsStream::synchronize() const {
+  hip_rt(hipStreamSynchronize((hipStream_t)stream()), "hipStreamSynchronize");
+}
+
+// ---------------------------------------------------------------------------
+std::shared_ptr<FullyRepGraph> FullyRepGraph::from_edges(NtsStream& cs, const torch::Tensor& src,
+                                                         const torch::Tensor& dst,
+                                                         VertexId vertices) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.dtype() == torch::kInt32 &&
+                  dst.dtype() == torch::kInt32 && src.numel() == dst.numel(),
+              "from_edges: src/dst must be int32 CUDA tensors of equal length");
+  auto g = std::make_shared<FullyRepGraph>();
+  g->device = cs.device();
+  g->global_vertices = vertices;
+  g->global_edges = (uint64_t)src.numel();
+  auto s = src.contiguous(), d = dst.contiguous();
+  g->column_offset = torch::empty({(int64_t)vertices + 1},
+                                  torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, g->device));
+  g->row_indices = torch::empty({(int64_t)std::max<uint64_t>(g->global_edges, 1)}, u32_opts(g->device));
+  g->in_degree = torch::empty({(int64_t)vertices}, u32_opts(g->device));
+  g->out_degree = torch::empty({(int64_t)vertices}, u32_opts(g->device));
+  hip_check(nts_hip_build_csc(cs.ctx(), dptr<uint32_t>(s), dptr<uint32_t>(d), g->global_edges,
+                              vertices, dptr<uint64_t>(g->column_offset),
+                              dptr<uint32_t>(g->row_indices)),
+            "nts_hip_build_csc");
+  hip_check(nts_hip_degrees(cs.ctx(), dptr<uint32_t>(s), dptr<uint32_t>(d), g->global_edges,
+                            vertices, dptr<uint32_t>(g->out_degree), dptr<uint32_t>(g->in_degree)),
+            "nts_hip_degrees");
+  cs.synchronize();
+  return g;
+}
+
+std::shared_ptr<FullyRepGraph> FullyRepGraph::from_csc(torch::Tensor column_offset,
+                                                       torch::Tensor row_indices,
+                                                       torch::Tensor in_degree,
+                                                       torch::Tensor out_degree) {
+  auto g = std::make_shared<FullyRepGraph>();
+  TORCH_CHECK(column_offset.dtype() == torch::kInt64 && row_indices.dtype() == torch::kInt32,
+              "from_csc: column_offset int64, row_indices int32");
+  g->device = column_offset.device().index();
+  g->global_vertices = (VertexId)(column_offset.numel() - 1);
+  g->global_edges = (uint64_t)row_indices.numel();
+  g->column_offset = column_offset.contiguous();
+  g->row_indices = row_indices.contiguous();
+  g->in_degree = in_degree.contiguous();
+  g->out_degree = out_degree.contiguous();
+  return g;
+}
+
+nts_graph_dev FullyRepGraph::dev() const {
+  nts_graph_dev d;
+  d.n_vertices = global_vertices;
+  d.n_edges = global_edges;
+  d.column_offset = dptr<uint64_t>(column_offset);
+  d.row_indices = dptr<uint32_t>(row_indices);
+  d.in_degree = dptr<uint32_t>(in_degree);
+  d.out_degree = dptr<uint32_t>(out_degree);
+  return d;
+}
+
+// ---------------------------------------------------------------------------
+sampCSC::sampCSC(int device, VertexId vc, VertexId ec, VertexId sc, bool csr, bool weights)
+    : v_cap(vc), e_cap(ec), s_cap(sc), has_csr(csr) {
+  auto U = u32_opts(device);
+  auto F = f32_opts(device);
+  const int64_t e1 = std::max<int64_t>(ec, 1), s1 = std::max<int64_t>(sc, 1);
+  column_offset = torch::empty({(int64_t)vc + 1}, U);
+  row_indices = torch::empty({e1}, U);
+  sample_ans = torch::empty({e1}, U);
+  edge_dst = torch::empty({e1}, U);
+  source = torch::empty({s1}, U);
+  sizes = torch::zeros({4}, U);
+  dst_count = torch::zeros({1}, U);
+  if (weights) edge_weight_forward = torch::empty({e1}, F);
+  if (csr) {
+    row_offset = torch::empty({(int64_t)sc + 1}, U);
+    column_indices = torch::empty({e1}, U);
+    if (weights) edge_weight_backward = torch::empty({e1}, F);
+  }
+}
+
+std::vector<VertexId> sampCSC::host_u32(const torch::Tensor& t, size_t n) const {
+  auto c = t.narrow(0, 0, (int64_t)n).cpu();
+  std::vector<VertexId> out(n);
+  if (n) std::memcpy(out.data(), c.data_ptr(), n * 4);
+  return out;
+}
+
+static std::vector<std::array<uint64_t, 3>> layer_caps(VertexId batch,
+                                                       const std::vector<int>& fanout,
+                                                       VertexId V, uint64_t E) {
+  std::vector<std::array<uint64_t, 3>> caps;
+  uint64_t v = batch;
+  for (int f : fanout) {
+    uint64_t e = f < 0 ? E : std::min<uint64_t>(v * (uint64_t)f, E);
+    uint64_t s = std::min<uint64_t>(e, V);
+    TORCH_CHECK(e <= 0xFFFFFFFFull, "sampled layer exceeds 2^32 edges");
+    caps.push_back({v, e, s});
+    v = s;
+  }
+  return caps;
+}
+
+SampledSubgraph::SampledSubgraph(int device, int layers_, const std::vector<int>& fanout_,
+                                 VertexId batch, VertexId vertices, uint64_t edges,
+                                 const std::vector<bool>& csr, bool weights)
+    : layers(layers_), fanout(fanout_) {
+  auto caps = layer_caps(batch, fanout, vertices, edges);
+  for (int l = 0; l < layers; ++l) {
+    bool c = csr.empty() ? true : (bool)csr[l];
+    sampled_sgs.push_back(new sampCSC(device, (VertexId)caps[l][0], (VertexId)caps[l][1],
+                                      (VertexId)caps[l][2], c, weights));
+  }
+  host_sizes = torch::empty({layers * 4}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true));
+}
+
+SampledSubgraph::~SampledSubgraph() {
+  for (auto* s : sampled_sgs) delete s;
+}
+
+// ---------------------------------------------------------------------------
+FastSampler::FastSampler(std::shared_ptr<FullyRepGraph> g, const std::vector<VertexId>& index,
+                         int layers, int batch_size, const std::vector<int>& fanout_,
+                         int pipeline_num, std::vector<bool> csr_layers, bool weights)
+    : whole_graph(g), layer(layers), fanout(fanout_), batch_cap_((VertexId)batch_size) {
+  TORCH_CHECK((int)fanout.size() == layers, "fanout size != layers");
+  if (pipeline_num < 1) pipeline_num = 1;
+  for (int i = 0; i < pipeline_num; ++i)
+    ssgs.push_back(new SampledSubgraph(g->device, layers, fanout, batch_cap_, g->global_vertices,
+                                       g->global_edges, csr_layers, weights));
+  ssg = ssgs[0];
+  set_sample_nids(index);
+}
+
+FastSampler::~FastSampler() {
+  for (auto* s : ssgs) delete s;
+}
+
+void FastSampler::set_sample_nids(const std::vector<VertexId>& ids) {
+  sample_nids = ids;
+  work_range[0] = 0;
+  work_range[1] = (VertexId)sample_nids.size();
+  work_offset = 0;
+  dev_nids_ = torch::empty({(int64_t)std::max<size_t>(ids.size(), 1)}, u32_opts(whole_graph->device));
+  if (!ids.empty()) {
+    auto h = torch::from_blob((void*)sample_nids.data(), {(int64_t)ids.size()}, torch::kInt32);
+    dev_nids_.narrow(0, 0, (int64_t)ids.size()).copy_(h);
+  }
+}
+
+SampledSubgraph* FastSampler::sample_gpu_fast(int batch_size, int ssg_id, NtsStream& cs,
+                                              WeightType w) {
+  double t0 = now_s();
+  TORCH_CHECK(work_offset < work_range[1], "sample_gpu_fast: no work left");
+  TORCH_CHECK((VertexId)batch_size <= batch_cap_, "batch larger than the sampler's capacity");
+  ssg = ssgs[ssg_id];
+  const VertexId actual = std::min<VertexId>((VertexId)batch_size, work_range[1] - work_offset);
+  hipStream_t st = (hipStream_t)cs.stream();
+  const nts_graph_dev g = whole_graph->dev();
+  const int wt = w == WeightType::Sum ? NTS_WEIGHT_SUM
+                                      : (w == WeightType::Mean ? NTS_WEIGHT_MEAN : NTS_WEIGHT_NONE);
+  const VertexId* dst = dptr<VertexId>(dev_nids_) + work_offset;
+  sampCSC* s0 = ssg->sampled_sgs[0];
+  hip_rt(hipMemsetD32Async(dptr<uint32_t>(s0->dst_count), (int)actual, 1, st), "hipMemsetD32Async");
+  const VertexId* vsz = dptr<VertexId>(s0->dst_count);
+  for (int l = 0; l < layer; ++l) {
+    sampCSC* s = ssg->sampled_sgs[l];
+    nts_sampcsc_dev o;
+    o.v_cap = s->v_cap;
+    o.e_cap = s->e_cap;
+    o.s_cap = s->s_cap;
+    o.destination = dst;
+    o.v_size = vsz;
+    o.column_offset = dptr<uint32_t>(s->column_offset);
+    o.row_indices = dptr<uint32_t>(s->row_indices);
+    o.sample_ans = dptr<uint32_t>(s->sample_ans);
+    o.edge_dst = dptr<uint32_t>(s->edge_dst);
+    o.source = dptr<uint32_t>(s->source);
+    o.edge_weight_forward = wt == NTS_WEIGHT_NONE ? nullptr : dptr<float>(s->edge_weight_forward);
+    o.row_offset = s->has_csr ? dptr<uint32_t>(s->row_offset) : nullptr;
+    o.column_indices = s->has_csr ? dptr<uint32_t>(s->column_indices) : nullptr;
+    o.edge_weight_backward =
+        (s->has_csr && wt != NTS_WEIGHT_NONE) ? dptr<float>(s->edge_weight_backward) : nullptr;
+    o.sizes = dptr<uint32_t>(s->sizes);
+    hip_check(nts_hip_sample_layer(cs.ctx(), &g, fanout[l], l, batch_seq, rng_mode, wt, &o),
+              "nts_hip_sample_layer");
+    // the reference keeps the destination as a view of the previous source
+    if (l == 0)
+      s->destination = dev_nids_.narrow(0, work_offset, std::max<int64_t>(actual, 0));
+    else
+      s->destination = ssg->sampled_sgs[l - 1]->source;
+    dst = o.source;
+    vsz = o.sizes + 2;
+  }
+  // one D2H of all layer sizes per batch (the reference syncs twice per layer)
+  int32_t* hs = ssg->host_sizes.data_ptr<int32_t>();
+  for (int l = 0; l < layer; ++l)
+    hip_rt(hipMemcpyAsync(hs + 4 * l, dptr<uint32_t>(ssg->sampled_sgs[l]->sizes), 16,
+                          hipMemcpyDeviceToHost, st),
+           "hipMemcpyAsync(sizes)");
+  hip_rt(hipStreamSynchronize(st), "hipStreamSynchronize");
+  for (int l = 0; l < layer; ++l) {
+    sampCSC* s = ssg->sampled_sgs[l];
+    s->v_size = (VertexId)hs[4 * l];
+    s->e_size = (VertexId)hs[4 * l + 1];
+    s->src_size = (VertexId)hs[4 * l + 2];
+    TORCH_CHECK(hs[4 * l + 3] == 0, "sampled layer ", l, " exceeded its capacity");
+    sampled_edges += s->e_size;
+  }
+  work_offset += actual;
+  ++batch_seq;
+  all_time += now_s() - t0;
+  return ssg;
+}
+
+void FastSampler::load_feature_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_feature,
+                                   const NtsVar& global_feature) {
+  sampCSC* top = sg->sampled_sgs[layer - 1];
+  const int64_t F = global_feature.size(1);
+  if (!local_feature.defined() || local_feature.size(0) != (int64_t)top->src_size ||
+      local_feature.size(1) != F)
+    local_feature = torch::empty({(int64_t)top->src_size, F}, f32_opts(whole_graph->device));
+  hip_check(nts_hip_gather_rows(cs.ctx(), global_feature.data_ptr<float>(),
+                                (uint64_t)global_feature.stride(0), top->dev_src(), nullptr,
+                                top->src_size, (uint32_t)F, local_feature.data_ptr<float>(),
+                                (uint64_t)local_feature.stride(0)),
+            "nts_hip_gather_rows");
+}
+
+void FastSampler::load_label_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_label,
+                                 const NtsVar& global_label) {
+  sampCSC* s0 = sg->sampled_sgs[0];
+  if (!local_label.defined() || local_label.size(0) != (int64_t)s0->v_size)
+    local_label = torch::empty({(int64_t)s0->v_size},
+                               torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, whole_graph->device));
+  hip_check(nts_hip_gather_labels(cs.ctx(), global_label.data_ptr<int64_t>(), s0->dev_dst(),
+                                  nullptr, s0->v_size, local_label.data_ptr<int64_t>()),
+            "nts_hip_gather_labels");
+}
+
+// ---------------------------------------------------------------------------
+namespace op {
+
+SingleGPUAllSampleGraphOp::SingleGPUAllSampleGraphOp(SampledSubgraph* sgs, FullyRepGraph* graph,
+                                                     int layer_, NtsStream* cs, bool gather)
+    : subgraphs(sgs), layer(layer_), cuda_stream(cs), gather_from_table(gather) {
+  (void)graph;
+}
+
+NtsVar SingleGPUAllSampleGraphOp::forward(NtsVar& f_input) {
+  sampCSC* sg = subgraphs->sampled_sgs[layer];
+  TORCH_CHECK(f_input.is_cuda() && f_input.dtype() == torch::kFloat32 && f_input.dim() == 2 &&
+                  f_input.stride(1) == 1,
+              "graph op input must be a row-major fp32 CUDA matrix");
+  TORCH_CHECK(gather_from_table || f_input.size(0) >= (int64_t)sg->src_size,
+              "graph op input has fewer rows than src_size");
+  const int64_t F = f_input.size(1);
+  NtsVar f_output = torch::empty({(int64_t)sg->v_size, F}, f32_opts(cuda_stream->device()));
+  hip_check(nts_hip_spmm_csc_fwd(cuda_stream->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
+                                 nullptr, sg->v_size, f_input.data_ptr<float>(),
+                                 (uint64_t)f_input.stride(0),
+                                 gather_from_table ? sg->dev_src() : nullptr, (uint32_t)F,
+                                 f_output.data_ptr<float>(), (uint64_t)F),
+            "nts_hip_spmm_csc_fwd");
+  if (output_requires_grad) f_output.set_requires_grad(true);
+  return f_output;
+}
+
+NtsVar SingleGPUAllSampleGraphOp::backward(NtsVar& g) {
+  sampCSC* sg = subgraphs->sampled_sgs[layer];
+  NtsVar go = g.contiguous();
+  const int64_t F = go.size(1);
+  TORCH_CHECK(go.size(0) == (int64_t)sg->v_size, "output grad rows != v_size");
+  if (sg->has_csr) {
+    NtsVar gi = torch::empty({(int64_t)sg->src_size, F}, f32_opts(cuda_stream->device()));
+    hip_check(nts_hip_spmm_csr_bwd(cuda_stream->ctx(), sg->dev_r_o(), sg->dev_c_i(),
+                                   sg->dev_e_w_b(), nullptr, sg->src_size, go.data_ptr<float>(),
+                                   (uint64_t)F, (uint32_t)F, gi.data_ptr<float>(), (uint64_t)F),
+              "nts_hip_spmm_csr_bwd");
+    return gi;
+  }
+  NtsVar gi = torch::zeros({(int64_t)sg->src_size, F}, f32_opts(cuda_stream->device()));
+  hip_check(nts_hip_spmm_csc_bwd_atomic(cuda_stream->ctx(), sg->dev_c_o(), sg->dev_r_i(),
+                                        sg->dev_e_w_f(), nullptr, sg->v_size, go.data_ptr<float>(),
+                                        (uint64_t)F, (uint32_t)F, gi.data_ptr<float>(), (uint64_t)F),
+            "nts_hip_spmm_csc_bwd_atomic");
+  return gi;
+}
+
+NtsVar SingleGPUSampleGraphOp::backward(NtsVar& g) {
+  TORCH_CHECK(subgraphs->sampled_sgs[layer]->has_csr,
+              "SingleGPUSampleGraphOp needs the CSR transpose");
+  return SingleGPUAllSampleGraphOp::backward(g);
+}
+
+}  // namespace op
+
+// ---------------------------------------------------------------------------
+namespace ctx {
+
+NtsContext::NtsContext() {}
+NtsContext::~NtsContext() { reset(); }
+
+void NtsContext::push_graph_op(op::ntsGraphOp* op, NtsVar& in, NtsVar& out) {
+  if (!training) {  // eval: ops are not recorded (and not leaked, unlike the reference)
+    delete op;
+    return;
+  }
+  ops_.push_back(Entry{GRAPHOP, op, in, out, NtsVar(), in.data_ptr(), out.data_ptr()});
+  ++count;
+}
+
+NtsVar NtsContext::runVertexForward(const std::function<NtsVar(NtsVar&, NtsVar&)>& fn,
+                                    NtsVar& nbr_input, NtsVar& vtx_input) {
+  NtsVar out = fn(nbr_input, vtx_input);
+  if (training) appendNNOp(nbr_input, out);
+  return out;
+}
+
+NtsVar NtsContext::runVertexForward(const std::function<NtsVar(NtsVar&)>& fn, NtsVar& nbr_input) {
+  NtsVar out = fn(nbr_input);
+  if (training) appendNNOp(nbr_input, out);
+  return out;
+}
+
+// core/ntsContext.hpp:384-405: consecutive NN ops are chained (libtorch
+// handles their backward), so only the segment's last output is kept.
+void NtsContext::appendNNOp(NtsVar& input_t, NtsVar& output_t) {
+  TORCH_CHECK(training, "appendNNOp in eval mode");
+  if (count > 0 && ops_.back().type == NNOP) {
+    ops_.back().output = output_t;
+    ops_.back().out_id = output_t.data_ptr();
+  } else {
+    ops_.push_back(Entry{NNOP, nullptr, input_t, output_t, NtsVar(), input_t.data_ptr(),
+                         output_t.data_ptr()});
+    ++count;
+  }
+}
+
+void NtsContext::pop_one_op() {
+  delete ops_.back().op;
+  ops_.pop_back();
+  --count;
+}
+
+// core/ntsContext.hpp:436-508: loss backward through libtorch, then walk the
+// stack alternating graph-op backward and libtorch backward; the bottom graph
+// op's backward is skipped.
+void NtsContext::self_backward(bool retain_graph) {
+  TORCH_CHECK(training && count > 0, "self_backward outside training");
+  Entry& top = ops_.back();
+  top.output.backward(torch::ones_like(top.output), {}, retain_graph);
+  if (count >= 2) ops_[count - 2].output_grad = top.input.grad();
+  pop_one_op();
+  while (count > 1 || (count == 1 && ops_.back().type == NNOP)) {
+    Entry& e = ops_.back();
+    const int t = count - 1;
+    if (e.type == GRAPHOP) {
+      if (!e.output_grad.defined()) e.output_grad = e.output.grad();
+      int pre = t;
+      for (; pre >= 0; --pre)
+        if (ops_[pre].out_id == e.in_id) break;
+      TORCH_CHECK(pre >= 0, "graph op input has no producer on the stack");
+      ops_[pre].output_grad = e.op->backward(e.output_grad);
+      pop_one_op();
+    } else {
+      if (!e.output_grad.defined()) e.output_grad = e.output.grad();
+      if (e.output_grad.defined() && e.output_grad.dim() > 1)
+        e.output.backward(e.output_grad, {}, retain_graph);
+      pop_one_op();
+    }
+  }
+  reset();
+}
+
+void NtsContext::reset() {
+  while (!ops_.empty()) pop_one_op();
+  count = 0;
+}
+
+}  // namespace ctx
+
+// ---------------------------------------------------------------------------
+Parameter::Parameter(size_t w, size_t h, ValueType alpha_, ValueType beta1_, ValueType beta2_,
+                     ValueType epsilon_, ValueType weight_decay_, int device, int64_t init_seed)
+    : row((int)w), col((int)h), alpha(alpha_), beta1(beta1_), beta2(beta2_), epsilon(epsilon_),
+      weight_decay(weight_decay_), beta1_t(beta1_), beta2_t(beta2_) {
+  // xavier_uniform_ (core/NtsScheduler.hpp:731-733), seeded for reproducibility
+  auto gen = at::detail::createCPUGenerator(init_seed);
+  const double a = std::sqrt(6.0 / (double)(w + h));
+  auto Wc = torch::empty({(int64_t)w, (int64_t)h}, torch::kFloat32).uniform_(-a, a, gen);
+  W = Wc.to(torch::Device(torch::kCUDA, device)).set_requires_grad(true);
+  M = torch::zeros_like(W).set_requires_grad(false);
+  V = torch::zeros_like(W).set_requires_grad(false);
+}
+
+static void adam_step(Parameter& p, NtsStream& cs, int bias_correction) {
+  TORCH_CHECK(p.W.grad().defined(), "Parameter has no gradient");
+  NtsVar g = p.W.grad().contiguous();
+  torch::NoGradGuard ng;
+  hip_check(nts_hip_adam(cs.ctx(), p.W.data_ptr<float>(), g.data_ptr<float>(),
+                         p.M.data_ptr<float>(), p.V.data_ptr<float>(), (uint64_t)p.W.numel(),
+                         p.alpha, p.beta1, p.beta2, p.epsilon, p.weight_decay, p.beta1_t,
+                         p.beta2_t, bias_correction),
+            "nts_hip_adam");
+}
+
+void Parameter::learnC2C_with_decay_Adam(NtsStream& cs) { adam_step(*this, cs, 1); }
+void Parameter::learn_local_with_decay_Adam(NtsStream& cs) { adam_step(*this, cs, 0); }
+
+void Parameter::next() {
+  beta1_t *= beta1;
+  beta2_t *= beta2;
+  ++curr_epoch;
+}
+
+void Parameter::zero_grad() {
+  if (W.grad().defined()) W.mutable_grad().zero_();
+}
+
+// ---------------------------------------------------------------------------
+Communicator::Communicator(int n, int r, const std::vector<uint8_t>& uid, int device)
+    : nranks(n), rank(r) {
+  TORCH_CHECK(uid.size() == 128, "RCCL unique id must be 128 bytes");
+  hip_check(nts_hip_comm_init(&comm_, n, r, uid.data(), device), "nts_hip_comm_init");
+}
+Communicator::~Communicator() { nts_hip_comm_destroy(comm_); }
+void Communicator::allreduce_sum(float* buf, uint64_t n, void* stream) {
+  hip_check(nts_hip_allreduce_sum_f32(comm_, buf, n, stream), "nts_hip_allreduce_sum_f32");
+}
+void Communicator::broadcast(float* buf, uint64_t n, int root, void* stream) {
+  hip_check(nts_hip_broadcast_f32(comm_, buf, n, root, stream), "nts_hip_broadcast_f32");
+}
+std::vector<uint8_t> Communicator::unique_id() {
+  std::vector<uint8_t> id(128);
+  hip_check(nts_hip_comm_unique_id(id.data()), "nts_hip_comm_unique_id");
+  return id;
+}
+
+}  // namespace nts

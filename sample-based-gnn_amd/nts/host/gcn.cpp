@@ -1,0 +1,243 @@
+// Model drivers: the GPU-sampled GCN / GraphSAGE toolkits.
+//   GCN_SAMPLE_ALLGPU_impl   toolkits/GCN_SAMPLE_ALLGPU.hpp  (GPU sampler, 1 GPU)
+//   GS_SAMPLE_ALLGPU         toolkits/GS_SAMPLE_ALLGPU.hpp   (same pipeline, Mean weights, :296)
+//   GCN_SAMPLE_ALL_MULTI     toolkits/GCN_SAMPLE_ALL_MULTI.hpp (data parallel, grad SUM all-reduce)
+// One class covers the three: the weight type and the optional communicator
+// select the variant.  Per batch: sample_gpu_fast -> load_label_gpu ->
+// [fused feature gather +] graph op -> vertexForward ... -> Loss ->
+// self_backward -> Update (all-reduce + Adam) -> zero_grad.
+#include "gcn.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <random>
+
+namespace nts {
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g, NtsVar feature,
+                                               NtsVar label, std::vector<VertexId> train_nids,
+                                               GCNConfig c, std::shared_ptr<Communicator> comm_)
+    : graph(std::move(g)), F(std::move(feature)), L_GT(std::move(label)), cfg(std::move(c)),
+      comm(std::move(comm_)) {
+  TORCH_CHECK(cfg.layer_size.size() >= 2, "need at least one layer");
+  TORCH_CHECK(cfg.fanout.size() == cfg.layer_size.size() - 1, "fanout per layer");
+  TORCH_CHECK(F.is_cuda() && F.dtype() == torch::kFloat32 && F.size(1) == cfg.layer_size[0],
+              "feature table must be fp32 [V, layer_size[0]] on the GPU");
+  cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+  if (cfg.shuffle) {  // shuffle_vec (toolkits/GCN_SAMPLE_GPU.hpp:175-180): mt19937(2000)
+    std::mt19937 gen(2000);
+    std::shuffle(train_nids.begin(), train_nids.end(), gen);
+  }
+  const int L = (int)cfg.fanout.size();
+  // CSR transposes only where a graph-op backward runs (every hop but the
+  // outermost, whose backward the context skips)
+  std::vector<bool> csr(L, cfg.deterministic_backward);
+  csr[L - 1] = false;
+  sampler = std::make_unique<FastSampler>(graph, train_nids, L, cfg.batch_size, cfg.fanout, 1, csr,
+                                          cfg.weight_type != WeightType::None);
+  sampler->rng_mode = cfg.rng_mode;
+  // size the scratch arena once so the training loop never allocates
+  uint64_t items = graph->global_vertices;
+  for (auto* s : sampler->ssg->sampled_sgs) items = std::max<uint64_t>({items, s->e_cap, s->v_cap});
+  hip_check(nts_hip_ctx_reserve(cs->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
+  init_nn();
+}
+
+GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
+  for (auto& e : ev_pool_) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  for (auto* p : P) delete p;
+}
+
+std::pair<hipEvent_t, hipEvent_t>& GCN_SAMPLE_ALLGPU_impl::next_events() {
+  if (ev_pending_ == ev_pool_.size()) {
+    hipEvent_t a, b;
+    TORCH_CHECK(hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess,
+                "hipEventCreate");
+    ev_pool_.push_back({a, b});
+  }
+  return ev_pool_[ev_pending_++];
+}
+
+// Sum the bottom-aggregation kernel times recorded since the last call
+// (synchronises on the last event; call outside the timed loop).
+double GCN_SAMPLE_ALLGPU_impl::resolve_profile() {
+  if (ev_pending_ == 0) return agg_ms;
+  TORCH_CHECK(hipEventSynchronize(ev_pool_[ev_pending_ - 1].second) == hipSuccess,
+              "hipEventSynchronize");
+  for (size_t i = 0; i < ev_pending_; ++i) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ev_pool_[i].first, ev_pool_[i].second);
+    agg_ms += ms;
+  }
+  ev_pending_ = 0;
+  return agg_ms;
+}
+
+void GCN_SAMPLE_ALLGPU_impl::init_nn() {
+  for (size_t i = 0; i + 1 < cfg.layer_size.size(); ++i)
+    P.push_back(new Parameter(cfg.layer_size[i], cfg.layer_size[i + 1], cfg.learn_rate, cfg.beta1,
+                              cfg.beta2, cfg.epsilon, cfg.weight_decay, graph->device,
+                              cfg.seed + (int64_t)i));
+  int64_t n = 0;
+  for (auto* p : P) n += p->W.numel();
+  grad_bucket = torch::zeros({n}, f32_opts(graph->device));
+  if (comm) {  // identical initial weights on every rank (init_parameter / Bcast)
+    torch::NoGradGuard ng;
+    for (auto* p : P) comm->broadcast(p->W.data_ptr<float>(), (uint64_t)p->W.numel(), 0, cs->stream());
+  }
+}
+
+void GCN_SAMPLE_ALLGPU_impl::set_weights(const std::vector<NtsVar>& ws) {
+  TORCH_CHECK(ws.size() == P.size(), "one tensor per layer");
+  torch::NoGradGuard ng;
+  for (size_t i = 0; i < P.size(); ++i) P[i]->W.copy_(ws[i]);
+}
+
+std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::weights() const {
+  std::vector<NtsVar> out;
+  for (auto* p : P) out.push_back(p->W.detach().clone());
+  return out;
+}
+
+// vertexForward (toolkits/GCN_SAMPLE_GPU.hpp:252-266): hidden layers
+// dropout(relu(XW)), the last layer log_softmax(XW).
+NtsVar GCN_SAMPLE_ALLGPU_impl::vertexForward(int l, NtsVar& a) {
+  const int L = (int)P.size();
+  if (l == L - 1) return P[l]->forward(a).log_softmax(1);
+  return torch::dropout(torch::relu(P[l]->forward(a)), cfg.drop_rate, ctx.is_train());
+}
+
+std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool keep) {
+  const int L = (int)P.size();
+  std::vector<NtsVar> acts;
+  NtsVar X0;
+  if (!cfg.fused_gather) sampler->load_feature_gpu(*cs, sg, X0, F);
+  NtsVar X = X0;
+  for (int l = 0; l < L; ++l) {
+    const int hop = L - 1 - l;
+    NtsVar Y;
+    const bool bottom = (l == 0);
+    std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
+    if (bottom && cfg.profile) {
+      if (ev_pending_ >= 4096) resolve_profile();
+      evp = &next_events();
+      (void)hipEventRecord(evp->first, (hipStream_t)cs->stream());
+    }
+    if (bottom && cfg.fused_gather)
+      Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true);
+    else
+      Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(X, sg, graph.get(), hop, cs.get(), false);
+    if (bottom) {
+      sampCSC* s = sg->sampled_sgs[hop];
+      const double Fd = (double)F.size(1);
+      // compulsory bytes: distinct src rows once, index+weight per edge,
+      // offsets, output rows (+ source map when fused)   
+      agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
+                   Fd * 4.0 * s->v_size + (cfg.fused_gather ? 4.0 * s->src_size : 0.0);
+      agg_calls += 1;
+      if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
+    }
+    X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(l, a); }, Y);
+    if (keep) {
+      acts.push_back(Y.detach());
+      acts.push_back(X.detach());
+    }
+  }
+  acts.push_back(X);
+  return acts;
+}
+
+void GCN_SAMPLE_ALLGPU_impl::Loss(NtsVar& left, NtsVar& right) {
+  NtsVar a = left.log_softmax(1);
+  loss = torch::nll_loss(a, right);
+  if (ctx.training) ctx.appendNNOp(left, loss);
+}
+
+void GCN_SAMPLE_ALLGPU_impl::Update() {
+  // GCN_SAMPLE_ALL_MULTI::Update (toolkits/GCN_SAMPLE_ALL_MULTI.hpp:367-377):
+  // SUM all-reduce of every W.grad — one fused RCCL call over a flat bucket.
+  if (comm && comm->nranks > 1) {
+    torch::NoGradGuard ng;
+    int64_t off = 0;
+    for (auto* p : P) {
+      const int64_t n = p->W.numel();
+      grad_bucket.narrow(0, off, n).copy_(p->W.grad().reshape({-1}));
+      off += n;
+    }
+    comm->allreduce_sum(grad_bucket.data_ptr<float>(), (uint64_t)grad_bucket.numel(), cs->stream());
+    off = 0;
+    for (auto* p : P) {
+      const int64_t n = p->W.numel();
+      p->W.mutable_grad().copy_(grad_bucket.narrow(0, off, n).view(p->W.sizes()));
+      off += n;
+    }
+  }
+  for (auto* p : P) {
+    if (cfg.bias_correction) p->learnC2C_with_decay_Adam(*cs);
+    else p->learn_local_with_decay_Adam(*cs);
+    p->next();
+  }
+}
+
+float GCN_SAMPLE_ALLGPU_impl::train_batch() {
+  double t0 = now_s();
+  SampledSubgraph* sg = sampler->sample_gpu_fast(cfg.batch_size, 0, *cs, cfg.weight_type);
+  double t1 = now_s();
+  sampler->load_label_gpu(*cs, sg, target, L_GT);
+  ctx.train();
+  auto acts = forward(sg, false);
+  NtsVar out = acts.back();
+  Loss(out, target);
+  ctx.self_backward(false);
+  Update();
+  for (auto* p : P) p->zero_grad();
+  double t2 = now_s();
+  sample_time += t1 - t0;
+  train_time += t2 - t1;
+  for (int l = 0; l < sg->layers; ++l) batch_edges += sg->sampled_sgs[l]->e_size;
+  ++batches;
+  return 0.f;  // the loss stays on the device (no per-step host sync)
+}
+
+float GCN_SAMPLE_ALLGPU_impl::run_epoch() {
+  sampler->restart();
+  float l = 0;
+  while (sampler->sample_not_finished()) l = train_batch();
+  return l;
+}
+
+std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<VertexId>& seeds,
+                                                         uint64_t batch_seq) {
+  const int L = (int)P.size();
+  std::vector<bool> csr(L, false);
+  FastSampler s(graph, seeds, L, (int)seeds.size(), cfg.fanout, 1, csr,
+                cfg.weight_type != WeightType::None);
+  s.rng_mode = cfg.rng_mode;
+  s.batch_seq = batch_seq;
+  SampledSubgraph* sg = s.sample_gpu_fast((int)seeds.size(), 0, *cs, cfg.weight_type);
+  ctx.eval();
+  torch::NoGradGuard ng;
+  auto acts = forward(sg, true);
+  acts.pop_back();
+  ctx.train();
+  cs->synchronize();
+  return acts;
+}
+
+void GCN_SAMPLE_ALLGPU_impl::reset_stats() {
+  resolve_profile();
+  sample_time = train_time = agg_ms = agg_bytes = 0;
+  batch_edges = 0;
+  batches = agg_calls = 0;
+}
+
+}  // namespace nts

@@ -1,0 +1,63 @@
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include "nts_host.hpp"
+
+namespace nts {
+
+struct GCNConfig {
+  std::vector<int> layer_size;  // LAYERS, e.g. 602-128-41
+  std::vector<int> fanout;      // FANOUT, layer 0 = nearest the seeds
+  int batch_size = 1024;        // BATCH_SIZE
+  float learn_rate = 0.01f, weight_decay = 1e-4f, drop_rate = 0.5f;
+  float beta1 = 0.9f, beta2 = 0.999f, epsilon = 1e-9f;  // toolkits/GCN_SAMPLE_GPU.hpp:115-117
+  int rng_mode = NTS_RNG_PHILOX;
+  WeightType weight_type = WeightType::Sum;  // GraphSAGE toolkits: Mean
+  bool fused_gather = true;           // gather features inside the bottom aggregation
+  bool bias_correction = false;       // false: learn_local_with_decay_Adam (GPU drivers)
+  bool deterministic_backward = true; // CSR transpose gather instead of atomics
+  bool shuffle = true;
+  bool profile = false;               // HIP events around the bottom aggregation
+  int64_t seed = 2000;
+};
+
+class GCN_SAMPLE_ALLGPU_impl {
+ public:
+  GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g, NtsVar feature, NtsVar label,
+                         std::vector<VertexId> train_nids, GCNConfig cfg,
+                         std::shared_ptr<Communicator> comm = nullptr);
+  ~GCN_SAMPLE_ALLGPU_impl();
+
+  void init_nn();
+  float train_batch();
+  float run_epoch();
+  // eval-mode forward over a given seed batch: [Y_0, X_1, Y_1, X_2, ...]
+  std::vector<NtsVar> forward_eval(const std::vector<VertexId>& seeds, uint64_t batch_seq);
+  void set_weights(const std::vector<NtsVar>& ws);
+  std::vector<NtsVar> weights() const;
+  void reset_stats();
+  double resolve_profile();
+
+  std::shared_ptr<FullyRepGraph> graph;
+  NtsVar F, L_GT, target, loss, grad_bucket;
+  GCNConfig cfg;
+  std::shared_ptr<Communicator> comm;
+  std::unique_ptr<NtsStream> cs;
+  std::unique_ptr<FastSampler> sampler;
+  std::vector<Parameter*> P;
+  ctx::NtsContext ctx;
+  // statistics
+  double sample_time = 0, train_time = 0, agg_ms = 0, agg_bytes = 0;
+  uint64_t batch_edges = 0, batches = 0, agg_calls = 0;
+
+ private:
+  NtsVar vertexForward(int l, NtsVar& a);
+  std::vector<NtsVar> forward(SampledSubgraph* sg, bool keep);
+  void Loss(NtsVar& left, NtsVar& right);
+  void Update();
+  std::pair<hipEvent_t, hipEvent_t>& next_events();
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool_;
+  size_t ev_pending_ = 0;
+};
+
+}  // namespace nts

@@ -1,0 +1,310 @@
+// C++ host layer (libtorch-ROCm) over the C-ABI in include/nts_hip.h.
+//
+// Mirrors the reference's operator / sampler surface so a toolkit written
+// against it reads the same:
+//   FullyRepGraph           core/FullyRepGraph.hpp:682-798   (HBM-resident here)
+//   sampCSC / SampledSubgraph core/coocsc.hpp:24-462, core/FullyRepGraph.hpp:30-681
+//   FastSampler             core/ntsFastSampler.hpp:28-1326  (GPU ctor + sample_gpu_fast)
+//   nts::op::ntsGraphOp     core/ntsBaseOp.hpp:28-45
+//   SingleGPUAllSampleGraphOp / SingleGPUSampleGraphOp  core/ntsSingleGPUSampleGraphOp.hpp:50-294
+//   nts::ctx::NtsContext    core/ntsContext.hpp:95-680
+//   Parameter               core/NtsScheduler.hpp:680-1029
+//   Cuda_Stream             cuda/ntsCUDA.hpp:177-595  -> NtsStream (one nts_hip_ctx)
+// Errors from the C-ABI throw std::runtime_error (the reference aborts).
+#pragma once
+
+#include <torch/torch.h>
+
+#include <functional>
+#include <memory>
+#include <stack>
+#include <string>
+#include <vector>
+
+#include "nts_hip.h"
+
+typedef uint32_t VertexId;
+typedef float ValueType;
+typedef torch::Tensor NtsVar;
+
+enum class WeightType { Sum, Mean, None };
+
+namespace nts {
+
+void hip_check(int rc, const char* what);
+
+// torch dtype used to store uint32 vertex ids (bit pattern kept)
+inline torch::TensorOptions u32_opts(int device) {
+  return torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, device);
+}
+inline torch::TensorOptions f32_opts(int device) {
+  return torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
+}
+template <typename T>
+inline T* dptr(const torch::Tensor& t) {
+  return t.defined() ? reinterpret_cast<T*>(t.data_ptr()) : nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// Cuda_Stream equivalent: one C-ABI context bound to one HIP stream.
+// ---------------------------------------------------------------------------
+class NtsStream {
+ public:
+  // stream == nullptr: torch's current stream on `device`.
+  NtsStream(int device, void* stream, uint64_t seed);
+  ~NtsStream();
+  NtsStream(const NtsStream&) = delete;
+  NtsStream& operator=(const NtsStream&) = delete;
+  void setNewStream(void* stream);  // Cuda_Stream::setNewStream
+  void* stream() const;
+  nts_hip_ctx* ctx() const { return ctx_; }
+  int device() const { return device_; }
+  void synchronize() const;
+
+ private:
+  nts_hip_ctx* ctx_ = nullptr;
+  int device_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// FullyRepGraph: replicated global CSC + degrees in HBM.
+// ---------------------------------------------------------------------------
+class FullyRepGraph {
+ public:
+  VertexId global_vertices = 0;
+  uint64_t global_edges = 0;
+  int device = 0;
+  torch::Tensor column_offset;  // int64 [V+1]
+  torch::Tensor row_indices;    // int32 [E]
+  torch::Tensor in_degree;      // int32 [V]  in_degree_for_backward
+  torch::Tensor out_degree;     // int32 [V]  out_degree_for_backward
+
+  // GenerateAll/ReadRepGraphFromRawFile from an edge list already on the device
+  // (src/dst int32 tensors in file order), degrees from the same list.
+  static std::shared_ptr<FullyRepGraph> from_edges(NtsStream& cs, const torch::Tensor& src,
+                                                   const torch::Tensor& dst, VertexId vertices);
+  // Wrap an existing device CSC (+ degrees).
+  static std::shared_ptr<FullyRepGraph> from_csc(torch::Tensor column_offset,
+                                                 torch::Tensor row_indices,
+                                                 torch::Tensor in_degree, torch::Tensor out_degree);
+  nts_graph_dev dev() const;
+};
+
+// ---------------------------------------------------------------------------
+// sampCSC: one sampled layer, device arrays sized by capacity (the
+// reference's dev_* mirrors + its global_data_buffer arena in one).
+// ---------------------------------------------------------------------------
+class sampCSC {
+ public:
+  VertexId v_size = 0, e_size = 0, src_size = 0;  // live sizes (host copy)
+  VertexId v_cap = 0, e_cap = 0, s_cap = 0;
+  bool has_csr = false;
+  torch::Tensor destination, column_offset, row_indices, sample_ans, edge_dst, source,
+      edge_weight_forward, row_offset, column_indices, edge_weight_backward, sizes;
+  torch::Tensor dst_count;  // layer-0 device scalar holding v_size (seeds)
+
+  sampCSC(int device, VertexId v_cap, VertexId e_cap, VertexId s_cap, bool csr, bool weights);
+  // the reference accessor names
+  VertexId* dev_dst() const { return dptr<VertexId>(destination); }
+  VertexId* dev_src() const { return dptr<VertexId>(source); }
+  VertexId* dev_c_o() const { return dptr<VertexId>(column_offset); }
+  VertexId* dev_r_i() const { return dptr<VertexId>(row_indices); }
+  VertexId* dev_r_o() const { return dptr<VertexId>(row_offset); }
+  VertexId* dev_c_i() const { return dptr<VertexId>(column_indices); }
+  ValueType* dev_e_w_f() const { return dptr<ValueType>(edge_weight_forward); }
+  ValueType* dev_e_w_b() const { return dptr<ValueType>(edge_weight_backward); }
+  ValueType* dev_e_w() const { return dptr<ValueType>(edge_weight_forward); }
+  const VertexId* dev_v_size() const { return dptr<VertexId>(sizes); }
+  const VertexId* dev_e_size() const { return dptr<VertexId>(sizes) + 1; }
+  const VertexId* dev_src_size() const { return dptr<VertexId>(sizes) + 2; }
+  // host copies (debug / tests): destination(), src(), c_o(), r_i(), ...
+  std::vector<VertexId> host_u32(const torch::Tensor& t, size_t n) const;
+};
+
+class SampledSubgraph {
+ public:
+  std::vector<sampCSC*> sampled_sgs;
+  int layers = 0;
+  std::vector<int> fanout;
+  torch::Tensor host_sizes;  // pinned int32 [layers*4]
+  SampledSubgraph(int device, int layers, const std::vector<int>& fanout, VertexId batch,
+                  VertexId vertices, uint64_t edges, const std::vector<bool>& csr,
+                  bool weights);
+  ~SampledSubgraph();
+};
+
+// ---------------------------------------------------------------------------
+// FastSampler (GPU form): sample_gpu_fast runs every hop on the device, with
+// one D2H copy of the layer sizes per batch.
+// ---------------------------------------------------------------------------
+class FastSampler {
+ public:
+  std::shared_ptr<FullyRepGraph> whole_graph;
+  VertexId work_range[2] = {0, 0};
+  VertexId work_offset = 0;
+  int layer = 0;
+  std::vector<int> fanout;
+  std::vector<VertexId> sample_nids;
+  SampledSubgraph* ssg = nullptr;
+  std::vector<SampledSubgraph*> ssgs;
+  int rng_mode = NTS_RNG_PHILOX;
+  uint64_t batch_seq = 0;  // keys the PHILOX stream (one per sampled batch)
+  double all_time = 0;     // sampler wall time (reference `all_time`)
+  uint64_t sampled_edges = 0;
+
+  // GPU ctor (core/ntsFastSampler.hpp:125-176).  csr_layers: which hops need
+  // the CSR transpose (backward); empty = all.
+  FastSampler(std::shared_ptr<FullyRepGraph> g, const std::vector<VertexId>& index, int layers,
+              int batch_size, const std::vector<int>& fanout, int pipeline_num = 1,
+              std::vector<bool> csr_layers = {}, bool weights = true);
+  ~FastSampler();
+
+  SampledSubgraph* sample_gpu_fast(int batch_size, int ssg_id, NtsStream& cs,
+                                   WeightType w = WeightType::Sum);
+  bool sample_not_finished() const { return work_offset < work_range[1]; }
+  void restart() { work_offset = work_range[0]; }
+  void set_sample_nids(const std::vector<VertexId>& ids);
+
+  // load_feature_gpu / load_label_gpu (core/ntsFastSampler.hpp:244-261, 414-426)
+  void load_feature_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_feature,
+                        const NtsVar& global_feature);
+  void load_label_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_label,
+                      const NtsVar& global_label);
+
+ private:
+  torch::Tensor dev_nids_;  // device copy of sample_nids
+  VertexId batch_cap_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// graph operators
+// ---------------------------------------------------------------------------
+namespace op {
+
+class ntsGraphOp {
+ public:
+  virtual ~ntsGraphOp() = default;
+  virtual NtsVar forward(NtsVar& f_input) = 0;
+  virtual NtsVar forward(NtsVar& f_input, std::vector<VertexId> cacheflag) {
+    (void)cacheflag;
+    return forward(f_input);
+  }
+  virtual NtsVar backward(NtsVar& output_grad) = 0;
+  bool output_requires_grad = true;
+};
+
+// SingleGPUAllSampleGraphOp (core/ntsSingleGPUSampleGraphOp.hpp:195-294):
+// forward Y = A^T X over the sampled CSC (hand kernel instead of cuSPARSE);
+// backward through the CSR transpose when the sampler built it
+// (deterministic), otherwise the atomic CSC scatter (Push_From_Dst_To_Src).
+// With `gather_from_table`, f_input is the global feature table and rows are
+// fetched through the layer's `source` (fused load_feature_gpu + aggregate).
+class SingleGPUAllSampleGraphOp : public ntsGraphOp {
+ public:
+  SingleGPUAllSampleGraphOp(SampledSubgraph* subgraphs, FullyRepGraph* graph, int layer,
+                            NtsStream* cs, bool gather_from_table = false);
+  NtsVar forward(NtsVar& f_input) override;
+  NtsVar backward(NtsVar& f_output_grad) override;
+
+  SampledSubgraph* subgraphs;
+  int layer;
+  NtsStream* cuda_stream;
+  bool gather_from_table;
+};
+
+// SingleGPUSampleGraphOp (core/ntsSingleGPUSampleGraphOp.hpp:50-176): same
+// forward; backward always through the CSR (row_offset/column_indices/e_w_b).
+class SingleGPUSampleGraphOp : public SingleGPUAllSampleGraphOp {
+ public:
+  using SingleGPUAllSampleGraphOp::SingleGPUAllSampleGraphOp;
+  NtsVar backward(NtsVar& f_output_grad) override;
+};
+
+}  // namespace op
+
+// ---------------------------------------------------------------------------
+// autodiff context (core/ntsContext.hpp)
+// ---------------------------------------------------------------------------
+namespace ctx {
+
+enum OpType { NNOP = 0, GRAPHOP = 1 };
+
+class NtsContext {
+ public:
+  NtsContext();
+  ~NtsContext();
+
+  template <typename GOPT, typename... Args>
+  NtsVar runGraphOp(NtsVar& f_input, Args&&... args) {
+    auto* curr = new GOPT(std::forward<Args>(args)...);
+    // The bottom graph op's input never needs a gradient (its backward is
+    // skipped, core/ntsContext.hpp:443-444); its output then needs none either,
+    // which spares autograd the dense dY of the first GEMM.
+    curr->output_requires_grad = !(training && count == 0);
+    NtsVar f_output = curr->forward(f_input);
+    push_graph_op(curr, f_input, f_output);
+    return f_output;
+  }
+  NtsVar runVertexForward(const std::function<NtsVar(NtsVar&, NtsVar&)>& fn, NtsVar& nbr_input,
+                          NtsVar& vtx_input);
+  NtsVar runVertexForward(const std::function<NtsVar(NtsVar&)>& fn, NtsVar& nbr_input);
+  void appendNNOp(NtsVar& input_t, NtsVar& output_t);
+  void self_backward(bool retain_graph = true);
+  void reset();
+  void train() { training = true; }
+  void eval() { training = false; }
+  bool is_train() const { return training; }
+
+  bool training = true;
+  int count = 0;
+
+ private:
+  struct Entry {
+    OpType type;
+    op::ntsGraphOp* op;  // owned (GRAPHOP)
+    NtsVar input, output, output_grad;
+    void* in_id;
+    void* out_id;
+  };
+  void push_graph_op(op::ntsGraphOp* op, NtsVar& in, NtsVar& out);
+  void pop_one_op();
+  std::vector<Entry> ops_;
+};
+
+}  // namespace ctx
+
+// ---------------------------------------------------------------------------
+// Parameter (core/NtsScheduler.hpp:680-1029), Adam via the fused HIP kernel.
+// ---------------------------------------------------------------------------
+struct Parameter {
+  NtsVar W, M, V;
+  int row, col;
+  ValueType alpha, beta1, beta2, epsilon, weight_decay;
+  ValueType beta1_t, beta2_t;
+  int curr_epoch = 0;
+  Parameter(size_t w, size_t h, ValueType alpha, ValueType beta1, ValueType beta2,
+            ValueType epsilon, ValueType weight_decay, int device, int64_t init_seed);
+  NtsVar forward(const NtsVar& x) const { return x.matmul(W); }
+  // Parameter::learnC2C_with_decay_Adam (bias-corrected, CPU driver semantics)
+  void learnC2C_with_decay_Adam(NtsStream& cs);
+  // Parameter::learn_local_with_decay_Adam (GPU drivers, no bias correction)
+  void learn_local_with_decay_Adam(NtsStream& cs);
+  void next();
+  void zero_grad();
+};
+
+// RCCL communicator (NCCL_Communicator replacement) — one per process.
+class Communicator {
+ public:
+  Communicator(int nranks, int rank, const std::vector<uint8_t>& uid, int device);
+  ~Communicator();
+  void allreduce_sum(float* buf, uint64_t n, void* stream);
+  void broadcast(float* buf, uint64_t n, int root, void* stream);
+  static std::vector<uint8_t> unique_id();
+  int nranks, rank;
+
+ private:
+  nts_hip_comm* comm_ = nullptr;
+};
+
+}  // namespace nts
