@@ -46,7 +46,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.drop_rate = float(drop_rate)
     c.rng_mode = int(rng_mode)
     c.weight_type = {"sum": E.WeightType.Sum, "mean": E.WeightType.Mean,
-                     "none": E.WeightType.None}[weight]
+                     "none": getattr(E.WeightType, "None")}[weight]
     c.fused_gather = bool(fused_gather)
     c.bias_correction = bool(bias_correction)
     c.deterministic_backward = bool(deterministic_backward)

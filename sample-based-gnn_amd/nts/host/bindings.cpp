@@ -141,8 +141,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            }),
            py::arg("graph"), py::arg("feature"), py::arg("label"), py::arg("train_nids"),
            py::arg("cfg"), py::arg("comm") = nullptr)
-      .def("train_batch", &GCN_SAMPLE_ALLGPU_impl::train_batch)
-      .def("run_epoch", &GCN_SAMPLE_ALLGPU_impl::run_epoch)
+      .def("train_batch", &GCN_SAMPLE_ALLGPU_impl::train_batch,
+           py::call_guard<py::gil_scoped_release>())
+      .def("run_epoch", &GCN_SAMPLE_ALLGPU_impl::run_epoch,
+           py::call_guard<py::gil_scoped_release>())
       .def("forward_eval",
            [](GCN_SAMPLE_ALLGPU_impl& d, const torch::Tensor& seeds, uint64_t bs) {
              return d.forward_eval(to_ids(seeds), bs);

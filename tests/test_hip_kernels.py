@@ -295,13 +295,13 @@ def test_adam_matches_reference_torch_expressions(hip, bias_correction):
                  float(b1t), float(b2t), bias_correction)
         b1t, b2t = np.float32(b1t * b1), np.float32(b2t * b2)
     torch.cuda.synchronize()
-    # M/V: bit-exact vs the reference's torch expressions.  W: torch's CPU
-    # sqrt is not correctly rounded on AVX512 hosts (1-ulp differences), so W
-    # is compared bit-exactly with an IEEE float32 restatement and to 2 ulp
-    # with torch.
-    assert torch.equal(m.cpu(), M)
-    assert torch.equal(v.cpu(), Vv)
-    np.testing.assert_array_max_ulp(w.cpu().numpy(), W.numpy(), maxulp=2)
+    # torch's CPU sqrt is not correctly rounded on AVX512 hosts (1-ulp
+    # differences that then feed the next step), so the kernel is compared
+    # bit-exactly with an IEEE float32 restatement of the same expressions and
+    # to fp32 tolerance with the reference's torch expressions.
+    torch.testing.assert_close(w.cpu(), W, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(m.cpu(), M, rtol=1e-5, atol=1e-9)
+    torch.testing.assert_close(v.cpu(), Vv, rtol=1e-5, atol=1e-12)
     Wn, Mn, Vn = W0.copy(), np.zeros_like(W0), np.zeros_like(W0)
     b1t, b2t = np.float32(b1), np.float32(b2)
     one = np.float32(1)
@@ -319,3 +319,5 @@ def test_adam_matches_reference_torch_expressions(hip, bias_correction):
             Wn = Wn - (alpha * Mn) / (np.sqrt(Vn) + eps)
         b1t, b2t = np.float32(b1t * b1), np.float32(b2t * b2)
     assert np.array_equal(w.cpu().numpy(), Wn)
+    assert np.array_equal(m.cpu().numpy(), Mn)
+    assert np.array_equal(v.cpu().numpy(), Vn)
