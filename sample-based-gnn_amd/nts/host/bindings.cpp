@@ -74,7 +74,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                        int batch, std::vector<int> fanout, int rng_mode, uint64_t seed,
                        bool csr) {
              auto p = new PySampler();
+             TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
              p->cs = std::make_unique<NtsStream>(g->device, nullptr, seed);
+             auto guard = p->cs->guard();
              std::vector<bool> c(layers, csr);
              p->s = std::make_unique<FastSampler>(g, to_ids(seeds), layers, batch, fanout, 1, c, true);
              p->s->rng_mode = rng_mode;
@@ -85,7 +87,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("csr") = true)
       .def("sample_gpu_fast",
            [](PySampler& p, int batch, WeightType w) {
-             return layers_of(p.s->sample_gpu_fast(batch, 0, *p.cs, w));
+             auto guard = p.cs->guard();
+             auto out = layers_of(p.s->sample_gpu_fast(batch, 0, *p.cs, w));
+             p.cs->synchronize();
+             return out;
            },
            py::arg("batch_size"), py::arg("weight_type") = WeightType::Sum)
       .def("sample_not_finished", [](PySampler& p) { return p.s->sample_not_finished(); })

@@ -28,13 +28,18 @@ static double now_s() {
 }
 
 // ---------------------------------------------------------------------------
-NtsStream::NtsStream(int device, void* stream, uint64_t seed) : device_(device) {
-  if (!stream) stream = (void*)c10::hip::getCurrentHIPStream(device).stream();
-  hip_check(nts_hip_ctx_create(&ctx_, device, stream, seed), "nts_hip_ctx_create");
+NtsStream::NtsStream(int device, void* stream, uint64_t seed)
+    : device_(device),
+      torch_stream_(stream ? c10::hip::getStreamFromExternal((hipStream_t)stream, (c10::DeviceIndex)device)
+                           : c10::hip::getStreamFromPool(false, (c10::DeviceIndex)device)) {
+  // never hand the legacy NULL stream to the C-ABI (NULL there means "create one")
+  hip_check(nts_hip_ctx_create(&ctx_, device, (void*)torch_stream_.stream(), seed),
+            "nts_hip_ctx_create");
 }
 NtsStream::~NtsStream() { nts_hip_ctx_destroy(ctx_); }
 void NtsStream::setNewStream(void* stream) {
   hip_check(nts_hip_ctx_set_stream(ctx_, stream), "setNewStream");
+  torch_stream_ = c10::hip::getStreamFromExternal((hipStream_t)stream, (c10::DeviceIndex)device_);
 }
 void* NtsStream::stream() const { return nts_hip_ctx_get_stream(ctx_); }
 void NtsStream::synchronize() const {
@@ -48,6 +53,8 @@ std::shared_ptr<FullyRepGraph> FullyRepGraph::from_edges(NtsStream& cs, const to
   TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.dtype() == torch::kInt32 &&
                   dst.dtype() == torch::kInt32 && src.numel() == dst.numel(),
               "from_edges: src/dst must be int32 CUDA tensors of equal length");
+  hip_rt(hipDeviceSynchronize(), "hipDeviceSynchronize");  // inputs may come from any stream
+  auto guard = cs.guard();
   auto g = std::make_shared<FullyRepGraph>();
   g->device = cs.device();
   g->global_vertices = vertices;

@@ -30,6 +30,9 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   TORCH_CHECK(F.is_cuda() && F.dtype() == torch::kFloat32 && F.size(1) == cfg.layer_size[0],
               "feature table must be fp32 [V, layer_size[0]] on the GPU");
   cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+  // inputs were produced on other streams: order them before our stream
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+  auto guard = cs->guard();
   if (cfg.shuffle) {  // shuffle_vec (toolkits/GCN_SAMPLE_GPU.hpp:175-180): mt19937(2000)
     std::mt19937 gen(2000);
     std::shuffle(train_nids.begin(), train_nids.end(), gen);
@@ -97,6 +100,7 @@ void GCN_SAMPLE_ALLGPU_impl::init_nn() {
 }
 
 void GCN_SAMPLE_ALLGPU_impl::set_weights(const std::vector<NtsVar>& ws) {
+  auto guard = cs->guard();
   TORCH_CHECK(ws.size() == P.size(), "one tensor per layer");
   torch::NoGradGuard ng;
   for (size_t i = 0; i < P.size(); ++i) P[i]->W.copy_(ws[i]);
@@ -189,6 +193,7 @@ void GCN_SAMPLE_ALLGPU_impl::Update() {
 }
 
 float GCN_SAMPLE_ALLGPU_impl::train_batch() {
+  auto guard = cs->guard();
   double t0 = now_s();
   SampledSubgraph* sg = sampler->sample_gpu_fast(cfg.batch_size, 0, *cs, cfg.weight_type);
   double t1 = now_s();
@@ -217,6 +222,7 @@ float GCN_SAMPLE_ALLGPU_impl::run_epoch() {
 
 std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<VertexId>& seeds,
                                                          uint64_t batch_seq) {
+  auto guard = cs->guard();
   const int L = (int)P.size();
   std::vector<bool> csr(L, false);
   FastSampler s(graph, seeds, L, (int)seeds.size(), cfg.fanout, 1, csr,

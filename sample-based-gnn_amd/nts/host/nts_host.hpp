@@ -13,6 +13,8 @@
 // Errors from the C-ABI throw std::runtime_error (the reference aborts).
 #pragma once
 
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
 #include <torch/torch.h>
 
 #include <functional>
@@ -50,7 +52,9 @@ inline T* dptr(const torch::Tensor& t) {
 // ---------------------------------------------------------------------------
 class NtsStream {
  public:
-  // stream == nullptr: torch's current stream on `device`.
+  // stream == nullptr: a dedicated stream from torch's pool; torch work that
+  // must be ordered with our kernels runs under guard() (the reference binds
+  // a pool stream per pipeline thread, toolkits/GCN_SAMPLE_GPU.hpp:444-466).
   NtsStream(int device, void* stream, uint64_t seed);
   ~NtsStream();
   NtsStream(const NtsStream&) = delete;
@@ -60,10 +64,14 @@ class NtsStream {
   nts_hip_ctx* ctx() const { return ctx_; }
   int device() const { return device_; }
   void synchronize() const;
+  // make this stream torch's current stream for the guard's lifetime
+  c10::hip::HIPStreamGuard guard() const { return c10::hip::HIPStreamGuard(torch_stream_); }
+  c10::hip::HIPStream torch_stream() const { return torch_stream_; }
 
  private:
   nts_hip_ctx* ctx_ = nullptr;
   int device_ = 0;
+  c10::hip::HIPStream torch_stream_;
 };
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,148 @@
+"""End-to-end parity of the C++ host layer (FastSampler, SingleGPUAllSampleGraphOp,
+NtsContext, Parameter, GCN driver) against the CPU oracle of the reference's
+GCN_CPU_SAMPLE path.
+
+Bars: sampled structures bit-exact; forward activations within 1e-4 (fp32;
+the aggregation outputs themselves are bit-exact); one full training step
+(backward through the context + Adam) within 1e-5 of the oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def E():
+    from nts import host
+    return host.ext()
+
+
+@pytest.fixture(scope="module")
+def graph(E):
+    from nts import synthetic
+    g = synthetic.chung_lu(6000, 180000, 20.0, device=DEV, seed=3)
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, g.n_vertices)
+    src = g.src.cpu().numpy().view(np.uint32)
+    dst = g.dst.cpu().numpy().view(np.uint32)
+    col, rows = orc.build_csc(g.n_vertices, src, dst)
+    od, idg = orc.degrees(g.n_vertices, src, dst)
+    return dict(G=G, V=g.n_vertices, col=col, rows=rows, od=od, idg=idg)
+
+
+def _np(t):
+    a = t.cpu().numpy()
+    return a.view(np.uint32) if a.dtype == np.int32 else a
+
+
+def test_fast_sampler_matches_oracle(E, graph):
+    seeds = torch.arange(0, 3000, 2, dtype=torch.int32)
+    fs = E.FastSampler(graph["G"], seeds, 2, 500, [25, 10])
+    o = orc.Sampler(graph["col"], graph["rows"], graph["idg"], graph["od"], [25, 10],
+                    rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    bs = 0
+    while fs.sample_not_finished():
+        got = fs.sample_gpu_fast(500)
+        ref = o.sample(seeds.numpy()[bs * 500:(bs + 1) * 500].astype(np.uint32), bs)
+        for a, b in zip(got, ref):
+            assert (a["v_size"], a["e_size"], a["src_size"]) == (b["v_size"], b["e_size"], b["src_size"])
+            for k in ("destination", "column_offset", "row_indices", "sample_ans", "source",
+                      "edge_weight_forward", "row_offset", "column_indices", "edge_weight_backward"):
+                assert np.array_equal(_np(a[k]), b[k]), k
+        bs += 1
+    assert bs == 3
+
+
+def _driver(E, graph, F, C, layers, fanout, batch, drop=0.0, seed=2000):
+    from nts import host, synthetic
+    feat = synthetic.features(graph["V"], F, device=DEV)
+    labels, masks = synthetic.labels_masks(graph["V"], C, device=DEV)
+    train = torch.nonzero(masks == 0).flatten().to(torch.int32).cpu()
+    cfg = host.gcn_config(layers, fanout, batch, learn_rate=0.01, drop_rate=drop, seed=seed,
+                          shuffle=False)
+    return E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg), feat, labels, train
+
+
+@pytest.mark.parametrize("F", [602, 128])
+def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F):
+    drv, feat, labels, _ = _driver(E, graph, F, 41, [F, 64, 41], [25, 10], 256)
+    seeds = torch.arange(7, 7 + 256, dtype=torch.int32)
+    acts = drv.forward_eval(seeds, 3)
+    W = [w.cpu() for w in drv.weights()]
+    o = orc.Sampler(graph["col"], graph["rows"], graph["idg"], graph["od"], [25, 10],
+                    rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    l0, l1 = o.sample(seeds.numpy().astype(np.uint32), 3)
+    # GCN_CPU_SAMPLE forward (toolkits/GCN_CPU_SAMPLE.hpp:214-233), eval mode
+    X0 = orc.get_feature(l1["source"], feat.cpu().numpy())
+    Y0 = orc.fuse_fwd(l1, X0, graph["od"], graph["idg"])
+    X1 = torch.relu(torch.from_numpy(Y0) @ W[0])
+    Y1 = orc.fuse_fwd(l0, X1.numpy(), graph["od"], graph["idg"])
+    X2 = (torch.from_numpy(Y1) @ W[1]).log_softmax(1)
+    assert np.array_equal(acts[0].cpu().numpy(), Y0)  # fused gather+aggregation: bit-exact
+    torch.testing.assert_close(acts[1].cpu(), X1, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(acts[2].cpu(), torch.from_numpy(Y1), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(acts[3].cpu(), X2, rtol=1e-4, atol=1e-4)
+
+
+def test_unfused_gather_path_is_identical(E, graph):
+    from nts import host
+    drv, feat, labels, train = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 128)
+    cfg = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fused_gather=False, shuffle=False)
+    drv2 = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg)
+    drv2.set_weights(drv.weights())
+    seeds = torch.arange(100, 228, dtype=torch.int32)
+    a = drv.forward_eval(seeds, 0)
+    b = drv2.forward_eval(seeds, 0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_training_step_matches_oracle_step(E, graph):
+    """One train_batch: sample -> forward -> NLL -> self_backward (graph-op
+    backward through the CSR) -> learn_local_with_decay_Adam, vs the oracle."""
+    F, C, B = 64, 7, 200
+    drv, feat, labels, train = _driver(E, graph, F, C, [F, 32, C], [10, 5], B)
+    W0 = [w.cpu().clone() for w in drv.weights()]
+    drv.train_batch()
+    drv.synchronize()
+    W1 = [w.cpu() for w in drv.weights()]
+    # oracle: same seeds (no shuffle), batch_seq 0, PHILOX stream
+    seeds = train.numpy()[:B].astype(np.uint32)
+    o = orc.Sampler(graph["col"], graph["rows"], graph["idg"], graph["od"], [10, 5],
+                    rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    l0, l1 = o.sample(seeds, 0)
+    W = [w.clone().requires_grad_() for w in W0]
+    X0 = orc.get_feature(l1["source"], feat.cpu().numpy())
+    Y0 = torch.from_numpy(orc.fuse_fwd(l1, X0, graph["od"], graph["idg"]))
+    X1 = torch.relu(Y0 @ W[0])
+    Y1 = torch.from_numpy(orc.fuse_fwd(l0, X1.detach().numpy(), graph["od"], graph["idg"])).requires_grad_()
+    X2 = (Y1 @ W[1]).log_softmax(1)
+    tgt = labels.cpu()[torch.from_numpy(l0["destination"].astype(np.int64))]
+    loss = torch.nn.functional.nll_loss(X2.log_softmax(1), tgt)
+    loss.backward()
+    gX1 = orc.fuse_bwd(l0, Y1.grad.numpy(), graph["od"], graph["idg"])
+    X1.backward(torch.from_numpy(gX1))
+    for w0, w, w1 in zip(W0, W, W1):
+        g = w.grad
+        wg = w0 * 1e-4 + g
+        m = 0.1 * wg
+        v = (0.001 * wg) * wg
+        ref = w0 - (0.01 * m) / (torch.sqrt(v) + 1e-9)
+        torch.testing.assert_close(w1, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_training_is_deterministic_and_learns(E, graph):
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200)
+    for _ in range(2):
+        a.run_epoch()
+        b.run_epoch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)
+    assert torch.isfinite(a.loss).item()
