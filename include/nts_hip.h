@@ -196,6 +196,17 @@ int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx *ctx, const uint32_t *column_offset,
                                 uint64_t ld_gout, uint32_t feature_size, float *g_in,
                                 uint64_t ld_gin);
 
+/* ---- dense layer update (MFMA fp32) -------------------------------------- */
+/* Row-major fp32 GEMM on the matrix cores (v_mfma_f32_32x32x2_f32):
+ *  trans_a == 0: C[M,N] = A[M,K] B[K,N]   — Parameter::forward x.matmul(W)
+ *                (core/NtsScheduler.hpp:859-862)
+ *  trans_a != 0: C[M,N] = A[K,M]^T B[K,N] — the weight gradient Y^T dZ that
+ *                libtorch's matmul backward computes for it.
+ * Long reductions are split over blocks and summed in a fixed order
+ * (deterministic).  May grow the context's scratch arena. */
+int nts_hip_gemm_f32(nts_hip_ctx *ctx, int trans_a, int M, int N, int K, const float *A,
+                     uint64_t lda, const float *B, uint64_t ldb, float *C, uint64_t ldc);
+
 /* ---- optimiser ---------------------------------------------------------- */
 /* Fused Adam step on one parameter (n elements), element-wise identical to
  *  bias_correction != 0: Parameter::learnC2C_with_decay_Adam (core/NtsScheduler.hpp:863-880)

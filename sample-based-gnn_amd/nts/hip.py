@@ -105,6 +105,16 @@ class HipContext:
                                                    v_cap, ptr(g_out), g_out.stride(0), F,
                                                    ptr(g_in), g_in.stride(0)))
 
+    def gemm(self, A, B, C, trans_a=False):
+        """C = A @ B (trans_a: A.T @ B) on the MFMA fp32 kernels."""
+        if trans_a:
+            K, M = A.shape
+        else:
+            M, K = A.shape
+        N = B.shape[1]
+        check(self.lib.nts_hip_gemm_f32(self.h, int(trans_a), M, N, K, ptr(A), A.stride(0), ptr(B),
+                                        B.stride(0), ptr(C), C.stride(0)))
+
     def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
         check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,
                                     beta1, beta2, eps, wd, beta1_t, beta2_t, int(bias_correction)))

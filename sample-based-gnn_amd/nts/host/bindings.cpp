@@ -134,6 +134,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("fused_gather", &GCNConfig::fused_gather)
       .def_readwrite("bias_correction", &GCNConfig::bias_correction)
       .def_readwrite("deterministic_backward", &GCNConfig::deterministic_backward)
+      .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
       .def_readwrite("shuffle", &GCNConfig::shuffle)
       .def_readwrite("profile", &GCNConfig::profile)
       .def_readwrite("seed", &GCNConfig::seed);

@@ -427,6 +427,50 @@ void NtsContext::reset() {
 }  // namespace ctx
 
 // ---------------------------------------------------------------------------
+namespace {
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+struct HipLinearFn : public torch::autograd::Function<HipLinearFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar x, NtsVar W, int64_t cs_ptr) {
+    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    NtsVar xc = x.contiguous(), Wc = W.contiguous();
+    const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
+    TORCH_CHECK(Wc.size(0) == K, "hip_linear: shape mismatch");
+    NtsVar Z = torch::empty({M, N}, xc.options());
+    hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)M, (int)N, (int)K, xc.data_ptr<float>(),
+                               (uint64_t)K, Wc.data_ptr<float>(), (uint64_t)N, Z.data_ptr<float>(),
+                               (uint64_t)N),
+              "nts_hip_gemm_f32(nn)");
+    ctx->save_for_backward({xc, Wc});
+    ctx->saved_data["cs"] = cs_ptr;
+    return Z;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto saved = ctx->get_saved_variables();
+    NtsVar x = saved[0], W = saved[1];
+    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    NtsVar g = grads[0].contiguous();
+    const int64_t M = x.size(0), K = x.size(1), N = W.size(1);
+    NtsVar dx, dW;
+    if (ctx->needs_input_grad(1)) {
+      dW = torch::empty({K, N}, W.options());
+      hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)K, (int)N, (int)M, x.data_ptr<float>(),
+                                 (uint64_t)K, g.data_ptr<float>(), (uint64_t)N,
+                                 dW.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_gemm_f32(tn)");
+    }
+    if (ctx->needs_input_grad(0)) dx = g.matmul(W.t());
+    return {dx, dW, NtsVar()};
+  }
+};
+}  // namespace
+
+NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {
+  return HipLinearFn::apply(x, W, reinterpret_cast<int64_t>(cs));
+}
+
+// ---------------------------------------------------------------------------
 Parameter::Parameter(size_t w, size_t h, ValueType alpha_, ValueType beta1_, ValueType beta2_,
                      ValueType epsilon_, ValueType weight_decay_, int device, int64_t init_seed)
     : row((int)w), col((int)h), alpha(alpha_), beta1(beta1_), beta2(beta2_), epsilon(epsilon_),

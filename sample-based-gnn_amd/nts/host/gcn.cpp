@@ -90,6 +90,8 @@ void GCN_SAMPLE_ALLGPU_impl::init_nn() {
     P.push_back(new Parameter(cfg.layer_size[i], cfg.layer_size[i + 1], cfg.learn_rate, cfg.beta1,
                               cfg.beta2, cfg.epsilon, cfg.weight_decay, graph->device,
                               cfg.seed + (int64_t)i));
+  if (cfg.hip_gemm)
+    for (auto* p : P) p->cs = cs.get();
   int64_t n = 0;
   for (auto* p : P) n += p->W.numel();
   grad_bucket = torch::zeros({n}, f32_opts(graph->device));

@@ -16,6 +16,7 @@ struct GCNConfig {
   bool fused_gather = true;           // gather features inside the bottom aggregation
   bool bias_correction = false;       // false: learn_local_with_decay_Adam (GPU drivers)
   bool deterministic_backward = true; // CSR transpose gather instead of atomics
+  bool hip_gemm = true;               // layer GEMMs on the hand-written MFMA kernels
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
   int64_t seed = 2000;

@@ -284,15 +284,20 @@ class NtsContext {
 // ---------------------------------------------------------------------------
 // Parameter (core/NtsScheduler.hpp:680-1029), Adam via the fused HIP kernel.
 // ---------------------------------------------------------------------------
+// x.matmul(W) on the MFMA fp32 kernels (nts_hip_gemm_f32) with its own
+// backward: dW = x^T dZ (split-reduction, deterministic), dx = dZ W^T.
+NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
+
 struct Parameter {
   NtsVar W, M, V;
+  NtsStream* cs = nullptr;  // set -> forward runs on the hand-written MFMA GEMM
   int row, col;
   ValueType alpha, beta1, beta2, epsilon, weight_decay;
   ValueType beta1_t, beta2_t;
   int curr_epoch = 0;
   Parameter(size_t w, size_t h, ValueType alpha, ValueType beta1, ValueType beta2,
             ValueType epsilon, ValueType weight_decay, int device, int64_t init_seed);
-  NtsVar forward(const NtsVar& x) const { return x.matmul(W); }
+  NtsVar forward(const NtsVar& x) const { return cs ? hip_linear(x, W, cs) : x.matmul(W); }
   // Parameter::learnC2C_with_decay_Adam (bias-corrected, CPU driver semantics)
   void learnC2C_with_decay_Adam(NtsStream& cs);
   // Parameter::learn_local_with_decay_Adam (GPU drivers, no bias correction)

@@ -321,3 +321,28 @@ def test_adam_matches_reference_torch_expressions(hip, bias_correction):
     assert np.array_equal(w.cpu().numpy(), Wn)
     assert np.array_equal(m.cpu().numpy(), Mn)
     assert np.array_equal(v.cpu().numpy(), Vn)
+
+
+@pytest.mark.parametrize("M,N,K", [(150000, 128, 602), (1000, 41, 128), (333, 7, 1433),
+                                   (5, 256, 100), (10000, 47, 256), (1, 1, 1), (64, 128, 0)])
+@pytest.mark.parametrize("trans_a", [False, True])
+def test_gemm_f32_mfma(hip, M, N, K, trans_a):
+    """MFMA fp32 GEMM vs torch fp64 (asymmetric data, ragged tails, long split
+    reductions).  Products are exact fp32, sums fp32 in a fixed order."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
+    if trans_a:  # C[M,N] = A[K,M]^T B[K,N]
+        A = torch.randn(K, M, device=DEV, generator=g)
+    else:
+        A = torch.randn(M, K, device=DEV, generator=g)
+    B = torch.randn(K, N, device=DEV, generator=g) + torch.arange(N, device=DEV) * 0.01
+    C = torch.full((M, N), float("nan"), device=DEV)
+    hip.gemm(A, B, C, trans_a=trans_a)
+    ref = (A.double().t() if trans_a else A.double()) @ B.double()
+    torch.cuda.synchronize()
+    tol = 2e-6 * max(K, 1) ** 0.5 + 1e-6
+    torch.testing.assert_close(C.double(), ref, rtol=tol, atol=tol * 4)
+    # deterministic: a second run is bit-identical
+    C2 = torch.empty_like(C)
+    hip.gemm(A, B, C2, trans_a=trans_a)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
