@@ -84,19 +84,14 @@ def main():
     # DP: contiguous equal slices (remainder dropped so every rank runs the same
     # number of steps; the reference gives it to the last GPU,
     # toolkits/GCN_SAMPLE_ALL_MULTI.hpp:564-575)
-    per = train.numel() // world
-    train = train[rank * per:(rank + 1) * per]
+    from nts import dist as ndist
+    train = ndist.shard_nids(train, world, rank)
     log(f"[bench] graph {args.shape}: V={V} E={En} F={F_dim} C={C}  ready in {time.time()-t0:.1f}s")
     src_host = g.src.cpu().numpy().view(np.uint32) if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
     dst_host = g.dst.cpu().numpy().view(np.uint32) if src_host is not None else None
     del g
 
-    comm = None
-    if world > 1:
-        import torch.distributed as dist
-        uid = [E.Communicator.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = E.Communicator(world, rank, uid[0], local_rank)
+    comm = ndist.make_communicator(E, world, rank, local_rank)
 
     fan = [int(x) for x in args.fanout.split("-")]
     layers = [F_dim, args.hidden, C]
