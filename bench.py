@@ -49,6 +49,8 @@ def parse():
     p.add_argument("--fanout", default="25-10")
     p.add_argument("--hidden", type=int, default=128)
     p.add_argument("--no-fused-gather", action="store_true")
+    p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
+    p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
     p.add_argument("--cpu-baseline-steps", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -97,7 +99,8 @@ def main():
     layers = [F_dim, args.hidden, C]
     cfg = host.gcn_config(layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4,
                           drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX,
-                          fused_gather=not args.no_fused_gather, profile=True)
+                          fused_gather=not args.no_fused_gather, profile=True,
+                          pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm)
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
 
     def step():
@@ -169,8 +172,9 @@ def main():
         "config": {
             "workload": (f"GCN_SAMPLE_ALLGPU-style 2-layer GCN {'-'.join(map(str, layers))}, fanout "
                          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic "
-                         f"(V={V}, E={En}); GPU sampler (Philox) + fused gather/aggregation + "
-                         f"rocBLAS GEMM + fused Adam"),
+                         f"(V={V}, E={En}); GPU sampler (Philox"
+                         f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation + "
+                         f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"),
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}",
             "fanout": args.fanout,

@@ -206,7 +206,7 @@ extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int
   NTS_CHECK_ARG(ctx && C, "NULL argument");
   NTS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return NTS_OK;
-  NTS_CHECK_ARG(A && B, "NULL operand");
+  NTS_CHECK_ARG((A && B) || K == 0, "NULL operand");
   NTS_CHECK_ARG(ldb >= (uint64_t)N && ldc >= (uint64_t)N, "leading dimension");
   NTS_CHECK_ARG(trans_a ? lda >= (uint64_t)M : lda >= (uint64_t)K, "lda");
   NTS_HIP_TRY(hipSetDevice(ctx->device));

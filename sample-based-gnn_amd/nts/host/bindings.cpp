@@ -135,6 +135,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("bias_correction", &GCNConfig::bias_correction)
       .def_readwrite("deterministic_backward", &GCNConfig::deterministic_backward)
       .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
+      .def_readwrite("pipeline", &GCNConfig::pipeline)
       .def_readwrite("shuffle", &GCNConfig::shuffle)
       .def_readwrite("profile", &GCNConfig::profile)
       .def_readwrite("seed", &GCNConfig::seed);
@@ -160,9 +161,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("weights", &GCN_SAMPLE_ALLGPU_impl::weights)
       .def("reset_stats", &GCN_SAMPLE_ALLGPU_impl::reset_stats)
       .def("resolve_profile", &GCN_SAMPLE_ALLGPU_impl::resolve_profile)
-      .def("sample_not_finished",
-           [](GCN_SAMPLE_ALLGPU_impl& d) { return d.sampler->sample_not_finished(); })
-      .def("restart", [](GCN_SAMPLE_ALLGPU_impl& d) { d.sampler->restart(); })
+      .def("sample_not_finished", &GCN_SAMPLE_ALLGPU_impl::has_batch)
+      .def("restart", &GCN_SAMPLE_ALLGPU_impl::restart)
       .def("synchronize", [](GCN_SAMPLE_ALLGPU_impl& d) { d.cs->synchronize(); })
       .def_property_readonly("loss", [](GCN_SAMPLE_ALLGPU_impl& d) { return d.loss; })
       .def_property_readonly("n_train", [](GCN_SAMPLE_ALLGPU_impl& d) { return d.sampler->work_range[1]; })

@@ -158,10 +158,14 @@ SampledSubgraph::SampledSubgraph(int device, int layers_, const std::vector<int>
                                       (VertexId)caps[l][2], c, weights));
   }
   host_sizes = torch::empty({layers * 4}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true));
+  hip_rt(hipEventCreateWithFlags(&sampled, hipEventDisableTiming), "hipEventCreate");
+  hip_rt(hipEventCreateWithFlags(&consumed, hipEventDisableTiming), "hipEventCreate");
 }
 
 SampledSubgraph::~SampledSubgraph() {
   for (auto* s : sampled_sgs) delete s;
+  (void)hipEventDestroy(sampled);
+  (void)hipEventDestroy(consumed);
 }
 
 // ---------------------------------------------------------------------------
@@ -196,12 +200,19 @@ void FastSampler::set_sample_nids(const std::vector<VertexId>& ids) {
 
 SampledSubgraph* FastSampler::sample_gpu_fast(int batch_size, int ssg_id, NtsStream& cs,
                                               WeightType w) {
+  issue_gpu_sample(batch_size, ssg_id, cs, w);
+  return finish_gpu_sample(ssg_id);
+}
+
+void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, WeightType w) {
   double t0 = now_s();
   TORCH_CHECK(work_offset < work_range[1], "sample_gpu_fast: no work left");
   TORCH_CHECK((VertexId)batch_size <= batch_cap_, "batch larger than the sampler's capacity");
+  TORCH_CHECK(ssg_id >= 0 && ssg_id < (int)ssgs.size(), "ssg_id out of range");
   ssg = ssgs[ssg_id];
   const VertexId actual = std::min<VertexId>((VertexId)batch_size, work_range[1] - work_offset);
   hipStream_t st = (hipStream_t)cs.stream();
+  hip_rt(hipStreamWaitEvent(st, ssg->consumed, 0), "hipStreamWaitEvent");
   const nts_graph_dev g = whole_graph->dev();
   const int wt = w == WeightType::Sum ? NTS_WEIGHT_SUM
                                       : (w == WeightType::Mean ? NTS_WEIGHT_MEAN : NTS_WEIGHT_NONE);
@@ -244,7 +255,20 @@ SampledSubgraph* FastSampler::sample_gpu_fast(int batch_size, int ssg_id, NtsStr
     hip_rt(hipMemcpyAsync(hs + 4 * l, dptr<uint32_t>(ssg->sampled_sgs[l]->sizes), 16,
                           hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(sizes)");
-  hip_rt(hipStreamSynchronize(st), "hipStreamSynchronize");
+  hip_rt(hipEventRecord(ssg->sampled, st), "hipEventRecord");
+  ssg->pending_batch = (int)actual;
+  work_offset += actual;
+  ++batch_seq;
+  all_time += now_s() - t0;
+}
+
+SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
+  double t0 = now_s();
+  ssg = ssgs[ssg_id];
+  TORCH_CHECK(ssg->pending_batch > 0, "finish_gpu_sample without a pending issue");
+  hip_rt(hipEventSynchronize(ssg->sampled), "hipEventSynchronize");
+  ssg->pending_batch = 0;
+  const int32_t* hs = ssg->host_sizes.data_ptr<int32_t>();
   for (int l = 0; l < layer; ++l) {
     sampCSC* s = ssg->sampled_sgs[l];
     s->v_size = (VertexId)hs[4 * l];
@@ -253,8 +277,6 @@ SampledSubgraph* FastSampler::sample_gpu_fast(int batch_size, int ssg_id, NtsStr
     TORCH_CHECK(hs[4 * l + 3] == 0, "sampled layer ", l, " exceeded its capacity");
     sampled_edges += s->e_size;
   }
-  work_offset += actual;
-  ++batch_seq;
   all_time += now_s() - t0;
   return ssg;
 }

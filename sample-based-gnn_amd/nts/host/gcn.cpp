@@ -42,13 +42,17 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // outermost, whose backward the context skips)
   std::vector<bool> csr(L, cfg.deterministic_backward);
   csr[L - 1] = false;
-  sampler = std::make_unique<FastSampler>(graph, train_nids, L, cfg.batch_size, cfg.fanout, 1, csr,
+  sampler = std::make_unique<FastSampler>(graph, train_nids, L, cfg.batch_size, cfg.fanout,
+                                          cfg.pipeline ? 2 : 1, csr,
                                           cfg.weight_type != WeightType::None);
   sampler->rng_mode = cfg.rng_mode;
-  // size the scratch arena once so the training loop never allocates
+  if (cfg.pipeline) ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+  // size the scratch arenas once so the training loop never allocates
   uint64_t items = graph->global_vertices;
   for (auto* s : sampler->ssg->sampled_sgs) items = std::max<uint64_t>({items, s->e_cap, s->v_cap});
   hip_check(nts_hip_ctx_reserve(cs->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
+  if (ss)
+    hip_check(nts_hip_ctx_reserve(ss->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
   init_nn();
 }
 
@@ -197,7 +201,25 @@ void GCN_SAMPLE_ALLGPU_impl::Update() {
 float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   auto guard = cs->guard();
   double t0 = now_s();
-  SampledSubgraph* sg = sampler->sample_gpu_fast(cfg.batch_size, 0, *cs, cfg.weight_type);
+  NtsStream& sst = ss ? *ss : *cs;
+  int slot;
+  if (prefetched_ >= 0) {
+    slot = prefetched_;
+    prefetched_ = -1;
+  } else {
+    slot = next_slot_;
+    sampler->issue_gpu_sample(cfg.batch_size, slot, sst, cfg.weight_type);
+  }
+  SampledSubgraph* sg = sampler->finish_gpu_sample(slot);
+  if (ss) {
+    next_slot_ = slot ^ 1;
+    if (sampler->sample_not_finished()) {  // prefetch the next batch behind this one
+      sampler->issue_gpu_sample(cfg.batch_size, next_slot_, *ss, cfg.weight_type);
+      prefetched_ = next_slot_;
+    }
+  }
+  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), sg->sampled, 0) == hipSuccess,
+              "hipStreamWaitEvent");
   double t1 = now_s();
   sampler->load_label_gpu(*cs, sg, target, L_GT);
   ctx.train();
@@ -207,6 +229,8 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   ctx.self_backward(false);
   Update();
   for (auto* p : P) p->zero_grad();
+  TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)cs->stream()) == hipSuccess,
+              "hipEventRecord");
   double t2 = now_s();
   sample_time += t1 - t0;
   train_time += t2 - t1;
@@ -215,10 +239,18 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   return 0.f;  // the loss stays on the device (no per-step host sync)
 }
 
-float GCN_SAMPLE_ALLGPU_impl::run_epoch() {
+void GCN_SAMPLE_ALLGPU_impl::restart() {
+  if (prefetched_ >= 0) {  // drop a prefetched batch of the previous pass
+    sampler->finish_gpu_sample(prefetched_);
+    prefetched_ = -1;
+  }
   sampler->restart();
+}
+
+float GCN_SAMPLE_ALLGPU_impl::run_epoch() {
+  restart();
   float l = 0;
-  while (sampler->sample_not_finished()) l = train_batch();
+  while (has_batch()) l = train_batch();
   return l;
 }
 

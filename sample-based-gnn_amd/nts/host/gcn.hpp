@@ -17,6 +17,7 @@ struct GCNConfig {
   bool bias_correction = false;       // false: learn_local_with_decay_Adam (GPU drivers)
   bool deterministic_backward = true; // CSR transpose gather instead of atomics
   bool hip_gemm = true;               // layer GEMMs on the hand-written MFMA kernels
+  bool pipeline = true;               // sample batch i+1 on its own stream while i trains
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
   int64_t seed = 2000;
@@ -32,6 +33,8 @@ class GCN_SAMPLE_ALLGPU_impl {
   void init_nn();
   float train_batch();
   float run_epoch();
+  bool has_batch() const { return prefetched_ >= 0 || sampler->sample_not_finished(); }
+  void restart();
   // eval-mode forward over a given seed batch: [Y_0, X_1, Y_1, X_2, ...]
   std::vector<NtsVar> forward_eval(const std::vector<VertexId>& seeds, uint64_t batch_seq);
   void set_weights(const std::vector<NtsVar>& ws);
@@ -43,7 +46,8 @@ class GCN_SAMPLE_ALLGPU_impl {
   NtsVar F, L_GT, target, loss, grad_bucket;
   GCNConfig cfg;
   std::shared_ptr<Communicator> comm;
-  std::unique_ptr<NtsStream> cs;
+  std::unique_ptr<NtsStream> cs;  // training stream
+  std::unique_ptr<NtsStream> ss;  // sampling stream (pipeline) — own scratch arena
   std::unique_ptr<FastSampler> sampler;
   std::vector<Parameter*> P;
   ctx::NtsContext ctx;
@@ -59,6 +63,8 @@ class GCN_SAMPLE_ALLGPU_impl {
   std::pair<hipEvent_t, hipEvent_t>& next_events();
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool_;
   size_t ev_pending_ = 0;
+  int prefetched_ = -1;  // slot holding an issued, not yet trained batch
+  int next_slot_ = 0;
 };
 
 }  // namespace nts

@@ -135,6 +135,9 @@ class SampledSubgraph {
   int layers = 0;
   std::vector<int> fanout;
   torch::Tensor host_sizes;  // pinned int32 [layers*4]
+  hipEvent_t sampled = nullptr;   // recorded after the sizes copy of the last issue
+  hipEvent_t consumed = nullptr;  // recorded by the trainer once it is done with the slot
+  int pending_batch = 0;          // seeds of the issued, not yet finished batch
   SampledSubgraph(int device, int layers, const std::vector<int>& fanout, VertexId batch,
                   VertexId vertices, uint64_t edges, const std::vector<bool>& csr,
                   bool weights);
@@ -169,6 +172,13 @@ class FastSampler {
 
   SampledSubgraph* sample_gpu_fast(int batch_size, int ssg_id, NtsStream& cs,
                                    WeightType w = WeightType::Sum);
+  // Split form for pipelining (the reference overlaps with PIPELINE_NUM host
+  // threads, toolkits/GCN_SAMPLE_GPU.hpp:289-394): issue enqueues every hop
+  // and the size copy on `cs` without blocking; finish waits for that batch
+  // and publishes v/e/src sizes.  A slot is reused only after its `consumed`
+  // event (recorded by the trainer) — issue makes `cs` wait for it.
+  void issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, WeightType w);
+  SampledSubgraph* finish_gpu_sample(int ssg_id);
   bool sample_not_finished() const { return work_offset < work_range[1]; }
   void restart() { work_offset = work_range[0]; }
   void set_sample_nids(const std::vector<VertexId>& ids);
