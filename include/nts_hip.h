@@ -105,8 +105,8 @@ typedef struct {
 /* ---- context ------------------------------------------------------------ */
 int nts_hip_abi_version(void);
 const char *nts_hip_last_error(void);
-/* Replaces `new Cuda_Stream()` (cuda/ntsCUDAGraphOP.cu:201-212).  stream may be
- * NULL (a non-blocking stream is created and owned).  seed feeds PHILOX and
+/* Replaces `new Cuda_Stream()` (cuda/ntsCUDAGraphOP.cu:201-212).  `stream` is
+ * used as given; NULL is HIP's legacy default stream.  seed feeds PHILOX and
  * the MT19937 generator (reference: 2000, core/ntsFastSampler.hpp:202). */
 int nts_hip_ctx_create(nts_hip_ctx **ctx, int device, void *stream, uint64_t seed);
 int nts_hip_ctx_destroy(nts_hip_ctx *ctx);

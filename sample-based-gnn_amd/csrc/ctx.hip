@@ -69,17 +69,9 @@ int nts_hip_ctx_create(nts_hip_ctx** out, int device, void* stream, uint64_t see
   nts_hip_ctx* ctx = new nts_hip_ctx();
   ctx->device = device;
   ctx->seed = seed;
-  if (stream) {
-    ctx->stream = (hipStream_t)stream;
-  } else {
-    hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-      set_error("hipStreamCreateWithFlags: %s", hipGetErrorString(e));
-      delete ctx;
-      return NTS_ERR_HIP;
-    }
-    ctx->own_stream = true;
-  }
+  // NULL is HIP's legacy default stream, used as-is (ordered with every other
+  // blocking stream of the device, like torch's default stream).
+  ctx->stream = (hipStream_t)stream;
   hipError_t e = hipMalloc(&ctx->mt_state, 625 * sizeof(uint32_t));
   if (e != hipSuccess) {
     set_error("hipMalloc(mt_state): %s", hipGetErrorString(e));
