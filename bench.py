@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
+    p.add_argument("--no-fuse-linear", action="store_true",
+                   help="bottom layer: aggregation and first GEMM as separate kernels")
     p.add_argument("--cpu-baseline-steps", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -100,7 +102,11 @@ def main():
     cfg = host.gcn_config(layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4,
                           drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX,
                           fused_gather=not args.no_fused_gather, profile=True,
-                          pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm)
+                          pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
+                          fuse_linear=not args.no_fuse_linear)
+    fused_linear = (not args.no_fused_gather and not args.no_fuse_linear and not args.no_hip_gemm
+                    and args.hidden <= 128)
+    agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
 
     def step():
@@ -173,7 +179,8 @@ def main():
             "workload": (f"GCN_SAMPLE_ALLGPU-style 2-layer GCN {'-'.join(map(str, layers))}, fanout "
                          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic "
                          f"(V={V}, E={En}); GPU sampler (Philox"
-                         f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation + "
+                         f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation"
+                         f"{' + layer-1 GEMM' if fused_linear else ''} + "
                          f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"),
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}",
@@ -185,7 +192,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_spmm_gather (fused feature gather + hop-1 aggregation)",
+            "kernel": agg_kernel + (" (feature gather + hop-1 aggregation + layer-1 GEMM)" if fused_linear
+                                    else " (fused feature gather + hop-1 aggregation)"),
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -198,7 +206,9 @@ def main():
     pmc = ROOT / "profiles" / "pmc_r01.json"
     if pmc.exists() and args.shape == "reddit" and args.batch == 10000 and world == 1:
         try:
-            result["roofline"]["traffic"] = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            info = json.loads(pmc.read_text())
+            if info.get("kernel", "").split("<")[0] == agg_kernel:
+                result["roofline"]["traffic"] = info.get("hbm_bytes_per_launch")
         except Exception:
             pass
 

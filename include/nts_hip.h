@@ -178,6 +178,19 @@ int nts_hip_spmm_csc_fwd(nts_hip_ctx *ctx, const uint32_t *column_offset,
                          const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
                          const uint32_t *x_row_map, uint32_t feature_size, float *y,
                          uint64_t ldy);
+/* Fused bottom layer of the GCN step: y = A x (exactly nts_hip_spmm_csc_fwd,
+ * bit-identical; y may be NULL when not needed) and z = y W (W: row-major
+ * [feature_size, out_size], out_size <= 128) on MFMA fp32, in one pass that
+ * overlaps the matrix work with the row gathers.  Replaces the pair
+ * SingleGPUAllSampleGraphOp::forward + Parameter::forward of the first layer
+ * (core/ntsSingleGPUSampleGraphOp.hpp:210-250, core/NtsScheduler.hpp:859-862).
+ * feature_size <= ~1270 (LDS tile of 32 rows). */
+int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                                const uint32_t *row_indices, const float *weight,
+                                const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
+                                const uint32_t *x_row_map, uint32_t feature_size, const float *W,
+                                uint32_t out_size, float *y, uint64_t ldy, float *z,
+                                uint64_t ldz);
 /* G_in[s,:] = sum_{j in [ro[s],ro[s+1])} w_b[j] * G_out[ci[j],:] (ascending dst
  * order, deterministic, atomic-free).  Replaces Gather_By_Src_From_Dst_Spmm
  * (cuda/ntsCUDAGraphOP.cu:901-1042) and MiniBatchFuseOp::backward

@@ -16,7 +16,8 @@ import shutil
 import statistics
 import sys
 
-DOMINANT = "k_spmm_gather<2, 64, 5, true>"
+# dominant kernel: the aggregation kernel with the largest total time
+PREFIXES = ("k_spmm_gather_linear<", "k_spmm_gather<")
 
 
 def load(path):
@@ -49,8 +50,11 @@ def main():
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
         lines.append(f"| `{r['Name'][:80]}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | "
                      f"{float(r['AverageNs'])/1e3:.1f} | {100*float(r['TotalDurationNs'])/tot:.1f} |")
-    dom = [r for r in rows if DOMINANT in r["Name"]]
+    dom = sorted((r for r in rows if r["Name"].startswith(PREFIXES)),
+                 key=lambda r: -float(r["TotalDurationNs"]))
     info = {}
+    DOMINANT = dom[0]["Name"] if dom else "k_spmm_gather<"
+    info["kernel"] = DOMINANT
     if dom:
         info["avg_ns"] = float(dom[0]["AverageNs"])
         info["calls"] = int(dom[0]["Calls"])
@@ -60,7 +64,7 @@ def main():
             continue
         per = pmc_per_kernel(load(p[0]), counter)
         for name, vals in per.items():
-            if DOMINANT in name:
+            if name.split("(")[0].strip() == DOMINANT.split("(")[0].strip():
                 info[counter] = statistics.median(vals)  # KiB per dispatch
     if "FETCH_SIZE" in info and "WRITE_SIZE" in info:
         info["hbm_bytes_per_launch"] = (2 * info["FETCH_SIZE"] + info["WRITE_SIZE"]) * 1024.0

@@ -266,6 +266,166 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   return launch_gather_vec<1, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused bottom layer: Y = A X (gathered through `map`) and Z = Y W in one pass.
+// Tiles of 32 destinations: phase 1 — each wave aggregates 8 rows exactly as
+// k_spmm_gather (same order and arithmetic, so Y is bit-identical), stores
+// them to Y (kept for the weight gradient) and into an LDS tile; phase 2 —
+// each wave multiplies the 32 x F LDS tile by a 32-column slice of W on
+// v_mfma_f32_32x32x2_f32.  The k range is split in halves between the two
+// lane halves of the MFMA (lanes 0-31: k in [0,Kh), lanes 32-63: [Kh,2Kh)),
+// so every lane reads two consecutive k with one conflict-free ds_read_b64
+// (row pitch LDP = 2Kh+2: LDP/2 odd spreads 32 rows over all 64 banks).
+// The gathers dominate (HBM/MALL); the MFMA phase of one block overlaps the
+// gather phase of the other block resident on the CU.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kTM = 32;
+
+template <int VEC, int NCH, bool MAP>
+__global__ __launch_bounds__(kAggThreads, 2) void k_spmm_gather_linear(
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
+    const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
+    const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t F,
+    const float* __restrict__ W, uint32_t N, float* __restrict__ y, uint64_t ldy,
+    float* __restrict__ z, uint64_t ldz, uint32_t Kh, uint32_t LDP) {
+  using V = VT<VEC>;
+  using T = typename V::T;
+  extern __shared__ float sY[];  // [kTM][LDP]
+  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t nv = F / VEC;
+  // zero the k padding [F, LDP) once: it multiplies W rows that are masked to
+  // zero, but LDS garbage could hold Inf/NaN
+  for (uint32_t i = threadIdx.x; i < kTM * (LDP - F); i += blockDim.x) {
+    const uint32_t r = i / (LDP - F), c = F + i % (LDP - F);
+    sY[r * LDP + c] = 0.f;
+  }
+  const uint32_t ntiles = (n + kTM - 1) / kTM;
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // ---- phase 1: aggregation of 32 rows (8 per wave) ----
+    for (int rr = wv; rr < kTM; rr += 4) {
+      const uint32_t d = tile * kTM + rr;
+      float* srow = sY + rr * LDP;
+      if (d >= n) {
+        for (uint32_t c = lane; c < F; c += 64) srow[c] = 0.f;
+        continue;
+      }
+      const uint32_t beg = off[d], end = off[d + 1];
+      T acc[NCH];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
+      uint32_t e = beg;
+      for (; e + kUnroll <= end; e += kUnroll) {
+        uint32_t r[kUnroll];
+        float ww[kUnroll];
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) {
+          r[j] = idx[e + j];
+          ww[j] = w ? w[e + j] : 1.0f;
+        }
+        if (MAP) {
+#pragma unroll
+          for (int j = 0; j < kUnroll; ++j) r[j] = map[r[j]];
+        }
+        T xv[kUnroll][NCH];
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j) {
+          const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r[j] * ldx);
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            const uint32_t col = lane + c * 64;
+            xv[j][c] = (col < nv) ? xrow[col] : V::zero();
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kUnroll; ++j)
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
+      }
+      for (; e < end; ++e) {
+        uint32_t r = idx[e];
+        const float we = w ? w[e] : 1.0f;
+        if (MAP) r = map[r];
+        const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r * ldx);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = lane + c * 64;
+          if (col < nv) acc[c] = V::madd(acc[c], xrow[col], we);
+        }
+      }
+      T* yrow = y ? reinterpret_cast<T*>(y + (uint64_t)d * ldy) : nullptr;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const uint32_t col = lane + c * 64;
+        if (col < nv) {
+          if (yrow) yrow[col] = acc[c];
+          const float* a = reinterpret_cast<const float*>(&acc[c]);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) srow[col * VEC + q] = a[q];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- phase 2: Z[tile, 32*wv .. +32) = sY[32 x F] W[F x 32-slice] ----
+    const int r = lane & 31, h = lane >> 5;
+    const uint32_t col = 32 * wv + r;
+    const bool col_ok = col < N;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+    const float* arow = sY + r * LDP + h * Kh;
+    const uint32_t kb = h * Kh;
+    for (uint32_t t = 0; t < Kh; t += 2) {
+      const float2 a2 = *reinterpret_cast<const float2*>(arow + t);
+      const uint32_t k0 = kb + t, k1 = k0 + 1;
+      const float b0 = (col_ok && k0 < F) ? W[(uint64_t)k0 * N + col] : 0.f;
+      const float b1 = (col_ok && k1 < F) ? W[(uint64_t)k1 * N + col] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.x, b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.y, b1, acc, 0, 0, 0);
+    }
+    if (col_ok) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t rowi = tile * kTM + 8 * (i >> 2) + 4 * h + (i & 3);
+        if (rowi < n) z[(uint64_t)rowi * ldz + col] = acc[i];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int VEC, bool MAP>
+static int launch_gather_linear_vec(hipStream_t st, int nch, uint32_t grid, size_t lds,
+                                    const uint32_t* off, const uint32_t* idx, const float* w,
+                                    const uint32_t* n_dev, uint32_t n_cap, const float* x,
+                                    uint64_t ldx, const uint32_t* map, uint32_t F, const float* W,
+                                    uint32_t N, float* y, uint64_t ldy, float* z, uint64_t ldz,
+                                    uint32_t Kh, uint32_t LDP) {
+#define NTS_GL(NCH)                                                                          \
+  do {                                                                                       \
+    NTS_HIP_TRY(hipFuncSetAttribute(                                                         \
+        reinterpret_cast<const void*>(&k_spmm_gather_linear<VEC, NCH, MAP>),                 \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                              \
+    hipLaunchKernelGGL((k_spmm_gather_linear<VEC, NCH, MAP>), dim3(grid), dim3(kAggThreads), \
+                       lds, st, off, idx, w, n_dev, n_cap, x, ldx, map, F, W, N, y, ldy, z,  \
+                       ldz, Kh, LDP);                                                        \
+  } while (0)
+  switch (nch) {
+    case 1: NTS_GL(1); break;
+    case 2: NTS_GL(2); break;
+    case 3: NTS_GL(3); break;
+    case 4: NTS_GL(4); break;
+    case 5: NTS_GL(5); break;
+    case 6: NTS_GL(6); break;
+    case 7: NTS_GL(7); break;
+    default: NTS_GL(8); break;
+  }
+#undef NTS_GL
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
 }  // namespace nts_hip
 
 using namespace nts_hip;
@@ -286,6 +446,49 @@ int nts_hip_spmm_csc_fwd(nts_hip_ctx* ctx, const uint32_t* column_offset,
                                x_row_map, feature_size, y, ldy);
   return launch_gather<false>(ctx->stream, column_offset, row_indices, weight, v, v_cap, x, ldx,
                               nullptr, feature_size, y, ldy);
+}
+
+int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx* ctx, const uint32_t* column_offset,
+                                const uint32_t* row_indices, const float* weight,
+                                const uint32_t* v, uint32_t v_cap, const float* x, uint64_t ldx,
+                                const uint32_t* x_row_map, uint32_t feature_size, const float* W,
+                                uint32_t out_size, float* y, uint64_t ldy, float* z,
+                                uint64_t ldz) {
+  NTS_CHECK_ARG(ctx && column_offset && row_indices && x && W && z, "NULL argument");
+  NTS_CHECK_ARG(ldx >= feature_size && (!y || ldy >= feature_size) && ldz >= out_size,
+                "leading dimension");
+  NTS_CHECK_ARG(out_size >= 1 && out_size <= 128, "out_size must be in [1, 128]");
+  if (v_cap == 0 || feature_size == 0) return NTS_OK;
+  const uint32_t F = feature_size;
+  const uint32_t half = (F + 1) / 2;
+  const uint32_t Kh = (half + 1) / 2 * 2;  // even
+  const uint32_t LDP = 2 * Kh + 2;          // LDP/2 odd: conflict-free ds_read_b64
+  const size_t lds = (size_t)kTM * LDP * sizeof(float);
+  NTS_CHECK_ARG(lds <= 160 * 1024, "feature_size too large for the fused kernel");
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  int vec = pick_vec(F, ldx, y ? ldy : ldx, x, y ? (const void*)y : (const void*)x);
+  const uint32_t nv = F / vec;
+  int nch = (int)std::min<uint32_t>((nv + 63) / 64, 8);
+  if ((nv + 63) / 64 > 8) vec = 0;  // rows wider than 512 vectors: not supported
+  NTS_CHECK_ARG(vec != 0, "feature_size too large for the fused kernel");
+  const uint32_t tiles = (v_cap + kTM - 1) / kTM;
+  const uint32_t grid = std::max(1u, std::min(tiles, 2048u));
+#define NTS_GLV(VEC, MAPB)                                                                     \
+  do {                                                                                         \
+    return launch_gather_linear_vec<VEC, MAPB>(ctx->stream, nch, grid, lds, column_offset,     \
+                                               row_indices, weight, v, v_cap, x, ldx,          \
+                                               x_row_map, F, W, out_size, y, ldy, z, ldz, Kh,  \
+                                               LDP);                                           \
+  } while (0)
+  if (x_row_map) {
+    if (vec == 4) NTS_GLV(4, true);
+    if (vec == 2) NTS_GLV(2, true);
+    NTS_GLV(1, true);
+  }
+  if (vec == 4) NTS_GLV(4, false);
+  if (vec == 2) NTS_GLV(2, false);
+  NTS_GLV(1, false);
+#undef NTS_GLV
 }
 
 int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,

@@ -30,7 +30,7 @@ EXPORTED = (
     "nts_hip_ctx_set_stream", "nts_hip_ctx_get_stream", "nts_hip_ctx_reserve",
     "nts_hip_rng_seed", "nts_hip_rng_state", "nts_hip_degrees", "nts_hip_build_csc",
     "nts_hip_sample_layer", "nts_hip_gather_rows", "nts_hip_gather_labels",
-    "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
+    "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csc_fwd_linear", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
     "nts_hip_gemm_f32", "nts_hip_adam", "nts_hip_comm_unique_id", "nts_hip_comm_init", "nts_hip_comm_destroy",
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
 )
@@ -88,6 +88,7 @@ def lib() -> C.CDLL:
         "nts_hip_gather_rows": ([P, P, U64, P, P, U32, U32, P, U64], I),
         "nts_hip_gather_labels": ([P, P, P, P, U32, P], I),
         "nts_hip_spmm_csc_fwd": ([P, P, P, P, P, U32, P, U64, P, U32, P, U64], I),
+        "nts_hip_spmm_csc_fwd_linear": ([P, P, P, P, P, U32, P, U64, P, U32, P, U32, P, U64, P, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),

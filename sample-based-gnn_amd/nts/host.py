@@ -35,7 +35,7 @@ def ext():
 def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, drop_rate=0.5,
                rng_mode=_abi.NTS_RNG_PHILOX, weight="sum", fused_gather=True,
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
-               seed=2000, hip_gemm=True, pipeline=True):
+               seed=2000, hip_gemm=True, pipeline=True, fuse_linear=True):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -52,6 +52,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.deterministic_backward = bool(deterministic_backward)
     c.hip_gemm = bool(hip_gemm)
     c.pipeline = bool(pipeline)
+    c.fuse_linear = bool(fuse_linear)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

@@ -136,6 +136,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("deterministic_backward", &GCNConfig::deterministic_backward)
       .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
       .def_readwrite("pipeline", &GCNConfig::pipeline)
+      .def_readwrite("fuse_linear", &GCNConfig::fuse_linear)
       .def_readwrite("shuffle", &GCNConfig::shuffle)
       .def_readwrite("profile", &GCNConfig::profile)
       .def_readwrite("seed", &GCNConfig::seed);

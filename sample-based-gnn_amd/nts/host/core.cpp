@@ -486,7 +486,53 @@ struct HipLinearFn : public torch::autograd::Function<HipLinearFn> {
     return {dx, dW, NtsVar()};
   }
 };
+struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, NtsVar y, int64_t sg_ptr,
+                        int64_t cs_ptr) {
+    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    auto* sg = reinterpret_cast<sampCSC*>(sg_ptr);
+    NtsVar Wc = W.contiguous();
+    const int64_t F = table.size(1), N = Wc.size(1);
+    NtsVar Z = torch::empty({(int64_t)sg->v_size, N}, table.options());
+    hip_check(nts_hip_spmm_csc_fwd_linear(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
+                                          nullptr, sg->v_size, table.data_ptr<float>(),
+                                          (uint64_t)table.stride(0), sg->dev_src(), (uint32_t)F,
+                                          Wc.data_ptr<float>(), (uint32_t)N, y.data_ptr<float>(),
+                                          (uint64_t)F, Z.data_ptr<float>(), (uint64_t)N),
+              "nts_hip_spmm_csc_fwd_linear");
+    ctx->save_for_backward({y, Wc});
+    ctx->saved_data["cs"] = cs_ptr;
+    return Z;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto saved = ctx->get_saved_variables();
+    NtsVar y = saved[0], W = saved[1];
+    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    NtsVar g = grads[0].contiguous();
+    const int64_t M = y.size(0), K = y.size(1), N = W.size(1);
+    NtsVar dW = torch::empty({K, N}, W.options());
+    hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)K, (int)N, (int)M, y.data_ptr<float>(),
+                               (uint64_t)K, g.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
+                               (uint64_t)N),
+              "nts_hip_gemm_f32(tn)");
+    return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar()};
+  }
+};
 }  // namespace
+
+bool hip_agg_linear_supported(int64_t F, int64_t N) {
+  const int64_t half = (F + 1) / 2, Kh = (half + 1) / 2 * 2, LDP = 2 * Kh + 2;
+  // mirrors the argument checks of nts_hip_spmm_csc_fwd_linear for a
+  // contiguous, 16-byte aligned table (torch allocations are)
+  const int64_t vec = F % 4 == 0 ? 4 : (F % 2 == 0 ? 2 : 1);
+  return F >= 1 && N >= 1 && N <= 128 && 32 * LDP * 4 <= 160 * 1024 && (F / vec + 63) / 64 <= 8;
+}
+
+NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg,
+                      NtsStream* cs) {
+  return HipAggLinearFn::apply(table, W, y, reinterpret_cast<int64_t>(sg),
+                               reinterpret_cast<int64_t>(cs));
+}
 
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {
   return HipLinearFn::apply(x, W, reinterpret_cast<int64_t>(cs));

@@ -142,6 +142,34 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       evp = &next_events();
       (void)hipEventRecord(evp->first, (hipStream_t)cs->stream());
     }
+    const bool fuse = bottom && cfg.fused_gather && cfg.fuse_linear && cfg.hip_gemm &&
+                      hip_agg_linear_supported(F.size(1), P[0]->W.size(1));
+    if (fuse) {
+      // graph op + Parameter::forward of the first layer in one kernel; the
+      // bottom graph op has no backward (core/ntsContext.hpp:443-444), so the
+      // pair is recorded as one NN op whose input is the feature table
+      sampCSC* s = sg->sampled_sgs[hop];
+      Y = torch::empty({(int64_t)s->v_size, F.size(1)}, F.options());
+      NtsVar Z = hip_agg_linear(F, P[0]->W, Y, s, cs.get());
+      if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
+      const double Fd = (double)F.size(1);
+      agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
+                   Fd * 4.0 * s->v_size + 4.0 * s->src_size +
+                   4.0 * (double)P[0]->W.size(1) * s->v_size;
+      agg_calls += 1;
+      NtsVar table = F;
+      X = ctx.runVertexForward(
+          [&](NtsVar&) {
+            if (l == L - 1) return Z.log_softmax(1);
+            return torch::dropout(torch::relu(Z), cfg.drop_rate, ctx.is_train());
+          },
+          table);
+      if (keep) {
+        acts.push_back(Y.detach());
+        acts.push_back(X.detach());
+      }
+      continue;
+    }
     if (bottom && cfg.fused_gather)
       Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true);
     else

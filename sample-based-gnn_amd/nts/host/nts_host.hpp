@@ -298,6 +298,15 @@ class NtsContext {
 // backward: dW = x^T dZ (split-reduction, deterministic), dx = dZ W^T.
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
 
+// Bottom layer fused: Y = A X (into the caller's `y`, bit-identical to the
+// graph op) and Z = Y W in one kernel (nts_hip_spmm_csc_fwd_linear); autograd
+// returns Z with dW = Y^T dZ.  X is the global feature table, rows fetched
+// through the layer's `source` (fused load_feature_gpu).
+NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg,
+                      NtsStream* cs);
+// whether the fused kernel supports this shape (feature rows fit the LDS tile, out <= 128)
+bool hip_agg_linear_supported(int64_t feature_size, int64_t out_size);
+
 struct Parameter {
   NtsVar W, M, V;
   NtsStream* cs = nullptr;  // set -> forward runs on the hand-written MFMA GEMM

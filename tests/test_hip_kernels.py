@@ -346,3 +346,46 @@ def test_gemm_f32_mfma(hip, M, N, K, trans_a):
     hip.gemm(A, B, C2, trans_a=trans_a)
     torch.cuda.synchronize()
     assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("F,N", [(602, 128), (602, 41), (128, 128), (41, 7), (1, 1), (100, 64),
+                                 (1433, 16)])
+@pytest.mark.parametrize("mapped", [True, False])
+def test_spmm_fwd_linear_fused(hip, cora, F, N, mapped):
+    """Fused bottom layer: Y bit-identical to the graph op (fuse_fwd, the
+    reference's aggregation order), Z = Y W on MFMA within fp32 GEMM tolerance."""
+    V, src, dst = cora
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    l0, l1 = o.sample(np.arange(0, V, 7, dtype=np.uint32))
+    rng = np.random.default_rng(F * 31 + N)
+    table = rng.standard_normal((V, F)).astype(np.float32)
+    X = orc.get_feature(l1["source"], table)
+    Y_ref = orc.fuse_fwd(l1, X, out_d, in_d)
+    v = l1["v_size"]
+    co, ri, wf = _t(l1["column_offset"]), _t(l1["row_indices"]), _t(l1["edge_weight_forward"])
+    vdev = torch.tensor([v], dtype=torch.int32, device=DEV)
+    W = _t(rng.standard_normal((F, N)).astype(np.float32))
+    y = torch.full((v + 3, F), float("nan"), device=DEV)
+    z = torch.full((v + 3, N), float("nan"), device=DEV)
+    x = _t(table) if mapped else _t(X)
+    rm = _t(l1["source"]) if mapped else None
+    half = (F + 1) // 2
+    Kh = (half + 1) // 2 * 2
+    if 32 * (2 * Kh + 2) * 4 > 160 * 1024 or (F + 63) // 64 > 8:
+        with pytest.raises(RuntimeError):
+            hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v + 3, x, W, z, y=y, row_map=rm)
+        return
+    hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v + 3, x, W, z, y=y, row_map=rm)
+    torch.cuda.synchronize()
+    assert np.array_equal(y[:v].cpu().numpy(), Y_ref)
+    assert torch.isnan(y[v:]).all() and torch.isnan(z[v:]).all()
+    ref = torch.from_numpy(Y_ref).double() @ W.cpu().double()
+    tol = 2e-6 * F ** 0.5 + 1e-6
+    torch.testing.assert_close(z[:v].cpu().double(), ref, rtol=tol, atol=tol * 4)
+    # without Y
+    z2 = torch.empty((v, N), device=DEV)
+    hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v, x, W, z2, row_map=rm)
+    torch.cuda.synchronize()
+    assert torch.equal(z2, z[:v])

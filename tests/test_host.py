@@ -94,11 +94,18 @@ def test_unfused_gather_path_is_identical(E, graph):
     cfg = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fused_gather=False, shuffle=False)
     drv2 = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg)
     drv2.set_weights(drv.weights())
+    cfg3 = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fuse_linear=False, shuffle=False)
+    drv3 = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg3)
+    drv3.set_weights(drv.weights())
     seeds = torch.arange(100, 228, dtype=torch.int32)
-    a = drv.forward_eval(seeds, 0)
-    b = drv2.forward_eval(seeds, 0)
-    for x, y in zip(a, b):
+    a = drv.forward_eval(seeds, 0)   # gather + aggregation + first GEMM in one kernel
+    b = drv2.forward_eval(seeds, 0)  # load_feature_gpu, graph op, HipLinear
+    c = drv3.forward_eval(seeds, 0)  # gather fused into the graph op, HipLinear
+    for x, y in zip(b, c):
         assert torch.equal(x, y)
+    assert torch.equal(a[0], b[0])  # aggregation itself is identical
+    for x, y in zip(a[1:], b[1:]):  # GEMM summation order differs
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-5)
 
 
 def test_training_step_matches_oracle_step(E, graph):
