@@ -51,8 +51,8 @@ def parse():
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
-    p.add_argument("--no-fuse-linear", action="store_true",
-                   help="bottom layer: aggregation and first GEMM as separate kernels")
+    p.add_argument("--fuse-linear", action="store_true",
+                   help="bottom layer: aggregation and first GEMM in one kernel")
     p.add_argument("--cpu-baseline-steps", type=int, default=1)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -103,8 +103,8 @@ def main():
                           drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX,
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
-                          fuse_linear=not args.no_fuse_linear)
-    fused_linear = (not args.no_fused_gather and not args.no_fuse_linear and not args.no_hip_gemm
+                          fuse_linear=args.fuse_linear)
+    fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and args.hidden <= 128)
     agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)

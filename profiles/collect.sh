@@ -1,17 +1,21 @@
 #!/bin/bash
 # Profile the headline bench on the GPU box (run from the repo root):
 #   kernel trace + stats, then two separate PMC passes (FETCH_SIZE, WRITE_SIZE)
+#   profiles/collect.sh <tag> <steps> [trace-only] [extra bench flags...]
 # Output: gpurun_out/prof_<tag>/... ; summarise with profiles/summarize.py
 set -e
 TAG=${1:-r01}
 STEPS=${2:-10}
+MODE=${3:-all}
+shift 3 || true
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $OUT/trace.log 2>&1
+  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline "$@" > $OUT/trace.log 2>&1
+[ "$MODE" = "trace-only" ] && { echo done; exit 0; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run --output-format csv -- \
-  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $OUT/fetch.log 2>&1
+  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline "$@" > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run --output-format csv -- \
-  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $OUT/write.log 2>&1
+  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline "$@" > $OUT/write.log 2>&1
 echo done

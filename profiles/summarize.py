@@ -50,7 +50,7 @@ def main():
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
         lines.append(f"| `{r['Name'][:80]}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | "
                      f"{float(r['AverageNs'])/1e3:.1f} | {100*float(r['TotalDurationNs'])/tot:.1f} |")
-    dom = sorted((r for r in rows if r["Name"].startswith(PREFIXES)),
+    dom = sorted((r for r in rows if any(pfx in r["Name"] for pfx in PREFIXES)),
                  key=lambda r: -float(r["TotalDurationNs"]))
     info = {}
     DOMINANT = dom[0]["Name"] if dom else "k_spmm_gather<"

@@ -3,13 +3,13 @@
 //
 // The layer GEMMs are tall-skinny: Z = Y W with Y [~150K x 602], W [602 x 128]
 // (Parameter::forward, core/NtsScheduler.hpp:859-862) and the weight gradient
-// dW = Y^T dZ (reduction over the ~150K sampled rows).  Library kernels run
-// these at ~40 TF/s; here the tiles are shaped for them:
+// dW = Y^T dZ (reduction over the ~150K sampled rows).  The library TN kernel
+// runs these at ~36-45 TF/s; here the tiles are shaped for them:
 //   NN: block 128 rows x 128 cols, 4 waves of 32 rows x 4 MFMA tiles; A rows
 //       are read straight into registers (16 consecutive k per lane — the k
 //       order inside an MFMA step is a free permutation shared by A and B),
-//       the B k-slice [32 x 128] is staged in LDS (double buffered) and shared
-//       by the 4 waves.
+//       the B k-slice [32 x 128] is staged in LDS (double buffered, permuted so
+//       one ds_read_b128 feeds a lane's 4 column tiles) and shared by the 4 waves.
 //   TN: C = A^T B with the long reduction split over blocks; per-split
 //       partial tiles are summed in split order by a second kernel
 //       (deterministic, no atomics).
@@ -20,139 +20,234 @@ namespace nts_hip {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kGT = 256;   // threads per block
-constexpr int kBM = 128;   // block rows (4 waves x 32)
-constexpr int kBN = 128;   // block cols (4 MFMA tiles of 32)
-constexpr int kBK = 32;    // k per step (16 MFMA 32x32x2 steps)
+constexpr int kBM = 64;    // block rows: 2 wave rows x 32
+constexpr int kBN = 128;   // block cols: 2 wave cols x 2 MFMA tiles of 32
+constexpr int kBK = 32;    // k per step (16 MFMA 32x32x2 k-pairs)
+constexpr int kAP = 36;    // NN A tile pitch (floats): ds_read_b128 conflict-free
 
-// Stage B[k0 .. k0+32) x [n0 .. n0+128) (row-major, ldb) into LDS.
-// Each thread moves 16 consecutive floats of one k-row.
-template <bool BVEC>
-__device__ __forceinline__ void load_b_slice(const float* __restrict__ B, uint64_t ldb, int K,
-                                             int N, int k0, int n0, float (&v)[16]) {
-  const int kk = threadIdx.x >> 3;
-  const int c = (threadIdx.x & 7) * 16;
-  const int k = k0 + kk;
-  const float* row = B + (uint64_t)k * ldb;
-  if (BVEC) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int col = n0 + c + 4 * q;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k < K && col < N) x = *reinterpret_cast<const float4*>(row + col);
-      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int col = n0 + c + q;
-      v[q] = (k < K && col < N) ? row[col] : 0.f;
-    }
-  }
+// Shared-memory image of one k-step (double buffered).
+//   NN: As[m][k] (pitch kAP)      -> lane reads 16 consecutive k: 4 x ds_read_b128
+//   TN: At[k][m]                  -> lane reads A[k][m] for 16 k:   16 x ds_read_b32
+//   Bs[k][j][r][t] = B[k0+k][n0 + 64j + 32t + r]  (t = 0,1)  -> one ds_read_b64
+//       gives a lane both column tiles of its wave column j, conflict-free.
+struct GemmSmem {
+  float a[2][kBM * kAP];
+  float b[2][kBK * kBN];
+};
+
+// zero (mk == 0) or keep (mk == ~0) a value without a branch or a select on
+// the loaded data's arrival
+__device__ __forceinline__ float msk(float v, uint32_t mk) {
+  return __uint_as_float(__float_as_uint(v) & mk);
 }
 
-__device__ __forceinline__ void store_b_slice(float (*Bs)[kBN], const float (&v)[16]) {
-  const int kk = threadIdx.x >> 3;
-  const int c = (threadIdx.x & 7) * 16;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    *reinterpret_cast<float4*>(&Bs[kk][c + 4 * q]) =
-        make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-}
-
-// 16 A values of this lane for the k-step at k0:
-//   NN (TRANS_A=false): A[row][k0 + 16h + s]       (row-major M x K)
-//   TN (TRANS_A=true):  A[k0 + 16h + s][row]       (row-major K x M)
+// Per-thread tile movers.  Global -> registers for one k-step (8 A floats +
+// 16 B floats per thread, every wave instruction reading whole 128-byte row
+// segments), registers -> LDS at the end of the step.  Loads are branch-free
+// with addresses clamped into the operands (k past K reads a valid element;
+// its LDS image is zeroed by mask), so the compiler counts outstanding loads
+// (vmcnt(N)) across steps instead of draining the queue: the two-deep
+// prefetch relies on it.  Row/column bases are computed once per block.
 template <bool TRANS_A, int AVEC>
-__device__ __forceinline__ void load_a(const float* __restrict__ A, uint64_t lda, int M, int K,
-                                       int64_t row, int k0, int h, float (&a)[16]) {
-  const int kb = k0 + 16 * h;
-  if (!TRANS_A) {
-    const bool ok = row < M;
-    const float* p = A + (uint64_t)row * lda + kb;
-    if (AVEC == 2) {
+struct ATile {
+  static constexpr int NP = 8 / AVEC;  // loads per thread per step
+  const float* base[TRANS_A ? 1 : NP];
+  int kc;      // NN: this thread's k column in the step;  TN: its first k row
+  int sdst;    // LDS offset of the first element
+  __device__ ATile(const float* A, uint64_t lda, int M, int K, int64_t m0) {
+    const int tid = threadIdx.x;
+    if (!TRANS_A) {  // A[m][k]: 64 rows x 32 k, rows tid/(32/AVEC) + (256/(32/AVEC)) p
+      constexpr int per = 32 / AVEC;
+      kc = (tid % per) * AVEC;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float2 x = make_float2(0.f, 0.f);
-        if (ok && kb + 2 * q < K) x = *reinterpret_cast<const float2*>(p + 2 * q);
-        a[2 * q] = x.x;
-        a[2 * q + 1] = x.y;
+      for (int p = 0; p < NP; ++p) {
+        const int64_t m = m0 + tid / per + (256 / per) * p;
+        base[p] = A + (uint64_t)(m < M ? m : M - 1) * lda;
       }
-    } else if (AVEC == 4) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok && kb + 4 * q < K) x = *reinterpret_cast<const float4*>(p + 4 * q);
-        a[4 * q] = x.x; a[4 * q + 1] = x.y; a[4 * q + 2] = x.z; a[4 * q + 3] = x.w;
-      }
-    } else {
-#pragma unroll
-      for (int s = 0; s < 16; ++s) a[s] = (ok && kb + s < K) ? p[s] : 0.f;
+      sdst = (tid / per) * kAP + kc;
+    } else {  // A[k][m]: 32 k x 64 m, k rows tid/(64/AVEC) + (256/(64/AVEC)) p
+      constexpr int per = 64 / AVEC;
+      const int64_t m = m0 + (tid % per) * AVEC;
+      base[0] = A + (m < M ? m : M - AVEC);
+      kc = tid / per;
+      sdst = kc * kBM + (tid % per) * AVEC;
     }
-  } else {
-    const bool ok = row < M;
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-      a[s] = (ok && kb + s < K) ? A[(uint64_t)(kb + s) * lda + row] : 0.f;
+    (void)K;
   }
-}
+  __device__ __forceinline__ void load(uint64_t lda, int K, int k0, float (&v)[8]) const {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float* src;
+      if (!TRANS_A) {
+        const int k = min(k0 + kc, K - AVEC);
+        src = base[p] + k;
+      } else {
+        const int k = min(k0 + kc + (256 / (64 / AVEC)) * p, K - 1);
+        src = base[0] + (uint64_t)k * lda;
+      }
+      if (AVEC == 4) {
+        const float4 x = *reinterpret_cast<const float4*>(src);
+        v[4 * p] = x.x; v[4 * p + 1] = x.y; v[4 * p + 2] = x.z; v[4 * p + 3] = x.w;
+      } else if (AVEC == 2) {
+        const float2 x = *reinterpret_cast<const float2*>(src);
+        v[2 * p] = x.x; v[2 * p + 1] = x.y;
+      } else {
+        v[p] = *src;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ sa, int K, int k0,
+                                        const float (&v)[8]) const {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      float* dst;
+      uint32_t mk;
+      if (!TRANS_A) {
+        dst = sa + sdst + (256 / (32 / AVEC)) * p * kAP;
+        mk = k0 + kc < K ? ~0u : 0u;
+      } else {
+        dst = sa + sdst + (256 / (64 / AVEC)) * p * kBM;
+        mk = k0 + kc + (256 / (64 / AVEC)) * p < K ? ~0u : 0u;
+      }
+      if (AVEC == 4)
+        *reinterpret_cast<float4*>(dst) = make_float4(msk(v[4 * p], mk), msk(v[4 * p + 1], mk),
+                                                      msk(v[4 * p + 2], mk), msk(v[4 * p + 3], mk));
+      else if (AVEC == 2)
+        *reinterpret_cast<float2*>(dst) = make_float2(msk(v[2 * p], mk), msk(v[2 * p + 1], mk));
+      else
+        *dst = msk(v[p], mk);
+    }
+  }
+};
+
+// B k-slice [32 x 128]: thread (kk = tid>>5, r = tid&31) moves k-rows kk + 8p,
+// columns r + 32t (t = 0..3): each load is 32 consecutive floats per half-wave.
+// BFULL (N % 128 == 0): the 4 columns are immediate offsets of one address.
+template <bool BFULL>
+struct BTile {
+  const float* base;
+  int coff[4];
+  int kk, r;
+  __device__ BTile(const float* B, int N, int n0) {
+    kk = threadIdx.x >> 5;
+    r = threadIdx.x & 31;
+    base = B + (BFULL ? n0 + r : 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) coff[t] = min(n0 + r + 32 * t, N - 1);
+  }
+  __device__ __forceinline__ void load(uint64_t ldb, int K, int k0, float (&v)[16]) const {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float* row = base + (uint64_t)min(k0 + kk + 8 * p, K - 1) * ldb;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[4 * p + t] = BFULL ? row[32 * t] : row[coff[t]];
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ sb, int K, int k0,
+                                        const float (&v)[16]) const {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint32_t mk = k0 + kk + 8 * p < K ? ~0u : 0u;
+      float* row = sb + (kk + 8 * p) * kBN;
+      *reinterpret_cast<float2*>(row + 2 * r) =
+          make_float2(msk(v[4 * p], mk), msk(v[4 * p + 1], mk));
+      *reinterpret_cast<float2*>(row + 64 + 2 * r) =
+          make_float2(msk(v[4 * p + 2], mk), msk(v[4 * p + 3], mk));
+    }
+  }
+};
 
 // C_tile = op(A) B over k in [kbeg, kend); result written to C (ldc) or to a
 // partial slab.  grid: x = M tiles, y = N tiles, z = k splits.
-template <bool TRANS_A, int AVEC, bool BVEC>
-__global__ __launch_bounds__(kGT) void k_gemm(int M, int N, int K, const float* __restrict__ A,
-                                              uint64_t lda, const float* __restrict__ B,
-                                              uint64_t ldb, float* __restrict__ C, uint64_t ldc,
-                                              int kchunk, uint64_t split_stride) {
-  __shared__ float Bs[2][kBK][kBN];
+// Wave w: rows 32*(w&1) .. +32 of the block tile, columns 64*(w>>1) .. +64.
+template <bool TRANS_A, int AVEC, bool BFULL>
+__global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const float* __restrict__ A,
+                                                 uint64_t lda, const float* __restrict__ B,
+                                                 uint64_t ldb, float* __restrict__ C, uint64_t ldc,
+                                                 int kchunk, uint64_t split_stride) {
+  __shared__ GemmSmem sm;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int64_t row = (int64_t)blockIdx.x * kBM + w * 32 + r;
+  const int wr = 32 * (w & 1), wc = w >> 1;
+  const int64_t m0 = (int64_t)blockIdx.x * kBM;
   const int n0 = blockIdx.y * kBN;
   const int kbeg = blockIdx.z * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  f32x16 acc[4];
+  f32x16 acc[2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  const ATile<TRANS_A, AVEC> at(A, lda, M, kend, m0);
+  const BTile<BFULL> bt(B, N, n0);
 
-  float a[16], bv[16];
-  if (kbeg < kend) {
-    load_a<TRANS_A, AVEC>(A, lda, M, kend, row, kbeg, h, a);
-    load_b_slice<BVEC>(B, ldb, kend, N, kbeg, n0, bv);
-    store_b_slice(Bs[0], bv);
-  }
-  __syncthreads();
-  int buf = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += kBK) {
-    const bool more = k0 + kBK < kend;
-    float an[16];
-    if (more) {
-      load_a<TRANS_A, AVEC>(A, lda, M, kend, row, k0 + kBK, h, an);
-      load_b_slice<BVEC>(B, ldb, kend, N, k0 + kBK, n0, bv);
+  // Two register staging sets: the global loads of k-step j+2 are issued at
+  // the start of step j (two steps of MFMA work cover the HBM latency), the
+  // set holding step j+1 is written to the other LDS buffer at its end.
+  float av0[8], bv0[16], av1[8], bv1[16];
+  const int nsteps = kbeg < kend ? (kend - kbeg + kBK - 1) / kBK : 0;
+  auto compute = [&](int cur) {
+    float a[16];
+    if (!TRANS_A) {
+      const float4* ap = reinterpret_cast<const float4*>(sm.a[cur] + (wr + r) * kAP + 16 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 x = ap[q];
+        a[4 * q] = x.x; a[4 * q + 1] = x.y; a[4 * q + 2] = x.z; a[4 * q + 3] = x.w;
+      }
+    } else {
+      const float* ap = sm.a[cur] + (16 * h) * kBM + wr + r;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) a[s] = ap[s * kBM];
     }
+    const float2* bp = reinterpret_cast<const float2*>(sm.b[cur] + (16 * h) * kBN + 64 * wc) + r;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float b = Bs[buf][16 * h + s][32 * t + r];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b, acc[t], 0, 0, 0);
-      }
+      const float2 b = bp[s * (kBN / 2)];
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b.x, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b.y, acc[1], 0, 0, 0);
     }
-    if (more) {
-      store_b_slice(Bs[buf ^ 1], bv);
-#pragma unroll
-      for (int s = 0; s < 16; ++s) a[s] = an[s];
-    }
-    __syncthreads();
-    buf ^= 1;
+  };
+  if (nsteps > 0) {
+    at.load(lda, kend, kbeg, av0);
+    bt.load(ldb, kend, kbeg, bv0);
+    at.load(lda, kend, kbeg + kBK, av1);
+    bt.load(ldb, kend, kbeg + kBK, bv1);
+    at.store(sm.a[0], kend, kbeg, av0);
+    bt.store(sm.b[0], kend, kbeg, bv0);
   }
+  __syncthreads();
+  int j = 0;
+  for (; j + 2 <= nsteps; j += 2) {
+    const int k0 = kbeg + j * kBK;
+    // step j: LDS buffer 0, loads of step j+2 -> set 0, set 1 (step j+1) -> buffer 1
+    // (sched_barrier: keep the loads at the head of the step and the stores at
+    // its tail — the scheduler would otherwise sink the loads below the MFMAs)
+    at.load(lda, kend, k0 + 2 * kBK, av0);
+    bt.load(ldb, kend, k0 + 2 * kBK, bv0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0);
+    __builtin_amdgcn_sched_barrier(0);
+    at.store(sm.a[1], kend, k0 + kBK, av1);
+    bt.store(sm.b[1], kend, k0 + kBK, bv1);
+    __syncthreads();
+    // step j+1: LDS buffer 1, loads of step j+3 -> set 1, set 0 (step j+2) -> buffer 0
+    at.load(lda, kend, k0 + 3 * kBK, av1);
+    bt.load(ldb, kend, k0 + 3 * kBK, bv1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1);
+    __builtin_amdgcn_sched_barrier(0);
+    at.store(sm.a[0], kend, k0 + 2 * kBK, av0);
+    bt.store(sm.b[0], kend, k0 + 2 * kBK, bv0);
+    __syncthreads();
+  }
+  if (j < nsteps) compute(0);  // odd step count: the last step is already in buffer 0
   // epilogue: acc[t][i] -> (row = 8*(i>>2) + 4*h + (i&3), col = 32t + r) of the wave tile
   float* Cb = C + (uint64_t)blockIdx.z * split_stride;
-  const int64_t wrow0 = (int64_t)blockIdx.x * kBM + w * 32;
+  const int64_t wrow0 = m0 + wr;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int col = n0 + 32 * t + r;
+  for (int t = 0; t < 2; ++t) {
+    const int col = n0 + 64 * wc + 32 * t + r;
     if (col >= N) continue;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -162,9 +257,36 @@ __global__ __launch_bounds__(kGT) void k_gemm(int M, int N, int K, const float* 
   }
 }
 
-// C = sum over splits of the partial slabs (in split order)
+// C = sum over splits of the partial slabs (in split order; loads run ahead of
+// the sequential adds).  VEC4: N % 4 == 0 and C 16-byte aligned rows.
+template <bool VEC4>
 __global__ void k_sum_splits(const float* __restrict__ part, int splits, uint64_t stride, int M,
                              int N, float* __restrict__ C, uint64_t ldc) {
+  if (VEC4) {
+    const uint64_t total = (uint64_t)M * N / 4;
+    const float4* p4 = reinterpret_cast<const float4*>(part);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      int z = 0;
+      for (; z + 4 <= splits; z += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = p4[(uint64_t)(z + u) * (stride / 4) + i];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+        }
+      }
+      for (; z < splits; ++z) {
+        const float4 v = p4[(uint64_t)z * (stride / 4) + i];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const uint64_t e = i * 4;
+      *reinterpret_cast<float4*>(C + (e / N) * ldc + (e % N)) = s;
+    }
+    return;
+  }
   const uint64_t total = (uint64_t)M * N;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (uint64_t)gridDim.x * blockDim.x) {
@@ -179,18 +301,18 @@ static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t 
                   const float* B, uint64_t ldb, float* C, uint64_t ldc, int splits, int kchunk,
                   uint64_t split_stride) {
   dim3 grid(ceil_div(M, kBM), ceil_div(N, kBN), splits);
-  const bool bvec = (N % 4 == 0) && (ldb % 4 == 0) && ((uintptr_t)B % 16 == 0);
+  // vector width of the A tile loads: rows of the loaded dimension must stay aligned
+  const int inner = TRANS_A ? M : K;
   int avec = 1;
-  if (!TRANS_A) {
-    if (K % 4 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
-    else if (K % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
-  }
-#define NTS_GEMM(AV, BV)                                                                        \
-  hipLaunchKernelGGL((k_gemm<TRANS_A, AV, BV>), grid, dim3(kGT), 0, st, M, N, K, A, lda, B, ldb, \
+  if (inner % 4 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
+  else if (inner % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
+  const bool bfull = N % kBN == 0;
+#define NTS_GEMM(AV, BF)                                                                          \
+  hipLaunchKernelGGL((k_gemm<TRANS_A, AV, BF>), grid, dim3(kGT), 0, st, M, N, K, A, lda, B, ldb, \
                      C, ldc, kchunk, split_stride)
-  if (avec == 4) { if (bvec) NTS_GEMM(4, true); else NTS_GEMM(4, false); }
-  else if (avec == 2) { if (bvec) NTS_GEMM(2, true); else NTS_GEMM(2, false); }
-  else { if (bvec) NTS_GEMM(1, true); else NTS_GEMM(1, false); }
+  if (avec == 4) { if (bfull) NTS_GEMM(4, true); else NTS_GEMM(4, false); }
+  else if (avec == 2) { if (bfull) NTS_GEMM(2, true); else NTS_GEMM(2, false); }
+  else { if (bfull) NTS_GEMM(1, true); else NTS_GEMM(1, false); }
 #undef NTS_GEMM
   NTS_LAUNCH_CHECK();
   return NTS_OK;
@@ -219,7 +341,8 @@ extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int
   const int tiles = (int)(ceil_div(M, kBM) * ceil_div(N, kBN));
   int splits = 1;
   const int ksteps = (K + kBK - 1) / kBK;
-  if (tiles < 512) splits = std::max(1, std::min(1024 / tiles, ksteps / 4));
+  // 3 blocks per CU are resident (LDS): aim the split grid at 768 blocks
+  if (tiles < 384) splits = std::max(1, std::min(768 / tiles, ksteps / 4));
   const int kchunk = ((ksteps + splits - 1) / splits) * kBK;
   splits = (K + kchunk - 1) / kchunk;
   if (splits == 1)
@@ -230,8 +353,14 @@ extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int
   float* part = (float*)ctx->scratch;
   NTS_RET(trans_a ? launch<true>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride)
                   : launch<false>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride));
-  const uint32_t g = std::max(1u, std::min(ceil_div(stride, 256), kMaxGrid));
-  hipLaunchKernelGGL(k_sum_splits, dim3(g), dim3(256), 0, st, part, splits, stride, M, N, C, ldc);
+  const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+  const uint32_t g = std::max(1u, std::min(ceil_div(v4 ? stride / 4 : stride, 256), kMaxGrid));
+  if (v4)
+    hipLaunchKernelGGL(k_sum_splits<true>, dim3(g), dim3(256), 0, st, part, splits, stride, M, N,
+                       C, ldc);
+  else
+    hipLaunchKernelGGL(k_sum_splits<false>, dim3(g), dim3(256), 0, st, part, splits, stride, M,
+                       N, C, ldc);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }

@@ -35,7 +35,7 @@ def ext():
 def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, drop_rate=0.5,
                rng_mode=_abi.NTS_RNG_PHILOX, weight="sum", fused_gather=True,
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
-               seed=2000, hip_gemm=True, pipeline=True, fuse_linear=True):
+               seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)

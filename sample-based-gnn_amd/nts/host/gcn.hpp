@@ -18,7 +18,7 @@ struct GCNConfig {
   bool deterministic_backward = true; // CSR transpose gather instead of atomics
   bool hip_gemm = true;               // layer GEMMs on the hand-written MFMA kernels
   bool pipeline = true;               // sample batch i+1 on its own stream while i trains
-  bool fuse_linear = true;            // bottom layer: gather + aggregation + GEMM in one kernel
+  bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
   int64_t seed = 2000;

@@ -373,7 +373,8 @@ def test_spmm_fwd_linear_fused(hip, cora, F, N, mapped):
     rm = _t(l1["source"]) if mapped else None
     half = (F + 1) // 2
     Kh = (half + 1) // 2 * 2
-    if 32 * (2 * Kh + 2) * 4 > 160 * 1024 or (F + 63) // 64 > 8:
+    vec = 4 if F % 4 == 0 else (2 if F % 2 == 0 else 1)
+    if 32 * (2 * Kh + 2) * 4 > 160 * 1024 or (F // vec + 63) // 64 > 8:
         with pytest.raises(RuntimeError):
             hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v + 3, x, W, z, y=y, row_map=rm)
         return

@@ -57,13 +57,13 @@ def test_fast_sampler_matches_oracle(E, graph):
     assert bs == 3
 
 
-def _driver(E, graph, F, C, layers, fanout, batch, drop=0.0, seed=2000):
+def _driver(E, graph, F, C, layers, fanout, batch, drop=0.0, seed=2000, **kw):
     from nts import host, synthetic
     feat = synthetic.features(graph["V"], F, device=DEV)
     labels, masks = synthetic.labels_masks(graph["V"], C, device=DEV)
     train = torch.nonzero(masks == 0).flatten().to(torch.int32).cpu()
     cfg = host.gcn_config(layers, fanout, batch, learn_rate=0.01, drop_rate=drop, seed=seed,
-                          shuffle=False)
+                          shuffle=False, **kw)
     return E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg), feat, labels, train
 
 
@@ -90,7 +90,7 @@ def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F):
 
 def test_unfused_gather_path_is_identical(E, graph):
     from nts import host
-    drv, feat, labels, train = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 128)
+    drv, feat, labels, train = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 128, fuse_linear=True)
     cfg = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fused_gather=False, shuffle=False)
     drv2 = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg)
     drv2.set_weights(drv.weights())
