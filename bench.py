@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
+    p.add_argument("--no-early-agg", action="store_true",
+                   help="bottom aggregation on the training stream instead of behind the sampler")
+    p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
     p.add_argument("--fuse-linear", action="store_true",
                    help="bottom layer: aggregation and first GEMM in one kernel")
     p.add_argument("--cpu-baseline-steps", type=int, default=1)
@@ -103,8 +106,10 @@ def main():
                           drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX,
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
-                          fuse_linear=args.fuse_linear)
+                          fuse_linear=args.fuse_linear, early_aggregate=not args.no_early_agg,
+                          sampler_priority=not args.no_priority)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
+                    and args.no_early_agg
                     and args.hidden <= 128)
     agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
@@ -156,6 +161,8 @@ def main():
         epoch_s = time.perf_counter() - te
         drv.resolve_profile()
 
+    layer_sizes = [{"v": int(l["v_size"]), "src": int(l["src_size"]), "e": int(l["e_size"])}
+                   for l in drv.last_layers]
     value = edges / elapsed
     agg_avg_ms = agg_ms / max(agg_calls, 1)
     achieved = (agg_bytes / max(agg_calls, 1)) / (agg_avg_ms * 1e-3) / 1e9 if agg_calls else None
@@ -180,6 +187,7 @@ def main():
                          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic "
                          f"(V={V}, E={En}); GPU sampler (Philox"
                          f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation"
+                         f"{' (issued behind the sampler)' if not args.no_early_agg and not args.no_fused_gather else ''}"
                          f"{' + layer-1 GEMM' if fused_linear else ''} + "
                          f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"),
             "global_batch": args.batch * world,
@@ -189,6 +197,7 @@ def main():
             "epoch_time_kind": "measured" if epoch_s is not None else "ms_per_step x batches/epoch",
             "batches_per_epoch_per_gpu": batches_per_epoch,
             "sampler_s_per_step": sample_s / args.steps,
+            "layer_sizes_top_down": layer_sizes,
         },
         "roofline": {
             "bound": "hbm",

@@ -120,27 +120,45 @@ struct ATile {
   }
 };
 
-// B k-slice [32 x 128]: thread (kk = tid>>5, r = tid&31) moves k-rows kk + 8p,
-// columns r + 32t (t = 0..3): each load is 32 consecutive floats per half-wave.
-// BFULL (N % 128 == 0): the 4 columns are immediate offsets of one address.
+// B k-slice [32 x 128] into the permuted image Bs[k][j][r][t] (col 64j+32t+r).
+// BFULL (N % 128 == 0, the usual hidden width): thread quad g = tid + 256i
+// (k = g/32, j = (g%32)/16, m = g%16) loads the float2 pairs at columns
+// 64j+2m and 64j+32+2m, which are exactly the 4 consecutive image slots
+// (r = 2m, 2m+1; t = 0, 1): 8 float2 loads + 4 ds_write_b128 per step.
+// Otherwise thread (kk = tid>>5, r = tid&31) moves k-rows kk + 8p, columns
+// r + 32t (clamped): 16 loads + 8 ds_write_b64.
 template <bool BFULL>
 struct BTile {
   const float* base;
   int coff[4];
   int kk, r;
   __device__ BTile(const float* B, int N, int n0) {
-    kk = threadIdx.x >> 5;
-    r = threadIdx.x & 31;
-    base = B + (BFULL ? n0 + r : 0);
+    const int tid = threadIdx.x;
+    if (BFULL) {
+      kk = tid >> 5;  // k row of quad i: kk + 8i
+      const int qq = tid & 31;
+      r = (qq >> 4) * 64 + 2 * (qq & 15);  // c0 (relative to n0); image slot 4*qq
+      base = B + n0 + r;
+    } else {
+      kk = tid >> 5;
+      r = tid & 31;
+      base = B;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) coff[t] = min(n0 + r + 32 * t, N - 1);
+      for (int t = 0; t < 4; ++t) coff[t] = min(n0 + r + 32 * t, N - 1);
+    }
   }
   __device__ __forceinline__ void load(uint64_t ldb, int K, int k0, float (&v)[16]) const {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const float* row = base + (uint64_t)min(k0 + kk + 8 * p, K - 1) * ldb;
+      if (BFULL) {
+        const float2 x0 = *reinterpret_cast<const float2*>(row);
+        const float2 x1 = *reinterpret_cast<const float2*>(row + 32);
+        v[4 * p] = x0.x; v[4 * p + 1] = x1.x; v[4 * p + 2] = x0.y; v[4 * p + 3] = x1.y;
+      } else {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) v[4 * p + t] = BFULL ? row[32 * t] : row[coff[t]];
+        for (int t = 0; t < 4; ++t) v[4 * p + t] = row[coff[t]];
+      }
     }
   }
   __device__ __forceinline__ void store(float* __restrict__ sb, int K, int k0,
@@ -149,10 +167,16 @@ struct BTile {
     for (int p = 0; p < 4; ++p) {
       const uint32_t mk = k0 + kk + 8 * p < K ? ~0u : 0u;
       float* row = sb + (kk + 8 * p) * kBN;
-      *reinterpret_cast<float2*>(row + 2 * r) =
-          make_float2(msk(v[4 * p], mk), msk(v[4 * p + 1], mk));
-      *reinterpret_cast<float2*>(row + 64 + 2 * r) =
-          make_float2(msk(v[4 * p + 2], mk), msk(v[4 * p + 3], mk));
+      if (BFULL) {
+        *reinterpret_cast<float4*>(row + 4 * (threadIdx.x & 31)) =
+            make_float4(msk(v[4 * p], mk), msk(v[4 * p + 1], mk), msk(v[4 * p + 2], mk),
+                        msk(v[4 * p + 3], mk));
+      } else {
+        *reinterpret_cast<float2*>(row + 2 * r) =
+            make_float2(msk(v[4 * p], mk), msk(v[4 * p + 1], mk));
+        *reinterpret_cast<float2*>(row + 64 + 2 * r) =
+            make_float2(msk(v[4 * p + 2], mk), msk(v[4 * p + 3], mk));
+      }
     }
   }
 };
@@ -306,7 +330,7 @@ static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t 
   int avec = 1;
   if (inner % 4 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
   else if (inner % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
-  const bool bfull = N % kBN == 0;
+  const bool bfull = N % kBN == 0 && ldb % 2 == 0 && (uintptr_t)B % 8 == 0;
 #define NTS_GEMM(AV, BF)                                                                          \
   hipLaunchKernelGGL((k_gemm<TRANS_A, AV, BF>), grid, dim3(kGT), 0, st, M, N, K, A, lda, B, ldb, \
                      C, ldc, kchunk, split_stride)

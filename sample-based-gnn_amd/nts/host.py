@@ -35,7 +35,8 @@ def ext():
 def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, drop_rate=0.5,
                rng_mode=_abi.NTS_RNG_PHILOX, weight="sum", fused_gather=True,
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
-               seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False):
+               seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False,
+               early_aggregate=True, sampler_priority=True):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -53,6 +54,8 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.hip_gemm = bool(hip_gemm)
     c.pipeline = bool(pipeline)
     c.fuse_linear = bool(fuse_linear)
+    c.early_aggregate = bool(early_aggregate)
+    c.sampler_priority = bool(sampler_priority)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

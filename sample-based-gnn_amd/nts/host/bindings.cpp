@@ -137,6 +137,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
       .def_readwrite("pipeline", &GCNConfig::pipeline)
       .def_readwrite("fuse_linear", &GCNConfig::fuse_linear)
+      .def_readwrite("early_aggregate", &GCNConfig::early_aggregate)
+      .def_readwrite("sampler_priority", &GCNConfig::sampler_priority)
       .def_readwrite("shuffle", &GCNConfig::shuffle)
       .def_readwrite("profile", &GCNConfig::profile)
       .def_readwrite("seed", &GCNConfig::seed);

@@ -28,11 +28,12 @@ static double now_s() {
 }
 
 // ---------------------------------------------------------------------------
-NtsStream::NtsStream(int device, void* stream, uint64_t seed)
+NtsStream::NtsStream(int device, void* stream, uint64_t seed, bool high_priority)
     : device_(device),
       torch_stream_(stream ? c10::hip::getStreamFromExternal((hipStream_t)stream, (c10::DeviceIndex)device)
-                           : c10::hip::getStreamFromPool(false, (c10::DeviceIndex)device)) {
-  // never hand the legacy NULL stream to the C-ABI (NULL there means "create one")
+                           : c10::hip::getStreamFromPool(high_priority, (c10::DeviceIndex)device)) {
+  // a pool stream, never the legacy NULL stream: our kernels must not
+  // serialise with every other blocking stream of the device
   hip_check(nts_hip_ctx_create(&ctx_, device, (void*)torch_stream_.stream(), seed),
             "nts_hip_ctx_create");
 }

@@ -46,13 +46,28 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                           cfg.pipeline ? 2 : 1, csr,
                                           cfg.weight_type != WeightType::None);
   sampler->rng_mode = cfg.rng_mode;
-  if (cfg.pipeline) ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+  if (cfg.pipeline)
+    ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed,
+                                     cfg.sampler_priority);
   // size the scratch arenas once so the training loop never allocates
   uint64_t items = graph->global_vertices;
   for (auto* s : sampler->ssg->sampled_sgs) items = std::max<uint64_t>({items, s->e_cap, s->v_cap});
   hip_check(nts_hip_ctx_reserve(cs->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
   if (ss)
     hip_check(nts_hip_ctx_reserve(ss->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
+  // The bottom graph op Y_0 = A_0 X depends on the sampled graph and the
+  // feature table only (not on the weights), so it is issued right behind the
+  // sampling, on the sampling stream: with the pipeline it runs while the
+  // previous batch trains (HBM-bound gather next to MFMA-bound GEMMs).
+  early_ = cfg.early_aggregate && cfg.fused_gather;
+  const int nslots = cfg.pipeline ? 2 : 1;
+  for (int i = 0; i < nslots; ++i) {
+    TORCH_CHECK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming) == hipSuccess,
+                "hipEventCreate");
+    if (early_)
+      pre_y_[i] = torch::empty({(int64_t)sampler->ssgs[i]->sampled_sgs[L - 1]->v_cap, F.size(1)},
+                               F.options());
+  }
   init_nn();
 }
 
@@ -61,7 +76,47 @@ GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
   }
+  for (auto* e : ready_)
+    if (e) (void)hipEventDestroy(e);
   for (auto* p : P) delete p;
+}
+
+// Sampling of one batch into `slot` (sample_gpu_fast's device part), then —
+// with early aggregation — the bottom graph op (fused feature gather +
+// aggregation, SingleGPUAllSampleGraphOp::forward on the feature table) on
+// the same stream.  Sizes are device-side: nothing here waits for the host.
+void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
+  sampler->issue_gpu_sample(cfg.batch_size, slot, st, cfg.weight_type);
+  if (early_) {
+    auto guard = st.guard();
+    const int L = (int)P.size();
+    sampCSC* s = sampler->ssgs[slot]->sampled_sgs[L - 1];
+    std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
+    if (cfg.profile) {
+      if (ev_pending_ >= 4096) resolve_profile();
+      evp = &next_events();
+      (void)hipEventRecord(evp->first, (hipStream_t)st.stream());
+    }
+    NtsVar& y = pre_y_[slot];
+    hip_check(nts_hip_spmm_csc_fwd(st.ctx(), s->dev_c_o(), s->dev_r_i(), s->dev_e_w_f(),
+                                   dptr<uint32_t>(s->sizes), s->v_cap, F.data_ptr<float>(),
+                                   (uint64_t)F.stride(0), s->dev_src(), (uint32_t)F.size(1),
+                                   y.data_ptr<float>(), (uint64_t)y.stride(0)),
+              "nts_hip_spmm_csc_fwd(early)");
+    if (evp) (void)hipEventRecord(evp->second, (hipStream_t)st.stream());
+  }
+  TORCH_CHECK(hipEventRecord(ready_[slot], (hipStream_t)st.stream()) == hipSuccess,
+              "hipEventRecord");
+}
+
+// compulsory bytes of the bottom aggregation: distinct src rows once, index +
+// weight per edge, offsets, output rows (+ source map when fused)  
+void GCN_SAMPLE_ALLGPU_impl::account_bottom(SampledSubgraph* sg, bool fused_map) {
+  sampCSC* s = sg->sampled_sgs[sg->layers - 1];
+  const double Fd = (double)F.size(1);
+  agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
+               Fd * 4.0 * s->v_size + (fused_map ? 4.0 * s->src_size : 0.0);
+  agg_calls += 1;
 }
 
 std::pair<hipEvent_t, hipEvent_t>& GCN_SAMPLE_ALLGPU_impl::next_events() {
@@ -126,13 +181,26 @@ NtsVar GCN_SAMPLE_ALLGPU_impl::vertexForward(int l, NtsVar& a) {
   return torch::dropout(torch::relu(P[l]->forward(a)), cfg.drop_rate, ctx.is_train());
 }
 
-std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool keep) {
+std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool keep,
+                                                     const NtsVar* pre_y) {
   const int L = (int)P.size();
   std::vector<NtsVar> acts;
   NtsVar X0;
   if (!cfg.fused_gather) sampler->load_feature_gpu(*cs, sg, X0, F);
-  NtsVar X = X0;
-  for (int l = 0; l < L; ++l) {
+  int l0 = 0;
+  NtsVar X;
+  if (pre_y) {  // bottom graph op already ran on the sampling stream (issue())
+    NtsVar Y = pre_y->narrow(0, 0, (int64_t)sg->sampled_sgs[L - 1]->v_size);
+    X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(0, a); }, Y);
+    if (keep) {
+      acts.push_back(Y.detach());
+      acts.push_back(X.detach());
+    }
+    l0 = 1;
+  } else {
+    X = X0;
+  }
+  for (int l = l0; l < L; ++l) {
     const int hop = L - 1 - l;
     NtsVar Y;
     const bool bottom = (l == 0);
@@ -175,13 +243,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
     else
       Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(X, sg, graph.get(), hop, cs.get(), false);
     if (bottom) {
-      sampCSC* s = sg->sampled_sgs[hop];
-      const double Fd = (double)F.size(1);
-      // compulsory bytes: distinct src rows once, index+weight per edge,
-      // offsets, output rows (+ source map when fused)   
-      agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
-                   Fd * 4.0 * s->v_size + (cfg.fused_gather ? 4.0 * s->src_size : 0.0);
-      agg_calls += 1;
+      account_bottom(sg, cfg.fused_gather);
       if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
     }
     X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(l, a); }, Y);
@@ -236,22 +298,23 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
     prefetched_ = -1;
   } else {
     slot = next_slot_;
-    sampler->issue_gpu_sample(cfg.batch_size, slot, sst, cfg.weight_type);
+    issue(slot, sst);
   }
   SampledSubgraph* sg = sampler->finish_gpu_sample(slot);
   if (ss) {
     next_slot_ = slot ^ 1;
     if (sampler->sample_not_finished()) {  // prefetch the next batch behind this one
-      sampler->issue_gpu_sample(cfg.batch_size, next_slot_, *ss, cfg.weight_type);
+      issue(next_slot_, *ss);
       prefetched_ = next_slot_;
     }
   }
-  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), sg->sampled, 0) == hipSuccess,
+  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[slot], 0) == hipSuccess,
               "hipStreamWaitEvent");
   double t1 = now_s();
   sampler->load_label_gpu(*cs, sg, target, L_GT);
   ctx.train();
-  auto acts = forward(sg, false);
+  if (early_) account_bottom(sg, true);
+  auto acts = forward(sg, false, early_ ? &pre_y_[slot] : nullptr);
   NtsVar out = acts.back();
   Loss(out, target);
   ctx.self_backward(false);

@@ -18,6 +18,8 @@ struct GCNConfig {
   bool deterministic_backward = true; // CSR transpose gather instead of atomics
   bool hip_gemm = true;               // layer GEMMs on the hand-written MFMA kernels
   bool pipeline = true;               // sample batch i+1 on its own stream while i trains
+  bool sampler_priority = true;       // pipelined sampler on a high-priority stream
+  bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
@@ -58,12 +60,19 @@ class GCN_SAMPLE_ALLGPU_impl {
 
  private:
   NtsVar vertexForward(int l, NtsVar& a);
-  std::vector<NtsVar> forward(SampledSubgraph* sg, bool keep);
+  std::vector<NtsVar> forward(SampledSubgraph* sg, bool keep, const NtsVar* pre_y = nullptr);
+  void issue(int slot, NtsStream& st);
+  void account_bottom(SampledSubgraph* sg, bool fused_map);
   void Loss(NtsVar& left, NtsVar& right);
   void Update();
   std::pair<hipEvent_t, hipEvent_t>& next_events();
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool_;
   size_t ev_pending_ = 0;
+  // early aggregation: per sampler slot, the bottom graph op's output and the
+  // event after which it (and the slot's sampled graph) is ready
+  NtsVar pre_y_[2];
+  hipEvent_t ready_[2] = {nullptr, nullptr};
+  bool early_ = false;
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch
   int next_slot_ = 0;
 };

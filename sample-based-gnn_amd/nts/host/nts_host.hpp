@@ -55,7 +55,10 @@ class NtsStream {
   // stream == nullptr: a dedicated stream from torch's pool; torch work that
   // must be ordered with our kernels runs under guard() (the reference binds
   // a pool stream per pipeline thread, toolkits/GCN_SAMPLE_GPU.hpp:444-466).
-  NtsStream(int device, void* stream, uint64_t seed);
+  // high_priority: the pool's high-priority stream (the pipelined sampler:
+  // its short, latency-bound kernels are dispatched ahead of the training
+  // stream's long ones, which fill the remaining CU slots)
+  NtsStream(int device, void* stream, uint64_t seed, bool high_priority = false);
   ~NtsStream();
   NtsStream(const NtsStream&) = delete;
   NtsStream& operator=(const NtsStream&) = delete;

@@ -153,3 +153,17 @@ def test_training_is_deterministic_and_learns(E, graph):
     for x, y in zip(a.weights(), b.weights()):
         assert torch.equal(x, y)
     assert torch.isfinite(a.loss).item()
+
+
+def test_early_aggregation_is_identical(E, graph):
+    """Bottom graph op issued behind the sampler (early_aggregate) vs inside the
+    forward: same sampled graphs, same kernels -> identical weights."""
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, early_aggregate=True)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, early_aggregate=False)
+    for _ in range(3):
+        a.train_batch()
+        b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)
