@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--no-early-agg", action="store_true",
                    help="bottom aggregation on the training stream instead of behind the sampler")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
+    p.add_argument("--no-fuse-act", action="store_true",
+                   help="relu/dropout as torch ops instead of the GEMM epilogue")
     p.add_argument("--fuse-linear", action="store_true",
                    help="bottom layer: aggregation and first GEMM in one kernel")
     p.add_argument("--cpu-baseline-steps", type=int, default=1)
@@ -107,7 +109,8 @@ def main():
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
                           fuse_linear=args.fuse_linear, early_aggregate=not args.no_early_agg,
-                          sampler_priority=not args.no_priority)
+                          sampler_priority=not args.no_priority,
+                          fuse_activation=not args.no_fuse_act)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and args.no_early_agg
                     and args.hidden <= 128)

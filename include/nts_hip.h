@@ -220,6 +220,24 @@ int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx *ctx, const uint32_t *column_offset,
 int nts_hip_gemm_f32(nts_hip_ctx *ctx, int trans_a, int M, int N, int K, const float *A,
                      uint64_t lda, const float *B, uint64_t ldb, float *C, uint64_t ldc);
 
+/* Hidden-layer forward with its activation fused into the GEMM epilogue:
+ *   C = dropout(relu(A B), p)   — vertexForward's
+ *   torch::dropout(torch::relu(x.matmul(W)), drop_rate, training)
+ *   (toolkits/GCN_SAMPLE_GPU.hpp:252-266).  Inverted dropout: kept elements
+ *   are scaled by 1/(1-p); keep(row, col) comes from Philox4x32-10 keyed by
+ *   `seed`, counter {row/4, col, offset} (word row%4 >= p*2^32), so the mask
+ *   is reproducible and never stored.  p == 0: plain relu (eval). */
+int nts_hip_gemm_relu_dropout_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *A,
+                                  uint64_t lda, const float *B, uint64_t ldb, float *C,
+                                  uint64_t ldc, float p, uint64_t seed, uint64_t offset);
+
+/* Its weight gradient: C[M,N] = A[K,M]^T (B ⊙ [X > 0] · scale), with B = dX
+ * (the gradient of the layer output) and X the forward output, scale =
+ * 1/(1-p): the relu and dropout backward fused into the operand load. */
+int nts_hip_gemm_tn_masked_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *A,
+                               uint64_t lda, const float *B, uint64_t ldb, const float *X,
+                               uint64_t ldx, float scale, float *C, uint64_t ldc);
+
 /* ---- optimiser ---------------------------------------------------------- */
 /* Fused Adam step on one parameter (n elements), element-wise identical to
  *  bias_correction != 0: Parameter::learnC2C_with_decay_Adam (core/NtsScheduler.hpp:863-880)

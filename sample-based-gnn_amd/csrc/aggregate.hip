@@ -22,6 +22,7 @@ struct VT<1> {
   __device__ static __forceinline__ T zero() { return 0.f; }
   __device__ static __forceinline__ T madd(T a, T x, float w) { return a + x * w; }
   __device__ static __forceinline__ T scale(T x, float w) { return x * w; }
+  __device__ static __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
 };
 template <>
 struct VT<2> {
@@ -31,6 +32,11 @@ struct VT<2> {
     return make_float2(a.x + x.x * w, a.y + x.y * w);
   }
   __device__ static __forceinline__ T scale(T x, float w) { return make_float2(x.x * w, x.y * w); }
+  __device__ static __forceinline__ void st_nt(T* p, T v) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 u = {v.x, v.y};
+    __builtin_nontemporal_store(u, reinterpret_cast<f2*>(p));
+  }
 };
 template <>
 struct VT<4> {
@@ -41,6 +47,11 @@ struct VT<4> {
   }
   __device__ static __forceinline__ T scale(T x, float w) {
     return make_float4(x.x * w, x.y * w, x.z * w, x.w * w);
+  }
+  __device__ static __forceinline__ void st_nt(T* p, T v) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4 u = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(u, reinterpret_cast<f4*>(p));
   }
 };
 
@@ -72,9 +83,9 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
         uint32_t r[kUnroll];
         float ww[kUnroll];
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {
-          r[j] = idx[e + j];
-          ww[j] = w ? w[e + j] : 1.0f;
+        for (int j = 0; j < kUnroll; ++j) {  // streamed once: do not keep in cache
+          r[j] = __builtin_nontemporal_load(idx + e + j);
+          ww[j] = w ? __builtin_nontemporal_load(w + e + j) : 1.0f;
         }
         if (MAP) {
 #pragma unroll
@@ -107,9 +118,9 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
         }
       }
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const uint32_t col = c0 + sl + c * LPD;
-        if (col < nv) yrow[col] = acc[c];
+      for (int c = 0; c < NCH; ++c) {  // output rows are not re-read here: keep them
+        const uint32_t col = c0 + sl + c * LPD;  // out of the cache that serves x rows
+        if (col < nv) V::st_nt(yrow + col, acc[c]);
       }
     }
   }

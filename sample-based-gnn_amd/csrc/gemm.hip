@@ -127,30 +127,35 @@ struct ATile {
 // (r = 2m, 2m+1; t = 0, 1): 8 float2 loads + 4 ds_write_b128 per step.
 // Otherwise thread (kk = tid>>5, r = tid&31) moves k-rows kk + 8p, columns
 // r + 32t (clamped): 16 loads + 8 ds_write_b64.
-template <bool BFULL>
+template <bool BFULL, bool BMASK>
 struct BTile {
+  static constexpr int NX = BMASK ? 16 : 1;
   const float* base;
+  const float* xbase;  // BMASK: the forward output X (same shape as B)
   int coff[4];
   int kk, r;
-  __device__ BTile(const float* B, int N, int n0) {
+  __device__ BTile(const float* B, const float* X, int N, int n0) {
     const int tid = threadIdx.x;
     if (BFULL) {
       kk = tid >> 5;  // k row of quad i: kk + 8i
       const int qq = tid & 31;
       r = (qq >> 4) * 64 + 2 * (qq & 15);  // c0 (relative to n0); image slot 4*qq
       base = B + n0 + r;
+      xbase = BMASK ? X + n0 + r : nullptr;
     } else {
       kk = tid >> 5;
       r = tid & 31;
       base = B;
+      xbase = X;
 #pragma unroll
       for (int t = 0; t < 4; ++t) coff[t] = min(n0 + r + 32 * t, N - 1);
     }
   }
-  __device__ __forceinline__ void load(uint64_t ldb, int K, int k0, float (&v)[16]) const {
+  __device__ __forceinline__ void load1(const float* b, uint64_t ld, int K, int k0,
+                                        float* v) const {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-      const float* row = base + (uint64_t)min(k0 + kk + 8 * p, K - 1) * ldb;
+      const float* row = b + (uint64_t)min(k0 + kk + 8 * p, K - 1) * ld;
       if (BFULL) {
         const float2 x0 = *reinterpret_cast<const float2*>(row);
         const float2 x1 = *reinterpret_cast<const float2*>(row + 32);
@@ -161,34 +166,61 @@ struct BTile {
       }
     }
   }
+  __device__ __forceinline__ void load(uint64_t ldb, uint64_t ldx, int K, int k0, float (&v)[16],
+                                       float (&vx)[NX]) const {
+    load1(base, ldb, K, k0, v);
+    if constexpr (BMASK) load1(xbase, ldx, K, k0, vx);
+  }
+  // B value as staged: k >= K -> 0; BMASK: G * scale where X > 0, else 0
+  // (relu + dropout backward: X = dropout(relu(Z)) > 0 exactly where dZ != 0)
+  __device__ __forceinline__ float val(const float (&v)[16], const float (&vx)[NX], int q,
+                                       uint32_t mk, float bscale) const {
+    if constexpr (BMASK) return vx[q] > 0.f ? msk(v[q], mk) * bscale : 0.f;
+    return msk(v[q], mk);
+  }
   __device__ __forceinline__ void store(float* __restrict__ sb, int K, int k0,
-                                        const float (&v)[16]) const {
+                                        const float (&v)[16], const float (&vx)[NX],
+                                        float bscale) const {
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const uint32_t mk = k0 + kk + 8 * p < K ? ~0u : 0u;
       float* row = sb + (kk + 8 * p) * kBN;
       if (BFULL) {
         *reinterpret_cast<float4*>(row + 4 * (threadIdx.x & 31)) =
-            make_float4(msk(v[4 * p], mk), msk(v[4 * p + 1], mk), msk(v[4 * p + 2], mk),
-                        msk(v[4 * p + 3], mk));
+            make_float4(val(v, vx, 4 * p, mk, bscale), val(v, vx, 4 * p + 1, mk, bscale),
+                        val(v, vx, 4 * p + 2, mk, bscale), val(v, vx, 4 * p + 3, mk, bscale));
       } else {
         *reinterpret_cast<float2*>(row + 2 * r) =
-            make_float2(msk(v[4 * p], mk), msk(v[4 * p + 1], mk));
+            make_float2(val(v, vx, 4 * p, mk, bscale), val(v, vx, 4 * p + 1, mk, bscale));
         *reinterpret_cast<float2*>(row + 64 + 2 * r) =
-            make_float2(msk(v[4 * p + 2], mk), msk(v[4 * p + 3], mk));
+            make_float2(val(v, vx, 4 * p + 2, mk, bscale), val(v, vx, 4 * p + 3, mk, bscale));
       }
     }
   }
 };
 
+// Fused extras of one launch.
+//   EPI:   C = keep(row, col) ? relu(AB) * scale : 0 — ReLU + inverted dropout;
+//          keep from Philox4x32-10 (key = seed, counter = {row>>2, col, offset})
+//          word row&3 >= keep_threshold (p * 2^32): P(keep) = 1 - p.
+//   BMASK: B = G * bscale where X > 0 (the backward of EPI, X its output).
+struct GemmExtra {
+  uint32_t keep_threshold = 0;
+  float scale = 1.f;
+  uint64_t seed = 0, offset = 0;
+  const float* bx = nullptr;
+  uint64_t ldbx = 0;
+  float bscale = 1.f;
+};
+
 // C_tile = op(A) B over k in [kbeg, kend); result written to C (ldc) or to a
 // partial slab.  grid: x = M tiles, y = N tiles, z = k splits.
 // Wave w: rows 32*(w&1) .. +32 of the block tile, columns 64*(w>>1) .. +64.
-template <bool TRANS_A, int AVEC, bool BFULL>
+template <bool TRANS_A, int AVEC, bool BFULL, bool EPI, bool BMASK>
 __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const float* __restrict__ A,
                                                  uint64_t lda, const float* __restrict__ B,
                                                  uint64_t ldb, float* __restrict__ C, uint64_t ldc,
-                                                 int kchunk, uint64_t split_stride) {
+                                                 int kchunk, uint64_t split_stride, GemmExtra ex) {
   __shared__ GemmSmem sm;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -203,12 +235,13 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
   const ATile<TRANS_A, AVEC> at(A, lda, M, kend, m0);
-  const BTile<BFULL> bt(B, N, n0);
+  const BTile<BFULL, BMASK> bt(B, ex.bx, N, n0);
+  constexpr int NX = BTile<BFULL, BMASK>::NX;
 
   // Two register staging sets: the global loads of k-step j+2 are issued at
   // the start of step j (two steps of MFMA work cover the HBM latency), the
   // set holding step j+1 is written to the other LDS buffer at its end.
-  float av0[8], bv0[16], av1[8], bv1[16];
+  float av0[8], bv0[16], av1[8], bv1[16], bx0[NX], bx1[NX];
   const int nsteps = kbeg < kend ? (kend - kbeg + kBK - 1) / kBK : 0;
   auto compute = [&](int cur) {
     float a[16];
@@ -234,11 +267,11 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
   };
   if (nsteps > 0) {
     at.load(lda, kend, kbeg, av0);
-    bt.load(ldb, kend, kbeg, bv0);
+    bt.load(ldb, ex.ldbx, kend, kbeg, bv0, bx0);
     at.load(lda, kend, kbeg + kBK, av1);
-    bt.load(ldb, kend, kbeg + kBK, bv1);
+    bt.load(ldb, ex.ldbx, kend, kbeg + kBK, bv1, bx1);
     at.store(sm.a[0], kend, kbeg, av0);
-    bt.store(sm.b[0], kend, kbeg, bv0);
+    bt.store(sm.b[0], kend, kbeg, bv0, bx0, ex.bscale);
   }
   __syncthreads();
   int j = 0;
@@ -248,21 +281,21 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
     // (sched_barrier: keep the loads at the head of the step and the stores at
     // its tail — the scheduler would otherwise sink the loads below the MFMAs)
     at.load(lda, kend, k0 + 2 * kBK, av0);
-    bt.load(ldb, kend, k0 + 2 * kBK, bv0);
+    bt.load(ldb, ex.ldbx, kend, k0 + 2 * kBK, bv0, bx0);
     __builtin_amdgcn_sched_barrier(0);
     compute(0);
     __builtin_amdgcn_sched_barrier(0);
     at.store(sm.a[1], kend, k0 + kBK, av1);
-    bt.store(sm.b[1], kend, k0 + kBK, bv1);
+    bt.store(sm.b[1], kend, k0 + kBK, bv1, bx1, ex.bscale);
     __syncthreads();
     // step j+1: LDS buffer 1, loads of step j+3 -> set 1, set 0 (step j+2) -> buffer 0
     at.load(lda, kend, k0 + 3 * kBK, av1);
-    bt.load(ldb, kend, k0 + 3 * kBK, bv1);
+    bt.load(ldb, ex.ldbx, kend, k0 + 3 * kBK, bv1, bx1);
     __builtin_amdgcn_sched_barrier(0);
     compute(1);
     __builtin_amdgcn_sched_barrier(0);
     at.store(sm.a[0], kend, k0 + 2 * kBK, av0);
-    bt.store(sm.b[0], kend, k0 + 2 * kBK, bv0);
+    bt.store(sm.b[0], kend, k0 + 2 * kBK, bv0, bx0, ex.bscale);
     __syncthreads();
   }
   if (j < nsteps) compute(0);  // odd step count: the last step is already in buffer 0
@@ -274,9 +307,22 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
     const int col = n0 + 64 * wc + 32 * t + r;
     if (col >= N) continue;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t rr = wrow0 + 8 * (i >> 2) + 4 * h + (i & 3);
-      if (rr < M) Cb[(uint64_t)rr * ldc + col] = acc[t][i];
+    for (int g = 0; g < 4; ++g) {  // 4 consecutive rows: one Philox call
+      const int64_t r4 = wrow0 + 8 * g + 4 * h;
+      float o[4] = {acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
+      if constexpr (EPI) {
+        const uint4 rnd = philox4x32_10(
+            make_uint4((uint32_t)(r4 >> 2), (uint32_t)col, (uint32_t)ex.offset,
+                       (uint32_t)(ex.offset >> 32)),
+            make_uint2((uint32_t)ex.seed, (uint32_t)(ex.seed >> 32)));
+        const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          o[q] = (wd[q] >= ex.keep_threshold && o[q] > 0.f) ? o[q] * ex.scale : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (r4 + q < M) Cb[(uint64_t)(r4 + q) * ldc + col] = o[q];
     }
   }
 }
@@ -320,20 +366,21 @@ __global__ void k_sum_splits(const float* __restrict__ part, int splits, uint64_
   }
 }
 
-template <bool TRANS_A>
+template <bool TRANS_A, bool EPI, bool BMASK>
 static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t lda,
                   const float* B, uint64_t ldb, float* C, uint64_t ldc, int splits, int kchunk,
-                  uint64_t split_stride) {
+                  uint64_t split_stride, const GemmExtra& ex) {
   dim3 grid(ceil_div(M, kBM), ceil_div(N, kBN), splits);
   // vector width of the A tile loads: rows of the loaded dimension must stay aligned
   const int inner = TRANS_A ? M : K;
   int avec = 1;
   if (inner % 4 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
   else if (inner % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
-  const bool bfull = N % kBN == 0 && ldb % 2 == 0 && (uintptr_t)B % 8 == 0;
-#define NTS_GEMM(AV, BF)                                                                          \
-  hipLaunchKernelGGL((k_gemm<TRANS_A, AV, BF>), grid, dim3(kGT), 0, st, M, N, K, A, lda, B, ldb, \
-                     C, ldc, kchunk, split_stride)
+  bool bfull = N % kBN == 0 && ldb % 2 == 0 && (uintptr_t)B % 8 == 0;
+  if (BMASK) bfull = bfull && ex.ldbx % 2 == 0 && (uintptr_t)ex.bx % 8 == 0;
+#define NTS_GEMM(AV, BF)                                                                      \
+  hipLaunchKernelGGL((k_gemm<TRANS_A, AV, BF, EPI, BMASK>), grid, dim3(kGT), 0, st, M, N, K, \
+                     A, lda, B, ldb, C, ldc, kchunk, split_stride, ex)
   if (avec == 4) { if (bfull) NTS_GEMM(4, true); else NTS_GEMM(4, false); }
   else if (avec == 2) { if (bfull) NTS_GEMM(2, true); else NTS_GEMM(2, false); }
   else { if (bfull) NTS_GEMM(1, true); else NTS_GEMM(1, false); }
@@ -342,41 +389,34 @@ static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t 
   return NTS_OK;
 }
 
-}  // namespace nts_hip
-
-using namespace nts_hip;
-
-extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int K,
-                                const float* A, uint64_t lda, const float* B, uint64_t ldb,
-                                float* C, uint64_t ldc) {
-  NTS_CHECK_ARG(ctx && C, "NULL argument");
-  NTS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative size");
-  if (M == 0 || N == 0) return NTS_OK;
-  NTS_CHECK_ARG((A && B) || K == 0, "NULL operand");
-  NTS_CHECK_ARG(ldb >= (uint64_t)N && ldc >= (uint64_t)N, "leading dimension");
-  NTS_CHECK_ARG(trans_a ? lda >= (uint64_t)M : lda >= (uint64_t)K, "lda");
-  NTS_HIP_TRY(hipSetDevice(ctx->device));
+// One GEMM: split the reduction when the output grid alone cannot fill the
+// chip (partials summed in split order by k_sum_splits: deterministic).  EPI
+// needs the complete sum, so it never splits.
+template <bool EPI, bool BMASK>
+static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float* A, uint64_t lda,
+                const float* B, uint64_t ldb, float* C, uint64_t ldc, const GemmExtra& ex) {
   hipStream_t st = ctx->stream;
-  if (K == 0) {
+  if (K == 0) {  // empty reduction: C = 0 (and relu/dropout of 0 is 0)
     for (int i = 0; i < M; ++i) NTS_HIP_TRY(hipMemsetAsync(C + (uint64_t)i * ldc, 0, N * 4, st));
     return NTS_OK;
   }
-  // split the reduction when the output grid alone cannot fill 256 CUs
   const int tiles = (int)(ceil_div(M, kBM) * ceil_div(N, kBN));
   int splits = 1;
   const int ksteps = (K + kBK - 1) / kBK;
   // 3 blocks per CU are resident (LDS): aim the split grid at 768 blocks
-  if (tiles < 384) splits = std::max(1, std::min(768 / tiles, ksteps / 4));
+  if (!EPI && tiles < 384) splits = std::max(1, std::min(768 / tiles, ksteps / 4));
   const int kchunk = ((ksteps + splits - 1) / splits) * kBK;
   splits = (K + kchunk - 1) / kchunk;
   if (splits == 1)
-    return trans_a ? launch<true>(st, M, N, K, A, lda, B, ldb, C, ldc, 1, kchunk, 0)
-                   : launch<false>(st, M, N, K, A, lda, B, ldb, C, ldc, 1, kchunk, 0);
+    return trans_a ? launch<true, EPI, BMASK>(st, M, N, K, A, lda, B, ldb, C, ldc, 1, kchunk, 0, ex)
+                   : launch<false, EPI, BMASK>(st, M, N, K, A, lda, B, ldb, C, ldc, 1, kchunk, 0, ex);
   const uint64_t stride = (uint64_t)M * N;
   NTS_RET(ensure_scratch(ctx, stride * splits * sizeof(float) + 256));
   float* part = (float*)ctx->scratch;
-  NTS_RET(trans_a ? launch<true>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride)
-                  : launch<false>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride));
+  const int rc =
+      trans_a ? launch<true, EPI, BMASK>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride, ex)
+              : launch<false, EPI, BMASK>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride, ex);
+  if (rc != NTS_OK) return rc;
   const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
   const uint32_t g = std::max(1u, std::min(ceil_div(v4 ? stride / 4 : stride, 256), kMaxGrid));
   if (v4)
@@ -387,4 +427,59 @@ extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int
                        N, C, ldc);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
+}
+
+}  // namespace nts_hip
+
+using namespace nts_hip;
+
+#define NTS_GEMM_ARGS_CHECK(trans_a)                                            \
+  NTS_CHECK_ARG(ctx && C, "NULL argument");                                     \
+  NTS_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative size");                   \
+  if (M == 0 || N == 0) return NTS_OK;                                          \
+  NTS_CHECK_ARG((A && B) || K == 0, "NULL operand");                            \
+  NTS_CHECK_ARG(ldb >= (uint64_t)N && ldc >= (uint64_t)N, "leading dimension"); \
+  NTS_CHECK_ARG((trans_a) ? lda >= (uint64_t)M : lda >= (uint64_t)K, "lda");    \
+  NTS_HIP_TRY(hipSetDevice(ctx->device))
+
+extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int K,
+                                const float* A, uint64_t lda, const float* B, uint64_t ldb,
+                                float* C, uint64_t ldc) {
+  NTS_GEMM_ARGS_CHECK(trans_a);
+  return trans_a ? gemm<false, false>(ctx, true, M, N, K, A, lda, B, ldb, C, ldc, GemmExtra())
+                 : gemm<false, false>(ctx, false, M, N, K, A, lda, B, ldb, C, ldc, GemmExtra());
+}
+
+extern "C" int nts_hip_gemm_relu_dropout_f32(nts_hip_ctx* ctx, int M, int N, int K, const float* A,
+                                             uint64_t lda, const float* B, uint64_t ldb, float* C,
+                                             uint64_t ldc, float p, uint64_t seed,
+                                             uint64_t offset) {
+  NTS_GEMM_ARGS_CHECK(false);
+  NTS_CHECK_ARG(p >= 0.f && p <= 1.f, "dropout probability must be in [0, 1]");
+  GemmExtra ex;
+  ex.seed = seed;
+  ex.offset = offset;
+  if (p >= 1.f) {  // everything dropped (torch returns zeros)
+    ex.keep_threshold = 0xFFFFFFFFu;
+    ex.scale = 0.f;
+  } else {
+    const double t = (double)p * 4294967296.0;
+    ex.keep_threshold = (uint32_t)std::min(t, 4294967295.0);
+    ex.scale = 1.0f / (1.0f - p);
+  }
+  return gemm<true, false>(ctx, false, M, N, K, A, lda, B, ldb, C, ldc, ex);
+}
+
+extern "C" int nts_hip_gemm_tn_masked_f32(nts_hip_ctx* ctx, int M, int N, int K, const float* A,
+                                          uint64_t lda, const float* B, uint64_t ldb,
+                                          const float* X, uint64_t ldx, float scale, float* C,
+                                          uint64_t ldc) {
+  NTS_GEMM_ARGS_CHECK(true);
+  NTS_CHECK_ARG(X || K == 0, "NULL mask operand");
+  NTS_CHECK_ARG(ldx >= (uint64_t)N, "ldx");
+  GemmExtra ex;
+  ex.bx = X;
+  ex.ldbx = ldx;
+  ex.bscale = scale;
+  return gemm<false, true>(ctx, true, M, N, K, A, lda, B, ldb, C, ldc, ex);
 }

@@ -32,20 +32,6 @@ constexpr int kSetCap = 1024;  // max fanout of the rejection path
 // ---------------------------------------------------------------------------
 // random words
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
-  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
-  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-    k.x += W0;
-    k.y += W1;
-  }
-  return c;
-}
-
 // Word `idx` of the PHILOX stream of (dst, layer, batch_seq).
 __device__ __forceinline__ uint32_t philox_word(uint64_t seed, uint32_t dst, uint32_t layer,
                                                 uint64_t batch_seq, uint32_t idx) {

@@ -121,6 +121,22 @@ class HipContext:
         check(self.lib.nts_hip_gemm_f32(self.h, int(trans_a), M, N, K, ptr(A), A.stride(0), ptr(B),
                                         B.stride(0), ptr(C), C.stride(0)))
 
+    def gemm_relu_dropout(self, A, B, C, p=0.0, seed=0, offset=0):
+        """C = dropout(relu(A @ B), p) with the Philox mask of (seed, offset)."""
+        M, K = A.shape
+        N = B.shape[1]
+        check(self.lib.nts_hip_gemm_relu_dropout_f32(self.h, M, N, K, ptr(A), A.stride(0), ptr(B),
+                                                     B.stride(0), ptr(C), C.stride(0), float(p),
+                                                     int(seed), int(offset)))
+
+    def gemm_tn_masked(self, A, G, X, C, scale=1.0):
+        """C = A.T @ (G * (X > 0) * scale)."""
+        K, M = A.shape
+        N = G.shape[1]
+        check(self.lib.nts_hip_gemm_tn_masked_f32(self.h, M, N, K, ptr(A), A.stride(0), ptr(G),
+                                                  G.stride(0), ptr(X), X.stride(0), float(scale),
+                                                  ptr(C), C.stride(0)))
+
     def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
         check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,
                                     beta1, beta2, eps, wd, beta1_t, beta2_t, int(bias_correction)))

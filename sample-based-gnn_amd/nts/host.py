@@ -36,7 +36,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                rng_mode=_abi.NTS_RNG_PHILOX, weight="sum", fused_gather=True,
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
                seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False,
-               early_aggregate=True, sampler_priority=True):
+               early_aggregate=True, sampler_priority=True, fuse_activation=True):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -56,6 +56,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.fuse_linear = bool(fuse_linear)
     c.early_aggregate = bool(early_aggregate)
     c.sampler_priority = bool(sampler_priority)
+    c.fuse_activation = bool(fuse_activation)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

@@ -487,6 +487,48 @@ struct HipLinearFn : public torch::autograd::Function<HipLinearFn> {
     return {dx, dW, NtsVar()};
   }
 };
+// dropout(relu(x W)) with the activation in the GEMM epilogue and its
+// backward in the weight-gradient GEMM's operand load (nts_hip.h).
+struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar x, NtsVar W, double p, int64_t seed,
+                        int64_t offset, int64_t cs_ptr) {
+    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    NtsVar xc = x.contiguous(), Wc = W.contiguous();
+    const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
+    TORCH_CHECK(Wc.size(0) == K, "hip_linear_act: shape mismatch");
+    NtsVar X = torch::empty({M, N}, xc.options());
+    hip_check(nts_hip_gemm_relu_dropout_f32(cs->ctx(), (int)M, (int)N, (int)K,
+                                            xc.data_ptr<float>(), (uint64_t)K,
+                                            Wc.data_ptr<float>(), (uint64_t)N, X.data_ptr<float>(),
+                                            (uint64_t)N, (float)p, (uint64_t)seed,
+                                            (uint64_t)offset),
+              "nts_hip_gemm_relu_dropout_f32");
+    ctx->save_for_backward({xc, Wc, X});
+    ctx->saved_data["cs"] = cs_ptr;
+    ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
+    return X;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto saved = ctx->get_saved_variables();
+    NtsVar x = saved[0], W = saved[1], X = saved[2];
+    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    const float scale = (float)ctx->saved_data["scale"].toDouble();
+    NtsVar g = grads[0].contiguous();
+    const int64_t M = x.size(0), K = x.size(1), N = W.size(1);
+    NtsVar dx, dW;
+    if (ctx->needs_input_grad(1)) {
+      dW = torch::empty({K, N}, W.options());
+      hip_check(nts_hip_gemm_tn_masked_f32(cs->ctx(), (int)K, (int)N, (int)M, x.data_ptr<float>(),
+                                           (uint64_t)K, g.data_ptr<float>(), (uint64_t)N,
+                                           X.data_ptr<float>(), (uint64_t)N, scale,
+                                           dW.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_gemm_tn_masked_f32");
+    }
+    if (ctx->needs_input_grad(0)) dx = (g * (X > 0).to(g.dtype()) * scale).matmul(W.t());
+    return {dx, dW, NtsVar(), NtsVar(), NtsVar(), NtsVar()};
+  }
+};
+
 struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, NtsVar y, int64_t sg_ptr,
                         int64_t cs_ptr) {
@@ -520,6 +562,12 @@ struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
   }
 };
 }  // namespace
+
+NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
+                      NtsStream* cs) {
+  return HipLinearActFn::apply(x, W, p, (int64_t)seed, (int64_t)offset,
+                               reinterpret_cast<int64_t>(cs));
+}
 
 bool hip_agg_linear_supported(int64_t F, int64_t N) {
   const int64_t half = (F + 1) / 2, Kh = (half + 1) / 2 * 2, LDP = 2 * Kh + 2;

@@ -178,6 +178,11 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::weights() const {
 NtsVar GCN_SAMPLE_ALLGPU_impl::vertexForward(int l, NtsVar& a) {
   const int L = (int)P.size();
   if (l == L - 1) return P[l]->forward(a).log_softmax(1);
+  if (cfg.hip_gemm && cfg.fuse_activation) {
+    const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
+    return hip_linear_act(a, P[l]->W, p, (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1,
+                          dropout_calls_++, cs.get());
+  }
   return torch::dropout(torch::relu(P[l]->forward(a)), cfg.drop_rate, ctx.is_train());
 }
 

@@ -18,6 +18,7 @@ struct GCNConfig {
   bool deterministic_backward = true; // CSR transpose gather instead of atomics
   bool hip_gemm = true;               // layer GEMMs on the hand-written MFMA kernels
   bool pipeline = true;               // sample batch i+1 on its own stream while i trains
+  bool fuse_activation = true;        // hidden layers: relu + dropout in the MFMA GEMM
   bool sampler_priority = true;       // pipelined sampler on a high-priority stream
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
@@ -73,6 +74,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   NtsVar pre_y_[2];
   hipEvent_t ready_[2] = {nullptr, nullptr};
   bool early_ = false;
+  uint64_t dropout_calls_ = 0;  // Philox offset of the fused dropout masks
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch
   int next_slot_ = 0;
 };

@@ -300,6 +300,10 @@ class NtsContext {
 // x.matmul(W) on the MFMA fp32 kernels (nts_hip_gemm_f32) with its own
 // backward: dW = x^T dZ (split-reduction, deterministic), dx = dZ W^T.
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
+// dropout(relu(x W), p) in one MFMA GEMM (activation in the epilogue, Philox
+// mask of (seed, offset)); autograd: dW = x^T (dX ⊙ [X > 0] / (1-p)) fused.
+NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
+                      NtsStream* cs);
 
 // Bottom layer fused: Y = A X (into the caller's `y`, bit-identical to the
 // graph op) and Z = Y W in one kernel (nts_hip_spmm_csc_fwd_linear); autograd

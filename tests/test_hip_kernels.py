@@ -390,3 +390,79 @@ def test_spmm_fwd_linear_fused(hip, cora, F, N, mapped):
     hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v, x, W, z2, row_map=rm)
     torch.cuda.synchronize()
     assert torch.equal(z2, z[:v])
+
+
+def _philox4x32_10(c, k):
+    """Philox4x32-10 reference (numpy uint64 arithmetic), c: 4 x uint32 arrays, k: 2 ints."""
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    c = [x.astype(np.uint64) for x in c]
+    k0, k1 = np.uint64(k[0]), np.uint64(k[1])
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(M0) * c[0]
+        p1 = np.uint64(M1) * c[2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c = [hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0]
+        k0 = (k0 + np.uint64(W0)) & mask
+        k1 = (k1 + np.uint64(W1)) & mask
+    return [x.astype(np.uint32) for x in c]
+
+
+def _dropout_keep(M, N, p, seed, offset):
+    rows = np.arange(M, dtype=np.uint64)[:, None] * np.ones((1, N), np.uint64)
+    cols = np.ones((M, 1), np.uint64) * np.arange(N, dtype=np.uint64)[None, :]
+    c = [(rows >> np.uint64(2)).astype(np.uint32), cols.astype(np.uint32),
+         np.full((M, N), offset & 0xFFFFFFFF, np.uint32), np.full((M, N), offset >> 32, np.uint32)]
+    w = _philox4x32_10(c, (seed & 0xFFFFFFFF, seed >> 32))
+    word = np.choose((rows & np.uint64(3)).astype(np.int64), w)
+    thr = min(int(p * 4294967296.0), 0xFFFFFFFF)
+    return word >= np.uint32(thr)
+
+
+@pytest.mark.parametrize("M,N,K,p", [(5000, 128, 602, 0.5), (333, 41, 100, 0.3), (1000, 128, 128, 0.0),
+                                     (64, 7, 33, 1.0)])
+def test_gemm_relu_dropout_epilogue(hip, M, N, K, p):
+    """dropout(relu(A @ B)) fused in the GEMM epilogue: the mask is the
+    documented Philox stream (checked against a numpy restatement), kept
+    values are relu(AB)/(1-p) within fp32 GEMM tolerance."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=DEV, generator=g)
+    B = torch.randn(K, N, device=DEV, generator=g)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    seed, offset = 0x1234_5678_9ABC, 77
+    hip.gemm_relu_dropout(A, B, C, p=p, seed=seed, offset=offset)
+    torch.cuda.synchronize()
+    Z = (A.double() @ B.double()).cpu()
+    keep = torch.from_numpy(_dropout_keep(M, N, p, seed, offset)) if p < 1.0 else torch.zeros(M, N, dtype=torch.bool)
+    scale = 1.0 / (1.0 - p) if p < 1.0 else 0.0
+    ref = torch.where(keep & (Z > 0), Z * scale, torch.zeros_like(Z))
+    tol = 2e-6 * K ** 0.5 + 1e-6
+    got = C.cpu().double()
+    # elements whose relu decision sits within rounding of 0 may legitimately differ
+    near0 = Z.abs() < 1e-4 * K ** 0.5
+    torch.testing.assert_close(got[~near0], ref[~near0], rtol=tol, atol=tol * 4 * max(scale, 1))
+    if 0 < p < 1:
+        frac = keep.double().mean().item()
+        assert abs(frac - (1 - p)) < 0.02
+    # same (seed, offset) -> same output; another offset -> another mask
+    C2 = torch.empty_like(C)
+    hip.gemm_relu_dropout(A, B, C2, p=p, seed=seed, offset=offset)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("M,N,K", [(602, 128, 20000), (128, 41, 3000), (64, 128, 77)])
+def test_gemm_tn_masked(hip, M, N, K):
+    """C = A^T (G * (X > 0) * scale): the relu+dropout backward fused into the
+    weight-gradient GEMM."""
+    g = torch.Generator(device=DEV).manual_seed(M * 3 + N + K)
+    A = torch.randn(K, M, device=DEV, generator=g)
+    G = torch.randn(K, N, device=DEV, generator=g)
+    X = torch.relu(torch.randn(K, N, device=DEV, generator=g))
+    C = torch.full((M, N), float("nan"), device=DEV)
+    hip.gemm_tn_masked(A, G, X, C, scale=2.0)
+    ref = A.double().t() @ (G.double() * (X > 0).double() * 2.0)
+    torch.cuda.synchronize()
+    tol = 2e-6 * K ** 0.5 + 1e-6
+    torch.testing.assert_close(C.double(), ref, rtol=tol, atol=tol * 8)

@@ -142,9 +142,10 @@ def test_training_step_matches_oracle_step(E, graph):
         torch.testing.assert_close(w1, ref, rtol=1e-5, atol=1e-5)
 
 
-def test_training_is_deterministic_and_learns(E, graph):
-    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200)
-    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200)
+@pytest.mark.parametrize("drop", [0.0, 0.5])
+def test_training_is_deterministic_and_learns(E, graph, drop):
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=drop)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=drop)
     for _ in range(2):
         a.run_epoch()
         b.run_epoch()
@@ -167,3 +168,17 @@ def test_early_aggregation_is_identical(E, graph):
     b.synchronize()
     for x, y in zip(a.weights(), b.weights()):
         assert torch.equal(x, y)
+
+
+def test_fused_activation_matches_torch_ops(E, graph):
+    """relu (+ dropout at p = 0) in the GEMM epilogue and its backward in the
+    weight-gradient GEMM vs torch relu/dropout around the plain GEMM."""
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, fuse_activation=True)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, fuse_activation=False)
+    for _ in range(3):
+        a.train_batch()
+        b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5)
