@@ -58,7 +58,7 @@ def parse():
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
     p.add_argument("--fuse-linear", action="store_true",
                    help="bottom layer: aggregation and first GEMM in one kernel")
-    p.add_argument("--cpu-baseline-steps", type=int, default=1)
+    p.add_argument("--cpu-baseline-steps", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     p.add_argument("--epoch", action="store_true", help="also time one full epoch")

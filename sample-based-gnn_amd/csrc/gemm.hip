@@ -1,15 +1,16 @@
-// fp32 GEMMs of the GCN layer update on the matrix cores (v_mfma_f32_32x32x2_f32,
-// exact fp32 products, fp32 accumulate).
+// fp32 GEMMs of the GCN layer update on the matrix cores (exact fp32 products,
+// fp32 accumulate: v_mfma_f32_32x32x2_f32 / v_mfma_f32_16x16x4_f32).
 //
 // The layer GEMMs are tall-skinny: Z = Y W with Y [~150K x 602], W [602 x 128]
 // (Parameter::forward, core/NtsScheduler.hpp:859-862) and the weight gradient
 // dW = Y^T dZ (reduction over the ~150K sampled rows).  The library TN kernel
-// runs these at ~36-45 TF/s; here the tiles are shaped for them:
-//   NN: block 128 rows x 128 cols, 4 waves of 32 rows x 4 MFMA tiles; A rows
-//       are read straight into registers (16 consecutive k per lane — the k
-//       order inside an MFMA step is a free permutation shared by A and B),
-//       the B k-slice [32 x 128] is staged in LDS (double buffered, permuted so
-//       one ds_read_b128 feeds a lane's 4 column tiles) and shared by the 4 waves.
+// runs these at ~36-45 TF/s; here:
+//   NN, W slice fits LDS (K <= 608): k_gemm_wres — the weight's column slice
+//       stays resident in LDS for the whole launch, A rows stream straight to
+//       registers, no barrier in the main loop (see its comment).
+//   NN otherwise, and TN: k_gemm — block 64 rows x 128 cols, 4 waves of
+//       32 x 64 on v_mfma_f32_32x32x2_f32, A and B k-slices staged in LDS
+//       (double buffered, register prefetch two steps deep).
 //   TN: C = A^T B with the long reduction split over blocks; per-split
 //       partial tiles are summed in split order by a second kernel
 //       (deterministic, no atomics).
@@ -366,6 +367,226 @@ __global__ void k_sum_splits(const float* __restrict__ part, int splits, uint64_
   }
 }
 
+// ---------------------------------------------------------------------------
+// NN with the weight slice resident in LDS (k_gemm_wres).
+//
+// The layer GEMM multiplies a tall activation [M x K] (M ~ 10^5) by a small
+// weight [K x N].  A 1024-thread block (16 waves, one block per CU) copies
+// the column slice W[:, n0 .. n0+NCOL) into LDS ONCE (K <= 624 at NCOL = 64,
+// K <= 312 at NCOL = 128) and then streams row tiles of A with no barrier in
+// the main loop:
+//   * v_mfma_f32_16x16x4_f32; lane (i, g) = (lane & 15, lane >> 4);
+//   * a wave task = 32 rows (2 row tiles) x NCOL columns (NCOL/16 col tiles);
+//   * lane (i, g) loads A[row i][k0 + 8g .. k0 + 8g + 7] of a 32-deep k-block
+//     straight to registers (128 contiguous bytes per row per k-block) —
+//     the k order inside a k-block is a free permutation shared with B:
+//     MFMA t of the block sums k = k0 + 8g + t over the four lane groups;
+//   * B operands come from LDS (lgkmcnt), so the only vector-memory queue
+//     entries are A's: the next k-block's rows are loaded a whole k-block
+//     (64 MFMAs) ahead without any in-order vmcnt stall;
+//   * LDS image sB[k][64q + 4i + jj] = W[k][n0 + (NCOL/16) i + 4q + jj]: one
+//     ds_read_b128 per (k, q) per lane, conflict-free under gfx950's b128
+//     lane grouping.
+// Column blocks of the same row tile run on the same XCD (block b and the
+// blocks b + 8·c), so the second read of an A tile is an L2/MALL hit.
+// Numerics: every output is one k-ordered fp32 fma chain (exact products),
+// fixed by the shapes — deterministic.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kWresRT = 2;  // 16-row tiles per wave task
+// 16 waves (4 per SIMD, <= 128 VGPRs) at NCOL = 64; 8 waves at NCOL = 128,
+// whose 32 accumulator registers more per lane need the larger budget
+template <int NCOL>
+constexpr int wres_threads() { return NCOL == 128 ? 512 : 1024; }
+
+// Raw loads of one 32-deep k-block of the wave's A rows (no masking: a select
+// on the loaded value would make the compiler wait for the load right away).
+template <int AVEC>
+__device__ __forceinline__ void wres_load_a(const float* const (&arow)[kWresRT], int kb, int g,
+                                            float (&a)[kWresRT][8]) {
+  const int kbase = 32 * kb + 8 * g;
+#pragma unroll
+  for (int rt = 0; rt < kWresRT; ++rt) {
+    const float* p = arow[rt] + kbase;
+    if (AVEC == 4) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float4 x = reinterpret_cast<const float4*>(p)[q];
+        a[rt][4 * q] = x.x; a[rt][4 * q + 1] = x.y; a[rt][4 * q + 2] = x.z; a[rt][4 * q + 3] = x.w;
+      }
+    } else if (AVEC == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float2 x = reinterpret_cast<const float2*>(p)[q];
+        a[rt][2 * q] = x.x; a[rt][2 * q + 1] = x.y;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a[rt][q] = p[q];
+    }
+  }
+}
+
+// The last (partial) k-block, issued before the main loop: raw loads at
+// clamped addresses (no select on the values here, see above) ...
+__device__ __forceinline__ void wres_load_tail(const float* const (&arow)[kWresRT], int K, int kb,
+                                               int g, float (&a)[kWresRT][8]) {
+  const int kbase = 32 * kb + 8 * g;
+#pragma unroll
+  for (int rt = 0; rt < kWresRT; ++rt)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[rt][e] = arow[rt][min(kbase + e, K - 1)];
+}
+// ... masked only when used (k >= K contributes 0 * padding)
+__device__ __forceinline__ void wres_mask_tail(int K, int kb, int g, float (&a)[kWresRT][8]) {
+  const int kbase = 32 * kb + 8 * g;
+#pragma unroll
+  for (int rt = 0; rt < kWresRT; ++rt)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[rt][e] = msk(a[rt][e], kbase + e < K ? ~0u : 0u);
+}
+
+template <int NCOL>
+__device__ __forceinline__ void wres_mfma(const float* __restrict__ bb, const float (&a)[kWresRT][8],
+                                          f32x4 (&acc)[kWresRT][NCOL / 16]) {
+  constexpr int CQ = NCOL / 64;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    f32x4 b[CQ];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) b[q] = *reinterpret_cast<const f32x4*>(bb + t * NCOL + 64 * q);
+#pragma unroll
+    for (int rt = 0; rt < kWresRT; ++rt)
+#pragma unroll
+      for (int q = 0; q < CQ; ++q)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          acc[rt][4 * q + jj] =
+              __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt][t], b[q][jj], acc[rt][4 * q + jj], 0, 0, 0);
+  }
+}
+
+template <int NCOL, int AVEC, bool EPI>
+__global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
+    int M, int N, int K, int nkb, const float* __restrict__ A, uint64_t lda,
+    const float* __restrict__ B, uint64_t ldb, float* __restrict__ C, uint64_t ldc, int ncb,
+    int vec_store, GemmExtra ex) {
+  extern __shared__ __attribute__((aligned(16))) float sB[];
+  constexpr int CT = NCOL / 16;  // 16-column tiles per wave task
+  constexpr int CQ = CT / 4;     // ds_read_b128 per k
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int cb = (blockIdx.x >> 3) % ncb;
+  const int bi = ((blockIdx.x >> 3) / ncb) * 8 + (blockIdx.x & 7);
+  const int bpc = gridDim.x / ncb;
+  const int n0 = cb * NCOL;
+  const int Kp = nkb * 32;
+  constexpr int WT = wres_threads<NCOL>();
+  // fill in float4 pieces: local columns 4c4 .. 4c4+3 land on 4 consecutive
+  // image slots (c = CT ii + j with j % 4 == 0 .. 3)
+  if (ldb % 4 == 0 && ((uintptr_t)B & 15) == 0) {
+#pragma unroll 4
+    for (int e = tid; e < Kp * (NCOL / 4); e += WT) {
+      const int k = e / (NCOL / 4), c = 4 * (e % (NCOL / 4));
+      const int ii = c / CT, j = c % CT;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k < K) v = *reinterpret_cast<const float4*>(B + (uint64_t)k * ldb + n0 + c);
+      *reinterpret_cast<float4*>(sB + k * NCOL + 64 * (j >> 2) + 4 * ii) = v;
+    }
+  } else {
+    for (int e = tid; e < Kp * NCOL; e += WT) {
+      const int k = e / NCOL, c = e % NCOL;
+      const int ii = c / CT, j = c % CT;
+      const float v = k < K ? B[(uint64_t)k * ldb + n0 + c] : 0.f;
+      sB[k * NCOL + 64 * (j >> 2) + 4 * ii + (j & 3)] = v;
+    }
+  }
+  __syncthreads();
+  (void)N;
+  const int rows_per_task = 16 * kWresRT;
+  const int ntask = (M + rows_per_task - 1) / rows_per_task;
+  const int nwaves = bpc * (WT / 64);
+  for (int task = wv * bpc + bi; task < ntask; task += nwaves) {
+    const int64_t m0 = (int64_t)task * rows_per_task;
+    const float* arow[kWresRT];
+#pragma unroll
+    for (int rt = 0; rt < kWresRT; ++rt) {
+      const int64_t r = m0 + 16 * rt + i;
+      arow[rt] = A + (uint64_t)(r < M ? r : M - 1) * lda;
+    }
+    f32x4 acc[kWresRT][CT];
+#pragma unroll
+    for (int rt = 0; rt < kWresRT; ++rt)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // full k-blocks (32 (kb+1) <= K) are read unmasked, two register sets
+    // alternate so that the next block's loads are in flight during the
+    // current block's 64 MFMAs; the partial last block is read masked.
+    const int nfull = K / 32;
+    float a0[kWresRT][8], a1[kWresRT][8], at[kWresRT][8];
+    const float* bb = sB + 8 * g * NCOL + 4 * i;
+    const bool tail = nfull < nkb;
+    if (tail) wres_load_tail(arow, K, nfull, g, at);
+    if (nfull > 0) wres_load_a<AVEC>(arow, 0, g, a0);
+    int kb = 0;
+    for (; kb + 2 <= nfull; kb += 2) {
+      wres_load_a<AVEC>(arow, kb + 1, g, a1);
+      __builtin_amdgcn_sched_barrier(0);
+      wres_mfma<NCOL>(bb + 32 * kb * NCOL, a0, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      // unconditional (clamped) so that every path through the loop has the
+      // same queue of loads: the compiler then waits with a count, not vmcnt(0)
+      wres_load_a<AVEC>(arow, min(kb + 2, nfull - 1), g, a0);
+      __builtin_amdgcn_sched_barrier(0);
+      wres_mfma<NCOL>(bb + 32 * (kb + 1) * NCOL, a1, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (kb < nfull) {  // odd number of full blocks: a0 holds block kb
+      wres_mfma<NCOL>(bb + 32 * kb * NCOL, a0, acc);
+      ++kb;
+    }
+    if (tail) {
+      wres_mask_tail(K, nfull, g, at);
+      wres_mfma<NCOL>(bb + 32 * nfull * NCOL, at, acc);
+    }
+    // epilogue: acc[rt][j][v] = C[m0 + 16 rt + 4 g + v][n0 + CT i + j]
+#pragma unroll
+    for (int rt = 0; rt < kWresRT; ++rt) {
+      const int64_t r4 = m0 + 16 * rt + 4 * g;
+      float o[4][CT];
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v][j] = acc[rt][j][v];
+        if constexpr (EPI) {
+          const int col = n0 + CT * i + j;
+          const uint4 rnd = philox4x32_10(
+              make_uint4((uint32_t)(r4 >> 2), (uint32_t)col, (uint32_t)ex.offset,
+                         (uint32_t)(ex.offset >> 32)),
+              make_uint2((uint32_t)ex.seed, (uint32_t)(ex.seed >> 32)));
+          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            o[v][j] = (wd[v] >= ex.keep_threshold && o[v][j] > 0.f) ? o[v][j] * ex.scale : 0.f;
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if (r4 + v >= M) continue;
+        float* crow = C + (uint64_t)(r4 + v) * ldc + n0 + CT * i;
+        if (vec_store) {
+#pragma unroll
+          for (int q = 0; q < CQ; ++q)
+            *reinterpret_cast<float4*>(crow + 4 * q) =
+                make_float4(o[v][4 * q], o[v][4 * q + 1], o[v][4 * q + 2], o[v][4 * q + 3]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < CT; ++j) crow[j] = o[v][j];
+        }
+      }
+    }
+  }
+}
+
 template <bool TRANS_A, bool EPI, bool BMASK>
 static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t lda,
                   const float* B, uint64_t ldb, float* C, uint64_t ldc, int splits, int kchunk,
@@ -392,6 +613,53 @@ static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t 
 // One GEMM: split the reduction when the output grid alone cannot fill the
 // chip (partials summed in split order by k_sum_splits: deterministic).  EPI
 // needs the complete sum, so it never splits.
+// Column slice width of k_gemm_wres for this shape (0: not applicable).
+static int wres_ncol(int M, int N, int K) {
+  if (M < 2048 || K < 1) return 0;
+  if (K <= 288 && N % 128 == 0) return 128;
+  if (K <= 608 && N % 64 == 0) return 64;
+  return 0;
+}
+
+template <bool EPI>
+static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const float* A, uint64_t lda,
+                       const float* B, uint64_t ldb, float* C, uint64_t ldc, const GemmExtra& ex) {
+  const int nkb = (K + 31) / 32;
+  const int ncb = N / ncol;
+  const int per = std::max(1, 32 / ncb);  // blocks per (XCD, column block)
+  const int grid = 8 * ncb * per;
+  const size_t lds = (size_t)nkb * 32 * ncol * sizeof(float);
+  int avec = 1;
+  if (K % 4 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
+  else if (K % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
+  const int vs = (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) ? 1 : 0;
+#define NTS_WRES(NC, AV)                                                                        \
+  do {                                                                                          \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_wres<NC, AV, EPI>),   \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
+    hipLaunchKernelGGL((k_gemm_wres<NC, AV, EPI>), dim3(grid), dim3(wres_threads<NC>()), lds, st, \
+                       M, N, K, nkb, A, lda, B, ldb, C, ldc, ncb, vs, ex);                      \
+  } while (0)
+  if (ncol == 128) {
+    if (avec == 4) NTS_WRES(128, 4); else if (avec == 2) NTS_WRES(128, 2); else NTS_WRES(128, 1);
+  } else {
+    if (avec == 4) NTS_WRES(64, 4); else if (avec == 2) NTS_WRES(64, 2); else NTS_WRES(64, 1);
+  }
+#undef NTS_WRES
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+// Kernel selection (NTS_GEMM_TILED=1 forces the LDS-tiled kernel everywhere,
+// for A/B comparisons).
+static bool force_tiled() {
+  static const bool f = [] {
+    const char* e = getenv("NTS_GEMM_TILED");
+    return e && e[0] == '1';
+  }();
+  return f;
+}
+
 template <bool EPI, bool BMASK>
 static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float* A, uint64_t lda,
                 const float* B, uint64_t ldb, float* C, uint64_t ldc, const GemmExtra& ex) {
@@ -399,6 +667,12 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
   if (K == 0) {  // empty reduction: C = 0 (and relu/dropout of 0 is 0)
     for (int i = 0; i < M; ++i) NTS_HIP_TRY(hipMemsetAsync(C + (uint64_t)i * ldc, 0, N * 4, st));
     return NTS_OK;
+  }
+  if (!force_tiled()) {
+    if (!trans_a && !BMASK) {
+      const int ncol = wres_ncol(M, N, K);
+      if (ncol) return launch_wres<EPI>(st, ncol, M, N, K, A, lda, B, ldb, C, ldc, ex);
+    }
   }
   const int tiles = (int)(ceil_div(M, kBM) * ceil_div(N, kBN));
   int splits = 1;

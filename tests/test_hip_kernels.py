@@ -324,7 +324,11 @@ def test_adam_matches_reference_torch_expressions(hip, bias_correction):
 
 
 @pytest.mark.parametrize("M,N,K", [(150000, 128, 602), (1000, 41, 128), (333, 7, 1433),
-                                   (5, 256, 100), (10000, 47, 256), (1, 1, 1), (64, 128, 0)])
+                                   (5, 256, 100), (10000, 47, 256), (1, 1, 1), (64, 128, 0),
+                                   # LDS-resident-weight NN / row-streaming TN kernels:
+                                   # odd K, 128-column slices, narrow N, tails
+                                   (4097, 128, 301), (3001, 256, 200), (2100, 64, 602),
+                                   (333, 256, 5000), (700, 128, 3)])
 @pytest.mark.parametrize("trans_a", [False, True])
 def test_gemm_f32_mfma(hip, M, N, K, trans_a):
     """MFMA fp32 GEMM vs torch fp64 (asymmetric data, ragged tails, long split
@@ -421,7 +425,7 @@ def _dropout_keep(M, N, p, seed, offset):
 
 
 @pytest.mark.parametrize("M,N,K,p", [(5000, 128, 602, 0.5), (333, 41, 100, 0.3), (1000, 128, 128, 0.0),
-                                     (64, 7, 33, 1.0)])
+                                     (64, 7, 33, 1.0), (4001, 256, 128, 0.5), (2050, 64, 77, 0.2)])
 def test_gemm_relu_dropout_epilogue(hip, M, N, K, p):
     """dropout(relu(A @ B)) fused in the GEMM epilogue: the mask is the
     documented Philox stream (checked against a numpy restatement), kept
@@ -452,7 +456,8 @@ def test_gemm_relu_dropout_epilogue(hip, M, N, K, p):
     assert torch.equal(C, C2)
 
 
-@pytest.mark.parametrize("M,N,K", [(602, 128, 20000), (128, 41, 3000), (64, 128, 77)])
+@pytest.mark.parametrize("M,N,K", [(602, 128, 20000), (128, 41, 3000), (64, 128, 77),
+                                   (602, 128, 135758), (1000, 256, 999)])
 def test_gemm_tn_masked(hip, M, N, K):
     """C = A^T (G * (X > 0) * scale): the relu+dropout backward fused into the
     weight-gradient GEMM."""
