@@ -269,7 +269,13 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   const Shape s = pick_shape(nv);
   const uint32_t gpb = kAggThreads / s.lpd;
   // enough waves to saturate HBM: 256 CUs x 16 waves, grid-stride beyond
-  const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), 4096u));
+  // (NTS_AGG_GRID caps it, leaving CU slots to a concurrently running stream)
+  static const uint32_t cap = [] {
+    const char* e = getenv("NTS_AGG_GRID");
+    const long v = e ? atol(e) : 0;
+    return v > 0 ? (uint32_t)v : 4096u;
+  }();
+  const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), cap));
   if (vec == 4)
     return launch_gather_vec<4, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
   if (vec == 2)

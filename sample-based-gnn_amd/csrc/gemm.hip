@@ -587,6 +587,259 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
   }
 }
 
+// ---------------------------------------------------------------------------
+// TN with a block-sized output tile in accumulators (k_gemm_tn_big):
+// C[M,N] = A[K,M]^T op(B)[K,N] — the weight gradient, M = layer input width
+// (~602), N = 128, K = sampled rows (~10^5).  A 512-thread block owns a
+// 640 x 128 output tile for one k-chunk: wave w keeps rows 80 w .. 80 w + 79
+// x all 128 columns in 40 v_mfma_f32_16x16x4_f32 accumulators (rows
+// interleaved over the lane index: row = 80 w + 5 i + rt, col = 8 i + j).
+// Each 16-deep k-step is staged coalesced into LDS (A rows [16 x 640], the
+// masked B rows [16 x 128]); per 4 k a lane reads 5 + 8 operand floats from
+// LDS for 40 MFMAs (the old 64 x 128 tile read one LDS value per MFMA).
+// Pitches make both reads conflict-free: LDY = 656 (rows of 4 lane groups
+// land on disjoint b32 banks at stride 5), LDG = 132.  Partial tiles of the
+// k-chunks are summed in a fixed order (k_sum_splits_tree).
+constexpr int kTbWaves = 8;
+constexpr int kTbRT = 5;
+constexpr int kTbRows = kTbWaves * 16 * kTbRT;  // 640
+constexpr int kTbKS = 16;                       // k rows per step
+constexpr int kTbLDY = 656;
+constexpr int kTbLDG = 132;
+
+struct TbSmem {
+  float y[2][kTbKS * kTbLDY];
+  float g[2][kTbKS * kTbLDG];
+};
+
+template <bool BMASK, int AVEC>
+__global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
+    int M, int N, int K, const float* __restrict__ A, uint64_t lda, const float* __restrict__ B,
+    uint64_t ldb, float* __restrict__ C, uint64_t ldc, int kchunk, uint64_t split_stride,
+    int nrg, int ncb, GemmExtra ex) {
+  extern __shared__ __attribute__((aligned(16))) float smem_raw[];
+  TbSmem& sm = *reinterpret_cast<TbSmem*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int rg = blockIdx.x % nrg;
+  const int cb = (blockIdx.x / nrg) % ncb;
+  const int split = blockIdx.x / (nrg * ncb);
+  const int r0 = rg * kTbRows, n0 = cb * 128;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nsteps = kbeg < kend ? (kend - kbeg + kTbKS - 1) / kTbKS : 0;
+  // staging roles: A element pairs e = tid + 512 p -> (k row e / 320, cols 2 (e % 320) + {0,1});
+  // B/X float4 q = tid -> (k row q / 32, cols 4 (q % 32) .. +3)
+  constexpr int NAV = kTbRows / AVEC;                  // vectors per staged A row
+  constexpr int NAL = kTbKS * NAV / (kTbWaves * 64);  // A loads per thread per step
+  // one register staging set: the loads of step st+1 are issued before the
+  // MFMAs of step st (which read LDS only) and written to the other LDS
+  // buffer after them
+  float av[NAL * AVEC];
+  float4 bv, xv;
+  const int bk = tid / 32, bc = 4 * (tid % 32);
+  auto load = [&](int step) {
+    const int kb = kbeg + step * kTbKS;
+#pragma unroll
+    for (int p = 0; p < NAL; ++p) {
+      const int e = tid + kTbWaves * 64 * p;
+      const int kk = min(kb + e / NAV, K - 1);
+      const int c = min(r0 + AVEC * (e % NAV), M - AVEC);
+      const float* src = A + (uint64_t)kk * lda + c;
+      if (AVEC == 2) {
+        const float2 x = *reinterpret_cast<const float2*>(src);
+        av[2 * p] = x.x; av[2 * p + 1] = x.y;
+      } else {
+        av[p] = *src;
+      }
+    }
+    const int kk = min(kb + bk, K - 1);
+    bv = *reinterpret_cast<const float4*>(B + (uint64_t)kk * ldb + n0 + bc);
+    if constexpr (BMASK) xv = *reinterpret_cast<const float4*>(ex.bx + (uint64_t)kk * ex.ldbx + n0 + bc);
+  };
+  auto store = [&](int step, float* sy, float* sg) {
+    const int kb = kbeg + step * kTbKS;
+#pragma unroll
+    for (int p = 0; p < NAL; ++p) {
+      const int e = tid + kTbWaves * 64 * p;
+      const int kr = e / NAV, c = AVEC * (e % NAV);
+#pragma unroll
+      for (int q = 0; q < AVEC; ++q) {
+        const bool ok = (kb + kr < kend) && (r0 + c + q < M);
+        sy[kr * kTbLDY + c + q] = ok ? av[AVEC * p + q] : 0.f;
+      }
+    }
+    const bool okk = kb + bk < kend;
+    float b4[4] = {bv.x, bv.y, bv.z, bv.w};
+    if constexpr (BMASK) {
+      const float x4[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) b4[q] = x4[q] > 0.f ? b4[q] * ex.bscale : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b4[q] = okk ? b4[q] : 0.f;
+    *reinterpret_cast<float4*>(sg + bk * kTbLDG + bc) = make_float4(b4[0], b4[1], b4[2], b4[3]);
+  };
+  f32x4 acc[kTbRT][8];
+#pragma unroll
+  for (int rt = 0; rt < kTbRT; ++rt)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const float* sy, const float* sg) {
+    const float* ya = sy + g * kTbLDY + wv * 16 * kTbRT + kTbRT * i;
+    const float* gb = sg + g * kTbLDG + 8 * i;
+#pragma unroll
+    for (int t = 0; t < kTbKS / 4; ++t) {
+      float a[kTbRT];
+#pragma unroll
+      for (int rt = 0; rt < kTbRT; ++rt) a[rt] = ya[4 * t * kTbLDY + rt];
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(gb + 4 * t * kTbLDG);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(gb + 4 * t * kTbLDG + 4);
+#pragma unroll
+      for (int rt = 0; rt < kTbRT; ++rt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt], b0[j], acc[rt][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[rt][4 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[rt], b1[j], acc[rt][4 + j], 0, 0, 0);
+      }
+    }
+  };
+  if (nsteps > 0) {
+    load(0);
+    store(0, sm.y[0], sm.g[0]);
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    load(st + 1);  // clamped rows past the chunk; masked (zero) when stored
+    __builtin_amdgcn_sched_barrier(0);
+    compute(sm.y[cur], sm.g[cur]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 1 < nsteps) store(st + 1, sm.y[cur ^ 1], sm.g[cur ^ 1]);
+    __syncthreads();
+  }
+  // acc[rt][j][v] = C[r0 + 80 wv + 5 (4 g + v) + rt][n0 + 8 i + j]
+  float* Cb = C + (uint64_t)split * split_stride;
+  const bool vec = (ldc % 4 == 0) && ((uintptr_t)Cb % 16 == 0);
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+#pragma unroll
+    for (int rt = 0; rt < kTbRT; ++rt) {
+      const int row = r0 + wv * 16 * kTbRT + kTbRT * (4 * g + v) + rt;
+      if (row >= M) continue;
+      float* crow = Cb + (uint64_t)row * ldc + n0 + 8 * i;
+      if (vec) {
+        reinterpret_cast<float4*>(crow)[0] =
+            make_float4(acc[rt][0][v], acc[rt][1][v], acc[rt][2][v], acc[rt][3][v]);
+        reinterpret_cast<float4*>(crow)[1] =
+            make_float4(acc[rt][4][v], acc[rt][5][v], acc[rt][6][v], acc[rt][7][v]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) crow[j] = acc[rt][j][v];
+      }
+    }
+  (void)N;
+}
+
+// C = sum over `splits` partial slabs [M x N] (ld N), as a fixed-shape tree:
+// thread s of a 16-thread group sums splits s, s+16, ... in order, then the
+// group combines its 16 sums pairwise in LDS (deterministic, every element
+// with 16-way parallel loads instead of one serial chain per element).
+__global__ __launch_bounds__(256) void k_sum_splits_tree(const float4* __restrict__ part,
+                                                         int splits, uint64_t stride4, int M,
+                                                         int N, float* __restrict__ C,
+                                                         uint64_t ldc) {
+  __shared__ float4 red[256];
+  const int s = threadIdx.x & 15;
+  const uint64_t e = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const uint64_t total = (uint64_t)M * N / 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < total) {
+    int z = s;
+    for (; z + 48 < splits; z += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[(uint64_t)(z + 16 * u) * stride4 + e];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; z < splits; z += 16) {
+      const float4 v = part[(uint64_t)z * stride4 + e];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int w = 8; w >= 1; w >>= 1) {
+    if (s < w) {
+      const float4 o = red[threadIdx.x + w];
+      float4& m = red[threadIdx.x];
+      m.x += o.x; m.y += o.y; m.z += o.z; m.w += o.w;
+    }
+    __syncthreads();
+  }
+  if (s == 0 && e < total) {
+    const uint64_t el = e * 4;
+    *reinterpret_cast<float4*>(C + (el / N) * ldc + (el % N)) = red[threadIdx.x];
+  }
+}
+
+static bool tn_big_ok(int M, int N, const float* B, uint64_t ldb, const GemmExtra& ex, bool bmask) {
+  if (M < 320 || N % 128 != 0 || ldb % 4 != 0 || (uintptr_t)B % 16 != 0) return false;
+  if (bmask && (ex.ldbx % 4 != 0 || (uintptr_t)ex.bx % 16 != 0)) return false;
+  return true;
+}
+
+template <bool BMASK>
+static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda,
+                         const float* B, uint64_t ldb, float* C, uint64_t ldc,
+                         const GemmExtra& ex) {
+  hipStream_t st = ctx->stream;
+  const int nrg = (M + kTbRows - 1) / kTbRows, ncb = N / 128;
+  int splits = std::max(1, std::min(256 / (nrg * ncb), (K + 4 * kTbKS - 1) / (4 * kTbKS)));
+  const int kchunk = ((K + splits - 1) / splits + kTbKS - 1) / kTbKS * kTbKS;
+  splits = (K + kchunk - 1) / kchunk;
+  const dim3 grid(nrg * ncb * splits);
+  const size_t lds = sizeof(TbSmem);
+  const bool a2 = M % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0;
+  const bool direct = splits == 1;
+  const uint64_t stride = (uint64_t)M * N;
+  float* out = C;
+  uint64_t ldo = ldc;
+  if (!direct) {
+    NTS_RET(ensure_scratch(ctx, stride * splits * sizeof(float) + 256));
+    out = (float*)ctx->scratch;
+    ldo = N;
+  }
+#define NTS_TB(AV)                                                                              \
+  do {                                                                                          \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_big<BMASK, AV>),   \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
+    hipLaunchKernelGGL((k_gemm_tn_big<BMASK, AV>), grid, dim3(kTbWaves * 64), lds, st, M, N, K, \
+                       A, lda, B, ldb, out, ldo, kchunk, direct ? (uint64_t)0 : stride, nrg,    \
+                       ncb, ex);                                                                \
+  } while (0)
+  if (a2) NTS_TB(2); else NTS_TB(1);
+#undef NTS_TB
+  NTS_LAUNCH_CHECK();
+  if (direct) return NTS_OK;
+  if (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) {
+    const uint32_t g = ceil_div(stride / 4, 16);
+    hipLaunchKernelGGL(k_sum_splits_tree, dim3(g), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(out), splits, stride / 4, M, N, C, ldc);
+  } else {
+    const uint32_t g = std::max(1u, std::min(ceil_div(stride, 256), kMaxGrid));
+    hipLaunchKernelGGL(k_sum_splits<false>, dim3(g), dim3(256), 0, st, out, splits, stride, M, N,
+                       C, ldc);
+  }
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
 template <bool TRANS_A, bool EPI, bool BMASK>
 static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t lda,
                   const float* B, uint64_t ldb, float* C, uint64_t ldc, int splits, int kchunk,
@@ -673,6 +926,8 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
       const int ncol = wres_ncol(M, N, K);
       if (ncol) return launch_wres<EPI>(st, ncol, M, N, K, A, lda, B, ldb, C, ldc, ex);
     }
+    if (trans_a && !EPI && tn_big_ok(M, N, B, ldb, ex, BMASK))
+      return launch_tn_big<BMASK>(ctx, M, N, K, A, lda, B, ldb, C, ldc, ex);
   }
   const int tiles = (int)(ceil_div(M, kBM) * ceil_div(N, kBN));
   int splits = 1;
