@@ -48,11 +48,15 @@ def parse():
     p.add_argument("--batch", type=int, default=10000)
     p.add_argument("--fanout", default="25-10")
     p.add_argument("--hidden", type=int, default=128)
+    p.add_argument("--layers", default=None,
+                   help="layer widths a-b-...-c (default: F-hidden-classes of the shape)")
+    p.add_argument("--weight", default="sum", choices=["sum", "mean"],
+                   help="edge weights: GCN sum (default) or GraphSAGE mean")
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
-    p.add_argument("--no-early-agg", action="store_true",
-                   help="bottom aggregation on the training stream instead of behind the sampler")
+    p.add_argument("--early-agg", action="store_true",
+                   help="issue the bottom aggregation behind the sampler on the sampling stream")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
     p.add_argument("--no-fuse-act", action="store_true",
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
@@ -61,7 +65,7 @@ def parse():
     p.add_argument("--cpu-baseline-steps", type=int, default=10)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    p.add_argument("--epoch", action="store_true", help="also time one full epoch")
+    p.add_argument("--no-epoch", action="store_true", help="skip the timed full epoch")
     p.add_argument("--scale", type=float, default=1.0)
     return p.parse_args()
 
@@ -103,17 +107,19 @@ def main():
     comm = ndist.make_communicator(E, world, rank, local_rank)
 
     fan = [int(x) for x in args.fanout.split("-")]
-    layers = [F_dim, args.hidden, C]
+    layers = ([int(x) for x in args.layers.split("-")] if args.layers else [F_dim, args.hidden, C])
+    if layers[0] != F_dim or len(layers) != len(fan) + 1:
+        raise SystemExit(f"--layers must start at the feature width {F_dim} and have one more "
+                         f"entry than --fanout")
     cfg = host.gcn_config(layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4,
-                          drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX,
+                          drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX, weight=args.weight,
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
-                          fuse_linear=args.fuse_linear, early_aggregate=not args.no_early_agg,
+                          fuse_linear=args.fuse_linear, early_aggregate=args.early_agg,
                           sampler_priority=not args.no_priority,
                           fuse_activation=not args.no_fuse_act)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
-                    and args.no_early_agg
-                    and args.hidden <= 128)
+                    and not args.early_agg and layers[1] <= 128)
     agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
 
@@ -153,8 +159,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         elapsed, edges = float(mx[0]), float(t[1])
 
+    # sizes of the last timed batch (before the epoch run replaces them)
+    layer_sizes = [{"v": int(l["v_size"]), "src": int(l["src_size"]), "e": int(l["e_size"])}
+                   for l in drv.last_layers]
     epoch_s = None
-    if args.epoch:
+    if not args.no_epoch:
         drv.restart()
         barrier()
         te = time.perf_counter()
@@ -163,9 +172,12 @@ def main():
         barrier()
         epoch_s = time.perf_counter() - te
         drv.resolve_profile()
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([epoch_s], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            epoch_s = float(t[0])
 
-    layer_sizes = [{"v": int(l["v_size"]), "src": int(l["src_size"]), "e": int(l["e_size"])}
-                   for l in drv.last_layers]
     value = edges / elapsed
     agg_avg_ms = agg_ms / max(agg_calls, 1)
     achieved = (agg_bytes / max(agg_calls, 1)) / (agg_avg_ms * 1e-3) / 1e9 if agg_calls else None
@@ -186,18 +198,22 @@ def main():
         "dtype": "fp32",
         "data": "synthetic Chung-Lu power-law graph (seed 2024), N(0,1) fp32 features (seed 7), uniform labels",
         "config": {
-            "workload": (f"GCN_SAMPLE_ALLGPU-style 2-layer GCN {'-'.join(map(str, layers))}, fanout "
+            "workload": (f"{'GS' if args.weight == 'mean' else 'GCN'}_SAMPLE_ALLGPU-style "
+                         f"{len(layers) - 1}-layer {'GraphSAGE (mean)' if args.weight == 'mean' else 'GCN'} "
+                         f"{'-'.join(map(str, layers))}, fanout "
                          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic "
                          f"(V={V}, E={En}); GPU sampler (Philox"
                          f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation"
-                         f"{' (issued behind the sampler)' if not args.no_early_agg and not args.no_fused_gather else ''}"
+                         f"{' (issued behind the sampler)' if args.early_agg and not args.no_fused_gather else ''}"
                          f"{' + layer-1 GEMM' if fused_linear else ''} + "
                          f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"),
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}",
             "fanout": args.fanout,
             "epoch_time_s": epoch_s if epoch_s is not None else elapsed / args.steps * batches_per_epoch,
-            "epoch_time_kind": "measured" if epoch_s is not None else "ms_per_step x batches/epoch",
+            "epoch_time_kind": ("measured: one full epoch over this rank's training shard, "
+                                "after the timed steps" if epoch_s is not None
+                                else "ms_per_step x batches/epoch"),
             "batches_per_epoch_per_gpu": batches_per_epoch,
             "sampler_s_per_step": sample_s / args.steps,
             "layer_sizes_top_down": layer_sizes,
@@ -215,12 +231,22 @@ def main():
             "algorithmic_bytes_per_launch": agg_bytes / max(agg_calls, 1),
         },
     }
-    pmc = ROOT / "profiles" / "pmc_r01.json"
-    if pmc.exists() and args.shape == "reddit" and args.batch == 10000 and world == 1:
+    # HBM traffic of the dominant kernel from the newest committed PMC pass
+    # (profiles/pmc_<tag>.json, FETCH_SIZE x 2 + WRITE_SIZE per launch) — valid for
+    # the default workload only
+    pmcs = sorted((ROOT / "profiles").glob("pmc_*.json"))
+    default_shape = (args.shape == "reddit" and args.batch == 10000 and args.fanout == "25-10"
+                     and layers == [602, 128, 41] and world == 1)
+    if pmcs and default_shape:
         try:
-            info = json.loads(pmc.read_text())
-            if info.get("kernel", "").split("<")[0] == agg_kernel:
-                result["roofline"]["traffic"] = info.get("hbm_bytes_per_launch")
+            info = json.loads(pmcs[-1].read_text())
+            if info.get("kernel", "").split("<")[0].split("::")[-1] == agg_kernel:
+                tb = float(info["hbm_bytes_per_launch"])
+                result["roofline"]["traffic"] = tb
+                result["roofline"]["traffic_source"] = pmcs[-1].name
+                # actual HBM bytes moved per launch / this run's launch time
+                result["roofline"]["traffic_GBs"] = tb / (agg_avg_ms * 1e-3) / 1e9
+                result["roofline"]["traffic_frac"] = result["roofline"]["traffic_GBs"] / HBM_PEAK_GBS
         except Exception:
             pass
 
