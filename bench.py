@@ -151,6 +151,7 @@ def main():
     agg_bytes = float(drv.agg_bytes)
     agg_calls = int(drv.agg_calls)
     sample_s = float(drv.sample_time)
+    train_host_s = float(drv.train_time)
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed, edges], dtype=torch.float64, device=dev)
@@ -216,6 +217,7 @@ def main():
                                 else "ms_per_step x batches/epoch"),
             "batches_per_epoch_per_gpu": batches_per_epoch,
             "sampler_s_per_step": sample_s / args.steps,
+            "host_train_issue_s_per_step": train_host_s / args.steps,
             "layer_sizes_top_down": layer_sizes,
         },
         "roofline": {

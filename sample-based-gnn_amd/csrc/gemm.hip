@@ -11,10 +11,12 @@
 //   NN otherwise, and TN: k_gemm — block 64 rows x 128 cols, 4 waves of
 //       32 x 64 on v_mfma_f32_32x32x2_f32, A and B k-slices staged in LDS
 //       (double buffered, register prefetch two steps deep).
-//   TN: C = A^T B with the long reduction split over blocks; per-split
-//       partial tiles are summed in split order by a second kernel
+//   TN: C = A^T B with the long reduction split over blocks; the partial
+//       tiles are summed by a second kernel in a fixed tree order
 //       (deterministic, no atomics).
 #include "common.hpp"
+
+#include <type_traits>
 
 namespace nts_hip {
 
@@ -325,45 +327,6 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
       for (int q = 0; q < 4; ++q)
         if (r4 + q < M) Cb[(uint64_t)(r4 + q) * ldc + col] = o[q];
     }
-  }
-}
-
-// C = sum over splits of the partial slabs (in split order; loads run ahead of
-// the sequential adds).  VEC4: N % 4 == 0 and C 16-byte aligned rows.
-template <bool VEC4>
-__global__ void k_sum_splits(const float* __restrict__ part, int splits, uint64_t stride, int M,
-                             int N, float* __restrict__ C, uint64_t ldc) {
-  if (VEC4) {
-    const uint64_t total = (uint64_t)M * N / 4;
-    const float4* p4 = reinterpret_cast<const float4*>(part);
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      int z = 0;
-      for (; z + 4 <= splits; z += 4) {
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = p4[(uint64_t)(z + u) * (stride / 4) + i];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
-        }
-      }
-      for (; z < splits; ++z) {
-        const float4 v = p4[(uint64_t)z * (stride / 4) + i];
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      const uint64_t e = i * 4;
-      *reinterpret_cast<float4*>(C + (e / N) * ldc + (e % N)) = s;
-    }
-    return;
-  }
-  const uint64_t total = (uint64_t)M * N;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += part[(uint64_t)z * stride + i];
-    C[(i / N) * ldc + (i % N)] = s;
   }
 }
 
@@ -746,46 +709,66 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
 // thread s of a 16-thread group sums splits s, s+16, ... in order, then the
 // group combines its 16 sums pairwise in LDS (deterministic, every element
 // with 16-way parallel loads instead of one serial chain per element).
-__global__ __launch_bounds__(256) void k_sum_splits_tree(const float4* __restrict__ part,
-                                                         int splits, uint64_t stride4, int M,
+// VEC = 4: float4 elements (N % 4 == 0, C 16-byte aligned rows), else floats.
+template <int VEC>
+__global__ __launch_bounds__(256) void k_sum_splits_tree(const float* __restrict__ part,
+                                                         int splits, uint64_t stride, int M,
                                                          int N, float* __restrict__ C,
                                                          uint64_t ldc) {
-  __shared__ float4 red[256];
+  using T = typename std::conditional<VEC == 4, float4, float>::type;
+  __shared__ T red[256];
   const int s = threadIdx.x & 15;
   const uint64_t e = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-  const uint64_t total = (uint64_t)M * N / 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const uint64_t total = (uint64_t)M * N / VEC;
+  const T* p = reinterpret_cast<const T*>(part);
+  const uint64_t st = stride / VEC;
+  auto add = [](T& a, const T& b) {
+    if constexpr (VEC == 4) {
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    } else {
+      a += b;
+    }
+  };
+  T acc;
+  if constexpr (VEC == 4) acc = make_float4(0.f, 0.f, 0.f, 0.f); else acc = 0.f;
   if (e < total) {
     int z = s;
     for (; z + 48 < splits; z += 64) {
-      float4 v[4];
+      T v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = part[(uint64_t)(z + 16 * u) * stride4 + e];
+      for (int u = 0; u < 4; ++u) v[u] = p[(uint64_t)(z + 16 * u) * st + e];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
-      }
+      for (int u = 0; u < 4; ++u) add(acc, v[u]);
     }
-    for (; z < splits; z += 16) {
-      const float4 v = part[(uint64_t)z * stride4 + e];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-    }
+    for (; z < splits; z += 16) add(acc, p[(uint64_t)z * st + e]);
   }
   red[threadIdx.x] = acc;
   __syncthreads();
 #pragma unroll
   for (int w = 8; w >= 1; w >>= 1) {
-    if (s < w) {
-      const float4 o = red[threadIdx.x + w];
-      float4& m = red[threadIdx.x];
-      m.x += o.x; m.y += o.y; m.z += o.z; m.w += o.w;
-    }
+    if (s < w) add(red[threadIdx.x], red[threadIdx.x + w]);
     __syncthreads();
   }
   if (s == 0 && e < total) {
-    const uint64_t el = e * 4;
-    *reinterpret_cast<float4*>(C + (el / N) * ldc + (el % N)) = red[threadIdx.x];
+    const uint64_t el = e * VEC;
+    *reinterpret_cast<T*>(C + (el / N) * ldc + (el % N)) = red[threadIdx.x];
   }
+}
+
+// Sum `splits` partial slabs (stride floats apart, ld N) into C.
+static int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
+                      float* C, uint64_t ldc) {
+  const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+  const uint64_t elems = stride / (v4 ? 4 : 1);
+  const uint32_t g = std::max(1u, ceil_div(elems, 16));
+  if (v4)
+    hipLaunchKernelGGL(k_sum_splits_tree<4>, dim3(g), dim3(256), 0, st, part, splits, stride, M, N,
+                       C, ldc);
+  else
+    hipLaunchKernelGGL(k_sum_splits_tree<1>, dim3(g), dim3(256), 0, st, part, splits, stride, M, N,
+                       C, ldc);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
 }
 
 static bool tn_big_ok(int M, int N, const float* B, uint64_t ldb, const GemmExtra& ex, bool bmask) {
@@ -827,17 +810,7 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
 #undef NTS_TB
   NTS_LAUNCH_CHECK();
   if (direct) return NTS_OK;
-  if (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) {
-    const uint32_t g = ceil_div(stride / 4, 16);
-    hipLaunchKernelGGL(k_sum_splits_tree, dim3(g), dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(out), splits, stride / 4, M, N, C, ldc);
-  } else {
-    const uint32_t g = std::max(1u, std::min(ceil_div(stride, 256), kMaxGrid));
-    hipLaunchKernelGGL(k_sum_splits<false>, dim3(g), dim3(256), 0, st, out, splits, stride, M, N,
-                       C, ldc);
-  }
-  NTS_LAUNCH_CHECK();
-  return NTS_OK;
+  return sum_splits(st, out, splits, stride, M, N, C, ldc);
 }
 
 template <bool TRANS_A, bool EPI, bool BMASK>
@@ -863,9 +836,6 @@ static int launch(hipStream_t st, int M, int N, int K, const float* A, uint64_t 
   return NTS_OK;
 }
 
-// One GEMM: split the reduction when the output grid alone cannot fill the
-// chip (partials summed in split order by k_sum_splits: deterministic).  EPI
-// needs the complete sum, so it never splits.
 // Column slice width of k_gemm_wres for this shape (0: not applicable).
 static int wres_ncol(int M, int N, int K) {
   if (M < 2048 || K < 1) return 0;
@@ -913,6 +883,9 @@ static bool force_tiled() {
   return f;
 }
 
+// One GEMM: split the reduction when the output grid alone cannot fill the
+// chip (partials summed in a fixed order by sum_splits: deterministic).  EPI
+// needs the complete sum, so it never splits.
 template <bool EPI, bool BMASK>
 static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float* A, uint64_t lda,
                 const float* B, uint64_t ldb, float* C, uint64_t ldc, const GemmExtra& ex) {
@@ -946,16 +919,7 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
       trans_a ? launch<true, EPI, BMASK>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride, ex)
               : launch<false, EPI, BMASK>(st, M, N, K, A, lda, B, ldb, part, N, splits, kchunk, stride, ex);
   if (rc != NTS_OK) return rc;
-  const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
-  const uint32_t g = std::max(1u, std::min(ceil_div(v4 ? stride / 4 : stride, 256), kMaxGrid));
-  if (v4)
-    hipLaunchKernelGGL(k_sum_splits<true>, dim3(g), dim3(256), 0, st, part, splits, stride, M, N,
-                       C, ldc);
-  else
-    hipLaunchKernelGGL(k_sum_splits<false>, dim3(g), dim3(256), 0, st, part, splits, stride, M,
-                       N, C, ldc);
-  NTS_LAUNCH_CHECK();
-  return NTS_OK;
+  return sum_splits(st, part, splits, stride, M, N, C, ldc);
 }
 
 }  // namespace nts_hip

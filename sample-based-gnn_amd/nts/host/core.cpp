@@ -621,8 +621,10 @@ void Parameter::next() {
   ++curr_epoch;
 }
 
+// The gradient is dropped rather than zero-filled: the next backward then
+// assigns W.grad instead of accumulating into zeros (no fill + add kernels).
 void Parameter::zero_grad() {
-  if (W.grad().defined()) W.mutable_grad().zero_();
+  if (W.grad().defined()) W.mutable_grad() = NtsVar();
 }
 
 // ---------------------------------------------------------------------------
