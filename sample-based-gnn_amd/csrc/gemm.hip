@@ -606,9 +606,14 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
     for (int p = 0; p < NAL; ++p) {
       const int e = tid + kTbWaves * 64 * p;
       const int kk = min(kb + e / NAV, K - 1);
-      const int c = min(r0 + AVEC * (e % NAV), M - AVEC);
+      // AVEC = 4 reads may run into the row padding (lda >= M rounded up to
+      // 4); columns >= M are zeroed when staged
+      const int c = min(r0 + AVEC * (e % NAV), AVEC == 4 ? (int)lda - 4 : M - AVEC);
       const float* src = A + (uint64_t)kk * lda + c;
-      if (AVEC == 2) {
+      if (AVEC == 4) {
+        const float4 x = *reinterpret_cast<const float4*>(src);
+        av[4 * p] = x.x; av[4 * p + 1] = x.y; av[4 * p + 2] = x.z; av[4 * p + 3] = x.w;
+      } else if (AVEC == 2) {
         const float2 x = *reinterpret_cast<const float2*>(src);
         av[2 * p] = x.x; av[2 * p + 1] = x.y;
       } else {
@@ -788,6 +793,7 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
   splits = (K + kchunk - 1) / kchunk;
   const dim3 grid(nrg * ncb * splits);
   const size_t lds = sizeof(TbSmem);
+  const bool a4 = lda % 4 == 0 && lda >= (uint64_t)(M + 3) / 4 * 4 && (uintptr_t)A % 16 == 0;
   const bool a2 = M % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0;
   const bool direct = splits == 1;
   const uint64_t stride = (uint64_t)M * N;
@@ -806,7 +812,7 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
                        A, lda, B, ldb, out, ldo, kchunk, direct ? (uint64_t)0 : stride, nrg,    \
                        ncb, ex);                                                                \
   } while (0)
-  if (a2) NTS_TB(2); else NTS_TB(1);
+  if (a4) NTS_TB(4); else if (a2) NTS_TB(2); else NTS_TB(1);
 #undef NTS_TB
   NTS_LAUNCH_CHECK();
   if (direct) return NTS_OK;
@@ -852,9 +858,11 @@ static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const floa
   const int per = std::max(1, 32 / ncb);  // blocks per (XCD, column block)
   const int grid = 8 * ncb * per;
   const size_t lds = (size_t)nkb * 32 * ncol * sizeof(float);
+  // vector width of the A row loads of the full k-blocks (the partial last
+  // block is read element-wise): only the row pitch and base alignment matter
   int avec = 1;
-  if (K % 4 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
-  else if (K % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
+  if (lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
+  else if (lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
   const int vs = (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) ? 1 : 0;
 #define NTS_WRES(NC, AV)                                                                        \
   do {                                                                                          \

@@ -324,12 +324,12 @@ NtsVar SingleGPUAllSampleGraphOp::forward(NtsVar& f_input) {
   TORCH_CHECK(gather_from_table || f_input.size(0) >= (int64_t)sg->src_size,
               "graph op input has fewer rows than src_size");
   const int64_t F = f_input.size(1);
-  NtsVar f_output = torch::empty({(int64_t)sg->v_size, F}, f32_opts(cuda_stream->device()));
+  NtsVar f_output = row_padded_empty((int64_t)sg->v_size, F, cuda_stream->device());
   hip_check(nts_hip_spmm_csc_fwd(cuda_stream->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
                                  nullptr, sg->v_size, f_input.data_ptr<float>(),
                                  (uint64_t)f_input.stride(0),
                                  gather_from_table ? sg->dev_src() : nullptr, (uint32_t)F,
-                                 f_output.data_ptr<float>(), (uint64_t)F),
+                                 f_output.data_ptr<float>(), (uint64_t)f_output.stride(0)),
             "nts_hip_spmm_csc_fwd");
   if (output_requires_grad) f_output.set_requires_grad(true);
   return f_output;
@@ -450,6 +450,20 @@ void NtsContext::reset() {
 }  // namespace ctx
 
 // ---------------------------------------------------------------------------
+// Row-major with unit column stride (rows may be padded); copies otherwise.
+NtsVar row_major(const NtsVar& x) {
+  return (x.dim() == 2 && x.stride(1) == 1 && x.stride(0) >= x.size(1)) ? x : x.contiguous();
+}
+
+// [rows, F] fp32 whose rows start on 128-byte boundaries for wide F (the
+// bottom aggregation output: aligned row writes, 16-byte A loads in the
+// GEMMs that consume it).
+NtsVar row_padded_empty(int64_t rows, int64_t F, int device) {
+  const int64_t ld = F >= 256 ? (F + 31) / 32 * 32 : F;
+  if (ld == F) return torch::empty({rows, F}, f32_opts(device));
+  return torch::empty_strided({rows, F}, {ld, 1}, f32_opts(device));
+}
+
 namespace {
 using torch::autograd::AutogradContext;
 using torch::autograd::variable_list;
@@ -457,13 +471,13 @@ using torch::autograd::variable_list;
 struct HipLinearFn : public torch::autograd::Function<HipLinearFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar x, NtsVar W, int64_t cs_ptr) {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
-    NtsVar xc = x.contiguous(), Wc = W.contiguous();
+    NtsVar xc = row_major(x), Wc = W.contiguous();
     const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
     TORCH_CHECK(Wc.size(0) == K, "hip_linear: shape mismatch");
     NtsVar Z = torch::empty({M, N}, xc.options());
     hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)M, (int)N, (int)K, xc.data_ptr<float>(),
-                               (uint64_t)K, Wc.data_ptr<float>(), (uint64_t)N, Z.data_ptr<float>(),
-                               (uint64_t)N),
+                               (uint64_t)xc.stride(0), Wc.data_ptr<float>(), (uint64_t)N,
+                               Z.data_ptr<float>(), (uint64_t)N),
               "nts_hip_gemm_f32(nn)");
     ctx->save_for_backward({xc, Wc});
     ctx->saved_data["cs"] = cs_ptr;
@@ -479,7 +493,7 @@ struct HipLinearFn : public torch::autograd::Function<HipLinearFn> {
     if (ctx->needs_input_grad(1)) {
       dW = torch::empty({K, N}, W.options());
       hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)K, (int)N, (int)M, x.data_ptr<float>(),
-                                 (uint64_t)K, g.data_ptr<float>(), (uint64_t)N,
+                                 (uint64_t)x.stride(0), g.data_ptr<float>(), (uint64_t)N,
                                  dW.data_ptr<float>(), (uint64_t)N),
                 "nts_hip_gemm_f32(tn)");
     }
@@ -493,12 +507,12 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar x, NtsVar W, double p, int64_t seed,
                         int64_t offset, int64_t cs_ptr) {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
-    NtsVar xc = x.contiguous(), Wc = W.contiguous();
+    NtsVar xc = row_major(x), Wc = W.contiguous();
     const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
     TORCH_CHECK(Wc.size(0) == K, "hip_linear_act: shape mismatch");
     NtsVar X = torch::empty({M, N}, xc.options());
     hip_check(nts_hip_gemm_relu_dropout_f32(cs->ctx(), (int)M, (int)N, (int)K,
-                                            xc.data_ptr<float>(), (uint64_t)K,
+                                            xc.data_ptr<float>(), (uint64_t)xc.stride(0),
                                             Wc.data_ptr<float>(), (uint64_t)N, X.data_ptr<float>(),
                                             (uint64_t)N, (float)p, (uint64_t)seed,
                                             (uint64_t)offset),
@@ -519,7 +533,7 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
     if (ctx->needs_input_grad(1)) {
       dW = torch::empty({K, N}, W.options());
       hip_check(nts_hip_gemm_tn_masked_f32(cs->ctx(), (int)K, (int)N, (int)M, x.data_ptr<float>(),
-                                           (uint64_t)K, g.data_ptr<float>(), (uint64_t)N,
+                                           (uint64_t)x.stride(0), g.data_ptr<float>(), (uint64_t)N,
                                            X.data_ptr<float>(), (uint64_t)N, scale,
                                            dW.data_ptr<float>(), (uint64_t)N),
                 "nts_hip_gemm_tn_masked_f32");

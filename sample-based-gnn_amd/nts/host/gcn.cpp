@@ -65,8 +65,8 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     TORCH_CHECK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming) == hipSuccess,
                 "hipEventCreate");
     if (early_)
-      pre_y_[i] = torch::empty({(int64_t)sampler->ssgs[i]->sampled_sgs[L - 1]->v_cap, F.size(1)},
-                               F.options());
+      pre_y_[i] = row_padded_empty((int64_t)sampler->ssgs[i]->sampled_sgs[L - 1]->v_cap,
+                                   F.size(1), graph->device);
   }
   init_nn();
 }

@@ -300,6 +300,10 @@ class NtsContext {
 // x.matmul(W) on the MFMA fp32 kernels (nts_hip_gemm_f32) with its own
 // backward: dW = x^T dZ (split-reduction, deterministic), dx = dZ W^T.
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
+// row-major fp32 views the HIP GEMMs take without a copy (unit column stride)
+NtsVar row_major(const NtsVar& x);
+// [rows, F] with 128-byte aligned rows when F >= 256 (padded leading dimension)
+NtsVar row_padded_empty(int64_t rows, int64_t F, int device);
 // dropout(relu(x W), p) in one MFMA GEMM (activation in the epilogue, Philox
 // mask of (seed, offset)); autograd: dW = x^T (dX ⊙ [X > 0] / (1-p)) fused.
 NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,

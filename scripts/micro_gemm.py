@@ -24,3 +24,7 @@ for (M, N, K) in [(136000, 128, 602), (225000, 128, 602), (10000, 41, 128), (136
     us2 = t(lambda: ctx.gemm(A, G, D, trans_a=True)); ut2 = t(lambda: torch.matmul(A.t(), G, out=D))
     print(f"M={M} N={N} K={K}: NN mfma {us:7.1f}us {fl/us/1e6:6.1f}TF  torch {ut:7.1f}us {fl/ut/1e6:6.1f}TF | "
           f"TN mfma {us2:7.1f}us {fl/us2/1e6:6.1f}TF torch {ut2:7.1f}us {fl/ut2/1e6:6.1f}TF", flush=True)
+    if K % 32:  # 128-byte aligned row pitch (the bottom aggregation output's layout)
+        Ap = torch.randn(M, (K + 31) // 32 * 32, device="cuda")[:, :K]
+        us3 = t(lambda: ctx.gemm(Ap, B, C)); us4 = t(lambda: ctx.gemm(Ap, G, D, trans_a=True))
+        print(f"   padded pitch {Ap.stride(0)}: NN {us3:7.1f}us {fl/us3/1e6:6.1f}TF | TN {us4:7.1f}us {fl/us4/1e6:6.1f}TF", flush=True)

@@ -471,3 +471,27 @@ def test_gemm_tn_masked(hip, M, N, K):
     torch.cuda.synchronize()
     tol = 2e-6 * K ** 0.5 + 1e-6
     torch.testing.assert_close(C.double(), ref, rtol=tol, atol=tol * 8)
+
+
+@pytest.mark.parametrize("M,N,K,trans_a", [(136000, 128, 602, False), (4099, 256, 301, False),
+                                           (602, 128, 20000, True), (333, 128, 777, True)])
+def test_gemm_padded_pitch(hip, M, N, K, trans_a):
+    """Row-padded operands (the bottom aggregation output has 128-byte aligned
+    rows): the 16-byte A-load paths read the pitch, never the padding's values."""
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    rows, cols = (K, M) if trans_a else (M, K)
+    ld = (cols + 31) // 32 * 32 + 32
+    big = torch.full((rows, ld), float("nan"), device=DEV)
+    A = big[:, :cols]
+    A.copy_(torch.randn(rows, cols, device=DEV, generator=g))
+    B = torch.randn(K, N, device=DEV, generator=g)
+    C = torch.full((M, N), float("nan"), device=DEV)
+    hip.gemm(A, B, C, trans_a=trans_a)
+    ref = (A.double().t() if trans_a else A.double()) @ B.double()
+    torch.cuda.synchronize()
+    tol = 2e-6 * K ** 0.5 + 1e-6
+    torch.testing.assert_close(C.double(), ref, rtol=tol, atol=tol * 4)
+    C2 = torch.empty_like(C)
+    hip.gemm(A.contiguous(), B, C2, trans_a=trans_a)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(C2, C, rtol=tol, atol=tol * 4)
