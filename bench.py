@@ -60,6 +60,10 @@ def parse():
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
     p.add_argument("--no-fuse-act", action="store_true",
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
+    p.add_argument("--sampler-cus", type=int, default=0,
+                   help="CUs reserved for the pipelined sampler stream (0: no partition)")
+    p.add_argument("--no-fuse-loss", action="store_true",
+                   help="output layer + loss as libtorch ops instead of the fused kernels")
     p.add_argument("--fuse-linear", action="store_true",
                    help="bottom layer: aggregation and first GEMM in one kernel")
     p.add_argument("--cpu-baseline-steps", type=int, default=10)
@@ -117,7 +121,8 @@ def main():
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
                           fuse_linear=args.fuse_linear, early_aggregate=args.early_agg,
                           sampler_priority=not args.no_priority,
-                          fuse_activation=not args.no_fuse_act)
+                          fuse_activation=not args.no_fuse_act,
+                          fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and not args.early_agg and layers[1] <= 128)
     agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")

@@ -238,6 +238,23 @@ int nts_hip_gemm_tn_masked_f32(nts_hip_ctx *ctx, int M, int N, int K, const floa
                                uint64_t lda, const float *B, uint64_t ldb, const float *X,
                                uint64_t ldx, float scale, float *C, uint64_t ldc);
 
+/* ---- output layer + loss (fused) ------------------------------------------ */
+/* Training forward of the last layer and the loss, in the reference's
+ * arithmetic: logits = Y W, log_softmax (vertexForward,
+ * toolkits/GCN_SAMPLE_ALLGPU.hpp:247-252), log_softmax again + mean
+ * nll_loss (Loss, :214-222).  Y [n x K] (ld ldy), W [K x C] row-major,
+ * labels int64 [n] in [0, C), C <= 64.  Writes the scalar loss (device).
+ * Replaces the libtorch matmul/log_softmax/nll_loss kernels of those lines. */
+int nts_hip_linear_xent_fwd(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int n, int K,
+                            const float *W, int C, const int64_t *labels, float *loss);
+/* Its backward for an upstream gradient *grad_loss (device scalar):
+ * dY [n x K] (ld K) and dW [K x C] (row-major), i.e. what libtorch's
+ * autograd produces through nll_loss, both log_softmaxes and the matmul.
+ * Deterministic (fixed-order reductions). */
+int nts_hip_linear_xent_bwd(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int n, int K,
+                            const float *W, int C, const int64_t *labels,
+                            const float *grad_loss, float *dY, float *dW);
+
 /* ---- optimiser ---------------------------------------------------------- */
 /* Fused Adam step on one parameter (n elements), element-wise identical to
  *  bias_correction != 0: Parameter::learnC2C_with_decay_Adam (core/NtsScheduler.hpp:863-880)

@@ -117,4 +117,9 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap,
                      uint32_t bits, void* tmp, hipStream_t stream);
 size_t radix_tmp_bytes(uint64_t n_cap);
+
+// C[M x N] = sum of `splits` partial slabs [M x N] (ld N, `stride` floats
+// apart) in a fixed order (deterministic; gemm.hip).
+int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
+               float* C, uint64_t ldc);
 }  // namespace nts_hip

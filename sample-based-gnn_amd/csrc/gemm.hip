@@ -761,7 +761,7 @@ __global__ __launch_bounds__(256) void k_sum_splits_tree(const float* __restrict
 }
 
 // Sum `splits` partial slabs (stride floats apart, ld N) into C.
-static int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
+int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
                       float* C, uint64_t ldc) {
   const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
   const uint64_t elems = stride / (v4 ? 4 : 1);

@@ -64,8 +64,24 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T* __restric
   if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
-// Scan one tile with a starting offset; writes out[i] for i <= n inside the tile.
+// Sum of partials[0 .. count) by the whole block (fixed order per thread,
+// fixed tree across threads: the same value in every block that asks).
 template <typename T>
+__device__ __forceinline__ T block_prefix_of(const T* partials, uint32_t count, T* wsum) {
+  T s = 0;
+  for (uint32_t i = threadIdx.x; i < count; i += kScanThreads) s += partials[i];
+  T tot;
+  (void)block_excl_scan(s, wsum, &tot);
+  __syncthreads();
+  return tot;
+}
+
+// Scan one tile with a starting offset; writes out[i] for i <= n inside the tile.
+// DIRECT: the offset is the sum of partials[0 .. blockIdx.x) (tile totals),
+// computed here — no separate scan of the partials (and no single-workgroup
+// kernel, which stalls for tens of microseconds behind a concurrent stream's
+// large kernels).  Otherwise partials[blockIdx.x] is already the offset.
+template <typename T, bool DIRECT>
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
                                                            const uint32_t* n_dev,
                                                            uint64_t n_cap,
@@ -76,6 +92,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
   __shared__ T tile[kScanTile + kScanTile / 16];
   __shared__ T wsum[kScanThreads / kWave];
   const int t = threadIdx.x;
+  T start = 0;
+  if (DIRECT) start = block_prefix_of(partials, blockIdx.x, wsum);
+  else if (partials) start = partials[blockIdx.x];
   // striped, coalesced load -> padded LDS
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
@@ -92,7 +111,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
     s += v[k];
   }
   T tot;
-  T run = block_excl_scan(s, wsum, &tot) + (partials ? partials[blockIdx.x] : T(0));
+  T run = block_excl_scan(s, wsum, &tot) + start;
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
@@ -115,13 +134,17 @@ size_t scan_tmp_elems(uint64_t n_cap) {
   return (nb + 1 + 63) / 64 * 64 + scan_tmp_elems<T>(nb);
 }
 
+// Tile counts up to which every block sums the preceding tile totals itself
+// (reduce + down: two kernels); beyond, the totals are scanned recursively.
+constexpr uint64_t kScanDirectTiles = 1024;
+
 template <typename T>
 int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T* tmp,
                    hipStream_t stream) {
   uint64_t nb = n_cap / kScanTile + 1;
   if (nb == 1) {
-    hipLaunchKernelGGL(k_scan_down<T>, dim3(1), dim3(kScanThreads), 0, stream, in, out, n_dev,
-                       n_cap, (const T*)nullptr);
+    hipLaunchKernelGGL((k_scan_down<T, false>), dim3(1), dim3(kScanThreads), 0, stream, in, out,
+                       n_dev, n_cap, (const T*)nullptr);
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
@@ -130,9 +153,15 @@ int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T
   hipLaunchKernelGGL(k_scan_reduce<T>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, in,
                      n_dev, n_cap, partials);
   NTS_LAUNCH_CHECK();
+  if (nb <= kScanDirectTiles) {
+    hipLaunchKernelGGL((k_scan_down<T, true>), dim3((uint32_t)nb), dim3(kScanThreads), 0, stream,
+                       in, out, n_dev, n_cap, (const T*)partials);
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   NTS_RET(scan_exclusive<T>(partials, partials, nullptr, nb, rest, stream));
-  hipLaunchKernelGGL(k_scan_down<T>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, in, out,
-                     n_dev, n_cap, (const T*)partials);
+  hipLaunchKernelGGL((k_scan_down<T, false>), dim3((uint32_t)nb), dim3(kScanThreads), 0, stream,
+                     in, out, n_dev, n_cap, (const T*)partials);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }

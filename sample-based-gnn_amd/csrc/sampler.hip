@@ -322,6 +322,7 @@ __global__ __launch_bounds__(kWave) void k_select_mt(SelectArgs a, uint32_t* mt_
 // ---- frontier compaction --------------------------------------------------
 constexpr int kMarkThreads = 256;
 constexpr int kMarkTile = kMarkThreads * 16;  // 4096 vertices per block
+constexpr uint32_t kMarkDirectTiles = 2048;     // k_mark_write sums the tile counts itself
 
 __device__ __forceinline__ uint32_t count16(uint4 m) {
   // marks are 0/1 bytes -> popcount of each word counts set bytes
@@ -346,28 +347,62 @@ __global__ __launch_bounds__(kMarkThreads) void k_mark_count(const uint8_t* __re
   }
 }
 
+// Also clears the byte map it consumed, so the next layer starts from zeros
+// without a memset (the map is zeroed once when allocated).
+// DIRECT: blk holds the per-tile counts and each block sums the ones before
+// its tile (and block 0 all of them, for src_size) — no scan kernel between
+// k_mark_count and this one; otherwise blk is the scanned offsets [nblk + 1].
+template <bool DIRECT>
 __global__ __launch_bounds__(kMarkThreads) void k_mark_write(
-    const uint8_t* __restrict__ marks, const uint32_t* __restrict__ blk_off, uint32_t nblk,
+    uint8_t* __restrict__ marks, const uint32_t* __restrict__ blk, uint32_t nblk,
     uint64_t n_vertices, uint32_t s_cap, uint32_t* __restrict__ source,
     uint32_t* __restrict__ src_index, uint32_t* sizes) {
   const uint64_t tid = (uint64_t)blockIdx.x * kMarkThreads + threadIdx.x;
-  const uint4 m = reinterpret_cast<const uint4*>(marks)[tid];
-  const uint32_t c = count16(m);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ uint32_t ws[kMarkThreads / kWave];
+  __shared__ uint32_t bo[2];
+  if (DIRECT) {
+    // fixed-order sums: tiles before this one, and (block 0) all tiles
+    uint32_t a = 0, b = 0;
+    for (uint32_t i = threadIdx.x; i < nblk; i += kMarkThreads) {
+      const uint32_t v = blk[i];
+      a += i < blockIdx.x ? v : 0u;
+      b += v;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o, kWave);
+      b += __shfl_down(b, o, kWave);
+    }
+    __shared__ uint32_t wa[kMarkThreads / kWave], wb[kMarkThreads / kWave];
+    if (lane == 0) { wa[w] = a; wb[w] = b; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t sa = 0, sb = 0;
+      for (int i = 0; i < kMarkThreads / kWave; ++i) { sa += wa[i]; sb += wb[i]; }
+      bo[0] = sa;
+      bo[1] = sb;
+    }
+  } else if (threadIdx.x == 0) {
+    bo[0] = blk[blockIdx.x];
+    bo[1] = blk[nblk];
+  }
+  const uint4 m = reinterpret_cast<const uint4*>(marks)[tid];
+  if (m.x | m.y | m.z | m.w) reinterpret_cast<uint4*>(marks)[tid] = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t c = count16(m);
   uint32_t inc = c;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
     uint32_t y = __shfl_up(inc, o, kWave);
     if (lane >= o) inc += y;
   }
-  __shared__ uint32_t ws[kMarkThreads / kWave];
   if (lane == 63) ws[w] = inc;
   __syncthreads();
-  uint32_t off = blk_off[blockIdx.x];
+  uint32_t off = bo[0];
   for (int i = 0; i < w; ++i) off += ws[i];
   uint32_t pos = off + inc - c;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    uint32_t s = blk_off[nblk];
+    uint32_t s = bo[1];
     sizes[2] = min(s, s_cap);
     if (s > s_cap) atomicOr(&sizes[3], 2u);
   }
@@ -501,10 +536,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                      o->sizes);
   NTS_LAUNCH_CHECK();
 
-  // 2) selection (marks the frontier)
-  // clear the whole scanned range (V rounded up to the 4096-vertex tile): the
-  // arena may be larger than this graph and hold marks of a previous one
-  NTS_HIP_TRY(hipMemsetAsync(ctx->marks, 0, (size_t)nblk_marks * kMarkTile, st));
+  // 2) selection (marks the frontier; the byte map is all zeros here: it is
+  // zeroed when allocated and k_mark_write clears what each layer set)
   SelectArgs a;
   a.goff = g->column_offset;
   a.grows = g->row_indices;
@@ -532,9 +565,16 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   hipLaunchKernelGGL(k_mark_count, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
                      t_blk);
   NTS_LAUNCH_CHECK();
-  NTS_RET(scan_exclusive<uint32_t>(t_blk, t_blk, nullptr, nblk_marks, t_scan_blk, st));
-  hipLaunchKernelGGL(k_mark_write, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
-                     t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index, o->sizes);
+  if (nblk_marks <= kMarkDirectTiles) {  // up to 8M vertices: no scan kernel
+    hipLaunchKernelGGL(k_mark_write<true>, dim3(nblk_marks), dim3(kMarkThreads), 0, st,
+                       ctx->marks, t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index,
+                       o->sizes);
+  } else {
+    NTS_RET(scan_exclusive<uint32_t>(t_blk, t_blk, nullptr, nblk_marks, t_scan_blk, st));
+    hipLaunchKernelGGL(k_mark_write<false>, dim3(nblk_marks), dim3(kMarkThreads), 0, st,
+                       ctx->marks, t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index,
+                       o->sizes);
+  }
   NTS_LAUNCH_CHECK();
 
   // 4) relabel to local ids + forward weights

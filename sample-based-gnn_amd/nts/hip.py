@@ -137,6 +137,17 @@ class HipContext:
                                                   G.stride(0), ptr(X), X.stride(0), float(scale),
                                                   ptr(C), C.stride(0)))
 
+    def linear_xent_fwd(self, Y, W, labels, loss):
+        """loss = nll_loss(log_softmax(log_softmax(Y @ W)), labels) (mean), fused."""
+        n, K = Y.shape
+        check(self.lib.nts_hip_linear_xent_fwd(self.h, ptr(Y), Y.stride(0), n, K, ptr(W), W.shape[1],
+                                               ptr(labels), ptr(loss)))
+
+    def linear_xent_bwd(self, Y, W, labels, grad_loss, dY, dW):
+        n, K = Y.shape
+        check(self.lib.nts_hip_linear_xent_bwd(self.h, ptr(Y), Y.stride(0), n, K, ptr(W), W.shape[1],
+                                               ptr(labels), ptr(grad_loss), ptr(dY), ptr(dW)))
+
     def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
         check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,
                                     beta1, beta2, eps, wd, beta1_t, beta2_t, int(bias_correction)))

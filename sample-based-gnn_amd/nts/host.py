@@ -36,7 +36,8 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                rng_mode=_abi.NTS_RNG_PHILOX, weight="sum", fused_gather=True,
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
                seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False,
-               early_aggregate=True, sampler_priority=True, fuse_activation=True):
+               early_aggregate=True, sampler_priority=True, fuse_activation=True,
+               fuse_loss=True, sampler_cus=0):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -57,6 +58,8 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.early_aggregate = bool(early_aggregate)
     c.sampler_priority = bool(sampler_priority)
     c.fuse_activation = bool(fuse_activation)
+    c.fuse_loss = bool(fuse_loss)
+    c.sampler_cus = int(sampler_cus)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

@@ -23,6 +23,12 @@ static void hip_rt(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// NTS_HOST_PROFILE=1: host-side durations of the sampler issue/finish calls
+static bool host_profile() {
+  static const bool on = getenv("NTS_HOST_PROFILE") != nullptr;
+  return on;
+}
+
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -37,7 +43,40 @@ NtsStream::NtsStream(int device, void* stream, uint64_t seed, bool high_priority
   hip_check(nts_hip_ctx_create(&ctx_, device, (void*)torch_stream_.stream(), seed),
             "nts_hip_ctx_create");
 }
-NtsStream::~NtsStream() { nts_hip_ctx_destroy(ctx_); }
+static hipStream_t create_masked(int device, const std::vector<uint32_t>& mask) {
+  hip_rt(hipSetDevice(device), "hipSetDevice");
+  hipStream_t s = nullptr;
+  hip_rt(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()),
+         "hipExtStreamCreateWithCUMask");
+  return s;
+}
+NtsStream::NtsStream(int device, const std::vector<uint32_t>& cu_mask, uint64_t seed)
+    : device_(device),
+      torch_stream_(c10::hip::getStreamFromExternal(create_masked(device, cu_mask),
+                                                    (c10::DeviceIndex)device)) {
+  owned_ = torch_stream_.stream();
+  hip_check(nts_hip_ctx_create(&ctx_, device, (void*)owned_, seed), "nts_hip_ctx_create");
+}
+NtsStream::~NtsStream() {
+  nts_hip_ctx_destroy(ctx_);
+  if (owned_) (void)hipStreamDestroy(owned_);
+}
+
+std::vector<uint32_t> cu_mask_spread(int device, int n, bool complement) {
+  hipDeviceProp_t prop;
+  hip_rt(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  const int total = prop.multiProcessorCount;
+  TORCH_CHECK(n > 0 && n < total, "CU partition size must be in (0, ", total, ")");
+  const int step = total / n;
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  int taken = 0;
+  for (int i = 0; i < total; ++i) {
+    const bool in = (i % step == 0) && taken < n;
+    if (in) ++taken;
+    if (in != complement) mask[i / 32] |= 1u << (i % 32);
+  }
+  return mask;
+}
 void NtsStream::setNewStream(void* stream) {
   hip_check(nts_hip_ctx_set_stream(ctx_, stream), "setNewStream");
   torch_stream_ = c10::hip::getStreamFromExternal((hipStream_t)stream, (c10::DeviceIndex)device_);
@@ -117,7 +156,6 @@ sampCSC::sampCSC(int device, VertexId vc, VertexId ec, VertexId sc, bool csr, bo
   edge_dst = torch::empty({e1}, U);
   source = torch::empty({s1}, U);
   sizes = torch::zeros({4}, U);
-  dst_count = torch::zeros({1}, U);
   if (weights) edge_weight_forward = torch::empty({e1}, F);
   if (csr) {
     row_offset = torch::empty({(int64_t)sc + 1}, U);
@@ -181,6 +219,7 @@ FastSampler::FastSampler(std::shared_ptr<FullyRepGraph> g, const std::vector<Ver
                                        g->global_edges, csr_layers, weights));
   ssg = ssgs[0];
   set_sample_nids(index);
+  dev_iota_ = torch::arange((int64_t)batch_cap_ + 1, u32_opts(g->device));
 }
 
 FastSampler::~FastSampler() {
@@ -213,14 +252,22 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   ssg = ssgs[ssg_id];
   const VertexId actual = std::min<VertexId>((VertexId)batch_size, work_range[1] - work_offset);
   hipStream_t st = (hipStream_t)cs.stream();
+  // The slot's previous batch must be trained before it is overwritten.  With
+  // several slots (pipelined sampler on its own stream) wait for that on the
+  // host: ROCm blocks every kernel launch on a stream whose queue waits on an
+  // unfinished event of another stream (~60 us each here), which would stall
+  // the whole issue loop; the event is normally complete already.
+  if (ssgs.size() > 1) hip_rt(hipEventSynchronize(ssg->consumed), "hipEventSynchronize");
   hip_rt(hipStreamWaitEvent(st, ssg->consumed, 0), "hipStreamWaitEvent");
   const nts_graph_dev g = whole_graph->dev();
   const int wt = w == WeightType::Sum ? NTS_WEIGHT_SUM
                                       : (w == WeightType::Mean ? NTS_WEIGHT_MEAN : NTS_WEIGHT_NONE);
   const VertexId* dst = dptr<VertexId>(dev_nids_) + work_offset;
   sampCSC* s0 = ssg->sampled_sgs[0];
-  hip_rt(hipMemsetD32Async(dptr<uint32_t>(s0->dst_count), (int)actual, 1, st), "hipMemsetD32Async");
-  const VertexId* vsz = dptr<VertexId>(s0->dst_count);
+  // layer-0 v_size as a device scalar without a per-batch memset: entry
+  // `actual` of the device table 0..batch_cap
+  (void)s0;
+  const VertexId* vsz = dptr<VertexId>(dev_iota_) + actual;
   for (int l = 0; l < layer; ++l) {
     sampCSC* s = ssg->sampled_sgs[l];
     nts_sampcsc_dev o;
@@ -240,8 +287,10 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
     o.edge_weight_backward =
         (s->has_csr && wt != NTS_WEIGHT_NONE) ? dptr<float>(s->edge_weight_backward) : nullptr;
     o.sizes = dptr<uint32_t>(s->sizes);
+    const double tl = now_s();
     hip_check(nts_hip_sample_layer(cs.ctx(), &g, fanout[l], l, batch_seq, rng_mode, wt, &o),
               "nts_hip_sample_layer");
+    if (host_profile()) fprintf(stderr, "[host] sample_layer %d: %.1f us\n", l, (now_s() - tl) * 1e6);
     // the reference keeps the destination as a view of the previous source
     if (l == 0)
       s->destination = dev_nids_.narrow(0, work_offset, std::max<int64_t>(actual, 0));
@@ -257,6 +306,7 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
                           hipMemcpyDeviceToHost, st),
            "hipMemcpyAsync(sizes)");
   hip_rt(hipEventRecord(ssg->sampled, st), "hipEventRecord");
+  if (host_profile()) fprintf(stderr, "[host] issue total: %.1f us\n", (now_s() - t0) * 1e6);
   ssg->pending_batch = (int)actual;
   work_offset += actual;
   ++batch_seq;
@@ -268,6 +318,7 @@ SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
   ssg = ssgs[ssg_id];
   TORCH_CHECK(ssg->pending_batch > 0, "finish_gpu_sample without a pending issue");
   hip_rt(hipEventSynchronize(ssg->sampled), "hipEventSynchronize");
+  if (host_profile()) fprintf(stderr, "[host] finish wait: %.1f us\n", (now_s() - t0) * 1e6);
   ssg->pending_batch = 0;
   const int32_t* hs = ssg->host_sizes.data_ptr<int32_t>();
   for (int l = 0; l < layer; ++l) {
@@ -575,6 +626,40 @@ struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
     return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar()};
   }
 };
+// Output layer + loss in two fused kernels (nts_hip.h): the forward writes
+// the scalar loss, the backward dY and dW for the upstream gradient.
+struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar y, NtsVar W, NtsVar target, int64_t cs_ptr) {
+    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    NtsVar yc = row_major(y), Wc = W.contiguous(), tc = target.contiguous();
+    const int64_t n = yc.size(0), K = yc.size(1), C = Wc.size(1);
+    TORCH_CHECK(Wc.size(0) == K && tc.numel() == n && tc.scalar_type() == torch::kInt64,
+                "hip_linear_xent: shape mismatch");
+    NtsVar loss = torch::empty({}, yc.options());
+    hip_check(nts_hip_linear_xent_fwd(cs->ctx(), yc.data_ptr<float>(), (uint64_t)yc.stride(0),
+                                      (int)n, (int)K, Wc.data_ptr<float>(), (int)C,
+                                      tc.data_ptr<int64_t>(), loss.data_ptr<float>()),
+              "nts_hip_linear_xent_fwd");
+    ctx->save_for_backward({yc, Wc, tc});
+    ctx->saved_data["cs"] = cs_ptr;
+    return loss;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto saved = ctx->get_saved_variables();
+    NtsVar y = saved[0], W = saved[1], t = saved[2];
+    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    NtsVar g = grads[0].contiguous();
+    const int64_t n = y.size(0), K = y.size(1), C = W.size(1);
+    NtsVar dY = torch::empty({n, K}, y.options());
+    NtsVar dW = torch::empty({K, C}, W.options());
+    hip_check(nts_hip_linear_xent_bwd(cs->ctx(), y.data_ptr<float>(), (uint64_t)y.stride(0),
+                                      (int)n, (int)K, W.data_ptr<float>(), (int)C,
+                                      t.data_ptr<int64_t>(), g.data_ptr<float>(),
+                                      dY.data_ptr<float>(), dW.data_ptr<float>()),
+              "nts_hip_linear_xent_bwd");
+    return {ctx->needs_input_grad(0) ? dY : NtsVar(), dW, NtsVar(), NtsVar()};
+  }
+};
 }  // namespace
 
 NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
@@ -599,6 +684,17 @@ NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* 
 
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {
   return HipLinearFn::apply(x, W, reinterpret_cast<int64_t>(cs));
+}
+
+bool hip_linear_xent_supported(int64_t K, int64_t C) {
+  // mirrors the argument checks of nts_hip_linear_xent_fwd/bwd (C <= 64,
+  // K % 16 == 0, W and 64 dZ rows in LDS)
+  const int64_t Cp = (C + 15) / 16 * 16;
+  return K >= 16 && K % 16 == 0 && C >= 1 && C <= 64 && (K * Cp + 64 * Cp) * 4 <= 160 * 1024;
+}
+
+NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs) {
+  return HipLinearXentFn::apply(y, W, target, reinterpret_cast<int64_t>(cs));
 }
 
 // ---------------------------------------------------------------------------

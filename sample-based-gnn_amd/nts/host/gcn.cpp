@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <chrono>
 #include <random>
+#include <cstdio>
+#include <cstdlib>
 
 namespace nts {
 
@@ -29,7 +31,12 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   TORCH_CHECK(cfg.fanout.size() == cfg.layer_size.size() - 1, "fanout per layer");
   TORCH_CHECK(F.is_cuda() && F.dtype() == torch::kFloat32 && F.size(1) == cfg.layer_size[0],
               "feature table must be fp32 [V, layer_size[0]] on the GPU");
-  cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+  if (cfg.pipeline && cfg.sampler_cus > 0)
+    cs = std::make_unique<NtsStream>(graph->device,
+                                     cu_mask_spread(graph->device, cfg.sampler_cus, true),
+                                     (uint64_t)cfg.seed);
+  else
+    cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
   // inputs were produced on other streams: order them before our stream
   TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
   auto guard = cs->guard();
@@ -42,11 +49,21 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // outermost, whose backward the context skips)
   std::vector<bool> csr(L, cfg.deterministic_backward);
   csr[L - 1] = false;
+  // Pipelined: three sampler slots.  Batch k+1 is sampled into the slot of
+  // batch k-2, whose training finished before batch k-1's began, so the
+  // sampling stream never waits on an unfinished event when its kernels are
+  // launched (with two slots it waits on batch k-1's training, and ROCm then
+  // blocks every launch on that stream in the host for ~60 us).
+  nslots_ = cfg.pipeline ? kSlots : 1;
   sampler = std::make_unique<FastSampler>(graph, train_nids, L, cfg.batch_size, cfg.fanout,
-                                          cfg.pipeline ? 2 : 1, csr,
+                                          nslots_, csr,
                                           cfg.weight_type != WeightType::None);
   sampler->rng_mode = cfg.rng_mode;
-  if (cfg.pipeline)
+  if (cfg.pipeline && cfg.sampler_cus > 0)
+    ss = std::make_unique<NtsStream>(graph->device,
+                                     cu_mask_spread(graph->device, cfg.sampler_cus, false),
+                                     (uint64_t)cfg.seed);
+  else if (cfg.pipeline)
     ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed,
                                      cfg.sampler_priority);
   // size the scratch arenas once so the training loop never allocates
@@ -60,8 +77,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // sampling, on the sampling stream: with the pipeline it runs while the
   // previous batch trains (HBM-bound gather next to MFMA-bound GEMMs).
   early_ = cfg.early_aggregate && cfg.fused_gather;
-  const int nslots = cfg.pipeline ? 2 : 1;
-  for (int i = 0; i < nslots; ++i) {
+  for (int i = 0; i < nslots_; ++i) {
     TORCH_CHECK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming) == hipSuccess,
                 "hipEventCreate");
     if (early_)
@@ -72,6 +88,16 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
 }
 
 GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
+  if (!tl_.empty()) {
+    (void)hipDeviceSynchronize();
+    const size_t from = tl_.size() > 80 ? tl_.size() - 80 : 0;
+    for (size_t i = from; i < tl_.size(); ++i) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, tl_[from].second, tl_[i].second);
+      fprintf(stderr, "[timeline] %s %9.1f us\n", tl_[i].first, ms * 1e3);
+    }
+    for (auto& e : tl_) (void)hipEventDestroy(e.second);
+  }
   for (auto& e : ev_pool_) {
     (void)hipEventDestroy(e.first);
     (void)hipEventDestroy(e.second);
@@ -85,7 +111,23 @@ GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
 // with early aggregation — the bottom graph op (fused feature gather +
 // aggregation, SingleGPUAllSampleGraphOp::forward on the feature table) on
 // the same stream.  Sizes are device-side: nothing here waits for the host.
+// NTS_TIMELINE=1: timing events at the start/end of every sampling and
+// training launch sequence, printed (relative to the first) at destruction —
+// the unperturbed GPU timeline of the two streams (a profiler slows the host).
+static bool timeline_on() {
+  static const bool on = getenv("NTS_TIMELINE") != nullptr;
+  return on;
+}
+void GCN_SAMPLE_ALLGPU_impl::mark(const char* what, NtsStream& st) {
+  if (!timeline_on() || tl_.size() > 4000) return;
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, (hipStream_t)st.stream());
+  tl_.push_back({what, e});
+}
+
 void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
+  mark("S<", st);
   sampler->issue_gpu_sample(cfg.batch_size, slot, st, cfg.weight_type);
   if (early_) {
     auto guard = st.guard();
@@ -107,6 +149,7 @@ void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
   }
   TORCH_CHECK(hipEventRecord(ready_[slot], (hipStream_t)st.stream()) == hipSuccess,
               "hipEventRecord");
+  mark("S>", st);
 }
 
 // compulsory bytes of the bottom aggregation: distinct src rows once, index +
@@ -187,7 +230,8 @@ NtsVar GCN_SAMPLE_ALLGPU_impl::vertexForward(int l, NtsVar& a) {
 }
 
 std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool keep,
-                                                     const NtsVar* pre_y) {
+                                                     const NtsVar* pre_y,
+                                                     const NtsVar* loss_target) {
   const int L = (int)P.size();
   std::vector<NtsVar> acts;
   NtsVar X0;
@@ -251,7 +295,11 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       account_bottom(sg, cfg.fused_gather);
       if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
     }
-    X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(l, a); }, Y);
+    if (loss_target && l == L - 1)  // vertexForward + Loss of the last layer, fused
+      X = ctx.runVertexForward(
+          [&](NtsVar& a) { return hip_linear_xent(a, P[l]->W, *loss_target, cs.get()); }, Y);
+    else
+      X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(l, a); }, Y);
     if (keep) {
       acts.push_back(Y.detach());
       acts.push_back(X.detach());
@@ -307,7 +355,7 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   }
   SampledSubgraph* sg = sampler->finish_gpu_sample(slot);
   if (ss) {
-    next_slot_ = slot ^ 1;
+    next_slot_ = (slot + 1) % nslots_;
     if (sampler->sample_not_finished()) {  // prefetch the next batch behind this one
       issue(next_slot_, *ss);
       prefetched_ = next_slot_;
@@ -316,17 +364,26 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[slot], 0) == hipSuccess,
               "hipStreamWaitEvent");
   double t1 = now_s();
+  mark("T<", *cs);
   sampler->load_label_gpu(*cs, sg, target, L_GT);
   ctx.train();
   if (early_) account_bottom(sg, true);
-  auto acts = forward(sg, false, early_ ? &pre_y_[slot] : nullptr);
-  NtsVar out = acts.back();
-  Loss(out, target);
+  const int L = (int)P.size();
+  const bool fuse_loss = cfg.fuse_loss && cfg.hip_gemm && L >= 2 &&
+                         hip_linear_xent_supported(P[L - 1]->W.size(0), P[L - 1]->W.size(1));
+  auto acts = forward(sg, false, early_ ? &pre_y_[slot] : nullptr, fuse_loss ? &target : nullptr);
+  if (fuse_loss) {
+    loss = acts.back();
+  } else {
+    NtsVar out = acts.back();
+    Loss(out, target);
+  }
   ctx.self_backward(false);
   Update();
   for (auto* p : P) p->zero_grad();
   TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)cs->stream()) == hipSuccess,
               "hipEventRecord");
+  mark("T>", *cs);
   double t2 = now_s();
   sample_time += t1 - t0;
   train_time += t2 - t1;

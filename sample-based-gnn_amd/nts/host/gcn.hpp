@@ -19,7 +19,9 @@ struct GCNConfig {
   bool hip_gemm = true;               // layer GEMMs on the hand-written MFMA kernels
   bool pipeline = true;               // sample batch i+1 on its own stream while i trains
   bool fuse_activation = true;        // hidden layers: relu + dropout in the MFMA GEMM
+  bool fuse_loss = true;              // training: output layer + log_softmax x2 + nll in 2 kernels
   bool sampler_priority = true;       // pipelined sampler on a high-priority stream
+  int sampler_cus = 0;                // > 0: the sampler stream owns this many CUs, training the rest
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
   bool shuffle = true;
@@ -61,18 +63,24 @@ class GCN_SAMPLE_ALLGPU_impl {
 
  private:
   NtsVar vertexForward(int l, NtsVar& a);
-  std::vector<NtsVar> forward(SampledSubgraph* sg, bool keep, const NtsVar* pre_y = nullptr);
+  // with `loss_target` (training), the last element is the fused scalar loss
+  std::vector<NtsVar> forward(SampledSubgraph* sg, bool keep, const NtsVar* pre_y = nullptr,
+                              const NtsVar* loss_target = nullptr);
   void issue(int slot, NtsStream& st);
   void account_bottom(SampledSubgraph* sg, bool fused_map);
   void Loss(NtsVar& left, NtsVar& right);
   void Update();
   std::pair<hipEvent_t, hipEvent_t>& next_events();
+  void mark(const char* what, NtsStream& st);
+  std::vector<std::pair<const char*, hipEvent_t>> tl_;  // NTS_TIMELINE events
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool_;
   size_t ev_pending_ = 0;
   // early aggregation: per sampler slot, the bottom graph op's output and the
   // event after which it (and the slot's sampled graph) is ready
-  NtsVar pre_y_[2];
-  hipEvent_t ready_[2] = {nullptr, nullptr};
+  static constexpr int kSlots = 3;  // sampler slots when pipelined (see the constructor)
+  int nslots_ = 1;
+  NtsVar pre_y_[kSlots];
+  hipEvent_t ready_[kSlots] = {nullptr, nullptr, nullptr};
   bool early_ = false;
   uint64_t dropout_calls_ = 0;  // Philox offset of the fused dropout masks
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch

@@ -59,6 +59,9 @@ class NtsStream {
   // its short, latency-bound kernels are dispatched ahead of the training
   // stream's long ones, which fill the remaining CU slots)
   NtsStream(int device, void* stream, uint64_t seed, bool high_priority = false);
+  // an owned stream restricted to the CUs set in `cu_mask` (one bit per CU,
+  // hipExtStreamCreateWithCUMask): partitions the device between streams
+  NtsStream(int device, const std::vector<uint32_t>& cu_mask, uint64_t seed);
   ~NtsStream();
   NtsStream(const NtsStream&) = delete;
   NtsStream& operator=(const NtsStream&) = delete;
@@ -73,6 +76,7 @@ class NtsStream {
 
  private:
   nts_hip_ctx* ctx_ = nullptr;
+  hipStream_t owned_ = nullptr;
   int device_ = 0;
   c10::hip::HIPStream torch_stream_;
 };
@@ -112,7 +116,6 @@ class sampCSC {
   bool has_csr = false;
   torch::Tensor destination, column_offset, row_indices, sample_ans, edge_dst, source,
       edge_weight_forward, row_offset, column_indices, edge_weight_backward, sizes;
-  torch::Tensor dst_count;  // layer-0 device scalar holding v_size (seeds)
 
   sampCSC(int device, VertexId v_cap, VertexId e_cap, VertexId s_cap, bool csr, bool weights);
   // the reference accessor names
@@ -194,6 +197,7 @@ class FastSampler {
 
  private:
   torch::Tensor dev_nids_;  // device copy of sample_nids
+  torch::Tensor dev_iota_;  // 0, 1, ..., batch_cap: device scalars for the layer-0 v_size
   VertexId batch_cap_ = 0;
 };
 
@@ -300,6 +304,13 @@ class NtsContext {
 // x.matmul(W) on the MFMA fp32 kernels (nts_hip_gemm_f32) with its own
 // backward: dW = x^T dZ (split-reduction, deterministic), dx = dZ W^T.
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
+// CU masks splitting the device: `n` CUs spread evenly over the chip
+// (every (total/n)-th CU) and the complement
+std::vector<uint32_t> cu_mask_spread(int device, int n, bool complement);
+// training output layer + loss: nll_loss(log_softmax(log_softmax(y W)), target)
+// in two fused kernels (nts_hip_linear_xent_fwd/bwd); returns the scalar loss
+bool hip_linear_xent_supported(int64_t K, int64_t C);
+NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs);
 // row-major fp32 views the HIP GEMMs take without a copy (unit column stride)
 NtsVar row_major(const NtsVar& x);
 // [rows, F] with 128-byte aligned rows when F >= 256 (padded leading dimension)

@@ -50,6 +50,19 @@ us_g = t(lambda: ctx.spmm_csc_fwd(l1.column_offset, l1.row_indices, l1.edge_weig
                                   l1.sizes[0:1], v1, feat, y602, row_map=l1.source))
 byts = 4.0 * F * s1 + 8.0 * e1 + 4.0 * (v1 + 1) + 4.0 * F * v1 + 4.0 * s1
 print(f"gather+agg 602: {us_g:.1f} us  ({byts / us_g / 1e3:.0f} GB/s algorithmic)")
+featp = torch.empty(g.n_vertices, 608, device=dev)[:, :F]
+featp.copy_(feat)
+y602p = torch.empty(v1, 608, device=dev)[:, :F]
+us_gp = t(lambda: ctx.spmm_csc_fwd(l1.column_offset, l1.row_indices, l1.edge_weight_forward,
+                                   l1.sizes[0:1], v1, featp, y602p, row_map=l1.source))
+print(f"gather+agg 602 from a 128-B aligned table (pitch 608), padded output: {us_gp:.1f} us")
+featp4 = torch.empty(g.n_vertices, 608, device=dev)
+featp4[:, :F].copy_(feat)
+featp4[:, F:] = 0
+y604 = torch.empty(v1, 608, device=dev)
+us_gp4 = t(lambda: ctx.spmm_csc_fwd(l1.column_offset, l1.row_indices, l1.edge_weight_forward,
+                                    l1.sizes[0:1], v1, featp4[:, :604], y604[:, :604], row_map=l1.source))
+print(f"  same, 604 columns as float4: {us_gp4:.1f} us")
 Hm = torch.randn(s1, 128, device=dev)
 y128 = torch.empty(v1, 128, device=dev)
 us_a = t(lambda: ctx.spmm_csc_fwd(l1.column_offset, l1.row_indices, l1.edge_weight_forward,

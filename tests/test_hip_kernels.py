@@ -495,3 +495,33 @@ def test_gemm_padded_pitch(hip, M, N, K, trans_a):
     hip.gemm(A.contiguous(), B, C2, trans_a=trans_a)
     torch.cuda.synchronize()
     torch.testing.assert_close(C2, C, rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize("n,K,C", [(10000, 128, 41), (1024, 256, 47), (33, 16, 7), (1, 16, 64),
+                                   (5000, 128, 2), (77, 32, 17)])
+def test_linear_xent_fused(hip, n, K, C):
+    """Fused output layer + loss vs libtorch's own ops on the same tensors
+    (Y @ W, log_softmax twice, mean nll_loss, autograd backward)."""
+    g = torch.Generator(device=DEV).manual_seed(n + K + C)
+    Y = torch.randn(n, K, device=DEV, generator=g)
+    W = torch.randn(K, C, device=DEV, generator=g) * 0.1
+    lab = torch.randint(0, C, (n,), device=DEV, generator=g)
+    loss = torch.full((), float("nan"), device=DEV)
+    hip.linear_xent_fwd(Y, W, lab, loss)
+    Yr, Wr = Y.double().requires_grad_(), W.double().requires_grad_()
+    ref = torch.nn.functional.nll_loss((Yr @ Wr).log_softmax(1).log_softmax(1), lab)
+    ref.backward(torch.tensor(1.7, dtype=torch.float64, device=DEV))
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss.double(), ref.detach(), rtol=1e-5, atol=1e-5)
+    dY = torch.full((n, K), float("nan"), device=DEV)
+    dW = torch.full((K, C), float("nan"), device=DEV)
+    gl = torch.tensor(1.7, device=DEV)
+    hip.linear_xent_bwd(Y, W, lab, gl, dY, dW)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(dY.double(), Yr.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(dW.double(), Wr.grad, rtol=1e-4, atol=1e-6)
+    dY2, dW2, loss2 = torch.empty_like(dY), torch.empty_like(dW), torch.empty_like(loss)
+    hip.linear_xent_fwd(Y, W, lab, loss2)
+    hip.linear_xent_bwd(Y, W, lab, gl, dY2, dW2)
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss2) and torch.equal(dY, dY2) and torch.equal(dW, dW2)
