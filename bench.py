@@ -62,6 +62,8 @@ def parse():
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
     p.add_argument("--sampler-cus", type=int, default=0,
                    help="CUs reserved for the pipelined sampler stream (0: no partition)")
+    p.add_argument("--no-pad-features", action="store_true",
+                   help="gather from the feature table as given (no 128-byte row pitch copy)")
     p.add_argument("--no-fuse-loss", action="store_true",
                    help="output layer + loss as libtorch ops instead of the fused kernels")
     p.add_argument("--fuse-linear", action="store_true",
@@ -122,7 +124,8 @@ def main():
                           fuse_linear=args.fuse_linear, early_aggregate=args.early_agg,
                           sampler_priority=not args.no_priority,
                           fuse_activation=not args.no_fuse_act,
-                          fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus)
+                          fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
+                          pad_features=not args.no_pad_features)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and not args.early_agg and layers[1] <= 128)
     agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")

@@ -37,7 +37,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
                seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False,
                early_aggregate=True, sampler_priority=True, fuse_activation=True,
-               fuse_loss=True, sampler_cus=0):
+               fuse_loss=True, sampler_cus=0, pad_features=True):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -60,6 +60,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.fuse_activation = bool(fuse_activation)
     c.fuse_loss = bool(fuse_loss)
     c.sampler_cus = int(sampler_cus)
+    c.pad_features = bool(pad_features)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

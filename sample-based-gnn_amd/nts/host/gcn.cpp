@@ -40,6 +40,15 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // inputs were produced on other streams: order them before our stream
   TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
   auto guard = cs->guard();
+  // Wide feature rows are re-laid with a 128-byte aligned pitch (one copy,
+  // +1% memory): a gathered row then spans the minimum number of cache lines
+  // (19 instead of ~19.8 for 602 floats), ~2% less traffic in the bottom
+  // aggregation, which reads every sampled row once per edge.
+  if (cfg.pad_features && F.size(1) >= 256 && F.size(1) % 32 != 0 && F.stride(1) == 1) {
+    NtsVar Fp = row_padded_empty(F.size(0), F.size(1), graph->device);
+    Fp.copy_(F);
+    F = Fp;
+  }
   if (cfg.shuffle) {  // shuffle_vec (toolkits/GCN_SAMPLE_GPU.hpp:175-180): mt19937(2000)
     std::mt19937 gen(2000);
     std::shuffle(train_nids.begin(), train_nids.end(), gen);

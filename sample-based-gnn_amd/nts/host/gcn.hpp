@@ -21,7 +21,8 @@ struct GCNConfig {
   bool fuse_activation = true;        // hidden layers: relu + dropout in the MFMA GEMM
   bool fuse_loss = true;              // training: output layer + log_softmax x2 + nll in 2 kernels
   bool sampler_priority = true;       // pipelined sampler on a high-priority stream
-  int sampler_cus = 0;                // > 0: the sampler stream owns this many CUs, training the rest
+  int sampler_cus = 0;
+  bool pad_features = true;           // copy wide feature tables to a 128-byte row pitch                // > 0: the sampler stream owns this many CUs, training the rest
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
   bool shuffle = true;
