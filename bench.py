@@ -128,7 +128,7 @@ def main():
                           pad_features=not args.no_pad_features)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and not args.early_agg and layers[1] <= 128)
-    agg_kernel = ("k_spmm_gather_linear" if fused_linear else "k_spmm_gather")
+    agg_kernel = ("k_agg_gemm" if fused_linear else "k_spmm_gather")
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
 
     def step():

@@ -178,19 +178,23 @@ int nts_hip_spmm_csc_fwd(nts_hip_ctx *ctx, const uint32_t *column_offset,
                          const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
                          const uint32_t *x_row_map, uint32_t feature_size, float *y,
                          uint64_t ldy);
-/* Fused bottom layer of the GCN step: y = A x (exactly nts_hip_spmm_csc_fwd,
- * bit-identical; y may be NULL when not needed) and z = y W (W: row-major
- * [feature_size, out_size], out_size <= 128) on MFMA fp32, in one pass that
- * overlaps the matrix work with the row gathers.  Replaces the pair
- * SingleGPUAllSampleGraphOp::forward + Parameter::forward of the first layer
- * (core/ntsSingleGPUSampleGraphOp.hpp:210-250, core/NtsScheduler.hpp:859-862).
- * feature_size <= ~1270 (LDS tile of 32 rows). */
+/* Fused bottom layer (SingleGPUAllSampleGraphOp::forward on the feature table
+ * followed by Parameter::forward and vertexForward's activation):
+ *   Y = A X  (rows of x gathered through x_row_map, bit-identical to
+ *             nts_hip_spmm_csc_fwd; written to y when y != NULL),
+ *   Z = Y W  (W [feature_size x out_size] row-major, MFMA fp32),
+ *   activation != 0: z = dropout(relu(Z), p) with the Philox mask of
+ *   nts_hip_gemm_relu_dropout_f32 (same seed/offset/(row, col) keys),
+ *   activation == 0: z = Z.
+ * out_size <= 128, feature_size <= 608.  The GEMM runs under the HBM-bound
+ * gather of the aggregation (two tiles per CU in alternating phases). */
 int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx *ctx, const uint32_t *column_offset,
                                 const uint32_t *row_indices, const float *weight,
                                 const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
                                 const uint32_t *x_row_map, uint32_t feature_size, const float *W,
                                 uint32_t out_size, float *y, uint64_t ldy, float *z,
-                                uint64_t ldz);
+                                uint64_t ldz, int activation, float p, uint64_t seed,
+                                uint64_t offset);
 /* G_in[s,:] = sum_{j in [ro[s],ro[s+1])} w_b[j] * G_out[ci[j],:] (ascending dst
  * order, deterministic, atomic-free).  Replaces Gather_By_Src_From_Dst_Spmm
  * (cuda/ntsCUDAGraphOP.cu:901-1042) and MiniBatchFuseOp::backward

@@ -285,160 +285,243 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
 
 
 // ---------------------------------------------------------------------------
-// Fused bottom layer: Y = A X (gathered through `map`) and Z = Y W in one pass.
-// Tiles of 32 destinations: phase 1 — each wave aggregates 8 rows exactly as
-// k_spmm_gather (same order and arithmetic, so Y is bit-identical), stores
-// them to Y (kept for the weight gradient) and into an LDS tile; phase 2 —
-// each wave multiplies the 32 x F LDS tile by a 32-column slice of W on
-// v_mfma_f32_32x32x2_f32.  The k range is split in halves between the two
-// lane halves of the MFMA (lanes 0-31: k in [0,Kh), lanes 32-63: [Kh,2Kh)),
-// so every lane reads two consecutive k with one conflict-free ds_read_b64
-// (row pitch LDP = 2Kh+2: LDP/2 odd spreads 32 rows over all 64 banks).
-// The gathers dominate (HBM/MALL); the MFMA phase of one block overlaps the
-// gather phase of the other block resident on the CU.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int kTM = 32;
+// Fused bottom layer: Y = A X (rows gathered through `map`), Z = Y W and
+// optionally X1 = dropout(relu(Z)) in one kernel (k_agg_gemm).
+//
+// A 256-thread block owns tiles of 32 destination rows:
+//  phase 1 — each wave aggregates 8 rows exactly as k_spmm_gather (same edge
+//     order and mul-then-add arithmetic: Y is bit-identical to the graph op),
+//     writes them to Y (kept for the weight gradient) and into the LDS tile;
+//  phase 2 — wave w computes Z[32 rows x 32 columns 32w .. 32w+31] on
+//     v_mfma_f32_16x16x4_f32 (2 x 2 tiles): A from the LDS tile, B = W rows
+//     streamed from L2 with a two-deep register prefetch (interleaved columns
+//     32w + 2i + j: one float2 per lane per k); epilogue relu + dropout with the
+//     Philox mask of nts_hip_gemm_relu_dropout_f32 (same (row, col) keys).
+// Two blocks per CU (LDS tile 32 x LDP floats, LDP = 2 mod 32: conflict-free
+// b32 reads of 16 rows x 2 k) so one block's MFMA phase runs under the other's
+// HBM-bound gather phase: the layer GEMM costs (almost) no extra time.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kAgTM = 32;         // rows per tile
+constexpr int kAgN = 128;         // output columns (4 waves x 32)
+constexpr int kAgMaxLDP = 640;    // 32 x 640 x 4 B = 80 KiB: two blocks per CU
 
-template <int VEC, int NCH, bool MAP>
-__global__ __launch_bounds__(kAggThreads, 2) void k_spmm_gather_linear(
-    const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
-    const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
-    const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t F,
-    const float* __restrict__ W, uint32_t N, float* __restrict__ y, uint64_t ldy,
-    float* __restrict__ z, uint64_t ldz, uint32_t Kh, uint32_t LDP) {
+struct AgArgs {
+  const uint32_t* off;
+  const uint32_t* idx;
+  const float* w;
+  const uint32_t* n_dev;
+  uint32_t n_cap;
+  const float* x;
+  uint64_t ldx;
+  const uint32_t* map;
+  uint32_t F;
+  const float* W;
+  uint32_t N;
+  float* y;
+  uint64_t ldy;
+  float* z;
+  uint64_t ldz;
+  uint32_t LDP;
+  uint32_t keep_threshold;
+  float scale;
+  uint64_t seed, offset;
+};
+
+template <int VEC, int NCH, bool MAP, bool ACT>
+__global__ __launch_bounds__(kAggThreads, 2) void k_agg_gemm(AgArgs a) {
   using V = VT<VEC>;
   using T = typename V::T;
-  extern __shared__ float sY[];  // [kTM][LDP]
-  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  extern __shared__ __attribute__((aligned(16))) float sY[];  // [kAgTM][LDP]
+  const uint32_t n = a.n_dev ? min(*a.n_dev, a.n_cap) : a.n_cap;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t nv = F / VEC;
-  // zero the k padding [F, LDP) once: it multiplies W rows that are masked to
-  // zero, but LDS garbage could hold Inf/NaN
-  for (uint32_t i = threadIdx.x; i < kTM * (LDP - F); i += blockDim.x) {
-    const uint32_t r = i / (LDP - F), c = F + i % (LDP - F);
+  const uint32_t nv = a.F / VEC;
+  const uint32_t LDP = a.LDP;
+  const uint32_t Kr = (a.F + 3) / 4 * 4;  // k range of the MFMA phase (zero padded)
+  // zero the k padding [F, Kr) of every LDS row once
+  for (uint32_t e = threadIdx.x; e < kAgTM * (Kr - a.F); e += blockDim.x) {
+    const uint32_t r = e / (Kr - a.F), c = a.F + e % (Kr - a.F);
     sY[r * LDP + c] = 0.f;
   }
-  const uint32_t ntiles = (n + kTM - 1) / kTM;
+  const int i = lane & 15, g = lane >> 4;
+  // this wave's output columns: 32 wv + 2 i + j (j = 0, 1); clamped for loads
+  const uint32_t col0 = 32 * wv + 2 * i;
+  const bool col_ok0 = col0 < a.N, col_ok1 = col0 + 1 < a.N;
+  // even N: one float2 per row (a pair past N is never stored); odd N: two
+  // clamped scalars
+  const bool wpair = (a.N % 2 == 0);
+  const uint32_t ccl = wpair ? min(col0, a.N - 2) : 0u;
+  const uint32_t cx = min(col0, a.N - 1), cy = min(col0 + 1, a.N - 1);
+  const uint32_t ntiles = (n + kAgTM - 1) / kAgTM;
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    // ---- phase 1: aggregation of 32 rows (8 per wave) ----
-    for (int rr = wv; rr < kTM; rr += 4) {
-      const uint32_t d = tile * kTM + rr;
-      float* srow = sY + rr * LDP;
-      if (d >= n) {
-        for (uint32_t c = lane; c < F; c += 64) srow[c] = 0.f;
-        continue;
-      }
-      const uint32_t beg = off[d], end = off[d + 1];
-      T acc[NCH];
+    // ---- phase 1: aggregation of 32 rows, 8 per wave, two rows at a time ----
+    // (rows rr and rr + 16 advance together: 8 gathered rows in flight per
+    // wave; per row the sum runs in edge order exactly as k_spmm_gather)
+    for (int rr = wv; rr < kAgTM / 2; rr += 4) {
+      const uint32_t dA = tile * kAgTM + rr, dB = dA + kAgTM / 2;
+      const bool okA = dA < n, okB = dB < n;
+      const uint32_t begA = okA ? a.off[dA] : 0u, endA = okA ? a.off[dA + 1] : 0u;
+      const uint32_t begB = okB ? a.off[dB] : 0u, endB = okB ? a.off[dB + 1] : 0u;
+      T accA[NCH], accB[NCH];
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
-      uint32_t e = beg;
-      for (; e + kUnroll <= end; e += kUnroll) {
-        uint32_t r[kUnroll];
-        float ww[kUnroll];
+      for (int c = 0; c < NCH; ++c) {
+        accA[c] = V::zero();
+        accB[c] = V::zero();
+      }
+      uint32_t eA = begA, eB = begB;
+      while (eA < endA || eB < endB) {  // wave-uniform
+        const uint32_t nA = min(endA - eA, (uint32_t)kUnroll), nB = min(endB - eB, (uint32_t)kUnroll);
+        uint32_t r[2 * kUnroll];
+        float ww[2 * kUnroll];
 #pragma unroll
         for (int j = 0; j < kUnroll; ++j) {
-          r[j] = idx[e + j];
-          ww[j] = w ? w[e + j] : 1.0f;
+          r[j] = j < (int)nA ? a.idx[eA + j] : 0u;
+          ww[j] = j < (int)nA ? (a.w ? a.w[eA + j] : 1.0f) : 0.f;
+          r[kUnroll + j] = j < (int)nB ? a.idx[eB + j] : 0u;
+          ww[kUnroll + j] = j < (int)nB ? (a.w ? a.w[eB + j] : 1.0f) : 0.f;
         }
         if (MAP) {
 #pragma unroll
-          for (int j = 0; j < kUnroll; ++j) r[j] = map[r[j]];
+          for (int j = 0; j < kUnroll; ++j) {
+            if (j < (int)nA) r[j] = a.map[r[j]];
+            if (j < (int)nB) r[kUnroll + j] = a.map[r[kUnroll + j]];
+          }
         }
-        T xv[kUnroll][NCH];
+        T xv[2 * kUnroll][NCH];
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {
-          const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r[j] * ldx);
+        for (int j = 0; j < 2 * kUnroll; ++j) {
+          const bool use = j < kUnroll ? j < (int)nA : (j - kUnroll) < (int)nB;
+          const T* xrow = reinterpret_cast<const T*>(a.x + (uint64_t)r[j] * a.ldx);
 #pragma unroll
           for (int c = 0; c < NCH; ++c) {
             const uint32_t col = lane + c * 64;
-            xv[j][c] = (col < nv) ? xrow[col] : V::zero();
+            xv[j][c] = (use && col < nv) ? xrow[col] : V::zero();
           }
         }
 #pragma unroll
         for (int j = 0; j < kUnroll; ++j)
 #pragma unroll
-          for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
+          for (int c = 0; c < NCH; ++c) {
+            if (j < (int)nA) accA[c] = V::madd(accA[c], xv[j][c], ww[j]);
+            if (j < (int)nB) accB[c] = V::madd(accB[c], xv[kUnroll + j][c], ww[kUnroll + j]);
+          }
+        eA += nA;
+        eB += nB;
       }
-      for (; e < end; ++e) {
-        uint32_t r = idx[e];
-        const float we = w ? w[e] : 1.0f;
-        if (MAP) r = map[r];
-        const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r * ldx);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t d = h ? dB : dA;
+        float* srow = sY + (rr + h * (kAgTM / 2)) * LDP;
+        T* yrow = (a.y && d < n) ? reinterpret_cast<T*>(a.y + (uint64_t)d * a.ldy) : nullptr;
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
           const uint32_t col = lane + c * 64;
-          if (col < nv) acc[c] = V::madd(acc[c], xrow[col], we);
-        }
-      }
-      T* yrow = y ? reinterpret_cast<T*>(y + (uint64_t)d * ldy) : nullptr;
+          if (col < nv) {
+            const T v = d < n ? (h ? accB[c] : accA[c]) : V::zero();
+            if (yrow) V::st_nt(yrow + col, v);
+            const float* av = reinterpret_cast<const float*>(&v);
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const uint32_t col = lane + c * 64;
-        if (col < nv) {
-          if (yrow) yrow[col] = acc[c];
-          const float* a = reinterpret_cast<const float*>(&acc[c]);
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) srow[col * VEC + q] = a[q];
+            for (int q = 0; q < VEC; ++q) srow[col * VEC + q] = av[q];
+          }
         }
       }
     }
     __syncthreads();
-    // ---- phase 2: Z[tile, 32*wv .. +32) = sY[32 x F] W[F x 32-slice] ----
-    const int r = lane & 31, h = lane >> 5;
-    const uint32_t col = 32 * wv + r;
-    const bool col_ok = col < N;
-    f32x16 acc;
+    // ---- phase 2: Z[tile rows][32 wv .. +32) = sY W on 16x16x4 MFMA ----
+    // step s: lane group g contributes k = 4 s + g; A = sY[16 rt + i][k],
+    // B = W[k][32 wv + 2 i + j]
+    f32x4 acc[2][2];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    const float* arow = sY + r * LDP + h * Kh;
-    const uint32_t kb = h * Kh;
-    for (uint32_t t = 0; t < Kh; t += 2) {
-      const float2 a2 = *reinterpret_cast<const float2*>(arow + t);
-      const uint32_t k0 = kb + t, k1 = k0 + 1;
-      const float b0 = (col_ok && k0 < F) ? W[(uint64_t)k0 * N + col] : 0.f;
-      const float b1 = (col_ok && k1 < F) ? W[(uint64_t)k1 * N + col] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.x, b0, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a2.y, b1, acc, 0, 0, 0);
-    }
-    if (col_ok) {
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t rowi = tile * kTM + 8 * (i >> 2) + 4 * h + (i & 3);
-        if (rowi < n) z[(uint64_t)rowi * ldz + col] = acc[i];
+      for (int j = 0; j < 2; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* a0 = sY + i * LDP + g;
+    const float* a1 = sY + (16 + i) * LDP + g;
+    const uint32_t nsteps = Kr / 4;
+    constexpr int PF = 8;  // k-steps per prefetch group
+    auto ldw = [&](uint32_t s, float2& b) {
+      const uint32_t k = min(4 * s + g, a.F - 1);  // k >= F multiplies a zero A
+      const float* wr = a.W + (uint64_t)k * a.N;
+      if (wpair) b = *reinterpret_cast<const float2*>(wr + ccl);
+      else b = make_float2(wr[cx], wr[cy]);
+    };
+    float2 bq[2][PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) ldw(q, bq[0][q]);
+    for (uint32_t s0 = 0; s0 < nsteps; s0 += 2 * PF) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const uint32_t sb = s0 + half * PF;
+        if (sb >= nsteps) break;
+        // prefetch the next group into the other register set
+#pragma unroll
+        for (int q = 0; q < PF; ++q) ldw(min(sb + PF + q, nsteps - 1), bq[half ^ 1][q]);
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          const uint32_t s = sb + q;
+          if (s >= nsteps) break;
+          const float x0 = a0[4 * s], x1 = a1[4 * s];
+          const float2 b = bq[half][q];
+          acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b.x, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b.y, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, b.x, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, b.y, acc[1][1], 0, 0, 0);
+        }
       }
     }
-    __syncthreads();
+    // epilogue: acc[rt][j][v] = Z[tile*32 + 16 rt + 4 g + v][col0 + j]
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const uint32_t r4 = tile * kAgTM + 16 * rt + 4 * g;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t col = col0 + j;
+        if (!(j ? col_ok1 : col_ok0)) continue;
+        float o[4] = {acc[rt][j][0], acc[rt][j][1], acc[rt][j][2], acc[rt][j][3]};
+        if constexpr (ACT) {
+          const uint4 rnd = philox4x32_10(
+              make_uint4(r4 >> 2, col, (uint32_t)a.offset, (uint32_t)(a.offset >> 32)),
+              make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
+          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            o[v] = (wd[v] >= a.keep_threshold && o[v] > 0.f) ? o[v] * a.scale : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (r4 + v < n) a.z[(uint64_t)(r4 + v) * a.ldz + col] = o[v];
+      }
+    }
+    __syncthreads();  // the LDS tile is rewritten by the next phase 1
   }
 }
 
-template <int VEC, bool MAP>
-static int launch_gather_linear_vec(hipStream_t st, int nch, uint32_t grid, size_t lds,
-                                    const uint32_t* off, const uint32_t* idx, const float* w,
-                                    const uint32_t* n_dev, uint32_t n_cap, const float* x,
-                                    uint64_t ldx, const uint32_t* map, uint32_t F, const float* W,
-                                    uint32_t N, float* y, uint64_t ldy, float* z, uint64_t ldz,
-                                    uint32_t Kh, uint32_t LDP) {
-#define NTS_GL(NCH)                                                                          \
-  do {                                                                                       \
-    NTS_HIP_TRY(hipFuncSetAttribute(                                                         \
-        reinterpret_cast<const void*>(&k_spmm_gather_linear<VEC, NCH, MAP>),                 \
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                              \
-    hipLaunchKernelGGL((k_spmm_gather_linear<VEC, NCH, MAP>), dim3(grid), dim3(kAggThreads), \
-                       lds, st, off, idx, w, n_dev, n_cap, x, ldx, map, F, W, N, y, ldy, z,  \
-                       ldz, Kh, LDP);                                                        \
+// LDS row pitch of the fused kernel: >= F rounded up to 4 (MFMA k range),
+// = 2 mod 32 (conflict-free reads); 0 when the tile does not fit two blocks per CU.
+static uint32_t ag_ldp(uint32_t F) {
+  const uint32_t k4 = (F + 3) / 4 * 4;
+  const uint32_t ldp = k4 + ((2u + 32u - k4 % 32u) % 32u);
+  return ldp <= (uint32_t)kAgMaxLDP ? ldp : 0u;
+}
+
+template <int VEC, bool MAP, bool ACT>
+static int launch_agg_gemm_vec(hipStream_t st, int nch, uint32_t grid, size_t lds,
+                               const AgArgs& a) {
+#define NTS_AG(NCH)                                                                        \
+  do {                                                                                     \
+    NTS_HIP_TRY(hipFuncSetAttribute(                                                       \
+        reinterpret_cast<const void*>(&k_agg_gemm<VEC, NCH, MAP, ACT>),                    \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                            \
+    hipLaunchKernelGGL((k_agg_gemm<VEC, NCH, MAP, ACT>), dim3(grid), dim3(kAggThreads),    \
+                       lds, st, a);                                                        \
   } while (0)
   switch (nch) {
-    case 1: NTS_GL(1); break;
-    case 2: NTS_GL(2); break;
-    case 3: NTS_GL(3); break;
-    case 4: NTS_GL(4); break;
-    case 5: NTS_GL(5); break;
-    case 6: NTS_GL(6); break;
-    case 7: NTS_GL(7); break;
-    default: NTS_GL(8); break;
+    case 1: NTS_AG(1); break;
+    case 2: NTS_AG(2); break;
+    case 3: NTS_AG(3); break;
+    case 4: NTS_AG(4); break;
+    default: NTS_AG(5); break;
   }
-#undef NTS_GL
+#undef NTS_AG
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }
@@ -470,42 +553,55 @@ int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx* ctx, const uint32_t* column_offset,
                                 const uint32_t* v, uint32_t v_cap, const float* x, uint64_t ldx,
                                 const uint32_t* x_row_map, uint32_t feature_size, const float* W,
                                 uint32_t out_size, float* y, uint64_t ldy, float* z,
-                                uint64_t ldz) {
+                                uint64_t ldz, int activation, float p, uint64_t seed,
+                                uint64_t offset) {
   NTS_CHECK_ARG(ctx && column_offset && row_indices && x && W && z, "NULL argument");
   NTS_CHECK_ARG(ldx >= feature_size && (!y || ldy >= feature_size) && ldz >= out_size,
                 "leading dimension");
-  NTS_CHECK_ARG(out_size >= 1 && out_size <= 128, "out_size must be in [1, 128]");
+  NTS_CHECK_ARG(out_size >= 1 && out_size <= (uint32_t)kAgN, "out_size must be in [1, 128]");
+  NTS_CHECK_ARG(p >= 0.f && p <= 1.f, "dropout probability must be in [0, 1]");
   if (v_cap == 0 || feature_size == 0) return NTS_OK;
   const uint32_t F = feature_size;
-  const uint32_t half = (F + 1) / 2;
-  const uint32_t Kh = (half + 1) / 2 * 2;  // even
-  const uint32_t LDP = 2 * Kh + 2;          // LDP/2 odd: conflict-free ds_read_b64
-  const size_t lds = (size_t)kTM * LDP * sizeof(float);
-  NTS_CHECK_ARG(lds <= 160 * 1024, "feature_size too large for the fused kernel");
-  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const uint32_t LDP = ag_ldp(F);
+  NTS_CHECK_ARG(LDP != 0, "feature_size too large for the fused kernel (<= 608)");
   int vec = pick_vec(F, ldx, y ? ldy : ldx, x, y ? (const void*)y : (const void*)x);
   const uint32_t nv = F / vec;
-  int nch = (int)std::min<uint32_t>((nv + 63) / 64, 8);
-  if ((nv + 63) / 64 > 8) vec = 0;  // rows wider than 512 vectors: not supported
-  NTS_CHECK_ARG(vec != 0, "feature_size too large for the fused kernel");
-  const uint32_t tiles = (v_cap + kTM - 1) / kTM;
-  const uint32_t grid = std::max(1u, std::min(tiles, 2048u));
-#define NTS_GLV(VEC, MAPB)                                                                     \
-  do {                                                                                         \
-    return launch_gather_linear_vec<VEC, MAPB>(ctx->stream, nch, grid, lds, column_offset,     \
-                                               row_indices, weight, v, v_cap, x, ldx,          \
-                                               x_row_map, F, W, out_size, y, ldy, z, ldz, Kh,  \
-                                               LDP);                                           \
-  } while (0)
-  if (x_row_map) {
-    if (vec == 4) NTS_GLV(4, true);
-    if (vec == 2) NTS_GLV(2, true);
-    NTS_GLV(1, true);
+  const int nch = (int)((nv + 63) / 64);
+  NTS_CHECK_ARG(nch <= 5, "feature_size too large for the fused kernel");
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  AgArgs a{column_offset, row_indices, weight, v, v_cap, x, ldx, x_row_map, F, W, out_size,
+           y, ldy, z, ldz, LDP, 0u, 1.f, seed, offset};
+  if (p >= 1.f) {
+    a.keep_threshold = 0xFFFFFFFFu;
+    a.scale = 0.f;
+  } else {
+    a.keep_threshold = (uint32_t)std::min((double)p * 4294967296.0, 4294967295.0);
+    a.scale = 1.0f / (1.0f - p);
   }
-  if (vec == 4) NTS_GLV(4, false);
-  if (vec == 2) NTS_GLV(2, false);
-  NTS_GLV(1, false);
-#undef NTS_GLV
+  const size_t lds = (size_t)kAgTM * LDP * sizeof(float);
+  const uint32_t tiles = (v_cap + kAgTM - 1) / kAgTM;
+  const uint32_t grid = std::max(1u, std::min(tiles, 512u));  // 2 blocks per CU
+  const hipStream_t st = ctx->stream;
+#define NTS_AGL(VEC, MAPB, ACTB) return launch_agg_gemm_vec<VEC, MAPB, ACTB>(st, nch, grid, lds, a)
+  if (activation) {
+    if (x_row_map) {
+      if (vec == 4) NTS_AGL(4, true, true);
+      if (vec == 2) NTS_AGL(2, true, true);
+      NTS_AGL(1, true, true);
+    }
+    if (vec == 4) NTS_AGL(4, false, true);
+    if (vec == 2) NTS_AGL(2, false, true);
+    NTS_AGL(1, false, true);
+  }
+  if (x_row_map) {
+    if (vec == 4) NTS_AGL(4, true, false);
+    if (vec == 2) NTS_AGL(2, true, false);
+    NTS_AGL(1, true, false);
+  }
+  if (vec == 4) NTS_AGL(4, false, false);
+  if (vec == 2) NTS_AGL(2, false, false);
+  NTS_AGL(1, false, false);
+#undef NTS_AGL
 }
 
 int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,

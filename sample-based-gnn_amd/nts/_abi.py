@@ -89,7 +89,8 @@ def lib() -> C.CDLL:
         "nts_hip_gather_rows": ([P, P, U64, P, P, U32, U32, P, U64], I),
         "nts_hip_gather_labels": ([P, P, P, P, U32, P], I),
         "nts_hip_spmm_csc_fwd": ([P, P, P, P, P, U32, P, U64, P, U32, P, U64], I),
-        "nts_hip_spmm_csc_fwd_linear": ([P, P, P, P, P, U32, P, U64, P, U32, P, U32, P, U64, P, U64], I),
+        "nts_hip_spmm_csc_fwd_linear": ([P, P, P, P, P, U32, P, U64, P, U32, P, U32, P, U64, P, U64,
+                                         I, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),

@@ -93,11 +93,13 @@ class HipContext:
                                             ptr(x), x.stride(0), ptr(row_map), F, ptr(y),
                                             y.stride(0)))
 
-    def spmm_csc_fwd_linear(self, co, ri, w, v_dev, v_cap, x, W, z, y=None, row_map=None):
+    def spmm_csc_fwd_linear(self, co, ri, w, v_dev, v_cap, x, W, z, y=None, row_map=None,
+                            activation=False, p=0.0, seed=0, offset=0):
         F = x.shape[1]
         check(self.lib.nts_hip_spmm_csc_fwd_linear(
             self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev), v_cap, ptr(x), x.stride(0), ptr(row_map),
-            F, ptr(W), W.shape[1], ptr(y), y.stride(0) if y is not None else F, ptr(z), z.stride(0)))
+            F, ptr(W), W.shape[1], ptr(y), y.stride(0) if y is not None else F, ptr(z), z.stride(0),
+            int(activation), float(p), int(seed), int(offset)))
 
     def spmm_csr_bwd(self, ro, ci, wb, s_dev, s_cap, g_out, g_in):
         F = g_out.shape[1]

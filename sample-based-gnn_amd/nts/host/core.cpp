@@ -594,9 +594,11 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
   }
 };
 
+// Bottom graph op + first layer (+ relu/dropout) in one kernel
+// (nts_hip_spmm_csc_fwd_linear); the weight gradient uses the stored Y.
 struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, NtsVar y, int64_t sg_ptr,
-                        int64_t cs_ptr) {
+                        int64_t cs_ptr, double p, int64_t seed, int64_t offset, bool act) {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     auto* sg = reinterpret_cast<sampCSC*>(sg_ptr);
     NtsVar Wc = W.contiguous();
@@ -606,24 +608,38 @@ struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
                                           nullptr, sg->v_size, table.data_ptr<float>(),
                                           (uint64_t)table.stride(0), sg->dev_src(), (uint32_t)F,
                                           Wc.data_ptr<float>(), (uint32_t)N, y.data_ptr<float>(),
-                                          (uint64_t)F, Z.data_ptr<float>(), (uint64_t)N),
+                                          (uint64_t)y.stride(0), Z.data_ptr<float>(), (uint64_t)N,
+                                          act ? 1 : 0, (float)p, (uint64_t)seed, (uint64_t)offset),
               "nts_hip_spmm_csc_fwd_linear");
-    ctx->save_for_backward({y, Wc});
+    ctx->save_for_backward({y, Wc, act ? Z : NtsVar()});
     ctx->saved_data["cs"] = cs_ptr;
+    ctx->saved_data["act"] = act;
+    ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
     return Z;
   }
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     auto saved = ctx->get_saved_variables();
     NtsVar y = saved[0], W = saved[1];
     auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    const bool act = ctx->saved_data["act"].toBool();
     NtsVar g = grads[0].contiguous();
     const int64_t M = y.size(0), K = y.size(1), N = W.size(1);
     NtsVar dW = torch::empty({K, N}, W.options());
-    hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)K, (int)N, (int)M, y.data_ptr<float>(),
-                               (uint64_t)K, g.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
-                               (uint64_t)N),
-              "nts_hip_gemm_f32(tn)");
-    return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar()};
+    if (act) {
+      NtsVar X = saved[2];
+      hip_check(nts_hip_gemm_tn_masked_f32(cs->ctx(), (int)K, (int)N, (int)M, y.data_ptr<float>(),
+                                           (uint64_t)y.stride(0), g.data_ptr<float>(), (uint64_t)N,
+                                           X.data_ptr<float>(), (uint64_t)N,
+                                           (float)ctx->saved_data["scale"].toDouble(),
+                                           dW.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_gemm_tn_masked_f32");
+    } else {
+      hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)K, (int)N, (int)M, y.data_ptr<float>(),
+                                 (uint64_t)y.stride(0), g.data_ptr<float>(), (uint64_t)N,
+                                 dW.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_gemm_f32(tn)");
+    }
+    return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
 // Output layer + loss in two fused kernels (nts_hip.h): the forward writes
@@ -669,17 +685,21 @@ NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
 }
 
 bool hip_agg_linear_supported(int64_t F, int64_t N) {
-  const int64_t half = (F + 1) / 2, Kh = (half + 1) / 2 * 2, LDP = 2 * Kh + 2;
-  // mirrors the argument checks of nts_hip_spmm_csc_fwd_linear for a
-  // contiguous, 16-byte aligned table (torch allocations are)
-  const int64_t vec = F % 4 == 0 ? 4 : (F % 2 == 0 ? 2 : 1);
-  return F >= 1 && N >= 1 && N <= 128 && 32 * LDP * 4 <= 160 * 1024 && (F / vec + 63) / 64 <= 8;
+  // mirrors the argument checks of nts_hip_spmm_csc_fwd_linear: the LDS tile
+  // pitch (F rounded up to 4, then to 2 mod 32) <= 640, N <= 128
+  const int64_t k4 = (F + 3) / 4 * 4, ldp = k4 + (2 + 32 - k4 % 32) % 32;
+  return F >= 1 && N >= 1 && N <= 128 && ldp <= 640;
 }
-
 NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg,
                       NtsStream* cs) {
   return HipAggLinearFn::apply(table, W, y, reinterpret_cast<int64_t>(sg),
-                               reinterpret_cast<int64_t>(cs));
+                               reinterpret_cast<int64_t>(cs), 0.0, (int64_t)0, (int64_t)0, false);
+}
+NtsVar hip_agg_linear_act(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg, double p,
+                          uint64_t seed, uint64_t offset, NtsStream* cs) {
+  return HipAggLinearFn::apply(table, W, y, reinterpret_cast<int64_t>(sg),
+                               reinterpret_cast<int64_t>(cs), p, (int64_t)seed, (int64_t)offset,
+                               true);
 }
 
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {

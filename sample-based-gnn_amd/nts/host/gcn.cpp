@@ -275,8 +275,13 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       // bottom graph op has no backward (core/ntsContext.hpp:443-444), so the
       // pair is recorded as one NN op whose input is the feature table
       sampCSC* s = sg->sampled_sgs[hop];
-      Y = torch::empty({(int64_t)s->v_size, F.size(1)}, F.options());
-      NtsVar Z = hip_agg_linear(F, P[0]->W, Y, s, cs.get());
+      Y = row_padded_empty((int64_t)s->v_size, F.size(1), graph->device);
+      const bool act = l < L - 1 && cfg.fuse_activation;  // hidden layer: dropout(relu)
+      const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
+      NtsVar Z = act ? hip_agg_linear_act(F, P[0]->W, Y, s, p,
+                                          (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1,
+                                          dropout_calls_++, cs.get())
+                     : hip_agg_linear(F, P[0]->W, Y, s, cs.get());
       if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
       const double Fd = (double)F.size(1);
       agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
@@ -287,6 +292,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       X = ctx.runVertexForward(
           [&](NtsVar&) {
             if (l == L - 1) return Z.log_softmax(1);
+            if (act) return Z;
             return torch::dropout(torch::relu(Z), cfg.drop_rate, ctx.is_train());
           },
           table);

@@ -328,6 +328,9 @@ NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* 
                       NtsStream* cs);
 // whether the fused kernel supports this shape (feature rows fit the LDS tile, out <= 128)
 bool hip_agg_linear_supported(int64_t feature_size, int64_t out_size);
+// ... and with vertexForward's dropout(relu(.)) fused (returns the activation)
+NtsVar hip_agg_linear_act(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg, double p,
+                          uint64_t seed, uint64_t offset, NtsStream* cs);
 
 struct Parameter {
   NtsVar W, M, V;

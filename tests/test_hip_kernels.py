@@ -375,10 +375,8 @@ def test_spmm_fwd_linear_fused(hip, cora, F, N, mapped):
     z = torch.full((v + 3, N), float("nan"), device=DEV)
     x = _t(table) if mapped else _t(X)
     rm = _t(l1["source"]) if mapped else None
-    half = (F + 1) // 2
-    Kh = (half + 1) // 2 * 2
-    vec = 4 if F % 4 == 0 else (2 if F % 2 == 0 else 1)
-    if 32 * (2 * Kh + 2) * 4 > 160 * 1024 or (F // vec + 63) // 64 > 8:
+    k4 = (F + 3) // 4 * 4
+    if k4 + (2 + 32 - k4 % 32) % 32 > 640:  # LDS tile of two blocks per CU
         with pytest.raises(RuntimeError):
             hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v + 3, x, W, z, y=y, row_map=rm)
         return
@@ -394,6 +392,16 @@ def test_spmm_fwd_linear_fused(hip, cora, F, N, mapped):
     hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v, x, W, z2, row_map=rm)
     torch.cuda.synchronize()
     assert torch.equal(z2, z[:v])
+    # relu + dropout epilogue: the mask of gemm_relu_dropout (same seed/offset keys)
+    p, seed, offset = 0.5, 0x1234_5678_9ABC, 5
+    za = torch.full((v, N), float("nan"), device=DEV)
+    hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v, x, W, za, row_map=rm, activation=True, p=p,
+                            seed=seed, offset=offset)
+    torch.cuda.synchronize()
+    keep = torch.from_numpy(_dropout_keep(v, N, p, seed, offset))
+    refa = torch.where(keep & (ref > 0), ref * 2.0, torch.zeros_like(ref))
+    near0 = ref.abs() < 1e-4 * F ** 0.5
+    torch.testing.assert_close(za.cpu().double()[~near0], refa[~near0], rtol=tol, atol=tol * 8)
 
 
 def _philox4x32_10(c, k):
