@@ -214,7 +214,8 @@ int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx *ctx, const uint32_t *column_offset,
                                 uint64_t ld_gin);
 
 /* ---- dense layer update (MFMA fp32) -------------------------------------- */
-/* Row-major fp32 GEMM on the matrix cores (v_mfma_f32_32x32x2_f32):
+/* Row-major fp32 GEMM on the matrix cores (v_mfma_f32_16x16x4_f32 /
+ * v_mfma_f32_32x32x2_f32, exact fp32 products, fp32 accumulate):
  *  trans_a == 0: C[M,N] = A[M,K] B[K,N]   — Parameter::forward x.matmul(W)
  *                (core/NtsScheduler.hpp:859-862)
  *  trans_a != 0: C[M,N] = A[K,M]^T B[K,N] — the weight gradient Y^T dZ that
@@ -258,6 +259,15 @@ int nts_hip_linear_xent_fwd(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int 
 int nts_hip_linear_xent_bwd(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int n, int K,
                             const float *W, int C, const int64_t *labels,
                             const float *grad_loss, float *dY, float *dW);
+
+/* Training call of the same layer: the loss AND its gradients dY, dW for an
+ * upstream gradient of exactly 1 (Loss followed by loss.backward(),
+ * toolkits/GCN_SAMPLE_ALLGPU.hpp:214-222 + core/ntsContext.hpp:436-440), in
+ * one pass over Y.  Bit-identical to nts_hip_linear_xent_fwd followed by
+ * nts_hip_linear_xent_bwd with *grad_loss == 1. */
+int nts_hip_linear_xent_train(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int n, int K,
+                              const float *W, int C, const int64_t *labels, float *loss,
+                              float *dY, float *dW);
 
 /* ---- optimiser ---------------------------------------------------------- */
 /* Fused Adam step on one parameter (n elements), element-wise identical to

@@ -60,7 +60,13 @@ constexpr int kUnroll = 4;
 
 // y[d, :] = sum_{e in [off[d], off[d+1])} w[e] * x[row(e), :]
 // row(e) = MAP ? map[idx[e]] : idx[e];  w == nullptr -> weight 1.
-template <int VEC, int LPD, int NCH, bool MAP>
+// Per destination the LPD-lane group loads up to LPD edges' (row, weight) at
+// once — one lane per edge, the map lookup included — and then fetches the
+// neighbour rows U at a time (row ids broadcast by __shfl, the tail batch
+// predicated), so a row costs off -> idx/map -> ceil(deg/U) row rounds of
+// memory latency instead of two dependent loads per U edges plus a serial
+// remainder.  The sum order is still the CSC edge order.
+template <int VEC, int LPD, int NCH, bool MAP, int U>
 __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
@@ -78,43 +84,37 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
       T acc[NCH];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
-      uint32_t e = beg;
-      for (; e + kUnroll <= end; e += kUnroll) {
-        uint32_t r[kUnroll];
-        float ww[kUnroll];
-#pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {  // streamed once: do not keep in cache
-          r[j] = __builtin_nontemporal_load(idx + e + j);
-          ww[j] = w ? __builtin_nontemporal_load(w + e + j) : 1.0f;
+      for (uint32_t cb = beg; cb < end; cb += LPD) {
+        const uint32_t ne = min(end - cb, (uint32_t)LPD);
+        uint32_t my_r = 0;
+        float my_w = 0.f;
+        if ((uint32_t)sl < ne) {  // streamed once: do not keep in cache
+          my_r = __builtin_nontemporal_load(idx + cb + sl);
+          my_w = w ? __builtin_nontemporal_load(w + cb + sl) : 1.0f;
+          if (MAP) my_r = map[my_r];
         }
-        if (MAP) {
+        for (uint32_t j0 = 0; j0 < ne; j0 += U) {
+          T xv[U][NCH];
+          float ww[U];
 #pragma unroll
-          for (int j = 0; j < kUnroll; ++j) r[j] = map[r[j]];
-        }
-        T xv[kUnroll][NCH];
+          for (int j = 0; j < U; ++j) {
+            const int src = (int)(j0 + j) & (LPD - 1);
+            const uint32_t r = (uint32_t)__shfl((int)my_r, src, LPD);
+            ww[j] = __shfl(my_w, src, LPD);
+            const bool ok = j0 + j < ne;
+            const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r * ldx);
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {
-          const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r[j] * ldx);
-#pragma unroll
-          for (int c = 0; c < NCH; ++c) {
-            const uint32_t col = c0 + sl + c * LPD;
-            xv[j][c] = (col < nv) ? xrow[col] : V::zero();
+            for (int c = 0; c < NCH; ++c) {
+              const uint32_t col = c0 + sl + c * LPD;
+              xv[j][c] = (ok && col < nv) ? xrow[col] : V::zero();
+            }
           }
-        }
 #pragma unroll
-        for (int j = 0; j < kUnroll; ++j)
+          for (int j = 0; j < U; ++j)
+            if (j0 + j < ne) {
 #pragma unroll
-          for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
-      }
-      for (; e < end; ++e) {
-        uint32_t r = idx[e];
-        const float we = w ? w[e] : 1.0f;
-        if (MAP) r = map[r];
-        const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r * ldx);
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const uint32_t col = c0 + sl + c * LPD;
-          if (col < nv) acc[c] = V::madd(acc[c], xrow[col], we);
+              for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
+            }
         }
       }
 #pragma unroll
@@ -234,14 +234,36 @@ static Shape pick_shape(uint32_t nv) {
   return {64, (int)std::min<uint32_t>(nch, 8)};
 }
 
+static int gather_u_env() {
+  static const int u = [] {
+    const char* e = getenv("NTS_GATHER_U");
+    return e ? atoi(e) : 0;
+  }();
+  return u;
+}
+constexpr int gather_u(int floats_per_lane) {
+  return floats_per_lane <= 4 ? 8 : 4;
+}
+
 template <int VEC, bool MAP>
 static int launch_gather_vec(hipStream_t st, uint32_t grid, Shape s, const uint32_t* off,
                              const uint32_t* idx, const float* w, const uint32_t* n_dev,
                              uint32_t n_cap, const float* x, uint64_t ldx, const uint32_t* map,
                              uint32_t nv, float* y, uint64_t ldy) {
-#define NTS_G(LPD, NCH)                                                                    \
-  hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP>), dim3(grid), dim3(kAggThreads), 0, \
-                     st, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy)
+// rows in flight per lane group: 8 for narrow rows, else 4 (register budget;
+// NTS_GATHER_U=5 selects 5 for the mid-width rows, e.g. F ~ 600 at fanout 10)
+#define NTS_G(LPD, NCH)                                                                     \
+  do {                                                                                      \
+    constexpr int u = gather_u(VEC * NCH);                                                  \
+    if (u == 4 && VEC * NCH <= 12 && gather_u_env() == 5)                                   \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 5>), dim3(grid),               \
+                         dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
+                         nv, y, ldy);                                                       \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u>), dim3(grid),               \
+                         dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
+                         nv, y, ldy);                                                       \
+  } while (0)
   if (s.lpd == 8) NTS_G(8, 1);
   else if (s.lpd == 16) NTS_G(16, 1);
   else if (s.lpd == 32) NTS_G(32, 1);

@@ -8,12 +8,13 @@
 //   NN, W slice fits LDS (K <= 608): k_gemm_wres — the weight's column slice
 //       stays resident in LDS for the whole launch, A rows stream straight to
 //       registers, no barrier in the main loop (see its comment).
-//   NN otherwise, and TN: k_gemm — block 64 rows x 128 cols, 4 waves of
-//       32 x 64 on v_mfma_f32_32x32x2_f32, A and B k-slices staged in LDS
-//       (double buffered, register prefetch two steps deep).
-//   TN: C = A^T B with the long reduction split over blocks; the partial
-//       tiles are summed by a second kernel in a fixed tree order
-//       (deterministic, no atomics).
+//   TN with M >= 320, N % 128 == 0: k_gemm_tn_big — a 640 x 128 output tile
+//       per block in accumulators, k-chunks split over blocks.
+//   otherwise: k_gemm — block 64 rows x 128 cols, 4 waves of 32 x 64 on
+//       v_mfma_f32_32x32x2_f32, A and B k-slices staged in LDS (double
+//       buffered, register prefetch two steps deep).
+//   Split reductions: partial tiles summed by k_sum_splits_tree in a fixed
+//       tree order (deterministic, no atomics).
 #include "common.hpp"
 
 #include <type_traits>
@@ -738,6 +739,13 @@ __global__ __launch_bounds__(256) void k_sum_splits_tree(const float* __restrict
   if constexpr (VEC == 4) acc = make_float4(0.f, 0.f, 0.f, 0.f); else acc = 0.f;
   if (e < total) {
     int z = s;
+    for (; z + 112 < splits; z += 128) {  // 8 loads in flight, summed in order
+      T v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(uint64_t)(z + 16 * u) * st + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) add(acc, v[u]);
+    }
     for (; z + 48 < splits; z += 64) {
       T v[4];
 #pragma unroll

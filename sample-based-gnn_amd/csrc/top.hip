@@ -7,18 +7,24 @@
 // ~idempotent but kept: same arithmetic as the reference), the mean negative
 // log-likelihood of the target class, and libtorch's backward of all of it.
 // On the GPU drivers that is ~12 tiny kernels per step (GEMM, 2 softmax, NLL,
-// fills, their backwards, dW and dY GEMMs).  Here: one forward kernel and one
-// backward kernel plus fixed-order reductions of their partials
-// (deterministic, no atomics).
+// fills, their backwards, dW and dY GEMMs).  Here one kernel template:
+//   LOSS: the loss (block partials, summed by the last block to finish in a
+//         fixed order — a ticket counter in the context, no extra launch);
+//   GRAD: dY and per-wave dW partials for the upstream gradient (*grad, or
+//         exactly 1 for the training call), summed by sum_splits.
+// forward = <LOSS>, backward = <GRAD>, train = <LOSS, GRAD> (bit-identical
+// to forward + backward with grad 1: same code, same orders).
 //
-// One wave owns 16 rows.  The three products run on v_mfma_f32_16x16x4_f32
-// (exact fp32 products, fp32 accumulation):
+// One wave owns 16 rows.  Its Y tile is staged into LDS with coalesced
+// 16-byte loads (all issued up front), then the three products run on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation):
 //   Z  [16 x Cp] = Y [16 x K] W [K x Cp]      (Cp = C rounded up to 16, <= 64)
 //   dY [16 x K]  = dZ [16 x Cp] W^T            (dZ staged through LDS)
 //   dW_part [K x Cp] = Y^T [K x 16] dZ [16 x Cp]  (one slab per wave)
 // W lives in LDS (zero-padded to Cp columns).  In the accumulator layout a lane
 // (i, g) holds Z[4g + v][16 ct + i]; row-wise softmax reductions run over the
-// 16 lanes of a group g (xor shuffles 1..8).
+// 16 lanes of a group g (xor shuffles 1..8).  Y tile pitch K + 4: the logits'
+// A reads (row i, k0 + g) hit 64 distinct banks.
 // Layout: Y [n x K] (ld ldy), W [K x C] row-major, labels int64 [n].
 #include "common.hpp"
 
@@ -35,10 +41,13 @@ struct TopArgs {
   uint64_t ldy;
   const float* W;
   const int64_t* labels;
-  const float* grad;  // backward: d loss (device scalar)
-  int n, K, C, Cp;
-  float* part;        // forward: [blocks] loss partials; backward: [waves][K*C] dW partials
-  float* dY;          // backward: [n x K]
+  const float* grad;  // GRAD: d loss (device scalar); nullptr = exactly 1
+  int n, K, C;
+  float* lpart;       // LOSS: [blocks] loss partials
+  float* loss;        // LOSS: the scalar
+  uint32_t* ticket;   // LOSS: zero between launches
+  float* part;        // GRAD: [waves][K*C] dW partials
+  float* dY;          // GRAD: [n x K]
 };
 
 __device__ __forceinline__ float grp_max(float v) {  // over the 16 lanes of a group
@@ -53,29 +62,71 @@ __device__ __forceinline__ float grp_sum(float v) {
 }
 
 // Stage W into LDS as sW[k][Cp] (zero columns >= C).
+template <int CP>
 __device__ __forceinline__ void stage_w(const TopArgs& a, float* sW) {
-  for (int e = threadIdx.x; e < a.K * a.Cp; e += kTopThreads) {
-    const int k = e / a.Cp, c = e % a.Cp;
+  for (int e = threadIdx.x; e < a.K * CP; e += kTopThreads) {
+    const int k = e / CP, c = e % CP;
     sW[e] = c < a.C ? a.W[(uint64_t)k * a.C + c] : 0.f;
   }
-  __syncthreads();
+}
+
+// Stage this wave's 16 Y rows into sY[16][K + 4] (rows >= n are zero).
+// VEC4: 16-byte loads (ldy % 4 == 0, Y 16-byte aligned).
+template <bool VEC4>
+__device__ __forceinline__ void stage_y(const TopArgs& a, float* sY, int r0, int lane) {
+  const int K = a.K, P = K + 4;
+  constexpr int B = 8;  // loads in flight per lane
+  if (VEC4) {
+    const int kq = K / 4, it = K / 16;  // float4 per row; per lane (16 rows x kq / 64)
+    for (int j0 = 0; j0 < it; j0 += B) {
+      float4 v[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int q = lane + kWave * (j0 + u), rr = q / kq, r = r0 + rr;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j0 + u < it && r < a.n)
+          v[u] = *reinterpret_cast<const float4*>(a.Y + (uint64_t)r * a.ldy + 4 * (q % kq));
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int q = lane + kWave * (j0 + u);
+        if (j0 + u < it) *reinterpret_cast<float4*>(sY + (q / kq) * P + 4 * (q % kq)) = v[u];
+      }
+    }
+  } else {
+    const int it = K / 4;  // 16 rows x K / 64 per lane
+    for (int j0 = 0; j0 < it; j0 += B) {
+      float v[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int q = lane + kWave * (j0 + u), r = r0 + q / K;
+        v[u] = (j0 + u < it && r < a.n) ? a.Y[(uint64_t)r * a.ldy + q % K] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int q = lane + kWave * (j0 + u);
+        if (j0 + u < it) sY[(q / K) * P + q % K] = v[u];
+      }
+    }
+  }
 }
 
 // Z tile of this wave's 16 rows: z[ct][v] = Z[r0 + 4g + v][16 ct + i].
 template <int NCT>
-__device__ __forceinline__ void wave_logits(const TopArgs& a, const float* sW, int r0, int i,
-                                            int g, f32x4 (&z)[NCT]) {
+__device__ __forceinline__ void wave_logits(int K, const float* sW, const float* sY, int i, int g,
+                                            f32x4 (&z)[NCT]) {
+  constexpr int CP = 16 * NCT;
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) z[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int row = min(r0 + i, a.n - 1);  // rows past n compute garbage, never stored
-  const float* yr = a.Y + (uint64_t)row * a.ldy;
-  for (int k0 = 0; k0 < a.K; k0 += 4) {
-    const int k = k0 + g;
-    const float av = k < a.K ? yr[k] : 0.f;
+  const float* yr = sY + i * (K + 4);
+  for (int k1 = 0; k1 < K; k1 += 16) {  // K % 16 == 0
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-      const float bv = k < a.K ? sW[k * a.Cp + 16 * ct + i] : 0.f;
-      z[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, z[ct], 0, 0, 0);
+    for (int k0 = k1; k0 < k1 + 16; k0 += 4) {
+      const float av = yr[k0 + g];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        z[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW[(k0 + g) * CP + 16 * ct + i], z[ct],
+                                                     0, 0, 0);
     }
   }
 }
@@ -116,165 +167,167 @@ __device__ __forceinline__ void log_softmax2(const f32x4 (&z)[NCT], int C, int i
   }
 }
 
-template <int NCT>
-__global__ __launch_bounds__(kTopThreads) void k_top_xent_fwd(TopArgs a) {
+static inline size_t top_lds(int K, int Cp) {
+  return ((size_t)K * Cp + (size_t)kTopWaves * 16 * (K + 4) + (size_t)kTopRows * Cp) *
+         sizeof(float);
+}
+
+template <int NCT, bool LOSS, bool GRAD, bool VEC4>
+__global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
+  constexpr int CP = 16 * NCT;
   extern __shared__ float smem[];
-  float* sW = smem;
   __shared__ float wl[kTopWaves];
-  stage_w(a, sW);
+  __shared__ uint32_t last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
+  const int K = a.K;
+  float* sW = smem;                                      // [K][CP]
+  float* sY = smem + K * CP + w * 16 * (K + 4);          // this wave's [16][K + 4]
+  float* dz = smem + K * CP + kTopWaves * 16 * (K + 4) + w * 16 * CP;  // [16][CP]
   const int r0 = blockIdx.x * kTopRows + w * kTopRowsPerWave;
+  stage_y<VEC4>(a, sY, r0, lane);
+  stage_w<CP>(a, sW);
+  __syncthreads();
   f32x4 z[NCT];
-  wave_logits<NCT>(a, sW, r0, i, g, z);
+  wave_logits<NCT>(K, sW, sY, i, g, z);
   float lp[NCT][4], lp2[NCT][4];
   log_softmax2<NCT>(z, a.C, i, lp, lp2);
-  // -lp2[target] of each valid row, summed in a fixed order (v, then groups)
-  float l = 0.f;
+  int tgt[4];
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int r = r0 + 4 * g + v;
-    const int t = r < a.n ? (int)a.labels[r] : -1;
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct)
-      if (16 * ct + i == t) l -= lp2[ct][v];
+    tgt[v] = r < a.n ? (int)a.labels[r] : -1;
   }
-  // lane-order reduction over the wave (deterministic)
+  if (LOSS) {
+    // -lp2[target] of each valid row, summed in a fixed order (v, then lanes)
+    float l = 0.f;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, kWave);
-  if (lane == 0) wl[w] = l;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int q = 0; q < kTopWaves; ++q) s += wl[q];
-    a.part[blockIdx.x] = s;
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (16 * ct + i == tgt[v]) l -= lp2[ct][v];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, kWave);
+    if (lane == 0) wl[w] = l;
   }
-}
-
-// loss = (sum of block partials) / n, fixed tree
-__global__ void k_top_loss_reduce(const float* part, int nblk, int n, float* loss) {
-  __shared__ float red[256];
-  float s = 0.f;
-  for (int b = threadIdx.x; b < nblk; b += 256) s += part[b];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = 128; w >= 1; w >>= 1) {
-    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *loss = red[0] / (float)n;
-}
-
-template <int NCT>
-__global__ __launch_bounds__(kTopThreads) void k_top_xent_bwd(TopArgs a) {
-  extern __shared__ float smem[];
-  float* sW = smem;                               // [K][Cp]
-  float* sD = smem + a.K * a.Cp;                  // [waves][16][Cp]: dZ rows of each wave
-  stage_w(a, sW);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int r0 = blockIdx.x * kTopRows + w * kTopRowsPerWave;
-  float* dz = sD + w * kTopRowsPerWave * a.Cp;
-  f32x4 z[NCT];
-  wave_logits<NCT>(a, sW, r0, i, g, z);
-  float lp[NCT][4], lp2[NCT][4];
-  log_softmax2<NCT>(z, a.C, i, lp, lp2);
-  const float gl = *a.grad / (float)a.n;
-  // nll backward, then y = log_softmax(x): dx = dy - exp(y) * sum(dy), twice
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int r = r0 + 4 * g + v;
-    const int t = r < a.n ? (int)a.labels[r] : -1;
-    float d2[NCT], s2 = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-      d2[ct] = (16 * ct + i == t) ? -gl : 0.f;
-      s2 += d2[ct];
-    }
-    s2 = grp_sum(s2);
-    float d1[NCT], s1 = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-      const bool on = 16 * ct + i < a.C;
-      d1[ct] = on ? d2[ct] - expf(lp2[ct][v]) * s2 : 0.f;
-      s1 += d1[ct];
-    }
-    s1 = grp_sum(s1);
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
-      const bool on = 16 * ct + i < a.C && r < a.n;
-      dz[(4 * g + v) * a.Cp + 16 * ct + i] = on ? d1[ct] - expf(lp[ct][v]) * s1 : 0.f;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's dZ stores landed
-  __builtin_amdgcn_wave_barrier();
-  // dY [16 x K] = dZ [16 x Cp] W^T: A lane (i,g) = dZ[i][c], B = W[k = 16 kt + i][c]
-  for (int kt = 0; kt < a.K / 16; ++kt) {
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c0 = 0; c0 < 16 * NCT; c0 += 4) {
-      const float av = dz[i * a.Cp + c0 + g];
-      const float bv = sW[(16 * kt + i) * a.Cp + c0 + g];
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
-    }
+  if (GRAD) {
+    const float gl = (a.grad ? *a.grad : 1.0f) / (float)a.n;
+    // nll backward, then y = log_softmax(x): dx = dy - exp(y) * sum(dy), twice
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int r = r0 + 4 * g + v;
-      if (r < a.n) a.dY[(uint64_t)r * a.K + 16 * kt + i] = acc[v];
+      float d2[NCT], s2 = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        d2[ct] = (16 * ct + i == tgt[v]) ? -gl : 0.f;
+        s2 += d2[ct];
+      }
+      s2 = grp_sum(s2);
+      float d1[NCT], s1 = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const bool on = 16 * ct + i < a.C;
+        d1[ct] = on ? d2[ct] - expf(lp2[ct][v]) * s2 : 0.f;
+        s1 += d1[ct];
+      }
+      s1 = grp_sum(s1);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const bool on = 16 * ct + i < a.C && r < a.n;
+        dz[(4 * g + v) * CP + 16 * ct + i] = on ? d1[ct] - expf(lp[ct][v]) * s1 : 0.f;
+      }
     }
-  }
-  // dW partial [K x Cp] = Y^T [K x 16] dZ [16 x Cp]:
-  //   A lane (i,g) = Y[r0 + 4s + g][16 kt + i], B = dZ[4s + g][16 ct + i]
-  float* pw = a.part + ((uint64_t)blockIdx.x * kTopWaves + w) * a.K * a.C;
-  for (int kt = 0; kt < a.K / 16; ++kt) {
-    f32x4 acc[NCT];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's dZ stores landed
+    __builtin_amdgcn_wave_barrier();
+    // dY [16 x K] = dZ [16 x CP] W^T: A lane (i,g) = dZ[i][c], B = W[k = 16 kt + i][c]
+    for (int kt = 0; kt < K / 16; ++kt) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int r = r0 + 4 * s + g;
-      const float av = r < a.n ? a.Y[(uint64_t)r * a.ldy + 16 * kt + i] : 0.f;
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
-        acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dz[(4 * s + g) * a.Cp + 16 * ct + i],
-                                                       acc[ct], 0, 0, 0);
-    }
-    // acc[ct][v] = dW[16 kt + 4 g + v][16 ct + i]
-#pragma unroll
-    for (int ct = 0; ct < NCT; ++ct)
+      for (int c0 = 0; c0 < CP; c0 += 4)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[i * CP + c0 + g],
+                                                   sW[(16 * kt + i) * CP + c0 + g], acc, 0, 0, 0);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const int c = 16 * ct + i;
-        if (c < a.C) pw[(uint64_t)(16 * kt + 4 * g + v) * a.C + c] = acc[ct][v];
+        const int r = r0 + 4 * g + v;
+        if (r < a.n) a.dY[(uint64_t)r * K + 16 * kt + i] = acc[v];
       }
+    }
+    // dW partial [K x CP] = Y^T [K x 16] dZ [16 x CP]:
+    //   A lane (i,g) = Y[r0 + 4s + g][16 kt + i], B = dZ[4s + g][16 ct + i]
+    float* pw = a.part + ((uint64_t)blockIdx.x * kTopWaves + w) * K * a.C;
+    for (int kt = 0; kt < K / 16; ++kt) {
+      f32x4 acc[NCT];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float av = sY[(4 * s + g) * (K + 4) + 16 * kt + i];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dz[(4 * s + g) * CP + 16 * ct + i],
+                                                         acc[ct], 0, 0, 0);
+      }
+      // acc[ct][v] = dW[16 kt + 4 g + v][16 ct + i]
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int c = 16 * ct + i;
+          if (c < a.C) pw[(uint64_t)(16 * kt + 4 * g + v) * a.C + c] = acc[ct][v];
+        }
+    }
+  }
+  if (LOSS) {
+    // block partial; the last block to finish sums all partials in index
+    // order (the same order whichever block is last) and resets the ticket
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+      for (int q = 0; q < kTopWaves; ++q) s += wl[q];
+      a.lpart[blockIdx.x] = s;
+      __threadfence();
+      last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && w == 0) {
+      __threadfence();
+      float s = 0.f;
+      for (uint32_t b = lane; b < gridDim.x; b += kWave)
+        s += __builtin_nontemporal_load(a.lpart + b);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, kWave);
+      if (lane == 0) {
+        *a.loss = s / (float)a.n;
+        *a.ticket = 0u;
+      }
+    }
   }
 }
 
-static size_t top_lds(int K, int Cp, bool bwd) {
-  return ((size_t)K * Cp + (bwd ? (size_t)kTopRows * Cp : 0)) * sizeof(float);
-}
-
-template <int NCT>
-static int launch_top(hipStream_t st, bool bwd, int nblk, size_t lds, const TopArgs& a) {
-  if (bwd) {
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_top_xent_bwd<NCT>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_top_xent_bwd<NCT>, dim3(nblk), dim3(kTopThreads), lds, st, a);
-  } else {
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_top_xent_fwd<NCT>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(k_top_xent_fwd<NCT>, dim3(nblk), dim3(kTopThreads), lds, st, a);
-  }
+template <int NCT, bool LOSS, bool GRAD>
+static int launch_top(hipStream_t st, int nblk, const TopArgs& a) {
+  const size_t lds = top_lds(a.K, 16 * NCT);
+  const bool v4 = a.ldy % 4 == 0 && (uintptr_t)a.Y % 16 == 0;
+  const void* f = v4 ? reinterpret_cast<const void*>(&k_top_xent<NCT, LOSS, GRAD, true>)
+                     : reinterpret_cast<const void*>(&k_top_xent<NCT, LOSS, GRAD, false>);
+  NTS_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (v4)
+    hipLaunchKernelGGL((k_top_xent<NCT, LOSS, GRAD, true>), dim3(nblk), dim3(kTopThreads), lds,
+                       st, a);
+  else
+    hipLaunchKernelGGL((k_top_xent<NCT, LOSS, GRAD, false>), dim3(nblk), dim3(kTopThreads), lds,
+                       st, a);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }
 
-static int launch_top_any(hipStream_t st, bool bwd, int nblk, size_t lds, const TopArgs& a) {
-  switch (a.Cp / 16) {
-    case 1: return launch_top<1>(st, bwd, nblk, lds, a);
-    case 2: return launch_top<2>(st, bwd, nblk, lds, a);
-    case 3: return launch_top<3>(st, bwd, nblk, lds, a);
-    default: return launch_top<4>(st, bwd, nblk, lds, a);
+template <bool LOSS, bool GRAD>
+static int launch_top_any(hipStream_t st, int nblk, int Cp, const TopArgs& a) {
+  switch (Cp / 16) {
+    case 1: return launch_top<1, LOSS, GRAD>(st, nblk, a);
+    case 2: return launch_top<2, LOSS, GRAD>(st, nblk, a);
+    case 3: return launch_top<3, LOSS, GRAD>(st, nblk, a);
+    default: return launch_top<4, LOSS, GRAD>(st, nblk, a);
   }
 }
 
@@ -284,43 +337,54 @@ using namespace nts_hip;
 
 extern "C" {
 
-int nts_hip_linear_xent_fwd(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
-                            const float* W, int C, const int64_t* labels, float* loss) {
-  NTS_CHECK_ARG(ctx && Y && W && labels && loss, "NULL argument");
+static int top_check(nts_hip_ctx* ctx, int n, int K, int C, uint64_t ldy) {
   NTS_CHECK_ARG(n > 0 && K > 0 && C > 0 && ldy >= (uint64_t)K, "shape");
   NTS_CHECK_ARG(C <= kWave, "class count above 64 is not supported by the fused loss");
   NTS_CHECK_ARG(K % 16 == 0, "the fused loss needs K % 16 == 0");
-  const int Cp = (C + 15) / 16 * 16;
-  const size_t lds = top_lds(K, Cp, true);
-  NTS_CHECK_ARG(lds <= 160 * 1024, "K x C too large for the fused loss");
+  NTS_CHECK_ARG(top_lds(K, (C + 15) / 16 * 16) <= 160 * 1024, "K x C too large for the fused loss");
   NTS_HIP_TRY(hipSetDevice(ctx->device));
-  const int nblk = (n + kTopRows - 1) / kTopRows;
-  NTS_RET(ensure_scratch(ctx, (size_t)nblk * sizeof(float) + 256));
-  TopArgs a{Y, ldy, W, labels, nullptr, n, K, C, Cp, (float*)ctx->scratch, nullptr};
-  NTS_RET(launch_top_any(ctx->stream, false, nblk, top_lds(K, Cp, false), a));
-  hipLaunchKernelGGL(k_top_loss_reduce, dim3(1), dim3(256), 0, ctx->stream, a.part, nblk, n, loss);
-  NTS_LAUNCH_CHECK();
   return NTS_OK;
+}
+
+// scratch: [loss partials, 64-float aligned][dW partial slabs]
+static int top_run(nts_hip_ctx* ctx, bool loss_on, bool grad_on, const float* Y, uint64_t ldy,
+                   int n, int K, const float* W, int C, const int64_t* labels,
+                   const float* grad_loss, float* loss, float* dY, float* dW) {
+  NTS_RET(top_check(ctx, n, K, C, ldy));
+  const int Cp = (C + 15) / 16 * 16;
+  const int nblk = (n + kTopRows - 1) / kTopRows;
+  const uint64_t slab = (uint64_t)K * C;
+  const int nslab = nblk * kTopWaves;
+  const size_t lp = ((size_t)nblk + 63) / 64 * 64;
+  NTS_RET(ensure_scratch(ctx, (lp + (grad_on ? (size_t)nslab * slab : 0)) * sizeof(float)));
+  float* base = (float*)ctx->scratch;
+  TopArgs a{Y, ldy, W, labels, grad_loss, n, K, C, base, loss, ctx->ticket, base + lp, dY};
+  hipStream_t st = ctx->stream;
+  if (loss_on && grad_on) NTS_RET((launch_top_any<true, true>(st, nblk, Cp, a)));
+  else if (loss_on) NTS_RET((launch_top_any<true, false>(st, nblk, Cp, a)));
+  else NTS_RET((launch_top_any<false, true>(st, nblk, Cp, a)));
+  if (grad_on) return sum_splits(st, a.part, nslab, slab, K, C, dW, (uint64_t)C);
+  return NTS_OK;
+}
+
+int nts_hip_linear_xent_fwd(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
+                            const float* W, int C, const int64_t* labels, float* loss) {
+  NTS_CHECK_ARG(ctx && Y && W && labels && loss, "NULL argument");
+  return top_run(ctx, true, false, Y, ldy, n, K, W, C, labels, nullptr, loss, nullptr, nullptr);
 }
 
 int nts_hip_linear_xent_bwd(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
                             const float* W, int C, const int64_t* labels, const float* grad_loss,
                             float* dY, float* dW) {
   NTS_CHECK_ARG(ctx && Y && W && labels && grad_loss && dY && dW, "NULL argument");
-  NTS_CHECK_ARG(n > 0 && K > 0 && C > 0 && ldy >= (uint64_t)K, "shape");
-  NTS_CHECK_ARG(C <= kWave, "class count above 64 is not supported by the fused loss");
-  NTS_CHECK_ARG(K % 16 == 0, "the fused loss needs K % 16 == 0");
-  const int Cp = (C + 15) / 16 * 16;
-  const size_t lds = top_lds(K, Cp, true);
-  NTS_CHECK_ARG(lds <= 160 * 1024, "K x C too large for the fused loss");
-  NTS_HIP_TRY(hipSetDevice(ctx->device));
-  const int nblk = (n + kTopRows - 1) / kTopRows;
-  const uint64_t slab = (uint64_t)K * C;
-  const int nslab = nblk * kTopWaves;
-  NTS_RET(ensure_scratch(ctx, (size_t)nslab * slab * sizeof(float) + 256));
-  TopArgs a{Y, ldy, W, labels, grad_loss, n, K, C, Cp, (float*)ctx->scratch, dY};
-  NTS_RET(launch_top_any(ctx->stream, true, nblk, lds, a));
-  return sum_splits(ctx->stream, a.part, nslab, slab, K, C, dW, (uint64_t)C);
+  return top_run(ctx, false, true, Y, ldy, n, K, W, C, labels, grad_loss, nullptr, dY, dW);
+}
+
+int nts_hip_linear_xent_train(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
+                              const float* W, int C, const int64_t* labels, float* loss,
+                              float* dY, float* dW) {
+  NTS_CHECK_ARG(ctx && Y && W && labels && loss && dY && dW, "NULL argument");
+  return top_run(ctx, true, true, Y, ldy, n, K, W, C, labels, nullptr, loss, dY, dW);
 }
 
 }  // extern "C"

@@ -150,6 +150,13 @@ class HipContext:
         check(self.lib.nts_hip_linear_xent_bwd(self.h, ptr(Y), Y.stride(0), n, K, ptr(W), W.shape[1],
                                                ptr(labels), ptr(grad_loss), ptr(dY), ptr(dW)))
 
+    def linear_xent_train(self, Y, W, labels, loss, dY, dW):
+        """The loss and its gradients for d loss = 1 in one pass (== fwd + bwd(1))."""
+        n, K = Y.shape
+        check(self.lib.nts_hip_linear_xent_train(self.h, ptr(Y), Y.stride(0), n, K, ptr(W),
+                                                 W.shape[1], ptr(labels), ptr(loss), ptr(dY),
+                                                 ptr(dW)))
+
     def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
         check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,
                                     beta1, beta2, eps, wd, beta1_t, beta2_t, int(bias_correction)))

@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 
 #include "nts_host.hpp"
@@ -416,6 +418,18 @@ NtsVar SingleGPUSampleGraphOp::backward(NtsVar& g) {
 }  // namespace op
 
 // ---------------------------------------------------------------------------
+// A persistent fp32 scalar 1 per device: the seed gradient of a scalar loss.
+// Kernels that precompute their backward for d loss = 1 recognise it by
+// identity (HipLinearXentFn); no fill kernel per step.
+const NtsVar& unit_scalar(const torch::Device& dev) {
+  static std::mutex mu;
+  static std::map<std::string, NtsVar> units;
+  std::lock_guard<std::mutex> lk(mu);
+  NtsVar& u = units[dev.str()];
+  if (!u.defined()) u = torch::ones({}, torch::TensorOptions().dtype(torch::kFloat32).device(dev));
+  return u;
+}
+
 namespace ctx {
 
 NtsContext::NtsContext() {}
@@ -469,7 +483,9 @@ void NtsContext::pop_one_op() {
 void NtsContext::self_backward(bool retain_graph) {
   TORCH_CHECK(training && count > 0, "self_backward outside training");
   Entry& top = ops_.back();
-  top.output.backward(torch::ones_like(top.output), {}, retain_graph);
+  const bool unit = top.output.dim() == 0 && top.output.scalar_type() == torch::kFloat32;
+  top.output.backward(unit ? unit_scalar(top.output.device()) : torch::ones_like(top.output), {},
+                      retain_graph);
   if (count >= 2) ops_[count - 2].output_grad = top.input.grad();
   pop_one_op();
   while (count > 1 || (count == 1 && ops_.back().type == NNOP)) {
@@ -642,20 +658,35 @@ struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
     return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
-// Output layer + loss in two fused kernels (nts_hip.h): the forward writes
-// the scalar loss, the backward dY and dW for the upstream gradient.
+// Output layer + loss in fused kernels (nts_hip.h).  Under grad mode the
+// forward runs the training kernel: loss, dY and dW for d loss = 1 in one pass
+// over Y; the backward returns them when the upstream gradient is the unit
+// seed of self_backward (exactly 1), and otherwise runs the backward kernel.
 struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
-  static NtsVar forward(AutogradContext* ctx, NtsVar y, NtsVar W, NtsVar target, int64_t cs_ptr) {
+  static NtsVar forward(AutogradContext* ctx, NtsVar y, NtsVar W, NtsVar target, int64_t cs_ptr,
+                        bool train) {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     NtsVar yc = row_major(y), Wc = W.contiguous(), tc = target.contiguous();
     const int64_t n = yc.size(0), K = yc.size(1), C = Wc.size(1);
     TORCH_CHECK(Wc.size(0) == K && tc.numel() == n && tc.scalar_type() == torch::kInt64,
                 "hip_linear_xent: shape mismatch");
     NtsVar loss = torch::empty({}, yc.options());
-    hip_check(nts_hip_linear_xent_fwd(cs->ctx(), yc.data_ptr<float>(), (uint64_t)yc.stride(0),
-                                      (int)n, (int)K, Wc.data_ptr<float>(), (int)C,
-                                      tc.data_ptr<int64_t>(), loss.data_ptr<float>()),
-              "nts_hip_linear_xent_fwd");
+    if (train) {
+      NtsVar dY = torch::empty({n, K}, yc.options());
+      NtsVar dW = torch::empty({K, C}, Wc.options());
+      hip_check(nts_hip_linear_xent_train(cs->ctx(), yc.data_ptr<float>(), (uint64_t)yc.stride(0),
+                                          (int)n, (int)K, Wc.data_ptr<float>(), (int)C,
+                                          tc.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                          dY.data_ptr<float>(), dW.data_ptr<float>()),
+                "nts_hip_linear_xent_train");
+      ctx->saved_data["dY"] = dY;
+      ctx->saved_data["dW"] = dW;
+    } else {
+      hip_check(nts_hip_linear_xent_fwd(cs->ctx(), yc.data_ptr<float>(), (uint64_t)yc.stride(0),
+                                        (int)n, (int)K, Wc.data_ptr<float>(), (int)C,
+                                        tc.data_ptr<int64_t>(), loss.data_ptr<float>()),
+                "nts_hip_linear_xent_fwd");
+    }
     ctx->save_for_backward({yc, Wc, tc});
     ctx->saved_data["cs"] = cs_ptr;
     return loss;
@@ -664,16 +695,26 @@ struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
     auto saved = ctx->get_saved_variables();
     NtsVar y = saved[0], W = saved[1], t = saved[2];
     auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
-    NtsVar g = grads[0].contiguous();
-    const int64_t n = y.size(0), K = y.size(1), C = W.size(1);
-    NtsVar dY = torch::empty({n, K}, y.options());
-    NtsVar dW = torch::empty({K, C}, W.options());
-    hip_check(nts_hip_linear_xent_bwd(cs->ctx(), y.data_ptr<float>(), (uint64_t)y.stride(0),
-                                      (int)n, (int)K, W.data_ptr<float>(), (int)C,
-                                      t.data_ptr<int64_t>(), g.data_ptr<float>(),
-                                      dY.data_ptr<float>(), dW.data_ptr<float>()),
-              "nts_hip_linear_xent_bwd");
-    return {ctx->needs_input_grad(0) ? dY : NtsVar(), dW, NtsVar(), NtsVar()};
+    NtsVar g = grads[0];
+    NtsVar dY, dW;
+    if (ctx->saved_data.count("dY") &&
+        g.data_ptr() == unit_scalar(g.device()).data_ptr()) {  // d loss == 1: precomputed
+      dY = ctx->saved_data["dY"].toTensor();
+      dW = ctx->saved_data["dW"].toTensor();
+    } else {
+      g = g.contiguous();
+      const int64_t n = y.size(0), K = y.size(1), C = W.size(1);
+      dY = torch::empty({n, K}, y.options());
+      dW = torch::empty({K, C}, W.options());
+      hip_check(nts_hip_linear_xent_bwd(cs->ctx(), y.data_ptr<float>(), (uint64_t)y.stride(0),
+                                        (int)n, (int)K, W.data_ptr<float>(), (int)C,
+                                        t.data_ptr<int64_t>(), g.data_ptr<float>(),
+                                        dY.data_ptr<float>(), dW.data_ptr<float>()),
+                "nts_hip_linear_xent_bwd");
+    }
+    ctx->saved_data.erase("dY");
+    ctx->saved_data.erase("dW");
+    return {ctx->needs_input_grad(0) ? dY : NtsVar(), dW, NtsVar(), NtsVar(), NtsVar()};
   }
 };
 }  // namespace
@@ -708,13 +749,16 @@ NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {
 
 bool hip_linear_xent_supported(int64_t K, int64_t C) {
   // mirrors the argument checks of nts_hip_linear_xent_fwd/bwd (C <= 64,
-  // K % 16 == 0, W and 64 dZ rows in LDS)
+  // K % 16 == 0, W, 64 Y rows and 64 dZ rows in LDS)
   const int64_t Cp = (C + 15) / 16 * 16;
-  return K >= 16 && K % 16 == 0 && C >= 1 && C <= 64 && (K * Cp + 64 * Cp) * 4 <= 160 * 1024;
+  return K >= 16 && K % 16 == 0 && C >= 1 && C <= 64 &&
+         (K * Cp + 64 * (K + 4) + 64 * Cp) * 4 <= 160 * 1024;
 }
 
 NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs) {
-  return HipLinearXentFn::apply(y, W, target, reinterpret_cast<int64_t>(cs));
+  // a backward follows only under grad mode with an input requiring grad
+  const bool train = torch::GradMode::is_enabled() && (y.requires_grad() || W.requires_grad());
+  return HipLinearXentFn::apply(y, W, target, reinterpret_cast<int64_t>(cs), train);
 }
 
 // ---------------------------------------------------------------------------

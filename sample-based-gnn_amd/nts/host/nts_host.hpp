@@ -309,6 +309,8 @@ NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
 std::vector<uint32_t> cu_mask_spread(int device, int n, bool complement);
 // training output layer + loss: nll_loss(log_softmax(log_softmax(y W)), target)
 // in two fused kernels (nts_hip_linear_xent_fwd/bwd); returns the scalar loss
+// Persistent fp32 scalar 1 on `dev` (the loss-backward seed).
+const NtsVar& unit_scalar(const torch::Device& dev);
 bool hip_linear_xent_supported(int64_t K, int64_t C);
 NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs);
 // row-major fp32 views the HIP GEMMs take without a copy (unit column stride)

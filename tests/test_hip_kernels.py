@@ -533,3 +533,32 @@ def test_linear_xent_fused(hip, n, K, C):
     hip.linear_xent_bwd(Y, W, lab, gl, dY2, dW2)
     torch.cuda.synchronize()
     assert torch.equal(loss, loss2) and torch.equal(dY, dY2) and torch.equal(dW, dW2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,K,C,pad", [(10000, 128, 41, 0), (77, 32, 17, 3), (1, 16, 64, 0),
+                                       (300, 256, 7, 4)])
+def test_linear_xent_train(hip, n, K, C, pad):
+    """The training call (loss + gradients for d loss = 1, one pass) is
+    bit-identical to forward + backward(1), also on padded / unaligned rows
+    (scalar staging path), and matches libtorch's autograd in fp64."""
+    g = torch.Generator(device=DEV).manual_seed(3 * n + K + C)
+    Yb = torch.randn(n, K + pad, device=DEV, generator=g)
+    Y = Yb[:, :K]
+    W = torch.randn(K, C, device=DEV, generator=g) * 0.1
+    lab = torch.randint(0, C, (n,), device=DEV, generator=g)
+    loss, loss2 = torch.full((), float("nan"), device=DEV), torch.full((), float("nan"), device=DEV)
+    dY, dW = torch.full((n, K), float("nan"), device=DEV), torch.full((K, C), float("nan"), device=DEV)
+    dY2, dW2 = torch.empty_like(dY), torch.empty_like(dW)
+    for _ in range(2):  # the second call checks the loss ticket was reset
+        hip.linear_xent_train(Y, W, lab, loss, dY, dW)
+    hip.linear_xent_fwd(Y, W, lab, loss2)
+    hip.linear_xent_bwd(Y, W, lab, torch.ones((), device=DEV), dY2, dW2)
+    torch.cuda.synchronize()
+    assert torch.equal(loss, loss2) and torch.equal(dY, dY2) and torch.equal(dW, dW2)
+    Yr, Wr = Y.double().requires_grad_(), W.double().requires_grad_()
+    ref = torch.nn.functional.nll_loss((Yr @ Wr).log_softmax(1).log_softmax(1), lab)
+    ref.backward()
+    torch.testing.assert_close(loss.double(), ref.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dY.double(), Yr.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(dW.double(), Wr.grad, rtol=1e-4, atol=1e-6)
