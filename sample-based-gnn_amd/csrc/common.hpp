@@ -93,7 +93,6 @@ struct nts_hip_ctx {
   void* scratch = nullptr;         // scans / radix sort temporaries
   size_t scratch_bytes = 0;
   uint32_t* mt_state = nullptr;    // 624 words + position (device)
-  uint32_t* ticket = nullptr;      // last-block counters (device, zero between launches)
 };
 
 namespace nts_hip {

@@ -72,12 +72,7 @@ int nts_hip_ctx_create(nts_hip_ctx** out, int device, void* stream, uint64_t see
   // NULL is HIP's legacy default stream, used as-is (ordered with every other
   // blocking stream of the device, like torch's default stream).
   ctx->stream = (hipStream_t)stream;
-  // mt_state: 625 words; the ticket counters follow at word 640
-  hipError_t e = hipMalloc(&ctx->mt_state, 704 * sizeof(uint32_t));
-  if (e == hipSuccess) {
-    ctx->ticket = ctx->mt_state + 640;
-    e = hipMemset(ctx->ticket, 0, 64 * sizeof(uint32_t));
-  }
+  hipError_t e = hipMalloc(&ctx->mt_state, 625 * sizeof(uint32_t));
   if (e != hipSuccess) {
     set_error("hipMalloc(mt_state): %s", hipGetErrorString(e));
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);

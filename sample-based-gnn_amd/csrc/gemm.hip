@@ -712,19 +712,20 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
 }
 
 // C = sum over `splits` partial slabs [M x N] (ld N), as a fixed-shape tree:
-// thread s of a 16-thread group sums splits s, s+16, ... in order, then the
-// group combines its 16 sums pairwise in LDS (deterministic, every element
-// with 16-way parallel loads instead of one serial chain per element).
-// VEC = 4: float4 elements (N % 4 == 0, C 16-byte aligned rows), else floats.
-template <int VEC>
+// thread s of a TPE-lane group sums splits s, s+TPE, ... in order (8 loads in
+// flight, the tail batch predicated), then the group combines its TPE sums
+// pairwise by shuffles (deterministic; every element with TPE-way parallel
+// loads instead of one serial chain).  VEC = 4: float4 elements (N % 4 == 0,
+// C 16-byte aligned rows), else floats.
+template <int VEC, int TPE>
 __global__ __launch_bounds__(256) void k_sum_splits_tree(const float* __restrict__ part,
                                                          int splits, uint64_t stride, int M,
                                                          int N, float* __restrict__ C,
                                                          uint64_t ldc) {
   using T = typename std::conditional<VEC == 4, float4, float>::type;
-  __shared__ T red[256];
-  const int s = threadIdx.x & 15;
-  const uint64_t e = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  constexpr int B = 8;
+  const int s = threadIdx.x % TPE;
+  const uint64_t e = (uint64_t)blockIdx.x * (256 / TPE) + threadIdx.x / TPE;
   const uint64_t total = (uint64_t)M * N / VEC;
   const T* p = reinterpret_cast<const T*>(part);
   const uint64_t st = stride / VEC;
@@ -735,51 +736,54 @@ __global__ __launch_bounds__(256) void k_sum_splits_tree(const float* __restrict
       a += b;
     }
   };
-  T acc;
-  if constexpr (VEC == 4) acc = make_float4(0.f, 0.f, 0.f, 0.f); else acc = 0.f;
+  auto zero = []() {
+    if constexpr (VEC == 4) return make_float4(0.f, 0.f, 0.f, 0.f); else return 0.f;
+  };
+  T acc = zero();
   if (e < total) {
-    int z = s;
-    for (; z + 112 < splits; z += 128) {  // 8 loads in flight, summed in order
-      T v[8];
+    for (int z = s; z < splits; z += B * TPE) {
+      T v[B];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(uint64_t)(z + 16 * u) * st + e];
+      for (int u = 0; u < B; ++u)
+        v[u] = z + TPE * u < splits ? p[(uint64_t)(z + TPE * u) * st + e] : zero();
 #pragma unroll
-      for (int u = 0; u < 8; ++u) add(acc, v[u]);
+      for (int u = 0; u < B; ++u)
+        if (z + TPE * u < splits) add(acc, v[u]);
     }
-    for (; z + 48 < splits; z += 64) {
-      T v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = p[(uint64_t)(z + 16 * u) * st + e];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) add(acc, v[u]);
-    }
-    for (; z < splits; z += 16) add(acc, p[(uint64_t)z * st + e]);
   }
-  red[threadIdx.x] = acc;
-  __syncthreads();
 #pragma unroll
-  for (int w = 8; w >= 1; w >>= 1) {
-    if (s < w) add(red[threadIdx.x], red[threadIdx.x + w]);
-    __syncthreads();
+  for (int o = TPE / 2; o >= 1; o >>= 1) {
+    if constexpr (VEC == 4) {
+      acc.x += __shfl_down(acc.x, o, TPE);
+      acc.y += __shfl_down(acc.y, o, TPE);
+      acc.z += __shfl_down(acc.z, o, TPE);
+      acc.w += __shfl_down(acc.w, o, TPE);
+    } else {
+      acc += __shfl_down(acc, o, TPE);
+    }
   }
   if (s == 0 && e < total) {
     const uint64_t el = e * VEC;
-    *reinterpret_cast<T*>(C + (el / N) * ldc + (el % N)) = red[threadIdx.x];
+    *reinterpret_cast<T*>(C + (el / N) * ldc + (el % N)) = acc;
   }
 }
 
 // Sum `splits` partial slabs (stride floats apart, ld N) into C.
 int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
-                      float* C, uint64_t ldc) {
+               float* C, uint64_t ldc) {
   const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+  const bool wide = splits > 256;  // 64 lanes per element, else 16
   const uint64_t elems = stride / (v4 ? 4 : 1);
-  const uint32_t g = std::max(1u, ceil_div(elems, 16));
-  if (v4)
-    hipLaunchKernelGGL(k_sum_splits_tree<4>, dim3(g), dim3(256), 0, st, part, splits, stride, M, N,
-                       C, ldc);
-  else
-    hipLaunchKernelGGL(k_sum_splits_tree<1>, dim3(g), dim3(256), 0, st, part, splits, stride, M, N,
-                       C, ldc);
+  const uint32_t g = std::max(1u, ceil_div(elems, wide ? 4 : 16));
+#define NTS_SS(V, T)                                                                         \
+  hipLaunchKernelGGL((k_sum_splits_tree<V, T>), dim3(g), dim3(256), 0, st, part, splits, stride, \
+                     M, N, C, ldc)
+  if (v4) {
+    if (wide) NTS_SS(4, 64); else NTS_SS(4, 16);
+  } else {
+    if (wide) NTS_SS(1, 64); else NTS_SS(1, 16);
+  }
+#undef NTS_SS
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }

@@ -8,10 +8,12 @@
 // log-likelihood of the target class, and libtorch's backward of all of it.
 // On the GPU drivers that is ~12 tiny kernels per step (GEMM, 2 softmax, NLL,
 // fills, their backwards, dW and dY GEMMs).  Here one kernel template:
-//   LOSS: the loss (block partials, summed by the last block to finish in a
-//         fixed order — a ticket counter in the context, no extra launch);
+//   LOSS: the loss (block partials);
 //   GRAD: dY and per-wave dW partials for the upstream gradient (*grad, or
-//         exactly 1 for the training call), summed by sum_splits.
+//         exactly 1 for the training call);
+// then k_top_finish sums the partials in a fixed order (deterministic, no
+// atomics).  dW partials are stored as chunks [k][ct][wave][16]: a wave
+// writes 64-byte runs and the finish kernel reads 256-byte runs.
 // forward = <LOSS>, backward = <GRAD>, train = <LOSS, GRAD> (bit-identical
 // to forward + backward with grad 1: same code, same orders).
 //
@@ -44,9 +46,7 @@ struct TopArgs {
   const float* grad;  // GRAD: d loss (device scalar); nullptr = exactly 1
   int n, K, C;
   float* lpart;       // LOSS: [blocks] loss partials
-  float* loss;        // LOSS: the scalar
-  uint32_t* ticket;   // LOSS: zero between launches
-  float* part;        // GRAD: [waves][K*C] dW partials
+  float* part;        // GRAD: dW partials [K][Cp/16][waves][16]
   float* dY;          // GRAD: [n x K]
 };
 
@@ -61,13 +61,28 @@ __device__ __forceinline__ float grp_sum(float v) {
   return v;
 }
 
-// Stage W into LDS as sW[k][Cp] (zero columns >= C).
+// Stage W into LDS as sW[k][Cp] (zero columns >= C): coalesced loads of the
+// contiguous [K x C] matrix, 8 in flight per thread.
 template <int CP>
 __device__ __forceinline__ void stage_w(const TopArgs& a, float* sW) {
-  for (int e = threadIdx.x; e < a.K * CP; e += kTopThreads) {
-    const int k = e / CP, c = e % CP;
-    sW[e] = c < a.C ? a.W[(uint64_t)k * a.C + c] : 0.f;
+  const int C = a.C, KC = a.K * C;
+  constexpr int B = 8;
+  for (int e0 = threadIdx.x; e0 < KC; e0 += B * kTopThreads) {
+    float v[B];
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int e = e0 + u * kTopThreads;
+      v[u] = e < KC ? a.W[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < B; ++u) {
+      const int e = e0 + u * kTopThreads;
+      if (e < KC) sW[(e / C) * CP + e % C] = v[u];
+    }
   }
+  const int pad = CP - C;
+  for (int e = threadIdx.x; e < a.K * pad; e += kTopThreads)
+    sW[(e / pad) * CP + C + e % pad] = 0.f;
 }
 
 // Stage this wave's 16 Y rows into sY[16][K + 4] (rows >= n are zero).
@@ -177,7 +192,6 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
   constexpr int CP = 16 * NCT;
   extern __shared__ float smem[];
   __shared__ float wl[kTopWaves];
-  __shared__ uint32_t last;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int K = a.K;
@@ -254,7 +268,8 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
     }
     // dW partial [K x CP] = Y^T [K x 16] dZ [16 x CP]:
     //   A lane (i,g) = Y[r0 + 4s + g][16 kt + i], B = dZ[4s + g][16 ct + i]
-    float* pw = a.part + ((uint64_t)blockIdx.x * kTopWaves + w) * K * a.C;
+    const uint64_t nslab = (uint64_t)gridDim.x * kTopWaves;
+    const uint64_t slab = (uint64_t)blockIdx.x * kTopWaves + w;
     for (int kt = 0; kt < K / 16; ++kt) {
       f32x4 acc[NCT];
 #pragma unroll
@@ -267,41 +282,71 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
           acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dz[(4 * s + g) * CP + 16 * ct + i],
                                                          acc[ct], 0, 0, 0);
       }
-      // acc[ct][v] = dW[16 kt + 4 g + v][16 ct + i]
+      // acc[ct][v] = dW[16 kt + 4 g + v][16 ct + i] -> chunk (k, ct), lane i
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int c = 16 * ct + i;
-          if (c < a.C) pw[(uint64_t)(16 * kt + 4 * g + v) * a.C + c] = acc[ct][v];
+          const uint64_t q = (uint64_t)(16 * kt + 4 * g + v) * NCT + ct;
+          a.part[(q * nslab + slab) * 16 + i] = acc[ct][v];
         }
     }
   }
   if (LOSS) {
-    // block partial; the last block to finish sums all partials in index
-    // order (the same order whichever block is last) and resets the ticket
     __syncthreads();
     if (threadIdx.x == 0) {
       float s = 0.f;
       for (int q = 0; q < kTopWaves; ++q) s += wl[q];
       a.lpart[blockIdx.x] = s;
-      __threadfence();
-      last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (last && w == 0) {
-      __threadfence();
-      float s = 0.f;
-      for (uint32_t b = lane; b < gridDim.x; b += kWave)
-        s += __builtin_nontemporal_load(a.lpart + b);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, kWave);
-      if (lane == 0) {
-        *a.loss = s / (float)a.n;
-        *a.ticket = 0u;
-      }
     }
   }
+}
+
+// Blocks [0, K*NCT): dW chunk (k, ct) = sum over the wave slabs — thread
+// (sg, i) sums slabs sg, sg+16, ... in order (8 loads in flight), then a fixed
+// pairwise tree over the 16 slab groups.  Block K*NCT (or 0 without GRAD):
+// loss = (sum of block partials, fixed tree) / n.
+template <int NCT>
+__global__ __launch_bounds__(256) void k_top_finish(const float* __restrict__ part, int nslab,
+                                                    const float* __restrict__ lpart, int nblk,
+                                                    int n, int K, int C, int nchunks,
+                                                    float* __restrict__ dW, float* loss) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  float acc = 0.f;
+  if ((int)blockIdx.x < nchunks) {
+    const int q = blockIdx.x, sg = t >> 4, i = t & 15;
+    const float* p = part + (uint64_t)q * nslab * 16 + i;
+    constexpr int B = 8;
+    for (int z = sg; z < nslab; z += 16 * B) {
+      float v[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) v[u] = z + 16 * u < nslab ? p[(uint64_t)(z + 16 * u) * 16] : 0.f;
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+        if (z + 16 * u < nslab) acc += v[u];
+    }
+    red[t] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int h = 128; h >= 16; h >>= 1) {
+      if (t < h) red[t] += red[t + h];
+      __syncthreads();
+    }
+    const int k = q / NCT, c = 16 * (q % NCT) + t;
+    if (t < 16 && c < C) dW[(uint64_t)k * C + c] = red[t];
+  } else {
+    for (int b = t; b < nblk; b += 256) acc += lpart[b];
+    red[t] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int h = 128; h >= 1; h >>= 1) {
+      if (t < h) red[t] += red[t + h];
+      __syncthreads();
+    }
+    if (t == 0) *loss = red[0] / (float)n;
+  }
+  (void)K;
 }
 
 template <int NCT, bool LOSS, bool GRAD>
@@ -331,6 +376,25 @@ static int launch_top_any(hipStream_t st, int nblk, int Cp, const TopArgs& a) {
   }
 }
 
+static int launch_finish(hipStream_t st, int Cp, const float* part, int nslab, const float* lpart,
+                         int nblk, int n, int K, int C, bool grad, bool loss_on, float* dW,
+                         float* loss) {
+  const int nchunks = grad ? K * (Cp / 16) : 0;
+  const dim3 grid(nchunks + (loss_on ? 1 : 0));
+#define NTS_F(NCT)                                                                             \
+  hipLaunchKernelGGL(k_top_finish<NCT>, grid, dim3(256), 0, st, part, nslab, lpart, nblk, n, K, \
+                     C, nchunks, dW, loss)
+  switch (Cp / 16) {
+    case 1: NTS_F(1); break;
+    case 2: NTS_F(2); break;
+    case 3: NTS_F(3); break;
+    default: NTS_F(4); break;
+  }
+#undef NTS_F
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
 }  // namespace nts_hip
 
 using namespace nts_hip;
@@ -346,25 +410,24 @@ static int top_check(nts_hip_ctx* ctx, int n, int K, int C, uint64_t ldy) {
   return NTS_OK;
 }
 
-// scratch: [loss partials, 64-float aligned][dW partial slabs]
+// scratch: [loss partials, 64-float aligned][dW partial chunks]
 static int top_run(nts_hip_ctx* ctx, bool loss_on, bool grad_on, const float* Y, uint64_t ldy,
                    int n, int K, const float* W, int C, const int64_t* labels,
                    const float* grad_loss, float* loss, float* dY, float* dW) {
   NTS_RET(top_check(ctx, n, K, C, ldy));
   const int Cp = (C + 15) / 16 * 16;
   const int nblk = (n + kTopRows - 1) / kTopRows;
-  const uint64_t slab = (uint64_t)K * C;
   const int nslab = nblk * kTopWaves;
   const size_t lp = ((size_t)nblk + 63) / 64 * 64;
-  NTS_RET(ensure_scratch(ctx, (lp + (grad_on ? (size_t)nslab * slab : 0)) * sizeof(float)));
+  NTS_RET(ensure_scratch(
+      ctx, (lp + (grad_on ? (size_t)nslab * K * Cp : 0)) * sizeof(float)));
   float* base = (float*)ctx->scratch;
-  TopArgs a{Y, ldy, W, labels, grad_loss, n, K, C, base, loss, ctx->ticket, base + lp, dY};
+  TopArgs a{Y, ldy, W, labels, grad_loss, n, K, C, base, base + lp, dY};
   hipStream_t st = ctx->stream;
   if (loss_on && grad_on) NTS_RET((launch_top_any<true, true>(st, nblk, Cp, a)));
   else if (loss_on) NTS_RET((launch_top_any<true, false>(st, nblk, Cp, a)));
   else NTS_RET((launch_top_any<false, true>(st, nblk, Cp, a)));
-  if (grad_on) return sum_splits(st, a.part, nslab, slab, K, C, dW, (uint64_t)C);
-  return NTS_OK;
+  return launch_finish(st, Cp, a.part, nslab, a.lpart, nblk, n, K, C, grad_on, loss_on, dW, loss);
 }
 
 int nts_hip_linear_xent_fwd(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
