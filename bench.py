@@ -81,6 +81,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # NTS_BENCH_SHARE_GPU=1: every rank on device 0 (rehearsing the DP path on a
+    # one-GPU box; the numbers are then not a scaling measurement)
+    if os.environ.get("NTS_BENCH_SHARE_GPU") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:

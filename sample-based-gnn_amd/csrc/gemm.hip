@@ -356,7 +356,7 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
 // Numerics: every output is one k-ordered fp32 fma chain (exact products),
 // fixed by the shapes — deterministic.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kWresRT = 2;  // 16-row tiles per wave task
+constexpr int kWresRT = 1;  // 16-row tiles per wave task
 // 16 waves (4 per SIMD, <= 128 VGPRs) at NCOL = 64; 8 waves at NCOL = 128,
 // whose 32 accumulator registers more per lane need the larger budget
 template <int NCOL>

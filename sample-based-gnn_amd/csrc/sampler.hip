@@ -201,6 +201,83 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
   }
 }
 
+// PHILOX for fanout <= 16: four destinations per wave, one 16-lane group each
+// (a round of 16 candidates covers a fanout-10 draw; the per-destination chain
+// dst -> offsets -> row ids is latency-bound, so four chains per wave in
+// flight instead of one).  Same result as k_select_philox: the first `need`
+// distinct accepted draws of the destination's stream, in draw order.
+constexpr int kGrp = 16;
+constexpr int kGrpPerWave = kWave / kGrp;
+
+__global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a) {
+  __shared__ uint32_t sets[kSelWaves * kGrpPerWave][kGrp];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gl = lane & (kGrp - 1), grp = lane >> 4;
+  const int gib = w * kGrpPerWave + grp;
+  uint32_t* set = sets[gib];
+  const uint32_t gshift = kGrp * grp;
+  const uint32_t lt16 = (1u << gl) - 1u;
+  const uint32_t v = a.sizes[0];
+  const uint32_t ng = gridDim.x * kSelWaves * kGrpPerWave;
+  for (uint32_t i = blockIdx.x * kSelWaves * kGrpPerWave + gib; i < v; i += ng) {
+    const uint32_t d = a.dst[i];
+    const uint64_t beg = a.goff[d];
+    const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
+    const uint32_t c = a.co[i];
+    const uint32_t n = a.co[i + 1] - c;
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged in k_finish_count)
+    if (n == deg) {
+      for (uint32_t k = gl; k < deg; k += kGrp) {
+        const uint32_t g = a.grows[beg + k];
+        a.ans[c + k] = g;
+        a.edst[c + k] = i;
+        a.marks[g] = 1;
+      }
+      continue;
+    }
+    if (n == 0) continue;
+    Draw dr;
+    dr.init(deg, true);
+    uint32_t count = 0, consumed = 0;
+    while (count < n) {  // group-uniform
+      const uint32_t remaining = n - count;
+      uint32_t val = 0;
+      const bool ok = dr.apply(philox_word(a.seed, d, a.layer, a.batch_seq, consumed + gl), val);
+      bool dup = false;
+      for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
+      const uint32_t okm = (uint32_t)(__ballot(ok) >> gshift) & 0xFFFFu;
+#pragma unroll
+      for (int j = 0; j < kGrp; ++j) {
+        const uint32_t vj = (uint32_t)__shfl((int)val, j, kGrp);
+        dup |= (j < gl) && ((okm >> j) & 1u) && (vj == val);
+      }
+      const bool isnew = ok && !dup;
+      const uint32_t newm = (uint32_t)(__ballot(isnew) >> gshift) & 0xFFFFu;
+      uint32_t take = newm;
+      if ((uint32_t)__popc(newm) >= remaining) {
+        uint32_t m = newm;
+        for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+        const int last = __ffs(m) - 1;
+        take = newm & ((2u << last) - 1u);
+        consumed += (uint32_t)last + 1u;
+      } else {
+        consumed += kGrp;
+      }
+      if ((take >> gl) & 1u) {
+        const uint32_t slot = count + (uint32_t)__popc(take & lt16);
+        set[slot] = val;
+        const uint32_t pos = c + slot;
+        const uint32_t g = a.grows[beg + val];
+        a.ans[pos] = g;
+        a.edst[pos] = i;
+        a.marks[g] = 1;
+      }
+      count += (uint32_t)__popc(take);
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
 // ---- MT19937 (reference stream) -------------------------------------------
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= y >> 11;
@@ -553,8 +630,14 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   a.batch_seq = batch_seq;
   a.seed = ctx->seed;
   if (rng_mode == NTS_RNG_PHILOX) {
-    const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves), 4096u));
-    hipLaunchKernelGGL(k_select_philox, dim3(gs), dim3(kSelThreads), 0, st, a);
+    if (fanout >= 0 && fanout <= kGrp) {
+      const uint32_t gs =
+          std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
+      hipLaunchKernelGGL(k_select_philox_g16, dim3(gs), dim3(kSelThreads), 0, st, a);
+    } else {
+      const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves), 4096u));
+      hipLaunchKernelGGL(k_select_philox, dim3(gs), dim3(kSelThreads), 0, st, a);
+    }
   } else {
     hipLaunchKernelGGL(k_select_mt, dim3(1), dim3(kWave), 0, st, a, ctx->mt_state,
                        rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0);

@@ -208,6 +208,9 @@ void GCN_SAMPLE_ALLGPU_impl::init_nn() {
   grad_bucket = torch::zeros({n}, f32_opts(graph->device));
   if (comm) {  // identical initial weights on every rank (init_parameter / Bcast)
     torch::NoGradGuard ng;
+    // the initialisation ran on libtorch's current stream: order it before the
+    // broadcast on the driver stream (construction time only)
+    TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
     for (auto* p : P) comm->broadcast(p->W.data_ptr<float>(), (uint64_t)p->W.numel(), 0, cs->stream());
   }
 }
