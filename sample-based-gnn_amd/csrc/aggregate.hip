@@ -23,6 +23,7 @@ struct VT<1> {
   __device__ static __forceinline__ T madd(T a, T x, float w) { return a + x * w; }
   __device__ static __forceinline__ T scale(T x, float w) { return x * w; }
   __device__ static __forceinline__ void st_nt(T* p, T v) { __builtin_nontemporal_store(v, p); }
+  __device__ static __forceinline__ void st_part(T* p, T v, uint32_t) { st_nt(p, v); }
 };
 template <>
 struct VT<2> {
@@ -36,6 +37,9 @@ struct VT<2> {
     typedef float f2 __attribute__((ext_vector_type(2)));
     f2 u = {v.x, v.y};
     __builtin_nontemporal_store(u, reinterpret_cast<f2*>(p));
+  }
+  __device__ static __forceinline__ void st_part(T* p, T v, uint32_t) {  // 1 of 2 valid
+    __builtin_nontemporal_store(v.x, reinterpret_cast<float*>(p));
   }
 };
 template <>
@@ -52,6 +56,12 @@ struct VT<4> {
     typedef float f4 __attribute__((ext_vector_type(4)));
     f4 u = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(u, reinterpret_cast<f4*>(p));
+  }
+  __device__ static __forceinline__ void st_part(T* p, T v, uint32_t nvalid) {  // 1..3 valid
+    float* q = reinterpret_cast<float*>(p);
+    __builtin_nontemporal_store(v.x, q);
+    if (nvalid > 1) __builtin_nontemporal_store(v.y, q + 1);
+    if (nvalid > 2) __builtin_nontemporal_store(v.z, q + 2);
   }
 };
 
@@ -71,7 +81,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
     const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t nv,
-    float* __restrict__ y, uint64_t ldy) {
+    float* __restrict__ y, uint64_t ldy, uint32_t last_valid) {
   using V = VT<VEC>;
   using T = typename V::T;
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
@@ -120,7 +130,11 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {  // output rows are not re-read here: keep them
         const uint32_t col = c0 + sl + c * LPD;  // out of the cache that serves x rows
-        if (col < nv) V::st_nt(yrow + col, acc[c]);
+        if (col + 1 < nv || (col + 1 == nv && last_valid == (uint32_t)VEC)) {
+          V::st_nt(yrow + col, acc[c]);
+        } else if (col + 1 == nv) {  // partial last vector: only the valid floats
+          V::st_part(yrow + col, acc[c], last_valid);
+        }
       }
     }
   }
@@ -242,27 +256,29 @@ static int gather_u_env() {
   return u;
 }
 constexpr int gather_u(int floats_per_lane) {
-  return floats_per_lane <= 4 ? 8 : 4;
+  return floats_per_lane <= 4 ? 8 : floats_per_lane <= 12 ? 5 : 4;
 }
 
 template <int VEC, bool MAP>
-static int launch_gather_vec(hipStream_t st, uint32_t grid, Shape s, const uint32_t* off,
+static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid, Shape s,
+                             const uint32_t* off,
                              const uint32_t* idx, const float* w, const uint32_t* n_dev,
                              uint32_t n_cap, const float* x, uint64_t ldx, const uint32_t* map,
                              uint32_t nv, float* y, uint64_t ldy) {
-// rows in flight per lane group: 8 for narrow rows, else 4 (register budget;
-// NTS_GATHER_U=5 selects 5 for the mid-width rows, e.g. F ~ 600 at fanout 10)
+// rows in flight per lane group: 8 for narrow rows, 5 for mid-width rows
+// (F ~ 600: 3 float4 per lane; fanout 10/25 -> full batches), 4 for the
+// widest (register budget); NTS_GATHER_U=4 forces 4 for the mid-width rows
 #define NTS_G(LPD, NCH)                                                                     \
   do {                                                                                      \
     constexpr int u = gather_u(VEC * NCH);                                                  \
-    if (u == 4 && VEC * NCH <= 12 && gather_u_env() == 5)                                   \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 5>), dim3(grid),               \
+    if (u == 5 && gather_u_env() == 4)                                                      \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4>), dim3(grid),               \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
-                         nv, y, ldy);                                                       \
+                         nv, y, ldy, last_valid);                                           \
     else                                                                                    \
       hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u>), dim3(grid),               \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
-                         nv, y, ldy);                                                       \
+                         nv, y, ldy, last_valid);                                           \
   } while (0)
   if (s.lpd == 8) NTS_G(8, 1);
   else if (s.lpd == 16) NTS_G(16, 1);
@@ -286,8 +302,16 @@ template <bool MAP>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
                          const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
                          uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy) {
-  const int vec = pick_vec(F, ldx, ldy, x, y);
-  const uint32_t nv = F / vec;
+  int vec = pick_vec(F, ldx, ldy, x, y);
+  // rows padded to a 16-byte multiple (the 128-byte feature / output pitch):
+  // float4 loads, the partial last vector reads pitch padding and stores only
+  // its valid floats
+  const uint32_t F4 = (F + 3) / 4 * 4;
+  if (vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
+      (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0)
+    vec = 4;
+  const uint32_t nv = (F + vec - 1) / vec;
+  const uint32_t last_valid = F - (nv - 1) * vec;
   const Shape s = pick_shape(nv);
   const uint32_t gpb = kAggThreads / s.lpd;
   // enough waves to saturate HBM: 256 CUs x 16 waves, grid-stride beyond
@@ -299,10 +323,13 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   }();
   const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), cap));
   if (vec == 4)
-    return launch_gather_vec<4, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
+    return launch_gather_vec<4, MAP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
+                                     map, nv, y, ldy);
   if (vec == 2)
-    return launch_gather_vec<2, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
-  return launch_gather_vec<1, MAP>(st, grid, s, off, idx, w, n_dev, n_cap, x, ldx, map, nv, y, ldy);
+    return launch_gather_vec<2, MAP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
+                                     map, nv, y, ldy);
+  return launch_gather_vec<1, MAP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
+                                   map, nv, y, ldy);
 }
 
 

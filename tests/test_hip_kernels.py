@@ -231,6 +231,17 @@ def test_spmm_fwd_bitexact_and_fused_gather(hip, cora, F):
     torch.cuda.synchronize()
     assert np.array_equal(y2.cpu().numpy(), Y_ref)
     assert np.array_equal(x0.cpu().numpy(), X)
+    # padded pitches (the 128-byte feature / output layout): float4 loads with a
+    # partial last vector; the pitch padding of the output stays untouched
+    if F % 4:
+        pad = (F + 31) // 32 * 32
+        tp = torch.full((V, pad), float("nan"), device=DEV)
+        tp[:, :F] = _t(table)
+        y3 = torch.full((v, pad), 7.0, device=DEV)
+        hip.spmm_csc_fwd(co, ri, wf, vdev, v, tp[:, :F], y3[:, :F], row_map=_t(l1["source"]))
+        torch.cuda.synchronize()
+        assert np.array_equal(y3[:, :F].cpu().numpy(), Y_ref)
+        assert (y3[:, F:] == 7.0).all()
 
 
 @pytest.mark.parametrize("F", [16, 41, 128, 602])
