@@ -58,6 +58,10 @@ def parse():
     p.add_argument("--early-agg", action="store_true",
                    help="issue the bottom aggregation behind the sampler on the sampling stream")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
+    p.add_argument("--cache-rate", type=float, default=-1.0,
+                   help="feature table in pinned host memory with this fraction of the "
+                        "highest-degree rows cached in HBM (GS_SAMPLE_PD_CACHE placement); "
+                        "default: whole table in HBM")
     p.add_argument("--no-fuse-act", action="store_true",
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
     p.add_argument("--sampler-cus", type=int, default=0,
@@ -129,7 +133,7 @@ def main():
                           sampler_priority=not args.no_priority,
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
-                          pad_features=not args.no_pad_features)
+                          pad_features=not args.no_pad_features, cache_rate=args.cache_rate)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and not args.early_agg and layers[1] <= 128)
     agg_kernel = ("k_agg_gemm" if fused_linear else "k_spmm_gather")
@@ -219,7 +223,9 @@ def main():
                          f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation"
                          f"{' (issued behind the sampler)' if args.early_agg and not args.no_fused_gather else ''}"
                          f"{' + layer-1 GEMM' if fused_linear else ''} + "
-                         f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"),
+                         f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"
+                         + (f"; features in pinned host memory, {args.cache_rate:.0%} of rows "
+                            f"(highest degree) cached in HBM" if args.cache_rate >= 0 else "")),
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}",
             "fanout": args.fanout,
@@ -250,7 +256,7 @@ def main():
     # the default workload only
     pmcs = sorted((ROOT / "profiles").glob("pmc_*.json"))
     default_shape = (args.shape == "reddit" and args.batch == 10000 and args.fanout == "25-10"
-                     and layers == [602, 128, 41] and world == 1)
+                     and layers == [602, 128, 41] and world == 1 and args.cache_rate < 0)
     if pmcs and default_shape:
         try:
             info = json.loads(pmcs[-1].read_text())

@@ -164,6 +164,37 @@ int nts_hip_gather_rows(nts_hip_ctx *ctx, const float *table, uint64_t ld_table,
 int nts_hip_gather_labels(nts_hip_ctx *ctx, const int64_t *labels, const uint32_t *index,
                           const uint32_t *n, uint32_t n_cap, int64_t *out);
 
+/* ---- HBM feature cache + host-pinned spill -------------------------------- */
+/* The reference keeps the feature table in pinned host memory and caches the
+ * rows of the highest-degree vertices on the GPU (GS_SAMPLE_PD_CACHE:
+ * determine_cache_node_idx / cache_high_degree / mark_cache_node,
+ * toolkits/GS_SAMPLE_PD_CACHE.hpp:1019-1112).  On MI355X every BASELINE
+ * config fits HBM, so this two-tier table is the path for tables that do not.
+ *
+ * Selection: cache_map[v] = slot of v if v is among the n_cache vertices of
+ * largest out_degree (ties: ascending id), else NTS_NOT_CACHED;
+ * cache_ids[slot] = v (may be NULL when n_cache == 0).  Slots follow the
+ * (degree descending, id ascending) order.  n_vertices < 2^31.  Fill the
+ * cache with nts_hip_gather_rows(table, cache_ids -> cache). */
+#define NTS_NOT_CACHED 0xFFFFFFFFu
+int nts_hip_cache_select(nts_hip_ctx *ctx, const uint32_t *out_degree, uint64_t n_vertices,
+                         uint64_t n_cache, uint32_t *cache_map, uint32_t *cache_ids);
+/* Pinned host memory mapped into the device address space (coarse-grained),
+ * for the spilled feature table (cudaMallocPinned, core/ntsDataloador.hpp:483). */
+int nts_hip_host_alloc(uint64_t bytes, void **host_ptr);
+int nts_hip_host_free(void *host_ptr);
+int nts_hip_host_device_pointer(void *host_ptr, void **dev_ptr);
+/* load_feature_gpu_cache (core/ntsFastSampler.hpp:263-317; kernels
+ * cuda/ntsCUDATransferKernel.cuh:154-183) in one pass:
+ *   out[i,:] = cache_map[index[i]] != NTS_NOT_CACHED ? cache[cache_map[index[i]],:]
+ *                                                   : host_table[index[i],:]
+ * host_table: device-visible pointer of the pinned host table (zero-copy). */
+int nts_hip_gather_rows_cached(nts_hip_ctx *ctx, const float *cache, uint64_t ld_cache,
+                               const uint32_t *cache_map, const float *host_table,
+                               uint64_t ld_host, const uint32_t *index, const uint32_t *n,
+                               uint32_t n_cap, uint32_t feature_size, float *out,
+                               uint64_t ld_out);
+
 /* ---- sampled aggregation ------------------------------------------------ */
 /* Y[d,:] = sum_{e in [co[d],co[d+1])} w[e] * X[row(e),:], summed in CSC edge
  * order as (x*w)+acc with no FMA contraction — the exact arithmetic of
@@ -178,6 +209,29 @@ int nts_hip_spmm_csc_fwd(nts_hip_ctx *ctx, const uint32_t *column_offset,
                          const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
                          const uint32_t *x_row_map, uint32_t feature_size, float *y,
                          uint64_t ldy);
+/* Stage the NON-cached rows of a layer's sources once into HBM:
+ *   stage[i,:] = host_table[index[i],:]  for every i with cache_map[index[i]] ==
+ *   NTS_NOT_CACHED (other rows of stage are left untouched).
+ * The host link then carries each distinct spilled row once per batch
+ * instead of once per sampled edge. */
+int nts_hip_stage_uncached_rows(nts_hip_ctx *ctx, const uint32_t *cache_map,
+                                const float *host_table, uint64_t ld_host, const uint32_t *index,
+                                const uint32_t *n, uint32_t n_cap, uint32_t feature_size,
+                                float *stage, uint64_t ld_stage);
+/* nts_hip_spmm_csc_fwd with the fused feature gather reading the two-tier
+ * table: for local src r = row_indices[e] and g = x_row_map[r], the row comes
+ * from cache[cache_map[g],:] when cached, else from spill[host_local ? r : g,:]
+ * — the pinned host table (host_local = 0) or the rows staged by
+ * nts_hip_stage_uncached_rows (host_local = 1).  load_feature_gpu_cache + the
+ * bottom graph op; bit-identical to nts_hip_spmm_csc_fwd on the full table
+ * for every cache content. */
+int nts_hip_spmm_csc_fwd_cached(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                                const uint32_t *row_indices, const float *weight,
+                                const uint32_t *v, uint32_t v_cap, const float *cache,
+                                uint64_t ld_cache, const uint32_t *cache_map,
+                                const float *spill, uint64_t ld_spill, int host_local,
+                                const uint32_t *x_row_map, uint32_t feature_size, float *y,
+                                uint64_t ldy);
 /* Fused bottom layer (SingleGPUAllSampleGraphOp::forward on the feature table
  * followed by Parameter::forward and vertexForward's activation):
  *   Y = A X  (rows of x gathered through x_row_map, bit-identical to

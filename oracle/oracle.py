@@ -151,3 +151,32 @@ def fuse_bwd(layer, G, out_deg, in_deg, weight_mean=False, threads=1):
                        _p(np.ascontiguousarray(in_deg, np.uint32)), _p(G), G.shape[1], _p(Gin),
                        int(weight_mean), threads)
     return Gin
+
+
+NOT_CACHED = 0xFFFFFFFF
+
+
+def cache_select(out_deg, n_cache):
+    """Degree-ordered feature-cache selection of GS_SAMPLE_PD_CACHE
+    (cache_high_degree + mark_cache_node, toolkits/GS_SAMPLE_PD_CACHE.hpp:1019-1047):
+    vertex ids sorted by out_degree_for_backward descending, the first n_cache
+    get slots 0, 1, ... in that order, every other vertex is not cached (-1).
+    The reference's std::sort leaves equal degrees in an unspecified order; the
+    tie rule restated here (ascending id) is this build's."""
+    out_deg = np.asarray(out_deg, np.uint32)
+    order = np.argsort(-out_deg.astype(np.int64), kind="stable").astype(np.uint32)
+    cmap = np.full(out_deg.size, NOT_CACHED, np.uint32)
+    cmap[order[:n_cache]] = np.arange(n_cache, dtype=np.uint32)
+    return cmap, order[:n_cache].copy()
+
+
+def get_feature_cached(idx, cache, cache_map, host_table):
+    """load_feature_gpu_cache (core/ntsFastSampler.hpp:263-317): rows of cached
+    vertices from the device cache, the others from the pinned host table."""
+    idx = np.asarray(idx, np.uint32)
+    slots = cache_map[idx]
+    out = np.empty((idx.size, host_table.shape[1]), np.float32)
+    hot = slots != NOT_CACHED
+    out[hot] = cache[slots[hot]]
+    out[~hot] = host_table[idx[~hot]]
+    return out

@@ -7,7 +7,7 @@ set -e
 TAG=${1:-r01}
 STEPS=${2:-10}
 MODE=${3:-all}
-shift 3 || true
+if [ $# -ge 3 ]; then shift 3; else shift $#; fi
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG}
 mkdir -p $OUT
@@ -18,4 +18,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/fetch -o run
   python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline "$@" > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/write -o run --output-format csv -- \
   python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline "$@" > $OUT/write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d $OUT/hit -o run --output-format csv -- \
+  python3 bench.py --steps $STEPS --warmup 3 --no-cpu-baseline "$@" > $OUT/hit.log 2>&1
 echo done

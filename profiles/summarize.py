@@ -58,7 +58,8 @@ def main():
     if dom:
         info["avg_ns"] = float(dom[0]["AverageNs"])
         info["calls"] = int(dom[0]["Calls"])
-    for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"),
+                          ("hit", "TCC_HIT_sum"), ("hit", "TCC_MISS_sum")):
         p = list(src.glob(f"{kind}/**/run_counter_collection.csv"))
         if not p:
             continue
@@ -75,6 +76,11 @@ def main():
         if "avg_ns" in info:
             lines.append(f"- at the traced average duration {info['avg_ns']/1e3:.1f} us: "
                          f"{info['hbm_bytes_per_launch']/info['avg_ns']:.0f} GB/s of HBM traffic")
+    if "TCC_HIT_sum" in info and "TCC_MISS_sum" in info:
+        h, m = info["TCC_HIT_sum"], info["TCC_MISS_sum"]
+        info["l2_hit_rate"] = h / max(h + m, 1.0)
+        lines.append(f"- L2 hit rate TCC_HIT/(HIT+MISS): {info['l2_hit_rate']:.3f} "
+                     f"({h:.3g} hits, {m:.3g} misses per dispatch)")
     (dst / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
     (dst / f"pmc_{tag}.json").write_text(json.dumps(info, indent=1) + "\n")
     print("\n".join(lines))

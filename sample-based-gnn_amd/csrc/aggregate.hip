@@ -76,12 +76,29 @@ constexpr int kUnroll = 4;
 // predicated), so a row costs off -> idx/map -> ceil(deg/U) row rounds of
 // memory latency instead of two dependent loads per U edges plus a serial
 // remainder.  The sum order is still the CSC edge order.
-template <int VEC, int LPD, int NCH, bool MAP, int U>
+//
+// TIER (two-tier feature table, load_feature_gpu_cache semantics,
+// core/ntsFastSampler.hpp:263-317): x is the HBM cache of the hottest rows
+// and tier.cmap[g] its slot for global row g, or kNotCached, in which case the
+// row is read from the host-pinned table tier.host (zero-copy over the host
+// link).  The per-edge id carries the tier in bit 31 (vertex ids < 2^31).
+// host_local: the non-cached rows were staged by local src id (tier.host is
+// then an HBM buffer [src_size, ldh], see nts_hip_stage_uncached_rows)
+struct Tier {
+  const uint32_t* cmap;
+  const float* host;
+  uint64_t ldh;
+  int host_local;
+};
+constexpr uint32_t kNotCached = 0xFFFFFFFFu;
+constexpr uint32_t kHostBit = 0x80000000u;
+
+template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER>
 __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
     const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t nv,
-    float* __restrict__ y, uint64_t ldy, uint32_t last_valid) {
+    float* __restrict__ y, uint64_t ldy, uint32_t last_valid, Tier tier) {
   using V = VT<VEC>;
   using T = typename V::T;
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
@@ -101,7 +118,12 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
         if ((uint32_t)sl < ne) {  // streamed once: do not keep in cache
           my_r = __builtin_nontemporal_load(idx + cb + sl);
           my_w = w ? __builtin_nontemporal_load(w + cb + sl) : 1.0f;
+          const uint32_t loc = my_r;
           if (MAP) my_r = map[my_r];
+          if (TIER) {
+            const uint32_t slot = tier.cmap[my_r];
+            my_r = slot != kNotCached ? slot : ((tier.host_local ? loc : my_r) | kHostBit);
+          }
         }
         for (uint32_t j0 = 0; j0 < ne; j0 += U) {
           T xv[U][NCH];
@@ -112,7 +134,9 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
             const uint32_t r = (uint32_t)__shfl((int)my_r, src, LPD);
             ww[j] = __shfl(my_w, src, LPD);
             const bool ok = j0 + j < ne;
-            const T* xrow = reinterpret_cast<const T*>(x + (uint64_t)r * ldx);
+            const T* xrow = reinterpret_cast<const T*>(
+                TIER && (r & kHostBit) ? tier.host + (uint64_t)(r & ~kHostBit) * tier.ldh
+                                       : x + (uint64_t)r * ldx);
 #pragma unroll
             for (int c = 0; c < NCH; ++c) {
               const uint32_t col = c0 + sl + c * LPD;
@@ -169,19 +193,30 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_scatter_atomic(
   }
 }
 
-template <int VEC, int LPD>
+// out[i,:] = table[index[i],:]; TIER: table is the HBM cache, rows whose
+// tier.cmap entry is kNotCached come from the host-pinned tier.host
+// (zero_copy_feature_move_gpu_cache + gather_feature_from_gpu_cache,
+// cuda/ntsCUDATransferKernel.cuh:154-183, in one pass).
+// STAGE (with TIER): only the rows that are not cached are copied, out row i
+// = host row index[i]; cached rows of `out` are left untouched.
+template <int VEC, int LPD, bool TIER, bool STAGE = false>
 __global__ __launch_bounds__(kAggThreads) void k_gather_rows(const float* __restrict__ table,
                                                             uint64_t ldt,
                                                             const uint32_t* __restrict__ index,
                                                             const uint32_t* n_dev, uint32_t n_cap,
                                                             uint32_t nv, float* __restrict__ out,
-                                                            uint64_t ldo) {
+                                                            uint64_t ldo, Tier tier) {
   using T = typename VT<VEC>::T;
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
   constexpr int GPB = kAggThreads / LPD;
   const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
   for (uint32_t i = blockIdx.x * GPB + grp; i < n; i += gridDim.x * GPB) {
-    const T* src = reinterpret_cast<const T*>(table + (uint64_t)index[i] * ldt);
+    const uint32_t g = index[i];
+    const uint32_t slot = TIER ? tier.cmap[g] : g;
+    if (STAGE && slot != kNotCached) continue;  // group-uniform
+    const T* src = reinterpret_cast<const T*>(
+        TIER && slot == kNotCached ? tier.host + (uint64_t)g * tier.ldh
+                                   : table + (uint64_t)slot * ldt);
     T* dst = reinterpret_cast<T*>(out + (uint64_t)i * ldo);
     for (uint32_t c = sl; c < nv; c += LPD) dst[c] = src[c];
   }
@@ -259,12 +294,12 @@ constexpr int gather_u(int floats_per_lane) {
   return floats_per_lane <= 4 ? 8 : floats_per_lane <= 12 ? 5 : 4;
 }
 
-template <int VEC, bool MAP>
+template <int VEC, bool MAP, bool TIER>
 static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid, Shape s,
                              const uint32_t* off,
                              const uint32_t* idx, const float* w, const uint32_t* n_dev,
                              uint32_t n_cap, const float* x, uint64_t ldx, const uint32_t* map,
-                             uint32_t nv, float* y, uint64_t ldy) {
+                             uint32_t nv, float* y, uint64_t ldy, Tier tier) {
 // rows in flight per lane group: 8 for narrow rows, 5 for mid-width rows
 // (F ~ 600: 3 float4 per lane; fanout 10/25 -> full batches), 4 for the
 // widest (register budget); NTS_GATHER_U=4 forces 4 for the mid-width rows
@@ -272,13 +307,13 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   do {                                                                                      \
     constexpr int u = gather_u(VEC * NCH);                                                  \
     if (u == 5 && gather_u_env() == 4)                                                      \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4>), dim3(grid),               \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4, TIER>), dim3(grid),         \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
-                         nv, y, ldy, last_valid);                                           \
+                         nv, y, ldy, last_valid, tier);                                     \
     else                                                                                    \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u>), dim3(grid),               \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u, TIER>), dim3(grid),         \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
-                         nv, y, ldy, last_valid);                                           \
+                         nv, y, ldy, last_valid, tier);                                     \
   } while (0)
   if (s.lpd == 8) NTS_G(8, 1);
   else if (s.lpd == 16) NTS_G(16, 1);
@@ -298,17 +333,20 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   return NTS_OK;
 }
 
-template <bool MAP>
+template <bool MAP, bool TIER = false>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
                          const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
-                         uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy) {
+                         uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy,
+                         Tier tier = Tier{nullptr, nullptr, 0, 0}) {
   int vec = pick_vec(F, ldx, ldy, x, y);
+  if (TIER) vec = std::min(vec, pick_vec(F, tier.ldh, ldx, tier.host, x));
   // rows padded to a 16-byte multiple (the 128-byte feature / output pitch):
   // float4 loads, the partial last vector reads pitch padding and stores only
   // its valid floats
   const uint32_t F4 = (F + 3) / 4 * 4;
   if (vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
-      (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0)
+      (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
+      (!TIER || (F4 <= tier.ldh && tier.ldh % 4 == 0 && (uintptr_t)tier.host % 16 == 0)))
     vec = 4;
   const uint32_t nv = (F + vec - 1) / vec;
   const uint32_t last_valid = F - (nv - 1) * vec;
@@ -323,13 +361,13 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   }();
   const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), cap));
   if (vec == 4)
-    return launch_gather_vec<4, MAP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
-                                     map, nv, y, ldy);
+    return launch_gather_vec<4, MAP, TIER>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
+                                     map, nv, y, ldy, tier);
   if (vec == 2)
-    return launch_gather_vec<2, MAP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
-                                     map, nv, y, ldy);
-  return launch_gather_vec<1, MAP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
-                                   map, nv, y, ldy);
+    return launch_gather_vec<2, MAP, TIER>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
+                                     map, nv, y, ldy, tier);
+  return launch_gather_vec<1, MAP, TIER>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
+                                   map, nv, y, ldy, tier);
 }
 
 
@@ -696,21 +734,20 @@ int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx* ctx, const uint32_t* column_offset,
   return NTS_OK;
 }
 
-int nts_hip_gather_rows(nts_hip_ctx* ctx, const float* table, uint64_t ld_table,
-                        const uint32_t* index, const uint32_t* n, uint32_t n_cap,
-                        uint32_t feature_size, float* out, uint64_t ld_out) {
-  NTS_CHECK_ARG(ctx && table && index && out, "NULL argument");
-  NTS_CHECK_ARG(ld_table >= feature_size && ld_out >= feature_size,
-                "leading dimension < feature_size");
-  if (n_cap == 0 || feature_size == 0) return NTS_OK;
-  NTS_HIP_TRY(hipSetDevice(ctx->device));
-  const int vec = pick_vec(feature_size, ld_table, ld_out, table, out);
+}  // extern "C"
+
+template <bool TIER, bool STAGE = false>
+static int gather_rows(nts_hip_ctx* ctx, const float* table, uint64_t ld_table,
+                       const uint32_t* index, const uint32_t* n, uint32_t n_cap,
+                       uint32_t feature_size, float* out, uint64_t ld_out, Tier tier) {
+  int vec = pick_vec(feature_size, ld_table, ld_out, table, out);
+  if (TIER) vec = std::min(vec, pick_vec(feature_size, tier.ldh, ld_out, tier.host, out));
   const uint32_t nv = feature_size / vec;
   const int lpd = nv <= 16 ? 16 : (nv <= 32 ? 32 : 64);
   const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, kAggThreads / lpd), 4096u));
 #define NTS_R(VEC, LPD)                                                                      \
-  hipLaunchKernelGGL((k_gather_rows<VEC, LPD>), dim3(grid), dim3(kAggThreads), 0, ctx->stream, \
-                     table, ld_table, index, n, n_cap, nv, out, ld_out)
+  hipLaunchKernelGGL((k_gather_rows<VEC, LPD, TIER, STAGE>), dim3(grid), dim3(kAggThreads), 0, \
+                     ctx->stream, table, ld_table, index, n, n_cap, nv, out, ld_out, tier)
   if (vec == 4) {
     if (lpd == 16) NTS_R(4, 16); else if (lpd == 32) NTS_R(4, 32); else NTS_R(4, 64);
   } else if (vec == 2) {
@@ -721,6 +758,68 @@ int nts_hip_gather_rows(nts_hip_ctx* ctx, const float* table, uint64_t ld_table,
 #undef NTS_R
   NTS_LAUNCH_CHECK();
   return NTS_OK;
+}
+
+extern "C" {
+
+int nts_hip_gather_rows(nts_hip_ctx* ctx, const float* table, uint64_t ld_table,
+                        const uint32_t* index, const uint32_t* n, uint32_t n_cap,
+                        uint32_t feature_size, float* out, uint64_t ld_out) {
+  NTS_CHECK_ARG(ctx && table && index && out, "NULL argument");
+  NTS_CHECK_ARG(ld_table >= feature_size && ld_out >= feature_size,
+                "leading dimension < feature_size");
+  if (n_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  return gather_rows<false>(ctx, table, ld_table, index, n, n_cap, feature_size, out, ld_out,
+                            Tier{nullptr, nullptr, 0, 0});
+}
+
+int nts_hip_gather_rows_cached(nts_hip_ctx* ctx, const float* cache, uint64_t ld_cache,
+                               const uint32_t* cache_map, const float* host_table,
+                               uint64_t ld_host, const uint32_t* index, const uint32_t* n,
+                               uint32_t n_cap, uint32_t feature_size, float* out,
+                               uint64_t ld_out) {
+  NTS_CHECK_ARG(ctx && cache_map && host_table && index && out, "NULL argument");
+  NTS_CHECK_ARG(ld_cache >= feature_size && ld_host >= feature_size && ld_out >= feature_size,
+                "leading dimension < feature_size");
+  if (n_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  // an empty cache (no HBM rows) still needs a non-NULL, aligned base
+  if (!cache) cache = host_table, ld_cache = ld_host;
+  return gather_rows<true>(ctx, cache, ld_cache, index, n, n_cap, feature_size, out, ld_out,
+                           Tier{cache_map, host_table, ld_host, 0});
+}
+
+int nts_hip_stage_uncached_rows(nts_hip_ctx* ctx, const uint32_t* cache_map,
+                                const float* host_table, uint64_t ld_host, const uint32_t* index,
+                                const uint32_t* n, uint32_t n_cap, uint32_t feature_size,
+                                float* stage, uint64_t ld_stage) {
+  NTS_CHECK_ARG(ctx && cache_map && host_table && index && stage, "NULL argument");
+  NTS_CHECK_ARG(ld_host >= feature_size && ld_stage >= feature_size,
+                "leading dimension < feature_size");
+  if (n_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  return gather_rows<true, true>(ctx, host_table, ld_host, index, n, n_cap, feature_size, stage,
+                                 ld_stage, Tier{cache_map, host_table, ld_host, 0});
+}
+
+int nts_hip_spmm_csc_fwd_cached(nts_hip_ctx* ctx, const uint32_t* column_offset,
+                                const uint32_t* row_indices, const float* weight,
+                                const uint32_t* v, uint32_t v_cap, const float* cache,
+                                uint64_t ld_cache, const uint32_t* cache_map,
+                                const float* host_table, uint64_t ld_host, int host_local,
+                                const uint32_t* x_row_map, uint32_t feature_size, float* y,
+                                uint64_t ldy) {
+  NTS_CHECK_ARG(ctx && column_offset && row_indices && cache_map && host_table && x_row_map && y,
+                "NULL argument");
+  NTS_CHECK_ARG(ld_cache >= feature_size && ld_host >= feature_size && ldy >= feature_size,
+                "leading dimension < feature_size");
+  if (v_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  if (!cache) cache = host_table, ld_cache = ld_host;
+  return launch_gather<true, true>(ctx->stream, column_offset, row_indices, weight, v, v_cap,
+                                   cache, ld_cache, x_row_map, feature_size, y, ldy,
+                                   Tier{cache_map, host_table, ld_host, host_local});
 }
 
 int nts_hip_gather_labels(nts_hip_ctx* ctx, const int64_t* labels, const uint32_t* index,

@@ -34,7 +34,11 @@ EXPORTED = (
     "nts_hip_gemm_f32", "nts_hip_gemm_relu_dropout_f32", "nts_hip_gemm_tn_masked_f32",
     "nts_hip_linear_xent_fwd", "nts_hip_linear_xent_bwd", "nts_hip_linear_xent_train", "nts_hip_adam", "nts_hip_comm_unique_id", "nts_hip_comm_init", "nts_hip_comm_destroy",
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
+    "nts_hip_cache_select", "nts_hip_host_alloc", "nts_hip_host_free",
+    "nts_hip_host_device_pointer", "nts_hip_gather_rows_cached", "nts_hip_spmm_csc_fwd_cached",
+    "nts_hip_stage_uncached_rows",
 )
+NTS_NOT_CACHED = 0xFFFFFFFF
 
 
 class GraphDev(C.Structure):
@@ -105,6 +109,13 @@ def lib() -> C.CDLL:
         "nts_hip_comm_destroy": ([P], I),
         "nts_hip_allreduce_sum_f32": ([P, P, U64, P], I),
         "nts_hip_broadcast_f32": ([P, P, U64, I, P], I),
+        "nts_hip_cache_select": ([P, P, U64, U64, P, P], I),
+        "nts_hip_host_alloc": ([U64, C.POINTER(P)], I),
+        "nts_hip_host_free": ([P], I),
+        "nts_hip_host_device_pointer": ([P, C.POINTER(P)], I),
+        "nts_hip_gather_rows_cached": ([P, P, U64, P, P, U64, P, P, U32, U32, P, U64], I),
+        "nts_hip_spmm_csc_fwd_cached": ([P, P, P, P, P, U32, P, U64, P, P, U64, I, P, U32, P, U64], I),
+        "nts_hip_stage_uncached_rows": ([P, P, P, U64, P, P, U32, U32, P, U64], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

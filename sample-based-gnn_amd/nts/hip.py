@@ -83,6 +83,32 @@ class HipContext:
         check(self.lib.nts_hip_gather_rows(self.h, ptr(table), table.stride(0), ptr(index),
                                            ptr(n_dev), n_cap, F, ptr(out), out.stride(0)))
 
+    def cache_select(self, out_degree, n_vertices: int, n_cache: int, cache_map, cache_ids):
+        check(self.lib.nts_hip_cache_select(self.h, ptr(out_degree), n_vertices, n_cache,
+                                            ptr(cache_map), ptr(cache_ids)))
+
+    def gather_rows_cached(self, cache, cache_map, host: "HostTable", index, n_dev, n_cap, out):
+        F = host.shape[1]
+        check(self.lib.nts_hip_gather_rows_cached(
+            self.h, ptr(cache), cache.stride(0) if cache is not None else host.ld, ptr(cache_map),
+            host.dev_ptr, host.ld, ptr(index), ptr(n_dev), n_cap, F, ptr(out), out.stride(0)))
+
+    def stage_uncached_rows(self, cache_map, host: "HostTable", index, n_dev, n_cap, stage):
+        F = host.shape[1]
+        check(self.lib.nts_hip_stage_uncached_rows(self.h, ptr(cache_map), host.dev_ptr, host.ld,
+                                                   ptr(index), ptr(n_dev), n_cap, F, ptr(stage),
+                                                   stage.stride(0)))
+
+    def spmm_csc_fwd_cached(self, co, ri, w, v_dev, v_cap, cache, cache_map, host: "HostTable",
+                            row_map, y, stage=None):
+        """stage: rows staged by local src id (stage_uncached_rows), else the host table."""
+        F = host.shape[1]
+        spill, ld = (stage.data_ptr(), stage.stride(0)) if stage is not None else (host.dev_ptr, host.ld)
+        check(self.lib.nts_hip_spmm_csc_fwd_cached(
+            self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev), v_cap, ptr(cache),
+            cache.stride(0) if cache is not None else ld, ptr(cache_map), spill, ld,
+            int(stage is not None), ptr(row_map), F, ptr(y), y.stride(0)))
+
     def gather_labels(self, labels, index, n_dev, n_cap, out):
         check(self.lib.nts_hip_gather_labels(self.h, ptr(labels), ptr(index), ptr(n_dev),
                                              n_cap, ptr(out)))
@@ -160,6 +186,38 @@ class HipContext:
     def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
         check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,
                                     beta1, beta2, eps, wd, beta1_t, beta2_t, int(bias_correction)))
+
+
+class HostTable:
+    """fp32 [rows, cols] table in pinned host memory mapped into the device
+    address space (nts_hip_host_alloc), row pitch `ld` floats.  `.tensor` is a
+    CPU view for filling it; `.dev_ptr` is what kernels read (zero-copy)."""
+
+    def __init__(self, rows: int, cols: int, ld: int | None = None):
+        lib = _abi.lib()
+        self.shape = (rows, cols)
+        self.ld = ld or cols
+        nbytes = max(rows * self.ld * 4, 4)
+        hp = C.c_void_p()
+        check(lib.nts_hip_host_alloc(nbytes, C.byref(hp)))
+        self._host = hp.value
+        dp = C.c_void_p()
+        check(lib.nts_hip_host_device_pointer(hp, C.byref(dp)))
+        self.dev_ptr = dp.value
+        buf = (C.c_float * (nbytes // 4)).from_address(self._host)
+        self.tensor = torch.frombuffer(buf, dtype=torch.float32).view(-1, self.ld)[:rows, :cols]
+
+    def close(self):
+        if getattr(self, "_host", None):
+            self.tensor = None
+            _abi.lib().nts_hip_host_free(C.c_void_p(self._host))
+            self._host = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 @dataclass

@@ -349,6 +349,73 @@ void FastSampler::load_feature_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& l
             "nts_hip_gather_rows");
 }
 
+void FastSampler::load_feature_gpu_cache(NtsStream& cs, SampledSubgraph* sg,
+                                         NtsVar& local_feature, const FeatureCache& fc) {
+  sampCSC* top = sg->sampled_sgs[layer - 1];
+  if (!local_feature.defined() || local_feature.size(0) != (int64_t)top->src_size ||
+      local_feature.size(1) != fc.F)
+    local_feature = torch::empty({(int64_t)top->src_size, fc.F}, f32_opts(whole_graph->device));
+  hip_check(nts_hip_gather_rows_cached(cs.ctx(), fc.cache_ptr(), fc.ld,
+                                       dptr<uint32_t>(fc.cache_map), fc.host_dev, fc.ld,
+                                       top->dev_src(), nullptr, top->src_size, (uint32_t)fc.F,
+                                       local_feature.data_ptr<float>(),
+                                       (uint64_t)local_feature.stride(0)),
+            "nts_hip_gather_rows_cached");
+}
+
+FeatureCache::FeatureCache(NtsStream& cs, const FullyRepGraph& g, const NtsVar& table,
+                           uint64_t n_cache_)
+    : n_vertices(g.global_vertices), n_cache(n_cache_), F(table.size(1)) {
+  TORCH_CHECK(table.is_cuda() && table.dtype() == torch::kFloat32 && table.dim() == 2 &&
+                  table.stride(1) == 1 && (uint64_t)table.size(0) == n_vertices,
+              "feature table must be fp32 [V, F] on the GPU");
+  TORCH_CHECK(n_cache <= n_vertices, "n_cache > V");
+  ld = (uint64_t)(F + 31) / 32 * 32;  // 128-byte rows in both tiers
+  void* hp = nullptr;
+  hip_check(nts_hip_host_alloc(n_vertices * ld * sizeof(float), &hp), "nts_hip_host_alloc");
+  host = static_cast<float*>(hp);
+  void* dp = nullptr;
+  hip_check(nts_hip_host_device_pointer(hp, &dp), "nts_hip_host_device_pointer");
+  host_dev = static_cast<const float*>(dp);
+  // spill: the whole table to the host (the reference's pinned
+  // local_feature, core/ntsDataloador.hpp:483), then the hot rows back to HBM
+  TORCH_CHECK(hipMemcpy2DAsync(host, ld * sizeof(float), table.data_ptr<float>(),
+                               (size_t)table.stride(0) * sizeof(float), (size_t)F * sizeof(float),
+                               (size_t)n_vertices, hipMemcpyDeviceToHost,
+                               (hipStream_t)cs.stream()) == hipSuccess,
+              "hipMemcpy2DAsync");
+  cache_map = torch::empty({(int64_t)n_vertices}, u32_opts(g.device));
+  if (n_cache) {
+    cache_ids = torch::empty({(int64_t)n_cache}, u32_opts(g.device));
+    cache = torch::empty({(int64_t)n_cache, (int64_t)ld}, f32_opts(g.device)).narrow(1, 0, F);
+  }
+  hip_check(nts_hip_cache_select(cs.ctx(), dptr<uint32_t>(g.out_degree), n_vertices, n_cache,
+                                 dptr<uint32_t>(cache_map), dptr<uint32_t>(cache_ids)),
+            "nts_hip_cache_select");
+  if (n_cache)  // gater_cpu_cache_feature_and_trans_to_gpu
+    hip_check(nts_hip_gather_rows(cs.ctx(), table.data_ptr<float>(), (uint64_t)table.stride(0),
+                                  dptr<uint32_t>(cache_ids), nullptr, (uint32_t)n_cache,
+                                  (uint32_t)F, cache.data_ptr<float>(), ld),
+              "nts_hip_gather_rows");
+  cs.synchronize();
+}
+
+void FeatureCache::aggregate(nts_hip_ctx* ctx, const sampCSC* s, const uint32_t* v_dev,
+                             uint32_t v_cap, const uint32_t* s_dev, uint32_t s_cap, float* stage,
+                             float* y, uint64_t ldy) const {
+  hip_check(nts_hip_stage_uncached_rows(ctx, dptr<uint32_t>(cache_map), host_dev, ld,
+                                        s->dev_src(), s_dev, s_cap, (uint32_t)F, stage, ld),
+            "nts_hip_stage_uncached_rows");
+  hip_check(nts_hip_spmm_csc_fwd_cached(ctx, s->dev_c_o(), s->dev_r_i(), s->dev_e_w_f(), v_dev,
+                                        v_cap, cache_ptr(), ld, dptr<uint32_t>(cache_map), stage,
+                                        ld, 1, s->dev_src(), (uint32_t)F, y, ldy),
+            "nts_hip_spmm_csc_fwd_cached");
+}
+
+FeatureCache::~FeatureCache() {
+  if (host) (void)nts_hip_host_free(host);
+}
+
 void FastSampler::load_label_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_label,
                                  const NtsVar& global_label) {
   sampCSC* s0 = sg->sampled_sgs[0];
@@ -364,13 +431,26 @@ void FastSampler::load_label_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& loc
 namespace op {
 
 SingleGPUAllSampleGraphOp::SingleGPUAllSampleGraphOp(SampledSubgraph* sgs, FullyRepGraph* graph,
-                                                     int layer_, NtsStream* cs, bool gather)
-    : subgraphs(sgs), layer(layer_), cuda_stream(cs), gather_from_table(gather) {
+                                                     int layer_, NtsStream* cs, bool gather,
+                                                     const FeatureCache* fc)
+    : subgraphs(sgs), layer(layer_), cuda_stream(cs), gather_from_table(gather),
+      feature_cache(fc) {
   (void)graph;
+  TORCH_CHECK(!fc || gather, "a feature cache needs gather_from_table");
 }
 
 NtsVar SingleGPUAllSampleGraphOp::forward(NtsVar& f_input) {
   sampCSC* sg = subgraphs->sampled_sgs[layer];
+  if (feature_cache) {  // two-tier table: f_input only carries the width
+    const FeatureCache& fc = *feature_cache;
+    NtsVar f_output = row_padded_empty((int64_t)sg->v_size, fc.F, cuda_stream->device());
+    NtsVar stage = torch::empty({(int64_t)std::max<uint32_t>(sg->src_size, 1), (int64_t)fc.ld},
+                                f32_opts(cuda_stream->device()));
+    fc.aggregate(cuda_stream->ctx(), sg, nullptr, sg->v_size, nullptr, sg->src_size,
+                 stage.data_ptr<float>(), f_output.data_ptr<float>(), (uint64_t)f_output.stride(0));
+    if (output_requires_grad) f_output.set_requires_grad(true);
+    return f_output;
+  }
   TORCH_CHECK(f_input.is_cuda() && f_input.dtype() == torch::kFloat32 && f_input.dim() == 2 &&
                   f_input.stride(1) == 1,
               "graph op input must be a row-major fp32 CUDA matrix");

@@ -49,6 +49,14 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     Fp.copy_(F);
     F = Fp;
   }
+  if (cfg.cache_rate >= 0.0) {
+    TORCH_CHECK(cfg.cache_rate < 1.0 || cfg.cache_rate == 1.0, "cache_rate must be in [0, 1]");
+    TORCH_CHECK(!cfg.fuse_linear, "the feature cache is not supported with fuse_linear");
+    const uint64_t V = graph->global_vertices;
+    const uint64_t n_cache = std::min<uint64_t>(V, (uint64_t)(cfg.cache_rate * (double)V));
+    fcache = std::make_unique<FeatureCache>(*cs, *graph, F, n_cache);
+    F = torch::empty({0, F.size(1)}, f32_opts(graph->device));  // HBM table released
+  }
   if (cfg.shuffle) {  // shuffle_vec (toolkits/GCN_SAMPLE_GPU.hpp:175-180): mt19937(2000)
     std::mt19937 gen(2000);
     std::shuffle(train_nids.begin(), train_nids.end(), gen);
@@ -92,6 +100,10 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     if (early_)
       pre_y_[i] = row_padded_empty((int64_t)sampler->ssgs[i]->sampled_sgs[L - 1]->v_cap,
                                    F.size(1), graph->device);
+    if (early_ && fcache)
+      stage_[i] = torch::empty({(int64_t)std::max<uint32_t>(sampler->ssgs[i]->sampled_sgs[L - 1]->s_cap, 1),
+                                (int64_t)fcache->ld},
+                               f32_opts(graph->device));
   }
   init_nn();
 }
@@ -149,11 +161,16 @@ void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
       (void)hipEventRecord(evp->first, (hipStream_t)st.stream());
     }
     NtsVar& y = pre_y_[slot];
-    hip_check(nts_hip_spmm_csc_fwd(st.ctx(), s->dev_c_o(), s->dev_r_i(), s->dev_e_w_f(),
-                                   dptr<uint32_t>(s->sizes), s->v_cap, F.data_ptr<float>(),
-                                   (uint64_t)F.stride(0), s->dev_src(), (uint32_t)F.size(1),
-                                   y.data_ptr<float>(), (uint64_t)y.stride(0)),
-              "nts_hip_spmm_csc_fwd(early)");
+    if (fcache)
+      fcache->aggregate(st.ctx(), s, dptr<uint32_t>(s->sizes), s->v_cap,
+                        dptr<uint32_t>(s->sizes) + 2, s->s_cap, stage_[slot].data_ptr<float>(),
+                        y.data_ptr<float>(), (uint64_t)y.stride(0));
+    else
+      hip_check(nts_hip_spmm_csc_fwd(st.ctx(), s->dev_c_o(), s->dev_r_i(), s->dev_e_w_f(),
+                                     dptr<uint32_t>(s->sizes), s->v_cap, F.data_ptr<float>(),
+                                     (uint64_t)F.stride(0), s->dev_src(), (uint32_t)F.size(1),
+                                     y.data_ptr<float>(), (uint64_t)y.stride(0)),
+                "nts_hip_spmm_csc_fwd(early)");
     if (evp) (void)hipEventRecord(evp->second, (hipStream_t)st.stream());
   }
   TORCH_CHECK(hipEventRecord(ready_[slot], (hipStream_t)st.stream()) == hipSuccess,
@@ -247,7 +264,12 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
   const int L = (int)P.size();
   std::vector<NtsVar> acts;
   NtsVar X0;
-  if (!cfg.fused_gather) sampler->load_feature_gpu(*cs, sg, X0, F);
+  if (!cfg.fused_gather) {
+    if (fcache)
+      sampler->load_feature_gpu_cache(*cs, sg, X0, *fcache);
+    else
+      sampler->load_feature_gpu(*cs, sg, X0, F);
+  }
   int l0 = 0;
   NtsVar X;
   if (pre_y) {  // bottom graph op already ran on the sampling stream (issue())
@@ -306,7 +328,8 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       continue;
     }
     if (bottom && cfg.fused_gather)
-      Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true);
+      Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true,
+                                                        fcache.get());
     else
       Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(X, sg, graph.get(), hop, cs.get(), false);
     if (bottom) {

@@ -27,6 +27,10 @@ struct GCNConfig {
   bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
+  // CACHE_RATE in [0, 1): the feature table moves to pinned host memory and
+  // the rows of the cache_rate * V highest-degree vertices stay in HBM
+  // (GS_SAMPLE_PD_CACHE's placement); < 0: the whole table in HBM
+  double cache_rate = -1.0;
   int64_t seed = 2000;
 };
 
@@ -56,6 +60,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   std::unique_ptr<NtsStream> cs;  // training stream
   std::unique_ptr<NtsStream> ss;  // sampling stream (pipeline) — own scratch arena
   std::unique_ptr<FastSampler> sampler;
+  std::unique_ptr<FeatureCache> fcache;  // two-tier feature table (cache_rate)
   std::vector<Parameter*> P;
   ctx::NtsContext ctx;
   // statistics
@@ -81,6 +86,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   static constexpr int kSlots = 3;  // sampler slots when pipelined (see the constructor)
   int nslots_ = 1;
   NtsVar pre_y_[kSlots];
+  NtsVar stage_[kSlots];  // early aggregation + feature cache: staged spill rows
   hipEvent_t ready_[kSlots] = {nullptr, nullptr, nullptr};
   bool early_ = false;
   uint64_t dropout_calls_ = 0;  // Philox offset of the fused dropout masks

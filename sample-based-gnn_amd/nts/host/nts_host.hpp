@@ -151,6 +151,38 @@ class SampledSubgraph {
 };
 
 // ---------------------------------------------------------------------------
+// HBM feature cache + host-pinned spill (GS_SAMPLE_PD_CACHE:
+// determine_cache_node_idx / cache_high_degree / mark_cache_node /
+// gater_cpu_cache_feature_and_trans_to_gpu, toolkits/GS_SAMPLE_PD_CACHE.hpp:1019-1112).
+// The full table moves to pinned host memory (device-mapped, zero-copy reads);
+// the rows of the n_cache highest-out-degree vertices stay in HBM.
+// ---------------------------------------------------------------------------
+class FeatureCache {
+ public:
+  // table: fp32 [V, F] on the GPU (any row pitch); n_cache <= V rows cached
+  FeatureCache(NtsStream& cs, const FullyRepGraph& g, const NtsVar& table, uint64_t n_cache);
+  ~FeatureCache();
+  FeatureCache(const FeatureCache&) = delete;
+  FeatureCache& operator=(const FeatureCache&) = delete;
+  uint64_t n_vertices = 0, n_cache = 0;
+  int64_t F = 0;
+  uint64_t ld = 0;               // row pitch (floats) of both tiers
+  float* host = nullptr;         // pinned host table [V, ld] (owned)
+  const float* host_dev = nullptr;  // its device-visible address
+  NtsVar cache;                  // HBM [n_cache, F] (pitch ld), undefined when n_cache == 0
+  NtsVar cache_map;              // u32 [V]: slot or NTS_NOT_CACHED
+  NtsVar cache_ids;              // u32 [n_cache]
+  const float* cache_ptr() const { return cache.defined() ? cache.data_ptr<float>() : nullptr; }
+  // the fused bottom graph op on the two-tier table: the layer's non-cached
+  // source rows are staged once into `stage` ([s_cap, ld] floats, HBM), then
+  // Y = A X reads cached rows from the cache and the others from the stage.
+  // v_dev / s_dev: device v_size / src_size (NULL: v_cap / s_cap are exact).
+  void aggregate(nts_hip_ctx* ctx, const sampCSC* s, const uint32_t* v_dev, uint32_t v_cap,
+                 const uint32_t* s_dev, uint32_t s_cap, float* stage, float* y,
+                 uint64_t ldy) const;
+};
+
+// ---------------------------------------------------------------------------
 // FastSampler (GPU form): sample_gpu_fast runs every hop on the device, with
 // one D2H copy of the layer sizes per batch.
 // ---------------------------------------------------------------------------
@@ -194,6 +226,10 @@ class FastSampler {
                         const NtsVar& global_feature);
   void load_label_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_label,
                       const NtsVar& global_label);
+  // load_feature_gpu_cache (core/ntsFastSampler.hpp:263-317): cached rows from
+  // HBM, the rest zero-copy from the pinned host table, in one kernel
+  void load_feature_gpu_cache(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_feature,
+                              const FeatureCache& cache);
 
  private:
   torch::Tensor dev_nids_;  // device copy of sample_nids
@@ -226,8 +262,11 @@ class ntsGraphOp {
 // fetched through the layer's `source` (fused load_feature_gpu + aggregate).
 class SingleGPUAllSampleGraphOp : public ntsGraphOp {
  public:
+  // feature_cache: with gather_from_table, rows come from the two-tier table
+  // (HBM cache + host spill) instead of f_input
   SingleGPUAllSampleGraphOp(SampledSubgraph* subgraphs, FullyRepGraph* graph, int layer,
-                            NtsStream* cs, bool gather_from_table = false);
+                            NtsStream* cs, bool gather_from_table = false,
+                            const FeatureCache* feature_cache = nullptr);
   NtsVar forward(NtsVar& f_input) override;
   NtsVar backward(NtsVar& f_output_grad) override;
 
@@ -235,6 +274,7 @@ class SingleGPUAllSampleGraphOp : public ntsGraphOp {
   int layer;
   NtsStream* cuda_stream;
   bool gather_from_table;
+  const FeatureCache* feature_cache;
 };
 
 // SingleGPUSampleGraphOp (core/ntsSingleGPUSampleGraphOp.hpp:50-176): same

@@ -573,3 +573,73 @@ def test_linear_xent_train(hip, n, K, C, pad):
     torch.testing.assert_close(loss.double(), ref.detach(), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dY.double(), Yr.grad, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(dW.double(), Wr.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("rate", [0.0, 0.05, 0.37, 1.0])
+@pytest.mark.parametrize("F", [41, 602])
+def test_feature_cache_two_tier(hip, cora, rate, F):
+    """HBM cache + host-pinned spill (GS_SAMPLE_PD_CACHE, load_feature_gpu_cache):
+    the selection equals the oracle's degree order, and both the two-tier row
+    gather and the fused two-tier aggregation are bit-identical to the
+    full-table paths for every cache size."""
+    from nts.hip import HostTable
+    V, src, dst = cora
+    g = _graph(hip, V, src, dst)
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    n_cache = int(round(rate * V))
+    cmap = torch.empty(V, dtype=torch.int32, device=DEV)
+    cids = torch.empty(max(n_cache, 1), dtype=torch.int32, device=DEV)
+    hip.cache_select(g.out_degree, V, n_cache, cmap, cids if n_cache else None)
+    torch.cuda.synchronize()
+    cmap_ref, cids_ref = orc.cache_select(out_d, n_cache)
+    assert np.array_equal(_np_u32(cmap), cmap_ref)
+    assert np.array_equal(_np_u32(cids)[:n_cache], cids_ref)
+    # host table with a 128-byte pitch (the bench layout), cache filled by gather_rows
+    rng = np.random.default_rng(F + 1)
+    table = rng.standard_normal((V, F)).astype(np.float32)
+    ld = (F + 31) // 32 * 32
+    host = HostTable(V, F, ld)
+    host.tensor.copy_(torch.from_numpy(table))
+    cache = None
+    if n_cache:
+        cache = torch.empty((n_cache, ld), device=DEV)[:, :F]
+        nc = torch.tensor([n_cache], dtype=torch.int32, device=DEV)
+        hip.gather_rows(_t(table), cids, nc, n_cache, cache)
+    # sampled layers (PHILOX) and the reference values
+    seeds = np.arange(0, V, 7, dtype=np.uint32)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX,
+                    order_mode=orc.ORDER_DRAW)
+    l0, l1 = o.sample(seeds)
+    X = orc.get_feature(l1["source"], table)
+    Y_ref = orc.fuse_fwd(l1, X, out_d, in_d)
+    s, v = l1["src_size"], l1["v_size"]
+    # two-tier row gather == get_feature (== the oracle's two-tier restatement)
+    x0 = torch.full((s, F), float("nan"), device=DEV)
+    n = torch.tensor([s], dtype=torch.int32, device=DEV)
+    hip.gather_rows_cached(cache, cmap, host, _t(l1["source"]), n, s, x0)
+    # fused two-tier aggregation == MiniBatchFuseOp::forward
+    co, ri, wf = _t(l1["column_offset"]), _t(l1["row_indices"]), _t(l1["edge_weight_forward"])
+    vdev = torch.tensor([v], dtype=torch.int32, device=DEV)
+    y = torch.full((v, ld), 5.0, device=DEV)
+    hip.spmm_csc_fwd_cached(co, ri, wf, vdev, v, cache, cmap, host, _t(l1["source"]), y[:, :F])
+    torch.cuda.synchronize()
+    assert np.array_equal(x0.cpu().numpy(), X)
+    if n_cache:
+        assert np.array_equal(
+            orc.get_feature_cached(l1["source"], cache.cpu().numpy(), cmap_ref, table), X)
+    assert np.array_equal(y[:, :F].cpu().numpy(), Y_ref)
+    assert (y[:, F:] == 5.0).all()
+    # spilled rows staged once per batch by local id, then the fused aggregation
+    stage = torch.full((s, ld), float("nan"), device=DEV)
+    hip.stage_uncached_rows(cmap, host, _t(l1["source"]), n, s, stage[:, :F])
+    y2 = torch.empty((v, F), device=DEV)
+    hip.spmm_csc_fwd_cached(co, ri, wf, vdev, v, cache, cmap, host, _t(l1["source"]), y2,
+                            stage=stage[:, :F])
+    torch.cuda.synchronize()
+    cold = cmap_ref[l1["source"]] == orc.NOT_CACHED
+    st = stage[:, :F].cpu().numpy()
+    assert np.array_equal(st[cold], X[cold])
+    assert np.isnan(st[~cold]).all()  # cached rows are never staged
+    assert np.array_equal(y2.cpu().numpy(), Y_ref)
+    host.close()

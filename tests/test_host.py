@@ -182,3 +182,22 @@ def test_fused_activation_matches_torch_ops(E, graph):
     b.synchronize()
     for x, y in zip(a.weights(), b.weights()):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("rate", [0.0, 0.25, 1.0])
+@pytest.mark.parametrize("early,fused", [(False, True), (True, True), (False, False)])
+def test_feature_cache_training_is_identical(E, graph, rate, early, fused):
+    """Features in pinned host memory with the highest-degree rows cached in
+    HBM (GS_SAMPLE_PD_CACHE placement, cache_rate) train to the same weights
+    as the all-HBM table: the two-tier reads change where rows come from, not
+    their values (fused graph op, early aggregation, and load_feature_gpu_cache)."""
+    kw = dict(early_aggregate=early, fused_gather=fused)
+    a, *_ = _driver(E, graph, 602, 7, [602, 32, 7], [10, 5], 200, drop=0.5, **kw)
+    b, *_ = _driver(E, graph, 602, 7, [602, 32, 7], [10, 5], 200, drop=0.5, cache_rate=rate, **kw)
+    for _ in range(3):
+        a.train_batch()
+        b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)

@@ -211,3 +211,23 @@ def test_fuse_fwd_matches_numpy_float32(cora):
             acc = acc + (G[ci[j]] * wb[j]).astype(np.float32)
         ref[r] = acc
     np.testing.assert_array_equal(Gin, ref)
+
+
+def test_cache_select_oracle_degree_order():
+    """cache_high_degree + mark_cache_node restated (GS_SAMPLE_PD_CACHE.hpp:1019-1047):
+    the cached set is the n highest out-degrees, slots follow (degree desc, id asc),
+    and the two-tier gather returns exactly get_feature's rows."""
+    rng = np.random.default_rng(5)
+    deg = rng.integers(1, 20, 500).astype(np.uint32)
+    for n in (0, 1, 37, 500):
+        cmap, ids = orc.cache_select(deg, n)
+        assert ids.size == n and np.array_equal(cmap[ids], np.arange(n, dtype=np.uint32))
+        assert (cmap != orc.NOT_CACHED).sum() == n
+        if 0 < n < 500:
+            hot = deg[ids]
+            assert hot.min() >= deg[cmap == orc.NOT_CACHED].max()
+            assert all(hot[i] > hot[i + 1] or ids[i] < ids[i + 1] for i in range(n - 1))
+        table = rng.standard_normal((500, 9)).astype(np.float32)
+        idx = rng.integers(0, 500, 300).astype(np.uint32)
+        cache = table[ids] if n else np.zeros((0, 9), np.float32)
+        assert np.array_equal(orc.get_feature_cached(idx, cache, cmap, table), table[idx])
