@@ -429,7 +429,7 @@ __device__ __forceinline__ void wres_mfma(const float* __restrict__ bb, const fl
   }
 }
 
-template <int NCOL, int AVEC, bool EPI>
+template <int NCOL, int AVEC, bool EPI, int DEPTH>
 __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
     int M, int N, int K, int nkb, const float* __restrict__ A, uint64_t lda,
     const float* __restrict__ B, uint64_t ldb, float* __restrict__ C, uint64_t ldc, int ncb,
@@ -482,32 +482,34 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
     for (int rt = 0; rt < kWresRT; ++rt)
 #pragma unroll
       for (int j = 0; j < CT; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // full k-blocks (32 (kb+1) <= K) are read unmasked, two register sets
-    // alternate so that the next block's loads are in flight during the
-    // current block's 64 MFMAs; the partial last block is read masked.
+    // full k-blocks (32 (kb+1) <= K) are read unmasked into DEPTH rotating
+    // register sets: the loads of blocks kb+1 .. kb+DEPTH-1 are in flight
+    // during block kb's MFMAs; the partial last block is read masked.
     const int nfull = K / 32;
-    float a0[kWresRT][8], a1[kWresRT][8], at[kWresRT][8];
+    float a[DEPTH][kWresRT][8], at[kWresRT][8];
     const float* bb = sB + 8 * g * NCOL + 4 * i;
     const bool tail = nfull < nkb;
     if (tail) wres_load_tail(arow, K, nfull, g, at);
-    if (nfull > 0) wres_load_a<AVEC>(arow, 0, g, a0);
+    if (nfull > 0) {
+#pragma unroll
+      for (int d = 0; d + 1 < DEPTH; ++d) wres_load_a<AVEC>(arow, min(d, nfull - 1), g, a[d]);
+    }
     int kb = 0;
-    for (; kb + 2 <= nfull; kb += 2) {
-      wres_load_a<AVEC>(arow, kb + 1, g, a1);
-      __builtin_amdgcn_sched_barrier(0);
-      wres_mfma<NCOL>(bb + 32 * kb * NCOL, a0, acc);
-      __builtin_amdgcn_sched_barrier(0);
-      // unconditional (clamped) so that every path through the loop has the
-      // same queue of loads: the compiler then waits with a count, not vmcnt(0)
-      wres_load_a<AVEC>(arow, min(kb + 2, nfull - 1), g, a0);
-      __builtin_amdgcn_sched_barrier(0);
-      wres_mfma<NCOL>(bb + 32 * (kb + 1) * NCOL, a1, acc);
-      __builtin_amdgcn_sched_barrier(0);
+    for (; kb + DEPTH <= nfull; kb += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        // unconditional (clamped) so that every path through the loop has the
+        // same queue of loads: the compiler then waits with a count, not vmcnt(0)
+        wres_load_a<AVEC>(arow, min(kb + d + DEPTH - 1, nfull - 1), g, a[(d + DEPTH - 1) % DEPTH]);
+        __builtin_amdgcn_sched_barrier(0);
+        wres_mfma<NCOL>(bb + 32 * (kb + d) * NCOL, a[d], acc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
-    if (kb < nfull) {  // odd number of full blocks: a0 holds block kb
-      wres_mfma<NCOL>(bb + 32 * kb * NCOL, a0, acc);
-      ++kb;
-    }
+    // remaining full blocks: a[r] holds block kb + r
+#pragma unroll
+    for (int r = 0; r + 1 < DEPTH; ++r)
+      if (kb + r < nfull) wres_mfma<NCOL>(bb + 32 * (kb + r) * NCOL, a[r], acc);
     if (tail) {
       wres_mask_tail(K, nfull, g, at);
       wres_mfma<NCOL>(bb + 32 * nfull * NCOL, at, acc);
@@ -571,18 +573,26 @@ constexpr int kTbKS = 16;                       // k rows per step
 constexpr int kTbLDY = 656;
 constexpr int kTbLDG = 132;
 
+// NB = 3 (STAGGER): waves 4-7 run half a k-step behind waves 0-3 (they
+// finish step st-1's second half after the barrier that ends step st-1), so
+// the two waves sharing a SIMD are not in lockstep at the barrier and the LDS
+// stores (MI355X_MICROARCH.md, workgroup rule 9).  A third LDS buffer keeps
+// step st-1 readable while step st+1 is stored.  Every output element keeps
+// the same k order: results are bit-identical to NB = 2.
+template <int NB>
 struct TbSmem {
-  float y[2][kTbKS * kTbLDY];
-  float g[2][kTbKS * kTbLDG];
+  float y[NB][kTbKS * kTbLDY];
+  float g[NB][kTbKS * kTbLDG];
 };
 
-template <bool BMASK, int AVEC>
+template <bool BMASK, int AVEC, bool STAGGER>
 __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
     int M, int N, int K, const float* __restrict__ A, uint64_t lda, const float* __restrict__ B,
     uint64_t ldb, float* __restrict__ C, uint64_t ldc, int kchunk, uint64_t split_stride,
     int nrg, int ncb, GemmExtra ex) {
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
-  TbSmem& sm = *reinterpret_cast<TbSmem*>(smem_raw);
+  constexpr int NB = STAGGER ? 3 : 2;
+  TbSmem<NB>& sm = *reinterpret_cast<TbSmem<NB>*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int rg = blockIdx.x % nrg;
@@ -653,11 +663,12 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
   for (int rt = 0; rt < kTbRT; ++rt)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](const float* sy, const float* sg) {
+  // k sub-steps t0 .. t1-1 of one staged step (4 k each)
+  auto compute = [&](const float* sy, const float* sg, int t0, int t1) {
     const float* ya = sy + g * kTbLDY + wv * 16 * kTbRT + kTbRT * i;
     const float* gb = sg + g * kTbLDG + 8 * i;
 #pragma unroll
-    for (int t = 0; t < kTbKS / 4; ++t) {
+    for (int t = t0; t < t1; ++t) {
       float a[kTbRT];
 #pragma unroll
       for (int rt = 0; rt < kTbRT; ++rt) a[rt] = ya[4 * t * kTbLDY + rt];
@@ -674,19 +685,37 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
       }
     }
   };
+  constexpr int TH = kTbKS / 8;  // half a step
+  const bool lag = STAGGER && wv >= kTbWaves / 2;
   if (nsteps > 0) {
     load(0);
     store(0, sm.y[0], sm.g[0]);
   }
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
-    const int cur = st & 1;
+    const int cur = st % NB, nxt = (st + 1) % NB, prv = (st + NB - 1) % NB;
     load(st + 1);  // clamped rows past the chunk; masked (zero) when stored
     __builtin_amdgcn_sched_barrier(0);
-    compute(sm.y[cur], sm.g[cur]);
+    if constexpr (!STAGGER) {
+      compute(sm.y[cur], sm.g[cur], 0, 2 * TH);
+    } else {
+      // two half steps through one (not unrolled) body: lead waves cur/0, cur/TH;
+      // lagging waves prv/TH (none at st = 0), cur/0
+#pragma unroll 1
+      for (int ph = 0; ph < 2; ++ph) {
+        if (lag && ph == 0 && st == 0) continue;
+        const int b = (lag && ph == 0) ? prv : cur;
+        const int t0 = lag ? (ph == 0 ? TH : 0) : ph * TH;
+        compute(sm.y[b] + 4 * t0 * kTbLDY, sm.g[b] + 4 * t0 * kTbLDG, 0, TH);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
-    if (st + 1 < nsteps) store(st + 1, sm.y[cur ^ 1], sm.g[cur ^ 1]);
+    if (st + 1 < nsteps) store(st + 1, sm.y[nxt], sm.g[nxt]);
     __syncthreads();
+  }
+  if (lag && nsteps > 0) {
+    const int last = (nsteps - 1) % NB;
+    compute(sm.y[last], sm.g[last], TH, 2 * TH);
   }
   // acc[rt][j][v] = C[r0 + 80 wv + 5 (4 g + v) + rt][n0 + 8 i + j]
   float* Cb = C + (uint64_t)split * split_stride;
@@ -804,7 +833,11 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
   const int kchunk = ((K + splits - 1) / splits + kTbKS - 1) / kTbKS * kTbKS;
   splits = (K + kchunk - 1) / kchunk;
   const dim3 grid(nrg * ncb * splits);
-  const size_t lds = sizeof(TbSmem);
+  static const bool stagger = [] {
+    const char* e = getenv("NTS_TN_STAGGER");
+    return !(e && e[0] == '0');
+  }();
+  const size_t lds = stagger ? sizeof(TbSmem<3>) : sizeof(TbSmem<2>);
   const bool a4 = lda % 4 == 0 && lda >= (uint64_t)(M + 3) / 4 * 4 && (uintptr_t)A % 16 == 0;
   const bool a2 = M % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0;
   const bool direct = splits == 1;
@@ -816,16 +849,22 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
     out = (float*)ctx->scratch;
     ldo = N;
   }
-#define NTS_TB(AV)                                                                              \
+#define NTS_TB_S(AV, SG)                                                                        \
   do {                                                                                          \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_big<BMASK, AV>),   \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_big<BMASK, AV, SG>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
-    hipLaunchKernelGGL((k_gemm_tn_big<BMASK, AV>), grid, dim3(kTbWaves * 64), lds, st, M, N, K, \
-                       A, lda, B, ldb, out, ldo, kchunk, direct ? (uint64_t)0 : stride, nrg,    \
+    hipLaunchKernelGGL((k_gemm_tn_big<BMASK, AV, SG>), grid, dim3(kTbWaves * 64), lds, st, M, N, \
+                       K, A, lda, B, ldb, out, ldo, kchunk, direct ? (uint64_t)0 : stride, nrg, \
                        ncb, ex);                                                                \
+  } while (0)
+#define NTS_TB(AV)                               \
+  do {                                           \
+    if (stagger) NTS_TB_S(AV, true);             \
+    else NTS_TB_S(AV, false);                    \
   } while (0)
   if (a4) NTS_TB(4); else if (a2) NTS_TB(2); else NTS_TB(1);
 #undef NTS_TB
+#undef NTS_TB_S
   NTS_LAUNCH_CHECK();
   if (direct) return NTS_OK;
   return sum_splits(st, out, splits, stride, M, N, C, ldc);
@@ -876,12 +915,22 @@ static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const floa
   if (lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
   else if (lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
   const int vs = (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) ? 1 : 0;
-#define NTS_WRES(NC, AV)                                                                        \
+  static const int depth = [] {
+    const char* e = getenv("NTS_WRES_DEPTH");
+    return e ? std::max(2, std::min(4, atoi(e))) : 2;
+  }();
+#define NTS_WRES_D(NC, AV, D)                                                                   \
   do {                                                                                          \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_wres<NC, AV, EPI>),   \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_wres<NC, AV, EPI, D>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
-    hipLaunchKernelGGL((k_gemm_wres<NC, AV, EPI>), dim3(grid), dim3(wres_threads<NC>()), lds, st, \
-                       M, N, K, nkb, A, lda, B, ldb, C, ldc, ncb, vs, ex);                      \
+    hipLaunchKernelGGL((k_gemm_wres<NC, AV, EPI, D>), dim3(grid), dim3(wres_threads<NC>()), lds, \
+                       st, M, N, K, nkb, A, lda, B, ldb, C, ldc, ncb, vs, ex);                  \
+  } while (0)
+#define NTS_WRES(NC, AV)                                       \
+  do {                                                         \
+    if (depth == 3) NTS_WRES_D(NC, AV, 3);                     \
+    else if (depth == 4) NTS_WRES_D(NC, AV, 4);                \
+    else NTS_WRES_D(NC, AV, 2);                                \
   } while (0)
   if (ncol == 128) {
     if (avec == 4) NTS_WRES(128, 4); else if (avec == 2) NTS_WRES(128, 2); else NTS_WRES(128, 1);
@@ -889,6 +938,7 @@ static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const floa
     if (avec == 4) NTS_WRES(64, 4); else if (avec == 2) NTS_WRES(64, 2); else NTS_WRES(64, 1);
   }
 #undef NTS_WRES
+#undef NTS_WRES_D
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }
