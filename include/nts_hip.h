@@ -284,8 +284,9 @@ int nts_hip_gemm_f32(nts_hip_ctx *ctx, int trans_a, int M, int N, int K, const f
  *   torch::dropout(torch::relu(x.matmul(W)), drop_rate, training)
  *   (toolkits/GCN_SAMPLE_GPU.hpp:252-266).  Inverted dropout: kept elements
  *   are scaled by 1/(1-p); keep(row, col) comes from Philox4x32-10 keyed by
- *   `seed`, counter {row/4, col, offset} (word row%4 >= p*2^32), so the mask
- *   is reproducible and never stored.  p == 0: plain relu (eval). */
+ *   `seed`, counter {row/4, col/2, offset}: 16 bits per element (word row%4,
+ *   low half for even col, high half for odd col) >= floor(p*2^16), so the
+ *   mask is reproducible and never stored.  p == 0: plain relu (eval). */
 int nts_hip_gemm_relu_dropout_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *A,
                                   uint64_t lda, const float *B, uint64_t ldb, float *C,
                                   uint64_t ldc, float p, uint64_t seed, uint64_t offset);

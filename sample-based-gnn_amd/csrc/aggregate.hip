@@ -559,19 +559,19 @@ __global__ __launch_bounds__(kAggThreads, 2) void k_agg_gemm(AgArgs a) {
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
       const uint32_t r4 = tile * kAgTM + 16 * rt + 4 * g;
+      uint4 rnd = make_uint4(0u, 0u, 0u, 0u);  // columns col0, col0 + 1: one call
+      if constexpr (ACT) rnd = dropout_words((uint64_t)r4, col0, a.seed, a.offset);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t col = col0 + j;
         if (!(j ? col_ok1 : col_ok0)) continue;
         float o[4] = {acc[rt][j][0], acc[rt][j][1], acc[rt][j][2], acc[rt][j][3]};
         if constexpr (ACT) {
-          const uint4 rnd = philox4x32_10(
-              make_uint4(r4 >> 2, col, (uint32_t)a.offset, (uint32_t)(a.offset >> 32)),
-              make_uint2((uint32_t)a.seed, (uint32_t)(a.seed >> 32)));
           const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
           for (int v = 0; v < 4; ++v)
-            o[v] = (wd[v] >= a.keep_threshold && o[v] > 0.f) ? o[v] * a.scale : 0.f;
+            o[v] = (dropout_bits(wd[v], col) >= a.keep_threshold && o[v] > 0.f) ? o[v] * a.scale
+                                                                                 : 0.f;
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v)
@@ -658,13 +658,8 @@ int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx* ctx, const uint32_t* column_offset,
   NTS_HIP_TRY(hipSetDevice(ctx->device));
   AgArgs a{column_offset, row_indices, weight, v, v_cap, x, ldx, x_row_map, F, W, out_size,
            y, ldy, z, ldz, LDP, 0u, 1.f, seed, offset};
-  if (p >= 1.f) {
-    a.keep_threshold = 0xFFFFFFFFu;
-    a.scale = 0.f;
-  } else {
-    a.keep_threshold = (uint32_t)std::min((double)p * 4294967296.0, 4294967295.0);
-    a.scale = 1.0f / (1.0f - p);
-  }
+  a.keep_threshold = dropout_threshold(p);
+  a.scale = p >= 1.f ? 0.f : 1.0f / (1.0f - p);
   const size_t lds = (size_t)kAgTM * LDP * sizeof(float);
   const uint32_t tiles = (v_cap + kAgTM - 1) / kAgTM;
   const uint32_t grid = std::max(1u, std::min(tiles, 512u));  // 2 blocks per CU

@@ -68,6 +68,24 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
   return c;
 }
 
+// Dropout keep bits shared by every fused relu/dropout epilogue: element
+// (row, col) takes 16 bits of Philox4x32-10 at counter {row/4, col/2,
+// offset_lo, offset_hi} under key `seed` — word row % 4, its low half for an
+// even col and its high half for an odd col — and is kept iff those bits are
+// >= floor(p * 65536).  One generator call covers a 4 x 2 element block.
+__device__ __forceinline__ uint4 dropout_words(uint64_t row, uint32_t col, uint64_t seed,
+                                               uint64_t offset) {
+  return philox4x32_10(
+      make_uint4((uint32_t)(row >> 2), col >> 1, (uint32_t)offset, (uint32_t)(offset >> 32)),
+      make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+}
+__device__ __forceinline__ uint32_t dropout_bits(uint32_t word, uint32_t col) {
+  return (col & 1u) ? (word >> 16) : (word & 0xFFFFu);
+}
+inline uint32_t dropout_threshold(double p) {
+  return p >= 1.0 ? 65536u : (uint32_t)std::min(p * 65536.0, 65536.0);
+}
+
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 inline uint32_t ceil_log2(uint64_t x) {
   uint32_t b = 0;

@@ -315,14 +315,12 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
       const int64_t r4 = wrow0 + 8 * g + 4 * h;
       float o[4] = {acc[t][4 * g], acc[t][4 * g + 1], acc[t][4 * g + 2], acc[t][4 * g + 3]};
       if constexpr (EPI) {
-        const uint4 rnd = philox4x32_10(
-            make_uint4((uint32_t)(r4 >> 2), (uint32_t)col, (uint32_t)ex.offset,
-                       (uint32_t)(ex.offset >> 32)),
-            make_uint2((uint32_t)ex.seed, (uint32_t)(ex.seed >> 32)));
+        const uint4 rnd = dropout_words((uint64_t)r4, (uint32_t)col, ex.seed, ex.offset);
         const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          o[q] = (wd[q] >= ex.keep_threshold && o[q] > 0.f) ? o[q] * ex.scale : 0.f;
+          o[q] = (dropout_bits(wd[q], (uint32_t)col) >= ex.keep_threshold && o[q] > 0.f)
+                     ? o[q] * ex.scale : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -429,7 +427,7 @@ __device__ __forceinline__ void wres_mfma(const float* __restrict__ bb, const fl
   }
 }
 
-template <int NCOL, int AVEC, bool EPI, int DEPTH>
+template <int NCOL, int AVEC, bool EPI, int DEPTH, bool XT>
 __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
     int M, int N, int K, int nkb, const float* __restrict__ A, uint64_t lda,
     const float* __restrict__ B, uint64_t ldb, float* __restrict__ C, uint64_t ldc, int ncb,
@@ -445,6 +443,30 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
   const int n0 = cb * NCOL;
   const int Kp = nkb * 32;
   constexpr int WT = wres_threads<NCOL>();
+  const int rows_per_task = 16 * kWresRT;
+  const int ntask = (M + rows_per_task - 1) / rows_per_task;
+  const int nwaves = bpc * (WT / 64);
+  const int nfull = K / 32;
+  auto rows_of = [&](int task, const float* (&ar)[kWresRT]) {
+    const int64_t m0 = (int64_t)min(task, ntask - 1) * rows_per_task;
+#pragma unroll
+    for (int rt = 0; rt < kWresRT; ++rt) {
+      const int64_t r = m0 + 16 * rt + i;
+      ar[rt] = A + (uint64_t)(r < M ? r : M - 1) * lda;
+    }
+  };
+  // XT (cross-task prefetch, needs nfull % DEPTH == 0): the loads that would
+  // re-read a task's last block fetch the next task's first blocks instead,
+  // and the first task's are issued before the weight slice is staged
+  const bool xt = XT && nfull >= DEPTH && nfull % DEPTH == 0;
+  float a[DEPTH][kWresRT][8], at[kWresRT][8];
+  int task = wv * bpc + bi;
+  const float* arow[kWresRT];
+  rows_of(task, arow);
+  if (xt && task < ntask) {
+#pragma unroll
+    for (int d = 0; d + 1 < DEPTH; ++d) wres_load_a<AVEC>(arow, d, g, a[d]);
+  }
   // fill in float4 pieces: local columns 4c4 .. 4c4+3 land on 4 consecutive
   // image slots (c = CT ii + j with j % 4 == 0 .. 3)
   if (ldb % 4 == 0 && ((uintptr_t)B & 15) == 0) {
@@ -466,17 +488,11 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
   }
   __syncthreads();
   (void)N;
-  const int rows_per_task = 16 * kWresRT;
-  const int ntask = (M + rows_per_task - 1) / rows_per_task;
-  const int nwaves = bpc * (WT / 64);
-  for (int task = wv * bpc + bi; task < ntask; task += nwaves) {
+  for (; task < ntask; task += nwaves) {
     const int64_t m0 = (int64_t)task * rows_per_task;
-    const float* arow[kWresRT];
-#pragma unroll
-    for (int rt = 0; rt < kWresRT; ++rt) {
-      const int64_t r = m0 + 16 * rt + i;
-      arow[rt] = A + (uint64_t)(r < M ? r : M - 1) * lda;
-    }
+    if (!xt || task != wv * bpc + bi) rows_of(task, arow);
+    const float* nrow[kWresRT];  // next task's rows (XT)
+    rows_of(task + nwaves, nrow);
     f32x4 acc[kWresRT][CT];
 #pragma unroll
     for (int rt = 0; rt < kWresRT; ++rt)
@@ -485,12 +501,10 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
     // full k-blocks (32 (kb+1) <= K) are read unmasked into DEPTH rotating
     // register sets: the loads of blocks kb+1 .. kb+DEPTH-1 are in flight
     // during block kb's MFMAs; the partial last block is read masked.
-    const int nfull = K / 32;
-    float a[DEPTH][kWresRT][8], at[kWresRT][8];
     const float* bb = sB + 8 * g * NCOL + 4 * i;
     const bool tail = nfull < nkb;
     if (tail) wres_load_tail(arow, K, nfull, g, at);
-    if (nfull > 0) {
+    if (!xt && nfull > 0) {
 #pragma unroll
       for (int d = 0; d + 1 < DEPTH; ++d) wres_load_a<AVEC>(arow, min(d, nfull - 1), g, a[d]);
     }
@@ -498,9 +512,19 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
     for (; kb + DEPTH <= nfull; kb += DEPTH) {
 #pragma unroll
       for (int d = 0; d < DEPTH; ++d) {
-        // unconditional (clamped) so that every path through the loop has the
-        // same queue of loads: the compiler then waits with a count, not vmcnt(0)
-        wres_load_a<AVEC>(arow, min(kb + d + DEPTH - 1, nfull - 1), g, a[(d + DEPTH - 1) % DEPTH]);
+        // unconditional (clamped / next task) so that every path through the
+        // loop has the same queue of loads: the compiler then waits with a
+        // count, not vmcnt(0)
+        const int j = kb + d + DEPTH - 1;
+        if (xt) {
+          const bool own = j < nfull;
+          const float* src[kWresRT];
+#pragma unroll
+          for (int rt = 0; rt < kWresRT; ++rt) src[rt] = own ? arow[rt] : nrow[rt];
+          wres_load_a<AVEC>(src, own ? j : j - nfull, g, a[(d + DEPTH - 1) % DEPTH]);
+        } else {
+          wres_load_a<AVEC>(arow, min(j, nfull - 1), g, a[(d + DEPTH - 1) % DEPTH]);
+        }
         __builtin_amdgcn_sched_barrier(0);
         wres_mfma<NCOL>(bb + 32 * (kb + d) * NCOL, a[d], acc);
         __builtin_amdgcn_sched_barrier(0);
@@ -523,16 +547,21 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
       for (int j = 0; j < CT; ++j) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) o[v][j] = acc[rt][j][v];
-        if constexpr (EPI) {
-          const int col = n0 + CT * i + j;
-          const uint4 rnd = philox4x32_10(
-              make_uint4((uint32_t)(r4 >> 2), (uint32_t)col, (uint32_t)ex.offset,
-                         (uint32_t)(ex.offset >> 32)),
-              make_uint2((uint32_t)ex.seed, (uint32_t)(ex.seed >> 32)));
+      }
+      if constexpr (EPI) {  // columns CT i + 2q, +1 share one generator call
+#pragma unroll
+        for (int q = 0; q < CT / 2; ++q) {
+          const uint32_t col = (uint32_t)(n0 + CT * i + 2 * q);
+          const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
           const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
-          for (int v = 0; v < 4; ++v)
-            o[v][j] = (wd[v] >= ex.keep_threshold && o[v][j] > 0.f) ? o[v][j] * ex.scale : 0.f;
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              float& x = o[v][2 * q + h];
+              x = (dropout_bits(wd[v], col + h) >= ex.keep_threshold && x > 0.f) ? x * ex.scale
+                                                                                 : 0.f;
+            }
         }
       }
 #pragma unroll
@@ -917,20 +946,27 @@ static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const floa
   const int vs = (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) ? 1 : 0;
   static const int depth = [] {
     const char* e = getenv("NTS_WRES_DEPTH");
-    return e ? std::max(2, std::min(4, atoi(e))) : 2;
+    return e ? std::max(2, std::min(3, atoi(e))) : 2;
   }();
-#define NTS_WRES_D(NC, AV, D)                                                                   \
+  static const bool xtask = [] {
+    const char* e = getenv("NTS_WRES_XT");
+    return !(e && e[0] == '0');
+  }();
+#define NTS_WRES_D(NC, AV, D, X)                                                                \
   do {                                                                                          \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_wres<NC, AV, EPI, D>), \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
-    hipLaunchKernelGGL((k_gemm_wres<NC, AV, EPI, D>), dim3(grid), dim3(wres_threads<NC>()), lds, \
-                       st, M, N, K, nkb, A, lda, B, ldb, C, ldc, ncb, vs, ex);                  \
+    NTS_HIP_TRY(hipFuncSetAttribute(                                                            \
+        reinterpret_cast<const void*>(&k_gemm_wres<NC, AV, EPI, D, X>),                         \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                                 \
+    hipLaunchKernelGGL((k_gemm_wres<NC, AV, EPI, D, X>), dim3(grid), dim3(wres_threads<NC>()),  \
+                       lds, st, M, N, K, nkb, A, lda, B, ldb, C, ldc, ncb, vs, ex);             \
   } while (0)
-#define NTS_WRES(NC, AV)                                       \
-  do {                                                         \
-    if (depth == 3) NTS_WRES_D(NC, AV, 3);                     \
-    else if (depth == 4) NTS_WRES_D(NC, AV, 4);                \
-    else NTS_WRES_D(NC, AV, 2);                                \
+#define NTS_WRES(NC, AV)                                            \
+  do {                                                              \
+    if (depth == 3) {                                               \
+      if (xtask) NTS_WRES_D(NC, AV, 3, true); else NTS_WRES_D(NC, AV, 3, false); \
+    } else {                                                        \
+      if (xtask) NTS_WRES_D(NC, AV, 2, true); else NTS_WRES_D(NC, AV, 2, false); \
+    }                                                               \
   } while (0)
   if (ncol == 128) {
     if (avec == 4) NTS_WRES(128, 4); else if (avec == 2) NTS_WRES(128, 2); else NTS_WRES(128, 1);
@@ -1022,14 +1058,8 @@ extern "C" int nts_hip_gemm_relu_dropout_f32(nts_hip_ctx* ctx, int M, int N, int
   GemmExtra ex;
   ex.seed = seed;
   ex.offset = offset;
-  if (p >= 1.f) {  // everything dropped (torch returns zeros)
-    ex.keep_threshold = 0xFFFFFFFFu;
-    ex.scale = 0.f;
-  } else {
-    const double t = (double)p * 4294967296.0;
-    ex.keep_threshold = (uint32_t)std::min(t, 4294967295.0);
-    ex.scale = 1.0f / (1.0f - p);
-  }
+  ex.keep_threshold = dropout_threshold(p);
+  ex.scale = p >= 1.f ? 0.f : 1.0f / (1.0f - p);  // p = 1: everything dropped (torch: zeros)
   return gemm<true, false>(ctx, false, M, N, K, A, lda, B, ldb, C, ldc, ex);
 }
 

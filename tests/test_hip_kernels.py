@@ -433,14 +433,17 @@ def _philox4x32_10(c, k):
 
 
 def _dropout_keep(M, N, p, seed, offset):
+    """Element (row, col): 16 bits of Philox4x32-10 at counter {row/4, col/2, offset}
+    (word row % 4, low half for even col, high half for odd), kept iff >= floor(p * 2^16)."""
     rows = np.arange(M, dtype=np.uint64)[:, None] * np.ones((1, N), np.uint64)
     cols = np.ones((M, 1), np.uint64) * np.arange(N, dtype=np.uint64)[None, :]
-    c = [(rows >> np.uint64(2)).astype(np.uint32), cols.astype(np.uint32),
+    c = [(rows >> np.uint64(2)).astype(np.uint32), (cols >> np.uint64(1)).astype(np.uint32),
          np.full((M, N), offset & 0xFFFFFFFF, np.uint32), np.full((M, N), offset >> 32, np.uint32)]
     w = _philox4x32_10(c, (seed & 0xFFFFFFFF, seed >> 32))
-    word = np.choose((rows & np.uint64(3)).astype(np.int64), w)
-    thr = min(int(p * 4294967296.0), 0xFFFFFFFF)
-    return word >= np.uint32(thr)
+    word = np.choose((rows & np.uint64(3)).astype(np.int64), w).astype(np.uint64)
+    bits = np.where((cols & np.uint64(1)) == 1, word >> np.uint64(16), word & np.uint64(0xFFFF))
+    thr = 65536 if p >= 1.0 else min(int(p * 65536.0), 65536)
+    return bits >= np.uint64(thr)
 
 
 @pytest.mark.parametrize("M,N,K,p", [(5000, 128, 602, 0.5), (333, 41, 100, 0.3), (1000, 128, 128, 0.0),
