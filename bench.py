@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--early-agg", action="store_true",
                    help="issue the bottom aggregation behind the sampler on the sampling stream")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
+    p.add_argument("--atomic-backward", action="store_true",
+                   help="graph-op backward by atomic CSC scatter (no CSR transpose in the "
+                        "sampler; nondeterministic sums)")
     p.add_argument("--cache-rate", type=float, default=-1.0,
                    help="feature table in pinned host memory with this fraction of the "
                         "highest-degree rows cached in HBM (GS_SAMPLE_PD_CACHE placement); "
@@ -133,7 +136,8 @@ def main():
                           sampler_priority=not args.no_priority,
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
-                          pad_features=not args.no_pad_features, cache_rate=args.cache_rate)
+                          pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
+                          deterministic_backward=not args.atomic_backward)
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and not args.early_agg and layers[1] <= 128)
     agg_kernel = ("k_agg_gemm" if fused_linear else "k_spmm_gather")

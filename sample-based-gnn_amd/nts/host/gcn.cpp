@@ -386,20 +386,32 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   auto guard = cs->guard();
   double t0 = now_s();
   NtsStream& sst = ss ? *ss : *cs;
+  // NTS_DIAG_REUSE_SAMPLE=1 (diagnostic only, not a valid measurement): sample
+  // once and train every step on that batch — the training stream's time
+  // without the sampler beside it
+  static const bool diag_reuse = getenv("NTS_DIAG_REUSE_SAMPLE") != nullptr;
   int slot;
-  if (prefetched_ >= 0) {
-    slot = prefetched_;
-    prefetched_ = -1;
+  SampledSubgraph* sg;
+  if (diag_reuse && reuse_slot_ >= 0) {
+    slot = reuse_slot_;
+    sg = sampler->ssgs[slot];
   } else {
-    slot = next_slot_;
-    issue(slot, sst);
-  }
-  SampledSubgraph* sg = sampler->finish_gpu_sample(slot);
-  if (ss) {
-    next_slot_ = (slot + 1) % nslots_;
-    if (sampler->sample_not_finished()) {  // prefetch the next batch behind this one
-      issue(next_slot_, *ss);
-      prefetched_ = next_slot_;
+    if (prefetched_ >= 0) {
+      slot = prefetched_;
+      prefetched_ = -1;
+    } else {
+      slot = next_slot_;
+      issue(slot, sst);
+    }
+    sg = sampler->finish_gpu_sample(slot);
+    if (diag_reuse) {
+      reuse_slot_ = slot;
+    } else if (ss) {
+      next_slot_ = (slot + 1) % nslots_;
+      if (sampler->sample_not_finished()) {  // prefetch the next batch behind this one
+        issue(next_slot_, *ss);
+        prefetched_ = next_slot_;
+      }
     }
   }
   TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[slot], 0) == hipSuccess,

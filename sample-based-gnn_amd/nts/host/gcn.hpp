@@ -92,6 +92,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   uint64_t dropout_calls_ = 0;  // Philox offset of the fused dropout masks
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch
   int next_slot_ = 0;
+  int reuse_slot_ = -1;  // NTS_DIAG_REUSE_SAMPLE
 };
 
 }  // namespace nts
