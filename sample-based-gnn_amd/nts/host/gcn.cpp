@@ -408,12 +408,21 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
       reuse_slot_ = slot;
     } else if (ss) {
       next_slot_ = (slot + 1) % nslots_;
-      if (sampler->sample_not_finished()) {  // prefetch the next batch behind this one
-        issue(next_slot_, *ss);
+      if (!pass_done_ && sampler->sample_not_finished()) {
+        issue(next_slot_, *ss);  // prefetch the next batch behind this one
         prefetched_ = next_slot_;
+      } else if (!pass_done_) {
+        // last batch of the pass: sample the first batch of the next pass now
+        // (same seeds, same stream position as after restart()), so the
+        // pipeline does not drain at every pass boundary
+        sampler->restart();
+        issue(next_slot_, *ss);
+        carry_ = next_slot_;
+        pass_done_ = true;
       }
     }
   }
+  fresh_pass_ = false;
   TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[slot], 0) == hipSuccess,
               "hipStreamWaitEvent");
   double t1 = now_s();
@@ -446,6 +455,16 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
 }
 
 void GCN_SAMPLE_ALLGPU_impl::restart() {
+  if (fresh_pass_) return;  // nothing trained since the last restart
+  fresh_pass_ = true;
+  if (carry_ >= 0) {  // the next pass's first batch is already in flight
+    TORCH_CHECK(prefetched_ < 0, "pipeline state");
+    prefetched_ = carry_;
+    carry_ = -1;
+    pass_done_ = false;
+    return;
+  }
+  pass_done_ = false;
   if (prefetched_ >= 0) {  // drop a prefetched batch of the previous pass
     sampler->finish_gpu_sample(prefetched_);
     prefetched_ = -1;

@@ -44,7 +44,9 @@ class GCN_SAMPLE_ALLGPU_impl {
   void init_nn();
   float train_batch();
   float run_epoch();
-  bool has_batch() const { return prefetched_ >= 0 || sampler->sample_not_finished(); }
+  bool has_batch() const {
+    return prefetched_ >= 0 || (!pass_done_ && sampler->sample_not_finished());
+  }
   void restart();
   // eval-mode forward over a given seed batch: [Y_0, X_1, Y_1, X_2, ...]
   std::vector<NtsVar> forward_eval(const std::vector<VertexId>& seeds, uint64_t batch_seq);
@@ -93,6 +95,11 @@ class GCN_SAMPLE_ALLGPU_impl {
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch
   int next_slot_ = 0;
   int reuse_slot_ = -1;  // NTS_DIAG_REUSE_SAMPLE
+  // pass boundary: the next pass's first batch is issued behind the current
+  // pass's last one (carry_), handed over by restart()
+  int carry_ = -1;
+  bool pass_done_ = false;
+  bool fresh_pass_ = true;
 };
 
 }  // namespace nts

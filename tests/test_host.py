@@ -201,3 +201,24 @@ def test_feature_cache_training_is_identical(E, graph, rate, early, fused):
     b.synchronize()
     for x, y in zip(a.weights(), b.weights()):
         assert torch.equal(x, y)
+
+
+def test_pipeline_carries_batches_across_passes(E, graph):
+    """The pipelined driver samples the next pass's first batch behind the
+    current pass's last one (no drain at pass boundaries); the batch sequence,
+    and so the trained weights, equal the unpipelined driver's over several
+    passes mixed with restart() calls."""
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 300, drop=0.5, pipeline=True)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 300, drop=0.5, pipeline=False)
+    for d in (a, b):
+        d.run_epoch()
+        d.restart()
+        d.restart()  # repeated restarts without training in between are no-ops
+        d.run_epoch()
+        for _ in range(3):  # bench-style stepping across a pass boundary
+            if not d.sample_not_finished():
+                d.restart()
+            d.train_batch()
+        d.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)
