@@ -140,3 +140,69 @@ class InputInfo:
             else:
                 info.extra[k] = v
         return info
+
+
+# ---------------------------------------------------------------------------
+# OGB node-property datasets -> the reference's on-disk formats
+# ---------------------------------------------------------------------------
+OGB_SPLIT = {"products": "sales_ranking", "proteins": "species", "proteinfunc": "species"}
+
+
+def ogb_edges_to_reference(src: np.ndarray, dst: np.ndarray, n_vertices: int):
+    """Edge list of transOGBData_To_NeutronStarData.py (data/OGBData/, lines 17-50):
+    append a self-loop per vertex, sort by source, emit (dst, src) then (src, dst)
+    for every row, drop repeated pairs keeping the first occurrence.  The
+    reference sorts with pandas' default (unstable) quicksort; equal sources
+    keep their file order here."""
+    a = np.concatenate([np.asarray(src, np.int64), np.arange(n_vertices, dtype=np.int64)])
+    b = np.concatenate([np.asarray(dst, np.int64), np.arange(n_vertices, dtype=np.int64)])
+    order = np.argsort(a, kind="stable")
+    a, b = a[order], b[order]
+    s = np.empty(2 * a.size, np.int64)
+    d = np.empty(2 * a.size, np.int64)
+    s[0::2], d[0::2] = b, a  # reverse edge first (":my_output_file.write(row[1], row[0])")
+    s[1::2], d[1::2] = a, b
+    key = s * np.int64(n_vertices) + d
+    _, first = np.unique(key, return_index=True)
+    keep = np.sort(first)
+    return s[keep].astype(np.uint32), d[keep].astype(np.uint32)
+
+
+def convert_ogb(root, name: str, out_dir=None) -> dict:
+    """Convert an OGB node-property dataset laid out as the reference expects
+    (`<root>/raw/edge.csv/edge.csv`, `raw/num-node-list.csv/...`,
+    `raw/node-label.csv/...`, `raw/node-feat.csv/...`,
+    `split/<split>/{train,valid,test}.csv/...`) into the reference's files:
+    `<name>.edge.self.bin` (binary u32 pairs, convert2binary.cpp),
+    `<name>.featuretable` (`id f...`), `<name>.labeltable` (`id label`),
+    `<name>.mask` (`id train|eval|test`, sorted by id).  Returns the paths."""
+    root = pathlib.Path(root)
+    out = pathlib.Path(out_dir) if out_dir else root / "Data"
+    out.mkdir(parents=True, exist_ok=True)
+    raw = root / "raw"
+    n = int(np.loadtxt(raw / "num-node-list.csv" / "num-node-list.csv", delimiter=",", ndmin=1)[0])
+    e = np.loadtxt(raw / "edge.csv" / "edge.csv", delimiter=",", dtype=np.int64, ndmin=2)
+    s, d = ogb_edges_to_reference(e[:, 0], e[:, 1], n)
+    paths = {"edge": out / f"{name}.edge.self.bin", "feature": out / f"{name}.featuretable",
+             "label": out / f"{name}.labeltable", "mask": out / f"{name}.mask"}
+    write_edge_file(paths["edge"], s, d)
+    labels = np.loadtxt(raw / "node-label.csv" / "node-label.csv", delimiter=",", dtype=str, ndmin=2)
+    with open(paths["label"], "w") as f:
+        for i, row in enumerate(labels):
+            f.write(f"{i} {' '.join(row)}\n")
+    feats = np.loadtxt(raw / "node-feat.csv" / "node-feat.csv", delimiter=",", dtype=str, ndmin=2)
+    with open(paths["feature"], "w") as f:
+        for i, row in enumerate(feats):
+            f.write(f"{i} {' '.join(row)}\n")
+    split = root / "split" / OGB_SPLIT.get(name, "time")
+    ids, kinds = [], []
+    for part, tag in (("train", "train"), ("valid", "eval"), ("test", "test")):
+        v = np.loadtxt(split / f"{part}.csv" / f"{part}.csv", delimiter=",", dtype=np.int64, ndmin=1)
+        ids.append(v.reshape(-1))
+        kinds += [tag] * v.size
+    ids = np.concatenate(ids)
+    order = np.argsort(ids, kind="stable")
+    with open(paths["mask"], "w") as f:
+        for k in order:
+            f.write(f"{ids[k]} {kinds[k]}\n")
+    return paths

@@ -231,3 +231,58 @@ def test_cache_select_oracle_degree_order():
         idx = rng.integers(0, 500, 300).astype(np.uint32)
         cache = table[ids] if n else np.zeros((0, 9), np.float32)
         assert np.array_equal(orc.get_feature_cached(idx, cache, cmap, table), table[idx])
+
+
+def _ogb_edges_loop(src, dst, n):
+    """Line-by-line restatement of transOGBData_To_NeutronStarData.py's edge steps."""
+    rows = list(zip(src.tolist(), dst.tolist())) + [(i, i) for i in range(n)]
+    rows = sorted(rows, key=lambda r: r[0])  # (stable here; pandas quicksort is not)
+    out = []
+    for a, b in rows:
+        out.append((b, a))
+        out.append((a, b))
+    seen, res = set(), []
+    for p in out:
+        if p not in seen:
+            seen.add(p)
+            res.append(p)
+    return res
+
+
+def test_ogb_edge_conversion_matches_loop_restatement():
+    from nts import dataloader
+    rng = np.random.default_rng(3)
+    n = 50
+    src = rng.integers(0, n, 300)
+    dst = rng.integers(0, n, 300)
+    s, d = dataloader.ogb_edges_to_reference(src, dst, n)
+    assert list(zip(s.tolist(), d.tolist())) == _ogb_edges_loop(src, dst, n)
+    pairs = set(zip(s.tolist(), d.tolist()))
+    assert all((b, a) in pairs for a, b in pairs)  # symmetric
+    assert all((i, i) in pairs for i in range(n))  # self-loops
+    assert len(pairs) == s.size  # no duplicates
+
+
+def test_convert_ogb_layout(tmp_path):
+    from nts import dataloader
+    root = tmp_path / "arxiv"
+    for sub in ("raw/edge.csv", "raw/num-node-list.csv", "raw/node-label.csv", "raw/node-feat.csv",
+                "split/time/train.csv", "split/time/valid.csv", "split/time/test.csv"):
+        (root / sub).mkdir(parents=True)
+    (root / "raw/num-node-list.csv/num-node-list.csv").write_text("5\n")
+    (root / "raw/edge.csv/edge.csv").write_text("0,1\n3,2\n1,4\n")
+    (root / "raw/node-label.csv/node-label.csv").write_text("\n".join("3 1 0 2 1".split()) + "\n")
+    (root / "raw/node-feat.csv/node-feat.csv").write_text(
+        "\n".join(f"{i}.5,{-i}.25" for i in range(5)) + "\n")
+    (root / "split/time/train.csv/train.csv").write_text("4\n0\n")
+    (root / "split/time/valid.csv/valid.csv").write_text("2\n")
+    (root / "split/time/test.csv/test.csv").write_text("1\n3\n")
+    p = dataloader.convert_ogb(root, "arxiv")
+    s, d = dataloader.read_edge_file(p["edge"])
+    assert list(zip(s.tolist(), d.tolist())) == _ogb_edges_loop(np.array([0, 3, 1]), np.array([1, 2, 4]), 5)
+    feats, labels, masks = dataloader.read_feature_label_mask(p["feature"], p["label"], p["mask"], 5, 2)
+    assert np.allclose(feats[:, 0], np.arange(5) + 0.5)
+    assert np.allclose(feats[:, 1], [float(f"{-i}.25") for i in range(5)])
+    assert labels.tolist() == [3, 1, 0, 2, 1]
+    assert masks.tolist() == [dataloader.MASK_TRAIN, dataloader.MASK_TEST, dataloader.MASK_VAL,
+                              dataloader.MASK_TEST, dataloader.MASK_TRAIN]
