@@ -66,6 +66,11 @@ extern "C" {
 #define NTS_WEIGHT_SUM 0
 #define NTS_WEIGHT_MEAN 1
 #define NTS_WEIGHT_NONE 2
+/* OR-ed into SUM / MEAN: UP_DEGREE — the degrees in the weights are the
+ * sampled layer's own (in = sampled edges of the dst, out = sampled edges of
+ * the src), SampledSubgraph::update_degrees(_GPU) (core/FullyRepGraph.hpp:189-217,
+ * cfg key UP_DEGREE, core/ntsFastSampler.hpp:691-693,1107-1108). */
+#define NTS_WEIGHT_UP_DEGREE 0x10
 
 typedef struct nts_hip_ctx nts_hip_ctx;
 typedef struct nts_hip_comm nts_hip_comm;

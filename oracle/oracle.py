@@ -18,6 +18,7 @@ LIB = HERE / "build" / "liboracle.so"
 RNG_PHILOX, RNG_MT_LEMIRE, RNG_MT_DIV = 0, 1, 2
 ORDER_DRAW, ORDER_UNORDERED_MAP = 0, 1
 W_SUM, W_MEAN, W_NONE = 0, 1, 2
+W_UP_DEGREE = 0x10  # OR-ed into the weight type: UP_DEGREE per-layer degrees
 
 _lib = None
 

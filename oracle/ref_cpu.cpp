@@ -102,7 +102,7 @@ struct Layer {
 
 enum { RNG_PHILOX = 0, RNG_MT_LEMIRE = 1, RNG_MT_DIV = 2 };
 enum { ORDER_DRAW = 0, ORDER_UNORDERED_MAP = 1 };
-enum { W_SUM = 0, W_MEAN = 1, W_NONE = 2 };
+enum { W_SUM = 0, W_MEAN = 1, W_NONE = 2, W_UP_DEGREE = 0x10 };
 
 struct Sampler {
   uint64_t V;
@@ -192,8 +192,13 @@ void orc_sampler_free(void* h) { delete (Sampler*)h; }
 // thread-local generator per worker like the reference (timing baseline only;
 // results then depend on the thread count, as the reference's do).
 int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_seq,
-                     int weight_type, int build_csr, int threads) {
+                     int weight_flags, int build_csr, int threads) {
   Sampler& s = *(Sampler*)h;
+  // UP_DEGREE (cfg key, core/GraphSegment.cpp:273-276): degrees recomputed from
+  // each sampled layer before its weights (SampledSubgraph::update_degrees,
+  // core/FullyRepGraph.hpp:189-207, called at core/ntsFastSampler.hpp:1107-1108)
+  const bool up_degree = (weight_flags & W_UP_DEGREE) != 0;
+  const int weight_type = weight_flags & 0xF;
   const int L = (int)s.layers.size();
   for (int i = 0; i < L; ++i) {
     Layer& ly = s.layers[i];
@@ -288,9 +293,18 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
           ly.column_indices[cursor[ly.row_indices[j]]++] = k;
     }
     // WeightCompute (core/coocsc.hpp:301-324) with Sum / Mean lambdas (:1111-1119)
-    auto wfun = [&](uint32_t src_g, uint32_t dst_g) -> float {
-      float w = norm_degree(s.outdeg[src_g], s.indeg[dst_g]);
-      if (weight_type == W_MEAN) w = w / s.indeg[dst_g];
+    std::vector<uint32_t> up_out, up_in;  // per local src / local dst (UP_DEGREE)
+    if (up_degree) {
+      up_out.assign(src_size, 0);
+      up_in.assign(v, 0);
+      for (uint32_t k = 0; k < v; ++k) up_in[k] = ly.column_offset[k + 1] - ly.column_offset[k];
+      for (uint32_t k = 0; k < e; ++k) up_out[ly.row_indices[k]]++;
+    }
+    auto wfun2 = [&](uint32_t src_l, uint32_t dst_l) -> float {
+      const uint32_t od = up_degree ? up_out[src_l] : s.outdeg[ly.source[src_l]];
+      const uint32_t id = up_degree ? up_in[dst_l] : s.indeg[ly.destination[dst_l]];
+      float w = norm_degree(od, id);
+      if (weight_type == W_MEAN) w = w / id;
       return w;
     };
     if (weight_type != W_NONE) {
@@ -298,10 +312,10 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
       ly.edge_weight_forward.assign(e, 0.f);
       for (uint32_t r = 0; r < src_size; ++r)
         for (uint32_t j = ly.row_offset[r]; j < ly.row_offset[r + 1]; ++j)
-          ly.edge_weight_backward[j] = wfun(ly.source[r], ly.destination[ly.column_indices[j]]);
+          ly.edge_weight_backward[j] = wfun2(r, ly.column_indices[j]);
       for (uint32_t k = 0; k < v; ++k)
         for (uint32_t j = ly.column_offset[k]; j < ly.column_offset[k + 1]; ++j)
-          ly.edge_weight_forward[j] = wfun(ly.source[ly.row_indices[j]], ly.destination[k]);
+          ly.edge_weight_forward[j] = wfun2(ly.row_indices[j], k);
     } else {
       ly.edge_weight_backward.clear();
       ly.edge_weight_forward.clear();

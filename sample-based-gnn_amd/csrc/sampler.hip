@@ -511,22 +511,42 @@ __device__ __forceinline__ float norm_degree(uint32_t out_src, uint32_t in_dst) 
   return 1.0f / (a * b);
 }
 
+// up_cnt != nullptr (UP_DEGREE): count the sampled edges per local src
+// instead of computing the weights (k_up_weight does, once counted)
 __global__ void k_relabel(const uint32_t* __restrict__ ans, const uint32_t* __restrict__ edst,
                           const uint32_t* __restrict__ dst, const uint32_t* __restrict__ src_index,
                           const uint32_t* __restrict__ out_deg, const uint32_t* __restrict__ in_deg,
                           const uint32_t* sizes, int weight_type, uint32_t* __restrict__ ri,
-                          float* __restrict__ wf) {
+                          float* __restrict__ wf, uint32_t* __restrict__ up_cnt) {
   const uint32_t e = sizes[1];
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x) {
     const uint32_t g = ans[k];
-    ri[k] = src_index[g];
-    if (weight_type != NTS_WEIGHT_NONE) {
+    const uint32_t r = src_index[g];
+    ri[k] = r;
+    if (up_cnt) {
+      atomicAdd(up_cnt + r, 1u);
+    } else if (weight_type != NTS_WEIGHT_NONE) {
       const uint32_t dg = dst[edst[k]];
       const uint32_t ind = in_deg[dg];
       float w = norm_degree(out_deg[g], ind);
       if (weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
       wf[k] = w;
     }
+  }
+}
+
+// UP_DEGREE weights: out = sampled edges of the src (counted by k_relabel),
+// in = sampled edges of the dst (its CSC segment)
+__global__ void k_up_weight(const uint32_t* __restrict__ ri, const uint32_t* __restrict__ edst,
+                            const uint32_t* __restrict__ co, const uint32_t* __restrict__ cnt,
+                            const uint32_t* sizes, int weight_type, float* __restrict__ wf) {
+  const uint32_t e = sizes[1];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x) {
+    const uint32_t d = edst[k];
+    const uint32_t ind = co[d + 1] - co[d];
+    float w = norm_degree(cnt[ri[k]], ind);
+    if (weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
+    wf[k] = w;
   }
 }
 
@@ -568,9 +588,13 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                     o->row_indices &&
                     o->sample_ans && o->edge_dst && o->source && o->sizes,
                 "missing sampCSC buffer");
+  const bool up_degree = (weight_type & NTS_WEIGHT_UP_DEGREE) != 0;
+  weight_type &= 0xF;
+  NTS_CHECK_ARG(weight_type >= NTS_WEIGHT_SUM && weight_type <= NTS_WEIGHT_NONE, "weight_type");
   NTS_CHECK_ARG(weight_type == NTS_WEIGHT_NONE || (o->edge_weight_forward && g->in_degree &&
                                                    g->out_degree),
                 "weights requested without buffers/degrees");
+  const bool up = up_degree && weight_type != NTS_WEIGHT_NONE;
   NTS_CHECK_ARG(rng_mode >= NTS_RNG_PHILOX && rng_mode <= NTS_RNG_MT19937_DIV, "rng_mode");
   NTS_CHECK_ARG(fanout <= kSetCap, "fanout above the rejection-path capacity (1024)");
   NTS_CHECK_ARG(g->n_vertices <= 0xFFFFFFFFull, "vertex count exceeds uint32 ids");
@@ -589,8 +613,9 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
+  const uint64_t up_n = up ? al(o->s_cap) : 0;
   const size_t need =
-      (scan_co + blk + scan_blk + sort_k + sort_v) * sizeof(uint32_t) + sort_tmp + 256;
+      (scan_co + blk + scan_blk + sort_k + sort_v + up_n) * sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
   uint32_t* w0 = (uint32_t*)ctx->scratch;
   uint32_t* t_scan_co = w0;
@@ -598,7 +623,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   uint32_t* t_scan_blk = t_blk + blk;
   uint32_t* t_skey = t_scan_blk + scan_blk;
   uint32_t* t_seid = t_skey + sort_k;
-  void* t_sort = (void*)(t_seid + sort_v);
+  uint32_t* t_up = t_seid + sort_v;
+  void* t_sort = (void*)(t_up + up_n);
 
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
@@ -661,10 +687,16 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   NTS_LAUNCH_CHECK();
 
   // 4) relabel to local ids + forward weights
+  if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, o->sample_ans, o->edge_dst,
                      o->destination, ctx->src_index, g->out_degree, g->in_degree, o->sizes,
-                     weight_type, o->row_indices, o->edge_weight_forward);
+                     weight_type, o->row_indices, o->edge_weight_forward, up ? t_up : nullptr);
   NTS_LAUNCH_CHECK();
+  if (up) {
+    hipLaunchKernelGGL(k_up_weight, dim3(ge), dim3(256), 0, st, o->row_indices, o->edge_dst,
+                       o->column_offset, t_up, o->sizes, weight_type, o->edge_weight_forward);
+    NTS_LAUNCH_CHECK();
+  }
 
   // 5) CSR transpose (stable in edge order = ascending local dst)
   if (csr) {

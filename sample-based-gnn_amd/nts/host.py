@@ -37,7 +37,8 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
                seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False,
                early_aggregate=True, sampler_priority=True, fuse_activation=True,
-               fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0):
+               fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0,
+               up_degree=False):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -62,6 +63,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.sampler_cus = int(sampler_cus)
     c.pad_features = bool(pad_features)
     c.cache_rate = float(cache_rate)
+    c.up_degree = bool(up_degree)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

@@ -262,8 +262,9 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   if (ssgs.size() > 1) hip_rt(hipEventSynchronize(ssg->consumed), "hipEventSynchronize");
   hip_rt(hipStreamWaitEvent(st, ssg->consumed, 0), "hipStreamWaitEvent");
   const nts_graph_dev g = whole_graph->dev();
-  const int wt = w == WeightType::Sum ? NTS_WEIGHT_SUM
-                                      : (w == WeightType::Mean ? NTS_WEIGHT_MEAN : NTS_WEIGHT_NONE);
+  int wt = w == WeightType::Sum ? NTS_WEIGHT_SUM
+                                : (w == WeightType::Mean ? NTS_WEIGHT_MEAN : NTS_WEIGHT_NONE);
+  if (up_degree && wt != NTS_WEIGHT_NONE) wt |= NTS_WEIGHT_UP_DEGREE;
   const VertexId* dst = dptr<VertexId>(dev_nids_) + work_offset;
   sampCSC* s0 = ssg->sampled_sgs[0];
   // layer-0 v_size as a device scalar without a per-batch memset: entry

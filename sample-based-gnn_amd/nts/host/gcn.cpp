@@ -76,6 +76,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                           nslots_, csr,
                                           cfg.weight_type != WeightType::None);
   sampler->rng_mode = cfg.rng_mode;
+  sampler->up_degree = cfg.up_degree;
   if (cfg.pipeline && cfg.sampler_cus > 0)
     ss = std::make_unique<NtsStream>(graph->device,
                                      cu_mask_spread(graph->device, cfg.sampler_cus, false),
@@ -487,6 +488,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<Verte
   FastSampler s(graph, seeds, L, (int)seeds.size(), cfg.fanout, 1, csr,
                 cfg.weight_type != WeightType::None);
   s.rng_mode = cfg.rng_mode;
+  s.up_degree = cfg.up_degree;
   s.batch_seq = batch_seq;
   SampledSubgraph* sg = s.sample_gpu_fast((int)seeds.size(), 0, *cs, cfg.weight_type);
   ctx.eval();

@@ -13,6 +13,7 @@ struct GCNConfig {
   float beta1 = 0.9f, beta2 = 0.999f, epsilon = 1e-9f;  // toolkits/GCN_SAMPLE_GPU.hpp:115-117
   int rng_mode = NTS_RNG_PHILOX;
   WeightType weight_type = WeightType::Sum;  // GraphSAGE toolkits: Mean
+  bool up_degree = false;             // UP_DEGREE cfg key (core/GraphSegment.cpp:273-276)
   bool fused_gather = true;           // gather features inside the bottom aggregation
   bool bias_correction = false;       // false: learn_local_with_decay_Adam (GPU drivers)
   bool deterministic_backward = true; // CSR transpose gather instead of atomics

@@ -197,6 +197,7 @@ class FastSampler {
   SampledSubgraph* ssg = nullptr;
   std::vector<SampledSubgraph*> ssgs;
   int rng_mode = NTS_RNG_PHILOX;
+  bool up_degree = false;  // UP_DEGREE: weights from each sampled layer's own degrees
   uint64_t batch_seq = 0;  // keys the PHILOX stream (one per sampled batch)
   double all_time = 0;     // sampler wall time (reference `all_time`)
   uint64_t sampled_edges = 0;

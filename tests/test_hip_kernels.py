@@ -162,7 +162,7 @@ def test_sampler_mt19937_div_mode(hip, cora):
 
 
 @pytest.mark.parametrize("case", ["cora", "random"])
-@pytest.mark.parametrize("weight_type", [0, 1, 2])
+@pytest.mark.parametrize("weight_type", [0, 1, 2, 0x10, 0x11])  # 0x10: UP_DEGREE
 def test_sampler_philox_matches_oracle(hip, cora, case, weight_type):
     V, src, dst = cora if case == "cora" else _random_graph(20000, 600000, 9)
     g = _graph(hip, V, src, dst)

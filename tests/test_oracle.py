@@ -16,6 +16,7 @@ import pytest
 
 from oracle import oracle as orc
 from nts import dataloader
+from conftest import GOLDEN
 
 # ---------------------------------------------------------------------------
 # hand-computed 5-vertex graph
@@ -286,3 +287,28 @@ def test_convert_ogb_layout(tmp_path):
     assert labels.tolist() == [3, 1, 0, 2, 1]
     assert masks.tolist() == [dataloader.MASK_TRAIN, dataloader.MASK_TEST, dataloader.MASK_VAL,
                               dataloader.MASK_TEST, dataloader.MASK_TRAIN]
+
+
+def test_up_degree_weights_use_sampled_layer_degrees():
+    """UP_DEGREE (SampledSubgraph::update_degrees, core/FullyRepGraph.hpp:189-207):
+    in = sampled edges of the dst, out = sampled edges of the src, then
+    nts_norm_degree (float of double sqrt, 1 / (a * b)); Mean divides by in."""
+    from nts import dataloader
+    src, dst = dataloader.read_edge_file(GOLDEN / "cora" / "cora.2708.edge.self")
+    V = 2708
+    col, rows = orc.build_csc(V, src, dst)
+    od, idg = orc.degrees(V, src, dst)
+    seeds = np.arange(0, V, 17, dtype=np.uint32)
+    for wt in (orc.W_SUM, orc.W_MEAN):
+        o = orc.Sampler(col, rows, idg, od, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+        for ly in o.sample(seeds, 0, wt | orc.W_UP_DEGREE):
+            co, ri = ly["column_offset"].astype(np.int64), ly["row_indices"]
+            ind = np.diff(co)
+            outd = np.bincount(ri, minlength=ly["src_size"])
+            dl = np.repeat(np.arange(ind.size), ind)
+            a = np.sqrt(outd[ri].astype(np.float64)).astype(np.float32)
+            b = np.sqrt(ind[dl].astype(np.float64)).astype(np.float32)
+            w = np.float32(1) / (a * b)
+            if wt == orc.W_MEAN:
+                w = w / ind[dl].astype(np.float32)
+            assert np.array_equal(ly["edge_weight_forward"], w)
