@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 1
+#define NTS_HIP_ABI_VERSION 2  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id */
 
 /* status codes */
 #define NTS_OK 0
@@ -105,6 +105,15 @@ typedef struct {
   uint32_t *sizes;                 /* device [4]: v_size, e_size, src_size,
                                       overflow flag (nonzero = a capacity was
                                       exceeded and the layer is truncated)     */
+  uint32_t *dst_local_id;          /* [v_cap] or NULL.  Non-NULL: every dst is
+                                      also put in the frontier (is_merge_src_dst,
+                                      core/ntsFastSampler.hpp:1050-1052, the GAT
+                                      drivers) and dst_local_id[d] = its local
+                                      src id (:1095-1097; set_dst_local_index,
+                                      cuda/ntsCUDAGraphOP.cu:1696).  s_cap must
+                                      then allow e + v sources.               */
+  uint32_t *csr_edge_id;           /* [e_cap] or NULL: CSC edge id of each CSR
+                                      slot (with row_offset)                   */
 } nts_sampcsc_dev;
 
 /* ---- context ------------------------------------------------------------ */
@@ -271,6 +280,34 @@ int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx *ctx, const uint32_t *column_offset,
                                 const uint32_t *v, uint32_t v_cap, const float *g_out,
                                 uint64_t ld_gout, uint32_t feature_size, float *g_in,
                                 uint64_t ld_gin);
+
+/* ---- GAT layer on a merged src/dst sampled block ------------------------- */
+/* The GAT_SAMPLE_ALL_GPU layer (toolkits/GAT_SAMPLE_ALL_GPU.hpp:308-391:
+ * BatchGPUSrcDstScatterOp -> leaky_relu(msg . W_att, 0.2) -> BatchGPUEdgeSoftMax
+ * -> e_msg * a -> BatchGPUAggregateDst -> relu; core/ntsPushdownGraphOp.hpp:490-748)
+ * without materialising the [e, 2F] messages.  H = X W [src_size x F] is the
+ * layer's transformed input (caller's GEMM); att = W_att [2F] (a1 = att[0:F]
+ * for the source half, a2 = att[F:2F] for the destination half).  Forward:
+ *   m[e] = leaky_relu(H[src_e].a1 + H[dst_local(d)].a2, 0.2),
+ *   a[e] = softmax over the edges of d of m,  Y[d] = relu(sum_e a[e] H[src_e]).
+ * One wave per destination, online softmax (running max/sum), edge order. */
+int nts_hip_gat_forward(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                        const uint32_t *row_indices, const uint32_t *dst_local_id,
+                        uint32_t v_size, const float *H, uint64_t ldh, uint32_t F,
+                        const float *att, float *m_out, float *a_out, float *Y, uint64_t ldy);
+/* Its backward for dL/dY = GY (deterministic: a per-destination pass and a
+ * per-source pass over the CSR with csr_edge_id; no atomics):
+ *   du[e] = dL/d(pre-leaky score of e), ds2[v] = dL/d(H[v].a2) (zero for
+ *   non-destinations), dH [src_size x F] = dL/dH, dS [src_size x 2] =
+ *   (dL/d(H[v].a1), dL/d(H[v].a2)) so that dW_att = H^T dS (caller's GEMM). */
+int nts_hip_gat_backward(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                         const uint32_t *row_indices, const uint32_t *dst_local_id,
+                         uint32_t v_size, const uint32_t *row_offset,
+                         const uint32_t *column_indices, const uint32_t *csr_edge_id,
+                         uint32_t src_size, const float *H, uint64_t ldh, uint32_t F,
+                         const float *att, const float *a, const float *m, const float *Y,
+                         uint64_t ldy, const float *GY, uint64_t ldg, float *du, float *ds2,
+                         float *dH, uint64_t lddh, float *dS);
 
 /* ---- dense layer update (MFMA fp32) -------------------------------------- */
 /* Row-major fp32 GEMM on the matrix cores (v_mfma_f32_16x16x4_f32 /

@@ -19,6 +19,7 @@ RNG_PHILOX, RNG_MT_LEMIRE, RNG_MT_DIV = 0, 1, 2
 ORDER_DRAW, ORDER_UNORDERED_MAP = 0, 1
 W_SUM, W_MEAN, W_NONE = 0, 1, 2
 W_UP_DEGREE = 0x10  # OR-ed into the weight type: UP_DEGREE per-layer degrees
+F_MERGE_SRC_DST = 0x20  # OR-ed: dsts merged into the frontier (GAT), dst_local_id
 
 _lib = None
 
@@ -43,6 +44,7 @@ def lib():
         L.orc_layer_size.argtypes = [P, I, P]
         L.orc_layer_copy.argtypes = [P, I] + [P] * 9
         L.orc_mt_state.argtypes = [P, P]
+        L.orc_layer_extra.argtypes = [P, I, P, P]
         L.orc_get_feature.argtypes = [U32, P, P, U32, P, I]
         L.orc_fuse_fwd.argtypes = [U32, P, P, P, P, P, P, P, U32, P, I, I]
         L.orc_fuse_bwd.argtypes = [U32, U32, P, P, P, P, P, P, P, U32, P, I, I]
@@ -113,6 +115,12 @@ class Sampler:
             "destination", "column_offset", "row_indices", "sample_ans", "source",
             "edge_weight_forward", "row_offset", "column_indices", "edge_weight_backward")])
         out.update(v_size=v, e_size=e, src_size=s)
+        dl, ce = np.zeros(v, np.uint32), np.zeros(e, np.uint32)
+        have = lib().orc_layer_extra(self.h, l, _p(dl), _p(ce))
+        if have & 1:
+            out["dst_local_id"] = dl
+        if have & 2:
+            out["csr_edge_id"] = ce
         return out
 
     def mt_state(self):

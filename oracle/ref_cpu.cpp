@@ -95,14 +95,14 @@ inline uint32_t philox_word(uint64_t seed, uint32_t d, uint32_t layer, uint64_t 
 
 struct Layer {
   std::vector<uint32_t> destination, column_offset, row_indices, sample_ans, source;
-  std::vector<uint32_t> row_offset, column_indices;
+  std::vector<uint32_t> row_offset, column_indices, csr_edge_id, dst_local_id;
   std::vector<float> edge_weight_forward, edge_weight_backward;
   uint32_t v_size = 0, e_size = 0, src_size = 0;
 };
 
 enum { RNG_PHILOX = 0, RNG_MT_LEMIRE = 1, RNG_MT_DIV = 2 };
 enum { ORDER_DRAW = 0, ORDER_UNORDERED_MAP = 1 };
-enum { W_SUM = 0, W_MEAN = 1, W_NONE = 2, W_UP_DEGREE = 0x10 };
+enum { W_SUM = 0, W_MEAN = 1, W_NONE = 2, W_UP_DEGREE = 0x10, F_MERGE_SRC_DST = 0x20 };
 
 struct Sampler {
   uint64_t V;
@@ -198,6 +198,10 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
   // each sampled layer before its weights (SampledSubgraph::update_degrees,
   // core/FullyRepGraph.hpp:189-207, called at core/ntsFastSampler.hpp:1107-1108)
   const bool up_degree = (weight_flags & W_UP_DEGREE) != 0;
+  // is_merge_src_dst (core/coocsc.hpp:405-411, set by the GAT drivers): every
+  // dst is marked in the frontier too (core/ntsFastSampler.hpp:1050-1052) and
+  // dst_local_id[d] = its local src id (:1095-1097)
+  const bool merge = (weight_flags & F_MERGE_SRC_DST) != 0;
   const int weight_type = weight_flags & 0xF;
   const int L = (int)s.layers.size();
   for (int i = 0; i < L; ++i) {
@@ -255,6 +259,11 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
         for (uint32_t k = 0; k < v; ++k) per_dst(k, tgen, pos);
       }
     }
+    if (merge)
+      for (uint32_t k = 0; k < v; ++k) {
+        const uint32_t g = ly.destination[k];
+        s.bitmap[g >> 6] |= 1ull << (g & 63);
+      }
     // bitmap scan in ascending order -> source, src_index (:1064-1083)
     ly.source.clear();
     for (uint64_t w = 0; w < s.bitmap.size(); ++w) {
@@ -272,6 +281,11 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
     }
     const uint32_t src_size = (uint32_t)ly.source.size();
     ly.src_size = src_size;
+    ly.dst_local_id.clear();
+    if (merge) {
+      ly.dst_local_id.resize(v);
+      for (uint32_t k = 0; k < v; ++k) ly.dst_local_id[k] = s.src_index[ly.destination[k]];
+    }
     // relabel (:1085-1099)
 #pragma omp parallel for num_threads(threads > 1 ? threads : 1)
     for (uint32_t k = 0; k < e; ++k) ly.row_indices[k] = s.src_index[ly.sample_ans[k]];
@@ -288,9 +302,13 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
       }
       ly.row_offset[src_size] = e;
       std::vector<uint32_t> cursor(ly.row_offset.begin(), ly.row_offset.end());
+      ly.csr_edge_id.assign(e, 0);
       for (uint32_t k = 0; k < v; ++k)
-        for (uint32_t j = ly.column_offset[k]; j < ly.column_offset[k + 1]; ++j)
-          ly.column_indices[cursor[ly.row_indices[j]]++] = k;
+        for (uint32_t j = ly.column_offset[k]; j < ly.column_offset[k + 1]; ++j) {
+          const uint32_t slot = cursor[ly.row_indices[j]]++;
+          ly.column_indices[slot] = k;
+          ly.csr_edge_id[slot] = j;
+        }
     }
     // WeightCompute (core/coocsc.hpp:301-324) with Sum / Mean lambdas (:1111-1119)
     std::vector<uint32_t> up_out, up_in;  // per local src / local dst (UP_DEGREE)
@@ -356,6 +374,16 @@ int orc_layer_copy(void* h, int l, uint32_t* destination, uint32_t* column_offse
   if (!ly.edge_weight_backward.empty())
     cp(edge_weight_backward, ly.edge_weight_backward.data(), ly.e_size * 4);
   return 0;
+}
+
+// merge-mode / CSR extras of layer l: dst_local_id [v_size] (if merged),
+// csr_edge_id [e_size] (if the CSR was built)
+int orc_layer_extra(void* h, int l, uint32_t* dst_local_id, uint32_t* csr_edge_id) {
+  Sampler& s = *(Sampler*)h;
+  const Layer& ly = s.layers[l];
+  if (!ly.dst_local_id.empty()) cp(dst_local_id, ly.dst_local_id.data(), ly.v_size * 4);
+  if (!ly.csr_edge_id.empty()) cp(csr_edge_id, ly.csr_edge_id.data(), ly.e_size * 4);
+  return (ly.dst_local_id.empty() ? 0 : 1) | (ly.csr_edge_id.empty() ? 0 : 2);
 }
 
 // Serialized std::mt19937 state (624 words + position), libstdc++ operator<<.

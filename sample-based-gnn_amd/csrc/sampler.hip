@@ -550,17 +550,33 @@ __global__ void k_up_weight(const uint32_t* __restrict__ ri, const uint32_t* __r
   }
 }
 
+// merged src/dst frontier (GAT): every dst is a source too
+__global__ void k_mark_dst(const uint32_t* __restrict__ dst, const uint32_t* sizes,
+                           uint8_t* __restrict__ marks) {
+  const uint32_t v = sizes[0];
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < v; d += gridDim.x * blockDim.x)
+    marks[dst[d]] = 1;
+}
+__global__ void k_dst_local(const uint32_t* __restrict__ dst, const uint32_t* __restrict__ src_index,
+                            const uint32_t* sizes, uint32_t* __restrict__ dl) {
+  const uint32_t v = sizes[0];
+  for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < v; d += gridDim.x * blockDim.x)
+    dl[d] = src_index[dst[d]];
+}
+
 // ---- CSR from sorted (local src, edge id) ----------------------------------
 __global__ void k_csr_finalize(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ seid,
                                const uint32_t* __restrict__ edst, const float* __restrict__ wf,
                                const uint32_t* sizes, uint32_t* __restrict__ ro,
-                               uint32_t* __restrict__ ci, float* __restrict__ wb) {
+                               uint32_t* __restrict__ ci, float* __restrict__ wb,
+                               uint32_t* __restrict__ ceid) {
   const uint32_t e = sizes[1];
   const uint32_t s = sizes[2];
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < e; j += gridDim.x * blockDim.x) {
     const uint32_t key = skey[j];
     const uint32_t eid = seid[j];
     ci[j] = edst[eid];
+    if (ceid) ceid[j] = eid;
     if (wb) wb[j] = wf ? wf[eid] : 0.0f;
     if (j == 0 || skey[j - 1] != key) {
       // rows between the previous key and this one are empty (cannot happen for
@@ -670,6 +686,12 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   }
   NTS_LAUNCH_CHECK();
 
+  if (o->dst_local_id) {
+    hipLaunchKernelGGL(k_mark_dst, dim3(gv), dim3(256), 0, st, o->destination, o->sizes,
+                       ctx->marks);
+    NTS_LAUNCH_CHECK();
+  }
+
   // 3) frontier: ascending compaction of the byte map
   hipLaunchKernelGGL(k_mark_count, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
                      t_blk);
@@ -685,6 +707,12 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                        o->sizes);
   }
   NTS_LAUNCH_CHECK();
+
+  if (o->dst_local_id) {
+    hipLaunchKernelGGL(k_dst_local, dim3(gv), dim3(256), 0, st, o->destination, ctx->src_index,
+                       o->sizes, o->dst_local_id);
+    NTS_LAUNCH_CHECK();
+  }
 
   // 4) relabel to local ids + forward weights
   if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
@@ -704,7 +732,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                              ceil_log2((uint64_t)o->s_cap + 1), t_sort, st));
     hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
                        weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
-                       o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward);
+                       o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
+                       o->csr_edge_id);
     NTS_LAUNCH_CHECK();
   }
   return NTS_OK;

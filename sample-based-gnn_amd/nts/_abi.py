@@ -17,6 +17,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
+ABI_VERSION = 2  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
@@ -36,7 +37,7 @@ EXPORTED = (
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
     "nts_hip_cache_select", "nts_hip_host_alloc", "nts_hip_host_free",
     "nts_hip_host_device_pointer", "nts_hip_gather_rows_cached", "nts_hip_spmm_csc_fwd_cached",
-    "nts_hip_stage_uncached_rows",
+    "nts_hip_stage_uncached_rows", "nts_hip_gat_forward", "nts_hip_gat_backward",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -59,7 +60,7 @@ class SampCSCDev(C.Structure):
         ("sample_ans", C.c_void_p), ("edge_dst", C.c_void_p), ("source", C.c_void_p),
         ("edge_weight_forward", C.c_void_p), ("row_offset", C.c_void_p),
         ("column_indices", C.c_void_p), ("edge_weight_backward", C.c_void_p),
-        ("sizes", C.c_void_p),
+        ("sizes", C.c_void_p), ("dst_local_id", C.c_void_p), ("csr_edge_id", C.c_void_p),
     ]
 
 
@@ -116,11 +117,17 @@ def lib() -> C.CDLL:
         "nts_hip_gather_rows_cached": ([P, P, U64, P, P, U64, P, P, U32, U32, P, U64], I),
         "nts_hip_spmm_csc_fwd_cached": ([P, P, P, P, P, U32, P, U64, P, P, U64, I, P, U32, P, U64], I),
         "nts_hip_stage_uncached_rows": ([P, P, P, U64, P, P, U32, U32, P, U64], I),
+        "nts_hip_gat_forward": ([P, P, P, P, U32, P, U64, U32, P, P, P, P, U64], I),
+        "nts_hip_gat_backward": ([P, P, P, P, U32, P, P, P, U32, P, U64, U32, P, P, P, P, U64,
+                                  P, U64, P, P, P, U64, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
+    if L.nts_hip_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {L.nts_hip_abi_version()}, the bindings expect "
+                          f"{ABI_VERSION}: rebuild it")
     _lib = L
     return L
 

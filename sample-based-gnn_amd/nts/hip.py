@@ -109,6 +109,18 @@ class HipContext:
             cache.stride(0) if cache is not None else ld, ptr(cache_map), spill, ld,
             int(stage is not None), ptr(row_map), F, ptr(y), y.stride(0)))
 
+    def gat_forward(self, co, ri, dl, v, H, att, m, a, Y):
+        F = H.shape[1]
+        check(self.lib.nts_hip_gat_forward(self.h, ptr(co), ptr(ri), ptr(dl), v, ptr(H), H.stride(0),
+                                           F, ptr(att), ptr(m), ptr(a), ptr(Y), Y.stride(0)))
+
+    def gat_backward(self, co, ri, dl, v, ro, ci, ceid, s, H, att, a, m, Y, GY, du, ds2, dH, dS):
+        F = H.shape[1]
+        check(self.lib.nts_hip_gat_backward(
+            self.h, ptr(co), ptr(ri), ptr(dl), v, ptr(ro), ptr(ci), ptr(ceid), s, ptr(H), H.stride(0),
+            F, ptr(att), ptr(a), ptr(m), ptr(Y), Y.stride(0), ptr(GY), GY.stride(0), ptr(du), ptr(ds2),
+            ptr(dH), dH.stride(0), ptr(dS)))
+
     def gather_labels(self, labels, index, n_dev, n_cap, out):
         check(self.lib.nts_hip_gather_labels(self.h, ptr(labels), ptr(index), ptr(n_dev),
                                              n_cap, ptr(out)))
@@ -246,6 +258,7 @@ class LayerBuffers:
     device: torch.device
     csr: bool = True
     weights: bool = True
+    merge: bool = False  # dsts merged into the frontier (GAT): dst_local_id + csr_edge_id
     t: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -265,6 +278,8 @@ class LayerBuffers:
                                               if self.weights else None)
         else:
             self.t["row_offset"] = self.t["column_indices"] = self.t["edge_weight_backward"] = None
+        self.t["dst_local_id"] = _u32(max(self.v_cap, 1), d) if self.merge else None
+        self.t["csr_edge_id"] = _u32(max(self.e_cap, 1), d) if (self.merge and self.csr) else None
 
     def __getattr__(self, k):
         t = self.__dict__.get("t")
@@ -278,21 +293,23 @@ class LayerBuffers:
             self.v_cap, self.e_cap, self.s_cap, ptr(self.destination), ptr(self.v_size),
             ptr(t["column_offset"]), ptr(t["row_indices"]), ptr(t["sample_ans"]), ptr(t["edge_dst"]),
             ptr(t["source"]), ptr(t["edge_weight_forward"]), ptr(t["row_offset"]),
-            ptr(t["column_indices"]), ptr(t["edge_weight_backward"]), ptr(t["sizes"]))
+            ptr(t["column_indices"]), ptr(t["edge_weight_backward"]), ptr(t["sizes"]),
+            ptr(t["dst_local_id"]), ptr(t["csr_edge_id"]))
 
     def sizes_host(self):
         s = self.t["sizes"].cpu().tolist()
         return s[0], s[1], s[2], s[3]
 
 
-def layer_caps(batch: int, fanouts, n_vertices: int, n_edges: int):
+def layer_caps(batch: int, fanouts, n_vertices: int, n_edges: int, merge: bool = False):
     """Upper bounds (v_cap, e_cap, s_cap) per layer: v_0 = B, e_l <= v_l * f_l
-    (or the edge count for fanout -1), s_l <= min(e_l, V), v_{l+1} = s_l."""
+    (or the edge count for fanout -1), s_l <= min(e_l (+ v_l when the dsts are
+    merged into the frontier), V), v_{l+1} = s_l."""
     caps = []
     v = batch
     for f in fanouts:
         e = n_edges if f < 0 else min(v * f, n_edges)
-        s = min(e, n_vertices)
+        s = min(e + (v if merge else 0), n_vertices)
         caps.append((v, e, s))
         v = s
     return caps

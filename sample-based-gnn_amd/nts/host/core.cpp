@@ -36,12 +36,21 @@ static double now_s() {
 }
 
 // ---------------------------------------------------------------------------
+// The structs of include/nts_hip.h are passed by pointer: a host layer built
+// against another header revision must not reach the kernels.
+static void check_abi() {
+  TORCH_CHECK(nts_hip_abi_version() == NTS_HIP_ABI_VERSION, "libnts_hip.so ABI ",
+              nts_hip_abi_version(), " != host layer ABI ", NTS_HIP_ABI_VERSION,
+              ": rebuild (python -c 'import __graft_entry__ as g; g.build()')");
+}
+
 NtsStream::NtsStream(int device, void* stream, uint64_t seed, bool high_priority)
     : device_(device),
       torch_stream_(stream ? c10::hip::getStreamFromExternal((hipStream_t)stream, (c10::DeviceIndex)device)
                            : c10::hip::getStreamFromPool(high_priority, (c10::DeviceIndex)device)) {
   // a pool stream, never the legacy NULL stream: our kernels must not
   // serialise with every other blocking stream of the device
+  check_abi();
   hip_check(nts_hip_ctx_create(&ctx_, device, (void*)torch_stream_.stream(), seed),
             "nts_hip_ctx_create");
 }
@@ -56,6 +65,7 @@ NtsStream::NtsStream(int device, const std::vector<uint32_t>& cu_mask, uint64_t 
     : device_(device),
       torch_stream_(c10::hip::getStreamFromExternal(create_masked(device, cu_mask),
                                                     (c10::DeviceIndex)device)) {
+  check_abi();
   owned_ = torch_stream_.stream();
   hip_check(nts_hip_ctx_create(&ctx_, device, (void*)owned_, seed), "nts_hip_ctx_create");
 }
@@ -147,6 +157,12 @@ nts_graph_dev FullyRepGraph::dev() const {
 }
 
 // ---------------------------------------------------------------------------
+void sampCSC::set_merge_src_dst() {
+  dst_local_id = torch::empty({std::max<int64_t>(v_cap, 1)}, u32_opts(column_offset.device().index()));
+  if (has_csr)
+    csr_edge_id = torch::empty({std::max<int64_t>(e_cap, 1)}, u32_opts(column_offset.device().index()));
+}
+
 sampCSC::sampCSC(int device, VertexId vc, VertexId ec, VertexId sc, bool csr, bool weights)
     : v_cap(vc), e_cap(ec), s_cap(sc), has_csr(csr) {
   auto U = u32_opts(device);
@@ -175,12 +191,12 @@ std::vector<VertexId> sampCSC::host_u32(const torch::Tensor& t, size_t n) const 
 
 static std::vector<std::array<uint64_t, 3>> layer_caps(VertexId batch,
                                                        const std::vector<int>& fanout,
-                                                       VertexId V, uint64_t E) {
+                                                       VertexId V, uint64_t E, bool merge) {
   std::vector<std::array<uint64_t, 3>> caps;
   uint64_t v = batch;
   for (int f : fanout) {
     uint64_t e = f < 0 ? E : std::min<uint64_t>(v * (uint64_t)f, E);
-    uint64_t s = std::min<uint64_t>(e, V);
+    uint64_t s = std::min<uint64_t>(e + (merge ? v : 0), V);
     TORCH_CHECK(e <= 0xFFFFFFFFull, "sampled layer exceeds 2^32 edges");
     caps.push_back({v, e, s});
     v = s;
@@ -190,13 +206,14 @@ static std::vector<std::array<uint64_t, 3>> layer_caps(VertexId batch,
 
 SampledSubgraph::SampledSubgraph(int device, int layers_, const std::vector<int>& fanout_,
                                  VertexId batch, VertexId vertices, uint64_t edges,
-                                 const std::vector<bool>& csr, bool weights)
+                                 const std::vector<bool>& csr, bool weights, bool merge)
     : layers(layers_), fanout(fanout_) {
-  auto caps = layer_caps(batch, fanout, vertices, edges);
+  auto caps = layer_caps(batch, fanout, vertices, edges, merge);
   for (int l = 0; l < layers; ++l) {
     bool c = csr.empty() ? true : (bool)csr[l];
     sampled_sgs.push_back(new sampCSC(device, (VertexId)caps[l][0], (VertexId)caps[l][1],
                                       (VertexId)caps[l][2], c, weights));
+    if (merge) sampled_sgs.back()->set_merge_src_dst();
   }
   host_sizes = torch::empty({layers * 4}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true));
   hip_rt(hipEventCreateWithFlags(&sampled, hipEventDisableTiming), "hipEventCreate");
@@ -212,13 +229,14 @@ SampledSubgraph::~SampledSubgraph() {
 // ---------------------------------------------------------------------------
 FastSampler::FastSampler(std::shared_ptr<FullyRepGraph> g, const std::vector<VertexId>& index,
                          int layers, int batch_size, const std::vector<int>& fanout_,
-                         int pipeline_num, std::vector<bool> csr_layers, bool weights)
+                         int pipeline_num, std::vector<bool> csr_layers, bool weights,
+                         bool merge_src_dst)
     : whole_graph(g), layer(layers), fanout(fanout_), batch_cap_((VertexId)batch_size) {
   TORCH_CHECK((int)fanout.size() == layers, "fanout size != layers");
   if (pipeline_num < 1) pipeline_num = 1;
   for (int i = 0; i < pipeline_num; ++i)
     ssgs.push_back(new SampledSubgraph(g->device, layers, fanout, batch_cap_, g->global_vertices,
-                                       g->global_edges, csr_layers, weights));
+                                       g->global_edges, csr_layers, weights, merge_src_dst));
   ssg = ssgs[0];
   set_sample_nids(index);
   dev_iota_ = torch::arange((int64_t)batch_cap_ + 1, u32_opts(g->device));
@@ -273,7 +291,7 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   const VertexId* vsz = dptr<VertexId>(dev_iota_) + actual;
   for (int l = 0; l < layer; ++l) {
     sampCSC* s = ssg->sampled_sgs[l];
-    nts_sampcsc_dev o;
+    nts_sampcsc_dev o{};
     o.v_cap = s->v_cap;
     o.e_cap = s->e_cap;
     o.s_cap = s->s_cap;
@@ -290,6 +308,8 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
     o.edge_weight_backward =
         (s->has_csr && wt != NTS_WEIGHT_NONE) ? dptr<float>(s->edge_weight_backward) : nullptr;
     o.sizes = dptr<uint32_t>(s->sizes);
+    o.dst_local_id = dptr<uint32_t>(s->dst_local_id);  // undefined (NULL) unless merged
+    o.csr_edge_id = dptr<uint32_t>(s->csr_edge_id);
     const double tl = now_s();
     hip_check(nts_hip_sample_layer(cs.ctx(), &g, fanout[l], l, batch_seq, rng_mode, wt, &o),
               "nts_hip_sample_layer");

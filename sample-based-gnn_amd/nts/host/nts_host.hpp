@@ -116,8 +116,13 @@ class sampCSC {
   bool has_csr = false;
   torch::Tensor destination, column_offset, row_indices, sample_ans, edge_dst, source,
       edge_weight_forward, row_offset, column_indices, edge_weight_backward, sizes;
+  // is_merge_src_dst (GAT): dst d is local src dst_local_id[d]; CSR slot j is
+  // CSC edge csr_edge_id[j] (both undefined unless set_merge_src_dst())
+  torch::Tensor dst_local_id, csr_edge_id;
 
   sampCSC(int device, VertexId v_cap, VertexId e_cap, VertexId s_cap, bool csr, bool weights);
+  void set_merge_src_dst();  // core/coocsc.hpp:405-411
+  VertexId* dev_dst_local_id() const { return dptr<VertexId>(dst_local_id); }
   // the reference accessor names
   VertexId* dev_dst() const { return dptr<VertexId>(destination); }
   VertexId* dev_src() const { return dptr<VertexId>(source); }
@@ -146,7 +151,8 @@ class SampledSubgraph {
   int pending_batch = 0;          // seeds of the issued, not yet finished batch
   SampledSubgraph(int device, int layers, const std::vector<int>& fanout, VertexId batch,
                   VertexId vertices, uint64_t edges, const std::vector<bool>& csr,
-                  bool weights);
+                  bool weights,
+                  bool merge = false);
   ~SampledSubgraph();
 };
 
@@ -206,7 +212,8 @@ class FastSampler {
   // the CSR transpose (backward); empty = all.
   FastSampler(std::shared_ptr<FullyRepGraph> g, const std::vector<VertexId>& index, int layers,
               int batch_size, const std::vector<int>& fanout, int pipeline_num = 1,
-              std::vector<bool> csr_layers = {}, bool weights = true);
+              std::vector<bool> csr_layers = {}, bool weights = true,
+              bool merge_src_dst = false);
   ~FastSampler();
 
   SampledSubgraph* sample_gpu_fast(int batch_size, int ssg_id, NtsStream& cs,
