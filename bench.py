@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--early-agg", action="store_true",
                    help="issue the bottom aggregation behind the sampler on the sampling stream")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
+    p.add_argument("--model", default="gcn", choices=["gcn", "gat"],
+                   help="gcn (headline) or gat (GAT_SAMPLE_ALL_GPU-style attention layers)")
     p.add_argument("--atomic-backward", action="store_true",
                    help="graph-op backward by atomic CSC scatter (no CSR transpose in the "
                         "sampler; nondeterministic sums)")
@@ -137,10 +139,13 @@ def main():
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
-                          deterministic_backward=not args.atomic_backward)
+                          deterministic_backward=not args.atomic_backward,
+                          gat=args.model == "gat")
     fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
                     and not args.early_agg and layers[1] <= 128)
     agg_kernel = ("k_agg_gemm" if fused_linear else "k_spmm_gather")
+    if args.model == "gat":
+        agg_kernel = "k_gat_fwd"  # not timed by the driver's bottom-aggregation events
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
 
     def step():
@@ -219,8 +224,8 @@ def main():
         "dtype": "fp32",
         "data": "synthetic Chung-Lu power-law graph (seed 2024), N(0,1) fp32 features (seed 7), uniform labels",
         "config": {
-            "workload": (f"{'GS' if args.weight == 'mean' else 'GCN'}_SAMPLE_ALLGPU-style "
-                         f"{len(layers) - 1}-layer {'GraphSAGE (mean)' if args.weight == 'mean' else 'GCN'} "
+            "workload": (f"{'GAT_SAMPLE_ALL_GPU' if args.model == 'gat' else ('GS' if args.weight == 'mean' else 'GCN') + '_SAMPLE_ALLGPU'}-style "
+                         f"{len(layers) - 1}-layer {'GAT' if args.model == 'gat' else ('GraphSAGE (mean)' if args.weight == 'mean' else 'GCN')} "
                          f"{'-'.join(map(str, layers))}, fanout "
                          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic "
                          f"(V={V}, E={En}); GPU sampler (Philox"

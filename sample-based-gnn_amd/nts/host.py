@@ -38,7 +38,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                seed=2000, hip_gemm=True, pipeline=True, fuse_linear=False,
                early_aggregate=True, sampler_priority=True, fuse_activation=True,
                fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0,
-               up_degree=False):
+               up_degree=False, gat=False):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -64,6 +64,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.pad_features = bool(pad_features)
     c.cache_rate = float(cache_rate)
     c.up_degree = bool(up_degree)
+    c.gat = bool(gat)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

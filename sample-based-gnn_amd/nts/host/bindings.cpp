@@ -144,6 +144,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("pad_features", &GCNConfig::pad_features)
       .def_readwrite("cache_rate", &GCNConfig::cache_rate)
       .def_readwrite("up_degree", &GCNConfig::up_degree)
+      .def_readwrite("gat", &GCNConfig::gat)
       .def_readwrite("fuse_activation", &GCNConfig::fuse_activation)
       .def_readwrite("shuffle", &GCNConfig::shuffle)
       .def_readwrite("profile", &GCNConfig::profile)

@@ -844,6 +844,95 @@ NtsVar hip_agg_linear_act(const NtsVar& table, const NtsVar& W, NtsVar& y, sampC
                                true);
 }
 
+// GAT layer on a merged src/dst sampled block (GAT_SAMPLE_ALL_GPU's chain,
+// toolkits/GAT_SAMPLE_ALL_GPU.hpp:322-388): H = X W on the MFMA GEMM, then
+// the fused attention/softmax/aggregation/relu kernel; the backward runs the
+// two deterministic GAT backward passes and three GEMMs (dW = X^T dH,
+// dW_att = H^T dS, dX = dH W^T).
+struct HipGATLayerFn : public torch::autograd::Function<HipGATLayerFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar X, NtsVar W, NtsVar Watt, int64_t sg_ptr,
+                        int64_t cs_ptr) {
+    auto* sg = reinterpret_cast<sampCSC*>(sg_ptr);
+    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    TORCH_CHECK(sg->dst_local_id.defined() && sg->csr_edge_id.defined(),
+                "GAT needs a merged src/dst layer with its CSR (set_merge_src_dst)");
+    NtsVar Xc = X.contiguous(), Wc = W.contiguous(), Ac = Watt.contiguous();
+    const int64_t s = sg->src_size, v = sg->v_size, e = sg->e_size;
+    const int64_t Fin = Xc.size(1), F = Wc.size(1);
+    TORCH_CHECK(Xc.size(0) == s && Wc.size(0) == Fin && Ac.numel() == 2 * F, "GAT layer shapes");
+    const int dev = cs->device();
+    NtsVar H = torch::empty({s, F}, f32_opts(dev));
+    hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)s, (int)F, (int)Fin, Xc.data_ptr<float>(),
+                               (uint64_t)Fin, Wc.data_ptr<float>(), (uint64_t)F,
+                               H.data_ptr<float>(), (uint64_t)F),
+              "nts_hip_gemm_f32(H)");
+    NtsVar m = torch::empty({std::max<int64_t>(e, 1)}, f32_opts(dev));
+    NtsVar a = torch::empty({std::max<int64_t>(e, 1)}, f32_opts(dev));
+    NtsVar Y = torch::empty({v, F}, f32_opts(dev));
+    hip_check(nts_hip_gat_forward(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_dst_local_id(),
+                                  (uint32_t)v, H.data_ptr<float>(), (uint64_t)F, (uint32_t)F,
+                                  Ac.data_ptr<float>(), m.data_ptr<float>(), a.data_ptr<float>(),
+                                  Y.data_ptr<float>(), (uint64_t)F),
+              "nts_hip_gat_forward");
+    ctx->save_for_backward({Xc, Wc, Ac, H, Y, m, a});
+    ctx->saved_data["sg"] = sg_ptr;
+    ctx->saved_data["cs"] = cs_ptr;
+    ctx->saved_data["x_grad"] = X.requires_grad();
+    return Y;
+  }
+  static torch::autograd::variable_list backward(AutogradContext* ctx,
+                                                 torch::autograd::variable_list grads) {
+    auto v_ = ctx->get_saved_variables();
+    NtsVar X = v_[0], W = v_[1], A = v_[2], H = v_[3], Y = v_[4], m = v_[5], a = v_[6];
+    auto* sg = reinterpret_cast<sampCSC*>(ctx->saved_data["sg"].toInt());
+    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    NtsVar GY = grads[0].contiguous();
+    const int64_t s = H.size(0), F = H.size(1), Fin = X.size(1), v = Y.size(0);
+    const int64_t e = sg->e_size;
+    const int dev = cs->device();
+    auto guard = cs->guard();
+    NtsVar du = torch::empty({std::max<int64_t>(e, 1)}, f32_opts(dev));
+    NtsVar ds2 = torch::empty({std::max<int64_t>(s, 1)}, f32_opts(dev));
+    NtsVar dH = torch::empty({s, F}, f32_opts(dev));
+    NtsVar dS = torch::empty({s, 2}, f32_opts(dev));
+    hip_check(nts_hip_gat_backward(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_dst_local_id(),
+                                   (uint32_t)v, sg->dev_r_o(), sg->dev_c_i(),
+                                   dptr<uint32_t>(sg->csr_edge_id), (uint32_t)s, H.data_ptr<float>(),
+                                   (uint64_t)F, (uint32_t)F, A.data_ptr<float>(), a.data_ptr<float>(),
+                                   m.data_ptr<float>(), Y.data_ptr<float>(), (uint64_t)F,
+                                   GY.data_ptr<float>(), (uint64_t)F, du.data_ptr<float>(),
+                                   ds2.data_ptr<float>(), dH.data_ptr<float>(), (uint64_t)F,
+                                   dS.data_ptr<float>()),
+              "nts_hip_gat_backward");
+    NtsVar dW = torch::empty({Fin, F}, f32_opts(dev));
+    hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)Fin, (int)F, (int)s, X.data_ptr<float>(),
+                               (uint64_t)Fin, dH.data_ptr<float>(), (uint64_t)F,
+                               dW.data_ptr<float>(), (uint64_t)F),
+              "nts_hip_gemm_f32(dW)");
+    NtsVar T = torch::empty({F, 2}, f32_opts(dev));
+    hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)F, 2, (int)s, H.data_ptr<float>(), (uint64_t)F,
+                               dS.data_ptr<float>(), 2, T.data_ptr<float>(), 2),
+              "nts_hip_gemm_f32(dW_att)");
+    NtsVar dA = T.t().contiguous().view({2 * F, 1});  // [a1 | a2] as W_att's rows
+    NtsVar dX;
+    if (ctx->saved_data["x_grad"].toBool()) {
+      NtsVar Wt = W.t().contiguous();
+      dX = torch::empty({s, Fin}, f32_opts(dev));
+      hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)s, (int)Fin, (int)F, dH.data_ptr<float>(),
+                                 (uint64_t)F, Wt.data_ptr<float>(), (uint64_t)Fin,
+                                 dX.data_ptr<float>(), (uint64_t)Fin),
+                "nts_hip_gemm_f32(dX)");
+    }
+    return {dX, dW, dA.view(A.sizes()), NtsVar(), NtsVar()};
+  }
+};
+
+NtsVar hip_gat_layer(const NtsVar& x, const NtsVar& W, const NtsVar& Watt, sampCSC* sg,
+                     NtsStream* cs) {
+  return HipGATLayerFn::apply(x, W, Watt, reinterpret_cast<int64_t>(sg),
+                              reinterpret_cast<int64_t>(cs));
+}
+
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {
   return HipLinearFn::apply(x, W, reinterpret_cast<int64_t>(cs));
 }

@@ -66,6 +66,10 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // outermost, whose backward the context skips)
   std::vector<bool> csr(L, cfg.deterministic_backward);
   csr[L - 1] = false;
+  if (cfg.gat) {  // every layer's backward runs over its CSR; dsts merged into the frontier
+    csr.assign(L, true);
+    TORCH_CHECK(!cfg.fuse_linear, "GAT: no fused bottom aggregation + GEMM");  // early_aggregate ignored
+  }
   // Pipelined: three sampler slots.  Batch k+1 is sampled into the slot of
   // batch k-2, whose training finished before batch k-1's began, so the
   // sampling stream never waits on an unfinished event when its kernels are
@@ -74,7 +78,8 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   nslots_ = cfg.pipeline ? kSlots : 1;
   sampler = std::make_unique<FastSampler>(graph, train_nids, L, cfg.batch_size, cfg.fanout,
                                           nslots_, csr,
-                                          cfg.weight_type != WeightType::None);
+                                          !cfg.gat && cfg.weight_type != WeightType::None,
+                                          cfg.gat);
   sampler->rng_mode = cfg.rng_mode;
   sampler->up_degree = cfg.up_degree;
   if (cfg.pipeline && cfg.sampler_cus > 0)
@@ -94,7 +99,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // feature table only (not on the weights), so it is issued right behind the
   // sampling, on the sampling stream: with the pipeline it runs while the
   // previous batch trains (HBM-bound gather next to MFMA-bound GEMMs).
-  early_ = cfg.early_aggregate && cfg.fused_gather;
+  early_ = cfg.early_aggregate && cfg.fused_gather && !cfg.gat;
   for (int i = 0; i < nslots_; ++i) {
     TORCH_CHECK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming) == hipSuccess,
                 "hipEventCreate");
@@ -150,7 +155,8 @@ void GCN_SAMPLE_ALLGPU_impl::mark(const char* what, NtsStream& st) {
 
 void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
   mark("S<", st);
-  sampler->issue_gpu_sample(cfg.batch_size, slot, st, cfg.weight_type);
+  sampler->issue_gpu_sample(cfg.batch_size, slot, st,
+                            cfg.gat ? WeightType::None : cfg.weight_type);
   if (early_) {
     auto guard = st.guard();
     const int L = (int)P.size();
@@ -215,10 +221,15 @@ double GCN_SAMPLE_ALLGPU_impl::resolve_profile() {
 }
 
 void GCN_SAMPLE_ALLGPU_impl::init_nn() {
-  for (size_t i = 0; i + 1 < cfg.layer_size.size(); ++i)
+  for (size_t i = 0; i + 1 < cfg.layer_size.size(); ++i) {
     P.push_back(new Parameter(cfg.layer_size[i], cfg.layer_size[i + 1], cfg.learn_rate, cfg.beta1,
                               cfg.beta2, cfg.epsilon, cfg.weight_decay, graph->device,
                               cfg.seed + (int64_t)i));
+    if (cfg.gat)  // attention vector W_att [2 F_{l+1}, 1] (GAT_SAMPLE_ALL_GPU.hpp:141-147)
+      P.push_back(new Parameter(2 * cfg.layer_size[i + 1], 1, cfg.learn_rate, cfg.beta1,
+                                cfg.beta2, cfg.epsilon, cfg.weight_decay, graph->device,
+                                cfg.seed + 1000 + (int64_t)i));
+  }
   if (cfg.hip_gemm)
     for (auto* p : P) p->cs = cs.get();
   int64_t n = 0;
@@ -351,6 +362,22 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
   return acts;
 }
 
+std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_gat(SampledSubgraph* sg) {
+  const int L = (int)sg->layers;
+  NtsVar X;
+  if (fcache)
+    sampler->load_feature_gpu_cache(*cs, sg, X, *fcache);
+  else
+    sampler->load_feature_gpu(*cs, sg, X, F);
+  std::vector<NtsVar> acts;
+  for (int l = 0; l < L; ++l) {
+    const int hop = L - 1 - l;  // X_{l+1} = relu(attention aggregate of X_l W_l)
+    X = hip_gat_layer(X, P[2 * l]->W, P[2 * l + 1]->W, sg->sampled_sgs[hop], cs.get());
+    acts.push_back(X);
+  }
+  return acts;
+}
+
 void GCN_SAMPLE_ALLGPU_impl::Loss(NtsVar& left, NtsVar& right) {
   NtsVar a = left.log_softmax(1);
   loss = torch::nll_loss(a, right);
@@ -432,16 +459,23 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   ctx.train();
   if (early_) account_bottom(sg, true);
   const int L = (int)P.size();
-  const bool fuse_loss = cfg.fuse_loss && cfg.hip_gemm && L >= 2 &&
-                         hip_linear_xent_supported(P[L - 1]->W.size(0), P[L - 1]->W.size(1));
-  auto acts = forward(sg, false, early_ ? &pre_y_[slot] : nullptr, fuse_loss ? &target : nullptr);
-  if (fuse_loss) {
-    loss = acts.back();
+  if (cfg.gat) {  // GAT_SAMPLE_ALL_GPU::Loss + loss.backward() (toolkits/GAT_SAMPLE_ALL_GPU.hpp:393-399)
+    auto acts = forward_gat(sg);
+    loss = torch::nll_loss(acts.back().log_softmax(1), target);
+    loss.backward();
+    ctx.reset();
   } else {
-    NtsVar out = acts.back();
-    Loss(out, target);
+    const bool fuse_loss = cfg.fuse_loss && cfg.hip_gemm && L >= 2 &&
+                           hip_linear_xent_supported(P[L - 1]->W.size(0), P[L - 1]->W.size(1));
+    auto acts = forward(sg, false, early_ ? &pre_y_[slot] : nullptr, fuse_loss ? &target : nullptr);
+    if (fuse_loss) {
+      loss = acts.back();
+    } else {
+      NtsVar out = acts.back();
+      Loss(out, target);
+    }
+    ctx.self_backward(false);
   }
-  ctx.self_backward(false);
   Update();
   for (auto* p : P) p->zero_grad();
   TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)cs->stream()) == hipSuccess,
@@ -483,18 +517,24 @@ float GCN_SAMPLE_ALLGPU_impl::run_epoch() {
 std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<VertexId>& seeds,
                                                          uint64_t batch_seq) {
   auto guard = cs->guard();
-  const int L = (int)P.size();
-  std::vector<bool> csr(L, false);
+  const int L = (int)cfg.fanout.size();
+  std::vector<bool> csr(L, cfg.gat);
   FastSampler s(graph, seeds, L, (int)seeds.size(), cfg.fanout, 1, csr,
-                cfg.weight_type != WeightType::None);
+                !cfg.gat && cfg.weight_type != WeightType::None, cfg.gat);
   s.rng_mode = cfg.rng_mode;
   s.up_degree = cfg.up_degree;
   s.batch_seq = batch_seq;
-  SampledSubgraph* sg = s.sample_gpu_fast((int)seeds.size(), 0, *cs, cfg.weight_type);
+  SampledSubgraph* sg = s.sample_gpu_fast((int)seeds.size(), 0, *cs,
+                                          cfg.gat ? WeightType::None : cfg.weight_type);
   ctx.eval();
   torch::NoGradGuard ng;
-  auto acts = forward(sg, true);
-  acts.pop_back();
+  std::vector<NtsVar> acts;
+  if (cfg.gat) {
+    acts = forward_gat(sg);
+  } else {
+    acts = forward(sg, true);
+    acts.pop_back();
+  }
   ctx.train();
   cs->synchronize();
   return acts;

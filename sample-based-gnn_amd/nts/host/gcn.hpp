@@ -14,6 +14,7 @@ struct GCNConfig {
   int rng_mode = NTS_RNG_PHILOX;
   WeightType weight_type = WeightType::Sum;  // GraphSAGE toolkits: Mean
   bool up_degree = false;             // UP_DEGREE cfg key (core/GraphSegment.cpp:273-276)
+  bool gat = false;                   // GAT_SAMPLE_ALL_GPU model (attention layers)
   bool fused_gather = true;           // gather features inside the bottom aggregation
   bool bias_correction = false;       // false: learn_local_with_decay_Adam (GPU drivers)
   bool deterministic_backward = true; // CSR transpose gather instead of atomics
@@ -76,6 +77,8 @@ class GCN_SAMPLE_ALLGPU_impl {
   std::vector<NtsVar> forward(SampledSubgraph* sg, bool keep, const NtsVar* pre_y = nullptr,
                               const NtsVar* loss_target = nullptr);
   void issue(int slot, NtsStream& st);
+  // GAT_SAMPLE_ALL_GPU::Forward (toolkits/GAT_SAMPLE_ALL_GPU.hpp:308-391)
+  std::vector<NtsVar> forward_gat(SampledSubgraph* sg);
   void account_bottom(SampledSubgraph* sg, bool fused_map);
   void Loss(NtsVar& left, NtsVar& right);
   void Update();

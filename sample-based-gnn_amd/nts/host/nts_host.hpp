@@ -352,6 +352,10 @@ class NtsContext {
 // x.matmul(W) on the MFMA fp32 kernels (nts_hip_gemm_f32) with its own
 // backward: dW = x^T dZ (split-reduction, deterministic), dx = dZ W^T.
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
+// one GAT layer (H = X W, attention softmax over each dst's sampled edges,
+// relu(sum a H[src])) on a merged src/dst layer: [src_size, F_in] -> [v_size, F]
+NtsVar hip_gat_layer(const NtsVar& x, const NtsVar& W, const NtsVar& Watt, sampCSC* sg,
+                     NtsStream* cs);
 // CU masks splitting the device: `n` CUs spread evenly over the chip
 // (every (total/n)-th CU) and the complement
 std::vector<uint32_t> cu_mask_spread(int device, int n, bool complement);
