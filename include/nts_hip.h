@@ -298,7 +298,8 @@ int nts_hip_gat_forward(nts_hip_ctx *ctx, const uint32_t *column_offset,
 /* Its backward for dL/dY = GY (deterministic: a per-destination pass and a
  * per-source pass over the CSR with csr_edge_id; no atomics):
  *   du[e] = dL/d(pre-leaky score of e), ds2[v] = dL/d(H[v].a2) (zero for
- *   non-destinations), dH [src_size x F] = dL/dH, dS [src_size x 2] =
+ *   non-destinations), GM [v_size x F] = GY masked by Y > 0 (scratch, ld ldm),
+ *   dH [src_size x F] = dL/dH, dS [src_size x 2] =
  *   (dL/d(H[v].a1), dL/d(H[v].a2)) so that dW_att = H^T dS (caller's GEMM). */
 int nts_hip_gat_backward(nts_hip_ctx *ctx, const uint32_t *column_offset,
                          const uint32_t *row_indices, const uint32_t *dst_local_id,
@@ -307,7 +308,7 @@ int nts_hip_gat_backward(nts_hip_ctx *ctx, const uint32_t *column_offset,
                          uint32_t src_size, const float *H, uint64_t ldh, uint32_t F,
                          const float *att, const float *a, const float *m, const float *Y,
                          uint64_t ldy, const float *GY, uint64_t ldg, float *du, float *ds2,
-                         float *dH, uint64_t lddh, float *dS);
+                         float *GM, uint64_t ldm, float *dH, uint64_t lddh, float *dS);
 
 /* ---- dense layer update (MFMA fp32) -------------------------------------- */
 /* Row-major fp32 GEMM on the matrix cores (v_mfma_f32_16x16x4_f32 /

@@ -14,7 +14,7 @@
 // neighbour row once and keeps an online softmax (running max / sum, the
 // accumulator rescaled when the max grows).  Backward (all deterministic,
 // no atomics):
-//   k_gat_bwd_dst  per dst: g = G (.) [X' > 0]; ga_e = g . H[src_e];
+//   k_gat_bwd_dst  per dst: g = G (.) [X' > 0] (stored: GM); ga_e = g . H[src_e];
 //                  du_e = a_e (ga_e - sum a ga) * leaky'(m_e); ds2[dst_local(d)] = sum du_e
 //   k_gat_bwd_src  per src v over the CSR: dH[v] = sum a_e g_{d_e} + ds1[v] a1 + ds2[v] a2,
 //                  ds1[v] = sum du_e;  dS[v] = (ds1[v], ds2[v])
@@ -24,6 +24,7 @@
 namespace nts_hip {
 
 constexpr int kGatThreads = 256;  // 4 waves, one destination / source each
+constexpr int kGatU = 4;          // neighbour rows in flight per wave
 
 __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
@@ -103,26 +104,39 @@ __global__ __launch_bounds__(kGatThreads) void k_gat_fwd(
     const uint32_t ne = min(end - cb, 64u);
     const uint32_t my_r = lane < (int)ne ? ri[cb + lane] : 0u;
     float my_m = 0.f;
-    for (uint32_t j = 0; j < ne; ++j) {
-      const uint32_t r = (uint32_t)__shfl((int)my_r, (int)j, 64);
-      const T* hr = reinterpret_cast<const T*>(H + (uint64_t)r * ldh);
-      T x[NCH];
-      float p1 = 0.f;
+    for (uint32_t j0 = 0; j0 < ne; j0 += kGatU) {  // kGatU neighbour rows in flight
+      T x[kGatU][NCH];
+      float p1[kGatU];
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const uint32_t col = lane + 64 * c;
-        x[c] = col < nvec ? hr[col] : G::zero();
-        p1 += G::dot(x[c], w1[c]);
+      for (int u = 0; u < kGatU; ++u) {
+        const bool ok = j0 + u < ne;
+        const uint32_t r = (uint32_t)__shfl((int)my_r, (int)min(j0 + u, ne - 1), 64);
+        const T* hr = reinterpret_cast<const T*>(H + (uint64_t)r * ldh);
+        p1[u] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = lane + 64 * c;
+          x[u][c] = (ok && col < nvec) ? hr[col] : G::zero();
+          p1[u] += G::dot(x[u][c], w1[c]);
+        }
       }
-      const float m = leaky(wave_sum(p1) + s2);
-      if (lane == (int)j) my_m = m;
-      const float Mn = fmaxf(M, m);
-      const float sc = expf(M - Mn);  // 0 for the first edge (M = -inf)
-      const float p = expf(m - Mn);
-      S = S * sc + p;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) acc[c] = G::axpy(G::scale(acc[c], sc), p, x[c]);
-      M = Mn;
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < kGatU; ++u) p1[u] += __shfl_xor(p1[u], o, 64);
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        if (j0 + u >= ne) break;
+        const float m = leaky(p1[u] + s2);
+        if (lane == (int)(j0 + u)) my_m = m;
+        const float Mn = fmaxf(M, m);
+        const float sc = expf(M - Mn);  // 0 for the first edge (M = -inf)
+        const float p = expf(m - Mn);
+        S = S * sc + p;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) acc[c] = G::axpy(G::scale(acc[c], sc), p, x[u][c]);
+        M = Mn;
+      }
     }
     if (lane < (int)ne) m_out[cb + lane] = my_m;
   }
@@ -144,7 +158,7 @@ __global__ __launch_bounds__(kGatThreads) void k_gat_bwd_dst(
     const uint32_t* __restrict__ dl, uint32_t nv_dst, const float* __restrict__ H, uint64_t ldh,
     uint32_t nvec, const float* __restrict__ a, const float* __restrict__ m,
     const float* __restrict__ Y, uint64_t ldy, const float* __restrict__ GY, uint64_t ldg,
-    float* __restrict__ du, float* __restrict__ ds2) {
+    float* __restrict__ du, float* __restrict__ ds2, float* __restrict__ GM, uint64_t ldm) {
   using G = GV<VEC>;
   using T = typename G::T;
   const int lane = threadIdx.x & 63;
@@ -152,11 +166,13 @@ __global__ __launch_bounds__(kGatThreads) void k_gat_bwd_dst(
   if (d >= nv_dst) return;
   const T* gy = reinterpret_cast<const T*>(GY + (uint64_t)d * ldg);
   const T* yy = reinterpret_cast<const T*>(Y + (uint64_t)d * ldy);
+  T* gm = reinterpret_cast<T*>(GM + (uint64_t)d * ldm);
   T g[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const uint32_t col = lane + 64 * c;
     g[c] = col < nvec ? G::mask(gy[col], yy[col]) : G::zero();
+    if (col < nvec) gm[col] = g[c];  // relu-masked gradient, read per edge by k_gat_bwd_src
   }
   const uint32_t beg = co[d], end = co[d + 1];
   // pass 1: ga_e = g . H[src_e] (kept by the lane owning e, chunk by chunk:
@@ -166,17 +182,27 @@ __global__ __launch_bounds__(kGatThreads) void k_gat_bwd_dst(
     const uint32_t ne = min(end - cb, 64u);
     const uint32_t my_r = lane < (int)ne ? ri[cb + lane] : 0u;
     float my_ga = 0.f;
-    for (uint32_t j = 0; j < ne; ++j) {
-      const uint32_t r = (uint32_t)__shfl((int)my_r, (int)j, 64);
-      const T* hr = reinterpret_cast<const T*>(H + (uint64_t)r * ldh);
-      float p = 0.f;
+    for (uint32_t j0 = 0; j0 < ne; j0 += kGatU) {
+      float p[kGatU];
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const uint32_t col = lane + 64 * c;
-        if (col < nvec) p += G::dot(g[c], hr[col]);
+      for (int u = 0; u < kGatU; ++u) {
+        const bool ok = j0 + u < ne;
+        const uint32_t r = (uint32_t)__shfl((int)my_r, (int)min(j0 + u, ne - 1), 64);
+        const T* hr = reinterpret_cast<const T*>(H + (uint64_t)r * ldh);
+        p[u] = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = lane + 64 * c;
+          if (ok && col < nvec) p[u] += G::dot(g[c], hr[col]);
+        }
       }
-      const float ga = wave_sum(p);
-      if (lane == (int)j) my_ga = ga;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < kGatU; ++u) p[u] += __shfl_xor(p[u], o, 64);
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u)
+        if (lane == (int)(j0 + u)) my_ga = p[u];
     }
     if (lane < (int)ne) {
       du[cb + lane] = my_ga;
@@ -202,9 +228,8 @@ __global__ __launch_bounds__(kGatThreads) void k_gat_bwd_src(
     const uint32_t* __restrict__ ro, const uint32_t* __restrict__ ci,
     const uint32_t* __restrict__ ceid, uint32_t nv_src, uint32_t nvec,
     const float* __restrict__ a, const float* __restrict__ du, const float* __restrict__ ds2,
-    const float* __restrict__ att, const float* __restrict__ Y, uint64_t ldy,
-    const float* __restrict__ GY, uint64_t ldg, float* __restrict__ dH, uint64_t lddh,
-    float* __restrict__ dS) {
+    const float* __restrict__ att, const float* __restrict__ GM, uint64_t ldm,
+    float* __restrict__ dH, uint64_t lddh, float* __restrict__ dS) {
   using G = GV<VEC>;
   using T = typename G::T;
   const int lane = threadIdx.x & 63;
@@ -226,16 +251,28 @@ __global__ __launch_bounds__(kGatThreads) void k_gat_bwd_src(
       my_u = du[eid];
     }
     s1 += my_u;
-    for (uint32_t j = 0; j < ne; ++j) {
-      const uint32_t dd = (uint32_t)__shfl((int)my_d, (int)j, 64);
-      const float w = __shfl(my_a, (int)j, 64);
-      const T* gy = reinterpret_cast<const T*>(GY + (uint64_t)dd * ldg);
-      const T* yy = reinterpret_cast<const T*>(Y + (uint64_t)dd * ldy);
+    for (uint32_t j0 = 0; j0 < ne; j0 += kGatU) {
+      T x[kGatU][NCH];
+      float w[kGatU];
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const uint32_t col = lane + 64 * c;
-        if (col < nvec) acc[c] = G::axpy(acc[c], w, G::mask(gy[col], yy[col]));
+      for (int u = 0; u < kGatU; ++u) {
+        const bool ok = j0 + u < ne;
+        const int jj = (int)min(j0 + u, ne - 1);
+        const uint32_t dd = (uint32_t)__shfl((int)my_d, jj, 64);
+        w[u] = ok ? __shfl(my_a, jj, 64) : 0.f;
+        const T* gm = reinterpret_cast<const T*>(GM + (uint64_t)dd * ldm);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = lane + 64 * c;
+          x[u][c] = (ok && col < nvec) ? gm[col] : G::zero();
+        }
       }
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u)
+        if (j0 + u < ne) {  // edge order kept
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) acc[c] = G::axpy(acc[c], w[u], x[u][c]);
+        }
     }
   }
   s1 = wave_sum(s1);
@@ -316,27 +353,29 @@ int nts_hip_gat_backward(nts_hip_ctx* ctx, const uint32_t* column_offset,
                          uint32_t src_size, const float* H, uint64_t ldh, uint32_t F,
                          const float* att, const float* a, const float* m, const float* Y,
                          uint64_t ldy, const float* GY, uint64_t ldg, float* du, float* ds2,
-                         float* dH, uint64_t lddh, float* dS) {
+                         float* GM, uint64_t ldm, float* dH, uint64_t lddh, float* dS) {
   NTS_CHECK_ARG(ctx && column_offset && row_indices && dst_local_id && row_offset &&
                     column_indices && csr_edge_id && H && att && a && m && Y && GY && du &&
-                    ds2 && dH && dS,
+                    ds2 && GM && dH && dS,
                 "NULL argument");
+  NTS_CHECK_ARG(ldm >= F, "leading dimension of GM");
   NTS_CHECK_ARG(ldh >= F && ldy >= F && ldg >= F && lddh >= F, "leading dimension");
   if (F == 0) return NTS_OK;
   NTS_HIP_TRY(hipSetDevice(ctx->device));
   const hipStream_t st = ctx->stream;
   if (src_size) NTS_HIP_TRY(hipMemsetAsync(ds2, 0, (size_t)src_size * sizeof(float), st));
   const bool v4 = gat_vec4(F, ldh, ldy, H, Y, att) && ldg % 4 == 0 && lddh % 4 == 0 &&
-                  ((uintptr_t)GY % 16) == 0 && ((uintptr_t)dH % 16) == 0;
+                  ldm % 4 == 0 && ((uintptr_t)GY % 16) == 0 && ((uintptr_t)dH % 16) == 0 &&
+                  ((uintptr_t)GM % 16) == 0;
   if (v_size) {
     const uint32_t n = v_size;
-#define ARGS column_offset, row_indices, dst_local_id, v_size, H, ldh, nvec, a, m, Y, ldy, GY, ldg, du, ds2
+#define ARGS column_offset, row_indices, dst_local_id, v_size, H, ldh, nvec, a, m, Y, ldy, GY, ldg, du, ds2, GM, ldm
     NTS_GAT_DISPATCH(k_gat_bwd_dst, ARGS);
 #undef ARGS
   }
   if (src_size) {
     const uint32_t n = src_size;
-#define ARGS row_offset, column_indices, csr_edge_id, src_size, nvec, a, du, ds2, att, Y, ldy, GY, ldg, dH, lddh, dS
+#define ARGS row_offset, column_indices, csr_edge_id, src_size, nvec, a, du, ds2, att, GM, ldm, dH, lddh, dS
     NTS_GAT_DISPATCH(k_gat_bwd_src, ARGS);
 #undef ARGS
   }

@@ -119,7 +119,7 @@ def lib() -> C.CDLL:
         "nts_hip_stage_uncached_rows": ([P, P, P, U64, P, P, U32, U32, P, U64], I),
         "nts_hip_gat_forward": ([P, P, P, P, U32, P, U64, U32, P, P, P, P, U64], I),
         "nts_hip_gat_backward": ([P, P, P, P, U32, P, P, P, U32, P, U64, U32, P, P, P, P, U64,
-                                  P, U64, P, P, P, U64, P], I),
+                                  P, U64, P, P, P, U64, P, U64, P], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -114,12 +114,15 @@ class HipContext:
         check(self.lib.nts_hip_gat_forward(self.h, ptr(co), ptr(ri), ptr(dl), v, ptr(H), H.stride(0),
                                            F, ptr(att), ptr(m), ptr(a), ptr(Y), Y.stride(0)))
 
-    def gat_backward(self, co, ri, dl, v, ro, ci, ceid, s, H, att, a, m, Y, GY, du, ds2, dH, dS):
+    def gat_backward(self, co, ri, dl, v, ro, ci, ceid, s, H, att, a, m, Y, GY, du, ds2, dH, dS,
+                     GM=None):
         F = H.shape[1]
+        if GM is None:
+            GM = torch.empty(max(v, 1), F, device=H.device)
         check(self.lib.nts_hip_gat_backward(
             self.h, ptr(co), ptr(ri), ptr(dl), v, ptr(ro), ptr(ci), ptr(ceid), s, ptr(H), H.stride(0),
             F, ptr(att), ptr(a), ptr(m), ptr(Y), Y.stride(0), ptr(GY), GY.stride(0), ptr(du), ptr(ds2),
-            ptr(dH), dH.stride(0), ptr(dS)))
+            ptr(GM), GM.stride(0), ptr(dH), dH.stride(0), ptr(dS)))
 
     def gather_labels(self, labels, index, n_dev, n_cap, out):
         check(self.lib.nts_hip_gather_labels(self.h, ptr(labels), ptr(index), ptr(n_dev),

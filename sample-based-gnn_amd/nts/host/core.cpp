@@ -361,8 +361,8 @@ void FastSampler::load_feature_gpu(NtsStream& cs, SampledSubgraph* sg, NtsVar& l
   sampCSC* top = sg->sampled_sgs[layer - 1];
   const int64_t F = global_feature.size(1);
   if (!local_feature.defined() || local_feature.size(0) != (int64_t)top->src_size ||
-      local_feature.size(1) != F)
-    local_feature = torch::empty({(int64_t)top->src_size, F}, f32_opts(whole_graph->device));
+      local_feature.size(1) != F)  // 128-byte row pitch: float4 rows for the GEMMs
+    local_feature = row_padded_empty((int64_t)top->src_size, F, whole_graph->device);
   hip_check(nts_hip_gather_rows(cs.ctx(), global_feature.data_ptr<float>(),
                                 (uint64_t)global_feature.stride(0), top->dev_src(), nullptr,
                                 top->src_size, (uint32_t)F, local_feature.data_ptr<float>(),
@@ -856,14 +856,14 @@ struct HipGATLayerFn : public torch::autograd::Function<HipGATLayerFn> {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     TORCH_CHECK(sg->dst_local_id.defined() && sg->csr_edge_id.defined(),
                 "GAT needs a merged src/dst layer with its CSR (set_merge_src_dst)");
-    NtsVar Xc = X.contiguous(), Wc = W.contiguous(), Ac = Watt.contiguous();
+    NtsVar Xc = row_major(X), Wc = W.contiguous(), Ac = Watt.contiguous();
     const int64_t s = sg->src_size, v = sg->v_size, e = sg->e_size;
     const int64_t Fin = Xc.size(1), F = Wc.size(1);
     TORCH_CHECK(Xc.size(0) == s && Wc.size(0) == Fin && Ac.numel() == 2 * F, "GAT layer shapes");
     const int dev = cs->device();
     NtsVar H = torch::empty({s, F}, f32_opts(dev));
     hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)s, (int)F, (int)Fin, Xc.data_ptr<float>(),
-                               (uint64_t)Fin, Wc.data_ptr<float>(), (uint64_t)F,
+                               (uint64_t)Xc.stride(0), Wc.data_ptr<float>(), (uint64_t)F,
                                H.data_ptr<float>(), (uint64_t)F),
               "nts_hip_gemm_f32(H)");
     NtsVar m = torch::empty({std::max<int64_t>(e, 1)}, f32_opts(dev));
@@ -895,18 +895,19 @@ struct HipGATLayerFn : public torch::autograd::Function<HipGATLayerFn> {
     NtsVar ds2 = torch::empty({std::max<int64_t>(s, 1)}, f32_opts(dev));
     NtsVar dH = torch::empty({s, F}, f32_opts(dev));
     NtsVar dS = torch::empty({s, 2}, f32_opts(dev));
+    NtsVar GM = torch::empty({std::max<int64_t>(v, 1), F}, f32_opts(dev));
     hip_check(nts_hip_gat_backward(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_dst_local_id(),
                                    (uint32_t)v, sg->dev_r_o(), sg->dev_c_i(),
                                    dptr<uint32_t>(sg->csr_edge_id), (uint32_t)s, H.data_ptr<float>(),
                                    (uint64_t)F, (uint32_t)F, A.data_ptr<float>(), a.data_ptr<float>(),
                                    m.data_ptr<float>(), Y.data_ptr<float>(), (uint64_t)F,
                                    GY.data_ptr<float>(), (uint64_t)F, du.data_ptr<float>(),
-                                   ds2.data_ptr<float>(), dH.data_ptr<float>(), (uint64_t)F,
-                                   dS.data_ptr<float>()),
+                                   ds2.data_ptr<float>(), GM.data_ptr<float>(), (uint64_t)F,
+                                   dH.data_ptr<float>(), (uint64_t)F, dS.data_ptr<float>()),
               "nts_hip_gat_backward");
     NtsVar dW = torch::empty({Fin, F}, f32_opts(dev));
     hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)Fin, (int)F, (int)s, X.data_ptr<float>(),
-                               (uint64_t)Fin, dH.data_ptr<float>(), (uint64_t)F,
+                               (uint64_t)X.stride(0), dH.data_ptr<float>(), (uint64_t)F,
                                dW.data_ptr<float>(), (uint64_t)F),
               "nts_hip_gemm_f32(dW)");
     NtsVar T = torch::empty({F, 2}, f32_opts(dev));
