@@ -265,7 +265,7 @@ def test_gat_training_deterministic_and_learns(E, graph):
     for _ in range(3):
         a.run_epoch()
         b.run_epoch()
-        losses.append(float(a.loss))
+        losses.append(float(a.loss.detach()))
     a.synchronize()
     b.synchronize()
     for x, y in zip(a.weights(), b.weights()):
