@@ -4,9 +4,11 @@ Reddit-shaped synthetic graph (BASELINE.json configs[1]: GCN_SAMPLE_GPU-style
 602-128-41, fanout 25-10, batch 10,000, V=232,965, E~114.8M incl. self-loops).
 
 A step = one mini-batch of the hot path, everything on the GPU: GPU neighbour
-sampling (2 hops) -> label gather -> fused feature gather + hop-1 aggregation
--> GEMM/ReLU/dropout -> hop-0 aggregation -> GEMM/log_softmax -> NLL ->
-backward (CSR transpose aggregation + GEMM grads) -> [RCCL all-reduce] -> Adam.
+sampling (2 hops, on its own stream, batches ahead) -> label gather -> bottom
+layer (transform-first: row-gathered GEMM X[src] W0, then the aggregation with
+relu/dropout fused) -> hop-0 aggregation -> output layer + log_softmax + NLL ->
+backward (CSR transpose aggregations, gathered weight-gradient GEMM) ->
+[RCCL all-reduce] -> Adam.
 
 value = sampled edges of all ranks in the K timed steps / max-over-ranks wall
 time.  Inputs are resident in HBM before the timed region.
@@ -17,6 +19,7 @@ Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import pathlib
@@ -30,13 +33,22 @@ sys.path.insert(0, str(ROOT / "sample-based-gnn_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-METRIC = "sampled-edges/sec + epoch time, 2-hop GCN on Reddit-shaped graph @1/2/4/8 GPUs"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TF = 157.3  # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
+SHAPE_NAMES = {"reddit": "Reddit", "products": "ogbn-products", "papers100m": "ogbn-papers100M",
+               "tiny": "tiny"}
 
 
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
+
+
+def default_cpu_threads() -> int:
+    """The reference's sampler uses nproc-1 threads (core/FullyRepGraph.hpp:49);
+    capped by the CPU share this job has (OMP_NUM_THREADS, 16 on the GPU box)."""
+    share = int(os.environ.get("OMP_NUM_THREADS") or 16)
+    return max(1, min((os.cpu_count() or 2) - 1, share))
 
 
 def parse():
@@ -50,13 +62,16 @@ def parse():
     p.add_argument("--hidden", type=int, default=128)
     p.add_argument("--layers", default=None,
                    help="layer widths a-b-...-c (default: F-hidden-classes of the shape)")
-    p.add_argument("--weight", default="sum", choices=["sum", "mean"],
-                   help="edge weights: GCN sum (default) or GraphSAGE mean")
+    p.add_argument("--weight", default="sum", choices=["sum", "mean", "mean-sampled"],
+                   help="edge weights: GCN sum (default), GraphSAGE mean (CPU formula) or the "
+                        "reference GPU kernel's mean (by sampled count)")
+    p.add_argument("--transform-first", type=int, default=-1, choices=[-1, 0, 1],
+                   help="bottom layer order: 1 A(XW), 0 (AX)W (the reference's), -1 auto")
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
     p.add_argument("--early-agg", action="store_true",
-                   help="issue the bottom aggregation behind the sampler on the sampling stream")
+                   help="aggregate-first: issue the bottom aggregation behind the sampler")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
     p.add_argument("--model", default="gcn", choices=["gcn", "gat"],
                    help="gcn (headline) or gat (GAT_SAMPLE_ALL_GPU-style attention layers)")
@@ -75,14 +90,30 @@ def parse():
                    help="gather from the feature table as given (no 128-byte row pitch copy)")
     p.add_argument("--no-fuse-loss", action="store_true",
                    help="output layer + loss as libtorch ops instead of the fused kernels")
-    p.add_argument("--fuse-linear", action="store_true",
-                   help="bottom layer: aggregation and first GEMM in one kernel")
-    p.add_argument("--cpu-baseline-steps", type=int, default=10)
+    p.add_argument("--epochs", type=int, default=3,
+                   help="full epochs after the timed steps; epoch time = mean of epochs 2..N")
+    p.add_argument("--sampler-batches", type=int, default=32,
+                   help="batches of the GPU sampler-only measurement (0: skip)")
+    p.add_argument("--cpu-max-steps", type=int, default=16,
+                   help="CPU baseline: at most this many batches of one epoch")
+    p.add_argument("--cpu-o0-steps", type=int, default=1,
+                   help="CPU baseline at the reference's -O0 build flags: batches (0: skip)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    p.add_argument("--no-epoch", action="store_true", help="skip the timed full epoch")
+    p.add_argument("--cpu-threads", type=int, default=default_cpu_threads())
     p.add_argument("--scale", type=float, default=1.0)
     return p.parse_args()
+
+
+def metric_name(args, layers) -> str:
+    hops = len(layers) - 1
+    model = {"gcn": "GCN" if args.weight == "sum" else "GraphSAGE", "gat": "GAT"}[args.model]
+    shape = SHAPE_NAMES.get(args.shape, args.shape)
+    return f"sampled-edges/sec + epoch time, {hops}-hop {model} on {shape}-shaped graph @1/2/4/8 GPUs"
+
+
+def lib_sha256() -> str:
+    from nts import _abi
+    return hashlib.sha256(_abi.LIB_PATH.read_bytes()).hexdigest()
 
 
 def main():
@@ -112,15 +143,16 @@ def main():
     V, En = g.n_vertices, g.n_edges
     feat = synthetic.features(V, F_dim, device=dev)
     labels, masks = synthetic.labels_masks(V, C, device=dev)
-    train = torch.nonzero(masks == 0).flatten().to(torch.int32).cpu()
+    train_all = torch.nonzero(masks == 0).flatten().to(torch.int32).cpu()
     # DP: contiguous equal slices (remainder dropped so every rank runs the same
     # number of steps; the reference gives it to the last GPU,
     # toolkits/GCN_SAMPLE_ALL_MULTI.hpp:564-575)
     from nts import dist as ndist
-    train = ndist.shard_nids(train, world, rank)
+    train = ndist.shard_nids(train_all, world, rank)
     log(f"[bench] graph {args.shape}: V={V} E={En} F={F_dim} C={C}  ready in {time.time()-t0:.1f}s")
-    src_host = g.src.cpu().numpy().view(np.uint32) if (rank == 0 and world == 1 and not args.no_cpu_baseline) else None
-    dst_host = g.dst.cpu().numpy().view(np.uint32) if src_host is not None else None
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    src_host = g.src.cpu().numpy().view(np.uint32) if want_cpu else None
+    dst_host = g.dst.cpu().numpy().view(np.uint32) if want_cpu else None
     del g
 
     comm = ndist.make_communicator(E, world, rank, local_rank)
@@ -134,35 +166,47 @@ def main():
                           drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX, weight=args.weight,
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
-                          fuse_linear=args.fuse_linear, early_aggregate=args.early_agg,
+                          transform_first=args.transform_first, early_aggregate=args.early_agg,
                           sampler_priority=not args.no_priority,
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
                           deterministic_backward=not args.atomic_backward,
                           gat=args.model == "gat")
-    fused_linear = (not args.no_fused_gather and args.fuse_linear and not args.no_hip_gemm
-                    and not args.early_agg and layers[1] <= 128)
-    agg_kernel = ("k_agg_gemm" if fused_linear else "k_spmm_gather")
-    if args.model == "gat":
-        agg_kernel = "k_gat_fwd"  # not timed by the driver's bottom-aggregation events
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
+    tf = bool(drv.transform_first)
 
     def step():
         if not drv.sample_not_finished():
             drv.restart()
         drv.train_batch()
 
-    for _ in range(args.warmup):
-        step()
-    drv.synchronize()
-    drv.reset_stats()
-
     def barrier():
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
         torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def sum_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t[0])
+
+    for _ in range(args.warmup):
+        step()
+    drv.synchronize()
+    drv.reset_stats()
 
     barrier()
     t0 = time.perf_counter()
@@ -171,47 +215,54 @@ def main():
     drv.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    agg_ms = drv.resolve_profile()
-    edges = float(drv.batch_edges)
-    agg_bytes = float(drv.agg_bytes)
-    agg_calls = int(drv.agg_calls)
+    prof = drv.resolve_profile()
+    edges_local = float(drv.batch_edges)
     sample_s = float(drv.sample_time)
     train_host_s = float(drv.train_time)
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed, edges], dtype=torch.float64, device=dev)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        elapsed, edges = float(mx[0]), float(t[1])
+    elapsed = max_over_ranks(elapsed)
+    edges = sum_over_ranks(edges_local)
 
-    # sizes of the last timed batch (before the epoch run replaces them)
+    # sizes of the last timed batch (before the epoch runs replace them)
     layer_sizes = [{"v": int(l["v_size"]), "src": int(l["src_size"]), "e": int(l["e_size"])}
                    for l in drv.last_layers]
-    epoch_s = None
-    if not args.no_epoch:
+    # ---- epoch time (mean of epochs 2..N) ----------------------------
+    epoch_times = []
+    for _ in range(max(args.epochs, 0)):
         drv.restart()
         barrier()
         te = time.perf_counter()
         drv.run_epoch()
         drv.synchronize()
         barrier()
-        epoch_s = time.perf_counter() - te
-        drv.resolve_profile()
-        if world > 1:
-            import torch.distributed as dist
-            t = torch.tensor([epoch_s], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            epoch_s = float(t[0])
-
-    value = edges / elapsed
-    agg_avg_ms = agg_ms / max(agg_calls, 1)
-    achieved = (agg_bytes / max(agg_calls, 1)) / (agg_avg_ms * 1e-3) / 1e9 if agg_calls else None
+        epoch_times.append(max_over_ranks(time.perf_counter() - te))
+    drv.resolve_profile()
     n_train_per_gpu = int(train.numel())
     batches_per_epoch = -(-n_train_per_gpu // args.batch)
+    if len(epoch_times) >= 2:
+        epoch_s, epoch_kind = float(np.mean(epoch_times[1:])), (
+            f"measured: mean of epochs 2..{len(epoch_times)} over this rank's training shard")
+    elif epoch_times:
+        epoch_s, epoch_kind = epoch_times[0], "measured: one epoch (the first)"
+    else:
+        epoch_s, epoch_kind = elapsed / args.steps * batches_per_epoch, "ms_per_step x batches/epoch"
 
+    # ---- GPU sampler alone (SURVEY §8d sampler-only rate) -------------------------
+    sampler_only = None
+    if args.sampler_batches > 0 and args.model == "gcn":
+        L = len(fan)
+        csr = [not args.atomic_backward] * (L - 1) + [tf]
+        wt = {"sum": E.WeightType.Sum, "mean": E.WeightType.Mean,
+              "mean-sampled": E.WeightType.MeanSampled}[args.weight]
+        r = E.sampler_throughput(G, train, args.batch, fan, wt, _abi.NTS_RNG_PHILOX,
+                                 args.sampler_batches, csr)
+        sampler_only = {"value": sum_over_ranks(r["edges"]) / max_over_ranks(r["seconds"]),
+                        "unit": "sampled-edges/s", "batches_per_gpu": int(r["batches"]),
+                        "note": "GPU sampler alone on its stream (3 batches in flight), all ranks"}
+
+    value = edges / elapsed
+    rl = roofline(prof, args, layers, world)
     result = {
-        "metric": METRIC,
+        "metric": metric_name(args, layers),
         "value": value,
         "unit": "sampled-edges/s",
         "n_gpus": world,
@@ -224,64 +275,29 @@ def main():
         "dtype": "fp32",
         "data": "synthetic Chung-Lu power-law graph (seed 2024), N(0,1) fp32 features (seed 7), uniform labels",
         "config": {
-            "workload": (f"{'GAT_SAMPLE_ALL_GPU' if args.model == 'gat' else ('GS' if args.weight == 'mean' else 'GCN') + '_SAMPLE_ALLGPU'}-style "
-                         f"{len(layers) - 1}-layer {'GAT' if args.model == 'gat' else ('GraphSAGE (mean)' if args.weight == 'mean' else 'GCN')} "
-                         f"{'-'.join(map(str, layers))}, fanout "
-                         f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic "
-                         f"(V={V}, E={En}); GPU sampler (Philox"
-                         f"{', pipelined' if not args.no_pipeline else ''}) + fused gather/aggregation"
-                         f"{' (issued behind the sampler)' if args.early_agg and not args.no_fused_gather else ''}"
-                         f"{' + layer-1 GEMM' if fused_linear else ''} + "
-                         f"{'torch' if args.no_hip_gemm else 'MFMA'} GEMM + fused Adam"
-                         + (f"; features in pinned host memory, {args.cache_rate:.0%} of rows "
-                            f"(highest degree) cached in HBM" if args.cache_rate >= 0 else "")),
+            "workload": workload_name(args, layers, V, En, tf),
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}",
             "fanout": args.fanout,
-            "epoch_time_s": epoch_s if epoch_s is not None else elapsed / args.steps * batches_per_epoch,
-            "epoch_time_kind": ("measured: one full epoch over this rank's training shard, "
-                                "after the timed steps" if epoch_s is not None
-                                else "ms_per_step x batches/epoch"),
+            "epoch_time_s": epoch_s,
+            "epoch_time_kind": epoch_kind,
+            "epoch_times_s": epoch_times,
             "batches_per_epoch_per_gpu": batches_per_epoch,
-            "sampler_s_per_step": sample_s / args.steps,
+            "gpu_sampler_only": sampler_only,
+            "host_sampler_wait_s_per_step": sample_s / args.steps,
             "host_train_issue_s_per_step": train_host_s / args.steps,
+            "bottom_layer": "transform-first A(X W)" if tf else "aggregate-first (A X) W",
             "layer_sizes_top_down": layer_sizes,
+            "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
+                             "workload": pmc_workload(args, layers, world)},
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": agg_kernel + (" (feature gather + hop-1 aggregation + layer-1 GEMM)" if fused_linear
-                                    else " (fused feature gather + hop-1 aggregation)"),
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": None,
-            "avg_launch_ms": agg_avg_ms,
-            "algorithmic_bytes_per_launch": agg_bytes / max(agg_calls, 1),
-        },
+        "roofline": rl,
     }
-    # HBM traffic of the dominant kernel from the newest committed PMC pass
-    # (profiles/pmc_<tag>.json, FETCH_SIZE x 2 + WRITE_SIZE per launch) — valid for
-    # the default workload only
-    pmcs = sorted((ROOT / "profiles").glob("pmc_*.json"))
-    default_shape = (args.shape == "reddit" and args.batch == 10000 and args.fanout == "25-10"
-                     and layers == [602, 128, 41] and world == 1 and args.cache_rate < 0)
-    if pmcs and default_shape:
-        try:
-            info = json.loads(pmcs[-1].read_text())
-            if info.get("kernel", "").split("<")[0].split("::")[-1] == agg_kernel:
-                tb = float(info["hbm_bytes_per_launch"])
-                result["roofline"]["traffic"] = tb
-                result["roofline"]["traffic_source"] = pmcs[-1].name
-                # actual HBM bytes moved per launch / this run's launch time
-                result["roofline"]["traffic_GBs"] = tb / (agg_avg_ms * 1e-3) / 1e9
-                result["roofline"]["traffic_frac"] = result["roofline"]["traffic_GBs"] / HBM_PEAK_GBS
-        except Exception:
-            pass
-
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(args, G, feat, labels, train, fan, layers,
-                                              src_host, dst_host, V)
+    if want_cpu:
+        result["cpu_baseline"] = cpu_baseline(args, G, feat, labels, train, fan, layers, V)
+        if sampler_only is not None and result["cpu_baseline"].get("sampler_only"):
+            result["config"]["gpu_vs_cpu_sampler_only"] = (
+                sampler_only["value"] / result["cpu_baseline"]["sampler_only"]["value"])
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -289,10 +305,111 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, G, feat, labels, train, fan, layers, src_host, dst_host, V):
-    """The reference CPU path restated (oracle/ref_cpu.cpp, GCN_CPU_SAMPLE.hpp:194-256)
-    timed on this host: sample_fast (OpenMP, thread-local mt19937), get_feature,
-    MiniBatchFuseOp fwd/bwd (CAS backward), libtorch CPU GEMM + Adam."""
+def workload_name(args, layers, V, En, tf) -> str:
+    if args.model == "gat":
+        kind, model = "GAT_SAMPLE_ALL_GPU", "GAT"
+    else:
+        kind = ("GS" if args.weight != "sum" else "GCN") + "_SAMPLE_ALLGPU"
+        model = {"sum": "GCN", "mean": "GraphSAGE (mean, CPU formula)",
+                 "mean-sampled": "GraphSAGE (mean by sampled count, GPU kernel formula)"}[args.weight]
+    s = (f"{kind}-style {len(layers) - 1}-layer {model} {'-'.join(map(str, layers))}, fanout "
+         f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic (V={V}, E={En}); "
+         f"GPU sampler (Philox{', pipelined' if not args.no_pipeline else ''}) + "
+         + ("transform-first bottom layer (row-gathered MFMA GEMM, aggregation + relu/dropout)"
+            if tf else "fused gather/aggregation")
+         + f" + {'torch' if args.no_hip_gemm else 'MFMA fp32'} GEMMs + fused loss + fused Adam")
+    if args.cache_rate >= 0:
+        s += (f"; features in pinned host memory, {args.cache_rate:.0%} of rows (highest degree) "
+              f"cached in HBM")
+    return s
+
+
+def roofline(prof: dict, args, layers, world) -> dict:
+    """Dominant kernel by device time over the timed steps (HIP events on the
+    stream that launches it), its algorithmic units / average launch time vs
+    the MI355X peak; every profiled kernel listed under `kernels`."""
+    kernels = {}
+    for name, st in prof.items():
+        if not st["calls"]:
+            continue
+        avg_s = st["ms"] / st["calls"] * 1e-3
+        gemm = name.startswith("gather_gemm")
+        per = st["units"] / st["calls"]
+        ach = per / avg_s / (1e12 if gemm else 1e9)
+        peak = FP32_MFMA_PEAK_TF if gemm else HBM_PEAK_GBS
+        kernels[name] = {
+            "bound": "mfma" if gemm else "hbm", "unit": "TFLOP/s" if gemm else "GB/s",
+            "achieved": ach, "peak": peak, "frac": ach / peak, "avg_launch_ms": avg_s * 1e3,
+            ("flops_per_launch" if gemm else "algorithmic_bytes_per_launch"): per,
+            "calls": st["calls"], "share_of_timed_ms": st["ms"]}
+    if not kernels:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": None, "traffic": None}
+    dom = max(kernels, key=lambda k: kernels[k]["share_of_timed_ms"])
+    k = kernels[dom]
+    rl = {"bound": k["bound"], "kernel": dom, "achieved": k["achieved"], "peak": k["peak"],
+          "unit": k["unit"], "frac": k["frac"], "traffic": None,
+          "avg_launch_ms": k["avg_launch_ms"], "kernels": kernels}
+    attach_pmc(rl, dom, args, layers, world)
+    return rl
+
+
+def pmc_workload(args, layers, world) -> str:
+    return (f"{args.shape}/{args.batch}/{args.fanout}/{'-'.join(map(str, layers))}/{args.weight}/"
+            f"w{world}/tf{args.transform_first}/{args.model}/c{args.cache_rate}")
+
+
+def attach_pmc(rl, dom, args, layers, world):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass
+    (profiles/pmc_*.json) — only if it was taken on this exact libnts_hip.so
+    build, this kernel and this workload; otherwise traffic stays null and
+    the reason is stated."""
+    wl = pmc_workload(args, layers, world)
+    sha = lib_sha256()
+    why = "no PMC pass recorded for this build/kernel/workload"
+    for f in sorted((ROOT / "profiles").glob("pmc_*.json"), reverse=True):
+        try:
+            info = json.loads(f.read_text())
+        except Exception:
+            continue
+        if info.get("profiler_kernel") != dom or info.get("workload") != wl:
+            continue
+        if info.get("lib_sha256") != sha:
+            why = f"{f.name} was taken on another libnts_hip.so build: not attached"
+            continue
+        for kname, kv in info.get("kernels", {}).items():
+            if kv.get("profiler_kernel") == dom and kv.get("hbm_bytes_per_launch"):
+                tb = float(kv["hbm_bytes_per_launch"])
+                rl["traffic"] = tb
+                rl["traffic_source"] = f"{f.name} ({kname})"
+                rl["traffic_GBs"] = tb / (rl["avg_launch_ms"] * 1e-3) / 1e9
+                rl["traffic_frac_of_hbm_peak"] = rl["traffic_GBs"] / HBM_PEAK_GBS
+                return
+    rl["traffic_note"] = why
+
+
+def cpu_info() -> dict:
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+
+
+def cpu_baseline(args, G, feat, labels, train, fan, layers, V):
+    """The reference CPU path restated (oracle/ref_cpu.cpp; toolkits/GCN_CPU_SAMPLE.hpp:194-256)
+    timed on this host over one epoch of the same workload (at most
+    --cpu-max-steps batches): sample_fast (OpenMP, thread-local mt19937),
+    get_feature, MiniBatchFuseOp fwd/bwd (CAS backward), libtorch CPU GEMM and
+    learnC2C_with_decay_Adam (core/NtsScheduler.hpp:863-880)."""
     from oracle import oracle as orc
     threads = max(1, args.cpu_threads)
     torch.set_num_threads(threads)
@@ -302,48 +419,90 @@ def cpu_baseline(args, G, feat, labels, train, fan, layers, src_host, dst_host, 
     out_d = G.out_degree.cpu().numpy().view(np.uint32)
     feat_h = feat.cpu().numpy()
     lab_h = labels.cpu()
-    s = orc.Sampler(col, rows, in_d, out_d, fan, seed=2000, rng_mode=orc.RNG_MT_LEMIRE,
-                    order_mode=orc.ORDER_UNORDERED_MAP)
-    gen = torch.Generator().manual_seed(0)
-    W = [torch.empty(a, b).uniform_(-(6 / (a + b)) ** 0.5, (6 / (a + b)) ** 0.5, generator=gen).requires_grad_()
-         for a, b in zip(layers[:-1], layers[1:])]
-    M = [torch.zeros_like(w) for w in W]
-    Vv = [torch.zeros_like(w) for w in W]
     ids = train.numpy().astype(np.uint32)
-    total_edges, total_t = 0, 0.0
-    for it in range(max(1, args.cpu_baseline_steps)):
-        seeds = ids[it * args.batch:(it + 1) * args.batch]
-        t0 = time.perf_counter()
-        l0, l1 = s.sample(seeds, it, orc.W_SUM, True, threads)
-        X0 = orc.get_feature(l1["source"], feat_h, threads)
-        Y0 = torch.from_numpy(orc.fuse_fwd(l1, X0, out_d, in_d, threads=threads))
-        X1 = torch.dropout(torch.relu(Y0 @ W[0]), 0.5, True)
-        Y1 = torch.from_numpy(orc.fuse_fwd(l0, X1.detach().numpy(), out_d, in_d, threads=threads))
-        Y1.requires_grad_()
-        X2 = Y1 @ W[1]
-        tgt = lab_h[torch.from_numpy(l0["destination"].astype(np.int64))]
-        loss = torch.nn.functional.nll_loss(X2.log_softmax(1), tgt)
-        loss.backward()
-        gX1 = orc.fuse_bwd(l0, Y1.grad.numpy(), out_d, in_d, threads=threads)
-        X1.backward(torch.from_numpy(gX1))
-        with torch.no_grad():  # learnC2C_with_decay_Adam
-            for i, w in enumerate(W):
-                wg = w.grad + 1e-4 * w
-                M[i] = 0.9 * M[i] + 0.1 * wg
-                Vv[i] = 0.999 * Vv[i] + 0.001 * wg * wg
-                w -= 0.001 * (M[i] / 0.1) / (torch.sqrt(Vv[i] / 0.001) + 1e-9)
-                w.grad = None
-        total_t += time.perf_counter() - t0
-        total_edges += l0["e_size"] + l1["e_size"]
-    return {
-        "value": total_edges / total_t,
+    n_batches = -(-ids.size // args.batch)
+    L = len(fan)
+    wmean = args.weight != "sum"
+    wt = {"sum": orc.W_SUM, "mean": orc.W_MEAN, "mean-sampled": orc.W_MEAN_SAMPLED}[args.weight]
+
+    def run(steps, variant):
+        with orc.variant(variant):
+            s = orc.Sampler(col, rows, in_d, out_d, fan, seed=2000, rng_mode=orc.RNG_MT_LEMIRE,
+                            order_mode=orc.ORDER_UNORDERED_MAP)
+            gen = torch.Generator().manual_seed(0)
+            W = [torch.empty(a, b).uniform_(-(6 / (a + b)) ** 0.5, (6 / (a + b)) ** 0.5,
+                                            generator=gen).requires_grad_()
+                 for a, b in zip(layers[:-1], layers[1:])]
+            M = [torch.zeros_like(w) for w in W]
+            Vv = [torch.zeros_like(w) for w in W]
+            b1, b2, lr, wd, eps = 0.9, 0.999, 0.001, 1e-4, 1e-9
+            b1t, b2t = b1, b2  # Parameter::beta1_t/beta2_t, advanced by next()
+            edges, t_all, t_samp = 0, 0.0, 0.0
+            for it in range(steps):
+                seeds = ids[it * args.batch:(it + 1) * args.batch]
+                t0 = time.perf_counter()
+                ls = s.sample(seeds, it, wt, True, threads)
+                t1 = time.perf_counter()
+                # GCN_CPU_SAMPLE forward: hop = L-1-l, features of the outermost source
+                X = torch.from_numpy(orc.get_feature(ls[-1]["source"], feat_h, threads))
+                Ys = []
+                for l in range(L):
+                    lay = ls[L - 1 - l]
+                    Y = torch.from_numpy(orc.fuse_fwd(lay, X.detach().numpy(), out_d, in_d,
+                                                      weight_mean=wmean, threads=threads))
+                    if l > 0:
+                        Y.requires_grad_()
+                    Ys.append((Y, X))
+                    Z = Y @ W[l]
+                    X = torch.dropout(torch.relu(Z), 0.5, True) if l < L - 1 else Z
+                tgt = lab_h[torch.from_numpy(ls[0]["destination"].astype(np.int64))]
+                loss = torch.nn.functional.nll_loss(X.log_softmax(1), tgt)
+                loss.backward()
+                for l in range(L - 1, 0, -1):  # graph-op backward (not the bottom one)
+                    Y, Xin = Ys[l]
+                    gX = orc.fuse_bwd(ls[L - 1 - l], Y.grad.numpy(), out_d, in_d,
+                                      weight_mean=wmean, threads=threads)
+                    Xin.backward(torch.from_numpy(gX))
+                with torch.no_grad():  # learnC2C_with_decay_Adam, bias-corrected
+                    for i, w in enumerate(W):
+                        wg = w.grad + wd * w
+                        M[i] = b1 * M[i] + (1 - b1) * wg
+                        Vv[i] = b2 * Vv[i] + (1 - b2) * wg * wg
+                        w -= lr * (M[i] / (1 - b1t)) / (torch.sqrt(Vv[i] / (1 - b2t)) + eps)
+                        w.grad = None
+                    b1t, b2t = b1t * b1, b2t * b2
+                t2 = time.perf_counter()
+                t_samp += t1 - t0
+                t_all += t2 - t0
+                edges += sum(l["e_size"] for l in ls)
+            return edges, t_all, t_samp
+
+    steps = max(1, min(args.cpu_max_steps, n_batches))
+    edges, t_all, t_samp = run(steps, "O3")
+    out = {
+        "value": edges / t_all,
         "unit": "sampled-edges/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"{max(1, args.cpu_baseline_steps)} GCN_CPU_SAMPLE training step(s) of batch "
-                   f"{args.batch} on the same graph ({total_edges} sampled edges, {total_t:.1f}s), "
-                   f"OpenMP {threads} threads, oracle/ref_cpu.cpp -O3 x86-64-v3 + torch CPU"),
+        "sample": (f"{steps} of the {n_batches} GCN_CPU_SAMPLE training steps of one epoch, batch "
+                   f"{args.batch}, same graph ({edges} sampled edges, {t_all:.1f}s), OpenMP "
+                   f"{threads} threads, oracle/ref_cpu.cpp -O3 x86-64-v3 + torch CPU"),
+        "sampler_only": {"value": edges / t_samp, "unit": "sampled-edges/s",
+                         "note": "sample_fast alone (OpenMP, thread-local mt19937)"},
+        "epoch_time_s": t_all / steps * n_batches,
+        "epoch_time_kind": ("measured: one full epoch" if steps == n_batches
+                            else f"estimate: per-step time of {steps} steps x {n_batches} batches"),
+        "threads_rule": "min(nproc - 1 (reference default), this job's CPU share)",
+        **cpu_info(),
     }
+    if args.cpu_o0_steps > 0:
+        e0, t0_all, t0_s = run(min(args.cpu_o0_steps, n_batches), "O0")
+        out["O0_build"] = {"value": e0 / t0_all, "sampler_only": e0 / t0_s,
+                           "unit": "sampled-edges/s",
+                           "note": (f"{min(args.cpu_o0_steps, n_batches)} step(s) with ref_cpu.cpp "
+                                    f"built -O0 like the reference's shipped build "
+                                    f"(CMakeLists.txt:109); torch CPU ops unchanged")}
+    return out
 
 
 if __name__ == "__main__":

@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 2  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id */
+#define NTS_HIP_ABI_VERSION 3  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+                                  3: transform-first entry points, fused agg+GEMM removed */
 
 /* status codes */
 #define NTS_OK 0
@@ -64,8 +65,14 @@ extern "C" {
  * (core/ntsFastSampler.hpp:27) with the CPU sampler's formulas
  * (core/ntsFastSampler.hpp:1111-1119, nts_norm_degree core/ntsBaseOp.hpp:652-657). */
 #define NTS_WEIGHT_SUM 0
-#define NTS_WEIGHT_MEAN 1
+#define NTS_WEIGHT_MEAN 1  /* CPU sampler: norm / in_degree(dst) of the full graph (:1111-1113) */
 #define NTS_WEIGHT_NONE 2
+/* The reference GPU kernel get_mean_weight (cuda/ntsCUDATransferKernel.cuh:319-342):
+ * norm / (sampled edge count of the dst).  Note the reference's GPU toolkits never
+ * reach it: sample_gpu_fast(int, int, WeightType) drops the weight type
+ * (core/ntsFastSampler.hpp:944-948), so GS_SAMPLE_ALLGPU
+ * actually trains with SUM weights.  Offered for the kernel's semantics. */
+#define NTS_WEIGHT_MEAN_SAMPLED 3
 /* OR-ed into SUM / MEAN: UP_DEGREE — the degrees in the weights are the
  * sampled layer's own (in = sampled edges of the dst, out = sampled edges of
  * the src), SampledSubgraph::update_degrees(_GPU) (core/FullyRepGraph.hpp:189-217,
@@ -246,23 +253,6 @@ int nts_hip_spmm_csc_fwd_cached(nts_hip_ctx *ctx, const uint32_t *column_offset,
                                 const float *spill, uint64_t ld_spill, int host_local,
                                 const uint32_t *x_row_map, uint32_t feature_size, float *y,
                                 uint64_t ldy);
-/* Fused bottom layer (SingleGPUAllSampleGraphOp::forward on the feature table
- * followed by Parameter::forward and vertexForward's activation):
- *   Y = A X  (rows of x gathered through x_row_map, bit-identical to
- *             nts_hip_spmm_csc_fwd; written to y when y != NULL),
- *   Z = Y W  (W [feature_size x out_size] row-major, MFMA fp32),
- *   activation != 0: z = dropout(relu(Z), p) with the Philox mask of
- *   nts_hip_gemm_relu_dropout_f32 (same seed/offset/(row, col) keys),
- *   activation == 0: z = Z.
- * out_size <= 128, feature_size <= 608.  The GEMM runs under the HBM-bound
- * gather of the aggregation (two tiles per CU in alternating phases). */
-int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx *ctx, const uint32_t *column_offset,
-                                const uint32_t *row_indices, const float *weight,
-                                const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
-                                const uint32_t *x_row_map, uint32_t feature_size, const float *W,
-                                uint32_t out_size, float *y, uint64_t ldy, float *z,
-                                uint64_t ldz, int activation, float p, uint64_t seed,
-                                uint64_t offset);
 /* G_in[s,:] = sum_{j in [ro[s],ro[s+1])} w_b[j] * G_out[ci[j],:] (ascending dst
  * order, deterministic, atomic-free).  Replaces Gather_By_Src_From_Dst_Spmm
  * (cuda/ntsCUDAGraphOP.cu:901-1042) and MiniBatchFuseOp::backward
@@ -272,6 +262,29 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx *ctx, const uint32_t *row_offset,
                          const uint32_t *s, uint32_t s_cap, const float *g_out,
                          uint64_t ld_gout, uint32_t feature_size, float *g_in,
                          uint64_t ld_gin);
+/* Transform-first bottom layer: when the layer narrows the rows
+ * (F_in > F_out), A (X W) replaces (A X) W — the reference aggregates first
+ * (SingleGPUAllSampleGraphOp::forward then Parameter::forward,
+ * toolkits/GCN_SAMPLE_GPU.hpp:252-266); both are linear, so they agree up to
+ * fp32 summation order.  The aggregation then runs over F_out-wide rows and
+ * vertexForward's activation moves into its epilogue:
+ *   y = dropout(relu(A x), p) with the Philox keep bits of
+ *   nts_hip_gemm_relu_dropout_f32 (same seed/offset/(row, col) keys, so both
+ *   orders drop the same elements); p == 0: relu only.  A, weights, v as in
+ *   nts_hip_spmm_csc_fwd (no row map). */
+int nts_hip_spmm_csc_fwd_act(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                             const uint32_t *row_indices, const float *weight, const uint32_t *v,
+                             uint32_t v_cap, const float *x, uint64_t ldx, uint32_t feature_size,
+                             float *y, uint64_t ldy, float p, uint64_t seed, uint64_t offset);
+/* Its backward through the CSR, the activation's backward fused into the loads:
+ *   G_in[s,:] = sum_j w_b[j] * (G_out[ci[j],:] ⊙ [X_act[ci[j],:] > 0] * scale)
+ * (X_act = the forward output of nts_hip_spmm_csc_fwd_act, scale = 1/(1-p));
+ * ascending dst order, deterministic. */
+int nts_hip_spmm_csr_bwd_masked(nts_hip_ctx *ctx, const uint32_t *row_offset,
+                                const uint32_t *column_indices, const float *weight_backward,
+                                const uint32_t *s, uint32_t s_cap, const float *g_out,
+                                uint64_t ld_gout, const float *x_act, uint64_t ld_act, float scale,
+                                uint32_t feature_size, float *g_in, uint64_t ld_gin);
 /* G_in[row_indices[e],:] += w[e] * G_out[d,:] with float atomics over the CSC
  * (g_in must be zeroed by the caller; summation order is not deterministic).
  * Replaces Push_From_Dst_To_Src_Spmm (cuda/ntsCUDAGraphOP.cu:621-770). */
@@ -321,6 +334,20 @@ int nts_hip_gat_backward(nts_hip_ctx *ctx, const uint32_t *column_offset,
  * (deterministic).  May grow the context's scratch arena. */
 int nts_hip_gemm_f32(nts_hip_ctx *ctx, int trans_a, int M, int N, int K, const float *A,
                      uint64_t lda, const float *B, uint64_t ldb, float *C, uint64_t ldc);
+
+/* Row-gathered forms for the transform-first bottom layer (A = the feature
+ * table, a_rows = the layer's `source`, so the gathered rows never land in HBM
+ * — the fused load_feature_gpu of core/ntsFastSampler.hpp:244-261):
+ *   nts_hip_gemm_gather_f32:    C[i,:] = A[a_rows[i],:] B        (i < M; A rows of K floats)
+ *   nts_hip_gemm_tn_gather_f32: C[M,N] = A[a_rows[0..K),:]^T B[K,N] (A rows of M floats)
+ * Same kernels and summation order as nts_hip_gemm_f32 on the gathered matrix
+ * (bit-identical to it). */
+int nts_hip_gemm_gather_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *A, uint64_t lda,
+                            const uint32_t *a_rows, const float *B, uint64_t ldb, float *C,
+                            uint64_t ldc);
+int nts_hip_gemm_tn_gather_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *A,
+                               uint64_t lda, const uint32_t *a_rows, const float *B, uint64_t ldb,
+                               float *C, uint64_t ldc);
 
 /* Hidden-layer forward with its activation fused into the GEMM epilogue:
  *   C = dropout(relu(A B), p)   — vertexForward's

@@ -14,26 +14,49 @@ import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
 LIB = HERE / "build" / "liboracle.so"
+# build variants: "O3" (-O3 x86-64-v3, the checker and the CPU baseline) and
+# "O0" (the reference's shipped -O0 flags, a secondary baseline figure)
+LIBS = {"O3": LIB, "O0": HERE / "build" / "liboracle_O0.so"}
 
 RNG_PHILOX, RNG_MT_LEMIRE, RNG_MT_DIV = 0, 1, 2
 ORDER_DRAW, ORDER_UNORDERED_MAP = 0, 1
-W_SUM, W_MEAN, W_NONE = 0, 1, 2
+W_SUM, W_MEAN, W_NONE, W_MEAN_SAMPLED = 0, 1, 2, 3
 W_UP_DEGREE = 0x10  # OR-ed into the weight type: UP_DEGREE per-layer degrees
 F_MERGE_SRC_DST = 0x20  # OR-ed: dsts merged into the frontier (GAT), dst_local_id
 
-_lib = None
+_libs = {}
+_active = "O3"
 
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
 
 
+class variant:
+    """`with oracle.variant("O0"):` — calls (and Samplers created) inside use
+    that build of ref_cpu.cpp."""
+
+    def __init__(self, name: str):
+        if name not in LIBS:
+            raise ValueError(name)
+        self.name = name
+
+    def __enter__(self):
+        global _active
+        self.prev, _active = _active, self.name
+        return self
+
+    def __exit__(self, *exc):
+        global _active
+        _active = self.prev
+
+
 def lib():
-    global _lib
-    if _lib is None:
-        if not LIB.exists():
+    if _active not in _libs:
+        path = LIBS[_active]
+        if not path.exists():
             build()
-        L = C.CDLL(str(LIB))
+        L = C.CDLL(str(path))
         P, U32, U64, I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
         L.orc_build_csc.argtypes = [U64, U64, P, P, P, P]
         L.orc_degrees.argtypes = [U64, U64, P, P, P, P]
@@ -48,8 +71,8 @@ def lib():
         L.orc_get_feature.argtypes = [U32, P, P, U32, P, I]
         L.orc_fuse_fwd.argtypes = [U32, P, P, P, P, P, P, P, U32, P, I, I]
         L.orc_fuse_bwd.argtypes = [U32, U32, P, P, P, P, P, P, P, U32, P, I, I]
-        _lib = L
-    return _lib
+        _libs[_active] = L
+    return _libs[_active]
 
 
 def _p(a):
@@ -86,24 +109,25 @@ class Sampler:
         self.fanout = np.ascontiguousarray(fanout, np.int32)
         self.L = len(fanout)
         V = self.col.size - 1
-        self.h = lib().orc_sampler_new(V, _p(self.col), _p(self.rows), _p(self.in_deg),
+        self.L_ = lib()
+        self.h = self.L_.orc_sampler_new(V, _p(self.col), _p(self.rows), _p(self.in_deg),
                                        _p(self.out_deg), self.L, _p(self.fanout), seed, rng_mode,
                                        order_mode)
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_sampler_free(self.h)
+            self.L_.orc_sampler_free(self.h)
             self.h = None
 
     def sample(self, seeds, batch_seq=0, weight_type=W_SUM, build_csr=True, threads=1):
         seeds = np.ascontiguousarray(seeds, np.uint32)
-        lib().orc_sample_batch(self.h, _p(seeds), seeds.size, batch_seq, weight_type,
+        self.L_.orc_sample_batch(self.h, _p(seeds), seeds.size, batch_seq, weight_type,
                                int(build_csr), threads)
         return [self.layer(l) for l in range(self.L)]
 
     def layer(self, l):
         sz = np.empty(3, np.uint32)
-        lib().orc_layer_size(self.h, l, _p(sz))
+        self.L_.orc_layer_size(self.h, l, _p(sz))
         v, e, s = (int(x) for x in sz)
         out = dict(
             destination=np.empty(v, np.uint32), column_offset=np.empty(v + 1, np.uint32),
@@ -111,12 +135,12 @@ class Sampler:
             source=np.empty(s, np.uint32), edge_weight_forward=np.zeros(e, np.float32),
             row_offset=np.zeros(s + 1, np.uint32), column_indices=np.zeros(e, np.uint32),
             edge_weight_backward=np.zeros(e, np.float32))
-        lib().orc_layer_copy(self.h, l, *[_p(out[k]) for k in (
+        self.L_.orc_layer_copy(self.h, l, *[_p(out[k]) for k in (
             "destination", "column_offset", "row_indices", "sample_ans", "source",
             "edge_weight_forward", "row_offset", "column_indices", "edge_weight_backward")])
         out.update(v_size=v, e_size=e, src_size=s)
         dl, ce = np.zeros(v, np.uint32), np.zeros(e, np.uint32)
-        have = lib().orc_layer_extra(self.h, l, _p(dl), _p(ce))
+        have = self.L_.orc_layer_extra(self.h, l, _p(dl), _p(ce))
         if have & 1:
             out["dst_local_id"] = dl
         if have & 2:
@@ -125,7 +149,7 @@ class Sampler:
 
     def mt_state(self):
         st = np.empty(625, np.uint32)
-        lib().orc_mt_state(self.h, _p(st))
+        self.L_.orc_mt_state(self.h, _p(st))
         return st
 
 

@@ -102,7 +102,12 @@ struct Layer {
 
 enum { RNG_PHILOX = 0, RNG_MT_LEMIRE = 1, RNG_MT_DIV = 2 };
 enum { ORDER_DRAW = 0, ORDER_UNORDERED_MAP = 1 };
-enum { W_SUM = 0, W_MEAN = 1, W_NONE = 2, W_UP_DEGREE = 0x10, F_MERGE_SRC_DST = 0x20 };
+// W_MEAN_SAMPLED: the reference GPU kernel get_mean_weight
+// (cuda/ntsCUDATransferKernel.cuh:319-342): norm / (sampled edges of the dst).
+// Its GPU toolkits never reach it (sample_gpu_fast drops the weight type,
+// core/ntsFastSampler.hpp:944-948).
+enum { W_SUM = 0, W_MEAN = 1, W_NONE = 2, W_MEAN_SAMPLED = 3, W_UP_DEGREE = 0x10,
+       F_MERGE_SRC_DST = 0x20 };
 
 struct Sampler {
   uint64_t V;
@@ -282,6 +287,12 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
     const uint32_t src_size = (uint32_t)ly.source.size();
     ly.src_size = src_size;
     ly.dst_local_id.clear();
+    // dst_local_id[k] = src_index[destination[k]] — indexed by the dst k.  The
+    // reference writes dst_local_id[id] = src_index_array[dst()[i]] with i the
+    // LAYER (core/ntsFastSampler.hpp:1096), which stores
+    // the local id of the i-th dst for every dst; this restatement (and the
+    // product) follows the evident intent (set_dst_local_index,
+    // cuda/ntsCUDAGraphOP.cu:1696) instead of replicating that defect.
     if (merge) {
       ly.dst_local_id.resize(v);
       for (uint32_t k = 0; k < v; ++k) ly.dst_local_id[k] = s.src_index[ly.destination[k]];
@@ -323,6 +334,8 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
       const uint32_t id = up_degree ? up_in[dst_l] : s.indeg[ly.destination[dst_l]];
       float w = norm_degree(od, id);
       if (weight_type == W_MEAN) w = w / id;
+      if (weight_type == W_MEAN_SAMPLED)
+        w = w / (float)(ly.column_offset[dst_l + 1] - ly.column_offset[dst_l]);
       return w;
     };
     if (weight_type != W_NONE) {

@@ -4,20 +4,41 @@
   python profiles/summarize.py <gpurun_out/prof_TAG> <TAG>
 
 Writes profiles/<TAG>_kernel_stats.csv (rocprofv3 --stats, as produced),
-profiles/<TAG>_summary.md (top kernels, per-step breakdown, PMC traffic of the
-fused aggregation) and profiles/pmc_<TAG>.json (HBM bytes per launch of the
-dominant kernel: FETCH_SIZE x 2 (gfx950 counts 128-B requests at 64 B,
-MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB per dispatch).
+profiles/<TAG>_summary.md (top kernels, the bench line's live HIP-event
+averages next to the trace's, PMC traffic) and profiles/pmc_<TAG>.json: per
+profiled kernel the HBM bytes per launch = FETCH_SIZE x 2 (gfx950 tallies
+128-B requests at 64 B, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (both KiB per
+dispatch), tagged with the libnts_hip.so sha256 and the workload the bench
+line reports, so bench.py attaches it only to the same build and workload.
 """
 import csv
 import json
 import pathlib
+import re
 import shutil
 import statistics
 import sys
 
-# dominant kernel: the aggregation kernel with the largest total time
-PREFIXES = ("k_spmm_gather_linear<", "k_spmm_gather<")
+# bench profiler kernel -> how its HIP kernel reads in a rocprofv3 trace
+def profiler_kernel(name: str):
+    m = re.search(r"nts_hip::(\w+)<([^>]*)>", name)
+    if not m:
+        return None
+    k, targs = m.group(1), [a.strip() for a in m.group(2).split(",")]
+    if k == "k_spmm_gather":
+        mode = targs[6] if len(targs) > 6 else "0"
+        if mode == "1":
+            return "bottom_aggregation"          # transform-first: A H + relu/dropout
+        if mode == "2":
+            return "bottom_backward"             # A^T (dX ⊙ mask)
+        if targs[3] == "true" and targs[5] == "false":
+            return "bottom_aggregation"          # aggregate-first: fused gather A X
+        return None
+    if k == "k_gemm_wres" and targs[2] == "false":
+        return "gather_gemm"                     # X[src] W0 (no epilogue)
+    if k == "k_gemm_tn_big" and targs[0] == "false":
+        return "gather_gemm_tn"                  # X[src]^T dH (no mask)
+    return None
 
 
 def load(path):
@@ -25,13 +46,11 @@ def load(path):
         return list(csv.DictReader(f))
 
 
-def pmc_per_kernel(rows, counter):
-    out = {}
-    for r in rows:
-        if r.get("Counter_Name") != counter:
-            continue
-        out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
-    return out
+def bench_line(log):
+    for line in reversed(pathlib.Path(log).read_text().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
 
 
 def main():
@@ -42,45 +61,61 @@ def main():
     shutil.copy(stats, dst / f"{tag}_kernel_stats.csv")
     rows = load(stats)
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    bl = bench_line(src / "trace.log")
+    meta = (bl or {}).get("config", {}).get("profile_meta", {})
     lines = [f"# rocprofv3 summary — {tag}", "",
-             "Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 "
-             "--no-cpu-baseline` (Reddit-shaped GCN 602-128-41, fanout 25-10, batch 10,000; the "
-             "trace includes graph generation / CSC build before the timed steps).", "",
+             f"Command: `rocprofv3 --kernel-trace --stats -- python3 bench.py {meta.get('argv', '')}` "
+             f"(the trace includes graph generation / CSC build before the timed steps).", "",
              "| kernel | calls | total ms | avg us | % |", "|---|---|---|---|---|"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:25]:
-        lines.append(f"| `{r['Name'][:80]}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | "
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | "
                      f"{float(r['AverageNs'])/1e3:.1f} | {100*float(r['TotalDurationNs'])/tot:.1f} |")
-    dom = sorted((r for r in rows if any(pfx in r["Name"] for pfx in PREFIXES)),
-                 key=lambda r: -float(r["TotalDurationNs"]))
-    info = {}
-    DOMINANT = dom[0]["Name"] if dom else "k_spmm_gather<"
-    info["kernel"] = DOMINANT
-    if dom:
-        info["avg_ns"] = float(dom[0]["AverageNs"])
-        info["calls"] = int(dom[0]["Calls"])
-    for kind, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"),
-                          ("hit", "TCC_HIT_sum"), ("hit", "TCC_MISS_sum")):
+    info = {"workload": meta.get("workload"), "lib_sha256": meta.get("lib_sha256"),
+            "profiler_kernel": (bl or {}).get("roofline", {}).get("kernel"), "kernels": {}}
+    live = (bl or {}).get("roofline", {}).get("kernels", {})
+    for r in rows:
+        pk = profiler_kernel(r["Name"])
+        if pk is None:
+            continue
+        cur = info["kernels"].get(r["Name"])
+        info["kernels"][r["Name"]] = {"profiler_kernel": pk, "avg_ns": float(r["AverageNs"]),
+                                      "calls": int(r["Calls"])}
+    counters = (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"), ("hit", "TCC_HIT_sum"),
+                ("hit", "TCC_MISS_sum"))
+    for kind, counter in counters:
         p = list(src.glob(f"{kind}/**/run_counter_collection.csv"))
         if not p:
             continue
-        per = pmc_per_kernel(load(p[0]), counter)
-        for name, vals in per.items():
-            if name.split("(")[0].strip() == DOMINANT.split("(")[0].strip():
-                info[counter] = statistics.median(vals)  # KiB per dispatch
-    if "FETCH_SIZE" in info and "WRITE_SIZE" in info:
-        info["hbm_bytes_per_launch"] = (2 * info["FETCH_SIZE"] + info["WRITE_SIZE"]) * 1024.0
-        lines += ["", f"## PMC traffic of `{DOMINANT}`", "",
-                  f"- FETCH_SIZE median {info['FETCH_SIZE']:.0f} KiB/dispatch (x2 gfx950 correction)",
-                  f"- WRITE_SIZE median {info['WRITE_SIZE']:.0f} KiB/dispatch",
-                  f"- HBM bytes per launch: {info['hbm_bytes_per_launch']/1e9:.3f} GB"]
-        if "avg_ns" in info:
-            lines.append(f"- at the traced average duration {info['avg_ns']/1e3:.1f} us: "
-                         f"{info['hbm_bytes_per_launch']/info['avg_ns']:.0f} GB/s of HBM traffic")
-    if "TCC_HIT_sum" in info and "TCC_MISS_sum" in info:
-        h, m = info["TCC_HIT_sum"], info["TCC_MISS_sum"]
-        info["l2_hit_rate"] = h / max(h + m, 1.0)
-        lines.append(f"- L2 hit rate TCC_HIT/(HIT+MISS): {info['l2_hit_rate']:.3f} "
-                     f"({h:.3g} hits, {m:.3g} misses per dispatch)")
+        per = {}
+        for r in load(p[0]):
+            if r.get("Counter_Name") == counter:
+                per.setdefault(r["Kernel_Name"].split("(")[0].strip(), []).append(float(r["Counter_Value"]))
+        for name, kv in info["kernels"].items():
+            vals = per.get(name.split("(")[0].strip())
+            if vals:
+                kv[counter] = statistics.median(vals)  # KiB per dispatch (median over launches)
+    lines += ["", "## Profiled kernels (bench `roofline.kernels`, live HIP events) vs the trace", "",
+              "| bench kernel | HIP kernel | live avg us | trace avg us | HBM GB/launch (PMC) | L2 hit |",
+              "|---|---|---|---|---|---|"]
+    for name, kv in info["kernels"].items():
+        if "FETCH_SIZE" in kv and "WRITE_SIZE" in kv:
+            kv["hbm_bytes_per_launch"] = (2 * kv["FETCH_SIZE"] + kv["WRITE_SIZE"]) * 1024.0
+        if "TCC_HIT_sum" in kv and "TCC_MISS_sum" in kv:
+            kv["l2_hit_rate"] = kv["TCC_HIT_sum"] / max(kv["TCC_HIT_sum"] + kv["TCC_MISS_sum"], 1.0)
+        lk = live.get(kv["profiler_kernel"], {})
+        alg = lk.get("algorithmic_bytes_per_launch")
+        if alg and "hbm_bytes_per_launch" in kv:
+            kv["traffic_over_algorithmic"] = kv["hbm_bytes_per_launch"] / alg
+        lines.append(
+            f"| {kv['profiler_kernel']} | `{name.split('(')[0][:70]}` | "
+            f"{lk.get('avg_launch_ms', float('nan')) * 1e3:.1f} | {kv['avg_ns'] / 1e3:.1f} | "
+            f"{kv.get('hbm_bytes_per_launch', float('nan')) / 1e9:.3f} | "
+            f"{kv.get('l2_hit_rate', float('nan')):.3f} |")
+        if "traffic_over_algorithmic" in kv:
+            lines.append(f"|  | counter / algorithmic bytes: {kv['traffic_over_algorithmic']:.2f} | | | | |")
+    if bl:
+        lines += ["", f"Bench line of the traced run: value {bl['value']:.4g} {bl['unit']}, "
+                      f"{bl['ms_per_step']:.3f} ms/step (profiled: slower than un-profiled)."]
     (dst / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
     (dst / f"pmc_{tag}.json").write_text(json.dumps(info, indent=1) + "\n")
     print("\n".join(lines))

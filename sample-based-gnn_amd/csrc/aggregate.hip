@@ -66,7 +66,6 @@ struct VT<4> {
 };
 
 constexpr int kAggThreads = 256;
-constexpr int kUnroll = 4;
 
 // y[d, :] = sum_{e in [off[d], off[d+1])} w[e] * x[row(e), :]
 // row(e) = MAP ? map[idx[e]] : idx[e];  w == nullptr -> weight 1.
@@ -93,14 +92,36 @@ struct Tier {
 constexpr uint32_t kNotCached = 0xFFFFFFFFu;
 constexpr uint32_t kHostBit = 0x80000000u;
 
-template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER>
+// MODE: what the gather computes around the weighted sum (MAP/TIER only with kAggPlain)
+//   kAggPlain: y = A x
+//   kAggAct:   y = dropout(relu(A x), p) — vertexForward's activation in the
+//              epilogue, keep bits keyed exactly like the GEMM epilogue of
+//              nts_hip_gemm_relu_dropout_f32 (dropout_words(row, col, seed, offset))
+//   kAggMask:  y = A (x ⊙ [mx > 0] · scale) — that activation's backward fused
+//              into the row loads (mx = the forward activation, same shape as x)
+enum { kAggPlain = 0, kAggAct = 1, kAggMask = 2 };
+struct AggExtra {
+  const float* mx = nullptr;
+  uint64_t ldm = 0;
+  float scale = 1.f;
+  uint32_t keep_threshold = 0;
+  uint64_t seed = 0, offset = 0;
+};
+
+template <int VEC>
+__device__ __forceinline__ float& vcomp(typename VT<VEC>::T& v, int q) {
+  return reinterpret_cast<float*>(&v)[q];
+}
+
+template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER, int MODE = kAggPlain>
 __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
     const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t nv,
-    float* __restrict__ y, uint64_t ldy, uint32_t last_valid, Tier tier) {
+    float* __restrict__ y, uint64_t ldy, uint32_t last_valid, Tier tier, AggExtra ax) {
   using V = VT<VEC>;
   using T = typename V::T;
+  static_assert(MODE == kAggPlain || (!MAP && !TIER), "activation modes gather local rows only");
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
   constexpr int GPB = kAggThreads / LPD;
   const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
@@ -127,6 +148,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
         }
         for (uint32_t j0 = 0; j0 < ne; j0 += U) {
           T xv[U][NCH];
+          T mv[MODE == kAggMask ? U : 1][MODE == kAggMask ? NCH : 1];
           float ww[U];
 #pragma unroll
           for (int j = 0; j < U; ++j) {
@@ -142,6 +164,25 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
               const uint32_t col = c0 + sl + c * LPD;
               xv[j][c] = (ok && col < nv) ? xrow[col] : V::zero();
             }
+            if constexpr (MODE == kAggMask) {
+              const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)r * ax.ldm);
+#pragma unroll
+              for (int c = 0; c < NCH; ++c) {
+                const uint32_t col = c0 + sl + c * LPD;
+                mv[j][c] = (ok && col < nv) ? mrow[col] : V::zero();
+              }
+            }
+          }
+          if constexpr (MODE == kAggMask) {  // dZ = dX ⊙ [X > 0] · scale
+#pragma unroll
+            for (int j = 0; j < U; ++j)
+#pragma unroll
+              for (int c = 0; c < NCH; ++c)
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) {
+                  float& g = vcomp<VEC>(xv[j][c], q);
+                  g = vcomp<VEC>(mv[j][c], q) > 0.f ? g * ax.scale : 0.f;
+                }
           }
 #pragma unroll
           for (int j = 0; j < U; ++j)
@@ -149,6 +190,25 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
 #pragma unroll
               for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
             }
+        }
+      }
+      if constexpr (MODE == kAggAct) {  // relu + inverted dropout, mask never stored
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t f0 = (c0 + sl + c * LPD) * VEC;  // first float column
+#pragma unroll
+          for (int q2 = 0; q2 < (VEC + 1) / 2; ++q2) {
+            uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
+            if (ax.keep_threshold) rnd = dropout_words((uint64_t)d, f0 + 2 * q2, ax.seed, ax.offset);
+            const uint32_t wd = (d & 3) == 0 ? rnd.x : (d & 3) == 1 ? rnd.y : (d & 3) == 2 ? rnd.z : rnd.w;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              if (2 * q2 + h >= VEC) break;
+              const uint32_t col = f0 + 2 * q2 + h;
+              float& v = vcomp<VEC>(acc[c], 2 * q2 + h);
+              v = (dropout_bits(wd, col) >= ax.keep_threshold && v > 0.f) ? v * ax.scale : 0.f;
+            }
+          }
         }
       }
 #pragma unroll
@@ -294,12 +354,12 @@ constexpr int gather_u(int floats_per_lane) {
   return floats_per_lane <= 4 ? 8 : floats_per_lane <= 12 ? 5 : 4;
 }
 
-template <int VEC, bool MAP, bool TIER>
+template <int VEC, bool MAP, bool TIER, int MODE>
 static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid, Shape s,
                              const uint32_t* off,
                              const uint32_t* idx, const float* w, const uint32_t* n_dev,
                              uint32_t n_cap, const float* x, uint64_t ldx, const uint32_t* map,
-                             uint32_t nv, float* y, uint64_t ldy, Tier tier) {
+                             uint32_t nv, float* y, uint64_t ldy, Tier tier, const AggExtra& ax) {
 // rows in flight per lane group: 8 for narrow rows, 5 for mid-width rows
 // (F ~ 600: 3 float4 per lane; fanout 10/25 -> full batches), 4 for the
 // widest (register budget); NTS_GATHER_U=4 forces 4 for the mid-width rows
@@ -307,13 +367,13 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   do {                                                                                      \
     constexpr int u = gather_u(VEC * NCH);                                                  \
     if (u == 5 && gather_u_env() == 4)                                                      \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4, TIER>), dim3(grid),         \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4, TIER, MODE>), dim3(grid),   \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
-                         nv, y, ldy, last_valid, tier);                                     \
+                         nv, y, ldy, last_valid, tier, ax);                                 \
     else                                                                                    \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u, TIER>), dim3(grid),         \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u, TIER, MODE>), dim3(grid),   \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
-                         nv, y, ldy, last_valid, tier);                                     \
+                         nv, y, ldy, last_valid, tier, ax);                                 \
   } while (0)
   if (s.lpd == 8) NTS_G(8, 1);
   else if (s.lpd == 16) NTS_G(16, 1);
@@ -333,18 +393,19 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   return NTS_OK;
 }
 
-template <bool MAP, bool TIER = false>
+template <bool MAP, bool TIER = false, int MODE = kAggPlain>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
                          const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
                          uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy,
-                         Tier tier = Tier{nullptr, nullptr, 0, 0}) {
+                         Tier tier = Tier{nullptr, nullptr, 0, 0}, AggExtra ax = AggExtra()) {
   int vec = pick_vec(F, ldx, ldy, x, y);
   if (TIER) vec = std::min(vec, pick_vec(F, tier.ldh, ldx, tier.host, x));
+  if (MODE == kAggMask) vec = std::min(vec, pick_vec(F, ax.ldm, ldx, ax.mx, x));
   // rows padded to a 16-byte multiple (the 128-byte feature / output pitch):
   // float4 loads, the partial last vector reads pitch padding and stores only
   // its valid floats
   const uint32_t F4 = (F + 3) / 4 * 4;
-  if (vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
+  if (MODE == kAggPlain && vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
       (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
       (!TIER || (F4 <= tier.ldh && tier.ldh % 4 == 0 && (uintptr_t)tier.host % 16 == 0)))
     vec = 4;
@@ -363,257 +424,15 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   }();
   const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), cap));
   if (vec == 4)
-    return launch_gather_vec<4, MAP, TIER>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
-                                     map, nv, y, ldy, tier);
+    return launch_gather_vec<4, MAP, TIER, MODE>(st, grid, last_valid, s, off, idx, w, n_dev,
+                                                 n_cap, x, ldx, map, nv, y, ldy, tier, ax);
   if (vec == 2)
-    return launch_gather_vec<2, MAP, TIER>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
-                                     map, nv, y, ldy, tier);
-  return launch_gather_vec<1, MAP, TIER>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap, x, ldx,
-                                   map, nv, y, ldy, tier);
+    return launch_gather_vec<2, MAP, TIER, MODE>(st, grid, last_valid, s, off, idx, w, n_dev,
+                                                 n_cap, x, ldx, map, nv, y, ldy, tier, ax);
+  return launch_gather_vec<1, MAP, TIER, MODE>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap,
+                                               x, ldx, map, nv, y, ldy, tier, ax);
 }
 
-
-// ---------------------------------------------------------------------------
-// Fused bottom layer: Y = A X (rows gathered through `map`), Z = Y W and
-// optionally X1 = dropout(relu(Z)) in one kernel (k_agg_gemm).
-//
-// A 256-thread block owns tiles of 32 destination rows:
-//  phase 1 — each wave aggregates 8 rows exactly as k_spmm_gather (same edge
-//     order and mul-then-add arithmetic: Y is bit-identical to the graph op),
-//     writes them to Y (kept for the weight gradient) and into the LDS tile;
-//  phase 2 — wave w computes Z[32 rows x 32 columns 32w .. 32w+31] on
-//     v_mfma_f32_16x16x4_f32 (2 x 2 tiles): A from the LDS tile, B = W rows
-//     streamed from L2 with a two-deep register prefetch (interleaved columns
-//     32w + 2i + j: one float2 per lane per k); epilogue relu + dropout with the
-//     Philox mask of nts_hip_gemm_relu_dropout_f32 (same (row, col) keys).
-// Two blocks per CU (LDS tile 32 x LDP floats, LDP = 2 mod 32: conflict-free
-// b32 reads of 16 rows x 2 k) so one block's MFMA phase runs under the other's
-// HBM-bound gather phase: the layer GEMM costs (almost) no extra time.
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kAgTM = 32;         // rows per tile
-constexpr int kAgN = 128;         // output columns (4 waves x 32)
-constexpr int kAgMaxLDP = 640;    // 32 x 640 x 4 B = 80 KiB: two blocks per CU
-
-struct AgArgs {
-  const uint32_t* off;
-  const uint32_t* idx;
-  const float* w;
-  const uint32_t* n_dev;
-  uint32_t n_cap;
-  const float* x;
-  uint64_t ldx;
-  const uint32_t* map;
-  uint32_t F;
-  const float* W;
-  uint32_t N;
-  float* y;
-  uint64_t ldy;
-  float* z;
-  uint64_t ldz;
-  uint32_t LDP;
-  uint32_t keep_threshold;
-  float scale;
-  uint64_t seed, offset;
-};
-
-template <int VEC, int NCH, bool MAP, bool ACT>
-__global__ __launch_bounds__(kAggThreads, 2) void k_agg_gemm(AgArgs a) {
-  using V = VT<VEC>;
-  using T = typename V::T;
-  extern __shared__ __attribute__((aligned(16))) float sY[];  // [kAgTM][LDP]
-  const uint32_t n = a.n_dev ? min(*a.n_dev, a.n_cap) : a.n_cap;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t nv = a.F / VEC;
-  const uint32_t LDP = a.LDP;
-  const uint32_t Kr = (a.F + 3) / 4 * 4;  // k range of the MFMA phase (zero padded)
-  // zero the k padding [F, Kr) of every LDS row once
-  for (uint32_t e = threadIdx.x; e < kAgTM * (Kr - a.F); e += blockDim.x) {
-    const uint32_t r = e / (Kr - a.F), c = a.F + e % (Kr - a.F);
-    sY[r * LDP + c] = 0.f;
-  }
-  const int i = lane & 15, g = lane >> 4;
-  // this wave's output columns: 32 wv + 2 i + j (j = 0, 1); clamped for loads
-  const uint32_t col0 = 32 * wv + 2 * i;
-  const bool col_ok0 = col0 < a.N, col_ok1 = col0 + 1 < a.N;
-  // even N: one float2 per row (a pair past N is never stored); odd N: two
-  // clamped scalars
-  const bool wpair = (a.N % 2 == 0);
-  const uint32_t ccl = wpair ? min(col0, a.N - 2) : 0u;
-  const uint32_t cx = min(col0, a.N - 1), cy = min(col0 + 1, a.N - 1);
-  const uint32_t ntiles = (n + kAgTM - 1) / kAgTM;
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    // ---- phase 1: aggregation of 32 rows, 8 per wave, two rows at a time ----
-    // (rows rr and rr + 16 advance together: 8 gathered rows in flight per
-    // wave; per row the sum runs in edge order exactly as k_spmm_gather)
-    for (int rr = wv; rr < kAgTM / 2; rr += 4) {
-      const uint32_t dA = tile * kAgTM + rr, dB = dA + kAgTM / 2;
-      const bool okA = dA < n, okB = dB < n;
-      const uint32_t begA = okA ? a.off[dA] : 0u, endA = okA ? a.off[dA + 1] : 0u;
-      const uint32_t begB = okB ? a.off[dB] : 0u, endB = okB ? a.off[dB + 1] : 0u;
-      T accA[NCH], accB[NCH];
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        accA[c] = V::zero();
-        accB[c] = V::zero();
-      }
-      uint32_t eA = begA, eB = begB;
-      while (eA < endA || eB < endB) {  // wave-uniform
-        const uint32_t nA = min(endA - eA, (uint32_t)kUnroll), nB = min(endB - eB, (uint32_t)kUnroll);
-        uint32_t r[2 * kUnroll];
-        float ww[2 * kUnroll];
-#pragma unroll
-        for (int j = 0; j < kUnroll; ++j) {
-          r[j] = j < (int)nA ? a.idx[eA + j] : 0u;
-          ww[j] = j < (int)nA ? (a.w ? a.w[eA + j] : 1.0f) : 0.f;
-          r[kUnroll + j] = j < (int)nB ? a.idx[eB + j] : 0u;
-          ww[kUnroll + j] = j < (int)nB ? (a.w ? a.w[eB + j] : 1.0f) : 0.f;
-        }
-        if (MAP) {
-#pragma unroll
-          for (int j = 0; j < kUnroll; ++j) {
-            if (j < (int)nA) r[j] = a.map[r[j]];
-            if (j < (int)nB) r[kUnroll + j] = a.map[r[kUnroll + j]];
-          }
-        }
-        T xv[2 * kUnroll][NCH];
-#pragma unroll
-        for (int j = 0; j < 2 * kUnroll; ++j) {
-          const bool use = j < kUnroll ? j < (int)nA : (j - kUnroll) < (int)nB;
-          const T* xrow = reinterpret_cast<const T*>(a.x + (uint64_t)r[j] * a.ldx);
-#pragma unroll
-          for (int c = 0; c < NCH; ++c) {
-            const uint32_t col = lane + c * 64;
-            xv[j][c] = (use && col < nv) ? xrow[col] : V::zero();
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < kUnroll; ++j)
-#pragma unroll
-          for (int c = 0; c < NCH; ++c) {
-            if (j < (int)nA) accA[c] = V::madd(accA[c], xv[j][c], ww[j]);
-            if (j < (int)nB) accB[c] = V::madd(accB[c], xv[kUnroll + j][c], ww[kUnroll + j]);
-          }
-        eA += nA;
-        eB += nB;
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t d = h ? dB : dA;
-        float* srow = sY + (rr + h * (kAgTM / 2)) * LDP;
-        T* yrow = (a.y && d < n) ? reinterpret_cast<T*>(a.y + (uint64_t)d * a.ldy) : nullptr;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const uint32_t col = lane + c * 64;
-          if (col < nv) {
-            const T v = d < n ? (h ? accB[c] : accA[c]) : V::zero();
-            if (yrow) V::st_nt(yrow + col, v);
-            const float* av = reinterpret_cast<const float*>(&v);
-#pragma unroll
-            for (int q = 0; q < VEC; ++q) srow[col * VEC + q] = av[q];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ---- phase 2: Z[tile rows][32 wv .. +32) = sY W on 16x16x4 MFMA ----
-    // step s: lane group g contributes k = 4 s + g; A = sY[16 rt + i][k],
-    // B = W[k][32 wv + 2 i + j]
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const float* a0 = sY + i * LDP + g;
-    const float* a1 = sY + (16 + i) * LDP + g;
-    const uint32_t nsteps = Kr / 4;
-    constexpr int PF = 8;  // k-steps per prefetch group
-    auto ldw = [&](uint32_t s, float2& b) {
-      const uint32_t k = min(4 * s + g, a.F - 1);  // k >= F multiplies a zero A
-      const float* wr = a.W + (uint64_t)k * a.N;
-      if (wpair) b = *reinterpret_cast<const float2*>(wr + ccl);
-      else b = make_float2(wr[cx], wr[cy]);
-    };
-    float2 bq[2][PF];
-#pragma unroll
-    for (int q = 0; q < PF; ++q) ldw(q, bq[0][q]);
-    for (uint32_t s0 = 0; s0 < nsteps; s0 += 2 * PF) {
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const uint32_t sb = s0 + half * PF;
-        if (sb >= nsteps) break;
-        // prefetch the next group into the other register set
-#pragma unroll
-        for (int q = 0; q < PF; ++q) ldw(min(sb + PF + q, nsteps - 1), bq[half ^ 1][q]);
-#pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          const uint32_t s = sb + q;
-          if (s >= nsteps) break;
-          const float x0 = a0[4 * s], x1 = a1[4 * s];
-          const float2 b = bq[half][q];
-          acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b.x, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, b.y, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, b.x, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, b.y, acc[1][1], 0, 0, 0);
-        }
-      }
-    }
-    // epilogue: acc[rt][j][v] = Z[tile*32 + 16 rt + 4 g + v][col0 + j]
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const uint32_t r4 = tile * kAgTM + 16 * rt + 4 * g;
-      uint4 rnd = make_uint4(0u, 0u, 0u, 0u);  // columns col0, col0 + 1: one call
-      if constexpr (ACT) rnd = dropout_words((uint64_t)r4, col0, a.seed, a.offset);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t col = col0 + j;
-        if (!(j ? col_ok1 : col_ok0)) continue;
-        float o[4] = {acc[rt][j][0], acc[rt][j][1], acc[rt][j][2], acc[rt][j][3]};
-        if constexpr (ACT) {
-          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            o[v] = (dropout_bits(wd[v], col) >= a.keep_threshold && o[v] > 0.f) ? o[v] * a.scale
-                                                                                 : 0.f;
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          if (r4 + v < n) a.z[(uint64_t)(r4 + v) * a.ldz + col] = o[v];
-      }
-    }
-    __syncthreads();  // the LDS tile is rewritten by the next phase 1
-  }
-}
-
-// LDS row pitch of the fused kernel: >= F rounded up to 4 (MFMA k range),
-// = 2 mod 32 (conflict-free reads); 0 when the tile does not fit two blocks per CU.
-static uint32_t ag_ldp(uint32_t F) {
-  const uint32_t k4 = (F + 3) / 4 * 4;
-  const uint32_t ldp = k4 + ((2u + 32u - k4 % 32u) % 32u);
-  return ldp <= (uint32_t)kAgMaxLDP ? ldp : 0u;
-}
-
-template <int VEC, bool MAP, bool ACT>
-static int launch_agg_gemm_vec(hipStream_t st, int nch, uint32_t grid, size_t lds,
-                               const AgArgs& a) {
-#define NTS_AG(NCH)                                                                        \
-  do {                                                                                     \
-    NTS_HIP_TRY(hipFuncSetAttribute(                                                       \
-        reinterpret_cast<const void*>(&k_agg_gemm<VEC, NCH, MAP, ACT>),                    \
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));                            \
-    hipLaunchKernelGGL((k_agg_gemm<VEC, NCH, MAP, ACT>), dim3(grid), dim3(kAggThreads),    \
-                       lds, st, a);                                                        \
-  } while (0)
-  switch (nch) {
-    case 1: NTS_AG(1); break;
-    case 2: NTS_AG(2); break;
-    case 3: NTS_AG(3); break;
-    case 4: NTS_AG(4); break;
-    default: NTS_AG(5); break;
-  }
-#undef NTS_AG
-  NTS_LAUNCH_CHECK();
-  return NTS_OK;
-}
 
 }  // namespace nts_hip
 
@@ -637,57 +456,6 @@ int nts_hip_spmm_csc_fwd(nts_hip_ctx* ctx, const uint32_t* column_offset,
                               nullptr, feature_size, y, ldy);
 }
 
-int nts_hip_spmm_csc_fwd_linear(nts_hip_ctx* ctx, const uint32_t* column_offset,
-                                const uint32_t* row_indices, const float* weight,
-                                const uint32_t* v, uint32_t v_cap, const float* x, uint64_t ldx,
-                                const uint32_t* x_row_map, uint32_t feature_size, const float* W,
-                                uint32_t out_size, float* y, uint64_t ldy, float* z,
-                                uint64_t ldz, int activation, float p, uint64_t seed,
-                                uint64_t offset) {
-  NTS_CHECK_ARG(ctx && column_offset && row_indices && x && W && z, "NULL argument");
-  NTS_CHECK_ARG(ldx >= feature_size && (!y || ldy >= feature_size) && ldz >= out_size,
-                "leading dimension");
-  NTS_CHECK_ARG(out_size >= 1 && out_size <= (uint32_t)kAgN, "out_size must be in [1, 128]");
-  NTS_CHECK_ARG(p >= 0.f && p <= 1.f, "dropout probability must be in [0, 1]");
-  if (v_cap == 0 || feature_size == 0) return NTS_OK;
-  const uint32_t F = feature_size;
-  const uint32_t LDP = ag_ldp(F);
-  NTS_CHECK_ARG(LDP != 0, "feature_size too large for the fused kernel (<= 608)");
-  int vec = pick_vec(F, ldx, y ? ldy : ldx, x, y ? (const void*)y : (const void*)x);
-  const uint32_t nv = F / vec;
-  const int nch = (int)((nv + 63) / 64);
-  NTS_CHECK_ARG(nch <= 5, "feature_size too large for the fused kernel");
-  NTS_HIP_TRY(hipSetDevice(ctx->device));
-  AgArgs a{column_offset, row_indices, weight, v, v_cap, x, ldx, x_row_map, F, W, out_size,
-           y, ldy, z, ldz, LDP, 0u, 1.f, seed, offset};
-  a.keep_threshold = dropout_threshold(p);
-  a.scale = p >= 1.f ? 0.f : 1.0f / (1.0f - p);
-  const size_t lds = (size_t)kAgTM * LDP * sizeof(float);
-  const uint32_t tiles = (v_cap + kAgTM - 1) / kAgTM;
-  const uint32_t grid = std::max(1u, std::min(tiles, 512u));  // 2 blocks per CU
-  const hipStream_t st = ctx->stream;
-#define NTS_AGL(VEC, MAPB, ACTB) return launch_agg_gemm_vec<VEC, MAPB, ACTB>(st, nch, grid, lds, a)
-  if (activation) {
-    if (x_row_map) {
-      if (vec == 4) NTS_AGL(4, true, true);
-      if (vec == 2) NTS_AGL(2, true, true);
-      NTS_AGL(1, true, true);
-    }
-    if (vec == 4) NTS_AGL(4, false, true);
-    if (vec == 2) NTS_AGL(2, false, true);
-    NTS_AGL(1, false, true);
-  }
-  if (x_row_map) {
-    if (vec == 4) NTS_AGL(4, true, false);
-    if (vec == 2) NTS_AGL(2, true, false);
-    NTS_AGL(1, true, false);
-  }
-  if (vec == 4) NTS_AGL(4, false, false);
-  if (vec == 2) NTS_AGL(2, false, false);
-  NTS_AGL(1, false, false);
-#undef NTS_AGL
-}
-
 int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
                          const uint32_t* column_indices, const float* weight_backward,
                          const uint32_t* s, uint32_t s_cap, const float* g_out, uint64_t ld_gout,
@@ -699,6 +467,45 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
   NTS_HIP_TRY(hipSetDevice(ctx->device));
   return launch_gather<false>(ctx->stream, row_offset, column_indices, weight_backward, s, s_cap,
                               g_out, ld_gout, nullptr, feature_size, g_in, ld_gin);
+}
+
+int nts_hip_spmm_csc_fwd_act(nts_hip_ctx* ctx, const uint32_t* column_offset,
+                             const uint32_t* row_indices, const float* weight, const uint32_t* v,
+                             uint32_t v_cap, const float* x, uint64_t ldx, uint32_t feature_size,
+                             float* y, uint64_t ldy, float p, uint64_t seed, uint64_t offset) {
+  NTS_CHECK_ARG(ctx && column_offset && row_indices && x && y, "NULL argument");
+  NTS_CHECK_ARG(ldx >= feature_size && ldy >= feature_size, "leading dimension < feature_size");
+  NTS_CHECK_ARG(p >= 0.f && p <= 1.f, "dropout probability must be in [0, 1]");
+  if (v_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  AggExtra ax;
+  ax.keep_threshold = dropout_threshold(p);
+  ax.scale = p >= 1.f ? 0.f : 1.0f / (1.0f - p);  // as the GEMM epilogue
+  ax.seed = seed;
+  ax.offset = offset;
+  return launch_gather<false, false, kAggAct>(ctx->stream, column_offset, row_indices, weight, v,
+                                              v_cap, x, ldx, nullptr, feature_size, y, ldy,
+                                              Tier{nullptr, nullptr, 0, 0}, ax);
+}
+
+int nts_hip_spmm_csr_bwd_masked(nts_hip_ctx* ctx, const uint32_t* row_offset,
+                                const uint32_t* column_indices, const float* weight_backward,
+                                const uint32_t* s, uint32_t s_cap, const float* g_out,
+                                uint64_t ld_gout, const float* x_act, uint64_t ld_act, float scale,
+                                uint32_t feature_size, float* g_in, uint64_t ld_gin) {
+  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && x_act && g_in, "NULL argument");
+  NTS_CHECK_ARG(ld_gout >= feature_size && ld_act >= feature_size && ld_gin >= feature_size,
+                "leading dimension < feature_size");
+  if (s_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  AggExtra ax;
+  ax.mx = x_act;
+  ax.ldm = ld_act;
+  ax.scale = scale;
+  return launch_gather<false, false, kAggMask>(ctx->stream, row_offset, column_indices,
+                                               weight_backward, s, s_cap, g_out, ld_gout, nullptr,
+                                               feature_size, g_in, ld_gin,
+                                               Tier{nullptr, nullptr, 0, 0}, ax);
 }
 
 int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx* ctx, const uint32_t* column_offset,

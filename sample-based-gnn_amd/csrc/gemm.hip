@@ -52,13 +52,18 @@ __device__ __forceinline__ float msk(float v, uint32_t mk) {
 // its LDS image is zeroed by mask), so the compiler counts outstanding loads
 // (vmcnt(N)) across steps instead of draining the queue: the two-deep
 // prefetch relies on it.  Row/column bases are computed once per block.
+// amap != nullptr: row r of the A operand is row amap[r] of the given matrix
+// (NN: the M rows; TN: the K rows) — the transform-first bottom layer reads
+// the feature table through the sampled layer's `source`.
 template <bool TRANS_A, int AVEC>
 struct ATile {
   static constexpr int NP = 8 / AVEC;  // loads per thread per step
   const float* base[TRANS_A ? 1 : NP];
+  const uint32_t* amap;
   int kc;      // NN: this thread's k column in the step;  TN: its first k row
   int sdst;    // LDS offset of the first element
-  __device__ ATile(const float* A, uint64_t lda, int M, int K, int64_t m0) {
+  __device__ ATile(const float* A, uint64_t lda, int M, int K, int64_t m0, const uint32_t* map)
+      : amap(map) {
     const int tid = threadIdx.x;
     if (!TRANS_A) {  // A[m][k]: 64 rows x 32 k, rows tid/(32/AVEC) + (256/(32/AVEC)) p
       constexpr int per = 32 / AVEC;
@@ -66,7 +71,8 @@ struct ATile {
 #pragma unroll
       for (int p = 0; p < NP; ++p) {
         const int64_t m = m0 + tid / per + (256 / per) * p;
-        base[p] = A + (uint64_t)(m < M ? m : M - 1) * lda;
+        const uint64_t mm = (uint64_t)(m < M ? m : M - 1);
+        base[p] = A + (amap ? (uint64_t)amap[mm] : mm) * lda;
       }
       sdst = (tid / per) * kAP + kc;
     } else {  // A[k][m]: 32 k x 64 m, k rows tid/(64/AVEC) + (256/(64/AVEC)) p
@@ -87,7 +93,7 @@ struct ATile {
         src = base[p] + k;
       } else {
         const int k = min(k0 + kc + (256 / (64 / AVEC)) * p, K - 1);
-        src = base[0] + (uint64_t)k * lda;
+        src = base[0] + (amap ? (uint64_t)amap[k] : (uint64_t)k) * lda;
       }
       if (AVEC == 4) {
         const float4 x = *reinterpret_cast<const float4*>(src);
@@ -215,6 +221,7 @@ struct GemmExtra {
   const float* bx = nullptr;
   uint64_t ldbx = 0;
   float bscale = 1.f;
+  const uint32_t* amap = nullptr;  // gathered A rows (see ATile)
 };
 
 // C_tile = op(A) B over k in [kbeg, kend); result written to C (ldc) or to a
@@ -238,7 +245,7 @@ __global__ __launch_bounds__(kGT, 3) void k_gemm(int M, int N, int K, const floa
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-  const ATile<TRANS_A, AVEC> at(A, lda, M, kend, m0);
+  const ATile<TRANS_A, AVEC> at(A, lda, M, kend, m0, ex.amap);
   const BTile<BFULL, BMASK> bt(B, ex.bx, N, n0);
   constexpr int NX = BTile<BFULL, BMASK>::NX;
 
@@ -452,7 +459,8 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
 #pragma unroll
     for (int rt = 0; rt < kWresRT; ++rt) {
       const int64_t r = m0 + 16 * rt + i;
-      ar[rt] = A + (uint64_t)(r < M ? r : M - 1) * lda;
+      const uint64_t rr = (uint64_t)(r < M ? r : M - 1);
+      ar[rt] = A + (ex.amap ? (uint64_t)ex.amap[rr] : rr) * lda;
     }
   };
   // XT (cross-task prefetch, needs nfull % DEPTH == 0): the loads that would
@@ -649,7 +657,8 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
       // AVEC = 4 reads may run into the row padding (lda >= M rounded up to
       // 4); columns >= M are zeroed when staged
       const int c = min(r0 + AVEC * (e % NAV), AVEC == 4 ? (int)lda - 4 : M - AVEC);
-      const float* src = A + (uint64_t)kk * lda + c;
+      const uint64_t row = ex.amap ? (uint64_t)ex.amap[kk] : (uint64_t)kk;
+      const float* src = A + row * lda + c;
       if (AVEC == 4) {
         const float4 x = *reinterpret_cast<const float4*>(src);
         av[4 * p] = x.x; av[4 * p + 1] = x.y; av[4 * p + 2] = x.z; av[4 * p + 3] = x.w;
@@ -1047,6 +1056,26 @@ extern "C" int nts_hip_gemm_f32(nts_hip_ctx* ctx, int trans_a, int M, int N, int
   NTS_GEMM_ARGS_CHECK(trans_a);
   return trans_a ? gemm<false, false>(ctx, true, M, N, K, A, lda, B, ldb, C, ldc, GemmExtra())
                  : gemm<false, false>(ctx, false, M, N, K, A, lda, B, ldb, C, ldc, GemmExtra());
+}
+
+extern "C" int nts_hip_gemm_gather_f32(nts_hip_ctx* ctx, int M, int N, int K, const float* A,
+                                       uint64_t lda, const uint32_t* a_rows, const float* B,
+                                       uint64_t ldb, float* C, uint64_t ldc) {
+  NTS_GEMM_ARGS_CHECK(false);
+  NTS_CHECK_ARG(a_rows || K == 0, "NULL row map");
+  GemmExtra ex;
+  ex.amap = a_rows;
+  return gemm<false, false>(ctx, false, M, N, K, A, lda, B, ldb, C, ldc, ex);
+}
+
+extern "C" int nts_hip_gemm_tn_gather_f32(nts_hip_ctx* ctx, int M, int N, int K, const float* A,
+                                          uint64_t lda, const uint32_t* a_rows, const float* B,
+                                          uint64_t ldb, float* C, uint64_t ldc) {
+  NTS_GEMM_ARGS_CHECK(true);
+  NTS_CHECK_ARG(a_rows || K == 0, "NULL row map");
+  GemmExtra ex;
+  ex.amap = a_rows;
+  return gemm<false, false>(ctx, true, M, N, K, A, lda, B, ldb, C, ldc, ex);
 }
 
 extern "C" int nts_hip_gemm_relu_dropout_f32(nts_hip_ctx* ctx, int M, int N, int K, const float* A,

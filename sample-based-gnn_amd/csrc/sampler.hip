@@ -512,12 +512,17 @@ __device__ __forceinline__ float norm_degree(uint32_t out_src, uint32_t in_dst) 
 }
 
 // up_cnt != nullptr (UP_DEGREE): count the sampled edges per local src
-// instead of computing the weights (k_up_weight does, once counted)
+// instead of computing the weights (k_up_weight does, once counted).
+// MEAN divides by the dst's full-graph in-degree (the CPU sampler,
+// core/ntsFastSampler.hpp:1111-1113); MEAN_SAMPLED by its sampled edge count
+// (the reference GPU kernel get_mean_weight, cuda/ntsCUDATransferKernel.cuh:319-342,
+// which its GPU toolkits never reach: SURVEY Appendix B-5).
 __global__ void k_relabel(const uint32_t* __restrict__ ans, const uint32_t* __restrict__ edst,
                           const uint32_t* __restrict__ dst, const uint32_t* __restrict__ src_index,
                           const uint32_t* __restrict__ out_deg, const uint32_t* __restrict__ in_deg,
-                          const uint32_t* sizes, int weight_type, uint32_t* __restrict__ ri,
-                          float* __restrict__ wf, uint32_t* __restrict__ up_cnt) {
+                          const uint32_t* __restrict__ co, const uint32_t* sizes,
+                          int weight_type, uint32_t* __restrict__ ri, float* __restrict__ wf,
+                          uint32_t* __restrict__ up_cnt) {
   const uint32_t e = sizes[1];
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x) {
     const uint32_t g = ans[k];
@@ -530,6 +535,7 @@ __global__ void k_relabel(const uint32_t* __restrict__ ans, const uint32_t* __re
       const uint32_t ind = in_deg[dg];
       float w = norm_degree(out_deg[g], ind);
       if (weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
+      if (weight_type == NTS_WEIGHT_MEAN_SAMPLED) w = w / (float)(co[edst[k] + 1] - co[edst[k]]);
       wf[k] = w;
     }
   }
@@ -545,7 +551,8 @@ __global__ void k_up_weight(const uint32_t* __restrict__ ri, const uint32_t* __r
     const uint32_t d = edst[k];
     const uint32_t ind = co[d + 1] - co[d];
     float w = norm_degree(cnt[ri[k]], ind);
-    if (weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
+    if (weight_type == NTS_WEIGHT_MEAN || weight_type == NTS_WEIGHT_MEAN_SAMPLED)
+      w = w / (float)ind;  // the dst's sampled count is its UP_DEGREE in-degree
     wf[k] = w;
   }
 }
@@ -606,7 +613,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                 "missing sampCSC buffer");
   const bool up_degree = (weight_type & NTS_WEIGHT_UP_DEGREE) != 0;
   weight_type &= 0xF;
-  NTS_CHECK_ARG(weight_type >= NTS_WEIGHT_SUM && weight_type <= NTS_WEIGHT_NONE, "weight_type");
+  NTS_CHECK_ARG(weight_type >= NTS_WEIGHT_SUM && weight_type <= NTS_WEIGHT_MEAN_SAMPLED,
+                "weight_type");
   NTS_CHECK_ARG(weight_type == NTS_WEIGHT_NONE || (o->edge_weight_forward && g->in_degree &&
                                                    g->out_degree),
                 "weights requested without buffers/degrees");
@@ -717,8 +725,9 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   // 4) relabel to local ids + forward weights
   if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, o->sample_ans, o->edge_dst,
-                     o->destination, ctx->src_index, g->out_degree, g->in_degree, o->sizes,
-                     weight_type, o->row_indices, o->edge_weight_forward, up ? t_up : nullptr);
+                     o->destination, ctx->src_index, g->out_degree, g->in_degree,
+                     o->column_offset, o->sizes, weight_type, o->row_indices,
+                     o->edge_weight_forward, up ? t_up : nullptr);
   NTS_LAUNCH_CHECK();
   if (up) {
     hipLaunchKernelGGL(k_up_weight, dim3(ge), dim3(256), 0, st, o->row_indices, o->edge_dst,

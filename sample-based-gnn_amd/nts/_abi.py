@@ -17,13 +17,14 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 2  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 3  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
 NTS_WEIGHT_SUM = 0
 NTS_WEIGHT_MEAN = 1
 NTS_WEIGHT_NONE = 2
+NTS_WEIGHT_MEAN_SAMPLED = 3
 
 # every symbol declared in include/nts_hip.h (checked by tests/test_abi.py)
 EXPORTED = (
@@ -31,7 +32,9 @@ EXPORTED = (
     "nts_hip_ctx_set_stream", "nts_hip_ctx_get_stream", "nts_hip_ctx_reserve",
     "nts_hip_rng_seed", "nts_hip_rng_state", "nts_hip_degrees", "nts_hip_build_csc",
     "nts_hip_sample_layer", "nts_hip_gather_rows", "nts_hip_gather_labels",
-    "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csc_fwd_linear", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
+    "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
+    "nts_hip_spmm_csc_fwd_act", "nts_hip_spmm_csr_bwd_masked", "nts_hip_gemm_gather_f32",
+    "nts_hip_gemm_tn_gather_f32",
     "nts_hip_gemm_f32", "nts_hip_gemm_relu_dropout_f32", "nts_hip_gemm_tn_masked_f32",
     "nts_hip_linear_xent_fwd", "nts_hip_linear_xent_bwd", "nts_hip_linear_xent_train", "nts_hip_adam", "nts_hip_comm_unique_id", "nts_hip_comm_init", "nts_hip_comm_destroy",
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
@@ -94,8 +97,10 @@ def lib() -> C.CDLL:
         "nts_hip_gather_rows": ([P, P, U64, P, P, U32, U32, P, U64], I),
         "nts_hip_gather_labels": ([P, P, P, P, U32, P], I),
         "nts_hip_spmm_csc_fwd": ([P, P, P, P, P, U32, P, U64, P, U32, P, U64], I),
-        "nts_hip_spmm_csc_fwd_linear": ([P, P, P, P, P, U32, P, U64, P, U32, P, U32, P, U64, P, U64,
-                                         I, F, U64, U64], I),
+        "nts_hip_spmm_csc_fwd_act": ([P, P, P, P, P, U32, P, U64, U32, P, U64, F, U64, U64], I),
+        "nts_hip_spmm_csr_bwd_masked": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
+        "nts_hip_gemm_gather_f32": ([P, I, I, I, P, U64, P, P, U64, P, U64], I),
+        "nts_hip_gemm_tn_gather_f32": ([P, I, I, I, P, U64, P, P, U64, P, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),

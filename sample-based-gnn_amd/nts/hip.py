@@ -134,13 +134,20 @@ class HipContext:
                                             ptr(x), x.stride(0), ptr(row_map), F, ptr(y),
                                             y.stride(0)))
 
-    def spmm_csc_fwd_linear(self, co, ri, w, v_dev, v_cap, x, W, z, y=None, row_map=None,
-                            activation=False, p=0.0, seed=0, offset=0):
+    def spmm_csc_fwd_act(self, co, ri, w, v_dev, v_cap, x, y, p=0.0, seed=0, offset=0):
+        """y = dropout(relu(A x), p) (transform-first bottom layer)."""
         F = x.shape[1]
-        check(self.lib.nts_hip_spmm_csc_fwd_linear(
-            self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev), v_cap, ptr(x), x.stride(0), ptr(row_map),
-            F, ptr(W), W.shape[1], ptr(y), y.stride(0) if y is not None else F, ptr(z), z.stride(0),
-            int(activation), float(p), int(seed), int(offset)))
+        check(self.lib.nts_hip_spmm_csc_fwd_act(self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev), v_cap,
+                                                ptr(x), x.stride(0), F, ptr(y), y.stride(0),
+                                                float(p), int(seed), int(offset)))
+
+    def spmm_csr_bwd_masked(self, ro, ci, wb, s_dev, s_cap, g_out, x_act, g_in, scale=1.0):
+        """g_in = A^T (g_out * (x_act > 0) * scale) over the CSR."""
+        F = g_out.shape[1]
+        check(self.lib.nts_hip_spmm_csr_bwd_masked(self.h, ptr(ro), ptr(ci), ptr(wb), ptr(s_dev),
+                                                   s_cap, ptr(g_out), g_out.stride(0), ptr(x_act),
+                                                   x_act.stride(0), float(scale), F, ptr(g_in),
+                                                   g_in.stride(0)))
 
     def spmm_csr_bwd(self, ro, ci, wb, s_dev, s_cap, g_out, g_in):
         F = g_out.shape[1]
@@ -163,6 +170,18 @@ class HipContext:
         N = B.shape[1]
         check(self.lib.nts_hip_gemm_f32(self.h, int(trans_a), M, N, K, ptr(A), A.stride(0), ptr(B),
                                         B.stride(0), ptr(C), C.stride(0)))
+
+    def gemm_gather(self, A, rows, B, C):
+        """C = A[rows] @ B (rows: int32 device tensor of row ids)."""
+        M, K, N = rows.numel(), A.shape[1], B.shape[1]
+        check(self.lib.nts_hip_gemm_gather_f32(self.h, M, N, K, ptr(A), A.stride(0), ptr(rows),
+                                               ptr(B), B.stride(0), ptr(C), C.stride(0)))
+
+    def gemm_tn_gather(self, A, rows, B, C):
+        """C = A[rows].T @ B."""
+        K, M, N = rows.numel(), A.shape[1], B.shape[1]
+        check(self.lib.nts_hip_gemm_tn_gather_f32(self.h, M, N, K, ptr(A), A.stride(0), ptr(rows),
+                                                  ptr(B), B.stride(0), ptr(C), C.stride(0)))
 
     def gemm_relu_dropout(self, A, B, C, p=0.0, seed=0, offset=0):
         """C = dropout(relu(A @ B), p) with the Philox mask of (seed, offset)."""

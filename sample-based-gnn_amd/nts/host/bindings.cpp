@@ -46,7 +46,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::enum_<WeightType>(m, "WeightType")
       .value("Sum", WeightType::Sum)
       .value("Mean", WeightType::Mean)
-      .value("None", WeightType::None);
+      .value("None", WeightType::None)
+      .value("MeanSampled", WeightType::MeanSampled);
 
   py::class_<FullyRepGraph, std::shared_ptr<FullyRepGraph>>(m, "FullyRepGraph")
       .def_static(
@@ -100,6 +101,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("work_offset", [](PySampler& p) { return p.s->work_offset; })
       .def_property_readonly("sampled_edges", [](PySampler& p) { return p.s->sampled_edges; });
 
+  m.def(
+      "sampler_throughput",
+      [](std::shared_ptr<FullyRepGraph> g, const torch::Tensor& seeds, int batch,
+         std::vector<int> fanout, WeightType w, int rng_mode, int n_batches,
+         std::vector<bool> csr) {
+        SamplerRate r;
+        {
+          py::gil_scoped_release nogil;
+          r = sampler_throughput(g, to_ids(seeds), batch, fanout, w, rng_mode, n_batches, csr);
+        }
+        py::dict d;
+        d["seconds"] = r.seconds;
+        d["edges"] = r.edges;
+        d["batches"] = r.batches;
+        return d;
+      },
+      py::arg("graph"), py::arg("seeds"), py::arg("batch_size"), py::arg("fanout"),
+      py::arg("weight_type") = WeightType::Sum, py::arg("rng_mode") = (int)NTS_RNG_PHILOX,
+      py::arg("n_batches") = 16, py::arg("csr_layers") = std::vector<bool>());
+
   py::class_<Communicator, std::shared_ptr<Communicator>>(m, "Communicator")
       .def(py::init([](int n, int r, py::bytes uid, int dev) {
         std::string s = uid;
@@ -136,7 +157,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("deterministic_backward", &GCNConfig::deterministic_backward)
       .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
       .def_readwrite("pipeline", &GCNConfig::pipeline)
-      .def_readwrite("fuse_linear", &GCNConfig::fuse_linear)
+      .def_readwrite("transform_first", &GCNConfig::transform_first)
       .def_readwrite("early_aggregate", &GCNConfig::early_aggregate)
       .def_readwrite("sampler_priority", &GCNConfig::sampler_priority)
       .def_readwrite("fuse_loss", &GCNConfig::fuse_loss)
@@ -170,7 +191,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_weights", &GCN_SAMPLE_ALLGPU_impl::set_weights)
       .def("weights", &GCN_SAMPLE_ALLGPU_impl::weights)
       .def("reset_stats", &GCN_SAMPLE_ALLGPU_impl::reset_stats)
-      .def("resolve_profile", &GCN_SAMPLE_ALLGPU_impl::resolve_profile)
+      .def("resolve_profile",
+           [](GCN_SAMPLE_ALLGPU_impl& d) {
+             // {kernel: {"ms": total device ms, "calls": n, "units": algorithmic
+             //  bytes (aggregations) or flops (GEMMs) summed over the calls}}
+             d.resolve_profile();
+             py::dict out;
+             for (int i = 0; i < KernelProfiler::kCount; ++i) {
+               const auto& st = d.prof.stat[i];
+               if (!st.calls) continue;
+               py::dict e;
+               e["ms"] = st.ms;
+               e["calls"] = st.calls;
+               e["units"] = st.units;
+               out[KernelProfiler::name(i)] = e;
+             }
+             return out;
+           })
+      .def_property_readonly("transform_first", &GCN_SAMPLE_ALLGPU_impl::transform_first)
       .def("sample_not_finished", &GCN_SAMPLE_ALLGPU_impl::has_batch)
       .def("restart", &GCN_SAMPLE_ALLGPU_impl::restart)
       .def("synchronize", [](GCN_SAMPLE_ALLGPU_impl& d) { d.cs->synchronize(); })
@@ -180,9 +218,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                              [](GCN_SAMPLE_ALLGPU_impl& d) { return layers_of(d.sampler->ssg); })
       .def_readonly("sample_time", &GCN_SAMPLE_ALLGPU_impl::sample_time)
       .def_readonly("train_time", &GCN_SAMPLE_ALLGPU_impl::train_time)
-      .def_readonly("agg_ms", &GCN_SAMPLE_ALLGPU_impl::agg_ms)
-      .def_readonly("agg_bytes", &GCN_SAMPLE_ALLGPU_impl::agg_bytes)
-      .def_readonly("agg_calls", &GCN_SAMPLE_ALLGPU_impl::agg_calls)
       .def_readonly("batch_edges", &GCN_SAMPLE_ALLGPU_impl::batch_edges)
       .def_readonly("batches", &GCN_SAMPLE_ALLGPU_impl::batches);
 }

@@ -280,8 +280,10 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   if (ssgs.size() > 1) hip_rt(hipEventSynchronize(ssg->consumed), "hipEventSynchronize");
   hip_rt(hipStreamWaitEvent(st, ssg->consumed, 0), "hipStreamWaitEvent");
   const nts_graph_dev g = whole_graph->dev();
-  int wt = w == WeightType::Sum ? NTS_WEIGHT_SUM
-                                : (w == WeightType::Mean ? NTS_WEIGHT_MEAN : NTS_WEIGHT_NONE);
+  int wt = w == WeightType::Sum           ? NTS_WEIGHT_SUM
+           : w == WeightType::Mean        ? NTS_WEIGHT_MEAN
+           : w == WeightType::MeanSampled ? NTS_WEIGHT_MEAN_SAMPLED
+                                          : NTS_WEIGHT_NONE;
   if (up_degree && wt != NTS_WEIGHT_NONE) wt |= NTS_WEIGHT_UP_DEGREE;
   const VertexId* dst = dptr<VertexId>(dev_nids_) + work_offset;
   sampCSC* s0 = ssg->sampled_sgs[0];
@@ -711,51 +713,82 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
   }
 };
 
-// Bottom graph op + first layer (+ relu/dropout) in one kernel
-// (nts_hip_spmm_csc_fwd_linear); the weight gradient uses the stored Y.
-struct HipAggLinearFn : public torch::autograd::Function<HipAggLinearFn> {
-  static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, NtsVar y, int64_t sg_ptr,
-                        int64_t cs_ptr, double p, int64_t seed, int64_t offset, bool act) {
+// Transform-first bottom layer (nts_hip.h):
+//   H = X[source] W      (row-gathered MFMA GEMM: load_feature_gpu fused away)
+//   X1 = dropout(relu(A H))  (the graph op over F_out-wide rows, activation in
+//                             the epilogue with the GEMM epilogue's mask keys)
+// backward: dH = A^T (dX1 ⊙ [X1 > 0] / (1-p)) over the CSR, dW = X[source]^T dH.
+// Recorded as one NN op whose input is the feature table (the bottom graph
+// op has no backward, core/ntsContext.hpp:443-444).
+struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, int64_t sg_ptr,
+                        int64_t cs_ptr, double p, int64_t seed, int64_t offset, int64_t prof_ptr,
+                        int64_t h_out) {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     auto* sg = reinterpret_cast<sampCSC*>(sg_ptr);
+    auto* prof = reinterpret_cast<KernelProfiler*>(prof_ptr);
     NtsVar Wc = W.contiguous();
     const int64_t F = table.size(1), N = Wc.size(1);
-    NtsVar Z = torch::empty({(int64_t)sg->v_size, N}, table.options());
-    hip_check(nts_hip_spmm_csc_fwd_linear(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
-                                          nullptr, sg->v_size, table.data_ptr<float>(),
-                                          (uint64_t)table.stride(0), sg->dev_src(), (uint32_t)F,
-                                          Wc.data_ptr<float>(), (uint32_t)N, y.data_ptr<float>(),
-                                          (uint64_t)y.stride(0), Z.data_ptr<float>(), (uint64_t)N,
-                                          act ? 1 : 0, (float)p, (uint64_t)seed, (uint64_t)offset),
-              "nts_hip_spmm_csc_fwd_linear");
-    ctx->save_for_backward({y, Wc, act ? Z : NtsVar()});
+    const int64_t s = sg->src_size, v = sg->v_size, e = sg->e_size;
+    TORCH_CHECK(Wc.size(0) == F && table.stride(1) == 1, "transform-first: shape mismatch");
+    const int dev = cs->device();
+    hipStream_t st = (hipStream_t)cs->stream();
+    NtsVar H = h_out ? NtsVar() : torch::empty({std::max<int64_t>(s, 1), N}, f32_opts(dev));
+    float* hp = h_out ? reinterpret_cast<float*>(h_out) : H.data_ptr<float>();
+    if (prof) prof->begin(KernelProfiler::GATHER_GEMM, st);
+    hip_check(nts_hip_gemm_gather_f32(cs->ctx(), (int)s, (int)N, (int)F, table.data_ptr<float>(),
+                                      (uint64_t)table.stride(0), sg->dev_src(),
+                                      Wc.data_ptr<float>(), (uint64_t)N, hp, (uint64_t)N),
+              "nts_hip_gemm_gather_f32");
+    if (prof) prof->end(KernelProfiler::GATHER_GEMM, st, 2.0 * (double)s * F * N);
+    NtsVar X1 = torch::empty({v, N}, f32_opts(dev));
+    if (prof) prof->begin(KernelProfiler::BOTTOM_AGG, st);
+    hip_check(nts_hip_spmm_csc_fwd_act(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
+                                       nullptr, (uint32_t)v, hp, (uint64_t)N, (uint32_t)N,
+                                       X1.data_ptr<float>(), (uint64_t)N, (float)p, (uint64_t)seed,
+                                       (uint64_t)offset),
+              "nts_hip_spmm_csc_fwd_act");
+    // compulsory bytes: each H row once, index + weight per edge, offsets, output
+    if (prof)
+      prof->end(KernelProfiler::BOTTOM_AGG, st,
+                4.0 * N * s + 8.0 * e + 4.0 * (v + 1) + 4.0 * N * v);
+    ctx->save_for_backward({table, Wc, X1});
+    ctx->saved_data["sg"] = sg_ptr;
     ctx->saved_data["cs"] = cs_ptr;
-    ctx->saved_data["act"] = act;
+    ctx->saved_data["prof"] = prof_ptr;
     ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
-    return Z;
+    return X1;
   }
   static variable_list backward(AutogradContext* ctx, variable_list grads) {
     auto saved = ctx->get_saved_variables();
-    NtsVar y = saved[0], W = saved[1];
+    NtsVar table = saved[0], W = saved[1], X1 = saved[2];
     auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
-    const bool act = ctx->saved_data["act"].toBool();
+    auto* sg = reinterpret_cast<sampCSC*>(ctx->saved_data["sg"].toInt());
+    auto* prof = reinterpret_cast<KernelProfiler*>(ctx->saved_data["prof"].toInt());
+    TORCH_CHECK(sg->has_csr, "transform-first backward needs the bottom layer's CSR");
     NtsVar g = grads[0].contiguous();
-    const int64_t M = y.size(0), K = y.size(1), N = W.size(1);
-    NtsVar dW = torch::empty({K, N}, W.options());
-    if (act) {
-      NtsVar X = saved[2];
-      hip_check(nts_hip_gemm_tn_masked_f32(cs->ctx(), (int)K, (int)N, (int)M, y.data_ptr<float>(),
-                                           (uint64_t)y.stride(0), g.data_ptr<float>(), (uint64_t)N,
-                                           X.data_ptr<float>(), (uint64_t)N,
-                                           (float)ctx->saved_data["scale"].toDouble(),
-                                           dW.data_ptr<float>(), (uint64_t)N),
-                "nts_hip_gemm_tn_masked_f32");
-    } else {
-      hip_check(nts_hip_gemm_f32(cs->ctx(), 1, (int)K, (int)N, (int)M, y.data_ptr<float>(),
-                                 (uint64_t)y.stride(0), g.data_ptr<float>(), (uint64_t)N,
-                                 dW.data_ptr<float>(), (uint64_t)N),
-                "nts_hip_gemm_f32(tn)");
-    }
+    const int64_t F = table.size(1), N = W.size(1), s = sg->src_size, v = sg->v_size;
+    const int dev = cs->device();
+    hipStream_t st = (hipStream_t)cs->stream();
+    NtsVar dH = torch::empty({std::max<int64_t>(s, 1), N}, f32_opts(dev));
+    if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
+    hip_check(nts_hip_spmm_csr_bwd_masked(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(),
+                                          nullptr, (uint32_t)s, g.data_ptr<float>(), (uint64_t)N,
+                                          X1.data_ptr<float>(), (uint64_t)N,
+                                          (float)ctx->saved_data["scale"].toDouble(), (uint32_t)N,
+                                          dH.data_ptr<float>(), (uint64_t)N),
+              "nts_hip_spmm_csr_bwd_masked");
+    if (prof)
+      prof->end(KernelProfiler::BOTTOM_BWD, st,
+                8.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
+    NtsVar dW = torch::empty({F, N}, W.options());
+    if (prof) prof->begin(KernelProfiler::GATHER_GEMM_TN, st);
+    hip_check(nts_hip_gemm_tn_gather_f32(cs->ctx(), (int)F, (int)N, (int)s, table.data_ptr<float>(),
+                                         (uint64_t)table.stride(0), sg->dev_src(),
+                                         dH.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
+                                         (uint64_t)N),
+              "nts_hip_gemm_tn_gather_f32");
+    if (prof) prof->end(KernelProfiler::GATHER_GEMM_TN, st, 2.0 * (double)s * F * N);
     return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
@@ -826,22 +859,65 @@ NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
                                reinterpret_cast<int64_t>(cs));
 }
 
-bool hip_agg_linear_supported(int64_t F, int64_t N) {
-  // mirrors the argument checks of nts_hip_spmm_csc_fwd_linear: the LDS tile
-  // pitch (F rounded up to 4, then to 2 mod 32) <= 640, N <= 128
-  const int64_t k4 = (F + 3) / 4 * 4, ldp = k4 + (2 + 32 - k4 % 32) % 32;
-  return F >= 1 && N >= 1 && N <= 128 && ldp <= 640;
+NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,
+                            uint64_t seed, uint64_t offset, NtsStream* cs, KernelProfiler* prof,
+                            float* h_out) {
+  return HipBottomTFFn::apply(table, W, reinterpret_cast<int64_t>(sg),
+                              reinterpret_cast<int64_t>(cs), p, (int64_t)seed, (int64_t)offset,
+                              reinterpret_cast<int64_t>(prof), reinterpret_cast<int64_t>(h_out));
 }
-NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg,
-                      NtsStream* cs) {
-  return HipAggLinearFn::apply(table, W, y, reinterpret_cast<int64_t>(sg),
-                               reinterpret_cast<int64_t>(cs), 0.0, (int64_t)0, (int64_t)0, false);
+
+// ---------------------------------------------------------------------------
+KernelProfiler::~KernelProfiler() {
+  for (auto& e : pool_) {
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
 }
-NtsVar hip_agg_linear_act(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg, double p,
-                          uint64_t seed, uint64_t offset, NtsStream* cs) {
-  return HipAggLinearFn::apply(table, W, y, reinterpret_cast<int64_t>(sg),
-                               reinterpret_cast<int64_t>(cs), p, (int64_t)seed, (int64_t)offset,
-                               true);
+const char* KernelProfiler::name(int id) {
+  static const char* n[kCount] = {"bottom_aggregation", "gather_gemm", "gather_gemm_tn",
+                                  "bottom_backward"};
+  return n[id];
+}
+void KernelProfiler::begin(Id id, hipStream_t st) {
+  if (open_[id] >= 0) return;  // nested begin: keep the outer interval
+  if (used_ >= 4096) resolve();
+  if (used_ == pool_.size()) {
+    Slot sl;
+    hip_rt(hipEventCreate(&sl.a), "hipEventCreate");
+    hip_rt(hipEventCreate(&sl.b), "hipEventCreate");
+    pool_.push_back(sl);
+  }
+  Slot& sl = pool_[used_];
+  sl.id = id;
+  sl.units = 0;
+  hip_rt(hipEventRecord(sl.a, st), "hipEventRecord");
+  open_[id] = (int)used_++;
+}
+void KernelProfiler::end(Id id, hipStream_t st, double units) {
+  const int k = open_[id];
+  if (k < 0) return;
+  hip_rt(hipEventRecord(pool_[k].b, st), "hipEventRecord");
+  pool_[k].units = units;
+  open_[id] = -1;
+}
+void KernelProfiler::resolve() {
+  for (size_t i = 0; i < used_; ++i) {
+    Slot& sl = pool_[i];
+    if (open_[sl.id] == (int)i) continue;  // never closed (exception): drop it
+    hip_rt(hipEventSynchronize(sl.b), "hipEventSynchronize");
+    float ms = 0;
+    hip_rt(hipEventElapsedTime(&ms, sl.a, sl.b), "hipEventElapsedTime");
+    stat[sl.id].ms += ms;
+    stat[sl.id].units += sl.units;
+    stat[sl.id].calls += 1;
+  }
+  used_ = 0;
+  for (int& o : open_) o = -1;
+}
+void KernelProfiler::reset() {
+  resolve();
+  for (auto& x : stat) x = Stat();
 }
 
 // GAT layer on a merged src/dst sampled block (GAT_SAMPLE_ALL_GPU's chain,

@@ -50,8 +50,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     F = Fp;
   }
   if (cfg.cache_rate >= 0.0) {
-    TORCH_CHECK(cfg.cache_rate < 1.0 || cfg.cache_rate == 1.0, "cache_rate must be in [0, 1]");
-    TORCH_CHECK(!cfg.fuse_linear, "the feature cache is not supported with fuse_linear");
+    TORCH_CHECK(cfg.cache_rate <= 1.0, "cache_rate must be in [0, 1]");
     const uint64_t V = graph->global_vertices;
     const uint64_t n_cache = std::min<uint64_t>(V, (uint64_t)(cfg.cache_rate * (double)V));
     fcache = std::make_unique<FeatureCache>(*cs, *graph, F, n_cache);
@@ -62,14 +61,22 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     std::shuffle(train_nids.begin(), train_nids.end(), gen);
   }
   const int L = (int)cfg.fanout.size();
+  // Bottom layer order: transform first when the first layer
+  // narrows the rows — the aggregation then gathers F_out-wide rows of X W
+  // (a table that stays in the Infinity Cache) instead of F_in-wide feature
+  // rows, at the price of a GEMM over the src rows instead of the dst rows.
+  const bool tf_ok = L >= 2 && !cfg.gat && !fcache && cfg.hip_gemm && cfg.fuse_activation;
+  if (cfg.transform_first == 1)
+    TORCH_CHECK(tf_ok, "transform_first needs >= 2 layers, the MFMA GEMMs with the fused "
+                       "activation, no GAT and no feature cache");
+  tf_ = tf_ok && (cfg.transform_first == 1 ||
+                  (cfg.transform_first < 0 && cfg.layer_size[0] > cfg.layer_size[1]));
   // CSR transposes only where a graph-op backward runs (every hop but the
-  // outermost, whose backward the context skips)
+  // outermost, whose backward the context skips — unless the bottom layer is
+  // transform-first: its aggregation then has a backward, dH = A^T dZ)
   std::vector<bool> csr(L, cfg.deterministic_backward);
-  csr[L - 1] = false;
-  if (cfg.gat) {  // every layer's backward runs over its CSR; dsts merged into the frontier
-    csr.assign(L, true);
-    TORCH_CHECK(!cfg.fuse_linear, "GAT: no fused bottom aggregation + GEMM");  // early_aggregate ignored
-  }
+  csr[L - 1] = tf_;
+  if (cfg.gat) csr.assign(L, true);  // every layer's backward runs over its CSR
   // Pipelined: three sampler slots.  Batch k+1 is sampled into the slot of
   // batch k-2, whose training finished before batch k-1's began, so the
   // sampling stream never waits on an unfinished event when its kernels are
@@ -99,7 +106,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // feature table only (not on the weights), so it is issued right behind the
   // sampling, on the sampling stream: with the pipeline it runs while the
   // previous batch trains (HBM-bound gather next to MFMA-bound GEMMs).
-  early_ = cfg.early_aggregate && cfg.fused_gather && !cfg.gat;
+  early_ = cfg.early_aggregate && cfg.fused_gather && !cfg.gat && !tf_;
   for (int i = 0; i < nslots_; ++i) {
     TORCH_CHECK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming) == hipSuccess,
                 "hipEventCreate");
@@ -124,10 +131,6 @@ GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
       fprintf(stderr, "[timeline] %s %9.1f us\n", tl_[i].first, ms * 1e3);
     }
     for (auto& e : tl_) (void)hipEventDestroy(e.second);
-  }
-  for (auto& e : ev_pool_) {
-    (void)hipEventDestroy(e.first);
-    (void)hipEventDestroy(e.second);
   }
   for (auto* e : ready_)
     if (e) (void)hipEventDestroy(e);
@@ -161,12 +164,7 @@ void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
     auto guard = st.guard();
     const int L = (int)P.size();
     sampCSC* s = sampler->ssgs[slot]->sampled_sgs[L - 1];
-    std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
-    if (cfg.profile) {
-      if (ev_pending_ >= 4096) resolve_profile();
-      evp = &next_events();
-      (void)hipEventRecord(evp->first, (hipStream_t)st.stream());
-    }
+    if (cfg.profile) prof.begin(KernelProfiler::BOTTOM_AGG, (hipStream_t)st.stream());
     NtsVar& y = pre_y_[slot];
     if (fcache)
       fcache->aggregate(st.ctx(), s, dptr<uint32_t>(s->sizes), s->v_cap,
@@ -178,7 +176,8 @@ void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
                                      (uint64_t)F.stride(0), s->dev_src(), (uint32_t)F.size(1),
                                      y.data_ptr<float>(), (uint64_t)y.stride(0)),
                 "nts_hip_spmm_csc_fwd(early)");
-    if (evp) (void)hipEventRecord(evp->second, (hipStream_t)st.stream());
+    // bytes are added when the batch's sizes are known (train_batch)
+    if (cfg.profile) prof.end(KernelProfiler::BOTTOM_AGG, (hipStream_t)st.stream(), 0.0);
   }
   TORCH_CHECK(hipEventRecord(ready_[slot], (hipStream_t)st.stream()) == hipSuccess,
               "hipEventRecord");
@@ -187,37 +186,11 @@ void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
 
 // compulsory bytes of the bottom aggregation: distinct src rows once, index +
 // weight per edge, offsets, output rows (+ source map when fused)  
-void GCN_SAMPLE_ALLGPU_impl::account_bottom(SampledSubgraph* sg, bool fused_map) {
+double GCN_SAMPLE_ALLGPU_impl::bottom_bytes(SampledSubgraph* sg, bool fused_map) const {
   sampCSC* s = sg->sampled_sgs[sg->layers - 1];
-  const double Fd = (double)F.size(1);
-  agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
-               Fd * 4.0 * s->v_size + (fused_map ? 4.0 * s->src_size : 0.0);
-  agg_calls += 1;
-}
-
-std::pair<hipEvent_t, hipEvent_t>& GCN_SAMPLE_ALLGPU_impl::next_events() {
-  if (ev_pending_ == ev_pool_.size()) {
-    hipEvent_t a, b;
-    TORCH_CHECK(hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess,
-                "hipEventCreate");
-    ev_pool_.push_back({a, b});
-  }
-  return ev_pool_[ev_pending_++];
-}
-
-// Sum the bottom-aggregation kernel times recorded since the last call
-// (synchronises on the last event; call outside the timed loop).
-double GCN_SAMPLE_ALLGPU_impl::resolve_profile() {
-  if (ev_pending_ == 0) return agg_ms;
-  TORCH_CHECK(hipEventSynchronize(ev_pool_[ev_pending_ - 1].second) == hipSuccess,
-              "hipEventSynchronize");
-  for (size_t i = 0; i < ev_pending_; ++i) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, ev_pool_[i].first, ev_pool_[i].second);
-    agg_ms += ms;
-  }
-  ev_pending_ = 0;
-  return agg_ms;
+  const double Fd = (double)(fcache ? fcache->F : F.size(1));
+  return Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
+         Fd * 4.0 * s->v_size + (fused_map ? 4.0 * s->src_size : 0.0);
 }
 
 void GCN_SAMPLE_ALLGPU_impl::init_nn() {
@@ -276,7 +249,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
   const int L = (int)P.size();
   std::vector<NtsVar> acts;
   NtsVar X0;
-  if (!cfg.fused_gather) {
+  if (!cfg.fused_gather && !tf_) {
     if (fcache)
       sampler->load_feature_gpu_cache(*cs, sg, X0, *fcache);
     else
@@ -299,55 +272,36 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
     const int hop = L - 1 - l;
     NtsVar Y;
     const bool bottom = (l == 0);
-    std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
-    if (bottom && cfg.profile) {
-      if (ev_pending_ >= 4096) resolve_profile();
-      evp = &next_events();
-      (void)hipEventRecord(evp->first, (hipStream_t)cs->stream());
-    }
-    const bool fuse = bottom && cfg.fused_gather && cfg.fuse_linear && cfg.hip_gemm &&
-                      hip_agg_linear_supported(F.size(1), P[0]->W.size(1));
-    if (fuse) {
-      // graph op + Parameter::forward of the first layer in one kernel; the
-      // bottom graph op has no backward (core/ntsContext.hpp:443-444), so the
-      // pair is recorded as one NN op whose input is the feature table
+    if (bottom && tf_) {  // transform-first: H = X[src] W, X1 = act(A H) (one NN op)
       sampCSC* s = sg->sampled_sgs[hop];
-      Y = row_padded_empty((int64_t)s->v_size, F.size(1), graph->device);
-      const bool act = l < L - 1 && cfg.fuse_activation;  // hidden layer: dropout(relu)
       const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
-      NtsVar Z = act ? hip_agg_linear_act(F, P[0]->W, Y, s, p,
-                                          (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1,
-                                          dropout_calls_++, cs.get())
-                     : hip_agg_linear(F, P[0]->W, Y, s, cs.get());
-      if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
-      const double Fd = (double)F.size(1);
-      agg_bytes += Fd * 4.0 * s->src_size + 8.0 * s->e_size + 4.0 * (s->v_size + 1) +
-                   Fd * 4.0 * s->v_size + 4.0 * s->src_size +
-                   4.0 * (double)P[0]->W.size(1) * s->v_size;
-      agg_calls += 1;
-      NtsVar table = F;
+      NtsVar h;
+      if (keep) h = torch::empty({(int64_t)std::max<uint32_t>(s->src_size, 1), P[0]->W.size(1)},
+                                 f32_opts(graph->device));
+      const uint64_t off = dropout_calls_++;
       X = ctx.runVertexForward(
-          [&](NtsVar&) {
-            if (l == L - 1) return Z.log_softmax(1);
-            if (act) return Z;
-            return torch::dropout(torch::relu(Z), cfg.drop_rate, ctx.is_train());
+          [&](NtsVar& t) {
+            return hip_bottom_transform(t, P[0]->W, s, p,
+                                        (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1, off,
+                                        cs.get(), profiler(),
+                                        keep ? h.data_ptr<float>() : nullptr);
           },
-          table);
+          F);
       if (keep) {
-        acts.push_back(Y.detach());
+        acts.push_back(h.narrow(0, 0, (int64_t)s->src_size));
         acts.push_back(X.detach());
       }
       continue;
     }
+    if (bottom && cfg.profile) prof.begin(KernelProfiler::BOTTOM_AGG, (hipStream_t)cs->stream());
     if (bottom && cfg.fused_gather)
       Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true,
                                                         fcache.get());
     else
       Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(X, sg, graph.get(), hop, cs.get(), false);
-    if (bottom) {
-      account_bottom(sg, cfg.fused_gather);
-      if (evp) (void)hipEventRecord(evp->second, (hipStream_t)cs->stream());
-    }
+    if (bottom && cfg.profile)
+      prof.end(KernelProfiler::BOTTOM_AGG, (hipStream_t)cs->stream(),
+               bottom_bytes(sg, cfg.fused_gather));
     if (loss_target && l == L - 1)  // vertexForward + Loss of the last layer, fused
       X = ctx.runVertexForward(
           [&](NtsVar& a) { return hip_linear_xent(a, P[l]->W, *loss_target, cs.get()); }, Y);
@@ -387,7 +341,7 @@ void GCN_SAMPLE_ALLGPU_impl::Loss(NtsVar& left, NtsVar& right) {
 void GCN_SAMPLE_ALLGPU_impl::Update() {
   // GCN_SAMPLE_ALL_MULTI::Update (toolkits/GCN_SAMPLE_ALL_MULTI.hpp:367-377):
   // SUM all-reduce of every W.grad — one fused RCCL call over a flat bucket.
-  if (comm && comm->nranks > 1) {
+  if (comm) {  // also at one rank: the same bucket, all-reduce and unpack run
     torch::NoGradGuard ng;
     int64_t off = 0;
     for (auto* p : P) {
@@ -457,7 +411,7 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   mark("T<", *cs);
   sampler->load_label_gpu(*cs, sg, target, L_GT);
   ctx.train();
-  if (early_) account_bottom(sg, true);
+  if (early_ && cfg.profile) prof.add_units(KernelProfiler::BOTTOM_AGG, bottom_bytes(sg, true));
   const int L = (int)P.size();
   if (cfg.gat) {  // GAT_SAMPLE_ALL_GPU::Loss + loss.backward() (toolkits/GAT_SAMPLE_ALL_GPU.hpp:393-399)
     auto acts = forward_gat(sg);
@@ -541,10 +495,53 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<Verte
 }
 
 void GCN_SAMPLE_ALLGPU_impl::reset_stats() {
-  resolve_profile();
-  sample_time = train_time = agg_ms = agg_bytes = 0;
+  prof.reset();
+  sample_time = train_time = 0;
   batch_edges = 0;
-  batches = agg_calls = 0;
+  batches = 0;
+}
+
+SamplerRate sampler_throughput(std::shared_ptr<FullyRepGraph> g, const std::vector<VertexId>& seeds,
+                               int batch_size, const std::vector<int>& fanout, WeightType w,
+                               int rng_mode, int n_batches, const std::vector<bool>& csr_layers) {
+  constexpr int kS = 3;
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+  NtsStream st(g->device, nullptr, 2000);
+  auto guard = st.guard();
+  const int L = (int)fanout.size();
+  FastSampler s(g, seeds, L, batch_size, fanout, kS, csr_layers, w != WeightType::None, false);
+  s.rng_mode = rng_mode;
+  uint64_t items = g->global_vertices;
+  for (auto* x : s.ssg->sampled_sgs) items = std::max<uint64_t>({items, x->e_cap, x->v_cap});
+  hip_check(nts_hip_ctx_reserve(st.ctx(), g->global_vertices, items), "nts_hip_ctx_reserve");
+  SamplerRate r;
+  auto run = [&](int n, bool count) {
+    int pending[kS] = {0, 0, 0};
+    for (int i = 0; i < n + kS; ++i) {
+      const int slot = i % kS;
+      if (pending[slot]) {
+        SampledSubgraph* sg = s.finish_gpu_sample(slot);
+        TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)st.stream()) == hipSuccess,
+                    "hipEventRecord");
+        pending[slot] = 0;
+        if (count) {
+          for (auto* x : sg->sampled_sgs) r.edges += x->e_size;
+          ++r.batches;
+        }
+      }
+      if (i >= n) continue;
+      if (!s.sample_not_finished()) s.restart();
+      s.issue_gpu_sample(batch_size, slot, st, w);
+      pending[slot] = 1;
+    }
+  };
+  run(std::min(n_batches, 4), false);  // warm-up (first-touch, code objects)
+  st.synchronize();
+  const auto t0 = std::chrono::steady_clock::now();
+  run(n_batches, true);
+  st.synchronize();
+  r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
 }
 
 }  // namespace nts

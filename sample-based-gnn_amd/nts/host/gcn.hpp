@@ -24,9 +24,12 @@ struct GCNConfig {
   bool fuse_loss = true;              // training: output layer + log_softmax x2 + nll in 2 kernels
   bool sampler_priority = true;       // pipelined sampler on a high-priority stream
   int sampler_cus = 0;
-  bool pad_features = true;           // copy wide feature tables to a 128-byte row pitch                // > 0: the sampler stream owns this many CUs, training the rest
+  bool pad_features = true;           // copy wide feature tables to a 128-byte row pitch
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
-  bool fuse_linear = false;           // bottom layer: gather + aggregation + GEMM in one kernel
+  // bottom layer order: 1 = transform first, A (X W) (rows narrowed before the
+  // aggregation), 0 = aggregate first, (A X) W (the reference's order),
+  // -1 = transform first iff the first layer narrows (F_in > F_out)
+  int transform_first = -1;
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
   // CACHE_RATE in [0, 1): the feature table moves to pinned host memory and
@@ -35,6 +38,19 @@ struct GCNConfig {
   double cache_rate = -1.0;
   int64_t seed = 2000;
 };
+
+// Sampler-only throughput of the GPU sampler (SURVEY §8d "sampler-only"
+// sampled-edges/s): FastSampler::sample_gpu_fast over `n_batches` batches of
+// `seeds` on its own stream, three slots in flight (issue / finish as the
+// pipelined driver does), nothing else on the device.  csr_layers as the
+// training driver builds them.
+struct SamplerRate {
+  double seconds = 0;
+  uint64_t edges = 0, batches = 0;
+};
+SamplerRate sampler_throughput(std::shared_ptr<FullyRepGraph> g, const std::vector<VertexId>& seeds,
+                               int batch_size, const std::vector<int>& fanout, WeightType w,
+                               int rng_mode, int n_batches, const std::vector<bool>& csr_layers);
 
 class GCN_SAMPLE_ALLGPU_impl {
  public:
@@ -55,7 +71,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   void set_weights(const std::vector<NtsVar>& ws);
   std::vector<NtsVar> weights() const;
   void reset_stats();
-  double resolve_profile();
+  void resolve_profile() { prof.resolve(); }
 
   std::shared_ptr<FullyRepGraph> graph;
   NtsVar F, L_GT, target, loss, grad_bucket;
@@ -68,8 +84,10 @@ class GCN_SAMPLE_ALLGPU_impl {
   std::vector<Parameter*> P;
   ctx::NtsContext ctx;
   // statistics
-  double sample_time = 0, train_time = 0, agg_ms = 0, agg_bytes = 0;
-  uint64_t batch_edges = 0, batches = 0, agg_calls = 0;
+  double sample_time = 0, train_time = 0;
+  uint64_t batch_edges = 0, batches = 0;
+  KernelProfiler prof;  // device time of the bottom-layer kernels (cfg.profile)
+  bool transform_first() const { return tf_; }
 
  private:
   NtsVar vertexForward(int l, NtsVar& a);
@@ -79,14 +97,14 @@ class GCN_SAMPLE_ALLGPU_impl {
   void issue(int slot, NtsStream& st);
   // GAT_SAMPLE_ALL_GPU::Forward (toolkits/GAT_SAMPLE_ALL_GPU.hpp:308-391)
   std::vector<NtsVar> forward_gat(SampledSubgraph* sg);
-  void account_bottom(SampledSubgraph* sg, bool fused_map);
+  double bottom_bytes(SampledSubgraph* sg, bool fused_map) const;
+  KernelProfiler* profiler() { return cfg.profile ? &prof : nullptr; }
   void Loss(NtsVar& left, NtsVar& right);
   void Update();
   std::pair<hipEvent_t, hipEvent_t>& next_events();
   void mark(const char* what, NtsStream& st);
   std::vector<std::pair<const char*, hipEvent_t>> tl_;  // NTS_TIMELINE events
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool_;
-  size_t ev_pending_ = 0;
+  bool tf_ = false;  // transform-first bottom layer (cfg.transform_first)
   // early aggregation: per sampler slot, the bottom graph op's output and the
   // event after which it (and the slot's sampled graph) is ready
   static constexpr int kSlots = 3;  // sampler slots when pipelined (see the constructor)

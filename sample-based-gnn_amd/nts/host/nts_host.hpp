@@ -29,7 +29,9 @@ typedef uint32_t VertexId;
 typedef float ValueType;
 typedef torch::Tensor NtsVar;
 
-enum class WeightType { Sum, Mean, None };
+// Sum / Mean / None: core/ntsFastSampler.hpp:27.  MeanSampled: the reference GPU
+// kernel get_mean_weight's formula (NTS_WEIGHT_MEAN_SAMPLED, nts_hip.h).
+enum class WeightType { Sum, Mean, None, MeanSampled };
 
 namespace nts {
 
@@ -374,17 +376,46 @@ NtsVar row_padded_empty(int64_t rows, int64_t F, int device);
 NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
                       NtsStream* cs);
 
-// Bottom layer fused: Y = A X (into the caller's `y`, bit-identical to the
-// graph op) and Z = Y W in one kernel (nts_hip_spmm_csc_fwd_linear); autograd
-// returns Z with dW = Y^T dZ.  X is the global feature table, rows fetched
-// through the layer's `source` (fused load_feature_gpu).
-NtsVar hip_agg_linear(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg,
-                      NtsStream* cs);
-// whether the fused kernel supports this shape (feature rows fit the LDS tile, out <= 128)
-bool hip_agg_linear_supported(int64_t feature_size, int64_t out_size);
-// ... and with vertexForward's dropout(relu(.)) fused (returns the activation)
-NtsVar hip_agg_linear_act(const NtsVar& table, const NtsVar& W, NtsVar& y, sampCSC* sg, double p,
-                          uint64_t seed, uint64_t offset, NtsStream* cs);
+// Device time of selected kernels on the stream that launches them (HIP
+// events; resolve() synchronises — call outside timed regions).  `units` are
+// the algorithmic bytes (aggregations) or flops (GEMMs) of one launch.
+class KernelProfiler {
+ public:
+  enum Id { BOTTOM_AGG = 0, GATHER_GEMM, GATHER_GEMM_TN, BOTTOM_BWD, kCount };
+  struct Stat {
+    double ms = 0, units = 0;
+    uint64_t calls = 0;
+  };
+  KernelProfiler() { for (int& o : open_) o = -1; }
+  ~KernelProfiler();
+  KernelProfiler(const KernelProfiler&) = delete;
+  KernelProfiler& operator=(const KernelProfiler&) = delete;
+  void begin(Id id, hipStream_t st);
+  void end(Id id, hipStream_t st, double units);
+  void resolve();
+  void reset();
+  void add_units(Id id, double units) { stat[id].units += units; }
+  static const char* name(int id);
+  Stat stat[kCount];
+
+ private:
+  struct Slot {
+    Id id = BOTTOM_AGG;
+    hipEvent_t a = nullptr, b = nullptr;
+    double units = 0;
+  };
+  std::vector<Slot> pool_;
+  size_t used_ = 0;
+  int open_[kCount];
+};
+
+// Transform-first bottom layer (nts_hip.h): X1 = dropout(relu(A (X[source] W)))
+// on the layer's sampled block `sg` (its CSR is needed for the backward);
+// autograd returns dW = X[source]^T (A^T (dX1 ⊙ mask)).  h_out != NULL: H =
+// X[source] W is written there ([src_size, F_out], eval / tests).
+NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,
+                            uint64_t seed, uint64_t offset, NtsStream* cs, KernelProfiler* prof,
+                            float* h_out = nullptr);
 
 struct Parameter {
   NtsVar W, M, V;

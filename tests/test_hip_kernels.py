@@ -168,7 +168,7 @@ def test_sampler_mt19937_div_mode(hip, cora):
 
 
 @pytest.mark.parametrize("case", ["cora", "random"])
-@pytest.mark.parametrize("weight_type", [0, 1, 2, 0x10, 0x11])  # 0x10: UP_DEGREE
+@pytest.mark.parametrize("weight_type", [0, 1, 2, 3, 0x10, 0x11, 0x13])  # 0x10: UP_DEGREE, 3: MEAN_SAMPLED
 def test_sampler_philox_matches_oracle(hip, cora, case, weight_type):
     V, src, dst = cora if case == "cora" else _random_graph(20000, 600000, 9)
     g = _graph(hip, V, src, dst)
@@ -388,56 +388,101 @@ def test_gemm_f32_mfma(hip, M, N, K, trans_a):
     assert torch.equal(C, C2)
 
 
-@pytest.mark.parametrize("F,N", [(602, 128), (602, 41), (128, 128), (41, 7), (1, 1), (100, 64),
-                                 (1433, 16)])
-@pytest.mark.parametrize("mapped", [True, False])
-def test_spmm_fwd_linear_fused(hip, cora, F, N, mapped):
-    """Fused bottom layer: Y bit-identical to the graph op (fuse_fwd, the
-    reference's aggregation order), Z = Y W on MFMA within fp32 GEMM tolerance."""
+@pytest.mark.parametrize("F", [1, 7, 41, 128, 256, 602])
+@pytest.mark.parametrize("p", [0.0, 0.5])
+def test_spmm_fwd_act_bitexact(hip, cora, F, p):
+    """Transform-first aggregation with vertexForward's activation in the
+    epilogue: dropout(relu(A x)) == the oracle's MiniBatchFuseOp sum followed by
+    the documented Philox keep mask (the GEMM epilogue's keys), bit for bit."""
     V, src, dst = cora
     col, rows = orc.build_csc(V, src, dst)
     out_d, in_d = orc.degrees(V, src, dst)
     o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
-    l0, l1 = o.sample(np.arange(0, V, 7, dtype=np.uint32))
-    rng = np.random.default_rng(F * 31 + N)
-    table = rng.standard_normal((V, F)).astype(np.float32)
-    X = orc.get_feature(l1["source"], table)
-    Y_ref = orc.fuse_fwd(l1, X, out_d, in_d)
+    l0, l1 = o.sample(np.arange(1, V, 9, dtype=np.uint32))
+    rng = np.random.default_rng(F + 100)
+    X = rng.standard_normal((l1["src_size"], F)).astype(np.float32)
+    Y = orc.fuse_fwd(l1, X, out_d, in_d)
     v = l1["v_size"]
-    co, ri, wf = _t(l1["column_offset"]), _t(l1["row_indices"]), _t(l1["edge_weight_forward"])
+    seed, offset = 0x0123_4567_89AB, 9
+    keep = _dropout_keep(v, F, p, seed, offset)
+    scale = np.float32(1.0 / (1.0 - p))
+    ref = np.where(keep & (Y > 0), Y * scale, np.float32(0)).astype(np.float32)
     vdev = torch.tensor([v], dtype=torch.int32, device=DEV)
-    W = _t(rng.standard_normal((F, N)).astype(np.float32))
     y = torch.full((v + 3, F), float("nan"), device=DEV)
-    z = torch.full((v + 3, N), float("nan"), device=DEV)
-    x = _t(table) if mapped else _t(X)
-    rm = _t(l1["source"]) if mapped else None
-    k4 = (F + 3) // 4 * 4
-    if k4 + (2 + 32 - k4 % 32) % 32 > 640:  # LDS tile of two blocks per CU
-        with pytest.raises(RuntimeError):
-            hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v + 3, x, W, z, y=y, row_map=rm)
-        return
-    hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v + 3, x, W, z, y=y, row_map=rm)
+    hip.spmm_csc_fwd_act(_t(l1["column_offset"]), _t(l1["row_indices"]),
+                         _t(l1["edge_weight_forward"]), vdev, v + 3, _t(X), y, p=p, seed=seed,
+                         offset=offset)
     torch.cuda.synchronize()
-    assert np.array_equal(y[:v].cpu().numpy(), Y_ref)
-    assert torch.isnan(y[v:]).all() and torch.isnan(z[v:]).all()
-    ref = torch.from_numpy(Y_ref).double() @ W.cpu().double()
-    tol = 2e-6 * F ** 0.5 + 1e-6
-    torch.testing.assert_close(z[:v].cpu().double(), ref, rtol=tol, atol=tol * 4)
-    # without Y
-    z2 = torch.empty((v, N), device=DEV)
-    hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v, x, W, z2, row_map=rm)
+    assert np.array_equal(y[:v].cpu().numpy(), ref)
+    assert torch.isnan(y[v:]).all()
+
+
+@pytest.mark.parametrize("F", [1, 7, 41, 128, 602])
+def test_spmm_csr_bwd_masked_bitexact(hip, cora, F):
+    """Its backward: A^T (G ⊙ [X > 0] * scale) over the CSR == the oracle's
+    dst-ordered MiniBatchFuseOp::backward of the masked gradient."""
+    V, src, dst = cora
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    _, l1 = o.sample(np.arange(2, V, 13, dtype=np.uint32))
+    rng = np.random.default_rng(F + 7)
+    v, s = l1["v_size"], l1["src_size"]
+    G = rng.standard_normal((v, F)).astype(np.float32)
+    Xa = np.maximum(rng.standard_normal((v, F)).astype(np.float32), 0) * np.float32(2)
+    dZ = np.where(Xa > 0, G * np.float32(2.0), np.float32(0)).astype(np.float32)
+    ref = orc.fuse_bwd(l1, dZ, out_d, in_d)
+    sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
+    gin = torch.full((s + 2, F), float("nan"), device=DEV)
+    hip.spmm_csr_bwd_masked(_t(l1["row_offset"]), _t(l1["column_indices"]),
+                            _t(l1["edge_weight_backward"]), sdev, s + 2, _t(G), _t(Xa), gin,
+                            scale=2.0)
     torch.cuda.synchronize()
-    assert torch.equal(z2, z[:v])
-    # relu + dropout epilogue: the mask of gemm_relu_dropout (same seed/offset keys)
-    p, seed, offset = 0.5, 0x1234_5678_9ABC, 5
-    za = torch.full((v, N), float("nan"), device=DEV)
-    hip.spmm_csc_fwd_linear(co, ri, wf, vdev, v, x, W, za, row_map=rm, activation=True, p=p,
-                            seed=seed, offset=offset)
+    assert np.array_equal(gin[:s].cpu().numpy(), ref)
+    assert torch.isnan(gin[s:]).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(3000, 128, 602), (2500, 64, 100), (500, 41, 100), (37, 7, 13)])
+def test_gemm_gather_rows(hip, M, N, K):
+    """C = table[rows] @ W with the rows gathered inside the GEMM: bit-identical
+    to the GEMM on the gathered copy, fp32-accurate vs fp64."""
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    V = 4 * M + 11
+    ld = (K + 31) // 32 * 32 if K >= 256 else K
+    table = torch.randn(V, ld, device=DEV, generator=g)[:, :K]
+    rows = torch.randperm(V, device=DEV, generator=g)[:M].to(torch.int32)
+    W = torch.randn(K, N, device=DEV, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    hip.gemm_gather(table, rows, W, C)
+    Xg = table[rows.long()].contiguous()
+    C2 = torch.empty(M, N, device=DEV)
+    hip.gemm(Xg, W, C2)
     torch.cuda.synchronize()
-    keep = torch.from_numpy(_dropout_keep(v, N, p, seed, offset))
-    refa = torch.where(keep & (ref > 0), ref * 2.0, torch.zeros_like(ref))
-    near0 = ref.abs() < 1e-4 * F ** 0.5
-    torch.testing.assert_close(za.cpu().double()[~near0], refa[~near0], rtol=tol, atol=tol * 8)
+    assert torch.equal(C, C2)
+    tol = 2e-6 * K ** 0.5 + 1e-6
+    torch.testing.assert_close(C.double(), Xg.double() @ W.double(), rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize("M,N,K", [(602, 128, 5000), (100, 256, 3000), (41, 7, 300), (602, 128, 17)])
+def test_gemm_tn_gather_rows(hip, M, N, K):
+    """dW = table[rows]^T @ G (the transform-first weight gradient): bit-identical
+    to the TN GEMM on the gathered copy, fp32-accurate vs fp64."""
+    g = torch.Generator(device=DEV).manual_seed(M * N + K)
+    V = 3 * K + 5
+    ld = (M + 31) // 32 * 32 if M >= 256 else M
+    table = torch.randn(V, ld, device=DEV, generator=g)[:, :M]
+    rows = torch.randint(0, V, (K,), device=DEV, generator=g).to(torch.int32)
+    G = torch.randn(K, N, device=DEV, generator=g)
+    C = torch.empty(M, N, device=DEV)
+    hip.gemm_tn_gather(table, rows, G, C)
+    Xg = table[rows.long()].contiguous()
+    C2 = torch.empty(M, N, device=DEV)
+    hip.gemm(Xg, G, C2, trans_a=True)
+    torch.cuda.synchronize()
+    tol = 2e-6 * K ** 0.5 + 1e-6
+    torch.testing.assert_close(C.double(), Xg.double().t() @ G.double(), rtol=tol, atol=tol * 4)
+    if ld == M:  # same operand layout -> same kernel and k order
+        assert torch.equal(C, C2)
 
 
 def _philox4x32_10(c, k):

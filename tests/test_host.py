@@ -57,19 +57,24 @@ def test_fast_sampler_matches_oracle(E, graph):
     assert bs == 3
 
 
-def _driver(E, graph, F, C, layers, fanout, batch, drop=0.0, seed=2000, **kw):
+def _driver(E, graph, F, C, layers, fanout, batch, drop=0.0, seed=2000, comm=None, **kw):
     from nts import host, synthetic
     feat = synthetic.features(graph["V"], F, device=DEV)
     labels, masks = synthetic.labels_masks(graph["V"], C, device=DEV)
     train = torch.nonzero(masks == 0).flatten().to(torch.int32).cpu()
     cfg = host.gcn_config(layers, fanout, batch, learn_rate=0.01, drop_rate=drop, seed=seed,
                           shuffle=False, **kw)
-    return E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg), feat, labels, train
+    drv = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg, comm)
+    return drv, feat, labels, train
 
 
-@pytest.mark.parametrize("F", [602, 128])
-def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F):
-    drv, feat, labels, _ = _driver(E, graph, F, 41, [F, 64, 41], [25, 10], 256)
+@pytest.mark.parametrize("F,tf", [(602, 0), (128, 0), (602, 1), (128, 1), (48, 1)])
+def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F, tf):
+    """tf = 0: aggregate first, the reference's order (Y0 bit-exact);
+    tf = 1: transform first, A (X W0): H = X W0 and every later activation
+    within the north-star's 1e-4 of the GCN_CPU_SAMPLE chain."""
+    drv, feat, labels, _ = _driver(E, graph, F, 41, [F, 64, 41], [25, 10], 256, transform_first=tf)
+    assert drv.transform_first == bool(tf)
     seeds = torch.arange(7, 7 + 256, dtype=torch.int32)
     acts = drv.forward_eval(seeds, 3)
     W = [w.cpu() for w in drv.weights()]
@@ -82,7 +87,11 @@ def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F):
     X1 = torch.relu(torch.from_numpy(Y0) @ W[0])
     Y1 = orc.fuse_fwd(l0, X1.numpy(), graph["od"], graph["idg"])
     X2 = (torch.from_numpy(Y1) @ W[1]).log_softmax(1)
-    assert np.array_equal(acts[0].cpu().numpy(), Y0)  # fused gather+aggregation: bit-exact
+    if tf:
+        H = torch.from_numpy(X0).double() @ W[0].double()
+        torch.testing.assert_close(acts[0].cpu().double(), H, rtol=1e-5, atol=1e-5)
+    else:
+        assert np.array_equal(acts[0].cpu().numpy(), Y0)  # fused gather+aggregation: bit-exact
     torch.testing.assert_close(acts[1].cpu(), X1, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(acts[2].cpu(), torch.from_numpy(Y1), rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(acts[3].cpu(), X2, rtol=1e-4, atol=1e-4)
@@ -90,29 +99,62 @@ def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F):
 
 def test_unfused_gather_path_is_identical(E, graph):
     from nts import host
-    drv, feat, labels, train = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 128, fuse_linear=True)
-    cfg = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fused_gather=False, shuffle=False)
+    drv, feat, labels, train = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 128, transform_first=0)
+    cfg = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fused_gather=False,
+                          shuffle=False, transform_first=0)
     drv2 = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg)
     drv2.set_weights(drv.weights())
-    cfg3 = host.gcn_config([96, 32, 7], [10, 5], 128, drop_rate=0.0, fuse_linear=False, shuffle=False)
-    drv3 = E.GCN_SAMPLE_ALLGPU_impl(graph["G"], feat, labels, train, cfg3)
-    drv3.set_weights(drv.weights())
     seeds = torch.arange(100, 228, dtype=torch.int32)
-    a = drv.forward_eval(seeds, 0)   # gather + aggregation + first GEMM in one kernel
-    b = drv2.forward_eval(seeds, 0)  # load_feature_gpu, graph op, HipLinear
-    c = drv3.forward_eval(seeds, 0)  # gather fused into the graph op, HipLinear
-    for x, y in zip(b, c):
+    a = drv.forward_eval(seeds, 0)   # gather fused into the graph op
+    b = drv2.forward_eval(seeds, 0)  # load_feature_gpu, then the graph op
+    for x, y in zip(a, b):
         assert torch.equal(x, y)
-    assert torch.equal(a[0], b[0])  # aggregation itself is identical
-    for x, y in zip(a[1:], b[1:]):  # GEMM summation order differs
-        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-5)
 
 
-def test_training_step_matches_oracle_step(E, graph):
+@pytest.mark.parametrize("drop", [0.0, 0.5])
+def test_transform_first_trains_like_aggregate_first(E, graph, drop):
+    """A (X W) vs (A X) W: the same sampled batches and dropout masks (the
+    aggregation epilogue uses the GEMM epilogue's keys), so one training step
+    agrees to fp32 summation order (loss, weights after Adam)."""
+    a, *_ = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 200, drop=drop, transform_first=1)
+    b, *_ = _driver(E, graph, 96, 7, [96, 32, 7], [10, 5], 200, drop=drop, transform_first=0)
+    assert a.transform_first and not b.transform_first
+    b.set_weights(a.weights())
+    a.train_batch()
+    b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    torch.testing.assert_close(a.loss, b.loss, rtol=1e-5, atol=1e-6)
+    for x, y in zip(a.weights(), b.weights()):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-4)
+
+
+def test_one_rank_communicator_is_identical(E, graph):
+    """The C++ data-parallel path on one GPU: initial ncclBroadcast of the
+    weights, the fused gradient bucket (pack -> ncclAllReduce SUM -> unpack)
+    every step (GCN_SAMPLE_ALL_MULTI::Update, toolkits/GCN_SAMPLE_ALL_MULTI.hpp:367-377).
+    At one rank the sum is the identity: bit-identical weights to comm=None."""
+    comm = E.Communicator(1, 0, E.Communicator.unique_id(), 0)
+    assert comm.nranks == 1
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5, comm=comm)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5)
+    for _ in range(3):
+        a.train_batch()
+        b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("tf", [0, 1])
+def test_training_step_matches_oracle_step(E, graph, tf):
     """One train_batch: sample -> forward -> NLL -> self_backward (graph-op
-    backward through the CSR) -> learn_local_with_decay_Adam, vs the oracle."""
+    backward through the CSR) -> learn_local_with_decay_Adam, vs the oracle
+    (tf = 1: the bottom layer transform-first, its backward through the bottom
+    layer's CSR and the row-gathered weight-gradient GEMM)."""
     F, C, B = 64, 7, 200
-    drv, feat, labels, train = _driver(E, graph, F, C, [F, 32, C], [10, 5], B)
+    drv, feat, labels, train = _driver(E, graph, F, C, [F, 32, C], [10, 5], B, transform_first=tf)
     W0 = [w.cpu().clone() for w in drv.weights()]
     drv.train_batch()
     drv.synchronize()
@@ -159,8 +201,10 @@ def test_training_is_deterministic_and_learns(E, graph, drop):
 def test_early_aggregation_is_identical(E, graph):
     """Bottom graph op issued behind the sampler (early_aggregate) vs inside the
     forward: same sampled graphs, same kernels -> identical weights."""
-    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, early_aggregate=True)
-    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, early_aggregate=False)
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, early_aggregate=True,
+                    transform_first=0)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, early_aggregate=False,
+                    transform_first=0)
     for _ in range(3):
         a.train_batch()
         b.train_batch()
@@ -173,7 +217,8 @@ def test_early_aggregation_is_identical(E, graph):
 def test_fused_activation_matches_torch_ops(E, graph):
     """relu (+ dropout at p = 0) in the GEMM epilogue and its backward in the
     weight-gradient GEMM vs torch relu/dropout around the plain GEMM."""
-    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, fuse_activation=True)
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, fuse_activation=True,
+                    transform_first=0)
     b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, fuse_activation=False)
     for _ in range(3):
         a.train_batch()
@@ -191,7 +236,7 @@ def test_feature_cache_training_is_identical(E, graph, rate, early, fused):
     HBM (GS_SAMPLE_PD_CACHE placement, cache_rate) train to the same weights
     as the all-HBM table: the two-tier reads change where rows come from, not
     their values (fused graph op, early aggregation, and load_feature_gpu_cache)."""
-    kw = dict(early_aggregate=early, fused_gather=fused)
+    kw = dict(early_aggregate=early, fused_gather=fused, transform_first=0)
     a, *_ = _driver(E, graph, 602, 7, [602, 32, 7], [10, 5], 200, drop=0.5, **kw)
     b, *_ = _driver(E, graph, 602, 7, [602, 32, 7], [10, 5], 200, drop=0.5, cache_rate=rate, **kw)
     for _ in range(3):

@@ -312,3 +312,27 @@ def test_up_degree_weights_use_sampled_layer_degrees():
             if wt == orc.W_MEAN:
                 w = w / ind[dl].astype(np.float32)
             assert np.array_equal(ly["edge_weight_forward"], w)
+
+
+def test_mean_sampled_weights_divide_by_sampled_count():
+    """W_MEAN_SAMPLED restates the reference GPU kernel get_mean_weight
+    (cuda/ntsCUDATransferKernel.cuh:319-342): the Sum weight
+    1/(sqrtf(out[src]) sqrtf(in[dst])) over full-graph degrees, divided by the
+    dst's sampled edge count (edges_num = end - start)."""
+    src, dst = dataloader.read_edge_file(GOLDEN / "cora" / "cora.2708.edge.self")
+    V = 2708
+    col, rows = orc.build_csc(V, src, dst)
+    od, idg = orc.degrees(V, src, dst)
+    seeds = np.arange(3, V, 13, dtype=np.uint32)
+    o = orc.Sampler(col, rows, idg, od, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    for ly in o.sample(seeds, 0, orc.W_MEAN_SAMPLED):
+        co = ly["column_offset"].astype(np.int64)
+        cnt = np.diff(co)
+        dl = np.repeat(np.arange(cnt.size), cnt)
+        g_src = ly["source"][ly["row_indices"]]
+        g_dst = ly["destination"][dl]
+        # sqrtf of the (exactly representable) integer degree == float(double sqrt)
+        a = np.sqrt(od[g_src].astype(np.float32))
+        b = np.sqrt(idg[g_dst].astype(np.float32))
+        w = (np.float32(1) / (a * b)) / cnt[dl].astype(np.float32)
+        assert np.array_equal(ly["edge_weight_forward"], w)
