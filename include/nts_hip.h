@@ -35,7 +35,8 @@ extern "C" {
 #endif
 
 #define NTS_HIP_ABI_VERSION 3  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
-                                  3: transform-first entry points, fused agg+GEMM removed */
+                                  3: transform-first entry points, fused agg+GEMM removed,
+                                     accuracy counts in the fused loss */
 
 /* status codes */
 #define NTS_OK 0
@@ -285,6 +286,14 @@ int nts_hip_spmm_csr_bwd_masked(nts_hip_ctx *ctx, const uint32_t *row_offset,
                                 const uint32_t *s, uint32_t s_cap, const float *g_out,
                                 uint64_t ld_gout, const float *x_act, uint64_t ld_act, float scale,
                                 uint32_t feature_size, float *g_in, uint64_t ld_gin);
+/* The activation's backward alone: out = g ⊙ [x_act > 0] * scale ([rows x
+ * feature_size], each with its leading dimension) — what libtorch's relu and
+ * dropout backward compute for vertexForward (toolkits/GCN_SAMPLE_GPU.hpp:252-266),
+ * in one pass; followed by nts_hip_spmm_csr_bwd it equals
+ * nts_hip_spmm_csr_bwd_masked (same arithmetic per element). */
+int nts_hip_act_backward(nts_hip_ctx *ctx, uint32_t rows, uint32_t feature_size, const float *g,
+                         uint64_t ldg, const float *x_act, uint64_t ldx, float scale, float *out,
+                         uint64_t ldo);
 /* G_in[row_indices[e],:] += w[e] * G_out[d,:] with float atomics over the CSC
  * (g_in must be zeroed by the caller; summation order is not deterministic).
  * Replaces Push_From_Dst_To_Src_Spmm (cuda/ntsCUDAGraphOP.cu:621-770). */
@@ -374,9 +383,13 @@ int nts_hip_gemm_tn_masked_f32(nts_hip_ctx *ctx, int M, int N, int K, const floa
  * toolkits/GCN_SAMPLE_ALLGPU.hpp:247-252), log_softmax again + mean
  * nll_loss (Loss, :214-222).  Y [n x K] (ld ldy), W [K x C] row-major,
  * labels int64 [n] in [0, C), C <= 64.  Writes the scalar loss (device).
+ * correct != NULL: *correct += the rows whose argmax (first index of the
+ * largest log_softmax value) is the label — getCorrect
+ * (toolkits/GCN_SAMPLE_ALLGPU.hpp:166-172) accumulated on the device.
  * Replaces the libtorch matmul/log_softmax/nll_loss kernels of those lines. */
 int nts_hip_linear_xent_fwd(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int n, int K,
-                            const float *W, int C, const int64_t *labels, float *loss);
+                            const float *W, int C, const int64_t *labels, float *loss,
+                            uint32_t *correct);
 /* Its backward for an upstream gradient *grad_loss (device scalar):
  * dY [n x K] (ld K) and dW [K x C] (row-major), i.e. what libtorch's
  * autograd produces through nll_loss, both log_softmaxes and the matmul.
@@ -392,7 +405,7 @@ int nts_hip_linear_xent_bwd(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int 
  * nts_hip_linear_xent_bwd with *grad_loss == 1. */
 int nts_hip_linear_xent_train(nts_hip_ctx *ctx, const float *Y, uint64_t ldy, int n, int K,
                               const float *W, int C, const int64_t *labels, float *loss,
-                              float *dY, float *dW);
+                              float *dY, float *dW, uint32_t *correct);
 
 /* ---- optimiser ---------------------------------------------------------- */
 /* Fused Adam step on one parameter (n elements), element-wise identical to

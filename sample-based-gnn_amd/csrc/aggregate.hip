@@ -112,8 +112,137 @@ template <int VEC>
 __device__ __forceinline__ float& vcomp(typename VT<VEC>::T& v, int q) {
   return reinterpret_cast<float*>(&v)[q];
 }
+template <int VEC>
+__device__ __forceinline__ float vcomp(const typename VT<VEC>::T& v, int q) {
+  return reinterpret_cast<const float*>(&v)[q];
+}
 
-template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER, int MODE = kAggPlain>
+// acc[c] += sum over the edges [beg, end) in edge order of w[e] * row(e)[col],
+// col = c0 + sl + c * LPD (one LPD-lane group, see k_spmm_gather)
+template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER, int MODE>
+__device__ __forceinline__ void gather_edges(typename VT<VEC>::T (&acc)[NCH], uint32_t beg,
+                                             uint32_t end, uint32_t c0, int sl,
+                                             const uint32_t* __restrict__ idx,
+                                             const float* __restrict__ w,
+                                             const float* __restrict__ x, uint64_t ldx,
+                                             const uint32_t* __restrict__ map, uint32_t nv,
+                                             const Tier& tier, const AggExtra& ax) {
+  using V = VT<VEC>;
+  using T = typename V::T;
+  for (uint32_t cb = beg; cb < end; cb += LPD) {
+    const uint32_t ne = min(end - cb, (uint32_t)LPD);
+    uint32_t my_r = 0;
+    float my_w = 0.f;
+    if ((uint32_t)sl < ne) {  // streamed once: do not keep in cache
+      my_r = __builtin_nontemporal_load(idx + cb + sl);
+      my_w = w ? __builtin_nontemporal_load(w + cb + sl) : 1.0f;
+      const uint32_t loc = my_r;
+      if (MAP) my_r = map[my_r];
+      if (TIER) {
+        const uint32_t slot = tier.cmap[my_r];
+        my_r = slot != kNotCached ? slot : ((tier.host_local ? loc : my_r) | kHostBit);
+      }
+    }
+    for (uint32_t j0 = 0; j0 < ne; j0 += U) {
+      T xv[U][NCH];
+      T mv[MODE == kAggMask ? U : 1][MODE == kAggMask ? NCH : 1];
+      float ww[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int src = (int)(j0 + j) & (LPD - 1);
+        const uint32_t r = (uint32_t)__shfl((int)my_r, src, LPD);
+        ww[j] = __shfl(my_w, src, LPD);
+        const bool ok = j0 + j < ne;
+        const T* xrow = reinterpret_cast<const T*>(
+            TIER && (r & kHostBit) ? tier.host + (uint64_t)(r & ~kHostBit) * tier.ldh
+                                   : x + (uint64_t)r * ldx);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = c0 + sl + c * LPD;
+          xv[j][c] = (ok && col < nv) ? xrow[col] : V::zero();
+        }
+        if constexpr (MODE == kAggMask) {
+          const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)r * ax.ldm);
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            const uint32_t col = c0 + sl + c * LPD;
+            mv[j][c] = (ok && col < nv) ? mrow[col] : V::zero();
+          }
+        }
+      }
+      if constexpr (MODE == kAggMask) {  // dZ = dX ⊙ [X > 0] · scale
+#pragma unroll
+        for (int j = 0; j < U; ++j)
+#pragma unroll
+          for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+              float& g = vcomp<VEC>(xv[j][c], q);
+              g = vcomp<VEC>(mv[j][c], q) > 0.f ? g * ax.scale : 0.f;
+            }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j0 + j < ne) {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
+        }
+    }
+  }
+}
+
+// epilogue of one output row: activation (kAggAct) and the store
+template <int VEC, int LPD, int NCH, int MODE>
+__device__ __forceinline__ void store_row(typename VT<VEC>::T (&acc)[NCH], uint32_t d, uint32_t c0,
+                                          int sl, uint32_t nv, uint32_t last_valid,
+                                          float* __restrict__ y, uint64_t ldy, const AggExtra& ax) {
+  using V = VT<VEC>;
+  using T = typename V::T;
+  if constexpr (MODE == kAggAct) {  // relu + inverted dropout, mask never stored
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const uint32_t f0 = (c0 + sl + c * LPD) * VEC;  // first float column
+#pragma unroll
+      for (int q2 = 0; q2 < (VEC + 1) / 2; ++q2) {
+        uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
+        if (ax.keep_threshold) rnd = dropout_words((uint64_t)d, f0 + 2 * q2, ax.seed, ax.offset);
+        const uint32_t wd = (d & 3) == 0 ? rnd.x : (d & 3) == 1 ? rnd.y : (d & 3) == 2 ? rnd.z : rnd.w;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (2 * q2 + h >= VEC) break;
+          const uint32_t col = f0 + 2 * q2 + h;
+          float& v = vcomp<VEC>(acc[c], 2 * q2 + h);
+          v = (dropout_bits(wd, col) >= ax.keep_threshold && v > 0.f) ? v * ax.scale : 0.f;
+        }
+      }
+    }
+  }
+  T* yrow = reinterpret_cast<T*>(y + (uint64_t)d * ldy);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {  // output rows are not re-read here: keep them
+    const uint32_t col = c0 + sl + c * LPD;  // out of the cache that serves x rows
+    if (col + 1 < nv || (col + 1 == nv && last_valid == (uint32_t)VEC)) {
+      V::st_nt(yrow + col, acc[c]);
+    } else if (col + 1 == nv) {  // partial last vector: only the valid floats
+      V::st_part(yrow + col, acc[c], last_valid);
+    }
+  }
+}
+
+// COOP (the CSR transposes, whose rows are as long as a source is popular —
+// hundreds of edges for the hubs of a power-law graph against ~6 on average):
+// a row longer than kLongRow(U) edges is not summed by its own lane group,
+// which would serialise ~len/U rounds of memory latency and set the whole
+// launch's time; the block's GPB groups each sum a contiguous GPB-th of its
+// edges (in edge order) and the partial sums are added in group order through
+// LDS.  Deterministic; rows up to kLongRow edges keep the serial edge order
+// (bit-identical to MiniBatchFuseOp::backward's), longer rows are summed as
+// GPB in-order pieces.  Needs one row per group (grid = ceil(n_cap / GPB)).
+template <int U>
+constexpr uint32_t kLongRow() { return 4 * U; }
+
+template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER, int MODE = kAggPlain,
+          bool COOP = false>
 __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
@@ -125,100 +254,59 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
   constexpr int GPB = kAggThreads / LPD;
   const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
+  __shared__ uint32_t long_rows[COOP ? GPB : 1];
+  __shared__ uint32_t n_long;
+  if (COOP) {
+    if (threadIdx.x == 0) n_long = 0;
+    __syncthreads();
+  }
   for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
     const uint32_t beg = off[d], end = off[d + 1];
-    T* yrow = reinterpret_cast<T*>(y + (uint64_t)d * ldy);
+    if (COOP && end - beg > kLongRow<U>()) {  // summed by the whole block below
+      if (sl == 0) long_rows[atomicAdd(&n_long, 1u)] = d;
+      continue;
+    }
     for (uint32_t c0 = 0; c0 < nv; c0 += LPD * NCH) {
       T acc[NCH];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
-      for (uint32_t cb = beg; cb < end; cb += LPD) {
-        const uint32_t ne = min(end - cb, (uint32_t)LPD);
-        uint32_t my_r = 0;
-        float my_w = 0.f;
-        if ((uint32_t)sl < ne) {  // streamed once: do not keep in cache
-          my_r = __builtin_nontemporal_load(idx + cb + sl);
-          my_w = w ? __builtin_nontemporal_load(w + cb + sl) : 1.0f;
-          const uint32_t loc = my_r;
-          if (MAP) my_r = map[my_r];
-          if (TIER) {
-            const uint32_t slot = tier.cmap[my_r];
-            my_r = slot != kNotCached ? slot : ((tier.host_local ? loc : my_r) | kHostBit);
-          }
-        }
-        for (uint32_t j0 = 0; j0 < ne; j0 += U) {
-          T xv[U][NCH];
-          T mv[MODE == kAggMask ? U : 1][MODE == kAggMask ? NCH : 1];
-          float ww[U];
+      gather_edges<VEC, LPD, NCH, MAP, U, TIER, MODE>(acc, beg, end, c0, sl, idx, w, x, ldx, map,
+                                                      nv, tier, ax);
+      store_row<VEC, LPD, NCH, MODE>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
+    }
+  }
+  if constexpr (COOP) {
+    __shared__ T part[GPB * LPD * NCH];
+    __syncthreads();
+    const uint32_t nl = n_long;  // the order rows are handled in does not matter
+    for (uint32_t i = 0; i < nl; ++i) {
+      const uint32_t d = long_rows[i];
+      const uint32_t beg = off[d], end = off[d + 1], len = end - beg;
+      const uint32_t pb = beg + (uint32_t)(((uint64_t)len * grp) / GPB);
+      const uint32_t pe = beg + (uint32_t)(((uint64_t)len * (grp + 1)) / GPB);
+      for (uint32_t c0 = 0; c0 < nv; c0 += LPD * NCH) {
+        T acc[NCH];
 #pragma unroll
-          for (int j = 0; j < U; ++j) {
-            const int src = (int)(j0 + j) & (LPD - 1);
-            const uint32_t r = (uint32_t)__shfl((int)my_r, src, LPD);
-            ww[j] = __shfl(my_w, src, LPD);
-            const bool ok = j0 + j < ne;
-            const T* xrow = reinterpret_cast<const T*>(
-                TIER && (r & kHostBit) ? tier.host + (uint64_t)(r & ~kHostBit) * tier.ldh
-                                       : x + (uint64_t)r * ldx);
+        for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
+        gather_edges<VEC, LPD, NCH, MAP, U, TIER, MODE>(acc, pb, pe, c0, sl, idx, w, x, ldx, map,
+                                                        nv, tier, ax);
 #pragma unroll
-            for (int c = 0; c < NCH; ++c) {
-              const uint32_t col = c0 + sl + c * LPD;
-              xv[j][c] = (ok && col < nv) ? xrow[col] : V::zero();
+        for (int c = 0; c < NCH; ++c) part[(grp * NCH + c) * LPD + sl] = acc[c];
+        __syncthreads();
+        if (grp == 0) {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            T s = part[c * LPD + sl];
+            for (int g = 1; g < GPB; ++g) {
+              const T q = part[(g * NCH + c) * LPD + sl];
+#pragma unroll
+              for (int k = 0; k < VEC; ++k) vcomp<VEC>(s, k) = vcomp<VEC>(s, k) + vcomp<VEC>(q, k);
             }
-            if constexpr (MODE == kAggMask) {
-              const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)r * ax.ldm);
-#pragma unroll
-              for (int c = 0; c < NCH; ++c) {
-                const uint32_t col = c0 + sl + c * LPD;
-                mv[j][c] = (ok && col < nv) ? mrow[col] : V::zero();
-              }
-            }
+            acc[c] = s;
           }
-          if constexpr (MODE == kAggMask) {  // dZ = dX ⊙ [X > 0] · scale
-#pragma unroll
-            for (int j = 0; j < U; ++j)
-#pragma unroll
-              for (int c = 0; c < NCH; ++c)
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) {
-                  float& g = vcomp<VEC>(xv[j][c], q);
-                  g = vcomp<VEC>(mv[j][c], q) > 0.f ? g * ax.scale : 0.f;
-                }
-          }
-#pragma unroll
-          for (int j = 0; j < U; ++j)
-            if (j0 + j < ne) {
-#pragma unroll
-              for (int c = 0; c < NCH; ++c) acc[c] = V::madd(acc[c], xv[j][c], ww[j]);
-            }
+          store_row<VEC, LPD, NCH, MODE>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
         }
-      }
-      if constexpr (MODE == kAggAct) {  // relu + inverted dropout, mask never stored
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const uint32_t f0 = (c0 + sl + c * LPD) * VEC;  // first float column
-#pragma unroll
-          for (int q2 = 0; q2 < (VEC + 1) / 2; ++q2) {
-            uint4 rnd = make_uint4(0u, 0u, 0u, 0u);
-            if (ax.keep_threshold) rnd = dropout_words((uint64_t)d, f0 + 2 * q2, ax.seed, ax.offset);
-            const uint32_t wd = (d & 3) == 0 ? rnd.x : (d & 3) == 1 ? rnd.y : (d & 3) == 2 ? rnd.z : rnd.w;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              if (2 * q2 + h >= VEC) break;
-              const uint32_t col = f0 + 2 * q2 + h;
-              float& v = vcomp<VEC>(acc[c], 2 * q2 + h);
-              v = (dropout_bits(wd, col) >= ax.keep_threshold && v > 0.f) ? v * ax.scale : 0.f;
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {  // output rows are not re-read here: keep them
-        const uint32_t col = c0 + sl + c * LPD;  // out of the cache that serves x rows
-        if (col + 1 < nv || (col + 1 == nv && last_valid == (uint32_t)VEC)) {
-          V::st_nt(yrow + col, acc[c]);
-        } else if (col + 1 == nv) {  // partial last vector: only the valid floats
-          V::st_part(yrow + col, acc[c], last_valid);
-        }
+        __syncthreads();
       }
     }
   }
@@ -279,6 +367,28 @@ __global__ __launch_bounds__(kAggThreads) void k_gather_rows(const float* __rest
                                    : table + (uint64_t)slot * ldt);
     T* dst = reinterpret_cast<T*>(out + (uint64_t)i * ldo);
     for (uint32_t c = sl; c < nv; c += LPD) dst[c] = src[c];
+  }
+}
+
+// out = g ⊙ [x > 0] · scale — the backward of dropout(relu(.)) given its
+// output x (relu zeroes and dropped elements are exactly the zeros of x)
+__global__ void k_act_backward(const float4* __restrict__ g, const float4* __restrict__ x,
+                               float4* __restrict__ out, uint64_t n4, float scale) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const float4 a = g[i], b = x[i];
+    out[i] = make_float4(b.x > 0.f ? a.x * scale : 0.f, b.y > 0.f ? a.y * scale : 0.f,
+                         b.z > 0.f ? a.z * scale : 0.f, b.w > 0.f ? a.w * scale : 0.f);
+  }
+}
+__global__ void k_act_backward_2d(const float* __restrict__ g, uint64_t ldg,
+                                  const float* __restrict__ x, uint64_t ldx, float* __restrict__ out,
+                                  uint64_t ldo, uint32_t rows, uint32_t F, float scale) {
+  const uint64_t n = (uint64_t)rows * F;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = i / F, c = i % F;
+    out[r * ldo + c] = x[r * ldx + c] > 0.f ? g[r * ldg + c] * scale : 0.f;
   }
 }
 
@@ -354,7 +464,7 @@ constexpr int gather_u(int floats_per_lane) {
   return floats_per_lane <= 4 ? 8 : floats_per_lane <= 12 ? 5 : 4;
 }
 
-template <int VEC, bool MAP, bool TIER, int MODE>
+template <int VEC, bool MAP, bool TIER, int MODE, bool COOP>
 static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid, Shape s,
                              const uint32_t* off,
                              const uint32_t* idx, const float* w, const uint32_t* n_dev,
@@ -367,11 +477,11 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   do {                                                                                      \
     constexpr int u = gather_u(VEC * NCH);                                                  \
     if (u == 5 && gather_u_env() == 4)                                                      \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4, TIER, MODE>), dim3(grid),   \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4, TIER, MODE, COOP>), dim3(grid), \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
                          nv, y, ldy, last_valid, tier, ax);                                 \
     else                                                                                    \
-      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u, TIER, MODE>), dim3(grid),   \
+      hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, u, TIER, MODE, COOP>), dim3(grid), \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
                          nv, y, ldy, last_valid, tier, ax);                                 \
   } while (0)
@@ -393,7 +503,7 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   return NTS_OK;
 }
 
-template <bool MAP, bool TIER = false, int MODE = kAggPlain>
+template <bool MAP, bool TIER = false, int MODE = kAggPlain, bool COOP = false>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
                          const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
                          uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy,
@@ -422,14 +532,15 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
     const long v = e ? atol(e) : 0;
     return v > 0 ? (uint32_t)v : (1u << 24);
   }();
-  const uint32_t grid = std::max(1u, std::min(ceil_div(n_cap, gpb), cap));
+  // COOP needs one row per lane group
+  const uint32_t grid = std::max(1u, COOP ? ceil_div(n_cap, gpb) : std::min(ceil_div(n_cap, gpb), cap));
   if (vec == 4)
-    return launch_gather_vec<4, MAP, TIER, MODE>(st, grid, last_valid, s, off, idx, w, n_dev,
+    return launch_gather_vec<4, MAP, TIER, MODE, COOP>(st, grid, last_valid, s, off, idx, w, n_dev,
                                                  n_cap, x, ldx, map, nv, y, ldy, tier, ax);
   if (vec == 2)
-    return launch_gather_vec<2, MAP, TIER, MODE>(st, grid, last_valid, s, off, idx, w, n_dev,
+    return launch_gather_vec<2, MAP, TIER, MODE, COOP>(st, grid, last_valid, s, off, idx, w, n_dev,
                                                  n_cap, x, ldx, map, nv, y, ldy, tier, ax);
-  return launch_gather_vec<1, MAP, TIER, MODE>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap,
+  return launch_gather_vec<1, MAP, TIER, MODE, COOP>(st, grid, last_valid, s, off, idx, w, n_dev, n_cap,
                                                x, ldx, map, nv, y, ldy, tier, ax);
 }
 
@@ -465,7 +576,8 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
                 "leading dimension < feature_size");
   if (s_cap == 0 || feature_size == 0) return NTS_OK;
   NTS_HIP_TRY(hipSetDevice(ctx->device));
-  return launch_gather<false>(ctx->stream, row_offset, column_indices, weight_backward, s, s_cap,
+  return launch_gather<false, false, kAggPlain, true>(ctx->stream, row_offset, column_indices,
+                                                      weight_backward, s, s_cap,
                               g_out, ld_gout, nullptr, feature_size, g_in, ld_gin);
 }
 
@@ -502,7 +614,7 @@ int nts_hip_spmm_csr_bwd_masked(nts_hip_ctx* ctx, const uint32_t* row_offset,
   ax.mx = x_act;
   ax.ldm = ld_act;
   ax.scale = scale;
-  return launch_gather<false, false, kAggMask>(ctx->stream, row_offset, column_indices,
+  return launch_gather<false, false, kAggMask, true>(ctx->stream, row_offset, column_indices,
                                                weight_backward, s, s_cap, g_out, ld_gout, nullptr,
                                                feature_size, g_in, ld_gin,
                                                Tier{nullptr, nullptr, 0, 0}, ax);
@@ -624,6 +736,32 @@ int nts_hip_spmm_csc_fwd_cached(nts_hip_ctx* ctx, const uint32_t* column_offset,
   return launch_gather<true, true>(ctx->stream, column_offset, row_indices, weight, v, v_cap,
                                    cache, ld_cache, x_row_map, feature_size, y, ldy,
                                    Tier{cache_map, host_table, ld_host, host_local});
+}
+
+int nts_hip_act_backward(nts_hip_ctx* ctx, uint32_t rows, uint32_t feature_size, const float* g,
+                         uint64_t ldg, const float* x_act, uint64_t ldx, float scale, float* out,
+                         uint64_t ldo) {
+  NTS_CHECK_ARG(ctx && g && x_act && out, "NULL argument");
+  NTS_CHECK_ARG(ldg >= feature_size && ldx >= feature_size && ldo >= feature_size,
+                "leading dimension < feature_size");
+  if (rows == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const uint64_t n = (uint64_t)rows * feature_size;
+  const bool flat = ldg == feature_size && ldx == feature_size && ldo == feature_size &&
+                    n % 4 == 0 && (uintptr_t)g % 16 == 0 && (uintptr_t)x_act % 16 == 0 &&
+                    (uintptr_t)out % 16 == 0;
+  if (flat) {
+    const uint32_t grid = std::max(1u, std::min(ceil_div(n / 4, 256), kMaxGrid));
+    hipLaunchKernelGGL(k_act_backward, dim3(grid), dim3(256), 0, ctx->stream,
+                       reinterpret_cast<const float4*>(g), reinterpret_cast<const float4*>(x_act),
+                       reinterpret_cast<float4*>(out), n / 4, scale);
+  } else {
+    const uint32_t grid = std::max(1u, std::min(ceil_div(n, 256), kMaxGrid));
+    hipLaunchKernelGGL(k_act_backward_2d, dim3(grid), dim3(256), 0, ctx->stream, g, ldg, x_act,
+                       ldx, out, ldo, rows, feature_size, scale);
+  }
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
 }
 
 int nts_hip_gather_labels(nts_hip_ctx* ctx, const int64_t* labels, const uint32_t* index,

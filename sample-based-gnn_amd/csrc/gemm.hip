@@ -496,11 +496,12 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
   }
   __syncthreads();
   (void)N;
+  // the next task's row pointers are resolved a whole task ahead (with a row
+  // map, a dependent load each) and handed over at the end of the task
+  const float* nrow[kWresRT];
+  rows_of(task + nwaves, nrow);
   for (; task < ntask; task += nwaves) {
     const int64_t m0 = (int64_t)task * rows_per_task;
-    if (!xt || task != wv * bpc + bi) rows_of(task, arow);
-    const float* nrow[kWresRT];  // next task's rows (XT)
-    rows_of(task + nwaves, nrow);
     f32x4 acc[kWresRT][CT];
 #pragma unroll
     for (int rt = 0; rt < kWresRT; ++rt)
@@ -546,6 +547,9 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
       wres_mask_tail(K, nfull, g, at);
       wres_mfma<NCOL>(bb + 32 * nfull * NCOL, at, acc);
     }
+#pragma unroll
+    for (int rt = 0; rt < kWresRT; ++rt) arow[rt] = nrow[rt];
+    rows_of(task + 2 * nwaves, nrow);
     // epilogue: acc[rt][j][v] = C[m0 + 16 rt + 4 g + v][n0 + CT i + j]
 #pragma unroll
     for (int rt = 0; rt < kWresRT; ++rt) {
@@ -648,17 +652,27 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
   float av[NAL * AVEC];
   float4 bv, xv;
   const int bk = tid / 32, bc = 4 * (tid % 32);
+  // A row of each staged element; with a row map these are dependent loads,
+  // resolved one step ahead (the map of step st+2 is read with step st+1)
+  uint32_t arow[NAL];
+  auto map_rows = [&](int step) {
+    const int kb = kbeg + step * kTbKS;
+#pragma unroll
+    for (int p = 0; p < NAL; ++p) {
+      const int kk = min(kb + (tid + kTbWaves * 64 * p) / NAV, K - 1);
+      arow[p] = ex.amap ? ex.amap[kk] : (uint32_t)kk;
+    }
+  };
+  map_rows(0);
   auto load = [&](int step) {
     const int kb = kbeg + step * kTbKS;
 #pragma unroll
     for (int p = 0; p < NAL; ++p) {
       const int e = tid + kTbWaves * 64 * p;
-      const int kk = min(kb + e / NAV, K - 1);
       // AVEC = 4 reads may run into the row padding (lda >= M rounded up to
       // 4); columns >= M are zeroed when staged
       const int c = min(r0 + AVEC * (e % NAV), AVEC == 4 ? (int)lda - 4 : M - AVEC);
-      const uint64_t row = ex.amap ? (uint64_t)ex.amap[kk] : (uint64_t)kk;
-      const float* src = A + row * lda + c;
+      const float* src = A + (uint64_t)arow[p] * lda + c;
       if (AVEC == 4) {
         const float4 x = *reinterpret_cast<const float4*>(src);
         av[4 * p] = x.x; av[4 * p + 1] = x.y; av[4 * p + 2] = x.z; av[4 * p + 3] = x.w;
@@ -672,6 +686,7 @@ __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
     const int kk = min(kb + bk, K - 1);
     bv = *reinterpret_cast<const float4*>(B + (uint64_t)kk * ldb + n0 + bc);
     if constexpr (BMASK) xv = *reinterpret_cast<const float4*>(ex.bx + (uint64_t)kk * ex.ldbx + n0 + bc);
+    map_rows(step + 1);
   };
   auto store = [&](int step, float* sy, float* sg) {
     const int kb = kbeg + step * kTbKS;

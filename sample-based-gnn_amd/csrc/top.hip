@@ -48,6 +48,7 @@ struct TopArgs {
   float* lpart;       // LOSS: [blocks] loss partials
   float* part;        // GRAD: dW partials [K][Cp/16][waves][16]
   float* dY;          // GRAD: [n x K]
+  uint32_t* cpart;    // LOSS with accuracy: [blocks] rows whose argmax is the label
 };
 
 __device__ __forceinline__ float grp_max(float v) {  // over the 16 lanes of a group
@@ -192,6 +193,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
   constexpr int CP = 16 * NCT;
   extern __shared__ float smem[];
   __shared__ float wl[kTopWaves];
+  __shared__ uint32_t wc[kTopWaves];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int K = a.K;
@@ -223,6 +225,36 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, kWave);
     if (lane == 0) wl[w] = l;
+    if (a.cpart) {
+      // getCorrect (toolkits/GCN_SAMPLE_ALLGPU.hpp:166-172): argmax of the
+      // log_softmax output (first index among equal values, as torch's
+      // argmax) == label
+      uint32_t ok = 0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          if (16 * ct + i < a.C && lp[ct][v] > best) {
+            best = lp[ct][v];
+            bi = 16 * ct + i;
+          }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float ob = __shfl_xor(best, o, kWave);
+          const int oi = __shfl_xor(bi, o, kWave);
+          if (ob > best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+          }
+        }
+        ok += (i == 0 && tgt[v] >= 0 && bi == tgt[v]) ? 1u : 0u;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) ok += __shfl_down(ok, o, kWave);
+      if (lane == 0) wc[w] = ok;
+    }
   }
   if (GRAD) {
     const float gl = (a.grad ? *a.grad : 1.0f) / (float)a.n;
@@ -296,8 +328,13 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
     __syncthreads();
     if (threadIdx.x == 0) {
       float s = 0.f;
-      for (int q = 0; q < kTopWaves; ++q) s += wl[q];
+      uint32_t c = 0;
+      for (int q = 0; q < kTopWaves; ++q) {
+        s += wl[q];
+        c += wc[q];
+      }
       a.lpart[blockIdx.x] = s;
+      if (a.cpart) a.cpart[blockIdx.x] = c;
     }
   }
 }
@@ -310,7 +347,9 @@ template <int NCT>
 __global__ __launch_bounds__(256) void k_top_finish(const float* __restrict__ part, int nslab,
                                                     const float* __restrict__ lpart, int nblk,
                                                     int n, int K, int C, int nchunks,
-                                                    float* __restrict__ dW, float* loss) {
+                                                    float* __restrict__ dW, float* loss,
+                                                    const uint32_t* __restrict__ cpart,
+                                                    uint32_t* correct) {
   __shared__ float red[256];
   const int t = threadIdx.x;
   float acc = 0.f;
@@ -336,15 +375,27 @@ __global__ __launch_bounds__(256) void k_top_finish(const float* __restrict__ pa
     const int k = q / NCT, c = 16 * (q % NCT) + t;
     if (t < 16 && c < C) dW[(uint64_t)k * C + c] = red[t];
   } else {
-    for (int b = t; b < nblk; b += 256) acc += lpart[b];
+    uint32_t c = 0;
+    for (int b = t; b < nblk; b += 256) {
+      acc += lpart[b];
+      if (cpart) c += cpart[b];
+    }
     red[t] = acc;
+    __shared__ uint32_t cred[256];
+    cred[t] = c;
     __syncthreads();
 #pragma unroll
     for (int h = 128; h >= 1; h >>= 1) {
-      if (t < h) red[t] += red[t + h];
+      if (t < h) {
+        red[t] += red[t + h];
+        cred[t] += cred[t + h];
+      }
       __syncthreads();
     }
-    if (t == 0) *loss = red[0] / (float)n;
+    if (t == 0) {
+      *loss = red[0] / (float)n;
+      if (correct) *correct += cred[0];  // accumulates over batches
+    }
   }
   (void)K;
 }
@@ -378,12 +429,12 @@ static int launch_top_any(hipStream_t st, int nblk, int Cp, const TopArgs& a) {
 
 static int launch_finish(hipStream_t st, int Cp, const float* part, int nslab, const float* lpart,
                          int nblk, int n, int K, int C, bool grad, bool loss_on, float* dW,
-                         float* loss) {
+                         float* loss, const uint32_t* cpart, uint32_t* correct) {
   const int nchunks = grad ? K * (Cp / 16) : 0;
   const dim3 grid(nchunks + (loss_on ? 1 : 0));
 #define NTS_F(NCT)                                                                             \
   hipLaunchKernelGGL(k_top_finish<NCT>, grid, dim3(256), 0, st, part, nslab, lpart, nblk, n, K, \
-                     C, nchunks, dW, loss)
+                     C, nchunks, dW, loss, cpart, correct)
   switch (Cp / 16) {
     case 1: NTS_F(1); break;
     case 2: NTS_F(2); break;
@@ -410,44 +461,49 @@ static int top_check(nts_hip_ctx* ctx, int n, int K, int C, uint64_t ldy) {
   return NTS_OK;
 }
 
-// scratch: [loss partials, 64-float aligned][dW partial chunks]
+// scratch: [loss partials, 64-float aligned][correct partials][dW partial chunks]
 static int top_run(nts_hip_ctx* ctx, bool loss_on, bool grad_on, const float* Y, uint64_t ldy,
                    int n, int K, const float* W, int C, const int64_t* labels,
-                   const float* grad_loss, float* loss, float* dY, float* dW) {
+                   const float* grad_loss, float* loss, float* dY, float* dW, uint32_t* correct) {
   NTS_RET(top_check(ctx, n, K, C, ldy));
   const int Cp = (C + 15) / 16 * 16;
   const int nblk = (n + kTopRows - 1) / kTopRows;
   const int nslab = nblk * kTopWaves;
   const size_t lp = ((size_t)nblk + 63) / 64 * 64;
   NTS_RET(ensure_scratch(
-      ctx, (lp + (grad_on ? (size_t)nslab * K * Cp : 0)) * sizeof(float)));
+      ctx, (2 * lp + (grad_on ? (size_t)nslab * K * Cp : 0)) * sizeof(float)));
   float* base = (float*)ctx->scratch;
-  TopArgs a{Y, ldy, W, labels, grad_loss, n, K, C, base, base + lp, dY};
+  uint32_t* cpart = (loss_on && correct) ? reinterpret_cast<uint32_t*>(base + lp) : nullptr;
+  TopArgs a{Y, ldy, W, labels, grad_loss, n, K, C, base, base + 2 * lp, dY, cpart};
   hipStream_t st = ctx->stream;
   if (loss_on && grad_on) NTS_RET((launch_top_any<true, true>(st, nblk, Cp, a)));
   else if (loss_on) NTS_RET((launch_top_any<true, false>(st, nblk, Cp, a)));
   else NTS_RET((launch_top_any<false, true>(st, nblk, Cp, a)));
-  return launch_finish(st, Cp, a.part, nslab, a.lpart, nblk, n, K, C, grad_on, loss_on, dW, loss);
+  return launch_finish(st, Cp, a.part, nslab, a.lpart, nblk, n, K, C, grad_on, loss_on, dW, loss,
+                       cpart, cpart ? correct : nullptr);
 }
 
 int nts_hip_linear_xent_fwd(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
-                            const float* W, int C, const int64_t* labels, float* loss) {
+                            const float* W, int C, const int64_t* labels, float* loss,
+                            uint32_t* correct) {
   NTS_CHECK_ARG(ctx && Y && W && labels && loss, "NULL argument");
-  return top_run(ctx, true, false, Y, ldy, n, K, W, C, labels, nullptr, loss, nullptr, nullptr);
+  return top_run(ctx, true, false, Y, ldy, n, K, W, C, labels, nullptr, loss, nullptr, nullptr,
+                 correct);
 }
 
 int nts_hip_linear_xent_bwd(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
                             const float* W, int C, const int64_t* labels, const float* grad_loss,
                             float* dY, float* dW) {
   NTS_CHECK_ARG(ctx && Y && W && labels && grad_loss && dY && dW, "NULL argument");
-  return top_run(ctx, false, true, Y, ldy, n, K, W, C, labels, grad_loss, nullptr, dY, dW);
+  return top_run(ctx, false, true, Y, ldy, n, K, W, C, labels, grad_loss, nullptr, dY, dW,
+                 nullptr);
 }
 
 int nts_hip_linear_xent_train(nts_hip_ctx* ctx, const float* Y, uint64_t ldy, int n, int K,
                               const float* W, int C, const int64_t* labels, float* loss,
-                              float* dY, float* dW) {
+                              float* dY, float* dW, uint32_t* correct) {
   NTS_CHECK_ARG(ctx && Y && W && labels && loss && dY && dW, "NULL argument");
-  return top_run(ctx, true, true, Y, ldy, n, K, W, C, labels, nullptr, loss, dY, dW);
+  return top_run(ctx, true, true, Y, ldy, n, K, W, C, labels, nullptr, loss, dY, dW, correct);
 }
 
 }  // extern "C"

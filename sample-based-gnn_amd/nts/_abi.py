@@ -34,7 +34,7 @@ EXPORTED = (
     "nts_hip_sample_layer", "nts_hip_gather_rows", "nts_hip_gather_labels",
     "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
     "nts_hip_spmm_csc_fwd_act", "nts_hip_spmm_csr_bwd_masked", "nts_hip_gemm_gather_f32",
-    "nts_hip_gemm_tn_gather_f32",
+    "nts_hip_gemm_tn_gather_f32", "nts_hip_act_backward",
     "nts_hip_gemm_f32", "nts_hip_gemm_relu_dropout_f32", "nts_hip_gemm_tn_masked_f32",
     "nts_hip_linear_xent_fwd", "nts_hip_linear_xent_bwd", "nts_hip_linear_xent_train", "nts_hip_adam", "nts_hip_comm_unique_id", "nts_hip_comm_init", "nts_hip_comm_destroy",
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
@@ -99,6 +99,7 @@ def lib() -> C.CDLL:
         "nts_hip_spmm_csc_fwd": ([P, P, P, P, P, U32, P, U64, P, U32, P, U64], I),
         "nts_hip_spmm_csc_fwd_act": ([P, P, P, P, P, U32, P, U64, U32, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd_masked": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
+        "nts_hip_act_backward": ([P, U32, U32, P, U64, P, U64, F, P, U64], I),
         "nts_hip_gemm_gather_f32": ([P, I, I, I, P, U64, P, P, U64, P, U64], I),
         "nts_hip_gemm_tn_gather_f32": ([P, I, I, I, P, U64, P, P, U64, P, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
@@ -106,9 +107,9 @@ def lib() -> C.CDLL:
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),
         "nts_hip_gemm_relu_dropout_f32": ([P, I, I, I, P, U64, P, U64, P, U64, F, U64, U64], I),
         "nts_hip_gemm_tn_masked_f32": ([P, I, I, I, P, U64, P, U64, P, U64, F, P, U64], I),
-        "nts_hip_linear_xent_fwd": ([P, P, U64, I, I, P, I, P, P], I),
+        "nts_hip_linear_xent_fwd": ([P, P, U64, I, I, P, I, P, P, P], I),
         "nts_hip_linear_xent_bwd": ([P, P, U64, I, I, P, I, P, P, P, P], I),
-        "nts_hip_linear_xent_train": ([P, P, U64, I, I, P, I, P, P, P, P], I),
+        "nts_hip_linear_xent_train": ([P, P, U64, I, I, P, I, P, P, P, P, P], I),
         "nts_hip_adam": ([P, P, P, P, P, U64, F, F, F, F, F, F, F, I], I),
         "nts_hip_comm_unique_id": ([P], I),
         "nts_hip_comm_init": ([C.POINTER(P), I, I, P, I], I),

@@ -171,6 +171,12 @@ class HipContext:
         check(self.lib.nts_hip_gemm_f32(self.h, int(trans_a), M, N, K, ptr(A), A.stride(0), ptr(B),
                                         B.stride(0), ptr(C), C.stride(0)))
 
+    def act_backward(self, g, x_act, out, scale=1.0):
+        """out = g * (x_act > 0) * scale."""
+        rows, F = g.shape
+        check(self.lib.nts_hip_act_backward(self.h, rows, F, ptr(g), g.stride(0), ptr(x_act),
+                                            x_act.stride(0), float(scale), ptr(out), out.stride(0)))
+
     def gemm_gather(self, A, rows, B, C):
         """C = A[rows] @ B (rows: int32 device tensor of row ids)."""
         M, K, N = rows.numel(), A.shape[1], B.shape[1]
@@ -199,23 +205,24 @@ class HipContext:
                                                   G.stride(0), ptr(X), X.stride(0), float(scale),
                                                   ptr(C), C.stride(0)))
 
-    def linear_xent_fwd(self, Y, W, labels, loss):
-        """loss = nll_loss(log_softmax(log_softmax(Y @ W)), labels) (mean), fused."""
+    def linear_xent_fwd(self, Y, W, labels, loss, correct=None):
+        """loss = nll_loss(log_softmax(log_softmax(Y @ W)), labels) (mean), fused;
+        correct (int32 device scalar) += rows whose argmax is the label."""
         n, K = Y.shape
         check(self.lib.nts_hip_linear_xent_fwd(self.h, ptr(Y), Y.stride(0), n, K, ptr(W), W.shape[1],
-                                               ptr(labels), ptr(loss)))
+                                               ptr(labels), ptr(loss), ptr(correct)))
 
     def linear_xent_bwd(self, Y, W, labels, grad_loss, dY, dW):
         n, K = Y.shape
         check(self.lib.nts_hip_linear_xent_bwd(self.h, ptr(Y), Y.stride(0), n, K, ptr(W), W.shape[1],
                                                ptr(labels), ptr(grad_loss), ptr(dY), ptr(dW)))
 
-    def linear_xent_train(self, Y, W, labels, loss, dY, dW):
+    def linear_xent_train(self, Y, W, labels, loss, dY, dW, correct=None):
         """The loss and its gradients for d loss = 1 in one pass (== fwd + bwd(1))."""
         n, K = Y.shape
         check(self.lib.nts_hip_linear_xent_train(self.h, ptr(Y), Y.stride(0), n, K, ptr(W),
                                                  W.shape[1], ptr(labels), ptr(loss), ptr(dY),
-                                                 ptr(dW)))
+                                                 ptr(dW), ptr(correct)))
 
     def adam(self, w, g, m, v, alpha, beta1, beta2, eps, wd, beta1_t, beta2_t, bias_correction):
         check(self.lib.nts_hip_adam(self.h, ptr(w), ptr(g), ptr(m), ptr(v), w.numel(), alpha,

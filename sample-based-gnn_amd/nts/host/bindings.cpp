@@ -189,6 +189,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            },
            py::arg("seeds"), py::arg("batch_seq") = 0)
       .def("set_weights", &GCN_SAMPLE_ALLGPU_impl::set_weights)
+      .def("train_correct", &GCN_SAMPLE_ALLGPU_impl::train_correct)
+      .def("reset_correct", &GCN_SAMPLE_ALLGPU_impl::reset_correct)
+      .def("evaluate",
+           [](GCN_SAMPLE_ALLGPU_impl& d, const torch::Tensor& nids) {
+             auto ids = to_ids(nids);
+             py::gil_scoped_release nogil;
+             return d.evaluate(ids);
+           },
+           py::arg("nids"))
       .def("weights", &GCN_SAMPLE_ALLGPU_impl::weights)
       .def("reset_stats", &GCN_SAMPLE_ALLGPU_impl::reset_stats)
       .def("resolve_profile",

@@ -771,16 +771,38 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     const int dev = cs->device();
     hipStream_t st = (hipStream_t)cs->stream();
     NtsVar dH = torch::empty({std::max<int64_t>(s, 1), N}, f32_opts(dev));
-    if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
-    hip_check(nts_hip_spmm_csr_bwd_masked(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(),
-                                          nullptr, (uint32_t)s, g.data_ptr<float>(), (uint64_t)N,
-                                          X1.data_ptr<float>(), (uint64_t)N,
-                                          (float)ctx->saved_data["scale"].toDouble(), (uint32_t)N,
-                                          dH.data_ptr<float>(), (uint64_t)N),
-              "nts_hip_spmm_csr_bwd_masked");
-    if (prof)
-      prof->end(KernelProfiler::BOTTOM_BWD, st,
-                8.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
+    const float scale = (float)ctx->saved_data["scale"].toDouble();
+    // dZ = dX1 ⊙ mask once per dst row, then the plain CSR gather (measured
+    // faster than applying the mask to every gathered row:
+    // nts_hip_spmm_csr_bwd_masked reads two rows per edge); NTS_TF_MASKED_BWD=1
+    // selects the fused form
+    static const bool fused_mask = getenv("NTS_TF_MASKED_BWD") != nullptr;
+    if (fused_mask) {
+      if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
+      hip_check(nts_hip_spmm_csr_bwd_masked(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(),
+                                            sg->dev_e_w_b(), nullptr, (uint32_t)s,
+                                            g.data_ptr<float>(), (uint64_t)N, X1.data_ptr<float>(),
+                                            (uint64_t)N, scale, (uint32_t)N, dH.data_ptr<float>(),
+                                            (uint64_t)N),
+                "nts_hip_spmm_csr_bwd_masked");
+      if (prof)
+        prof->end(KernelProfiler::BOTTOM_BWD, st,
+                  8.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
+    } else {
+      NtsVar dZ = torch::empty({std::max<int64_t>(v, 1), N}, f32_opts(dev));
+      hip_check(nts_hip_act_backward(cs->ctx(), (uint32_t)v, (uint32_t)N, g.data_ptr<float>(),
+                                     (uint64_t)N, X1.data_ptr<float>(), (uint64_t)N, scale,
+                                     dZ.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_act_backward");
+      if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
+      hip_check(nts_hip_spmm_csr_bwd(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(),
+                                     nullptr, (uint32_t)s, dZ.data_ptr<float>(), (uint64_t)N,
+                                     (uint32_t)N, dH.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_spmm_csr_bwd");
+      if (prof)
+        prof->end(KernelProfiler::BOTTOM_BWD, st,
+                  4.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
+    }
     NtsVar dW = torch::empty({F, N}, W.options());
     if (prof) prof->begin(KernelProfiler::GATHER_GEMM_TN, st);
     hip_check(nts_hip_gemm_tn_gather_f32(cs->ctx(), (int)F, (int)N, (int)s, table.data_ptr<float>(),
@@ -798,7 +820,8 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
 // seed of self_backward (exactly 1), and otherwise runs the backward kernel.
 struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar y, NtsVar W, NtsVar target, int64_t cs_ptr,
-                        bool train) {
+                        bool train, int64_t correct_ptr) {
+    auto* correct = reinterpret_cast<uint32_t*>(correct_ptr);
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     NtsVar yc = row_major(y), Wc = W.contiguous(), tc = target.contiguous();
     const int64_t n = yc.size(0), K = yc.size(1), C = Wc.size(1);
@@ -811,14 +834,14 @@ struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
       hip_check(nts_hip_linear_xent_train(cs->ctx(), yc.data_ptr<float>(), (uint64_t)yc.stride(0),
                                           (int)n, (int)K, Wc.data_ptr<float>(), (int)C,
                                           tc.data_ptr<int64_t>(), loss.data_ptr<float>(),
-                                          dY.data_ptr<float>(), dW.data_ptr<float>()),
+                                          dY.data_ptr<float>(), dW.data_ptr<float>(), correct),
                 "nts_hip_linear_xent_train");
       ctx->saved_data["dY"] = dY;
       ctx->saved_data["dW"] = dW;
     } else {
       hip_check(nts_hip_linear_xent_fwd(cs->ctx(), yc.data_ptr<float>(), (uint64_t)yc.stride(0),
                                         (int)n, (int)K, Wc.data_ptr<float>(), (int)C,
-                                        tc.data_ptr<int64_t>(), loss.data_ptr<float>()),
+                                        tc.data_ptr<int64_t>(), loss.data_ptr<float>(), correct),
                 "nts_hip_linear_xent_fwd");
     }
     ctx->save_for_backward({yc, Wc, tc});
@@ -848,7 +871,7 @@ struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
     }
     ctx->saved_data.erase("dY");
     ctx->saved_data.erase("dW");
-    return {ctx->needs_input_grad(0) ? dY : NtsVar(), dW, NtsVar(), NtsVar(), NtsVar()};
+    return {ctx->needs_input_grad(0) ? dY : NtsVar(), dW, NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
 }  // namespace
@@ -1022,10 +1045,12 @@ bool hip_linear_xent_supported(int64_t K, int64_t C) {
          (K * Cp + 64 * (K + 4) + 64 * Cp) * 4 <= 160 * 1024;
 }
 
-NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs) {
+NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs,
+                       uint32_t* correct) {
   // a backward follows only under grad mode with an input requiring grad
   const bool train = torch::GradMode::is_enabled() && (y.requires_grad() || W.requires_grad());
-  return HipLinearXentFn::apply(y, W, target, reinterpret_cast<int64_t>(cs), train);
+  return HipLinearXentFn::apply(y, W, target, reinterpret_cast<int64_t>(cs), train,
+                                reinterpret_cast<int64_t>(correct));
 }
 
 // ---------------------------------------------------------------------------

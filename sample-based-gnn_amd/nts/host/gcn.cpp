@@ -69,8 +69,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   if (cfg.transform_first == 1)
     TORCH_CHECK(tf_ok, "transform_first needs >= 2 layers, the MFMA GEMMs with the fused "
                        "activation, no GAT and no feature cache");
-  tf_ = tf_ok && (cfg.transform_first == 1 ||
-                  (cfg.transform_first < 0 && cfg.layer_size[0] > cfg.layer_size[1]));
+  tf_ = tf_ok && cfg.transform_first == 1;
   // CSR transposes only where a graph-op backward runs (every hop but the
   // outermost, whose backward the context skips — unless the bottom layer is
   // transform-first: its aggregation then has a backward, dH = A^T dZ)
@@ -118,6 +117,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                 (int64_t)fcache->ld},
                                f32_opts(graph->device));
   }
+  correct_ = torch::zeros({1}, u32_opts(graph->device));
   init_nn();
 }
 
@@ -304,7 +304,10 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
                bottom_bytes(sg, cfg.fused_gather));
     if (loss_target && l == L - 1)  // vertexForward + Loss of the last layer, fused
       X = ctx.runVertexForward(
-          [&](NtsVar& a) { return hip_linear_xent(a, P[l]->W, *loss_target, cs.get()); }, Y);
+          [&](NtsVar& a) {
+            return hip_linear_xent(a, P[l]->W, *loss_target, cs.get(), count_to_);
+          },
+          Y);
     else
       X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(l, a); }, Y);
     if (keep) {
@@ -416,16 +419,20 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   if (cfg.gat) {  // GAT_SAMPLE_ALL_GPU::Loss + loss.backward() (toolkits/GAT_SAMPLE_ALL_GPU.hpp:393-399)
     auto acts = forward_gat(sg);
     loss = torch::nll_loss(acts.back().log_softmax(1), target);
+    count_correct(acts.back(), target);
     loss.backward();
     ctx.reset();
   } else {
     const bool fuse_loss = cfg.fuse_loss && cfg.hip_gemm && L >= 2 &&
                            hip_linear_xent_supported(P[L - 1]->W.size(0), P[L - 1]->W.size(1));
+    count_to_ = dptr<uint32_t>(correct_);
     auto acts = forward(sg, false, early_ ? &pre_y_[slot] : nullptr, fuse_loss ? &target : nullptr);
+    count_to_ = nullptr;
     if (fuse_loss) {
       loss = acts.back();
     } else {
       NtsVar out = acts.back();
+      count_correct(out, target);
       Loss(out, target);
     }
     ctx.self_backward(false);
@@ -492,6 +499,64 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<Verte
   ctx.train();
   cs->synchronize();
   return acts;
+}
+
+void GCN_SAMPLE_ALLGPU_impl::count_correct(const NtsVar& out, const NtsVar& tgt) {
+  torch::NoGradGuard ng;
+  correct_.add_(out.argmax(1).eq(tgt).sum().to(torch::kInt32));
+}
+
+uint64_t GCN_SAMPLE_ALLGPU_impl::train_correct() {
+  cs->synchronize();
+  return (uint64_t)(uint32_t)correct_.cpu().item<int32_t>();
+}
+
+void GCN_SAMPLE_ALLGPU_impl::reset_correct() {
+  auto guard = cs->guard();
+  correct_.zero_();
+}
+
+double GCN_SAMPLE_ALLGPU_impl::evaluate(const std::vector<VertexId>& nids) {
+  if (nids.empty()) return 0.0;
+  auto guard = cs->guard();
+  const int L = (int)cfg.fanout.size();
+  const WeightType wt = cfg.gat ? WeightType::None : cfg.weight_type;
+  std::vector<bool> csr(L, cfg.gat);
+  FastSampler s(graph, nids, L, cfg.batch_size, cfg.fanout, 1, csr, wt != WeightType::None,
+                cfg.gat);
+  s.rng_mode = cfg.rng_mode;
+  s.up_degree = cfg.up_degree;
+  s.batch_seq = eval_seq;
+  NtsVar correct = torch::zeros({1}, u32_opts(graph->device));
+  const bool fuse_loss = !cfg.gat && cfg.fuse_loss && cfg.hip_gemm && L >= 2 &&
+                         hip_linear_xent_supported(P[L - 1]->W.size(0), P[L - 1]->W.size(1));
+  ctx.eval();
+  {
+    torch::NoGradGuard ng;
+    NtsVar tgt;
+    while (s.sample_not_finished()) {
+      SampledSubgraph* sg = s.sample_gpu_fast(cfg.batch_size, 0, *cs, wt);
+      s.load_label_gpu(*cs, sg, tgt, L_GT);
+      if (cfg.gat) {
+        auto acts = forward_gat(sg);
+        correct.add_(acts.back().argmax(1).eq(tgt).sum().to(torch::kInt32));
+      } else if (fuse_loss) {
+        count_to_ = dptr<uint32_t>(correct);
+        forward(sg, false, nullptr, &tgt);
+        count_to_ = nullptr;
+      } else {
+        auto acts = forward(sg, false);
+        correct.add_(acts.back().argmax(1).eq(tgt).sum().to(torch::kInt32));
+      }
+      // the sampler slot is reused by the next batch: order it behind this forward
+      TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)cs->stream()) == hipSuccess,
+                  "hipEventRecord");
+    }
+  }
+  ctx.train();
+  eval_seq = s.batch_seq;
+  cs->synchronize();
+  return (double)(uint32_t)correct.cpu().item<int32_t>() / (double)nids.size();
 }
 
 void GCN_SAMPLE_ALLGPU_impl::reset_stats() {

@@ -28,7 +28,8 @@ struct GCNConfig {
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   // bottom layer order: 1 = transform first, A (X W) (rows narrowed before the
   // aggregation), 0 = aggregate first, (A X) W (the reference's order),
-  // -1 = transform first iff the first layer narrows (F_in > F_out)
+  // -1 = auto: aggregate first (measured faster with the fp32 MFMA GEMMs at
+  // C2, DESIGN §3: the transform-first GEMMs run over the src rows)
   int transform_first = -1;
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
@@ -69,6 +70,15 @@ class GCN_SAMPLE_ALLGPU_impl {
   // eval-mode forward over a given seed batch: [Y_0, X_1, Y_1, X_2, ...]
   std::vector<NtsVar> forward_eval(const std::vector<VertexId>& seeds, uint64_t batch_seq);
   void set_weights(const std::vector<NtsVar>& ws);
+  // Accuracy (getCorrect / Test, toolkits/GCN_SAMPLE_ALLGPU.hpp:166-213,361-383):
+  // training batches count their correct rows on the device as they train
+  // (no per-batch sync); train_correct() reads the count (synchronises).
+  uint64_t train_correct();
+  void reset_correct();
+  // Forward(eval_sampler, 1/2): eval mode over `nids` in batches of the
+  // training batch size, sampled like training (the reference's eval/test
+  // samplers); returns correct / |nids|.
+  double evaluate(const std::vector<VertexId>& nids);
   std::vector<NtsVar> weights() const;
   void reset_stats();
   void resolve_profile() { prof.resolve(); }
@@ -88,6 +98,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   uint64_t batch_edges = 0, batches = 0;
   KernelProfiler prof;  // device time of the bottom-layer kernels (cfg.profile)
   bool transform_first() const { return tf_; }
+  uint64_t eval_seq = uint64_t(1) << 40;  // PHILOX stream of the evaluation batches
 
  private:
   NtsVar vertexForward(int l, NtsVar& a);
@@ -103,6 +114,9 @@ class GCN_SAMPLE_ALLGPU_impl {
   void Update();
   std::pair<hipEvent_t, hipEvent_t>& next_events();
   void mark(const char* what, NtsStream& st);
+  void count_correct(const NtsVar& out, const NtsVar& tgt);  // non-fused output layers
+  NtsVar correct_;        // int32 [1]: correct rows of the training batches since reset
+  uint32_t* count_to_ = nullptr;  // where forward's fused loss adds its correct count
   std::vector<std::pair<const char*, hipEvent_t>> tl_;  // NTS_TIMELINE events
   bool tf_ = false;  // transform-first bottom layer (cfg.transform_first)
   // early aggregation: per sampler slot, the bottom graph op's output and the

@@ -366,7 +366,9 @@ std::vector<uint32_t> cu_mask_spread(int device, int n, bool complement);
 // Persistent fp32 scalar 1 on `dev` (the loss-backward seed).
 const NtsVar& unit_scalar(const torch::Device& dev);
 bool hip_linear_xent_supported(int64_t K, int64_t C);
-NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs);
+// correct != NULL: *correct += rows whose argmax is the target (getCorrect)
+NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, NtsStream* cs,
+                       uint32_t* correct = nullptr);
 // row-major fp32 views the HIP GEMMs take without a copy (unit column stride)
 NtsVar row_major(const NtsVar& x);
 // [rows, F] with 128-byte aligned rows when F >= 256 (padded leading dimension)

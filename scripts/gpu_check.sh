@@ -1,11 +1,25 @@
 #!/bin/bash
-# GPU-box routine: tests, then bench variants.  Each GPU step has its own limit
-# and the chain stops at the first failure.
+# One GPU round trip: parity suite, smoke, default bench, aggregate-first A/B.
+#   scripts/gpu_check.sh [tag] [pytest -k expr]
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS FAILED; tail -40 gpurun_out/gpu_tests.log; exit 1; }
-tail -2 gpurun_out/gpu_tests.log
-for v in "" "--no-fuse-act" "--no-early-agg" "--no-pipeline"; do
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline $v > gpurun_out/bench_ab.json 2> gpurun_out/bench_ab.err || { echo BENCH FAILED $v; tail -20 gpurun_out/bench_ab.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/bench_ab.json'));print('$v', round(d['ms_per_step'],3),'ms', round(d['value']/1e6),'M edges/s', 'agg', round(d['roofline']['avg_launch_ms'],3), 'ms frac', round(d['roofline']['frac'],3))"
-done
+TAG=${1:-chk}
+K=${2:-}
+O=gpurun_out/$TAG
+mkdir -p $O
+if [ -n "$K" ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+else
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=12 > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+fi
+grep -E "passed|failed|s call" $O/tests.log | head -16
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+timeout -k 10 300 python -u bench.py --transform-first 0 --no-cpu-baseline --epochs 1 --sampler-batches 0 > $O/bench_af.json 2> $O/bench_af.err || { echo "bench af failed"; tail -20 $O/bench_af.err; exit 1; }
+python - <<PY
+import json
+for f in ("$O/bench.json", "$O/bench_af.json"):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f, round(d["ms_per_step"], 4), "ms/step", "%.4g" % d["value"], d["roofline"].get("kernel"), {k: (round(v["avg_launch_ms"]*1e3,1), round(v["frac"],3)) for k, v in d["roofline"].get("kernels", {}).items()})
+PY
+echo ok

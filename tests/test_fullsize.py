@@ -1,0 +1,234 @@
+"""Full-size correctness of the benched configurations.
+
+The parity suite runs on Cora-sized graphs; these tests run the HIP path at
+the sizes BASELINE.json's configs are benched on and check it there:
+  * C2 Reddit-shaped (V=232,965, E~114.8M, batch 10,000, fanout 25-10): the
+    whole sampled batch bit-exact vs the oracle's PHILOX restatement of
+    FastSampler::sample_fast (core/ntsFastSampler.hpp:962-1140), the fused
+    gather + hop-1 aggregation bit-exact vs MiniBatchFuseOp, the
+    transform-first bottom layer within 1e-4 of the GCN_CPU_SAMPLE chain, and
+    the size-independent properties (source strictly ascending, row_indices <
+    src_size, e_size = sum min(deg, f), sampled ids a sub-multiset of each
+    dst's neighbour list).
+  * C3 ogbn-products-shaped, 3 layers 15-10-5, batch 1,024, Mean weights:
+    the same sampler checks and the bottom aggregation.
+  * C5-class: a graph past 2^31 edges (u64 CSC offsets, the sampler reading
+    neighbour lists that start beyond 2^31) and a feature table past 2^32
+    floats (64-bit row offsets in the gathers).
+Memory is freed between tests; each runs in well under the per-test limit.
+"""
+import gc
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def E():
+    from nts import host
+    return host.ext()
+
+
+def _np(t):
+    a = t.cpu().numpy()
+    return a.view(np.uint32) if a.dtype == np.int32 else a
+
+
+def _free():
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _properties(G, layers, fanout, V):
+    """Size-independent properties of one sampled batch, on the device."""
+    col = G.column_offset  # int64 [V+1]
+    rows = G.row_indices.long() & 0xFFFFFFFF
+    for ly, f in zip(layers, fanout):
+        v, e, s = ly["v_size"], ly["e_size"], ly["src_size"]
+        dst = ly["destination"].long() & 0xFFFFFFFF
+        src = ly["source"].long() & 0xFFFFFFFF
+        co = ly["column_offset"].long()
+        ri = ly["row_indices"].long() & 0xFFFFFFFF
+        ans = ly["sample_ans"].long() & 0xFFFFFFFF
+        deg = col[dst + 1] - col[dst]
+        want = deg if f < 0 else torch.clamp(deg, max=f)
+        assert int(want.sum()) == e, "e_size != sum min(deg, f)"
+        assert torch.equal(co[1:] - co[:-1], want), "per-dst counts"
+        assert bool((src[1:] > src[:-1]).all()), "source not strictly ascending"
+        assert int(src.max()) < V
+        assert bool((ri < s).all()), "row_indices >= src_size"
+        assert torch.equal(src[ri], ans), "row_indices do not map to sample_ans"
+        # every sampled id is a neighbour of its dst, at most as often as it
+        # occurs in the neighbour list (distinct positions of a multigraph)
+        d_of_e = torch.repeat_interleave(torch.arange(v, device=DEV), want)
+        ks = torch.sort(d_of_e * V + ans).values
+        uk, cnt = torch.unique_consecutive(ks, return_counts=True)
+        n_of = torch.repeat_interleave(torch.arange(v, device=DEV), deg)
+        base = torch.repeat_interleave(col[dst] - torch.cumsum(deg, 0) + deg, deg)
+        nbr = rows[base + torch.arange(int(deg.sum()), device=DEV)]
+        kn = torch.sort(n_of * V + nbr).values
+        have = torch.searchsorted(kn, uk, right=True) - torch.searchsorted(kn, uk, right=False)
+        assert bool((have >= cnt).all()), "a sampled id is not a neighbour (or repeats a position)"
+        del ks, uk, cnt, n_of, base, nbr, kn, have, d_of_e
+
+
+def _compare_oracle(got, ref):
+    for a, b in zip(got, ref):
+        assert (a["v_size"], a["e_size"], a["src_size"]) == (b["v_size"], b["e_size"], b["src_size"])
+        for k in ("destination", "column_offset", "row_indices", "sample_ans", "source",
+                  "edge_weight_forward", "row_offset", "column_indices", "edge_weight_backward"):
+            if k in a and a[k] is not None:
+                assert np.array_equal(_np(a[k]), b[k]), k
+
+
+def test_c2_reddit_shaped_full_batch(E):
+    from nts import host, synthetic
+    g, F, C = synthetic.shaped("reddit", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    src_h, dst_h = g.src.cpu().numpy().view(np.uint32), g.dst.cpu().numpy().view(np.uint32)
+    del g
+    fan, B = [25, 10], 10_000
+    seeds = torch.from_numpy(np.random.default_rng(5).choice(V, B, replace=False).astype(np.int32))
+    fs = E.FastSampler(G, seeds, 2, B, fan)
+    got = fs.sample_gpu_fast(B)
+    _properties(G, got, fan, V)
+    assert got[1]["e_size"] > 1_000_000 and got[1]["src_size"] > 200_000  # the benched shape
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    od, idg = orc.degrees(V, src_h, dst_h)
+    assert np.array_equal(od, _np(G.out_degree)) and np.array_equal(idg, _np(G.in_degree))
+    o = orc.Sampler(col, rows, idg, od, fan, rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    ref = o.sample(seeds.numpy().astype(np.uint32), 0)
+    _compare_oracle(got, ref)
+    # fused gather + hop-1 aggregation (the bottom graph op) bit-exact, full batch
+    from nts.hip import HipContext
+    hip = HipContext(0)
+    feat = synthetic.features(V, F, device=DEV)
+    l1 = got[1]
+    v1 = l1["v_size"]
+    y = torch.empty(v1, F, device=DEV)
+    hip.spmm_csc_fwd(l1["column_offset"], l1["row_indices"], l1["edge_weight_forward"], None, v1,
+                     feat, y, row_map=l1["source"])
+    X0 = orc.get_feature(ref[1]["source"], feat.cpu().numpy(), threads=8)
+    Y0 = orc.fuse_fwd(ref[1], X0, od, idg, threads=8)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), Y0)
+    # transform-first bottom layer at full size: A (X W) vs (A X) W within 1e-4
+    W = torch.randn(F, 128, device=DEV, generator=torch.Generator(device=DEV).manual_seed(1)) * 0.05
+    H = torch.empty(l1["src_size"], 128, device=DEV)
+    hip.gemm_gather(feat, l1["source"], W, H)
+    X1 = torch.empty(v1, 128, device=DEV)
+    hip.spmm_csc_fwd_act(l1["column_offset"], l1["row_indices"], l1["edge_weight_forward"], None,
+                         v1, H, X1, p=0.0)
+    ref_x1 = torch.relu(torch.from_numpy(Y0).to(DEV).double() @ W.double())
+    torch.testing.assert_close(X1.double(), ref_x1, rtol=1e-4, atol=1e-4)
+    del fs, got, feat, y, H, X1, G
+    _free()
+
+
+def test_c3_products_shaped_three_layers_mean(E):
+    from nts import synthetic
+    g, F, C = synthetic.shaped("products", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    fan, B = [15, 10, 5], 1024
+    seeds = torch.from_numpy(np.random.default_rng(6).choice(V, B, replace=False).astype(np.int32))
+    fs = E.FastSampler(G, seeds, 3, B, fan)
+    got = fs.sample_gpu_fast(B, E.WeightType.Mean)
+    _properties(G, got, fan, V)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    od, idg = _np(G.out_degree), _np(G.in_degree)
+    o = orc.Sampler(col, rows, idg, od, fan, rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    ref = o.sample(seeds.numpy().astype(np.uint32), 0, orc.W_MEAN)
+    _compare_oracle(got, ref)
+    from nts.hip import HipContext
+    hip = HipContext(0)
+    feat = synthetic.features(V, F, device=DEV)
+    l2 = got[2]
+    y = torch.empty(l2["v_size"], F, device=DEV)
+    hip.spmm_csc_fwd(l2["column_offset"], l2["row_indices"], l2["edge_weight_forward"], None,
+                     l2["v_size"], feat, y, row_map=l2["source"])
+    X0 = orc.get_feature(ref[2]["source"], feat.cpu().numpy(), threads=8)
+    Y0 = orc.fuse_fwd(ref[2], X0, od, idg, weight_mean=True, threads=8)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), Y0)
+    del fs, got, feat, y, G
+    _free()
+
+
+def test_c5_class_past_2e31_edges(E):
+    """u64 CSC offsets: 2.3 x 10^9 edges on 2M vertices; seeds whose neighbour
+    lists start past 2^31 are sampled bit-exactly vs the oracle."""
+    from nts import synthetic
+    V, En = 2_000_000, 2_300_000_000
+    g = synthetic.chung_lu(V, En, 20.0, device=DEV, seed=77)
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    _free()
+    col_d = G.column_offset
+    assert int(col_d[-1]) == En and int(col_d[-1]) > 2 ** 31
+    late = torch.nonzero(col_d[:-1] > 2 ** 31 + 5).flatten()
+    seeds = late[torch.randperm(late.numel(), device=DEV,
+                                generator=torch.Generator(device=DEV).manual_seed(3))[:512]]
+    seeds = seeds.to(torch.int32).cpu()
+    fan = [15, 10]
+    fs = E.FastSampler(G, seeds, 2, 512, fan)
+    got = fs.sample_gpu_fast(512)
+    _properties(G, got, fan, V)
+    col = col_d.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    od, idg = _np(G.out_degree), _np(G.in_degree)
+    o = orc.Sampler(col, rows, idg, od, fan, rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    ref = o.sample(seeds.numpy().astype(np.uint32), 0)
+    _compare_oracle(got, ref)
+    del fs, got, G, rows
+    _free()
+
+
+def test_feature_rows_past_2e32_floats(E):
+    """64-bit row offsets in the gathers: a [35M x 128] fp32 table (4.48 x 10^9
+    floats, 17.9 GB); rows past the 2^32-float mark are gathered, aggregated
+    and multiplied (row-gathered GEMM) exactly like torch indexing of them."""
+    from nts.hip import HipContext
+    hip = HipContext(0)
+    Vt, F = 35_000_000, 128
+    table = torch.empty(Vt, F, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    ids = torch.randint(2 ** 32 // F + 1, Vt, (4096,), device=DEV, generator=gen)
+    ids[:16] = torch.arange(Vt - 16, Vt, device=DEV)
+    table[ids] = torch.randn(ids.numel(), F, device=DEV, generator=gen)
+    idx = ids.to(torch.int32)
+    n = torch.tensor([idx.numel()], dtype=torch.int32, device=DEV)
+    out = torch.empty(idx.numel(), F, device=DEV)
+    hip.gather_rows(table, idx, n, idx.numel(), out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, table[ids])
+    # fused-gather aggregation: dst d sums rows idx[4d .. 4d+3] with weight 1
+    v = idx.numel() // 4
+    co = torch.arange(0, 4 * v + 1, 4, dtype=torch.int32, device=DEV)
+    ri = torch.arange(4 * v, dtype=torch.int32, device=DEV)
+    y = torch.empty(v, F, device=DEV)
+    hip.spmm_csc_fwd(co, ri, None, None, v, table, y, row_map=idx)
+    r = table[ids].view(v, 4, F)
+    ref = ((r[:, 0] + r[:, 1]) + r[:, 2]) + r[:, 3]  # edge order, 1.0 weights
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    W = torch.randn(F, 64, device=DEV, generator=gen)
+    C = torch.empty(idx.numel(), 64, device=DEV)
+    hip.gemm_gather(table, idx, W, C)
+    C2 = torch.empty_like(C)
+    hip.gemm(table[ids].contiguous(), W, C2)
+    torch.cuda.synchronize()
+    assert torch.equal(C, C2)
+    del table, out, y, C, C2
+    _free()
