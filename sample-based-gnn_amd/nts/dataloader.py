@@ -13,8 +13,11 @@
 """
 from __future__ import annotations
 
+import ctypes as C
 import io
+import os
 import pathlib
+import tempfile
 import zipfile
 from dataclasses import dataclass, field
 
@@ -23,13 +26,81 @@ import numpy as np
 MASK_TRAIN, MASK_VAL, MASK_TEST, MASK_OTHER = 0, 1, 2, 3
 MASK_UNLISTED = 0x01010101
 
+_IO_PATH = pathlib.Path(__file__).resolve().parent / "lib" / "libnts_io.so"
+_io_lib = None
+
+
+def _io():
+    """libnts_io.so (include/nts_io.h): the native loaders (built by build())."""
+    global _io_lib
+    if _io_lib is None:
+        if not _IO_PATH.exists():
+            raise ImportError(f"{_IO_PATH} missing: run __graft_entry__.build()")
+        L = C.CDLL(str(_IO_PATH))
+        L.nts_io_last_error.restype = C.c_char_p
+        L.nts_io_edge_count.argtypes = [C.c_char_p]
+        L.nts_io_edge_count.restype = C.c_int64
+        L.nts_io_read_edges.argtypes = [C.c_char_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.nts_io_read_feature_label_mask.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p,
+                                                     C.c_uint64, C.c_uint32, C.c_void_p,
+                                                     C.c_void_p, C.c_void_p, C.c_int]
+        _io_lib = L
+    return _io_lib
+
+
+def _io_check(rc):
+    if rc != 0:
+        raise IOError(_io().nts_io_last_error().decode(errors="replace"))
+
+
+def edge_count(path) -> int:
+    n = _io().nts_io_edge_count(str(path).encode())
+    if n < 0:
+        raise IOError(_io().nts_io_last_error().decode(errors="replace"))
+    return int(n)
+
+
+def read_edges(path, first: int = 0, count: int | None = None):
+    """Edges [first, first + count) of a binary edge file (memory-mapped read)."""
+    E = edge_count(path)
+    count = E - first if count is None else count
+    src = np.empty(count, np.uint32)
+    dst = np.empty(count, np.uint32)
+    _io_check(_io().nts_io_read_edges(str(path).encode(), first, count,
+                                      src.ctypes.data_as(C.c_void_p), dst.ctypes.data_as(C.c_void_p)))
+    return src, dst
+
 
 def read_edge_file(path) -> tuple[np.ndarray, np.ndarray]:
-    e = np.fromfile(path, dtype=np.uint32)
-    if e.size % 2:
-        raise ValueError(f"{path}: size is not a multiple of 8 bytes")
-    e = e.reshape(-1, 2)
-    return np.ascontiguousarray(e[:, 0]), np.ascontiguousarray(e[:, 1])
+    return read_edges(path)
+
+
+def load_edges_to_device(path, device, chunk: int = 1 << 26):
+    """Stream a binary edge file of any size into int32 device tensors
+    (src, dst) in chunks of `chunk` edges through a pinned staging buffer:
+    host memory stays bounded by the chunk, not the file (FullyRepGraph then
+    builds the CSC on the device, nts_hip_build_csc)."""
+    import torch
+    E = edge_count(path)
+    src = torch.empty(E, dtype=torch.int32, device=device)
+    dst = torch.empty(E, dtype=torch.int32, device=device)
+    stage = [torch.empty((2, min(chunk, max(E, 1))), dtype=torch.int32).pin_memory() for _ in range(2)]
+    ev = [None, None]
+    for i, first in enumerate(range(0, E, chunk)):
+        n = min(chunk, E - first)
+        buf = stage[i % 2]
+        if ev[i % 2] is not None:
+            ev[i % 2].synchronize()  # the previous copy out of this buffer is done
+        a = buf[0, :n].numpy().view(np.uint32)
+        b = buf[1, :n].numpy().view(np.uint32)
+        _io_check(_io().nts_io_read_edges(str(path).encode(), first, n,
+                                          a.ctypes.data_as(C.c_void_p), b.ctypes.data_as(C.c_void_p)))
+        src[first:first + n].copy_(buf[0, :n], non_blocking=True)
+        dst[first:first + n].copy_(buf[1, :n], non_blocking=True)
+        ev[i % 2] = torch.cuda.Event()
+        ev[i % 2].record()
+    torch.cuda.synchronize(device)
+    return src, dst
 
 
 def write_edge_file(path, src: np.ndarray, dst: np.ndarray) -> None:
@@ -48,8 +119,41 @@ def _text(path) -> str:
     return p.read_text()
 
 
-def read_feature_label_mask(feature_path, label_path, mask_path, n_vertices: int, n_features: int):
-    """readFeature_Label_Mask (core/ntsDataloador.hpp:999-1064) for one partition covering all ids."""
+def _plain_file(path, tmpdir):
+    """The path itself, or the member of a one-file .zip extracted to tmpdir
+    (the reference ships cora.featuretable zipped)."""
+    p = pathlib.Path(path)
+    if p.suffix != ".zip":
+        return p
+    with zipfile.ZipFile(p) as z:
+        name = z.namelist()[0]
+        out = pathlib.Path(tmpdir) / pathlib.Path(name).name
+        out.write_bytes(z.read(name))
+    return out
+
+
+def read_feature_label_mask(feature_path, label_path, mask_path, n_vertices: int, n_features: int,
+                            threads: int | None = None):
+    """readFeature_Label_Mask (core/ntsDataloador.hpp:999-1064) for one partition
+    covering all ids, parsed natively in parallel (libnts_io.so): the k-th
+    feature, label and mask lines belong together, the vertex id is the feature
+    line's; unlisted vertices keep zero features / label 0 / mask 0x01010101."""
+    feats = np.zeros((n_vertices, n_features), np.float32)
+    labels = np.zeros(n_vertices, np.int64)
+    masks = np.full(n_vertices, MASK_UNLISTED, np.int32)
+    threads = threads or min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS") or 16))
+    with tempfile.TemporaryDirectory() as td:
+        fp, lp, mp = (_plain_file(x, td) for x in (feature_path, label_path, mask_path))
+        _io_check(_io().nts_io_read_feature_label_mask(
+            str(fp).encode(), str(lp).encode(), str(mp).encode(), n_vertices, n_features,
+            feats.ctypes.data_as(C.c_void_p), labels.ctypes.data_as(C.c_void_p),
+            masks.ctypes.data_as(C.c_void_p), threads))
+    return feats, labels, masks
+
+
+def read_feature_label_mask_numpy(feature_path, label_path, mask_path, n_vertices: int,
+                                  n_features: int):
+    """A plain numpy restatement of the same reader (small files; tests)."""
     feats = np.zeros((n_vertices, n_features), np.float32)
     labels = np.zeros(n_vertices, np.int64)
     masks = np.full(n_vertices, MASK_UNLISTED, np.int32)
@@ -57,15 +161,52 @@ def read_feature_label_mask(feature_path, label_path, mask_path, n_vertices: int
     ids = ftab[:, 0].astype(np.int64)
     feats[ids] = ftab[:, 1:1 + n_features].astype(np.float32)
     ltab = np.loadtxt(io.StringIO(_text(label_path)), dtype=np.int64, ndmin=2)
-    # labels/masks are read line-by-line alongside the feature lines
     labels[ids] = ltab[: ids.size, 1]
     kinds = {"train": MASK_TRAIN, "eval": MASK_VAL, "val": MASK_VAL, "test": MASK_TEST}
     mlines = _text(mask_path).split()
-    mids = np.array(mlines[0::2], np.int64)
     mvals = np.array([kinds.get(s, MASK_OTHER) for s in mlines[1::2]], np.int32)
     masks[ids] = mvals[: ids.size]
-    del mids
     return feats, labels, masks
+
+
+# ---------------------------------------------------------------------------
+# PRE_SAMPLE_FILE (core/ntsBaseOp.hpp:427-497): the hot vertices of every
+# super-batch found by preSample, as
+#   uint32 counts[S]            (vertices of super-batch 0 .. S-1)
+#   uint32 ids[sum(counts)]     (super-batch 0's ids, then 1's, ...)
+# ---------------------------------------------------------------------------
+def presample_file_name(edge_file, batch_size: int, fanout_string: str, pipeline_num: int) -> str:
+    """Default name when PRE_SAMPLE_FILE is unset or missing (:432-439):
+    <edge file up to its last '.'>.pre_sample_b<B>_f<fanout>_p<pipeline>.bin"""
+    e = str(edge_file)
+    dot = e.rfind(".")
+    return e[:dot + 1] + f"pre_sample_b{batch_size}_f{fanout_string}_p{pipeline_num}.bin"
+
+
+def write_presample_file(path, counts, ids) -> None:
+    counts = np.ascontiguousarray(counts, np.uint32)
+    ids = np.ascontiguousarray(ids, np.uint32)
+    if int(counts.sum(dtype=np.uint64)) != ids.size:
+        raise ValueError("ids must hold sum(counts) vertices")
+    with open(path, "wb") as f:
+        f.write(counts.tobytes())
+        f.write(ids.tobytes())
+
+
+def read_presample_file(path, n_super_batches: int, of_rate: float = 1.0):
+    """The reader of :475-497: per super-batch i keep its first
+    (VertexId)(counts[i] * of_rate) ids.  Returns (kept counts, concatenated ids)."""
+    raw = np.fromfile(path, dtype=np.uint32)
+    if raw.size < n_super_batches:
+        raise ValueError(f"{path}: fewer than {n_super_batches} counts")
+    counts = raw[:n_super_batches].astype(np.uint64)
+    body = raw[n_super_batches:]
+    if int(counts.sum()) > body.size:
+        raise ValueError(f"{path}: truncated id section")
+    keep = np.array([int(np.float32(c) * np.float32(of_rate)) for c in counts], np.uint32)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int64)
+    ids = np.concatenate([body[s:s + k] for s, k in zip(starts, keep)]) if keep.size else body[:0]
+    return keep, ids.astype(np.uint32)
 
 
 def random_generate(n_vertices: int, n_features: int, n_classes: int, seed: int = 1,
@@ -104,6 +245,7 @@ class InputInfo:
     cache_rate: float = 0.1
     up_degree: bool = False
     gpu_num: int = 1
+    pre_sample_file: str = ""
     extra: dict = field(default_factory=dict)
 
     @property
@@ -127,6 +269,7 @@ class InputInfo:
             "DROP_RATE": ("drop_rate", float), "BATCH_SIZE": ("batch_size", int),
             "PIPELINE_NUM": ("pipeline_num", int), "CACHE_RATE": ("cache_rate", float),
             "UP_DEGREE": ("up_degree", lambda s: bool(int(s))), "GPU_NUM": ("gpu_num", int),
+            "PRE_SAMPLE_FILE": ("pre_sample_file", str),
         }
         for raw in pathlib.Path(path).read_text().splitlines():
             line = raw.strip()

@@ -57,10 +57,14 @@ def _path(base: pathlib.Path, p: str) -> pathlib.Path:
     return q if q.is_absolute() else (base / q)
 
 
-def load_inputs(info: dataloader.InputInfo, base: pathlib.Path, n_classes: int):
-    """Edge list (binary u32 pairs, streamed), features/labels/masks (text or
+def load_inputs(info: dataloader.InputInfo, base: pathlib.Path, n_classes: int, device=None):
+    """Edge list (binary u32 pairs; with `device`, streamed in chunks straight
+    into int32 device tensors), features/labels/masks (text or
     FEATURE_FILE:random)."""
-    src, dst = dataloader.read_edge_file(_path(base, info.edge_file))
+    if device is None:
+        src, dst = dataloader.read_edge_file(_path(base, info.edge_file))
+    else:
+        src, dst = dataloader.load_edges_to_device(_path(base, info.edge_file), device)
     V = info.vertices
     F = info.layers[0]
     if info.feature_file in ("", "random"):
@@ -113,9 +117,10 @@ def run(cfg_path, epochs=None, device=0, out=print) -> dict:
     dev = torch.device("cuda", device)
     E = host.ext()
     t0 = time.time()
-    src, dst, feats, labels, masks = load_inputs(info, base, n_classes)
-    G = E.FullyRepGraph.from_edges(torch.from_numpy(src.view(np.int32)).to(dev),
-                                   torch.from_numpy(dst.view(np.int32)).to(dev), info.vertices)
+    src, dst, feats, labels, masks = load_inputs(info, base, n_classes, device=dev)
+    G = E.FullyRepGraph.from_edges(src, dst, info.vertices)
+    n_edges = src.numel()
+    del src, dst
     feat = torch.from_numpy(feats).to(dev)
     lab = torch.from_numpy(labels).to(dev)
     ids = {k: np.nonzero(masks == v)[0].astype(np.int32) for k, v in
@@ -126,7 +131,7 @@ def run(cfg_path, epochs=None, device=0, out=print) -> dict:
     drv = build_driver(E, info, G, feat, lab, train, dev, comm)
     if rank == 0:
         out(f"GNNmini::Engine[MI355X.GPU.{info.algorithm}] running [{epochs}] Epochs "
-            f"(V={info.vertices}, E={src.size}, layers {info.layer_string}, fanout "
+            f"(V={info.vertices}, E={n_edges}, layers {info.layer_string}, fanout "
             f"{info.fanout_string}, batch {info.batch_size}; loaded in {time.time() - t0:.1f}s)")
     hist = []
     for ep in range(epochs):
