@@ -122,6 +122,16 @@ typedef struct {
                                       then allow e + v sources.               */
   uint32_t *csr_edge_id;           /* [e_cap] or NULL: CSC edge id of each CSR
                                       slot (with row_offset)                   */
+  const uint32_t *omit_map;        /* [V] or NULL: a dst d with omit_map[d] ==
+                                      omit_key samples no neighbours
+                                      (sample_gpu_fast_omit, bottom layer of
+                                      the PD-cache toolkits,
+                                      core/ntsFastSampler.hpp:711-915)         */
+  uint32_t omit_key;
+  const uint32_t *omit_loc;        /* [V] with omit_map: the PD cache row of d */
+  uint32_t *omit_row;              /* [v_cap] with omit_map: omit_loc[dst[i]]
+                                      for an omitted dst i, else NTS_NOT_CACHED
+                                      (the batch's own snapshot of the cache) */
 } nts_sampcsc_dev;
 
 /* ---- context ------------------------------------------------------------ */
@@ -302,6 +312,41 @@ int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx *ctx, const uint32_t *column_offset,
                                 const uint32_t *v, uint32_t v_cap, const float *g_out,
                                 uint64_t ld_gout, uint32_t feature_size, float *g_in,
                                 uint64_t ld_gin);
+
+/* ---- NeutronOrch PD cache (toolkits/GCN_SAMPLE_PD_CACHE.hpp) -------------- */
+/* preSample's hot-vertex count (get_most_neighbor, core/ntsBaseOp.hpp:330-404):
+ * old[seeds[i]] = 1; then (layers - 1) times new[u] += old[v] for every
+ * in-neighbour u of v in the CSC (column_offset[v] .. [v+1]); counts = the
+ * last `new` (all zeros when layers == 1, as the reference's).  tmp: [V]. */
+int nts_hip_presample_counts(nts_hip_ctx *ctx, const nts_graph_dev *graph, const uint32_t *seeds,
+                             uint32_t n_seeds, int layers, uint32_t *counts, uint32_t *tmp);
+/* ... and its selection: total = (number of non-zero counts) + 1 (V when none
+ * is zero), n = (uint32)((float)total * cache_rate) (clamped to V), pivot =
+ * the n-th largest count (0-based, descending), out_ids = the first n vertex
+ * ids in ascending order whose count >= pivot (the reference's single-thread
+ * order), *out_n = n (device scalar).  out_ids: [V]. */
+int nts_hip_presample_select(nts_hip_ctx *ctx, const uint32_t *counts, uint64_t n_vertices,
+                             float cache_rate, uint32_t *out_ids, uint32_t *out_n);
+/* set_cache_index for one super-batch: cache_map[ids[i]] = key,
+ * cache_location[ids[i]] = i for i < n (gnndatum->set_cache_index). */
+int nts_hip_pd_set_cache(nts_hip_ctx *ctx, const uint32_t *ids, uint32_t n, uint32_t key,
+                         uint32_t *cache_map, uint32_t *cache_location);
+/* load_share_embedding (dev_load_share_embedding_kernel,
+ * cuda/ntsCUDATransferKernel.cuh:454-500): for the bottom layer's dsts
+ * i < *v, emb[i,:] = share[omit_row[i],:] when omit_row[i] != NTS_NOT_CACHED
+ * (omit_row: written by nts_hip_sample_layer with omit_map; rows of other dsts
+ * untouched).  The reference tests cache_map[dst[i]] == super_batch_id at
+ * this point; the sampled layer's own record is the same decision, taken when
+ * it was sampled, so a later super-batch may already reuse cache_map. */
+int nts_hip_pd_load_share(nts_hip_ctx *ctx, const uint32_t *omit_row, const uint32_t *v,
+                          uint32_t v_cap, const float *share, uint64_t ld_share,
+                          uint32_t feature_size, float *emb, uint64_t ld_emb);
+/* vertexForward's activation alone, y = dropout(relu(x), p) with the keep
+ * bits of nts_hip_gemm_relu_dropout_f32 (same seed/offset/(row, col) keys):
+ * after a GEMM whose rows are replaced by the PD cache. */
+int nts_hip_relu_dropout_f32(nts_hip_ctx *ctx, uint32_t rows, uint32_t feature_size,
+                             const float *x, uint64_t ldx, float p, uint64_t seed,
+                             uint64_t offset, float *y, uint64_t ldy);
 
 /* ---- GAT layer on a merged src/dst sampled block ------------------------- */
 /* The GAT_SAMPLE_ALL_GPU layer (toolkits/GAT_SAMPLE_ALL_GPU.hpp:308-391:

@@ -71,6 +71,9 @@ def lib():
         L.orc_get_feature.argtypes = [U32, P, P, U32, P, I]
         L.orc_fuse_fwd.argtypes = [U32, P, P, P, P, P, P, P, U32, P, I, I]
         L.orc_fuse_bwd.argtypes = [U32, U32, P, P, P, P, P, P, P, U32, P, I, I]
+        L.orc_sampler_set_omit.argtypes = [P, P, U32]
+        L.orc_pushdown_fwd.argtypes = [U32, U32, P, P, P, P, P, U32, P]
+        L.orc_presample.argtypes = [U64, P, P, P, U32, I, C.c_float, P, P, P]
         _libs[_active] = L
     return _libs[_active]
 
@@ -118,6 +121,12 @@ class Sampler:
         if getattr(self, "h", None):
             self.L_.orc_sampler_free(self.h)
             self.h = None
+
+    def set_omit(self, omit_map=None, omit_key=0):
+        """sample_gpu_fast_omit: in the last layer, dsts with omit_map[d] == key
+        sample nothing (None: off)."""
+        self._omit = None if omit_map is None else np.ascontiguousarray(omit_map, np.uint32)
+        self.L_.orc_sampler_set_omit(self.h, _p(self._omit), int(omit_key))
 
     def sample(self, seeds, batch_seq=0, weight_type=W_SUM, build_csr=True, threads=1):
         seeds = np.ascontiguousarray(seeds, np.uint32)
@@ -213,3 +222,29 @@ def get_feature_cached(idx, cache, cache_map, host_table):
     out[hot] = cache[slots[hot]]
     out[~hot] = host_table[idx[~hot]]
     return out
+
+
+def pushdown_fwd(layer, X, v_begin=0, v_end=None):
+    """PushDownBatchOp::forward over dst rows [v_begin, v_end) of a sampled
+    layer (global feature table X, the layer's forward weights)."""
+    X = np.ascontiguousarray(X, np.float32)
+    v_end = layer["v_size"] if v_end is None else v_end
+    Y = np.empty((v_end - v_begin, X.shape[1]), np.float32)
+    lib().orc_pushdown_fwd(v_begin, v_end, _p(layer["column_offset"]), _p(layer["row_indices"]),
+                           _p(layer["source"]), _p(layer["edge_weight_forward"]), _p(X),
+                           X.shape[1], _p(Y))
+    return Y
+
+
+def presample(col, rows, seeds, layers, cache_rate):
+    """get_most_neighbor of one super-batch: (counts [V], hot ids)."""
+    col = np.ascontiguousarray(col, np.uint64)
+    rows = np.ascontiguousarray(rows, np.uint32)
+    seeds = np.ascontiguousarray(seeds, np.uint32)
+    V = col.size - 1
+    counts = np.empty(V, np.uint32)
+    ids = np.empty(V, np.uint32)
+    n = np.zeros(1, np.uint32)
+    lib().orc_presample(V, _p(col), _p(rows), _p(seeds), seeds.size, layers, float(cache_rate),
+                        _p(counts), _p(ids), _p(n))
+    return counts, ids[:int(n[0])].copy()

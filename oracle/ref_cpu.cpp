@@ -122,6 +122,10 @@ struct Sampler {
   std::vector<Layer> layers;
   std::vector<uint32_t> src_index;
   std::vector<uint64_t> bitmap;
+  // sample_gpu_fast_omit (core/ntsFastSampler.hpp:711-915): in the LAST layer a
+  // dst with omit_map[dst] == omit_key samples nothing
+  const uint32_t* omit_map = nullptr;
+  uint32_t omit_key = 0;
 };
 
 // std::uniform_int_distribution<int>(0, range-1) in its libstdc++ <= 10 form
@@ -192,6 +196,12 @@ void* orc_sampler_new(uint64_t V, const uint64_t* off, const uint32_t* rows,
 
 void orc_sampler_free(void* h) { delete (Sampler*)h; }
 
+void orc_sampler_set_omit(void* h, const uint32_t* omit_map, uint32_t omit_key) {
+  Sampler& s = *(Sampler*)h;
+  s.omit_map = omit_map;
+  s.omit_key = omit_key;
+}
+
 // FastSampler::sample_fast (core/ntsFastSampler.hpp:962-1140) for one batch,
 // single sampler thread.  threads > 1 runs the dst loops under OpenMP with a
 // thread-local generator per worker like the reference (timing baseline only;
@@ -223,6 +233,7 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
       ly.column_offset[k] = acc;
       uint32_t d = ly.destination[k];
       uint32_t nbrs = (uint32_t)(s.off[d + 1] - s.off[d]);
+      if (s.omit_map && i == L - 1 && s.omit_map[d] == s.omit_key) nbrs = 0;  // omit
       int f = s.fanout[i];
       uint32_t ret = (f < 0) ? nbrs : std::min(nbrs, (uint32_t)f);
       acc += ret;
@@ -241,6 +252,7 @@ int orc_sample_batch(void* h, const uint32_t* seeds, uint32_t B, uint64_t batch_
       uint32_t deg = (uint32_t)(s.off[d + 1] - beg);
       uint32_t c = ly.column_offset[k];
       uint32_t num = ly.column_offset[k + 1] - c;
+      if (num == 0) return;
       if (deg > fan_u) {
         draw_distinct(s, gen, d, (uint32_t)i, batch_seq, deg, num, pos);
         for (uint32_t p = 0; p < num; ++p) ly.sample_ans[c + p] = s.rows[beg + pos[p]];
@@ -409,6 +421,68 @@ int orc_mt_state(void* h, uint32_t* out625) {
     ss >> x;
     out625[i] = (uint32_t)x;
   }
+  return 0;
+}
+
+// nts::op::PushDownBatchOp::forward (core/ntsPushdownGraphOp.hpp:108-160): rows
+// [v_begin, v_end) of one sampled layer, Y[d - v_begin] = sum_e e_w_f[e] *
+// X[source[row_indices[e]]] (the GLOBAL feature table, the sampled forward
+// weights), zero-initialised, nts_comp arithmetic (mul then add)
+int orc_pushdown_fwd(uint32_t v_begin, uint32_t v_end, const uint32_t* co, const uint32_t* ri,
+                     const uint32_t* source, const float* ewf, const float* X, uint32_t F,
+                     float* Y) {
+  for (uint32_t d = v_begin; d < v_end; ++d) {
+    float* out = Y + (uint64_t)(d - v_begin) * F;
+    std::fill(out, out + F, 0.0f);
+    for (uint32_t e = co[d]; e < co[d + 1]; ++e) {
+      const float* in = X + (uint64_t)source[ri[e]] * F;
+      const float w = ewf[e];
+      for (uint32_t k = 0; k < F; ++k) out[k] = in[k] * w + out[k];
+    }
+  }
+  return 0;
+}
+
+// preSample's get_most_neighbor (core/ntsBaseOp.hpp:330-404, the cache_rate
+// overload) for one super-batch, single thread:
+//   old[seeds] = 1; (layers-1) x { new = 0; new[u] += old[v] for u in the CSC
+//   segment of v with old[v] > 0; swap }; counts = new
+//   sorted = counts descending; total = (index of the first 0) + 1
+//   (V when there is none — the reference leaves it unset); n = (VertexId)
+//   (total * cache_rate) (float product); pivot = sorted[n] (clamped: n <= V,
+//   pivot 0 at n == V); ids = the first n vertices, ascending, with
+//   counts >= pivot (the reference's OpenMP loop visits them in this order
+//   on one thread)
+int orc_presample(uint64_t V, const uint64_t* off, const uint32_t* rows, const uint32_t* seeds,
+                  uint32_t n_seeds, int layers, float cache_rate, uint32_t* counts_out,
+                  uint32_t* ids_out, uint32_t* n_out) {
+  std::vector<uint32_t> oldc(V, 0), newc(V, 0);
+  for (uint32_t i = 0; i < n_seeds; ++i) oldc[seeds[i]] = 1;
+  for (int layer = 1; layer < layers; ++layer) {
+    if (layer != 1) {
+      std::swap(oldc, newc);
+      std::fill(newc.begin(), newc.end(), 0u);
+    }
+    for (uint64_t v = 0; v < V; ++v)
+      if (oldc[v] > 0)
+        for (uint64_t e = off[v]; e < off[v + 1]; ++e) newc[rows[e]] += oldc[v];
+  }
+  std::vector<uint32_t> sorted(newc);
+  std::sort(sorted.begin(), sorted.end(), [](uint32_t a, uint32_t b) { return a > b; });
+  uint64_t total = V;
+  for (uint64_t i = 0; i < V; ++i)
+    if (sorted[i] == 0) {
+      total = i + 1;
+      break;
+    }
+  uint64_t n = (uint64_t)((float)total * cache_rate);
+  if (n > V) n = V;
+  const uint32_t pivot = n < V ? sorted[n] : 0u;
+  uint64_t k = 0;
+  for (uint64_t v = 0; v < V && k < n; ++v)
+    if (newc[v] >= pivot) ids_out[k++] = (uint32_t)v;
+  *n_out = (uint32_t)n;
+  if (counts_out) std::memcpy(counts_out, newc.data(), V * sizeof(uint32_t));
   return 0;
 }
 

@@ -71,9 +71,15 @@ struct Draw {
 // ---------------------------------------------------------------------------
 // per-layer kernels
 // ---------------------------------------------------------------------------
+// omit_map (sample_gpu_fast_omit, core/ntsFastSampler.hpp:711-915, kernel
+// sample_processing_get_co_gpu_kernel_omit cuda/ntsCUDATransferKernel.cuh:795-818):
+// a dst with omit_map[dst] == omit_key samples no neighbours (its bottom-layer
+// embedding comes from the PD cache)
 __global__ void k_count(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
                         const uint32_t* v_in, uint32_t v_cap, int fanout,
-                        uint32_t* __restrict__ co, uint32_t* sizes) {
+                        uint32_t* __restrict__ co, uint32_t* sizes,
+                        const uint32_t* __restrict__ omit_map, uint32_t omit_key,
+                        const uint32_t* __restrict__ omit_loc, uint32_t* __restrict__ omit_row) {
   const uint32_t v_req = *v_in;
   const uint32_t v = min(v_req, v_cap);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -83,6 +89,11 @@ __global__ void k_count(const uint64_t* __restrict__ goff, const uint32_t* __res
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < v; i += gridDim.x * blockDim.x) {
     uint32_t d = dst[i];
     uint32_t deg = (uint32_t)(goff[d + 1] - goff[d]);
+    if (omit_map) {
+      const bool om = omit_map[d] == omit_key;
+      if (om) deg = 0;
+      if (omit_row) omit_row[i] = om ? omit_loc[d] : 0xFFFFFFFFu;
+    }
     co[i] = (fanout < 0) ? deg : min(deg, (uint32_t)fanout);
   }
 }
@@ -624,6 +635,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   NTS_CHECK_ARG(g->n_vertices <= 0xFFFFFFFFull, "vertex count exceeds uint32 ids");
   const bool csr = o->row_offset != nullptr;
   NTS_CHECK_ARG(!csr || o->column_indices, "CSR requested without column_indices");
+  NTS_CHECK_ARG(!o->omit_row || (o->omit_map && o->omit_loc), "omit_row needs omit_map + omit_loc");
   NTS_HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   const uint64_t V = g->n_vertices;
@@ -655,7 +667,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
 
   // 1) per-dst counts -> column_offset, e_size
   hipLaunchKernelGGL(k_count, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                     o->v_size, o->v_cap, fanout, o->column_offset, o->sizes);
+                     o->v_size, o->v_cap, fanout, o->column_offset, o->sizes, o->omit_map,
+                     o->omit_key, o->omit_loc, o->omit_row);
   NTS_LAUNCH_CHECK();
   NTS_RET(scan_exclusive<uint32_t>(o->column_offset, o->column_offset, o->sizes, o->v_cap,
                                    t_scan_co, st));

@@ -34,7 +34,9 @@ EXPORTED = (
     "nts_hip_sample_layer", "nts_hip_gather_rows", "nts_hip_gather_labels",
     "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
     "nts_hip_spmm_csc_fwd_act", "nts_hip_spmm_csr_bwd_masked", "nts_hip_gemm_gather_f32",
-    "nts_hip_gemm_tn_gather_f32", "nts_hip_act_backward",
+    "nts_hip_gemm_tn_gather_f32", "nts_hip_act_backward", "nts_hip_presample_counts",
+    "nts_hip_presample_select", "nts_hip_pd_set_cache", "nts_hip_pd_load_share",
+    "nts_hip_relu_dropout_f32",
     "nts_hip_gemm_f32", "nts_hip_gemm_relu_dropout_f32", "nts_hip_gemm_tn_masked_f32",
     "nts_hip_linear_xent_fwd", "nts_hip_linear_xent_bwd", "nts_hip_linear_xent_train", "nts_hip_adam", "nts_hip_comm_unique_id", "nts_hip_comm_init", "nts_hip_comm_destroy",
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
@@ -64,6 +66,8 @@ class SampCSCDev(C.Structure):
         ("edge_weight_forward", C.c_void_p), ("row_offset", C.c_void_p),
         ("column_indices", C.c_void_p), ("edge_weight_backward", C.c_void_p),
         ("sizes", C.c_void_p), ("dst_local_id", C.c_void_p), ("csr_edge_id", C.c_void_p),
+        ("omit_map", C.c_void_p), ("omit_key", C.c_uint32), ("omit_loc", C.c_void_p),
+        ("omit_row", C.c_void_p),
     ]
 
 
@@ -100,6 +104,11 @@ def lib() -> C.CDLL:
         "nts_hip_spmm_csc_fwd_act": ([P, P, P, P, P, U32, P, U64, U32, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd_masked": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
         "nts_hip_act_backward": ([P, U32, U32, P, U64, P, U64, F, P, U64], I),
+        "nts_hip_presample_counts": ([P, C.POINTER(GraphDev), P, U32, I, P, P], I),
+        "nts_hip_presample_select": ([P, P, U64, F, P, P], I),
+        "nts_hip_pd_set_cache": ([P, P, U32, U32, P, P], I),
+        "nts_hip_pd_load_share": ([P, P, P, U32, P, U64, U32, P, U64], I),
+        "nts_hip_relu_dropout_f32": ([P, U32, U32, P, U64, F, U64, U64, P, U64], I),
         "nts_hip_gemm_gather_f32": ([P, I, I, I, P, U64, P, P, U64, P, U64], I),
         "nts_hip_gemm_tn_gather_f32": ([P, I, I, I, P, U64, P, P, U64, P, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),

@@ -177,6 +177,30 @@ class HipContext:
         check(self.lib.nts_hip_act_backward(self.h, rows, F, ptr(g), g.stride(0), ptr(x_act),
                                             x_act.stride(0), float(scale), ptr(out), out.stride(0)))
 
+    # ---- PD cache ----------------------------------------------------------------
+    def presample_counts(self, graph: "DeviceGraph", seeds, layers: int, counts, tmp):
+        g = graph.as_struct()
+        check(self.lib.nts_hip_presample_counts(self.h, C.byref(g), ptr(seeds), seeds.numel(),
+                                                layers, ptr(counts), ptr(tmp)))
+
+    def presample_select(self, counts, cache_rate: float, out_ids, out_n):
+        check(self.lib.nts_hip_presample_select(self.h, ptr(counts), counts.numel(),
+                                                float(cache_rate), ptr(out_ids), ptr(out_n)))
+
+    def pd_set_cache(self, ids, key: int, cache_map, cache_location):
+        check(self.lib.nts_hip_pd_set_cache(self.h, ptr(ids), ids.numel(), key, ptr(cache_map),
+                                            ptr(cache_location)))
+
+    def pd_load_share(self, omit_row, v_dev, v_cap, share, emb):
+        F = emb.shape[1]
+        check(self.lib.nts_hip_pd_load_share(self.h, ptr(omit_row), ptr(v_dev), v_cap, ptr(share),
+                                             share.stride(0), F, ptr(emb), emb.stride(0)))
+
+    def relu_dropout(self, x, y, p=0.0, seed=0, offset=0):
+        rows, F = x.shape
+        check(self.lib.nts_hip_relu_dropout_f32(self.h, rows, F, ptr(x), x.stride(0), float(p),
+                                                int(seed), int(offset), ptr(y), y.stride(0)))
+
     def gemm_gather(self, A, rows, B, C):
         """C = A[rows] @ B (rows: int32 device tensor of row ids)."""
         M, K, N = rows.numel(), A.shape[1], B.shape[1]
@@ -288,6 +312,9 @@ class LayerBuffers:
     csr: bool = True
     weights: bool = True
     merge: bool = False  # dsts merged into the frontier (GAT): dst_local_id + csr_edge_id
+    omit_map: torch.Tensor | None = None  # PD cache: dsts with omit_map[d] == omit_key sample nothing
+    omit_key: int = 0
+    omit_loc: torch.Tensor | None = None  # ... their cache rows, recorded per dst in t["omit_row"]
     t: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -309,6 +336,7 @@ class LayerBuffers:
             self.t["row_offset"] = self.t["column_indices"] = self.t["edge_weight_backward"] = None
         self.t["dst_local_id"] = _u32(max(self.v_cap, 1), d) if self.merge else None
         self.t["csr_edge_id"] = _u32(max(self.e_cap, 1), d) if (self.merge and self.csr) else None
+        self.t["omit_row"] = _u32(max(self.v_cap, 1), d) if self.omit_map is not None else None
 
     def __getattr__(self, k):
         t = self.__dict__.get("t")
@@ -323,7 +351,8 @@ class LayerBuffers:
             ptr(t["column_offset"]), ptr(t["row_indices"]), ptr(t["sample_ans"]), ptr(t["edge_dst"]),
             ptr(t["source"]), ptr(t["edge_weight_forward"]), ptr(t["row_offset"]),
             ptr(t["column_indices"]), ptr(t["edge_weight_backward"]), ptr(t["sizes"]),
-            ptr(t["dst_local_id"]), ptr(t["csr_edge_id"]))
+            ptr(t["dst_local_id"]), ptr(t["csr_edge_id"]), ptr(self.omit_map), self.omit_key,
+            ptr(self.omit_loc), ptr(t.get("omit_row")))
 
     def sizes_host(self):
         s = self.t["sizes"].cpu().tolist()

@@ -38,7 +38,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                seed=2000, hip_gemm=True, pipeline=True, transform_first=-1,
                early_aggregate=True, sampler_priority=True, fuse_activation=True,
                fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0,
-               up_degree=False, gat=False):
+               up_degree=False, gat=False, pd_cache=False, pd_rate=0.2, pd_super_batch=4):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -66,6 +66,9 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.cache_rate = float(cache_rate)
     c.up_degree = bool(up_degree)
     c.gat = bool(gat)
+    c.pd_cache = bool(pd_cache)
+    c.pd_rate = float(pd_rate)
+    c.pd_super_batch = int(pd_super_batch)
     c.shuffle = bool(shuffle)
     c.profile = bool(profile)
     c.seed = int(seed)

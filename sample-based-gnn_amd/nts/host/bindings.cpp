@@ -158,6 +158,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
       .def_readwrite("pipeline", &GCNConfig::pipeline)
       .def_readwrite("transform_first", &GCNConfig::transform_first)
+      .def_readwrite("pd_cache", &GCNConfig::pd_cache)
+      .def_readwrite("pd_rate", &GCNConfig::pd_rate)
+      .def_readwrite("pd_super_batch", &GCNConfig::pd_super_batch)
       .def_readwrite("early_aggregate", &GCNConfig::early_aggregate)
       .def_readwrite("sampler_priority", &GCNConfig::sampler_priority)
       .def_readwrite("fuse_loss", &GCNConfig::fuse_loss)
@@ -190,6 +193,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("seeds"), py::arg("batch_seq") = 0)
       .def("set_weights", &GCN_SAMPLE_ALLGPU_impl::set_weights)
       .def("train_correct", &GCN_SAMPLE_ALLGPU_impl::train_correct)
+      .def("presample", &GCN_SAMPLE_ALLGPU_impl::presample)
+      .def("set_presample", &GCN_SAMPLE_ALLGPU_impl::set_presample)
       .def("reset_correct", &GCN_SAMPLE_ALLGPU_impl::reset_correct)
       .def("evaluate",
            [](GCN_SAMPLE_ALLGPU_impl& d, const torch::Tensor& nids) {

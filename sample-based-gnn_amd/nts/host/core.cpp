@@ -312,6 +312,14 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
     o.sizes = dptr<uint32_t>(s->sizes);
     o.dst_local_id = dptr<uint32_t>(s->dst_local_id);  // undefined (NULL) unless merged
     o.csr_edge_id = dptr<uint32_t>(s->csr_edge_id);
+    if (l == layer - 1 && omit_map) {
+      if (!s->omit_row.defined())
+        s->omit_row = torch::empty({std::max<int64_t>(s->v_cap, 1)}, u32_opts(whole_graph->device));
+      o.omit_map = omit_map;
+      o.omit_key = omit_key;
+      o.omit_loc = omit_loc;
+      o.omit_row = dptr<uint32_t>(s->omit_row);
+    }
     const double tl = now_s();
     hip_check(nts_hip_sample_layer(cs.ctx(), &g, fanout[l], l, batch_seq, rng_mode, wt, &o),
               "nts_hip_sample_layer");
@@ -880,6 +888,43 @@ NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
                       NtsStream* cs) {
   return HipLinearActFn::apply(x, W, p, (int64_t)seed, (int64_t)offset,
                                reinterpret_cast<int64_t>(cs));
+}
+
+// dropout(relu(x)) on its own (nts_hip_relu_dropout_f32, the GEMM epilogue's
+// keep bits); backward dx = dy ⊙ [y > 0] / (1-p) (nts_hip_act_backward)
+struct HipActFn : public torch::autograd::Function<HipActFn> {
+  static NtsVar forward(AutogradContext* ctx, NtsVar x, double p, int64_t seed, int64_t offset,
+                        int64_t cs_ptr) {
+    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    NtsVar xc = row_major(x);
+    NtsVar y = torch::empty({xc.size(0), xc.size(1)}, xc.options());
+    hip_check(nts_hip_relu_dropout_f32(cs->ctx(), (uint32_t)xc.size(0), (uint32_t)xc.size(1),
+                                       xc.data_ptr<float>(), (uint64_t)xc.stride(0), (float)p,
+                                       (uint64_t)seed, (uint64_t)offset, y.data_ptr<float>(),
+                                       (uint64_t)y.size(1)),
+              "nts_hip_relu_dropout_f32");
+    ctx->save_for_backward({y});
+    ctx->saved_data["cs"] = cs_ptr;
+    ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
+    return y;
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    NtsVar y = ctx->get_saved_variables()[0];
+    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
+    NtsVar g = grads[0].contiguous();
+    NtsVar dx = torch::empty_like(y);
+    hip_check(nts_hip_act_backward(cs->ctx(), (uint32_t)y.size(0), (uint32_t)y.size(1),
+                                   g.data_ptr<float>(), (uint64_t)g.size(1), y.data_ptr<float>(),
+                                   (uint64_t)y.size(1),
+                                   (float)ctx->saved_data["scale"].toDouble(),
+                                   dx.data_ptr<float>(), (uint64_t)dx.size(1)),
+              "nts_hip_act_backward");
+    return {dx, NtsVar(), NtsVar(), NtsVar(), NtsVar()};
+  }
+};
+
+NtsVar hip_relu_dropout(const NtsVar& x, double p, uint64_t seed, uint64_t offset, NtsStream* cs) {
+  return HipActFn::apply(x, p, (int64_t)seed, (int64_t)offset, reinterpret_cast<int64_t>(cs));
 }
 
 NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,

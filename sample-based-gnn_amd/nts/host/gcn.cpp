@@ -65,7 +65,8 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // narrows the rows — the aggregation then gathers F_out-wide rows of X W
   // (a table that stays in the Infinity Cache) instead of F_in-wide feature
   // rows, at the price of a GEMM over the src rows instead of the dst rows.
-  const bool tf_ok = L >= 2 && !cfg.gat && !fcache && cfg.hip_gemm && cfg.fuse_activation;
+  const bool tf_ok = L >= 2 && !cfg.gat && !fcache && cfg.hip_gemm && cfg.fuse_activation &&
+                     !cfg.pd_cache;
   if (cfg.transform_first == 1)
     TORCH_CHECK(tf_ok, "transform_first needs >= 2 layers, the MFMA GEMMs with the fused "
                        "activation, no GAT and no feature cache");
@@ -105,7 +106,14 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // feature table only (not on the weights), so it is issued right behind the
   // sampling, on the sampling stream: with the pipeline it runs while the
   // previous batch trains (HBM-bound gather next to MFMA-bound GEMMs).
-  early_ = cfg.early_aggregate && cfg.fused_gather && !cfg.gat && !tf_;
+  early_ = cfg.early_aggregate && cfg.fused_gather && !cfg.gat && !tf_ && !cfg.pd_cache;
+  if (cfg.pd_cache) {
+    TORCH_CHECK(!cfg.gat && L >= 2 && cfg.hip_gemm && cfg.pd_super_batch >= 1 &&
+                    cfg.pd_rate >= 0.0,
+                "PD cache: GCN/GraphSAGE with >= 2 layers on the MFMA GEMMs");
+    pd_cache_map_ = torch::full({(int64_t)graph->global_vertices}, -1, u32_opts(graph->device));
+    pd_cache_loc_ = torch::zeros({(int64_t)graph->global_vertices}, u32_opts(graph->device));
+  }
   for (int i = 0; i < nslots_; ++i) {
     TORCH_CHECK(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming) == hipSuccess,
                 "hipEventCreate");
@@ -119,6 +127,10 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   }
   correct_ = torch::zeros({1}, u32_opts(graph->device));
   init_nn();
+  if (cfg.pd_cache) {  // preSample on the device (the Python runner may replace it)
+    auto hot = presample();
+    set_presample(hot.first, hot.second);
+  }
 }
 
 GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
@@ -158,8 +170,10 @@ void GCN_SAMPLE_ALLGPU_impl::mark(const char* what, NtsStream& st) {
 
 void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
   mark("S<", st);
+  if (cfg.pd_cache) pd_issue(slot, st);
   sampler->issue_gpu_sample(cfg.batch_size, slot, st,
                             cfg.gat ? WeightType::None : cfg.weight_type);
+  sampler->omit_map = nullptr;
   if (early_) {
     auto guard = st.guard();
     const int L = (int)P.size();
@@ -302,6 +316,33 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
     if (bottom && cfg.profile)
       prof.end(KernelProfiler::BOTTOM_AGG, (hipStream_t)cs->stream(),
                bottom_bytes(sg, cfg.fused_gather));
+    if (bottom && pd_active_) {
+      // GCN_SAMPLE_PD_CACHE::Forward (toolkits/GCN_SAMPLE_PD_CACHE.hpp:916-945):
+      // Y W, the cached dsts' rows replaced by the super-batch's (A X) W
+      // (load_share_embedding), then relu + dropout.  The omitted dsts have no
+      // sampled edges, so their rows of Y are zero and add nothing to dW.
+      sampCSC* s = sg->sampled_sgs[hop];
+      const uint64_t off = dropout_calls_++;
+      const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
+      X = ctx.runVertexForward(
+          [&](NtsVar& a) {
+            NtsVar Z = P[0]->forward(a);
+            hip_check(nts_hip_pd_load_share(cs->ctx(), dptr<uint32_t>(s->omit_row), nullptr,
+                                            s->v_size, pd_share_.data_ptr<float>(),
+                                            (uint64_t)pd_share_.stride(0), (uint32_t)Z.size(1),
+                                            Z.data_ptr<float>(), (uint64_t)Z.stride(0)),
+                      "nts_hip_pd_load_share");
+            if (l == L - 1) return Z.log_softmax(1);
+            return hip_relu_dropout(Z, p, (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1, off,
+                                    cs.get());
+          },
+          Y);
+      if (keep) {
+        acts.push_back(Y.detach());
+        acts.push_back(X.detach());
+      }
+      continue;
+    }
     if (loss_target && l == L - 1)  // vertexForward + Loss of the last layer, fused
       X = ctx.runVertexForward(
           [&](NtsVar& a) {
@@ -411,6 +452,7 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[slot], 0) == hipSuccess,
               "hipStreamWaitEvent");
   double t1 = now_s();
+  if (cfg.pd_cache) pd_train(slot);
   mark("T<", *cs);
   sampler->load_label_gpu(*cs, sg, target, L_GT);
   ctx.train();
@@ -437,6 +479,7 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
     }
     ctx.self_backward(false);
   }
+  pd_active_ = false;
   Update();
   for (auto* p : P) p->zero_grad();
   TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)cs->stream()) == hipSuccess,
@@ -557,6 +600,140 @@ double GCN_SAMPLE_ALLGPU_impl::evaluate(const std::vector<VertexId>& nids) {
   eval_seq = s.batch_seq;
   cs->synchronize();
   return (double)(uint32_t)correct.cpu().item<int32_t>() / (double)nids.size();
+}
+
+// ---------------------------------------------------------------------------
+// PD cache
+std::pair<std::vector<uint32_t>, std::vector<uint32_t>> GCN_SAMPLE_ALLGPU_impl::presample() {
+  auto guard = cs->guard();
+  const std::vector<VertexId>& ids = sampler->sample_nids;  // shuffled like training
+  const uint64_t sbs = (uint64_t)cfg.batch_size * (uint64_t)cfg.pd_super_batch;
+  const uint64_t n_sb = (ids.size() + sbs - 1) / sbs;
+  const uint64_t V = graph->global_vertices;
+  NtsVar seeds = torch::empty({(int64_t)std::max<size_t>(ids.size(), 1)}, u32_opts(graph->device));
+  if (!ids.empty())
+    seeds.narrow(0, 0, (int64_t)ids.size())
+        .copy_(torch::from_blob((void*)ids.data(), {(int64_t)ids.size()}, torch::kInt32));
+  NtsVar counts = torch::empty({(int64_t)V}, u32_opts(graph->device));
+  NtsVar tmp = torch::empty({(int64_t)V}, u32_opts(graph->device));
+  NtsVar out = torch::empty({(int64_t)V}, u32_opts(graph->device));
+  NtsVar n_dev = torch::empty({1}, u32_opts(graph->device));
+  const nts_graph_dev g = graph->dev();
+  std::vector<uint32_t> cnt(n_sb), all;
+  // get_most_neighbor over `layers` = the number of GNN layers (the driver's
+  // gnnctx->layer_size.size() - 1, toolkits/GCN_SAMPLE_PD_CACHE.hpp:989)
+  const int layers = (int)cfg.fanout.size();
+  for (uint64_t b = 0; b < n_sb; ++b) {
+    const uint64_t beg = b * sbs, n = std::min<uint64_t>(sbs, ids.size() - beg);
+    hip_check(nts_hip_presample_counts(cs->ctx(), &g, dptr<uint32_t>(seeds) + beg, (uint32_t)n,
+                                       layers, dptr<uint32_t>(counts), dptr<uint32_t>(tmp)),
+              "nts_hip_presample_counts");
+    hip_check(nts_hip_presample_select(cs->ctx(), dptr<uint32_t>(counts), V, (float)cfg.pd_rate,
+                                       dptr<uint32_t>(out), dptr<uint32_t>(n_dev)),
+              "nts_hip_presample_select");
+    cs->synchronize();
+    cnt[b] = (uint32_t)n_dev.cpu().item<int32_t>();
+    auto h = out.narrow(0, 0, (int64_t)cnt[b]).cpu();
+    const uint32_t* hp = reinterpret_cast<const uint32_t*>(h.data_ptr<int32_t>());
+    all.insert(all.end(), hp, hp + cnt[b]);
+  }
+  return {cnt, all};
+}
+
+void GCN_SAMPLE_ALLGPU_impl::set_presample(const std::vector<uint32_t>& counts,
+                                           const std::vector<uint32_t>& ids) {
+  TORCH_CHECK(cfg.pd_cache, "set_presample needs the PD cache (cfg.pd_cache)");
+  auto guard = cs->guard();
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+  pd_counts_ = counts;
+  pd_offset_.assign(counts.size() + 1, 0);
+  for (size_t i = 0; i < counts.size(); ++i) pd_offset_[i + 1] = pd_offset_[i] + counts[i];
+  TORCH_CHECK(pd_offset_.back() == ids.size(), "PD cache: ids must hold sum(counts) vertices");
+  uint32_t mx = 1;
+  for (uint32_t c : counts) mx = std::max(mx, c);
+  std::vector<VertexId> hot(ids.begin(), ids.end());
+  if (hot.empty()) hot.push_back(0);  // a sampler needs a non-empty id list
+  const int L = (int)cfg.fanout.size();
+  // CPU side of the reference (:740-745): a 1-layer sampler over the hot ids
+  // with the bottom layer's fanout, consumed super-batch by super-batch
+  pd_sampler_ = std::make_unique<FastSampler>(graph, hot, 1, (int)mx,
+                                              std::vector<int>{cfg.fanout[L - 1]}, kPdRing,
+                                              std::vector<bool>{false},
+                                              cfg.weight_type != WeightType::None, false);
+  pd_sampler_->rng_mode = cfg.rng_mode;
+  pd_sampler_->batch_seq = uint64_t(1) << 48;  // a PHILOX stream of its own
+  const int64_t Fin = cfg.layer_size[0];
+  for (int i = 0; i < kPdRing; ++i) pd_y_[i] = torch::empty({(int64_t)mx, Fin}, f32_opts(graph->device));
+  pd_share_ = torch::empty({(int64_t)mx, (int64_t)cfg.layer_size[1]}, f32_opts(graph->device));
+  pd_ids_ = torch::empty({(int64_t)std::max<size_t>(ids.size(), 1)}, u32_opts(graph->device));
+  if (!ids.empty())
+    pd_ids_.narrow(0, 0, (int64_t)ids.size())
+        .copy_(torch::from_blob((void*)ids.data(), {(int64_t)ids.size()}, torch::kInt32));
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+}
+
+// At sampling time, for a batch that opens a super-batch: its hot vertices get
+// the next key in cache_map / cache_location (set_cache_index), their
+// 1-layer neighbourhoods are sampled and aggregated (PushDownBatchOp: the
+// reference's CPU thread; here the fused gather on the sampling stream).  Every
+// batch then samples its bottom layer with the super-batch's key omitted.
+void GCN_SAMPLE_ALLGPU_impl::pd_issue(int slot, NtsStream& st) {
+  const uint64_t bip = (sampler->work_offset - sampler->work_range[0]) / (uint64_t)cfg.batch_size;
+  const int sb = (int)(bip / (uint64_t)cfg.pd_super_batch);
+  const bool first = bip % (uint64_t)cfg.pd_super_batch == 0;
+  TORCH_CHECK(sb < (int)pd_counts_.size(), "PD cache: more super-batches than preSampled");
+  if (first) {
+    pd_next_key_++;
+    const uint32_t n = pd_counts_[sb];
+    auto guard = st.guard();
+    hip_check(nts_hip_pd_set_cache(st.ctx(), dptr<uint32_t>(pd_ids_) + pd_offset_[sb], n,
+                                   pd_next_key_, dptr<uint32_t>(pd_cache_map_),
+                                   dptr<uint32_t>(pd_cache_loc_)),
+              "nts_hip_pd_set_cache");
+    if (n) {
+      const int ring = (int)(pd_next_key_ % kPdRing);
+      pd_sampler_->work_offset = (VertexId)pd_offset_[sb];
+      pd_sampler_->issue_gpu_sample((int)n, ring, st, cfg.weight_type);
+      sampCSC* h = pd_sampler_->ssgs[ring]->sampled_sgs[0];
+      NtsVar& y = pd_y_[ring];
+      hip_check(nts_hip_spmm_csc_fwd(st.ctx(), h->dev_c_o(), h->dev_r_i(), h->dev_e_w_f(),
+                                     dptr<uint32_t>(h->sizes), h->v_cap, F.data_ptr<float>(),
+                                     (uint64_t)F.stride(0), h->dev_src(), (uint32_t)F.size(1),
+                                     y.data_ptr<float>(), (uint64_t)y.stride(0)),
+                "nts_hip_spmm_csc_fwd(pd)");
+    }
+  }
+  pd_slot_key_[slot] = (int)pd_next_key_;
+  pd_slot_sb_[slot] = sb;
+  pd_slot_first_[slot] = first;
+  sampler->omit_map = dptr<uint32_t>(pd_cache_map_);
+  sampler->omit_key = pd_next_key_;
+  sampler->omit_loc = dptr<uint32_t>(pd_cache_loc_);
+}
+
+// Before the forward of a batch: at the super-batch's first batch, the shared
+// embedding = (A X) W with the current weights (the reference's CPU GEMM with
+// the W of shared_W_queue, :821-840); later batches of the super-batch reuse it.
+void GCN_SAMPLE_ALLGPU_impl::pd_train(int slot) {
+  pd_key_ = (uint32_t)pd_slot_key_[slot];
+  pd_active_ = true;
+  if (!pd_slot_first_[slot]) return;
+  const int sb = pd_slot_sb_[slot];
+  const uint32_t n = pd_counts_[sb];
+  if (n == 0) return;
+  const int ring = (int)(pd_key_ % kPdRing);
+  pd_sampler_->finish_gpu_sample(ring);  // its sizes (the batch's own sync already covered it)
+  auto guard = cs->guard();
+  torch::NoGradGuard ng;
+  NtsVar Wc = P[0]->W.contiguous();
+  hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)n, (int)Wc.size(1), (int)Wc.size(0),
+                             pd_y_[ring].data_ptr<float>(), (uint64_t)pd_y_[ring].stride(0),
+                             Wc.data_ptr<float>(), (uint64_t)Wc.size(1),
+                             pd_share_.data_ptr<float>(), (uint64_t)pd_share_.stride(0)),
+            "nts_hip_gemm_f32(pd share)");
+  TORCH_CHECK(hipEventRecord(pd_sampler_->ssgs[ring]->consumed, (hipStream_t)cs->stream()) ==
+                  hipSuccess,
+              "hipEventRecord");
 }
 
 void GCN_SAMPLE_ALLGPU_impl::reset_stats() {

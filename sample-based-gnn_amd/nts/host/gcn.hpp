@@ -37,6 +37,15 @@ struct GCNConfig {
   // the rows of the cache_rate * V highest-degree vertices stay in HBM
   // (GS_SAMPLE_PD_CACHE's placement); < 0: the whole table in HBM
   double cache_rate = -1.0;
+  // NeutronOrch PD cache (GCN_SAMPLE_PD_CACHE): training seeds in
+  // super-batches of pd_super_batch mini-batches (PIPELINE_NUM); per
+  // super-batch the hot vertices (preSample, rate pd_rate = CACHE_RATE) get
+  // their bottom-layer embedding (A X) W once, at the super-batch's first
+  // batch, and every batch of the super-batch skips sampling their bottom
+  // neighbourhoods and takes those rows instead.  Training only; aggregate-first.
+  bool pd_cache = false;
+  double pd_rate = 0.2;
+  int pd_super_batch = 4;
   int64_t seed = 2000;
 };
 
@@ -79,6 +88,12 @@ class GCN_SAMPLE_ALLGPU_impl {
   // training batch size, sampled like training (the reference's eval/test
   // samplers); returns correct / |nids|.
   double evaluate(const std::vector<VertexId>& nids);
+  // PD cache: the hot vertices of every super-batch (preSample on the device,
+  // per super-batch counts + their concatenated ids, the PRE_SAMPLE_FILE
+  // layout), or replace them (e.g. read from a PRE_SAMPLE_FILE)
+  std::pair<std::vector<uint32_t>, std::vector<uint32_t>> presample();
+  void set_presample(const std::vector<uint32_t>& counts, const std::vector<uint32_t>& ids);
+  uint64_t pd_hits = 0;  // bottom-layer dsts served from the PD cache (host count, sampled batches)
   std::vector<NtsVar> weights() const;
   void reset_stats();
   void resolve_profile() { prof.resolve(); }
@@ -117,6 +132,22 @@ class GCN_SAMPLE_ALLGPU_impl {
   void count_correct(const NtsVar& out, const NtsVar& tgt);  // non-fused output layers
   NtsVar correct_;        // int32 [1]: correct rows of the training batches since reset
   uint32_t* count_to_ = nullptr;  // where forward's fused loss adds its correct count
+  // ---- PD cache state ----
+  static constexpr int kPdRing = 4;  // super-batches in flight (sampler lookahead)
+  void pd_issue(int slot, NtsStream& st);  // per batch, at sampling time
+  void pd_train(int slot);                 // per batch, before its forward
+  std::vector<uint32_t> pd_counts_;   // hot vertices per super-batch
+  std::vector<uint64_t> pd_offset_;   // their offsets in the concatenated id list
+  NtsVar pd_ids_, pd_cache_map_, pd_cache_loc_;  // device: ids; u32 [V] map / location
+  std::unique_ptr<FastSampler> pd_sampler_;      // 1 layer (bottom fanout) over the hot ids
+  NtsVar pd_y_[kPdRing];              // their aggregation A X, per ring slot
+  NtsVar pd_share_;                   // (A X) W of the current super-batch
+  uint32_t pd_next_key_ = 0;
+  int pd_slot_key_[3] = {0, 0, 0};    // per sampler slot (kSlots): its super-batch key
+  int pd_slot_sb_[3] = {-1, -1, -1};  // ... its super-batch index in the pass
+  bool pd_slot_first_[3] = {false, false, false};
+  uint32_t pd_key_ = 0;               // key of the batch being trained (forward)
+  bool pd_active_ = false;
   std::vector<std::pair<const char*, hipEvent_t>> tl_;  // NTS_TIMELINE events
   bool tf_ = false;  // transform-first bottom layer (cfg.transform_first)
   // early aggregation: per sampler slot, the bottom graph op's output and the

@@ -121,6 +121,8 @@ class sampCSC {
   // is_merge_src_dst (GAT): dst d is local src dst_local_id[d]; CSR slot j is
   // CSC edge csr_edge_id[j] (both undefined unless set_merge_src_dst())
   torch::Tensor dst_local_id, csr_edge_id;
+  // PD cache (sampled with an omit map): per dst its cache row or NTS_NOT_CACHED
+  torch::Tensor omit_row;
 
   sampCSC(int device, VertexId v_cap, VertexId e_cap, VertexId s_cap, bool csr, bool weights);
   void set_merge_src_dst();  // core/coocsc.hpp:405-411
@@ -207,6 +209,11 @@ class FastSampler {
   int rng_mode = NTS_RNG_PHILOX;
   bool up_degree = false;  // UP_DEGREE: weights from each sampled layer's own degrees
   uint64_t batch_seq = 0;  // keys the PHILOX stream (one per sampled batch)
+  // sample_gpu_fast_omit (core/ntsFastSampler.hpp:711-915): when set, the
+  // bottom layer skips the dsts with omit_map[d] == omit_key
+  const uint32_t* omit_map = nullptr;
+  uint32_t omit_key = 0;
+  const uint32_t* omit_loc = nullptr;  // cache rows; recorded in the layer's omit_row
   double all_time = 0;     // sampler wall time (reference `all_time`)
   uint64_t sampled_edges = 0;
 
@@ -410,6 +417,9 @@ class KernelProfiler {
   size_t used_ = 0;
   int open_[kCount];
 };
+
+// dropout(relu(x), p) as its own autograd op (the GEMM epilogue's mask keys)
+NtsVar hip_relu_dropout(const NtsVar& x, double p, uint64_t seed, uint64_t offset, NtsStream* cs);
 
 // Transform-first bottom layer (nts_hip.h): X1 = dropout(relu(A (X[source] W)))
 // on the layer's sampled block `sg` (its CSR is needed for the backward);

@@ -17,9 +17,14 @@ the MI355X path of this build; the mapping is:
                                       its get_mean_weight formula)
   GCNSAMPLEALLMULTI                   data parallel: launch one process per GPU
                                       with torch.distributed.run
-  GCNSAMPLEPDCACHE / GSSAMPLEPDCACHE  GCN / GraphSAGE with the PD-cache
-                                      placement: features in pinned host
-                                      memory, FEATURE_CACHE_RATE of them in HBM
+  GCNSAMPLEPDCACHE / GSSAMPLEPDCACHE  GCN / GraphSAGE with the NeutronOrch PD
+                                      cache: super-batches of PIPELINE_NUM
+                                      batches, CACHE_RATE hot vertices each
+                                      (preSample; PRE_SAMPLE_FILE read, or
+                                      written when missing); with
+                                      FEATURE_CACHE_RATE the feature table
+                                      moves to pinned host memory with that
+                                      fraction cached in HBM
   GATSAMPLEALLGPU                     GAT
 
 Usage:  python -m nts.run path/to/job.cfg [--epochs N] [--device D] [--json out.json]
@@ -46,8 +51,8 @@ ALGORITHMS = {
     "GCNSAMPLEALLGPU": ("gcn", "sum", "philox", False, None),
     "GSSAMPLEALLGPU": ("gcn", "mean", "philox", False, None),
     "GCNSAMPLEALLMULTI": ("gcn", "sum", "philox", False, None),
-    "GCNSAMPLEPDCACHE": ("gcn", "sum", "philox", False, "cache"),
-    "GSSAMPLEPDCACHE": ("gcn", "mean", "philox", False, "cache"),
+    "GCNSAMPLEPDCACHE": ("gcn", "sum", "philox", False, "pd"),
+    "GSSAMPLEPDCACHE": ("gcn", "mean", "philox", False, "pd"),
     "GATSAMPLEALLGPU": ("gat", "none", "philox", False, None),
 }
 
@@ -88,16 +93,38 @@ def build_driver(E, info: dataloader.InputInfo, G, feat, labels, train_ids, devi
     if weight == "mean" and info.extra.get("MEAN_WEIGHT", "").lower() == "gpu":
         weight = "mean-sampled"
     cache_rate = -1.0
-    if place == "cache":
-        cache_rate = float(info.extra.get("FEATURE_CACHE_RATE", info.cache_rate))
+    pd = place == "pd"
+    if pd and "FEATURE_CACHE_RATE" in info.extra:
+        cache_rate = float(info.extra["FEATURE_CACHE_RATE"])
     cfg = host.gcn_config(
         info.layers, info.fanout, info.batch_size, learn_rate=info.learn_rate,
         weight_decay=info.weight_decay, drop_rate=info.drop_rate,
         rng_mode=_abi.NTS_RNG_MT19937_LEMIRE if rng == "mt" else _abi.NTS_RNG_PHILOX,
         weight="none" if model == "gat" else weight, bias_correction=bias,
         pipeline=info.pipeline_num > 1, up_degree=info.up_degree, gat=model == "gat",
-        cache_rate=cache_rate, shuffle=True)
+        cache_rate=cache_rate, shuffle=True, pd_cache=pd, pd_rate=info.cache_rate,
+        pd_super_batch=max(info.pipeline_num, 1))
     return E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train_ids, cfg, comm)
+
+
+def pd_presample_file(drv, info, base, out=print):
+    """PRE_SAMPLE_FILE (core/ntsBaseOp.hpp:427-497): read the hot vertices of
+    every super-batch if the file exists, else keep the device preSample the
+    driver ran and write it (default name when the key is unset)."""
+    name = info.pre_sample_file or dataloader.presample_file_name(
+        _path(base, info.edge_file), info.batch_size, info.fanout_string, info.pipeline_num)
+    path = _path(base, name)
+    counts, ids = drv.presample()
+    if path.exists():
+        kc, kids = dataloader.read_presample_file(path, len(counts))
+        drv.set_presample(kc.tolist(), kids.tolist())
+        out(f"pre sample file: {path} (read, {len(kc)} super-batches, {kids.size} hot vertices)")
+    else:
+        try:
+            dataloader.write_presample_file(path, counts, ids)
+            out(f"pre sample file: {path} (written, {len(counts)} super-batches, {len(ids)} hot vertices)")
+        except OSError:
+            out(f"pre sample file: {path} not writable; using the device preSample")
 
 
 def run(cfg_path, epochs=None, device=0, out=print) -> dict:
@@ -129,6 +156,8 @@ def run(cfg_path, epochs=None, device=0, out=print) -> dict:
     train = torch.from_numpy(ndist.shard_nids(ids["train"], world, rank))
     comm = ndist.make_communicator(E, world, rank, device)
     drv = build_driver(E, info, G, feat, lab, train, dev, comm)
+    if ALGORITHMS.get(info.algorithm.upper(), ("",) * 5)[4] == "pd":
+        pd_presample_file(drv, info, base, out if rank == 0 else (lambda s: None))
     if rank == 0:
         out(f"GNNmini::Engine[MI355X.GPU.{info.algorithm}] running [{epochs}] Epochs "
             f"(V={info.vertices}, E={n_edges}, layers {info.layer_string}, fanout "

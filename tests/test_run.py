@@ -66,3 +66,24 @@ def test_gcn_cpu_sample_algorithm_runs_mt19937_and_bias_corrected_adam():
     (d / "job.cfg").write_text(text)
     res = run.run(d / "job.cfg", epochs=3, out=lambda s: None)
     assert res["epochs"][-1]["train_acc"] > 0.5
+
+
+@pytest.mark.gpu
+def test_pd_cache_cora_job_and_presample_file(tmp_path):
+    """The reference's own job (ALGORITHM:GCNSAMPLEPDCACHE, CACHE_RATE 0.2,
+    PIPELINE_NUM 4): trains with the PD cache, writes the PRE_SAMPLE_FILE on
+    the first run and reads it back on the second with the same result."""
+    import shutil
+    from nts import run
+    for f in ("cora.2708.edge.self", "cora.featuretable.zip", "cora.labeltable", "cora.mask"):
+        shutil.copy(GOLDEN / "cora" / f, tmp_path / f)
+    text = CFG.read_text().replace("ALGORITHM:GCNSAMPLEALLGPU", "ALGORITHM:GCNSAMPLEPDCACHE")
+    (tmp_path / "job.cfg").write_text(text + "PRE_SAMPLE_FILE:hot.bin\n")
+    lines = []
+    r1 = run.run(tmp_path / "job.cfg", epochs=4, out=lines.append)
+    assert (tmp_path / "hot.bin").exists() and any("written" in l for l in lines)
+    lines2 = []
+    r2 = run.run(tmp_path / "job.cfg", epochs=4, out=lines2.append)
+    assert any("(read" in l for l in lines2)
+    assert [e["train_correct"] for e in r1["epochs"]] == [e["train_correct"] for e in r2["epochs"]]
+    assert r1["epochs"][-1]["train_acc"] > 0.7
