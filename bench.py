@@ -67,6 +67,10 @@ def parse():
                         "reference GPU kernel's mean (by sampled count)")
     p.add_argument("--transform-first", type=int, default=-1, choices=[-1, 0, 1],
                    help="bottom layer order: 1 A(XW), 0 (AX)W (the reference's), -1 auto")
+    p.add_argument("--gemm", default="f32", choices=["f32", "split3"],
+                   help="layer GEMM arithmetic: f32 = fp32-input MFMA; split3 = fp32 operands "
+                        "split exactly into three bf16 pieces, six piece products on the bf16 "
+                        "MFMA (fp32-accurate, csrc/gemm3.hip)")
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
@@ -172,7 +176,7 @@ def main():
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
                           deterministic_backward=not args.atomic_backward,
-                          gat=args.model == "gat")
+                          gat=args.model == "gat", gemm=args.gemm)
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
     tf = bool(drv.transform_first)
 
@@ -287,6 +291,8 @@ def main():
             "host_sampler_wait_s_per_step": sample_s / args.steps,
             "host_train_issue_s_per_step": train_host_s / args.steps,
             "bottom_layer": "transform-first A(X W)" if tf else "aggregate-first (A X) W",
+            "gemm": {"f32": "fp32-input MFMA",
+                     "split3": "fp32 split into 3 bf16 pieces, 6 products, fp32 accumulate"}[args.gemm],
             "layer_sizes_top_down": layer_sizes,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
                              "workload": pmc_workload(args, layers, world)},
@@ -356,7 +362,7 @@ def roofline(prof: dict, args, layers, world) -> dict:
 
 def pmc_workload(args, layers, world) -> str:
     return (f"{args.shape}/{args.batch}/{args.fanout}/{'-'.join(map(str, layers))}/{args.weight}/"
-            f"w{world}/tf{args.transform_first}/{args.model}/c{args.cache_rate}")
+            f"w{world}/tf{args.transform_first}/{args.model}/c{args.cache_rate}/{args.gemm}")
 
 
 def attach_pmc(rl, dom, args, layers, world):

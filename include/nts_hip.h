@@ -34,9 +34,10 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 3  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 4  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
-                                     accuracy counts in the fused loss */
+                                     accuracy counts in the fused loss;
+                                  4: PD cache entry points + omit fields, GEMM mode */
 
 /* status codes */
 #define NTS_OK 0
@@ -149,6 +150,17 @@ void *nts_hip_ctx_get_stream(nts_hip_ctx *ctx);
  * (keeps every call graph-capturable).  n_vertices: |V| of the graph;
  * max_items: largest e_cap / v_cap that will be passed. */
 int nts_hip_ctx_reserve(nts_hip_ctx *ctx, uint64_t n_vertices, uint64_t max_items);
+/* Arithmetic of the dense layer GEMMs issued through this context
+ * (nts_hip_gemm_*, the bottom-layer transform): NTS_GEMM_F32 = the fp32-input
+ * MFMA (one fp32 fma chain per output, the reference's fp32 GEMM semantics);
+ * NTS_GEMM_SPLIT3 = fp32 operands split exactly into three bf16 pieces, the
+ * six significant piece products on the bf16 MFMA with fp32 accumulation
+ * (error vs fp64 of the same order as the fp32 path; csrc/gemm3.hip).
+ * Shapes the split kernels do not take run on the fp32 path. */
+#define NTS_GEMM_F32 0
+#define NTS_GEMM_SPLIT3 1
+int nts_hip_ctx_set_gemm_mode(nts_hip_ctx *ctx, int mode);
+int nts_hip_ctx_get_gemm_mode(nts_hip_ctx *ctx);
 /* Re-seed the MT19937 state (std::mt19937(seed)).  Enqueued on the stream. */
 int nts_hip_rng_seed(nts_hip_ctx *ctx, uint64_t seed);
 /* Copy the MT19937 state (624 words + position) to host; synchronises. */

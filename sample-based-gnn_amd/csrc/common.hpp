@@ -111,6 +111,7 @@ struct nts_hip_ctx {
   void* scratch = nullptr;         // scans / radix sort temporaries
   size_t scratch_bytes = 0;
   uint32_t* mt_state = nullptr;    // 624 words + position (device)
+  int gemm_mode = NTS_GEMM_F32;    // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode)
 };
 
 namespace nts_hip {
@@ -140,4 +141,14 @@ size_t radix_tmp_bytes(uint64_t n_cap);
 // apart) in a fixed order (deterministic; gemm.hip).
 int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
                float* C, uint64_t ldc);
+
+// fp32-accurate GEMMs on the bf16 matrix cores (gemm3.hip, NTS_GEMM_SPLIT3)
+bool gemm3_nn_ok(int M, int N, int K, const float* A, uint64_t lda);
+bool gemm3_tn_ok(int M, int N, int K);
+int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,
+             const uint32_t* amap, const float* B, uint64_t ldb, float* C, uint64_t ldc,
+             uint32_t keep_threshold, float scale, uint64_t seed, uint64_t offset);
+int gemm3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda,
+             const uint32_t* amap, const float* B, uint64_t ldb, const float* X, uint64_t ldx,
+             float bscale, float* C, uint64_t ldc);
 }  // namespace nts_hip

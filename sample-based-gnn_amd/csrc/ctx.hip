@@ -109,6 +109,15 @@ int nts_hip_ctx_set_stream(nts_hip_ctx* ctx, void* stream) {
 
 void* nts_hip_ctx_get_stream(nts_hip_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+int nts_hip_ctx_set_gemm_mode(nts_hip_ctx* ctx, int mode) {
+  NTS_CHECK_ARG(ctx, "ctx is NULL");
+  NTS_CHECK_ARG(mode == NTS_GEMM_F32 || mode == NTS_GEMM_SPLIT3, "unknown GEMM mode");
+  ctx->gemm_mode = mode;
+  return NTS_OK;
+}
+
+int nts_hip_ctx_get_gemm_mode(nts_hip_ctx* ctx) { return ctx ? ctx->gemm_mode : NTS_GEMM_F32; }
+
 int nts_hip_ctx_reserve(nts_hip_ctx* ctx, uint64_t n_vertices, uint64_t max_items) {
   NTS_CHECK_ARG(ctx, "ctx is NULL");
   NTS_HIP_TRY(hipSetDevice(ctx->device));

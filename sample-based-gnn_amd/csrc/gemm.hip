@@ -1024,6 +1024,14 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
     for (int i = 0; i < M; ++i) NTS_HIP_TRY(hipMemsetAsync(C + (uint64_t)i * ldc, 0, N * 4, st));
     return NTS_OK;
   }
+  if (ctx->gemm_mode == NTS_GEMM_SPLIT3) {
+    if (!trans_a && !BMASK && gemm3_nn_ok(M, N, K, A, lda))
+      return gemm3_nn(ctx, EPI, M, N, K, A, lda, ex.amap, B, ldb, C, ldc, ex.keep_threshold,
+                      ex.scale, ex.seed, ex.offset);
+    if (trans_a && !EPI && gemm3_tn_ok(M, N, K))
+      return gemm3_tn(ctx, M, N, K, A, lda, ex.amap, B, ldb, BMASK ? ex.bx : nullptr, ex.ldbx,
+                      ex.bscale, C, ldc);
+  }
   if (!force_tiled()) {
     if (!trans_a && !BMASK) {
       const int ncol = wres_ncol(M, N, K);

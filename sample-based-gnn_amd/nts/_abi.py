@@ -17,10 +17,12 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 3  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 4  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
+NTS_GEMM_F32 = 0
+NTS_GEMM_SPLIT3 = 1
 NTS_WEIGHT_SUM = 0
 NTS_WEIGHT_MEAN = 1
 NTS_WEIGHT_NONE = 2
@@ -30,6 +32,7 @@ NTS_WEIGHT_MEAN_SAMPLED = 3
 EXPORTED = (
     "nts_hip_abi_version", "nts_hip_last_error", "nts_hip_ctx_create", "nts_hip_ctx_destroy",
     "nts_hip_ctx_set_stream", "nts_hip_ctx_get_stream", "nts_hip_ctx_reserve",
+    "nts_hip_ctx_set_gemm_mode", "nts_hip_ctx_get_gemm_mode",
     "nts_hip_rng_seed", "nts_hip_rng_state", "nts_hip_degrees", "nts_hip_build_csc",
     "nts_hip_sample_layer", "nts_hip_gather_rows", "nts_hip_gather_labels",
     "nts_hip_spmm_csc_fwd", "nts_hip_spmm_csr_bwd", "nts_hip_spmm_csc_bwd_atomic",
@@ -92,6 +95,8 @@ def lib() -> C.CDLL:
         "nts_hip_ctx_destroy": ([P], I),
         "nts_hip_ctx_set_stream": ([P, P], I),
         "nts_hip_ctx_get_stream": ([P], P),
+        "nts_hip_ctx_set_gemm_mode": ([P, I], I),
+        "nts_hip_ctx_get_gemm_mode": ([P], I),
         "nts_hip_ctx_reserve": ([P, U64, U64], I),
         "nts_hip_rng_seed": ([P, U64], I),
         "nts_hip_rng_state": ([P, P], I),

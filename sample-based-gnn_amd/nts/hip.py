@@ -31,6 +31,11 @@ class HipContext:
         check(self.lib.nts_hip_ctx_create(C.byref(h), device, C.c_void_p(self.stream.cuda_stream), seed))
         self.h = h
 
+    def set_gemm_mode(self, mode: int):
+        """NTS_GEMM_F32 (fp32-input MFMA) or NTS_GEMM_SPLIT3 (fp32-accurate
+        three-piece bf16 split on the bf16 MFMA) for this context's GEMMs."""
+        check(self.lib.nts_hip_ctx_set_gemm_mode(self.h, int(mode)))
+
     def close(self):
         if self.h:
             self.lib.nts_hip_ctx_destroy(self.h)

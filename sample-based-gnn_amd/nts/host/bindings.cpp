@@ -158,6 +158,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("hip_gemm", &GCNConfig::hip_gemm)
       .def_readwrite("pipeline", &GCNConfig::pipeline)
       .def_readwrite("transform_first", &GCNConfig::transform_first)
+      .def_readwrite("gemm_mode", &GCNConfig::gemm_mode)
       .def_readwrite("pd_cache", &GCNConfig::pd_cache)
       .def_readwrite("pd_rate", &GCNConfig::pd_rate)
       .def_readwrite("pd_super_batch", &GCNConfig::pd_super_batch)

@@ -37,6 +37,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                      (uint64_t)cfg.seed);
   else
     cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+  hip_check(nts_hip_ctx_set_gemm_mode(cs->ctx(), cfg.gemm_mode), "nts_hip_ctx_set_gemm_mode");
   // inputs were produced on other streams: order them before our stream
   TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
   auto guard = cs->guard();
@@ -100,8 +101,10 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   uint64_t items = graph->global_vertices;
   for (auto* s : sampler->ssg->sampled_sgs) items = std::max<uint64_t>({items, s->e_cap, s->v_cap});
   hip_check(nts_hip_ctx_reserve(cs->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
-  if (ss)
+  if (ss) {
     hip_check(nts_hip_ctx_reserve(ss->ctx(), graph->global_vertices, items), "nts_hip_ctx_reserve");
+    hip_check(nts_hip_ctx_set_gemm_mode(ss->ctx(), cfg.gemm_mode), "nts_hip_ctx_set_gemm_mode");
+  }
   // The bottom graph op Y_0 = A_0 X depends on the sampled graph and the
   // feature table only (not on the weights), so it is issued right behind the
   // sampling, on the sampling stream: with the pipeline it runs while the
