@@ -113,6 +113,35 @@ def main():
             f"{kv.get('l2_hit_rate', float('nan')):.3f} |")
         if "traffic_over_algorithmic" in kv:
             lines.append(f"|  | counter / algorithmic bytes: {kv['traffic_over_algorithmic']:.2f} | | | | |")
+    # engine counters of the heaviest kernels (own pass: SQ / GRBM)
+    sqp = list(src.glob("sq/**/run_counter_collection.csv"))
+    if sqp:
+        per = {}
+        for r in load(sqp[0]):
+            per.setdefault(r["Kernel_Name"].split("(")[0].strip(), {}).setdefault(
+                r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        lines += ["", "## Engine counters (own rocprofv3 --pmc pass; medians per dispatch)", "",
+                  "MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); "
+                  "clock = GRBM_GUI_ACTIVE / 8 / trace duration (MI355X_MICROARCH.md: DVFS); "
+                  "wait = SQ_WAIT_ANY / SQ_WAVE_CYCLES.", "",
+                  "| kernel | trace avg us | MFMA busy | clock GHz | wave wait | LDS bank-conflict cycles |",
+                  "|---|---|---|---|---|---|"]
+        engine = {}
+        for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:12]:
+            c = per.get(r["Name"].split("(")[0].strip())
+            if not c:
+                continue
+            med = {k: statistics.median(v) for k, v in c.items()}
+            gui = med.get("GRBM_GUI_ACTIVE", 0.0)
+            avg_us = float(r["AverageNs"]) / 1e3
+            busy = med.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (128.0 * gui) if gui else float("nan")
+            clk = gui / 8.0 / (avg_us * 1e3) if avg_us else float("nan")
+            wait = med.get("SQ_WAIT_ANY", 0.0) / med["SQ_WAVE_CYCLES"] if med.get("SQ_WAVE_CYCLES") else float("nan")
+            engine[r["Name"]] = {"mfma_busy": busy, "clock_ghz": clk, "wave_wait": wait,
+                                 "lds_bank_conflict_cycles": med.get("SQ_LDS_BANK_CONFLICT")}
+            lines.append(f"| `{r['Name'].split('(')[0][:70]}` | {avg_us:.1f} | {busy:.2f} | {clk:.2f} | "
+                         f"{wait:.2f} | {med.get('SQ_LDS_BANK_CONFLICT', float('nan')):.3g} |")
+        info["engine"] = engine
     if bl:
         lines += ["", f"Bench line of the traced run: value {bl['value']:.4g} {bl['unit']}, "
                       f"{bl['ms_per_step']:.3f} ms/step (profiled: slower than un-profiled)."]
