@@ -480,6 +480,377 @@ __global__ __launch_bounds__(kS3Threads, 1) void k_gemm3_tn(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
+// v2 kernels (the default; NTS_S3_V1=1 selects the first generation above):
+// 2 waves per SIMD that never meet at the same barrier (NN: two independent
+// 4-wave blocks per CU; TN: one 8-wave block), every operand
+// software-pipelined in registers two k-steps ahead, the split of step s+1
+// beside the MFMAs of step s, no branches on runtime flags in the k-loop.
+constexpr int kS3V2Threads = 256;
+
+// NN: C = A B (+ relu/dropout), A rows optionally gathered.  The M rows are
+// cut into 16-row tiles spread evenly over the grid's waves (t_lo .. t_hi); a
+// wave runs them two at a time (a missing second tile is a clamped duplicate
+// that is not stored) x all 128 columns of its column block.  Per 32-deep
+// k-step:
+//   A: each lane loads its fragment A[row i][k0 + 8g .. +7] straight into
+//      registers (two 16-byte loads per tile, two steps ahead) and splits it
+//      into three bf16 pieces one step ahead;
+//   B: the block copies the weight's pre-split 24 KB fragment image of the
+//      step into LDS (registers -> ds_write, double-buffered, one barrier per
+//      step); a wave reads 3 fragments per column tile for both row tiles.
+template <bool EPI, bool AMAP>
+__global__ __launch_bounds__(kS3V2Threads, 2) void k_s3_nn(int M, int N, int K,
+                                                           const float* __restrict__ A, uint64_t lda,
+                                                           const char* __restrict__ bimg,
+                                                           float* __restrict__ C, uint64_t ldc,
+                                                           int rounds, Gemm3Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char s3v2[];  // [2][kS3Img]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * 128;
+  const int T = (M + 15) / 16;
+  const int64_t W = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
+  const int t_lo = (int)(gw * T / W), t_hi = max((int)((gw + 1) * T / W), t_lo + 1);
+  const int nsteps = (K + 31) / 32, nfull = K / 32;
+  const size_t bstep = (size_t)gridDim.y * kS3Img;
+  const char* bsrc = bimg + (size_t)blockIdx.y * kS3Img + 16 * tid;
+
+  const float* rbase[2];
+  f32x4 acc[2][8];
+  float4 xa[2][2];     // [tile][half]: raw A fragments of the next step
+  bf16x8 pa[2][2][3];  // [slot][tile][piece]
+  uint4 br0, br1, br2, br3, br4, br5;  // this thread's 6 x 16 B of a step's B image
+
+  auto load_b = [&](int s) {
+    const uint4* p = reinterpret_cast<const uint4*>(bsrc + (size_t)s * bstep);
+    br0 = p[0]; br1 = p[256]; br2 = p[512]; br3 = p[768]; br4 = p[1024]; br5 = p[1280];
+  };
+  auto store_b = [&](int buf) {
+    uint4* p = reinterpret_cast<uint4*>(s3v2 + buf * kS3Img + 16 * tid);
+    p[0] = br0; p[256] = br1; p[512] = br2; p[768] = br3; p[1024] = br4; p[1280] = br5;
+  };
+  // the partial last step reads up to 7 floats past K inside the row pitch
+  // (the launcher requires lda >= K rounded up to 8) and zeroes them
+  auto load_a = [&](int s, float4 (&x)[2][2]) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const float* p = rbase[rt] + 32 * s + 8 * g;
+      x[rt][0] = *reinterpret_cast<const float4*>(p);
+      x[rt][1] = *reinterpret_cast<const float4*>(p + 4);
+    }
+    if (s >= nfull) {
+      const int k = 32 * s + 8 * g;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        x[rt][0].x = k + 0 < K ? x[rt][0].x : 0.f;
+        x[rt][0].y = k + 1 < K ? x[rt][0].y : 0.f;
+        x[rt][0].z = k + 2 < K ? x[rt][0].z : 0.f;
+        x[rt][0].w = k + 3 < K ? x[rt][0].w : 0.f;
+        x[rt][1].x = k + 4 < K ? x[rt][1].x : 0.f;
+        x[rt][1].y = k + 5 < K ? x[rt][1].y : 0.f;
+        x[rt][1].z = k + 6 < K ? x[rt][1].z : 0.f;
+        x[rt][1].w = k + 7 < K ? x[rt][1].w : 0.f;
+      }
+    }
+  };
+  auto split_a = [&](const float4 (&x)[2][2], bf16x8 (&p)[2][3]) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const float v[8] = {x[rt][0].x, x[rt][0].y, x[rt][0].z, x[rt][0].w,
+                          x[rt][1].x, x[rt][1].y, x[rt][1].z, x[rt][1].w};
+      split3(v, p[rt][0], p[rt][1], p[rt][2]);
+    }
+  };
+  // MFMAs of one step, B fragments read one column tile ahead (scheduling
+  // fences keep the live fragments at two column tiles); the next step's A
+  // pieces (split_next) are computed beside column tiles 1 and 4
+  auto mma = [&](int buf, const bf16x8 (&p)[2][3], auto&& split_next) {
+    const char* img = s3v2 + buf * kS3Img;
+    bf16x8 b[2][3];
+    get3(img, kS3Frag, lane, b[0]);
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      if (ct + 1 < 8) get3(img + (ct + 1) * 3 * kS3Frag, kS3Frag, lane, b[(ct + 1) & 1]);
+      acc[0][ct] = mfma6(p[0], b[ct & 1], acc[0][ct]);
+      acc[1][ct] = mfma6(p[1], b[ct & 1], acc[1][ct]);
+      if (ct == 5) split_next(0);
+      if (ct == 6) split_next(1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int base = t_lo + 2 * rd;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int64_t row = (int64_t)min(base + rt, t_hi - 1) * 16 + i;
+      const uint64_t rr = (uint64_t)(row < M ? row : M - 1);
+      rbase[rt] = A + (AMAP ? (uint64_t)ex.amap[rr] : rr) * lda;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();  // the previous round's reads of both B buffers are done
+    load_b(0);
+    load_a(0, xa);
+    store_b(0);
+    load_b(min(1, nsteps - 1));
+    split_a(xa, pa[0]);
+    // step s: B(s) in buffer s&1, pieces of A(s) in pa[s&1], raw B(s+1) in
+    // registers; A(s+1) is loaded at the top of step s and split late in it
+    auto step = [&](int s, auto par) {
+      constexpr int P = decltype(par)::value;
+      // unconditional (clamped) loads, stores and splits: a conditional
+      // consumer makes the compiler's wait-count tracking assume loads still in
+      // flight and drain them before reusing registers
+      __syncthreads();
+      store_b(1 - P);
+      load_b(min(s + 2, nsteps - 1));
+      load_a(min(s + 1, nsteps - 1), xa);
+      mma(P, pa[P], [&](int rt) {
+        const float v[8] = {xa[rt][0].x, xa[rt][0].y, xa[rt][0].z, xa[rt][0].w,
+                            xa[rt][1].x, xa[rt][1].y, xa[rt][1].z, xa[rt][1].w};
+        split3(v, pa[1 - P][rt][0], pa[1 - P][rt][1], pa[1 - P][rt][2]);
+      });
+    };
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, std::integral_constant<int, 0>());
+      if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>());
+    }
+    // acc[rt][ct][v] = C[16 t + 4 g + v][n0 + 16 ct + i]
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      if (base + rt >= t_hi) continue;
+      const int64_t r4 = (int64_t)(base + rt) * 16 + 4 * g;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+        if ((int)col >= N) continue;
+        float o[4] = {acc[rt][ct][0], acc[rt][ct][1], acc[rt][ct][2], acc[rt][ct][3]};
+        if constexpr (EPI) {
+          const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
+          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+      }
+    }
+  }
+}
+
+// TN: C[M x N] = A[K x M]^T op(B)[K x N] (weight gradient; A's K rows
+// optionally gathered through a row map, op(B) = B or the relu/dropout
+// backward B * bscale where X > 0).  An 8-wave block takes one k-chunk, a
+// range of A's 16-column tiles (M-dimension tiles split evenly over the
+// blocks, then over the waves, at most TPW per wave; a missing tile is a
+// clamped duplicate that is not stored) and 128 columns of B.  The chunks'
+// partial tiles are summed in a fixed order (sum_splits): deterministic.
+//   A^T fragments come straight from global memory into registers: lane
+//     (i, g) of tile t loads A[k0 + 8g + j][16 t + i] (j = 0..7, one dword
+//     each, rows through the map; ids a step before the values, the values
+//     two steps before their MFMAs) and splits them one step ahead;
+//   B rows are loaded 8 floats per thread, masked, split and written to LDS
+//     as three bf16 images with plain 256-byte rows (16-byte chunks
+//     XOR-swizzled), double-buffered, and read back TRANSPOSED as MFMA B
+//     fragments by ds_read_b64_tr_b16 (k rows 8g..8g+3 and 8g+4..8g+7 of the
+//     fragment's 16 columns).
+constexpr int kS3TnV2Threads = 512;
+constexpr int kS3TnV2Img = 32 * 256;            // one piece of one step: 32 rows x 128 bf16
+constexpr int kS3TnV2Lds = 2 * 3 * kS3TnV2Img;  // 2 stages x 3 pieces = 48 KB
+
+// byte offset of 16-byte chunk `ch` (0..15) of row `row` in a [32][256 B] image
+__device__ __forceinline__ int s3_tr_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <int TPW, bool BMASK, bool AMAP>
+__global__ __launch_bounds__(kS3TnV2Threads, 1) void k_s3_tn(int M, int N, int K,
+                                                             const float* __restrict__ A, uint64_t lda,
+                                                             const float* __restrict__ B, uint64_t ldb,
+                                                             float* __restrict__ C, uint64_t ldc,
+                                                             int kchunk, uint64_t split_stride,
+                                                             int nmb, int nnb, Gemm3Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char s3tn[];  // [2][3][kS3TnV2Img]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int mb = blockIdx.x % nmb;
+  const int nb = (blockIdx.x / nmb) % nnb;
+  const int split = blockIdx.x / (nmb * nnb);
+  const int n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int b_lo = mb * T / nmb, b_cnt = (mb + 1) * T / nmb - b_lo;
+  const int w_lo = b_lo + wv * b_cnt / 8, w_hi = b_lo + (wv + 1) * b_cnt / 8;  // this wave's tiles
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nsteps = kbeg < kend ? (kend - kbeg + 31) / 32 : 0;
+
+  int acol[TPW];  // this lane's A column per tile (clamped)
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acol[t] = min(16 * min(w_lo + t, max(w_hi - 1, w_lo)) + i, M - 1);
+  // B staging role: row br = tid >> 4 of the step, columns bc .. bc + 7
+  const int br = tid >> 4, bc = 8 * (tid & 15);
+  const bool bok = n0 + bc < N;  // N % 16 == 0
+  const float* bcol = B + (bok ? n0 + bc : 0);
+  const float* xcol = BMASK ? ex.bx + (bok ? n0 + bc : 0) : nullptr;
+
+  f32x4 acc[TPW][8];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint32_t rid[2][8];   // A row ids of two steps
+  float xa[TPW][8];     // raw A^T fragments of the next step (per tile)
+  bf16x8 pa[TPW][3];    // split pieces of the current step
+  float4 braw[2], xraw[BMASK ? 2 : 1];
+
+  auto load_ids = [&](int s, uint32_t (&r)[8]) {
+    const int k0 = kbeg + 32 * s + 8 * g;
+    if constexpr (AMAP) {
+      if (k0 + 8 <= kend) {
+        const uint4 u0 = *reinterpret_cast<const uint4*>(ex.amap + k0);
+        const uint4 u1 = *reinterpret_cast<const uint4*>(ex.amap + k0 + 4);
+        r[0] = u0.x; r[1] = u0.y; r[2] = u0.z; r[3] = u0.w;
+        r[4] = u1.x; r[5] = u1.y; r[6] = u1.z; r[7] = u1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = ex.amap[min(k0 + j, kend - 1)];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (uint32_t)min(k0 + j, kend - 1);
+    }
+  };
+  // one tile's fragment of step s (rows past the chunk zeroed: the pad may hold anything)
+  auto load_x = [&](int s, const uint32_t (&r)[8], int t) {
+    const int k0 = kbeg + 32 * s + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xa[t][j] = A[(uint64_t)r[j] * lda + acol[t]];
+    if (k0 + 8 > kend) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + j >= kend) xa[t][j] = 0.f;
+    }
+  };
+  auto load_b = [&](int s) {
+    const int k = min(kbeg + 32 * s + br, kend - 1);
+    const float4* p = reinterpret_cast<const float4*>(bcol + (uint64_t)k * ldb);
+    braw[0] = p[0];
+    braw[1] = p[1];
+    if constexpr (BMASK) {
+      const float4* px = reinterpret_cast<const float4*>(xcol + (uint64_t)k * ex.ldbx);
+      xraw[0] = px[0];
+      xraw[1] = px[1];
+    }
+  };
+  auto store_b = [&](int s, int buf) {
+    const bool ok = bok && kbeg + 32 * s + br < kend;
+    float v[8] = {braw[0].x, braw[0].y, braw[0].z, braw[0].w,
+                  braw[1].x, braw[1].y, braw[1].z, braw[1].w};
+    if constexpr (BMASK) {
+      const float xs[8] = {xraw[0].x, xraw[0].y, xraw[0].z, xraw[0].w,
+                           xraw[1].x, xraw[1].y, xraw[1].z, xraw[1].w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xs[u] > 0.f ? v[u] * ex.bscale : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = ok ? v[u] : 0.f;
+    bf16x8 q0, q1, q2;
+    split3(v, q0, q1, q2);
+    char* dst = s3tn + buf * 3 * kS3TnV2Img + s3_tr_off(br, bc / 8);
+    *reinterpret_cast<bf16x8*>(dst) = q0;
+    *reinterpret_cast<bf16x8*>(dst + kS3TnV2Img) = q1;
+    *reinterpret_cast<bf16x8*>(dst + 2 * kS3TnV2Img) = q2;
+  };
+  // transposed fragment reads: lane 4q+p of each 16-lane group addresses row
+  // r0 + q, columns 4p .. 4p+3 of the column tile (chunk 2 ct + (p >> 1), +8 B)
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int off_lo = s3_tr_off(8 * g + tq, tp >> 1) + 8 * (tp & 1);
+  const int off_hi = s3_tr_off(8 * g + 4 + tq, tp >> 1) + 8 * (tp & 1);
+  auto read_b = [&](int buf, int ct, bf16x8 (&b)[3]) {
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc) {
+      const char* img = s3tn + (buf * 3 + pc) * kS3TnV2Img;
+      // chunk 2 ct + c: the XOR swizzle acts on the low 4 chunk bits, and
+      // 2 ct only touches bits the row-dependent XOR also touches, so apply
+      // it to the chunk index (ch ^ f) = (2ct + c) ^ f = 2ct ^ (c ^ f) for c < 2
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(img + (off_lo ^ (32 * ct))));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (lds_s16x4*)(img + (off_hi ^ (32 * ct))));
+      const s16x8 c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      b[pc] = __builtin_bit_cast(bf16x8, c);
+    }
+  };
+
+  if (nsteps > 0) {
+    load_ids(0, rid[0]);
+    if (nsteps > 1) load_ids(1, rid[1]);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) load_x(0, rid[0], t);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) split3(xa[t], pa[t][0], pa[t][1], pa[t][2]);
+    if (nsteps > 1)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) load_x(1, rid[1], t);
+    if (nsteps > 2) load_ids(2, rid[0]);
+    load_b(0);
+    store_b(0, 0);
+    if (nsteps > 1) load_b(1);
+  }
+  // step s: B pieces of s in buffer s&1, A pieces of s in pa, raw A of s+1 in
+  // xa, ids of s+2 in rid[s&1], raw B of s+1 in braw.  Tile by tile: the
+  // tile's 8 x 6 MFMAs, then its pieces of s+1 (split beside the next tile's
+  // MFMAs) and the loads of its fragment of s+2.
+  auto step = [&](int s, auto par) {
+    constexpr int P = decltype(par)::value;
+    __syncthreads();
+    if (s + 1 < nsteps) store_b(s + 1, 1 - P);
+    if (s + 2 < nsteps) load_b(s + 2);
+    if (s + 3 < nsteps) load_ids(s + 3, rid[1 - P]);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        bf16x8 b[3];
+        read_b(P, ct, b);
+        acc[t][ct] = mfma6(pa[t], b, acc[t][ct]);
+      }
+      if (s + 1 < nsteps) split3(xa[t], pa[t][0], pa[t][1], pa[t][2]);
+      if (s + 2 < nsteps) load_x(s + 2, rid[P], t);
+    }
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, std::integral_constant<int, 0>());
+    if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>());
+  }
+  // acc[t][ct][v] = C[16 (w_lo + t) + 4 g + v][n0 + 16 ct + i]
+  float* Cb = C + (uint64_t)split * split_stride;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (w_lo + t >= w_hi) continue;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 16 * (w_lo + t) + 4 * g + v;
+      if (row >= M) continue;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const int col = n0 + 16 * ct + i;
+        if (col < N) Cb[(uint64_t)row * ldc + col] = acc[t][ct][v];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers (called by gemm.hip's dispatcher when the context's GEMM mode is
 // NTS_GEMM_SPLIT3 and the shape qualifies)
 
@@ -489,6 +860,22 @@ bool gemm3_nn_ok(int M, int N, int K, const float* A, uint64_t lda) {
   return M >= 256 && K >= 1 && N % 16 == 0 && lda % 4 == 0 && (uintptr_t)A % 16 == 0;
 }
 bool gemm3_tn_ok(int M, int N, int K) { return M >= 1 && K >= 256 && N % 16 == 0; }
+
+// Kernel generation per GEMM kind (A/B switches): TN runs v2 unless
+// NTS_S3_V1=1; NN runs v1 (measured equal or faster on the layer shapes)
+// unless NTS_S3_NN2=1.
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return e && e[0] == '1';
+}
+static bool use_v1() {
+  static const bool v = env_on("NTS_S3_V1");
+  return v;
+}
+static bool nn_v2() {
+  static const bool v = env_on("NTS_S3_NN2") && !env_on("NTS_S3_V1");
+  return v;
+}
 
 int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,
              const uint32_t* amap, const float* B, uint64_t ldb, float* C, uint64_t ldc,
@@ -522,8 +909,34 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
   const int64_t W = (int64_t)gx * 8;
   const int max_tiles = (int)((T + W - 1) / W);
   const int rounds = (max_tiles + 1) / 2;
+  if (nn_v2() && lda >= (uint64_t)((K + 7) / 8 * 8)) {
+    // v2: two 4-wave blocks per CU over all column blocks; tiles spread
+    // evenly over the waves (at least one each), two per round
+    int gx2 = std::max(1, 512 / ncb);
+    gx2 = std::min(gx2, std::max(1, T / 4));
+    const int64_t W2 = (int64_t)gx2 * 4;
+    const int per_wave = (int)((T + W2 - 1) / W2);
+    const int rounds2 = (per_wave + 1) / 2;
+    const dim3 grid2(gx2, ncb);
+    const int lds = 2 * kS3Img;
+#define NTS_S3NN(E, MP)                                                                        \
+  do {                                                                                         \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_s3_nn<E, MP>),             \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));          \
+    hipLaunchKernelGGL((k_s3_nn<E, MP>), grid2, dim3(kS3V2Threads), lds, ctx->stream, M, N, K,   \
+                       A, lda, bimg, C, ldc, rounds2, ex);                                     \
+  } while (0)
+    if (epi) {
+      if (amap) NTS_S3NN(true, true); else NTS_S3NN(true, false);
+    } else {
+      if (amap) NTS_S3NN(false, true); else NTS_S3NN(false, false);
+    }
+#undef NTS_S3NN
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   const dim3 grid(gx, ncb);
-#define NTS_G3NN(E, MP)                                                                       \
+#define NTS_G3NN(E, MP)                                                                     \
   do {                                                                                          \
     NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm3_nn<E, MP>),         \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kS3NnLds));     \
@@ -553,6 +966,46 @@ int gemm3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda
   ex.bx = X;
   ex.ldbx = ldx;
   ex.bscale = bscale;
+  const bool v2_ok = ldb % 4 == 0 && (uintptr_t)B % 16 == 0 &&
+                     (!X || (ldx % 4 == 0 && (uintptr_t)X % 16 == 0)) &&
+                     (!amap || (uintptr_t)amap % 16 == 0);
+  if (!use_v1() && v2_ok) {
+    // v2: 8-wave blocks of up to 8 x TPW column tiles of A x 128 columns,
+    // the reduction split so that one block lands on every CU
+    constexpr int TPW = 3;
+    const int T = (M + 15) / 16;
+    const int nmb = (T + 8 * TPW - 1) / (8 * TPW), nnb = (N + 127) / 128;
+    const int ksteps = (K + 31) / 32;
+    int splits = std::max(1, std::min(256 / (nmb * nnb), ksteps / 4));
+    const int kchunk = ((ksteps + splits - 1) / splits) * 32;
+    splits = (K + kchunk - 1) / kchunk;
+    const uint64_t stride = (uint64_t)M * N;
+    float* out = C;
+    uint64_t ldo = ldc;
+    if (splits > 1) {
+      NTS_RET(ensure_scratch(ctx, stride * splits * sizeof(float) + 256));
+      out = (float*)ctx->scratch;
+      ldo = N;
+    }
+    const dim3 grid(nmb * nnb * splits);
+#define NTS_S3TN(BM, MP)                                                                          \
+  do {                                                                                            \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_s3_tn<TPW, BM, MP>),          \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kS3TnV2Lds));      \
+    hipLaunchKernelGGL((k_s3_tn<TPW, BM, MP>), grid, dim3(kS3TnV2Threads), kS3TnV2Lds, ctx->stream, M, \
+                       N, K, A, lda, B, ldb, out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0,   \
+                       nmb, nnb, ex);                                                             \
+  } while (0)
+    if (X) {
+      if (amap) NTS_S3TN(true, true); else NTS_S3TN(true, false);
+    } else {
+      if (amap) NTS_S3TN(false, true); else NTS_S3TN(false, false);
+    }
+#undef NTS_S3TN
+    NTS_LAUNCH_CHECK();
+    if (splits == 1) return NTS_OK;
+    return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+  }
   const int nrg = (M + kS3TnRows - 1) / kS3TnRows, ncb = (N + 127) / 128;
   int splits = std::max(1, std::min(256 / (nrg * ncb), (K + 4 * 32 - 1) / (4 * 32)));
   const int kchunk = ((K + splits - 1) / splits + 31) / 32 * 32;
