@@ -498,7 +498,7 @@ constexpr int kS3V2Threads = 256;
 //   B: the block copies the weight's pre-split 24 KB fragment image of the
 //      step into LDS (registers -> ds_write, double-buffered, one barrier per
 //      step); a wave reads 3 fragments per column tile for both row tiles.
-template <bool EPI, bool AMAP>
+template <bool EPI, bool AMAP, int DIAG = 0>
 __global__ __launch_bounds__(kS3V2Threads, 2) void k_s3_nn(int M, int N, int K,
                                                            const float* __restrict__ A, uint64_t lda,
                                                            const char* __restrict__ bimg,
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(kS3V2Threads, 2) void k_s3_nn(int M, int N, int K,
 
   const float* rbase[2];
   f32x4 acc[2][8];
-  float4 xa[2][2];     // [tile][half]: raw A fragments of the next step
+  float4 xa[2][2][2];  // [slot][tile][half]: raw A fragments of the next two steps
   bf16x8 pa[2][2][3];  // [slot][tile][piece]
   uint4 br0, br1, br2, br3, br4, br5;  // this thread's 6 x 16 B of a step's B image
 
@@ -569,14 +569,19 @@ __global__ __launch_bounds__(kS3V2Threads, 2) void k_s3_nn(int M, int N, int K,
   auto mma = [&](int buf, const bf16x8 (&p)[2][3], auto&& split_next) {
     const char* img = s3v2 + buf * kS3Img;
     bf16x8 b[2][3];
-    get3(img, kS3Frag, lane, b[0]);
+    if constexpr (DIAG & 4) {
+      b[0][0] = p[1][0]; b[0][1] = p[1][1]; b[0][2] = p[1][2];
+      b[1][0] = p[0][0]; b[1][1] = p[0][1]; b[1][2] = p[0][2];
+    } else {
+      get3(img, kS3Frag, lane, b[0]);
+    }
 #pragma unroll
     for (int ct = 0; ct < 8; ++ct) {
-      if (ct + 1 < 8) get3(img + (ct + 1) * 3 * kS3Frag, kS3Frag, lane, b[(ct + 1) & 1]);
+      if (!(DIAG & 4) && ct + 1 < 8) get3(img + (ct + 1) * 3 * kS3Frag, kS3Frag, lane, b[(ct + 1) & 1]);
       acc[0][ct] = mfma6(p[0], b[ct & 1], acc[0][ct]);
       acc[1][ct] = mfma6(p[1], b[ct & 1], acc[1][ct]);
-      if (ct == 5) split_next(0);
-      if (ct == 6) split_next(1);
+      if (ct == 1) split_next(0);
+      if (ct == 4) split_next(1);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -593,25 +598,35 @@ __global__ __launch_bounds__(kS3V2Threads, 2) void k_s3_nn(int M, int N, int K,
     }
     __syncthreads();  // the previous round's reads of both B buffers are done
     load_b(0);
-    load_a(0, xa);
+    load_a(0, xa[0]);
+    load_a(min(1, nsteps - 1), xa[1]);
     store_b(0);
     load_b(min(1, nsteps - 1));
-    split_a(xa, pa[0]);
+    split_a(xa[0], pa[0]);
     // step s: B(s) in buffer s&1, pieces of A(s) in pa[s&1], raw B(s+1) in
-    // registers; A(s+1) is loaded at the top of step s and split late in it
+    // registers, raw A(s+1) in xa[(s+1)&1]; A(s+2) is loaded into xa[s&1]
     auto step = [&](int s, auto par) {
       constexpr int P = decltype(par)::value;
       // unconditional (clamped) loads, stores and splits: a conditional
       // consumer makes the compiler's wait-count tracking assume loads still in
       // flight and drain them before reusing registers
-      __syncthreads();
-      store_b(1 - P);
-      load_b(min(s + 2, nsteps - 1));
-      load_a(min(s + 1, nsteps - 1), xa);
+      if constexpr (!(DIAG & 8)) __syncthreads();
+      if constexpr (!(DIAG & 1)) {
+        store_b(1 - P);
+        load_b(min(s + 2, nsteps - 1));
+        load_a(min(s + 2, nsteps - 1), xa[P]);
+      }
       mma(P, pa[P], [&](int rt) {
-        const float v[8] = {xa[rt][0].x, xa[rt][0].y, xa[rt][0].z, xa[rt][0].w,
-                            xa[rt][1].x, xa[rt][1].y, xa[rt][1].z, xa[rt][1].w};
-        split3(v, pa[1 - P][rt][0], pa[1 - P][rt][1], pa[1 - P][rt][2]);
+        const float v[8] = {xa[1 - P][rt][0].x, xa[1 - P][rt][0].y, xa[1 - P][rt][0].z,
+                            xa[1 - P][rt][0].w, xa[1 - P][rt][1].x, xa[1 - P][rt][1].y,
+                            xa[1 - P][rt][1].z, xa[1 - P][rt][1].w};
+        if constexpr (DIAG & 2) {
+          pa[1 - P][rt][0] = __builtin_bit_cast(bf16x8, xa[1 - P][rt][0]);
+          pa[1 - P][rt][1] = pa[P][rt][0];
+          pa[1 - P][rt][2] = pa[P][rt][1];
+        } else {
+          split3(v, pa[1 - P][rt][0], pa[1 - P][rt][1], pa[1 - P][rt][2]);
+        }
       });
     };
     for (int s = 0; s < nsteps; s += 2) {
@@ -919,12 +934,28 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
     const int rounds2 = (per_wave + 1) / 2;
     const dim3 grid2(gx2, ncb);
     const int lds = 2 * kS3Img;
+#define NTS_S3NN_D(E, MP, D)                                                                   \
+  do {                                                                                         \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_s3_nn<E, MP, D>),          \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));          \
+    hipLaunchKernelGGL((k_s3_nn<E, MP, D>), grid2, dim3(kS3V2Threads), lds, ctx->stream, M, N, K,\
+                       A, lda, bimg, C, ldc, rounds2, ex);                                     \
+  } while (0)
 #define NTS_S3NN(E, MP)                                                                        \
   do {                                                                                         \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_s3_nn<E, MP>),             \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));          \
-    hipLaunchKernelGGL((k_s3_nn<E, MP>), grid2, dim3(kS3V2Threads), lds, ctx->stream, M, N, K,   \
-                       A, lda, bimg, C, ldc, rounds2, ex);                                     \
+    if (!(E) && !(MP) && diag) {                                                               \
+      switch (diag) {                                                                          \
+        case 1: NTS_S3NN_D(false, false, 1); break;                                            \
+        case 2: NTS_S3NN_D(false, false, 2); break;                                            \
+        case 4: NTS_S3NN_D(false, false, 4); break;                                            \
+        case 8: NTS_S3NN_D(false, false, 8); break;                                            \
+        case 3: NTS_S3NN_D(false, false, 3); break;                                            \
+        case 15: NTS_S3NN_D(false, false, 15); break;                                          \
+        default: NTS_S3NN_D(false, false, 0);                                                  \
+      }                                                                                        \
+    } else {                                                                                   \
+      NTS_S3NN_D(E, MP, 0);                                                                    \
+    }                                                                                          \
   } while (0)
     if (epi) {
       if (amap) NTS_S3NN(true, true); else NTS_S3NN(true, false);

@@ -174,89 +174,112 @@ template size_t scan_tmp_elems<uint32_t>(uint64_t);
 template size_t scan_tmp_elems<uint64_t>(uint64_t);
 
 // ============================================================================
-// stable LSD radix sort (8-bit digits)
+// stable LSD radix sort: D-bit digits (D <= 9, passes = ceil(bits / 9)),
+// 4096-item tiles.  Per pass: per-tile digit counts (digit-major), one
+// exclusive scan over them, then a scatter in which each wave ranks its 1,024
+// contiguous items against a running per-wave digit count in LDS (match-any by
+// ballots, no barrier inside the item loop) — three barriers per tile.
+// Tiles past the device-side count n exit at once.
 // ============================================================================
 constexpr int kRadixThreads = 256;
-constexpr int kRadixItems = 8;
-constexpr int kRadixTile = kRadixThreads * kRadixItems;  // 2048
-constexpr int kRadixBins = 256;
+constexpr int kRadixItems = 16;
+constexpr int kRadixTile = kRadixThreads * kRadixItems;  // 4096
+constexpr int kRadixMaxBits = 9;
+constexpr int kRadixMaxBins = 1 << kRadixMaxBits;
 
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys,
                                                               const uint32_t* n_dev,
                                                               uint64_t n_cap, uint32_t shift,
-                                                              uint32_t* hist, uint32_t nb) {
-  __shared__ uint32_t h[kRadixBins];
+                                                              uint32_t mask, uint32_t* hist,
+                                                              uint32_t nb) {
+  __shared__ uint32_t h[kRadixMaxBins];
   const int t = threadIdx.x;
-  h[t] = 0;
+  const uint32_t bins = mask + 1;
+  for (uint32_t d = t; d < bins; d += kRadixThreads) h[d] = 0;
   __syncthreads();
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+  if (base < n) {
 #pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    uint64_t i = base + (uint64_t)k * kRadixThreads + t;
-    if (i < n) atomicAdd(&h[(keys[i] >> shift) & 255u], 1u);
+    for (int k = 0; k < kRadixItems; ++k) {
+      const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
+      if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
+    }
   }
   __syncthreads();
-  hist[(uint64_t)t * nb + blockIdx.x] = h[t];  // digit-major
+  for (uint32_t d = t; d < bins; d += kRadixThreads) hist[(uint64_t)d * nb + blockIdx.x] = h[d];
 }
 
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* n_dev,
-    uint64_t n_cap, uint32_t shift, const uint32_t* __restrict__ hist, uint32_t nb) {
-  __shared__ uint32_t goff[kRadixBins];                    // global offset of this block's digit run
-  __shared__ uint32_t wcnt[kRadixThreads / kWave][kRadixBins];  // per-wave digit counts -> prefixes
+    uint64_t n_cap, uint32_t shift, uint32_t dbits, const uint32_t* __restrict__ hist,
+    uint32_t nb) {
+  __shared__ uint32_t wh[kRadixThreads / kWave][kRadixMaxBins];  // per-wave counts -> offsets
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-  goff[t] = hist[(uint64_t)t * nb + blockIdx.x];
+  if (base >= n) return;  // whole tile past the end (uniform per block)
+  const uint32_t mask = (1u << dbits) - 1u, bins = mask + 1;
+  for (uint32_t d = t; d < bins; d += kRadixThreads)
+#pragma unroll
+    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) wh[ww][d] = 0;
+  __syncthreads();
+  // wave w ranks items base + 1024 w + 64 k + lane (index order) against its
+  // running digit counts
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t wbase = base + (uint64_t)w * (kRadixItems * kWave);
+  uint32_t key[kRadixItems], val[kRadixItems], rank[kRadixItems];
+#pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
+    const uint64_t i = wbase + (uint64_t)k * kWave + lane;
     const bool valid = i < n;
-    uint32_t key = valid ? keys_in[i] : 0u;
-    uint32_t val = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-    uint32_t d = (key >> shift) & 255u;
+    key[k] = valid ? keys_in[i] : 0u;
+    val[k] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+  }
 #pragma unroll
-    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) wcnt[ww][t] = 0;
-    __syncthreads();
-    // lanes of this wave holding the same digit (match-any via 8 ballots)
+  for (int k = 0; k < kRadixItems; ++k) {
+    const bool valid = wbase + (uint64_t)k * kWave + lane < n;
+    const uint32_t d = (key[k] >> shift) & mask;
     uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      bool bit = (d >> b) & 1u;
-      uint64_t m = __ballot(bit);
+    for (uint32_t b = 0; b < dbits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
       peers &= bit ? m : ~m;
     }
-    uint32_t rank = __popcll(peers & lt_mask);
-    if (valid && rank == 0) wcnt[w][d] = __popcll(peers);
-    __syncthreads();
-    {  // thread t owns digit t: exclusive prefix over waves, advance running base
-      uint32_t run = goff[t];
+    const uint32_t prev = wh[w][d];
+    const uint32_t before = (uint32_t)__popcll(peers & lt_mask);
+    rank[k] = prev + before;
+    if (valid && before == 0) wh[w][d] = prev + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // digit d's slice of this tile starts at the scanned count; waves follow in order
+  for (uint32_t d = t; d < bins; d += kRadixThreads) {
+    uint32_t run = hist[(uint64_t)d * nb + blockIdx.x];
 #pragma unroll
-      for (int ww = 0; ww < kRadixThreads / kWave; ++ww) {
-        uint32_t c = wcnt[ww][t];
-        wcnt[ww][t] = run;
-        run += c;
-      }
-      goff[t] = run;
+    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) {
+      const uint32_t c = wh[ww][d];
+      wh[ww][d] = run;
+      run += c;
     }
-    __syncthreads();
-    if (valid) {
-      uint32_t pos = wcnt[w][d] + rank;
-      keys_out[pos] = key;
-      vals_out[pos] = val;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    if (wbase + (uint64_t)k * kWave + lane < n) {
+      const uint32_t pos = wh[w][(key[k] >> shift) & mask] + rank[k];
+      keys_out[pos] = key[k];
+      vals_out[pos] = val[k];
     }
-    __syncthreads();
   }
 }
 
 size_t radix_tmp_bytes(uint64_t n_cap) {
   uint64_t nb = (n_cap + kRadixTile - 1) / kRadixTile;
   if (nb == 0) nb = 1;
-  size_t hist = (size_t)kRadixBins * nb + 1;
+  size_t hist = (size_t)kRadixMaxBins * nb + 1;
   size_t elems = 2 * ((n_cap + 63) / 64 * 64) + (hist + 63) / 64 * 64 +
-                 scan_tmp_elems<uint32_t>(kRadixBins * nb) + 64;
+                 scan_tmp_elems<uint32_t>(kRadixMaxBins * nb) + 64;
   return elems * sizeof(uint32_t);
 }
 
@@ -269,23 +292,25 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
   uint32_t* ktmp = (uint32_t*)tmp;
   uint32_t* vtmp = ktmp + n_al;
   uint32_t* hist = vtmp + n_al;
-  uint64_t hist_n = (uint64_t)kRadixBins * nb;
-  uint32_t* stmp = hist + (hist_n + 1 + 63) / 64 * 64;
-  int npass = (int)((bits + 7) / 8);
-  if (npass < 1) npass = 1;
+  if (bits < 1) bits = 1;
+  const int npass = (int)((bits + kRadixMaxBits - 1) / kRadixMaxBits);
+  const uint32_t dbits = (bits + npass - 1) / npass;
+  const uint32_t mask = (1u << dbits) - 1u;
+  const uint64_t hist_n = (uint64_t)(mask + 1) * nb;
+  uint32_t* stmp = hist + ((uint64_t)kRadixMaxBins * nb + 1 + 63) / 64 * 64;
   const uint32_t* ksrc = keys_in;
   const uint32_t* vsrc = vals_in;
   for (int p = 0; p < npass; ++p) {
     bool to_out = ((npass - 1 - p) % 2) == 0;
     uint32_t* kdst = to_out ? keys_out : ktmp;
     uint32_t* vdst = to_out ? vals_out : vtmp;
-    uint32_t shift = 8u * p;
+    const uint32_t shift = dbits * p;
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev,
-                       n_cap, shift, hist, nb);
+                       n_cap, shift, mask, hist, nb);
     NTS_LAUNCH_CHECK();
     NTS_RET(scan_exclusive<uint32_t>(hist, hist, nullptr, hist_n, stmp, stream));
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc,
-                       kdst, vdst, n_dev, n_cap, shift, (const uint32_t*)hist, nb);
+                       kdst, vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb);
     NTS_LAUNCH_CHECK();
     ksrc = kdst;
     vsrc = vdst;
