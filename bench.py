@@ -67,7 +67,7 @@ def parse():
                         "reference GPU kernel's mean (by sampled count)")
     p.add_argument("--transform-first", type=int, default=-1, choices=[-1, 0, 1],
                    help="bottom layer order: 1 A(XW), 0 (AX)W (the reference's), -1 auto")
-    p.add_argument("--gemm", default="f32", choices=["f32", "split3"],
+    p.add_argument("--gemm", default="split3", choices=["f32", "split3"],
                    help="layer GEMM arithmetic: f32 = fp32-input MFMA; split3 = fp32 operands "
                         "split exactly into three bf16 pieces, six piece products on the bf16 "
                         "MFMA (fp32-accurate, csrc/gemm3.hip)")
@@ -323,7 +323,9 @@ def workload_name(args, layers, V, En, tf) -> str:
          f"GPU sampler (Philox{', pipelined' if not args.no_pipeline else ''}) + "
          + ("transform-first bottom layer (row-gathered MFMA GEMM, aggregation + relu/dropout)"
             if tf else "fused gather/aggregation")
-         + f" + {'torch' if args.no_hip_gemm else 'MFMA fp32'} GEMMs + fused loss + fused Adam")
+         + " + " + ("torch" if args.no_hip_gemm else
+                    {"f32": "fp32-input MFMA", "split3": "fp32-accurate split-bf16 MFMA"}[args.gemm])
+         + " GEMMs + fused loss + fused Adam")
     if args.cache_rate >= 0:
         s += (f"; features in pinned host memory, {args.cache_rate:.0%} of rows (highest degree) "
               f"cached in HBM")

@@ -33,7 +33,7 @@ struct GCNConfig {
   int transform_first = -1;
   // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode): NTS_GEMM_F32 (fp32-input
   // MFMA) or NTS_GEMM_SPLIT3 (fp32-accurate three-piece bf16 split)
-  int gemm_mode = NTS_GEMM_F32;
+  int gemm_mode = NTS_GEMM_SPLIT3;
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
   // CACHE_RATE in [0, 1): the feature table moves to pinned host memory and
