@@ -21,11 +21,15 @@
 //               through a row map; a 512-thread block streams 32-deep k-slices
 //               of B (split and laid out in MFMA fragment order in LDS, double
 //               buffered) past 8 waves that each own 2 row tiles x 128 columns.
-//   k_gemm3_tn  C = A^T op(B) (weight gradient; relu/dropout backward fused in
-//               the B load), A's k rows optionally gathered: a 320 x 128
-//               output tile per block, k-slices of A and B staged transposed
-//               into fragment order, the long reduction split over blocks and
+//   k_s3_tn     C = A^T op(B) (weight gradient; relu/dropout backward fused in
+//               the B load), A's k rows optionally gathered: 8-wave blocks
+//               over one k-chunk, A^T fragments loaded straight to registers
+//               and split there, B staged as bf16 pieces in LDS and read with
+//               ds_read_b64_tr_b16, the long reduction split over blocks and
 //               summed in a fixed order (sum_splits) — deterministic.
+//   k_gemm3_tn  the first-generation TN (NTS_S3_V1=1): a 320 x 128 output
+//               tile per block, k-slices of A and B staged transposed into
+//               fragment order.
 #include "common.hpp"
 
 namespace nts_hip {
@@ -480,184 +484,11 @@ __global__ __launch_bounds__(kS3Threads, 1) void k_gemm3_tn(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
-// v2 kernels (the default; NTS_S3_V1=1 selects the first generation above):
-// 2 waves per SIMD that never meet at the same barrier (NN: two independent
-// 4-wave blocks per CU; TN: one 8-wave block), every operand
-// software-pipelined in registers two k-steps ahead, the split of step s+1
-// beside the MFMAs of step s, no branches on runtime flags in the k-loop.
-constexpr int kS3V2Threads = 256;
-
-// NN: C = A B (+ relu/dropout), A rows optionally gathered.  The M rows are
-// cut into 16-row tiles spread evenly over the grid's waves (t_lo .. t_hi); a
-// wave runs them two at a time (a missing second tile is a clamped duplicate
-// that is not stored) x all 128 columns of its column block.  Per 32-deep
-// k-step:
-//   A: each lane loads its fragment A[row i][k0 + 8g .. +7] straight into
-//      registers (two 16-byte loads per tile, two steps ahead) and splits it
-//      into three bf16 pieces one step ahead;
-//   B: the block copies the weight's pre-split 24 KB fragment image of the
-//      step into LDS (registers -> ds_write, double-buffered, one barrier per
-//      step); a wave reads 3 fragments per column tile for both row tiles.
-template <bool EPI, bool AMAP, int DIAG = 0>
-__global__ __launch_bounds__(kS3V2Threads, 2) void k_s3_nn(int M, int N, int K,
-                                                           const float* __restrict__ A, uint64_t lda,
-                                                           const char* __restrict__ bimg,
-                                                           float* __restrict__ C, uint64_t ldc,
-                                                           int rounds, Gemm3Extra ex) {
-  extern __shared__ __attribute__((aligned(16))) char s3v2[];  // [2][kS3Img]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.y * 128;
-  const int T = (M + 15) / 16;
-  const int64_t W = (int64_t)gridDim.x * 4;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + wv;
-  const int t_lo = (int)(gw * T / W), t_hi = max((int)((gw + 1) * T / W), t_lo + 1);
-  const int nsteps = (K + 31) / 32, nfull = K / 32;
-  const size_t bstep = (size_t)gridDim.y * kS3Img;
-  const char* bsrc = bimg + (size_t)blockIdx.y * kS3Img + 16 * tid;
-
-  const float* rbase[2];
-  f32x4 acc[2][8];
-  float4 xa[2][2][2];  // [slot][tile][half]: raw A fragments of the next two steps
-  bf16x8 pa[2][2][3];  // [slot][tile][piece]
-  uint4 br0, br1, br2, br3, br4, br5;  // this thread's 6 x 16 B of a step's B image
-
-  auto load_b = [&](int s) {
-    const uint4* p = reinterpret_cast<const uint4*>(bsrc + (size_t)s * bstep);
-    br0 = p[0]; br1 = p[256]; br2 = p[512]; br3 = p[768]; br4 = p[1024]; br5 = p[1280];
-  };
-  auto store_b = [&](int buf) {
-    uint4* p = reinterpret_cast<uint4*>(s3v2 + buf * kS3Img + 16 * tid);
-    p[0] = br0; p[256] = br1; p[512] = br2; p[768] = br3; p[1024] = br4; p[1280] = br5;
-  };
-  // the partial last step reads up to 7 floats past K inside the row pitch
-  // (the launcher requires lda >= K rounded up to 8) and zeroes them
-  auto load_a = [&](int s, float4 (&x)[2][2]) {
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const float* p = rbase[rt] + 32 * s + 8 * g;
-      x[rt][0] = *reinterpret_cast<const float4*>(p);
-      x[rt][1] = *reinterpret_cast<const float4*>(p + 4);
-    }
-    if (s >= nfull) {
-      const int k = 32 * s + 8 * g;
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        x[rt][0].x = k + 0 < K ? x[rt][0].x : 0.f;
-        x[rt][0].y = k + 1 < K ? x[rt][0].y : 0.f;
-        x[rt][0].z = k + 2 < K ? x[rt][0].z : 0.f;
-        x[rt][0].w = k + 3 < K ? x[rt][0].w : 0.f;
-        x[rt][1].x = k + 4 < K ? x[rt][1].x : 0.f;
-        x[rt][1].y = k + 5 < K ? x[rt][1].y : 0.f;
-        x[rt][1].z = k + 6 < K ? x[rt][1].z : 0.f;
-        x[rt][1].w = k + 7 < K ? x[rt][1].w : 0.f;
-      }
-    }
-  };
-  auto split_a = [&](const float4 (&x)[2][2], bf16x8 (&p)[2][3]) {
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const float v[8] = {x[rt][0].x, x[rt][0].y, x[rt][0].z, x[rt][0].w,
-                          x[rt][1].x, x[rt][1].y, x[rt][1].z, x[rt][1].w};
-      split3(v, p[rt][0], p[rt][1], p[rt][2]);
-    }
-  };
-  // MFMAs of one step, B fragments read one column tile ahead (scheduling
-  // fences keep the live fragments at two column tiles); the next step's A
-  // pieces (split_next) are computed beside column tiles 1 and 4
-  auto mma = [&](int buf, const bf16x8 (&p)[2][3], auto&& split_next) {
-    const char* img = s3v2 + buf * kS3Img;
-    bf16x8 b[2][3];
-    if constexpr (DIAG & 4) {
-      b[0][0] = p[1][0]; b[0][1] = p[1][1]; b[0][2] = p[1][2];
-      b[1][0] = p[0][0]; b[1][1] = p[0][1]; b[1][2] = p[0][2];
-    } else {
-      get3(img, kS3Frag, lane, b[0]);
-    }
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct) {
-      if (!(DIAG & 4) && ct + 1 < 8) get3(img + (ct + 1) * 3 * kS3Frag, kS3Frag, lane, b[(ct + 1) & 1]);
-      acc[0][ct] = mfma6(p[0], b[ct & 1], acc[0][ct]);
-      acc[1][ct] = mfma6(p[1], b[ct & 1], acc[1][ct]);
-      if (ct == 1) split_next(0);
-      if (ct == 4) split_next(1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  for (int rd = 0; rd < rounds; ++rd) {
-    const int base = t_lo + 2 * rd;
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int64_t row = (int64_t)min(base + rt, t_hi - 1) * 16 + i;
-      const uint64_t rr = (uint64_t)(row < M ? row : M - 1);
-      rbase[rt] = A + (AMAP ? (uint64_t)ex.amap[rr] : rr) * lda;
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    __syncthreads();  // the previous round's reads of both B buffers are done
-    load_b(0);
-    load_a(0, xa[0]);
-    load_a(min(1, nsteps - 1), xa[1]);
-    store_b(0);
-    load_b(min(1, nsteps - 1));
-    split_a(xa[0], pa[0]);
-    // step s: B(s) in buffer s&1, pieces of A(s) in pa[s&1], raw B(s+1) in
-    // registers, raw A(s+1) in xa[(s+1)&1]; A(s+2) is loaded into xa[s&1]
-    auto step = [&](int s, auto par) {
-      constexpr int P = decltype(par)::value;
-      // unconditional (clamped) loads, stores and splits: a conditional
-      // consumer makes the compiler's wait-count tracking assume loads still in
-      // flight and drain them before reusing registers
-      if constexpr (!(DIAG & 8)) __syncthreads();
-      if constexpr (!(DIAG & 1)) {
-        store_b(1 - P);
-        load_b(min(s + 2, nsteps - 1));
-        load_a(min(s + 2, nsteps - 1), xa[P]);
-      }
-      mma(P, pa[P], [&](int rt) {
-        const float v[8] = {xa[1 - P][rt][0].x, xa[1 - P][rt][0].y, xa[1 - P][rt][0].z,
-                            xa[1 - P][rt][0].w, xa[1 - P][rt][1].x, xa[1 - P][rt][1].y,
-                            xa[1 - P][rt][1].z, xa[1 - P][rt][1].w};
-        if constexpr (DIAG & 2) {
-          pa[1 - P][rt][0] = __builtin_bit_cast(bf16x8, xa[1 - P][rt][0]);
-          pa[1 - P][rt][1] = pa[P][rt][0];
-          pa[1 - P][rt][2] = pa[P][rt][1];
-        } else {
-          split3(v, pa[1 - P][rt][0], pa[1 - P][rt][1], pa[1 - P][rt][2]);
-        }
-      });
-    };
-    for (int s = 0; s < nsteps; s += 2) {
-      step(s, std::integral_constant<int, 0>());
-      if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>());
-    }
-    // acc[rt][ct][v] = C[16 t + 4 g + v][n0 + 16 ct + i]
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      if (base + rt >= t_hi) continue;
-      const int64_t r4 = (int64_t)(base + rt) * 16 + 4 * g;
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-        const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
-        if ((int)col >= N) continue;
-        float o[4] = {acc[rt][ct][0], acc[rt][ct][1], acc[rt][ct][2], acc[rt][ct][3]};
-        if constexpr (EPI) {
-          const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
-          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
-        }
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
-      }
-    }
-  }
-}
-
+// TN v2 (the default for TN; NTS_S3_V1=1 selects k_gemm3_tn above): two
+// waves per SIMD, every operand software-pipelined in registers ahead of its
+// MFMAs, the split of step s+1 beside the MFMAs of step s (the loads and
+// splits of the last steps are skipped by uniform branches: clamped
+// unconditional ones measured slower here, their live ranges spill).
 // TN: C[M x N] = A[K x M]^T op(B)[K x N] (weight gradient; A's K rows
 // optionally gathered through a row map, op(B) = B or the relu/dropout
 // backward B * bscale where X > 0).  An 8-wave block takes one k-chunk, a
@@ -876,19 +707,15 @@ bool gemm3_nn_ok(int M, int N, int K, const float* A, uint64_t lda) {
 }
 bool gemm3_tn_ok(int M, int N, int K) { return M >= 1 && K >= 256 && N % 16 == 0; }
 
-// Kernel generation per GEMM kind (A/B switches): TN runs v2 unless
-// NTS_S3_V1=1; NN runs v1 (measured equal or faster on the layer shapes)
-// unless NTS_S3_NN2=1.
-static bool env_on(const char* name) {
-  const char* e = getenv(name);
-  return e && e[0] == '1';
-}
+// NTS_S3_V1=1: the first-generation TN kernel (k_gemm3_tn), for A/B.  (A
+// second-generation NN kernel with the same register pipeline as k_s3_tn
+// measured equal to k_gemm3_nn on the gathered shape and slower on the dense
+// one — DESIGN §3 — so NN keeps k_gemm3_nn.)
 static bool use_v1() {
-  static const bool v = env_on("NTS_S3_V1");
-  return v;
-}
-static bool nn_v2() {
-  static const bool v = env_on("NTS_S3_NN2") && !env_on("NTS_S3_V1");
+  static const bool v = [] {
+    const char* e = getenv("NTS_S3_V1");
+    return e && e[0] == '1';
+  }();
   return v;
 }
 
@@ -924,48 +751,6 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
   const int64_t W = (int64_t)gx * 8;
   const int max_tiles = (int)((T + W - 1) / W);
   const int rounds = (max_tiles + 1) / 2;
-  if (nn_v2() && lda >= (uint64_t)((K + 7) / 8 * 8)) {
-    // v2: two 4-wave blocks per CU over all column blocks; tiles spread
-    // evenly over the waves (at least one each), two per round
-    int gx2 = std::max(1, 512 / ncb);
-    gx2 = std::min(gx2, std::max(1, T / 4));
-    const int64_t W2 = (int64_t)gx2 * 4;
-    const int per_wave = (int)((T + W2 - 1) / W2);
-    const int rounds2 = (per_wave + 1) / 2;
-    const dim3 grid2(gx2, ncb);
-    const int lds = 2 * kS3Img;
-#define NTS_S3NN_D(E, MP, D)                                                                   \
-  do {                                                                                         \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_s3_nn<E, MP, D>),          \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));          \
-    hipLaunchKernelGGL((k_s3_nn<E, MP, D>), grid2, dim3(kS3V2Threads), lds, ctx->stream, M, N, K,\
-                       A, lda, bimg, C, ldc, rounds2, ex);                                     \
-  } while (0)
-#define NTS_S3NN(E, MP)                                                                        \
-  do {                                                                                         \
-    if (!(E) && !(MP) && diag) {                                                               \
-      switch (diag) {                                                                          \
-        case 1: NTS_S3NN_D(false, false, 1); break;                                            \
-        case 2: NTS_S3NN_D(false, false, 2); break;                                            \
-        case 4: NTS_S3NN_D(false, false, 4); break;                                            \
-        case 8: NTS_S3NN_D(false, false, 8); break;                                            \
-        case 3: NTS_S3NN_D(false, false, 3); break;                                            \
-        case 15: NTS_S3NN_D(false, false, 15); break;                                          \
-        default: NTS_S3NN_D(false, false, 0);                                                  \
-      }                                                                                        \
-    } else {                                                                                   \
-      NTS_S3NN_D(E, MP, 0);                                                                    \
-    }                                                                                          \
-  } while (0)
-    if (epi) {
-      if (amap) NTS_S3NN(true, true); else NTS_S3NN(true, false);
-    } else {
-      if (amap) NTS_S3NN(false, true); else NTS_S3NN(false, false);
-    }
-#undef NTS_S3NN
-    NTS_LAUNCH_CHECK();
-    return NTS_OK;
-  }
   const dim3 grid(gx, ncb);
 #define NTS_G3NN(E, MP)                                                                     \
   do {                                                                                          \
