@@ -125,16 +125,23 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # NTS_BENCH_SHARE_GPU=1: every rank on device 0 (rehearsing the DP path on a
-    # one-GPU box; the numbers are then not a scaling measurement)
-    if os.environ.get("NTS_BENCH_SHARE_GPU") == "1":
+    # NTS_BENCH_SHARE_GPU=1: every rank on device 0 — a rehearsal of the
+    # multi-rank control flow on a one-GPU box (RCCL refuses two ranks on one
+    # device, so the ranks then talk over gloo and train without the gradient
+    # all-reduce; the numbers are not a scaling measurement)
+    shared = os.environ.get("NTS_BENCH_SHARE_GPU") == "1"
+    if shared:
         local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    cdev = torch.device("cpu") if shared else dev  # device of the timing collectives
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from nts import host, synthetic
     from nts import _abi
@@ -159,7 +166,7 @@ def main():
     dst_host = g.dst.cpu().numpy().view(np.uint32) if want_cpu else None
     del g
 
-    comm = ndist.make_communicator(E, world, rank, local_rank)
+    comm = None if shared else ndist.make_communicator(E, world, rank, local_rank)
 
     fan = [int(x) for x in args.fanout.split("-")]
     layers = ([int(x) for x in args.layers.split("-")] if args.layers else [F_dim, args.hidden, C])
@@ -195,7 +202,7 @@ def main():
         if world == 1:
             return x
         import torch.distributed as dist
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
@@ -203,7 +210,7 @@ def main():
         if world == 1:
             return x
         import torch.distributed as dist
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t[0])
 
@@ -281,7 +288,7 @@ def main():
         "config": {
             "workload": workload_name(args, layers, V, En, tf),
             "global_batch": args.batch * world,
-            "parallelism": f"dp{world}",
+            "parallelism": f"dp{world}" + ("-shared-gpu-rehearsal (gloo, no all-reduce)" if shared and world > 1 else ""),
             "fanout": args.fanout,
             "epoch_time_s": epoch_s,
             "epoch_time_kind": epoch_kind,

@@ -21,6 +21,8 @@ import sys
 
 # bench profiler kernel -> how its HIP kernel reads in a rocprofv3 trace
 def profiler_kernel(name: str):
+    if "nts_hip::k_gat_fwd" in name:
+        return "gat_forward"
     m = re.search(r"nts_hip::(\w+)<([^>]*)>", name)
     if not m:
         return None
@@ -36,8 +38,12 @@ def profiler_kernel(name: str):
         return None
     if k == "k_gemm_wres" and targs[2] == "false":
         return "gather_gemm"                     # X[src] W0 (no epilogue)
+    if k == "k_gemm3_nn" and targs == ["false", "true"]:
+        return "gather_gemm"                     # split-bf16 X[src] W0
     if k == "k_gemm_tn_big" and targs[0] == "false":
         return "gather_gemm_tn"                  # X[src]^T dH (no mask)
+    if k == "k_s3_tn" and targs[1:] == ["false", "true"]:
+        return "gather_gemm_tn"                  # split-bf16 X[src]^T dH
     return None
 
 

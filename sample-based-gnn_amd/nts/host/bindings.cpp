@@ -19,7 +19,7 @@ static py::list layers_of(SampledSubgraph* sg) {
   for (auto* s : sg->sampled_sgs) {
     py::dict d;
     auto n = [](const torch::Tensor& t, int64_t k) {
-      return t.defined() ? t.narrow(0, 0, k) : torch::Tensor();
+      return t.defined() ? t.narrow(0, 0, std::min<int64_t>(k, t.size(0))) : torch::Tensor();
     };
     d["v_size"] = s->v_size;
     d["e_size"] = s->e_size;
@@ -230,7 +230,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("loss", [](GCN_SAMPLE_ALLGPU_impl& d) { return d.loss; })
       .def_property_readonly("n_train", [](GCN_SAMPLE_ALLGPU_impl& d) { return d.sampler->work_range[1]; })
       .def_property_readonly("last_layers",
-                             [](GCN_SAMPLE_ALLGPU_impl& d) { return layers_of(d.sampler->ssg); })
+                             [](GCN_SAMPLE_ALLGPU_impl& d) {
+                               // the last TRAINED batch (the sampler's current
+                               // slot may already hold the next, in flight)
+                               return layers_of(d.last_sg ? d.last_sg : d.sampler->ssg);
+                             })
       .def_readonly("sample_time", &GCN_SAMPLE_ALLGPU_impl::sample_time)
       .def_readonly("train_time", &GCN_SAMPLE_ALLGPU_impl::train_time)
       .def_readonly("batch_edges", &GCN_SAMPLE_ALLGPU_impl::batch_edges)

@@ -944,7 +944,7 @@ KernelProfiler::~KernelProfiler() {
 }
 const char* KernelProfiler::name(int id) {
   static const char* n[kCount] = {"bottom_aggregation", "gather_gemm", "gather_gemm_tn",
-                                  "bottom_backward"};
+                                  "bottom_backward", "gat_forward"};
   return n[id];
 }
 void KernelProfiler::begin(Id id, hipStream_t st) {
@@ -995,9 +995,10 @@ void KernelProfiler::reset() {
 // dW_att = H^T dS, dX = dH W^T).
 struct HipGATLayerFn : public torch::autograd::Function<HipGATLayerFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar X, NtsVar W, NtsVar Watt, int64_t sg_ptr,
-                        int64_t cs_ptr) {
+                        int64_t cs_ptr, int64_t prof_ptr) {
     auto* sg = reinterpret_cast<sampCSC*>(sg_ptr);
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
+    auto* prof = reinterpret_cast<KernelProfiler*>(prof_ptr);
     TORCH_CHECK(sg->dst_local_id.defined() && sg->csr_edge_id.defined(),
                 "GAT needs a merged src/dst layer with its CSR (set_merge_src_dst)");
     NtsVar Xc = row_major(X), Wc = W.contiguous(), Ac = Watt.contiguous();
@@ -1013,11 +1014,18 @@ struct HipGATLayerFn : public torch::autograd::Function<HipGATLayerFn> {
     NtsVar m = torch::empty({std::max<int64_t>(e, 1)}, f32_opts(dev));
     NtsVar a = torch::empty({std::max<int64_t>(e, 1)}, f32_opts(dev));
     NtsVar Y = torch::empty({v, F}, f32_opts(dev));
+    hipStream_t st = (hipStream_t)cs->stream();
+    if (prof) prof->begin(KernelProfiler::GAT_FWD, st);
     hip_check(nts_hip_gat_forward(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_dst_local_id(),
                                   (uint32_t)v, H.data_ptr<float>(), (uint64_t)F, (uint32_t)F,
                                   Ac.data_ptr<float>(), m.data_ptr<float>(), a.data_ptr<float>(),
                                   Y.data_ptr<float>(), (uint64_t)F),
               "nts_hip_gat_forward");
+    // compulsory bytes: H rows once, offsets, row index + score + weight per
+    // edge, dst local ids, W_att, output rows
+    if (prof)
+      prof->end(KernelProfiler::GAT_FWD, st,
+                4.0 * F * s + 4.0 * (v + 1) + 12.0 * e + 4.0 * v + 8.0 * F + 4.0 * F * v);
     ctx->save_for_backward({Xc, Wc, Ac, H, Y, m, a});
     ctx->saved_data["sg"] = sg_ptr;
     ctx->saved_data["cs"] = cs_ptr;
@@ -1068,14 +1076,14 @@ struct HipGATLayerFn : public torch::autograd::Function<HipGATLayerFn> {
                                  dX.data_ptr<float>(), (uint64_t)Fin),
                 "nts_hip_gemm_f32(dX)");
     }
-    return {dX, dW, dA.view(A.sizes()), NtsVar(), NtsVar()};
+    return {dX, dW, dA.view(A.sizes()), NtsVar(), NtsVar(), NtsVar()};
   }
 };
 
 NtsVar hip_gat_layer(const NtsVar& x, const NtsVar& W, const NtsVar& Watt, sampCSC* sg,
-                     NtsStream* cs) {
+                     NtsStream* cs, KernelProfiler* prof) {
   return HipGATLayerFn::apply(x, W, Watt, reinterpret_cast<int64_t>(sg),
-                              reinterpret_cast<int64_t>(cs));
+                              reinterpret_cast<int64_t>(cs), reinterpret_cast<int64_t>(prof));
 }
 
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs) {

@@ -373,7 +373,8 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_gat(SampledSubgraph* sg) {
   std::vector<NtsVar> acts;
   for (int l = 0; l < L; ++l) {
     const int hop = L - 1 - l;  // X_{l+1} = relu(attention aggregate of X_l W_l)
-    X = hip_gat_layer(X, P[2 * l]->W, P[2 * l + 1]->W, sg->sampled_sgs[hop], cs.get());
+    X = hip_gat_layer(X, P[2 * l]->W, P[2 * l + 1]->W, sg->sampled_sgs[hop], cs.get(),
+                      profiler());
     acts.push_back(X);
   }
   return acts;
@@ -452,6 +453,7 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
     }
   }
   fresh_pass_ = false;
+  last_sg = sg;
   TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[slot], 0) == hipSuccess,
               "hipStreamWaitEvent");
   double t1 = now_s();

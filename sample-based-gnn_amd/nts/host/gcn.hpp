@@ -118,6 +118,8 @@ class GCN_SAMPLE_ALLGPU_impl {
   bool transform_first() const { return tf_; }
   uint64_t eval_seq = uint64_t(1) << 40;  // PHILOX stream of the evaluation batches
 
+  SampledSubgraph* last_sg = nullptr;  // the batch the last train_batch() trained on
+
  private:
   NtsVar vertexForward(int l, NtsVar& a);
   // with `loss_target` (training), the last element is the fused scalar loss

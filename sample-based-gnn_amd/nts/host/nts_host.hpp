@@ -363,8 +363,9 @@ class NtsContext {
 NtsVar hip_linear(const NtsVar& x, const NtsVar& W, NtsStream* cs);
 // one GAT layer (H = X W, attention softmax over each dst's sampled edges,
 // relu(sum a H[src])) on a merged src/dst layer: [src_size, F_in] -> [v_size, F]
+class KernelProfiler;
 NtsVar hip_gat_layer(const NtsVar& x, const NtsVar& W, const NtsVar& Watt, sampCSC* sg,
-                     NtsStream* cs);
+                     NtsStream* cs, KernelProfiler* prof = nullptr);
 // CU masks splitting the device: `n` CUs spread evenly over the chip
 // (every (total/n)-th CU) and the complement
 std::vector<uint32_t> cu_mask_spread(int device, int n, bool complement);
@@ -390,7 +391,7 @@ NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
 // the algorithmic bytes (aggregations) or flops (GEMMs) of one launch.
 class KernelProfiler {
  public:
-  enum Id { BOTTOM_AGG = 0, GATHER_GEMM, GATHER_GEMM_TN, BOTTOM_BWD, kCount };
+  enum Id { BOTTOM_AGG = 0, GATHER_GEMM, GATHER_GEMM_TN, BOTTOM_BWD, GAT_FWD, kCount };
   struct Stat {
     double ms = 0, units = 0;
     uint64_t calls = 0;

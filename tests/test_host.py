@@ -316,3 +316,21 @@ def test_gat_training_deterministic_and_learns(E, graph):
     for x, y in zip(a.weights(), b.weights()):
         assert torch.equal(x, y)
     assert all(np.isfinite(losses))
+
+
+def test_last_layers_is_the_trained_batch_across_a_partial_batch(E, graph):
+    """bench.py reads last_layers after the timed steps; with the pipeline the
+    sampler's current slot already holds the next (possibly partial) batch.
+    last_layers must describe the batch just trained, whatever its size."""
+    drv, _, _, train = _driver(E, graph, 32, 5, [32, 16, 5], [10, 5], 1000)
+    n = int(train.numel())
+    sizes = [min(1000, n - 1000 * b) for b in range((n + 999) // 1000)]
+    assert sizes[-1] < 1000  # the pass ends with a partial batch
+    for step in range(2 * len(sizes) + 1):
+        if not drv.sample_not_finished():
+            drv.restart()
+        drv.train_batch()
+        lay = drv.last_layers
+        assert lay[0]["v_size"] == sizes[step % len(sizes)]
+        assert lay[0]["destination"].numel() == lay[0]["v_size"]
+    drv.synchronize()
