@@ -1,0 +1,78 @@
+"""bench.py's reporting logic on CPU: the roofline picks the dominant kernel by
+device time and divides its algorithmic units by the live average launch; a
+committed PMC pass is attached only when it was taken on this very
+libnts_hip.so build, kernel and workload (a stale pass is refused, with the
+reason stated); the metric label follows the workload."""
+import importlib.util
+import json
+import pathlib
+import types
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _args(**kw):
+    base = dict(shape="reddit", batch=10000, fanout="25-10", weight="sum", transform_first=-1,
+                model="gcn", cache_rate=-1.0, gemm="split3", no_hip_gemm=False, no_pipeline=False)
+    base.update(kw)
+    return types.SimpleNamespace(**base)
+
+
+def test_roofline_dominant_kernel_and_units(bench, monkeypatch):
+    monkeypatch.setattr(bench, "attach_pmc", lambda *a, **k: None)
+    prof = {"bottom_aggregation": {"ms": 10.0, "calls": 20, "units": 20 * 0.87e9},
+            "gat_forward": {"ms": 0.0, "calls": 0, "units": 0.0},
+            "gather_gemm": {"ms": 2.0, "calls": 20, "units": 20 * 35e9}}
+    rl = bench.roofline(prof, _args(), [602, 128, 41], 1)
+    assert rl["kernel"] == "bottom_aggregation" and rl["bound"] == "hbm"
+    assert rl["avg_launch_ms"] == pytest.approx(0.5)
+    assert rl["achieved"] == pytest.approx(0.87e9 / 0.5e-3 / 1e9)
+    assert rl["frac"] == pytest.approx(rl["achieved"] / bench.HBM_PEAK_GBS)
+    assert rl["kernels"]["gather_gemm"]["bound"] == "mfma"
+    assert "gat_forward" not in rl["kernels"]
+
+
+def test_pmc_attached_only_for_the_same_build_and_workload(bench, monkeypatch, tmp_path):
+    (tmp_path / "profiles").mkdir()
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "abc")
+    args, layers = _args(), [602, 128, 41]
+    wl = bench.pmc_workload(args, layers, 1)
+    info = {"workload": wl, "lib_sha256": "abc", "profiler_kernel": "bottom_aggregation",
+            "kernels": {"k": {"profiler_kernel": "bottom_aggregation",
+                              "hbm_bytes_per_launch": 3.75e9}}}
+    (tmp_path / "profiles" / "pmc_x.json").write_text(json.dumps(info))
+    rl = {"avg_launch_ms": 0.5}
+    bench.attach_pmc(rl, "bottom_aggregation", args, layers, 1)
+    assert rl["traffic"] == pytest.approx(3.75e9)
+    assert rl["traffic_GBs"] == pytest.approx(3.75e9 / 0.5e-3 / 1e9)
+    # another build: refused, reason stated
+    info["lib_sha256"] = "old"
+    (tmp_path / "profiles" / "pmc_x.json").write_text(json.dumps(info))
+    rl = {"avg_launch_ms": 0.5}
+    bench.attach_pmc(rl, "bottom_aggregation", args, layers, 1)
+    assert "traffic" not in rl and "another libnts_hip.so build" in rl["traffic_note"]
+    # another workload: not attached
+    info["lib_sha256"] = "abc"
+    (tmp_path / "profiles" / "pmc_x.json").write_text(json.dumps(info))
+    rl = {"avg_launch_ms": 0.5}
+    bench.attach_pmc(rl, "bottom_aggregation", _args(batch=1024), layers, 1)
+    assert "traffic" not in rl
+
+
+def test_metric_and_workload_labels(bench):
+    assert "2-hop GCN on Reddit-shaped" in bench.metric_name(_args(), [602, 128, 41])
+    assert "3-hop GraphSAGE on ogbn-products-shaped" in bench.metric_name(
+        _args(shape="products", weight="mean"), [100, 256, 256, 47])
+    w = bench.workload_name(_args(), [602, 128, 41], 232965, 114848857, False)
+    assert "split-bf16" in w and "fused gather/aggregation" in w
