@@ -668,7 +668,14 @@ void GCN_SAMPLE_ALLGPU_impl::set_presample(const std::vector<uint32_t>& counts,
   pd_sampler_->rng_mode = cfg.rng_mode;
   pd_sampler_->batch_seq = uint64_t(1) << 48;  // a PHILOX stream of its own
   const int64_t Fin = cfg.layer_size[0];
-  for (int i = 0; i < kPdRing; ++i) pd_y_[i] = torch::empty({(int64_t)mx, Fin}, f32_opts(graph->device));
+  for (int i = 0; i < kPdRing; ++i) {
+    pd_y_[i] = torch::empty({(int64_t)mx, Fin}, f32_opts(graph->device));
+    if (fcache)  // the hot rows' neighbours may be spilled to the host table
+      pd_stage_[i] = torch::empty(
+          {(int64_t)std::max<uint32_t>(pd_sampler_->ssgs[i]->sampled_sgs[0]->s_cap, 1),
+           (int64_t)fcache->ld},
+          f32_opts(graph->device));
+  }
   pd_share_ = torch::empty({(int64_t)mx, (int64_t)cfg.layer_size[1]}, f32_opts(graph->device));
   pd_ids_ = torch::empty({(int64_t)std::max<size_t>(ids.size(), 1)}, u32_opts(graph->device));
   if (!ids.empty())
@@ -701,11 +708,16 @@ void GCN_SAMPLE_ALLGPU_impl::pd_issue(int slot, NtsStream& st) {
       pd_sampler_->issue_gpu_sample((int)n, ring, st, cfg.weight_type);
       sampCSC* h = pd_sampler_->ssgs[ring]->sampled_sgs[0];
       NtsVar& y = pd_y_[ring];
-      hip_check(nts_hip_spmm_csc_fwd(st.ctx(), h->dev_c_o(), h->dev_r_i(), h->dev_e_w_f(),
-                                     dptr<uint32_t>(h->sizes), h->v_cap, F.data_ptr<float>(),
-                                     (uint64_t)F.stride(0), h->dev_src(), (uint32_t)F.size(1),
-                                     y.data_ptr<float>(), (uint64_t)y.stride(0)),
-                "nts_hip_spmm_csc_fwd(pd)");
+      if (fcache)  // two-tier table: cached rows from HBM, the rest staged once from the host
+        fcache->aggregate(st.ctx(), h, dptr<uint32_t>(h->sizes), h->v_cap,
+                          dptr<uint32_t>(h->sizes) + 2, h->s_cap, pd_stage_[ring].data_ptr<float>(),
+                          y.data_ptr<float>(), (uint64_t)y.stride(0));
+      else
+        hip_check(nts_hip_spmm_csc_fwd(st.ctx(), h->dev_c_o(), h->dev_r_i(), h->dev_e_w_f(),
+                                       dptr<uint32_t>(h->sizes), h->v_cap, F.data_ptr<float>(),
+                                       (uint64_t)F.stride(0), h->dev_src(), (uint32_t)F.size(1),
+                                       y.data_ptr<float>(), (uint64_t)y.stride(0)),
+                  "nts_hip_spmm_csc_fwd(pd)");
     }
   }
   pd_slot_key_[slot] = (int)pd_next_key_;

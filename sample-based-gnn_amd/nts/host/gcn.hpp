@@ -146,6 +146,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   NtsVar pd_ids_, pd_cache_map_, pd_cache_loc_;  // device: ids; u32 [V] map / location
   std::unique_ptr<FastSampler> pd_sampler_;      // 1 layer (bottom fanout) over the hot ids
   NtsVar pd_y_[kPdRing];              // their aggregation A X, per ring slot
+  NtsVar pd_stage_[kPdRing];          // spilled feature rows of that aggregation (feature cache)
   NtsVar pd_share_;                   // (A X) W of the current super-batch
   uint32_t pd_next_key_ = 0;
   int pd_slot_key_[3] = {0, 0, 0};    // per sampler slot (kSlots): its super-batch key

@@ -285,3 +285,24 @@ def test_pd_driver_step_matches_oracle_chain(E, graph):
     ref = torch.nn.functional.nll_loss(out.log_softmax(1), tgt)
     assert np.isin(l1["destination"], hot).sum() > 10  # the cache is exercised
     assert abs(loss - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cache_rate", [0.0, 0.3])
+def test_pd_driver_with_feature_cache_is_identical(E, graph, cache_rate):
+    """GS_SAMPLE_PD_CACHE's placement: the feature table in pinned host memory
+    with the highest-degree rows cached in HBM.  The PD push-down aggregation
+    of the hot vertices then reads the two-tier table too; training is
+    bit-identical to the all-HBM table."""
+    a, *_ = _pd_driver(E, graph, 0.3, pd_cache=True, pd_rate=0.3, pd_super_batch=2,
+                       drop_rate=0.5, early_aggregate=False)
+    b, *_ = _pd_driver(E, graph, 0.3, pd_cache=True, pd_rate=0.3, pd_super_batch=2,
+                       drop_rate=0.5, early_aggregate=False, cache_rate=cache_rate)
+    b.set_weights(a.weights())
+    for _ in range(5):
+        a.train_batch()
+        b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)
