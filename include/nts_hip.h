@@ -155,10 +155,14 @@ int nts_hip_ctx_reserve(nts_hip_ctx *ctx, uint64_t n_vertices, uint64_t max_item
  * MFMA (one fp32 fma chain per output, the reference's fp32 GEMM semantics);
  * NTS_GEMM_SPLIT3 = fp32 operands split exactly into three bf16 pieces, the
  * six significant piece products on the bf16 MFMA with fp32 accumulation
- * (error vs fp64 of the same order as the fp32 path; csrc/gemm3.hip).
- * Shapes the split kernels do not take run on the fp32 path. */
+ * (error vs fp64 of the same order as the fp32 path; csrc/gemm3.hip) for
+ * the GEMMs whose reduction (NN) or output rows (TN) span >= 256 — narrower
+ * ones run faster on the fp32 path and take it; NTS_GEMM_SPLIT3_ALL = the
+ * split kernels for every shape they take (kernel tests).  Shapes the split
+ * kernels do not take run on the fp32 path. */
 #define NTS_GEMM_F32 0
 #define NTS_GEMM_SPLIT3 1
+#define NTS_GEMM_SPLIT3_ALL 2
 int nts_hip_ctx_set_gemm_mode(nts_hip_ctx *ctx, int mode);
 int nts_hip_ctx_get_gemm_mode(nts_hip_ctx *ctx);
 /* Re-seed the MT19937 state (std::mt19937(seed)).  Enqueued on the stream. */

@@ -111,7 +111,8 @@ void* nts_hip_ctx_get_stream(nts_hip_ctx* ctx) { return ctx ? (void*)ctx->stream
 
 int nts_hip_ctx_set_gemm_mode(nts_hip_ctx* ctx, int mode) {
   NTS_CHECK_ARG(ctx, "ctx is NULL");
-  NTS_CHECK_ARG(mode == NTS_GEMM_F32 || mode == NTS_GEMM_SPLIT3, "unknown GEMM mode");
+  NTS_CHECK_ARG(mode == NTS_GEMM_F32 || mode == NTS_GEMM_SPLIT3 || mode == NTS_GEMM_SPLIT3_ALL,
+                "unknown GEMM mode");
   ctx->gemm_mode = mode;
   return NTS_OK;
 }

@@ -1024,7 +1024,11 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
     for (int i = 0; i < M; ++i) NTS_HIP_TRY(hipMemsetAsync(C + (uint64_t)i * ldc, 0, N * 4, st));
     return NTS_OK;
   }
-  if (ctx->gemm_mode == NTS_GEMM_SPLIT3) {
+  // The split kernels pay off on wide reductions / wide outputs (the C2
+  // bottom layer, K = M = 602); narrow ones (products-shaped F = 100) run
+  // faster on the fp32-input MFMA kernels (C3: 0.716 vs 0.740 ms/step).
+  if (ctx->gemm_mode == NTS_GEMM_SPLIT3_ALL ||
+      (ctx->gemm_mode == NTS_GEMM_SPLIT3 && (trans_a ? M : K) >= 256)) {
     if (!trans_a && !BMASK && gemm3_nn_ok(M, N, K, A, lda))
       return gemm3_nn(ctx, EPI, M, N, K, A, lda, ex.amap, B, ldb, C, ldc, ex.keep_threshold,
                       ex.scale, ex.seed, ex.offset);

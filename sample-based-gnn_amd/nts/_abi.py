@@ -23,6 +23,7 @@ NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
 NTS_GEMM_F32 = 0
 NTS_GEMM_SPLIT3 = 1
+NTS_GEMM_SPLIT3_ALL = 2  # the split kernels for every shape they take (kernel tests)
 NTS_WEIGHT_SUM = 0
 NTS_WEIGHT_MEAN = 1
 NTS_WEIGHT_NONE = 2

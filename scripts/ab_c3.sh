@@ -12,5 +12,5 @@ print('$tag', round(d['ms_per_step'],4), 'ms/step', 'issue', round(c['host_train
 }
 run split3
 run f32 --gemm f32
-NTS_DIAG_REUSE_SAMPLE=1 run reuse_split3
+NTS_DIAG_REUSE_SAMPLE=1 run reuse_split3 --epochs 0
 run nopipe --no-pipeline

@@ -23,7 +23,7 @@ def ctxs():
     from nts.hip import HipContext
     f32 = HipContext(0, seed=2000)
     s3 = HipContext(0, seed=2000)
-    s3.set_gemm_mode(_abi.NTS_GEMM_SPLIT3)
+    s3.set_gemm_mode(_abi.NTS_GEMM_SPLIT3_ALL)  # every shape on the split kernels
     return f32, s3
 
 
