@@ -86,6 +86,12 @@ def parse():
                    help="feature table in pinned host memory with this fraction of the "
                         "highest-degree rows cached in HBM (GS_SAMPLE_PD_CACHE placement); "
                         "default: whole table in HBM")
+    p.add_argument("--pd-cache", action="store_true",
+                   help="NeutronOrch PD cache (GS_SAMPLE_PD_CACHE): per super-batch the hot "
+                        "vertices' bottom layer is aggregated once and shared")
+    p.add_argument("--pd-rate", type=float, default=0.2, help="PD cache: CACHE_RATE of hot vertices")
+    p.add_argument("--pd-super-batch", type=int, default=4,
+                   help="PD cache: batches per super-batch (PIPELINE_NUM)")
     p.add_argument("--no-fuse-act", action="store_true",
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
     p.add_argument("--sampler-cus", type=int, default=0,
@@ -183,7 +189,8 @@ def main():
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
                           deterministic_backward=not args.atomic_backward,
-                          gat=args.model == "gat", gemm=args.gemm)
+                          gat=args.model == "gat", gemm=args.gemm, pd_cache=args.pd_cache,
+                          pd_rate=args.pd_rate, pd_super_batch=args.pd_super_batch)
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
     tf = bool(drv.transform_first)
 
@@ -336,6 +343,9 @@ def workload_name(args, layers, V, En, tf) -> str:
     if args.cache_rate >= 0:
         s += (f"; features in pinned host memory, {args.cache_rate:.0%} of rows (highest degree) "
               f"cached in HBM")
+    if args.pd_cache:
+        s += (f"; NeutronOrch PD cache (GS_SAMPLE_PD_CACHE): {args.pd_rate:.0%} hot vertices per "
+              f"super-batch of {args.pd_super_batch} batches, their bottom layer shared")
     return s
 
 
@@ -371,7 +381,8 @@ def roofline(prof: dict, args, layers, world) -> dict:
 
 def pmc_workload(args, layers, world) -> str:
     return (f"{args.shape}/{args.batch}/{args.fanout}/{'-'.join(map(str, layers))}/{args.weight}/"
-            f"w{world}/tf{args.transform_first}/{args.model}/c{args.cache_rate}/{args.gemm}")
+            f"w{world}/tf{args.transform_first}/{args.model}/c{args.cache_rate}/{args.gemm}"
+            + (f"/pd{args.pd_rate}x{args.pd_super_batch}" if args.pd_cache else ""))
 
 
 def attach_pmc(rl, dom, args, layers, world):
