@@ -191,7 +191,11 @@ def main():
                           deterministic_backward=not args.atomic_backward,
                           gat=args.model == "gat", gemm=args.gemm, pd_cache=args.pd_cache,
                           pd_rate=args.pd_rate, pd_super_batch=args.pd_super_batch)
+    log(f"[bench] building the driver (feature placement, PD-cache preSample: may take a while "
+        f"on large graphs)")
+    t0 = time.time()
     drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg, comm)
+    log(f"[bench] driver ready in {time.time() - t0:.1f}s")
     tf = bool(drv.transform_first)
 
     def step():

@@ -40,29 +40,83 @@ __global__ void k_presample_push(const uint64_t* __restrict__ off, const uint32_
   }
 }
 
-// keys = ~count (ascending keys = descending counts), and the non-zero count
-__global__ void k_presample_keys(const uint32_t* __restrict__ cnt, uint64_t V,
-                                 uint32_t* __restrict__ keys, uint32_t* nnz) {
+// The selection needs only the count at descending rank n (the pivot): a
+// three-level radix select (11 + 11 + 10 bits) over the non-zero counts
+// instead of a sort of all V keys (papers100M-shaped: 111 M vertices per
+// super-batch).  nnz = number of non-zero counts.
+__global__ void k_presample_nnz(const uint32_t* __restrict__ cnt, uint64_t V, uint32_t* nnz) {
   uint32_t local = 0;
   for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
-       v += (uint64_t)gridDim.x * blockDim.x) {
-    keys[v] = ~cnt[v];
+       v += (uint64_t)gridDim.x * blockDim.x)
     local += cnt[v] != 0;
-  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) local += __shfl_down(local, o, kWave);
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(nnz, local);
 }
 
-// n = (uint32)((float)total * rate), pivot = the n-th largest count
-__global__ void k_presample_pivot(const uint32_t* __restrict__ sorted_keys, uint64_t V,
-                                  const uint32_t* nnz, float rate, uint32_t* n_out,
-                                  uint32_t* pivot) {
+// n = (uint32)((float)total * rate) with total = nnz + 1 (V when none is zero);
+// the select state: st[0] = rank still wanted, st[1] = pivot bits so far,
+// st[2] = 1 when the pivot lies among the non-zero counts
+__global__ void k_presample_n(const uint32_t* nnz, uint64_t V, float rate, uint32_t* n_out,
+                              uint32_t* st) {
   const uint64_t total = *nnz < V ? (uint64_t)*nnz + 1 : V;
   uint64_t n = (uint64_t)((float)total * rate);
   if (n > V) n = V;
   *n_out = (uint32_t)n;
-  *pivot = n < V ? ~sorted_keys[n] : 0u;
+  st[0] = (uint32_t)n;
+  st[1] = 0;
+  st[2] = n < *nnz ? 1u : 0u;
+}
+
+constexpr int kSelBins = 2048;
+// histogram of bits [shift, shift + width) of the non-zero counts whose bits
+// above shift + width equal the pivot prefix so far
+__global__ __launch_bounds__(256) void k_presample_hist(const uint32_t* __restrict__ cnt, uint64_t V,
+                                                        const uint32_t* st, int shift, int width,
+                                                        uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kSelBins];
+  if (!st[2]) return;  // pivot is 0: nothing to select
+  for (int i = threadIdx.x; i < kSelBins; i += 256) h[i] = 0;
+  __syncthreads();
+  const uint32_t prefix = st[1];
+  const int hi = shift + width;
+  const uint32_t mask = (1u << width) - 1u;
+  for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v < V;
+       v += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t c = cnt[v];
+    if (c != 0 && (hi >= 32 || (c >> hi) == prefix)) atomicAdd(&h[(c >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kSelBins; i += 256)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// one block: the bin holding the wanted rank (from the top), appended to the
+// prefix; the histogram is cleared for the next level
+__global__ __launch_bounds__(256) void k_presample_pick(uint32_t* __restrict__ hist, int width,
+                                                        uint32_t* st) {
+  __shared__ uint32_t h[kSelBins];
+  const int bins = 1 << width;
+  for (int i = threadIdx.x; i < kSelBins; i += 256) {
+    h[i] = i < bins ? hist[i] : 0u;
+    hist[i] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && st[2]) {
+    uint32_t want = st[0], acc = 0;
+    int b = bins - 1;
+    for (; b > 0; --b) {
+      if (acc + h[b] > want) break;
+      acc += h[b];
+    }
+    st[0] = want - acc;
+    st[1] = (st[1] << width) | (uint32_t)b;
+  }
+}
+
+// the pivot: the selected count, or 0 when the rank falls among the zeros
+__global__ void k_presample_pivot(const uint32_t* st, uint32_t* pivot) {
+  *pivot = st[2] ? st[1] : 0u;
 }
 
 __global__ void k_presample_flag(const uint32_t* __restrict__ cnt, uint64_t V,
@@ -183,24 +237,28 @@ int nts_hip_presample_select(nts_hip_ctx* ctx, const uint32_t* counts, uint64_t 
   hipStream_t st = ctx->stream;
   auto al = [](uint64_t x) { return (x + 63) / 64 * 64; };
   const uint64_t w = al(V + 1);
-  const size_t sort_tmp = radix_tmp_bytes(V);
   const size_t scan_tmp = scan_tmp_elems<uint32_t>(V) + 64;
-  NTS_RET(ensure_scratch(ctx, (5 * w + scan_tmp + 64) * sizeof(uint32_t) + sort_tmp + 256));
-  uint32_t* keys = (uint32_t*)ctx->scratch;
-  uint32_t* skeys = keys + w;
-  uint32_t* svals = skeys + w;
-  uint32_t* flag = svals + w;
+  NTS_RET(ensure_scratch(ctx, (2 * w + kSelBins + scan_tmp + 64) * sizeof(uint32_t) + 256));
+  uint32_t* flag = (uint32_t*)ctx->scratch;
   uint32_t* pos = flag + w;
-  uint32_t* misc = pos + w;  // [0] nnz, [1] pivot
+  uint32_t* hist = pos + w;  // [kSelBins]
+  uint32_t* misc = hist + kSelBins;  // [0] nnz, [1] pivot, [4..6] select state
   uint32_t* stmp = misc + 64;
-  void* rtmp = (void*)(stmp + scan_tmp);
-  NTS_HIP_TRY(hipMemsetAsync(misc, 0, 2 * sizeof(uint32_t), st));
+  NTS_HIP_TRY(hipMemsetAsync(hist, 0, (kSelBins + 64) * sizeof(uint32_t), st));
   const uint32_t gs = std::max(1u, std::min(ceil_div(V, 256), kMaxGrid));
-  hipLaunchKernelGGL(k_presample_keys, dim3(gs), dim3(256), 0, st, counts, V, keys, misc);
+  hipLaunchKernelGGL(k_presample_nnz, dim3(gs), dim3(256), 0, st, counts, V, misc);
   NTS_LAUNCH_CHECK();
-  NTS_RET(radix_sort_pairs(keys, nullptr, skeys, svals, nullptr, V, 32, rtmp, st));
-  hipLaunchKernelGGL(k_presample_pivot, dim3(1), dim3(1), 0, st, skeys, V, misc, cache_rate,
-                     out_n, misc + 1);
+  hipLaunchKernelGGL(k_presample_n, dim3(1), dim3(1), 0, st, misc, V, cache_rate, out_n, misc + 4);
+  NTS_LAUNCH_CHECK();
+  const int levels[3][2] = {{21, 11}, {10, 11}, {0, 10}};  // (shift, width), high bits first
+  for (const auto& lv : levels) {
+    hipLaunchKernelGGL(k_presample_hist, dim3(gs), dim3(256), 0, st, counts, V, misc + 4, lv[0],
+                       lv[1], hist);
+    NTS_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_presample_pick, dim3(1), dim3(256), 0, st, hist, lv[1], misc + 4);
+    NTS_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_presample_pivot, dim3(1), dim3(1), 0, st, misc + 4, misc + 1);
   NTS_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_presample_flag, dim3(gs), dim3(256), 0, st, counts, V, misc + 1, flag);
   NTS_LAUNCH_CHECK();

@@ -159,6 +159,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("pipeline", &GCNConfig::pipeline)
       .def_readwrite("transform_first", &GCNConfig::transform_first)
       .def_readwrite("gemm_mode", &GCNConfig::gemm_mode)
+      .def_readwrite("overlap_allreduce", &GCNConfig::overlap_allreduce)
       .def_readwrite("pd_cache", &GCNConfig::pd_cache)
       .def_readwrite("pd_rate", &GCNConfig::pd_rate)
       .def_readwrite("pd_super_batch", &GCNConfig::pd_super_batch)
@@ -226,7 +227,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("transform_first", &GCN_SAMPLE_ALLGPU_impl::transform_first)
       .def("sample_not_finished", &GCN_SAMPLE_ALLGPU_impl::has_batch)
       .def("restart", &GCN_SAMPLE_ALLGPU_impl::restart)
-      .def("synchronize", [](GCN_SAMPLE_ALLGPU_impl& d) { d.cs->synchronize(); })
+      .def("synchronize", [](GCN_SAMPLE_ALLGPU_impl& d) { d.sync(); })
       .def_property_readonly("loss", [](GCN_SAMPLE_ALLGPU_impl& d) { return d.loss; })
       .def_property_readonly("n_train", [](GCN_SAMPLE_ALLGPU_impl& d) { return d.sampler->work_range[1]; })
       .def_property_readonly("last_layers",

@@ -1131,6 +1131,14 @@ static void adam_step(Parameter& p, NtsStream& cs, int bias_correction) {
             "nts_hip_adam");
 }
 
+void Parameter::adam_from(NtsStream& cs, const float* grad, bool bias_correction) {
+  torch::NoGradGuard ng;
+  hip_check(nts_hip_adam(cs.ctx(), W.data_ptr<float>(), grad, M.data_ptr<float>(),
+                         V.data_ptr<float>(), (uint64_t)W.numel(), alpha, beta1, beta2, epsilon,
+                         weight_decay, beta1_t, beta2_t, bias_correction ? 1 : 0),
+            "nts_hip_adam");
+}
+
 void Parameter::learnC2C_with_decay_Adam(NtsStream& cs) { adam_step(*this, cs, 1); }
 void Parameter::learn_local_with_decay_Adam(NtsStream& cs) { adam_step(*this, cs, 0); }
 

@@ -130,6 +130,14 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   }
   correct_ = torch::zeros({1}, u32_opts(graph->device));
   init_nn();
+  defer_ = comm && (cfg.overlap_allreduce == 1 || (cfg.overlap_allreduce < 0 && comm->nranks > 1));
+  if (defer_) {
+    TORCH_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking) == hipSuccess,
+                "hipStreamCreate");
+    TORCH_CHECK(hipEventCreateWithFlags(&grads_packed_, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&grads_reduced_, hipEventDisableTiming) == hipSuccess,
+                "hipEventCreate");
+  }
   if (cfg.pd_cache) {  // preSample on the device (the Python runner may replace it)
     auto hot = presample();
     set_presample(hot.first, hot.second);
@@ -149,6 +157,12 @@ GCN_SAMPLE_ALLGPU_impl::~GCN_SAMPLE_ALLGPU_impl() {
   }
   for (auto* e : ready_)
     if (e) (void)hipEventDestroy(e);
+  if (defer_) {
+    (void)hipDeviceSynchronize();
+    (void)hipEventDestroy(grads_packed_);
+    (void)hipEventDestroy(grads_reduced_);
+    (void)hipStreamDestroy(comm_stream_);
+  }
   for (auto* p : P) delete p;
 }
 
@@ -235,13 +249,15 @@ void GCN_SAMPLE_ALLGPU_impl::init_nn() {
 }
 
 void GCN_SAMPLE_ALLGPU_impl::set_weights(const std::vector<NtsVar>& ws) {
+  flush_update();
   auto guard = cs->guard();
   TORCH_CHECK(ws.size() == P.size(), "one tensor per layer");
   torch::NoGradGuard ng;
   for (size_t i = 0; i < P.size(); ++i) P[i]->W.copy_(ws[i]);
 }
 
-std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::weights() const {
+std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::weights() {
+  flush_update();
   std::vector<NtsVar> out;
   for (auto* p : P) out.push_back(p->W.detach().clone());
   return out;
@@ -276,6 +292,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
   NtsVar X;
   if (pre_y) {  // bottom graph op already ran on the sampling stream (issue())
     NtsVar Y = pre_y->narrow(0, 0, (int64_t)sg->sampled_sgs[L - 1]->v_size);
+    flush_update();
     X = ctx.runVertexForward([&](NtsVar& a) { return vertexForward(0, a); }, Y);
     if (keep) {
       acts.push_back(Y.detach());
@@ -290,6 +307,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
     NtsVar Y;
     const bool bottom = (l == 0);
     if (bottom && tf_) {  // transform-first: H = X[src] W, X1 = act(A H) (one NN op)
+      flush_update();
       sampCSC* s = sg->sampled_sgs[hop];
       const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
       NtsVar h;
@@ -319,6 +337,9 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
     if (bottom && cfg.profile)
       prof.end(KernelProfiler::BOTTOM_AGG, (hipStream_t)cs->stream(),
                bottom_bytes(sg, cfg.fused_gather));
+    // the previous step's all-reduce ran beside this bottom aggregation,
+    // which does not read W; its optimizer step goes in here
+    if (bottom) flush_update();
     if (bottom && pd_active_) {
       // GCN_SAMPLE_PD_CACHE::Forward (toolkits/GCN_SAMPLE_PD_CACHE.hpp:916-945):
       // Y W, the cached dsts' rows replaced by the super-batch's (A X) W
@@ -364,6 +385,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
 }
 
 std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_gat(SampledSubgraph* sg) {
+  flush_update();
   const int L = (int)sg->layers;
   NtsVar X;
   if (fcache)
@@ -389,6 +411,25 @@ void GCN_SAMPLE_ALLGPU_impl::Loss(NtsVar& left, NtsVar& right) {
 void GCN_SAMPLE_ALLGPU_impl::Update() {
   // GCN_SAMPLE_ALL_MULTI::Update (toolkits/GCN_SAMPLE_ALL_MULTI.hpp:367-377):
   // SUM all-reduce of every W.grad — one fused RCCL call over a flat bucket.
+  if (defer_) {
+    // pack on the training stream, reduce on the comm stream; the Adam step
+    // runs in flush_update() once the next batch first needs W
+    TORCH_CHECK(!pending_update_, "deferred update still pending");
+    torch::NoGradGuard ng;
+    int64_t off = 0;
+    for (auto* p : P) {
+      const int64_t n = p->W.numel();
+      grad_bucket.narrow(0, off, n).copy_(p->W.grad().reshape({-1}));
+      off += n;
+    }
+    TORCH_CHECK(hipEventRecord(grads_packed_, (hipStream_t)cs->stream()) == hipSuccess &&
+                    hipStreamWaitEvent(comm_stream_, grads_packed_, 0) == hipSuccess,
+                "hipEventRecord/hipStreamWaitEvent");
+    comm->allreduce_sum(grad_bucket.data_ptr<float>(), (uint64_t)grad_bucket.numel(), comm_stream_);
+    TORCH_CHECK(hipEventRecord(grads_reduced_, comm_stream_) == hipSuccess, "hipEventRecord");
+    pending_update_ = true;
+    return;
+  }
   if (comm) {  // also at one rank: the same bucket, all-reduce and unpack run
     torch::NoGradGuard ng;
     int64_t off = 0;
@@ -409,6 +450,20 @@ void GCN_SAMPLE_ALLGPU_impl::Update() {
     if (cfg.bias_correction) p->learnC2C_with_decay_Adam(*cs);
     else p->learn_local_with_decay_Adam(*cs);
     p->next();
+  }
+}
+
+void GCN_SAMPLE_ALLGPU_impl::flush_update() {
+  if (!pending_update_) return;
+  pending_update_ = false;
+  auto guard = cs->guard();
+  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), grads_reduced_, 0) == hipSuccess,
+              "hipStreamWaitEvent");
+  int64_t off = 0;
+  for (auto* p : P) {
+    p->adam_from(*cs, grad_bucket.data_ptr<float>() + off, cfg.bias_correction != 0);
+    p->next();
+    off += p->W.numel();
   }
 }
 
@@ -525,6 +580,7 @@ float GCN_SAMPLE_ALLGPU_impl::run_epoch() {
 
 std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward_eval(const std::vector<VertexId>& seeds,
                                                          uint64_t batch_seq) {
+  flush_update();
   auto guard = cs->guard();
   const int L = (int)cfg.fanout.size();
   std::vector<bool> csr(L, cfg.gat);
@@ -565,6 +621,7 @@ void GCN_SAMPLE_ALLGPU_impl::reset_correct() {
 }
 
 double GCN_SAMPLE_ALLGPU_impl::evaluate(const std::vector<VertexId>& nids) {
+  flush_update();
   if (nids.empty()) return 0.0;
   auto guard = cs->guard();
   const int L = (int)cfg.fanout.size();
@@ -732,6 +789,7 @@ void GCN_SAMPLE_ALLGPU_impl::pd_issue(int slot, NtsStream& st) {
 // embedding = (A X) W with the current weights (the reference's CPU GEMM with
 // the W of shared_W_queue, :821-840); later batches of the super-batch reuse it.
 void GCN_SAMPLE_ALLGPU_impl::pd_train(int slot) {
+  flush_update();
   pd_key_ = (uint32_t)pd_slot_key_[slot];
   pd_active_ = true;
   if (!pd_slot_first_[slot]) return;

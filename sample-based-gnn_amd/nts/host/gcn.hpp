@@ -34,6 +34,11 @@ struct GCNConfig {
   // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode): NTS_GEMM_F32 (fp32-input
   // MFMA) or NTS_GEMM_SPLIT3 (fp32-accurate three-piece bf16 split)
   int gemm_mode = NTS_GEMM_SPLIT3;
+  // data parallel: the gradient all-reduce of step k runs on a stream of its
+  // own and the optimizer step waits for it only where step k+1 first reads
+  // W (after its bottom aggregation, which does not depend on W): -1 = on with
+  // more than one rank, 1 = always (also at one rank, for tests), 0 = off
+  int overlap_allreduce = -1;
   bool shuffle = true;
   bool profile = false;               // HIP events around the bottom aggregation
   // CACHE_RATE in [0, 1): the feature table moves to pinned host memory and
@@ -97,7 +102,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   std::pair<std::vector<uint32_t>, std::vector<uint32_t>> presample();
   void set_presample(const std::vector<uint32_t>& counts, const std::vector<uint32_t>& ids);
   uint64_t pd_hits = 0;  // bottom-layer dsts served from the PD cache (host count, sampled batches)
-  std::vector<NtsVar> weights() const;
+  std::vector<NtsVar> weights();
   void reset_stats();
   void resolve_profile() { prof.resolve(); }
 
@@ -119,6 +124,13 @@ class GCN_SAMPLE_ALLGPU_impl {
   uint64_t eval_seq = uint64_t(1) << 40;  // PHILOX stream of the evaluation batches
 
   SampledSubgraph* last_sg = nullptr;  // the batch the last train_batch() trained on
+  // finish a deferred optimizer step (overlap_allreduce); every public entry
+  // that reads or writes the weights calls it
+  void flush_update();
+  void sync() {
+    flush_update();
+    cs->synchronize();
+  }
 
  private:
   NtsVar vertexForward(int l, NtsVar& a);
@@ -132,6 +144,10 @@ class GCN_SAMPLE_ALLGPU_impl {
   KernelProfiler* profiler() { return cfg.profile ? &prof : nullptr; }
   void Loss(NtsVar& left, NtsVar& right);
   void Update();
+  bool defer_ = false;            // overlap_allreduce in effect
+  bool pending_update_ = false;   // an all-reduce is in flight, its Adam not yet run
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t grads_packed_ = nullptr, grads_reduced_ = nullptr;
   std::pair<hipEvent_t, hipEvent_t>& next_events();
   void mark(const char* what, NtsStream& st);
   void count_correct(const NtsVar& out, const NtsVar& tgt);  // non-fused output layers

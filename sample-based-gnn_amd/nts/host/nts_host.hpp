@@ -444,6 +444,8 @@ struct Parameter {
   void learnC2C_with_decay_Adam(NtsStream& cs);
   // Parameter::learn_local_with_decay_Adam (GPU drivers, no bias correction)
   void learn_local_with_decay_Adam(NtsStream& cs);
+  // either variant with the gradient taken from `grad` (a reduced bucket slice)
+  void adam_from(NtsStream& cs, const float* grad, bool bias_correction);
   void next();
   void zero_grad();
 };

@@ -129,16 +129,20 @@ def test_transform_first_trains_like_aggregate_first(E, graph, drop):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-4)
 
 
-def test_one_rank_communicator_is_identical(E, graph):
+@pytest.mark.parametrize("overlap,tf", [(0, 0), (1, 0), (1, 1)])
+def test_one_rank_communicator_is_identical(E, graph, overlap, tf):
     """The C++ data-parallel path on one GPU: initial ncclBroadcast of the
     weights, the fused gradient bucket (pack -> ncclAllReduce SUM -> unpack)
-    every step (GCN_SAMPLE_ALL_MULTI::Update, toolkits/GCN_SAMPLE_ALL_MULTI.hpp:367-377).
-    At one rank the sum is the identity: bit-identical weights to comm=None."""
+    every step (GCN_SAMPLE_ALL_MULTI::Update, toolkits/GCN_SAMPLE_ALL_MULTI.hpp:367-377);
+    overlap = 1: the all-reduce on its own stream with the optimizer step
+    deferred past the next batch's bottom aggregation.  At one rank the sum
+    is the identity: bit-identical weights to comm=None."""
     comm = E.Communicator(1, 0, E.Communicator.unique_id(), 0)
     assert comm.nranks == 1
-    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5, comm=comm)
-    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5)
-    for _ in range(3):
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5, comm=comm,
+                    overlap_allreduce=overlap, transform_first=tf)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5, transform_first=tf)
+    for _ in range(5):
         a.train_batch()
         b.train_batch()
     a.synchronize()
