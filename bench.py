@@ -71,6 +71,9 @@ def parse():
                    help="layer GEMM arithmetic: f32 = fp32-input MFMA; split3 = fp32 operands "
                         "split exactly into three bf16 pieces, six piece products on the bf16 "
                         "MFMA (fp32-accurate, csrc/gemm3.hip)")
+    p.add_argument("--pair-table", type=int, default=1, choices=[0, 1, 2],
+                   help="transform-first GEMMs on the feature table's f16 pair table "
+                        "(csrc/gemmh2.hip): 0 off, 1 forward GEMM, 2 forward + weight gradient")
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
@@ -189,7 +192,7 @@ def main():
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
                           deterministic_backward=not args.atomic_backward,
-                          gat=args.model == "gat", gemm=args.gemm, pd_cache=args.pd_cache,
+                          gat=args.model == "gat", gemm=args.gemm, pair_table=args.pair_table, pd_cache=args.pd_cache,
                           pd_rate=args.pd_rate, pd_super_batch=args.pd_super_batch)
     log(f"[bench] building the driver (feature placement, PD-cache preSample: may take a while "
         f"on large graphs)")

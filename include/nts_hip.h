@@ -34,10 +34,11 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 4  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 5  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
                                      accuracy counts in the fused loss;
-                                  4: PD cache entry points + omit fields, GEMM mode */
+                                  4: PD cache entry points + omit fields, GEMM mode;
+                                  5: two-piece f16 pair-table GEMMs (nts_hip_h2_*) */
 
 /* status codes */
 #define NTS_OK 0
@@ -418,6 +419,37 @@ int nts_hip_gemm_gather_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *
 int nts_hip_gemm_tn_gather_f32(nts_hip_ctx *ctx, int M, int N, int K, const float *A,
                                uint64_t lda, const uint32_t *a_rows, const float *B, uint64_t ldb,
                                float *C, uint64_t ldc);
+
+/* Two-piece f16 forms of the two GEMMs above (csrc/gemmh2.hip), for a STATIC
+ * A table pre-split once ("pair table"): row r is scaled by a power of two
+ * rs[r] so that its largest |x| / rs[r] lies in [2^14, 2^15), and each
+ * x / rs[r] is stored as one 32-bit word = f16 y0 (low half) + f16 y1 (high
+ * half), y0 = f16(y), y1 = f16(y - y0): 22 significant bits.  Products run as
+ * y0 b0 + y0 b1 + y1 b0 on the f16 MFMA with fp32 accumulation (three MFMAs
+ * per k-slice where NTS_GEMM_SPLIT3 needs six), the scales applied exactly
+ * to the fp32 result: error vs fp64 within a small factor of the fp32 GEMM's
+ * (tests/test_gemm_h2.py).  Same operations as nts_hip_gemm_gather_f32 /
+ * nts_hip_gemm_tn_gather_f32 on the transform-first bottom layer
+ * (toolkits/GCN_SAMPLE_ALLGPU.hpp:247-266 x.matmul(W) and its weight gradient).
+ *   nts_hip_h2_split_rows:  X [R x K] (ld ldx) -> P [R x Kp] words (ld ldp,
+ *                           Kp % 32 == 0, zero past K) + rs [R]
+ *   nts_hip_gemm_h2_gather: C[i,:] = act(X[a_rows[i],:] W) with X given as
+ *                           (P, rs); W [K x N] fp32 (N % 16 == 0, N <= 1024);
+ *                           relu_dropout != 0: the fused relu + inverted
+ *                           dropout of nts_hip_gemm_relu_dropout_f32 (same
+ *                           mask bits); a_rows NULL = rows 0..M-1
+ *   nts_hip_gemm_h2_tn_gather: C[M,N] = X[a_rows[0..K),:M]^T op(B[K,N]),
+ *                           op(B) = B, or B * bscale where Xm > 0 when Xm != NULL
+ * May grow the context's scratch arena. */
+int nts_hip_h2_split_rows(nts_hip_ctx *ctx, uint64_t R, uint32_t K, const float *X, uint64_t ldx,
+                          uint32_t Kp, uint32_t *P, uint64_t ldp, float *rs);
+int nts_hip_gemm_h2_gather(nts_hip_ctx *ctx, int relu_dropout, int M, int N, int Kp,
+                           const uint32_t *P, uint64_t ldp, const float *rs, const uint32_t *a_rows,
+                           const float *W, uint64_t ldw, int K, float *C, uint64_t ldc, float p,
+                           uint64_t seed, uint64_t offset);
+int nts_hip_gemm_h2_tn_gather(nts_hip_ctx *ctx, int M, int N, int K, const uint32_t *P, uint64_t ldp,
+                              const float *rs, const uint32_t *a_rows, const float *B, uint64_t ldb,
+                              const float *Xm, uint64_t ldx, float bscale, float *C, uint64_t ldc);
 
 /* Hidden-layer forward with its activation fused into the GEMM epilogue:
  *   C = dropout(relu(A B), p)   — vertexForward's

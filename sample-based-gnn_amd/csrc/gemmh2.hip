@@ -1,0 +1,1077 @@
+// fp32 layer GEMMs on the f16 matrix cores with two-piece operands
+// (NTS_GEMM_H2): the transform-first bottom layer's row-gathered GEMMs.
+//
+// Every fp32 operand row (or column) is brought to a power-of-two scale s so
+// that its largest |x| / s lies in [2^14, 2^15), and y = x / s (exact) is
+// split into two fp16 pieces
+//     y0 = f16(y),  y1 = f16(y - y0)            (round to nearest even)
+// y - y0 is exact in fp32 and |y - y0| <= 2^-11 |y|, so y0 + y1 carries 22
+// significant bits: |y - y0 - y1| <= 2^-23 |y| while y1 is a normal fp16
+// (|y| >= 2^-2), and <= 2^-25 absolute below that, i.e. <= 2^-39 of the
+// row's largest element.  A product a·b becomes the three f16 products
+//     a0 b0 + a0 b1 + a1 b0           (dropped: a1 b1 <= 2^-22 |a b|)
+// each exact in the fp32 accumulator of v_mfma_f32_16x16x32_f16, and the
+// scales are applied to the fp32 result (exact: powers of two).  Three f16
+// MFMAs per k-slice against six bf16 ones in gemm3.hip (NTS_GEMM_SPLIT3):
+// the same fp32-level error bound up to a small constant (measured against
+// fp64 in tests/test_gemm_h2.py), half the matrix-core work.
+//
+// The feature table is static, so its rows are pre-split once (at driver
+// construction) into a "pair table": one 32-bit word per element, f16 y0 in
+// the low half and y1 in the high half, rows zero-padded to a multiple of 32
+// words, plus a row scale rs[r] (float, a power of two).  The word layout
+// keeps the fp32 path's byte addresses: the NN kernel's A slabs are the same
+// 16-byte global_load_lds pieces as k_gemm3_nn's, the TN kernel's A^T
+// fragments the same dword loads as k_s3_tn's — and no split work is left in
+// either loop.
+//
+// Kernels:
+//   k_h2_split_rows  fp32 rows -> pair table + row scales (one wave per row)
+//   k_colmax         per-column max |rs[row] * B[row, c]| (as float bits,
+//                    atomicMax) — the column scales of W (NN) and of dH (TN)
+//   k_h2_split_b     W [K x N] -> the NN kernel's two-piece fragment image
+//   k_h2_nn          C = diag(rs[amap]) P[amap] W (+ relu/dropout epilogue)
+//   k_h2_tn          C = P[amap]^T diag(rs[amap]) op(B) (weight gradient),
+//                    op = B or the relu/dropout backward B * bscale where X > 0
+#include "common.hpp"
+
+namespace nts_hip {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4h __attribute__((ext_vector_type(4)));
+typedef short s16x4h __attribute__((ext_vector_type(4)));
+typedef short s16x8h __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4h lds_s16x4h;
+typedef __attribute__((address_space(3))) void* lds_ptr_h;
+
+constexpr int kH2Frag = 64 * 16;  // one fragment image: 64 lanes x 8 f16
+
+// scale exponent for a block whose largest magnitude is m: y = x * 2^e puts
+// m * 2^e in [2^14, 2^15); the scale returned to the caller is 2^-e
+__device__ __forceinline__ int h2_exp(float m) {
+  if (!(m > 0.f) || !(m < INFINITY)) return 0;
+  int e;
+  (void)frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
+  return 15 - e;
+}
+
+__device__ __forceinline__ uint32_t h2_pair(float y) {
+  const _Float16 h0 = (_Float16)y;
+  const _Float16 h1 = (_Float16)(y - (float)h0);
+  return (uint32_t)__builtin_bit_cast(uint16_t, h0) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+}
+
+// 8 pair words -> the y0 and y1 fragment vectors (v_perm_b32 pairs)
+__device__ __forceinline__ void h2_unpack(const uint32_t (&w)[8], f16x8& p0, f16x8& p1) {
+  uint32_t lo[4], hi[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lo[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x05040100u);
+    hi[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x07060302u);
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 a = {lo[0], lo[1], lo[2], lo[3]}, b = {hi[0], hi[1], hi[2], hi[3]};
+  p0 = __builtin_bit_cast(f16x8, a);
+  p1 = __builtin_bit_cast(f16x8, b);
+}
+
+// acc += a * b over one 32-deep k-slice (small products first)
+__device__ __forceinline__ f32x4h mfma3(const f16x8 (&a)[2], const f16x8 (&b)[2], f32x4h acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// pair table: one wave per row
+__global__ __launch_bounds__(256) void k_h2_split_rows(uint64_t R, uint32_t K, const float* __restrict__ X,
+                                                      uint64_t ldx, uint32_t Kp, uint32_t* __restrict__ P,
+                                                      uint64_t ldp, float* __restrict__ rs) {
+  const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const float* x = X + r * ldx;
+  float m = 0.f;
+  for (uint32_t k = lane; k < K; k += 64) m = fmaxf(m, fabsf(x[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const int e = h2_exp(m);
+  uint32_t* p = P + r * ldp;
+  for (uint32_t k = lane; k < Kp; k += 64) p[k] = k < K ? h2_pair(ldexpf(x[k], e)) : 0u;
+  if (lane == 0) rs[r] = ldexpf(1.f, -e);
+}
+
+// out[c] = max(out[c], max over rows k of |B[k, c]| * (rs ? rs[amap ? amap[k] : k] : 1)) as
+// float bits (non-negative floats order like their bit patterns); out zeroed
+// by the caller; rsg != NULL: rsg[k] = that row scale.  Thread t: column quad
+// q = t % Q, row lane t / Q.
+__global__ __launch_bounds__(256) void k_colmax(const float* __restrict__ B, uint64_t ldb, uint64_t K,
+                                               int N, const float* __restrict__ rs,
+                                               const uint32_t* __restrict__ amap, uint64_t rows_per_block,
+                                               uint32_t* __restrict__ out, float* __restrict__ rsg) {
+  __shared__ float red[256 * 4];
+  const int Q = N / 4, RL = 256 / Q;
+  const int t = threadIdx.x, q = t % Q, rl = t / Q;
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+  const uint64_t k0 = (uint64_t)blockIdx.x * rows_per_block;
+  const uint64_t k1 = k0 + rows_per_block < K ? k0 + rows_per_block : K;
+  if (rl < RL) {
+    for (uint64_t k = k0 + rl; k < k1; k += RL) {
+      const float4 v = *reinterpret_cast<const float4*>(B + k * ldb + 4 * q);
+      const float s = rs ? fabsf(rs[amap ? amap[k] : k]) : 1.f;
+      if (rsg && q == 0) rsg[k] = s;  // the row's scale, gathered once for the TN kernel
+      m[0] = fmaxf(m[0], fabsf(v.x) * s);
+      m[1] = fmaxf(m[1], fabsf(v.y) * s);
+      m[2] = fmaxf(m[2], fabsf(v.z) * s);
+      m[3] = fmaxf(m[3], fabsf(v.w) * s);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[4 * t + j] = m[j];
+  __syncthreads();
+  if (rl == 0) {
+    for (int l = 1; l < RL; ++l)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = fmaxf(m[j], red[4 * (l * Q + q) + j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) atomicMax(out + 4 * q + j, __float_as_uint(m[j]));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// B (W, [K x N]) -> img[s][cb][ct][piece][lane] (16 B) =
+//   piece of W[32 s + 8 (lane >> 4) + j][128 cb + 16 ct + (lane & 15)] * 2^e(col)
+// zero past K and N; cmax[col] = the column max bits (k_colmax).
+constexpr int kH2Img = 8 * 2 * kH2Frag;  // one (step, column block) image: 16 KB
+
+__global__ __launch_bounds__(256) void k_h2_split_b(const float* __restrict__ B, uint64_t ldb, int K,
+                                                   int N, int total, int ncb,
+                                                   const uint32_t* __restrict__ cmax,
+                                                   char* __restrict__ out) {
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= total) return;
+  const int lane = id & 63, ct = (id >> 6) & 7, rest = id >> 9;
+  const int cb = rest % ncb, s = rest / ncb;
+  const int col = cb * 128 + ct * 16 + (lane & 15);
+  const int k0 = 32 * s + 8 * (lane >> 4);
+  const int e = col < N ? h2_exp(__uint_as_float(cmax[col])) : 0;
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    w[j] = (col < N && k0 + j < K) ? h2_pair(ldexpf(B[(uint64_t)(k0 + j) * ldb + col], e)) : 0u;
+  f16x8 p0, p1;
+  h2_unpack(w, p0, p1);
+  char* dst = out + (size_t)rest * kH2Img + ct * 2 * kH2Frag + 16 * lane;
+  *reinterpret_cast<f16x8*>(dst) = p0;
+  *reinterpret_cast<f16x8*>(dst + kH2Frag) = p1;
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_addr_h(const void* p) {
+  return (uint32_t)(uintptr_t)(lds_ptr_h)p;
+}
+// 16 bytes per lane from `src` to LDS (wave-uniform base `lds`) + 16 * lane
+// (inline asm: see gemm3.hip — a compiler-visible LDS DMA drains the pipeline)
+__device__ __forceinline__ void glds16h(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+__device__ __forceinline__ void raw_barrier_h() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct H2Extra {
+  uint32_t keep_threshold = 0;  // EPI: relu + inverted dropout (common.hpp dropout_*)
+  float scale = 1.f;
+  uint64_t seed = 0, offset = 0;
+  const uint32_t* amap = nullptr;  // gathered A rows (NN: M rows, TN: K rows)
+  const float* rs = nullptr;       // row scales of the pair table
+  const uint32_t* cmax = nullptr;  // column max bits (W for NN, rs * op(B) for TN)
+  const float* rsg = nullptr;      // TN v2: the B rows' scales rs[amap[k]], gathered
+  const float* bx = nullptr;       // TN BMASK: op(B) = B * bscale where X > 0
+  uint64_t ldbx = 0;
+  float bscale = 1.f;
+};
+
+// NN.  The structure of k_gemm3_nn (gemm3.hip): 8 waves, one column block of
+// 128 per grid.y, 16-row tiles two at a time per wave, B's image (2 pieces,
+// 16 KB per step, 2 stages) and A's pair slabs (3 stages) by global_load_lds,
+// counted vmcnt waits and raw barriers.  K is the pair table's padded width
+// (a multiple of 32: no partial step).  Per step and row tile: 8 column tiles
+// x 3 MFMAs.  Epilogue: rs[row] * 2^-e(col) * acc, then relu/dropout.
+constexpr int kH2NnThreads = 512;
+constexpr int kH2NnAWave = 2 * 2048;
+constexpr int kH2NnA = 8 * kH2NnAWave;
+constexpr int kH2NnLds = 2 * kH2Img + 3 * kH2NnA;  // 32 + 96 KB
+
+template <bool EPI, bool AMAP>
+__global__ __launch_bounds__(kH2NnThreads, 1) void k_h2_nn(int M, int N, int K,
+                                                          const uint32_t* __restrict__ A, uint64_t lda,
+                                                          const char* __restrict__ bimg,
+                                                          float* __restrict__ C, uint64_t ldc, int rounds,
+                                                          H2Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char h2nn[];
+  char* const sb = h2nn;
+  char* const sa = h2nn + 2 * kH2Img;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * 128;
+  const int T = (M + 15) / 16;
+  const int64_t W = (int64_t)gridDim.x * 8;
+  const int64_t gw = (int64_t)blockIdx.x * 8 + wv;
+  const int t_lo = (int)(gw * T / W), t_hi = (int)((gw + 1) * T / W);
+  const int nsteps = K / 32;
+  const size_t bstride = (size_t)gridDim.y * kH2Img;
+  const uint32_t lsb = lds_addr_h(sb), lsa = lds_addr_h(sa);
+  const char* bsrc = bimg + (size_t)blockIdx.y * kH2Img + wv * 1024 + 16 * lane;
+  const int gr = (lane >> 1) & 15, gpo = 8 * (lane >> 5) + 4 * (lane & 1);
+  const uint32_t* arow[2];
+  auto set_rows = [&](int rd) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int t = min(t_lo + 2 * rd + rt, T - 1);
+      const int64_t row = (int64_t)t * 16 + gr;
+      const uint64_t rr = (uint64_t)(row < M ? row : M - 1);
+      arow[rt] = A + (AMAP ? (uint64_t)ex.amap[rr] : rr) * lda + gpo;
+    }
+  };
+  auto issue_b = [&](int s) {
+    const uint32_t dst = lsb + (s & 1) * kH2Img + wv * 1024;
+    const char* src = bsrc + (size_t)s * bstride;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) glds16h(src + 8192 * p, dst + 8192 * p);
+  };
+  auto issue_a = [&](int s) {
+    const uint32_t dst = lsa + (s % 3) * kH2NnA + wv * kH2NnAWave;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) glds16h(arow[rt] + 32 * s + 16 * q, dst + rt * 2048 + q * 1024);
+  };
+  f32x4h acc[2][8];
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));
+    set_rows(rd);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
+    issue_b(0);
+    if (nsteps > 0) issue_a(0);
+    if (nsteps > 1) issue_a(1);
+    for (int s = 0; s < nsteps; ++s) {
+      // B(s) and A(s) landed (A(s+1), issued after B(s), may stay in flight):
+      // per step a wave issues 2 (B) + 4 (A) pieces
+      if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      raw_barrier_h();
+      if (s + 1 < nsteps) issue_b(s + 1);
+      if (s + 2 < nsteps) issue_a(s + 2);
+      if (nt == 0) continue;
+      const char* as = sa + (s % 3) * kH2NnA + wv * kH2NnAWave + 32 * (i + 16 * g);
+      f16x8 a[2][2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const uint4 u = *reinterpret_cast<const uint4*>(as + rt * 2048);
+        const uint4 v = *reinterpret_cast<const uint4*>(as + rt * 2048 + 16);
+        const uint32_t w[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        h2_unpack(w, a[rt][0], a[rt][1]);
+      }
+      const char* img = sb + (s & 1) * kH2Img;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        f16x8 b[2];
+        b[0] = *reinterpret_cast<const f16x8*>(img + ct * 2 * kH2Frag + 16 * lane);
+        b[1] = *reinterpret_cast<const f16x8*>(img + ct * 2 * kH2Frag + kH2Frag + 16 * lane);
+        acc[0][ct] = mfma3(a[0], b, acc[0][ct]);
+        if (nt == 2) acc[1][ct] = mfma3(a[1], b, acc[1][ct]);
+      }
+    }
+    raw_barrier_h();
+    // acc[rt][ct][v] = C[16 t + 4 g + v][n0 + 16 ct + i]
+    float cs[8];
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      const int col = n0 + 16 * ct + i;
+      cs[ct] = col < N ? ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[col]))) : 0.f;
+    }
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      if (rt >= nt) continue;
+      const int64_t r4 = (int64_t)(t_lo + 2 * rd + rt) * 16 + 4 * g;
+      float rsv[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const uint64_t rr = (uint64_t)(r4 + v < M ? r4 + v : M - 1);
+        rsv[v] = ex.rs[AMAP ? (uint64_t)ex.amap[rr] : rr];
+      }
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+        if ((int)col >= N) continue;
+        float o[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v] = acc[rt][ct][v] * cs[ct] * rsv[v];
+        if constexpr (EPI) {
+          const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
+          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// TN: C[M x N] = A[K x M]^T diag(rs) op(B)[K x N], A the pair table (K rows
+// through the map, M <= its width), the structure of k_s3_tn (gemm3.hip): an
+// 8-wave block takes one k-chunk, up to 8 x TPW column tiles of A and 128
+// columns of B; A^T fragments are pair words loaded straight to registers (two
+// steps ahead) and unpacked there; B rows are loaded 8 floats per thread,
+// multiplied by their row's scale rs[amap[k]] and by 2^e(col) from the
+// column max, split into two f16 pieces and written to LDS (XOR-swizzled
+// 256-byte rows), read back transposed by ds_read_b64_tr_b16.  Partials are
+// scaled by 2^-e(col) and summed in a fixed order (sum_splits).
+constexpr int kH2TnThreads = 512;
+constexpr int kH2TnImg = 32 * 256;            // one piece of one step: 32 rows x 128 f16
+constexpr int kH2TnLds = 2 * 2 * kH2TnImg;    // 2 stages x 2 pieces = 32 KB
+
+__device__ __forceinline__ int h2_tr_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+template <int TPW, bool BMASK, bool AMAP>
+__global__ __launch_bounds__(kH2TnThreads, 1) void k_h2_tn(int M, int N, int K,
+                                                          const uint32_t* __restrict__ A, uint64_t lda,
+                                                          const float* __restrict__ B, uint64_t ldb,
+                                                          float* __restrict__ C, uint64_t ldc, int kchunk,
+                                                          uint64_t split_stride, int nmb, int nnb,
+                                                          H2Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char h2tn[];  // [2][2][kH2TnImg]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int mb = blockIdx.x % nmb;
+  const int nb = (blockIdx.x / nmb) % nnb;
+  const int split = blockIdx.x / (nmb * nnb);
+  const int n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int b_lo = mb * T / nmb, b_cnt = (mb + 1) * T / nmb - b_lo;
+  const int w_lo = b_lo + wv * b_cnt / 8, w_hi = b_lo + (wv + 1) * b_cnt / 8;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nsteps = kbeg < kend ? (kend - kbeg + 31) / 32 : 0;
+
+  int acol[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acol[t] = min(16 * min(w_lo + t, max(w_hi - 1, w_lo)) + i, M - 1);
+  // B staging role: row br = tid >> 4 of the step, columns bc .. bc + 7
+  const int br = tid >> 4, bc = 8 * (tid & 15);
+  const bool bok = n0 + bc < N;  // N % 16 == 0
+  const float* bcol = B + (bok ? n0 + bc : 0);
+  const float* xcol = BMASK ? ex.bx + (bok ? n0 + bc : 0) : nullptr;
+  // column exponent: from the max of |rs * B| (times bscale for the masked
+  // operand, an upper bound of |rs * op(B)|)
+  auto col_exp = [&](int col) {
+    float m = __uint_as_float(ex.cmax[col]);
+    if constexpr (BMASK) m *= ex.bscale;
+    return h2_exp(m);
+  };
+  int bexp[8];  // 2^e(col) of this thread's 8 B columns
+#pragma unroll
+  for (int u = 0; u < 8; ++u) bexp[u] = bok ? col_exp(n0 + bc + u) : 0;
+
+  f32x4h acc[TPW][8];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[t][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
+  uint32_t rid[2][8];
+  uint32_t xa[TPW][8];
+  f16x8 pa[TPW][2];
+  float4 braw[2], xraw[BMASK ? 2 : 1];
+  float brs = 0.f;
+
+  auto load_ids = [&](int s, uint32_t (&r)[8]) {
+    const int k0 = kbeg + 32 * s + 8 * g;
+    if constexpr (AMAP) {
+      if (k0 + 8 <= kend) {
+        const uint4 u0 = *reinterpret_cast<const uint4*>(ex.amap + k0);
+        const uint4 u1 = *reinterpret_cast<const uint4*>(ex.amap + k0 + 4);
+        r[0] = u0.x; r[1] = u0.y; r[2] = u0.z; r[3] = u0.w;
+        r[4] = u1.x; r[5] = u1.y; r[6] = u1.z; r[7] = u1.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = ex.amap[min(k0 + j, kend - 1)];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = (uint32_t)min(k0 + j, kend - 1);
+    }
+  };
+  auto load_x = [&](int s, const uint32_t (&r)[8], int t) {
+    const int k0 = kbeg + 32 * s + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xa[t][j] = A[(uint64_t)r[j] * lda + acol[t]];
+    if (k0 + 8 > kend) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + j >= kend) xa[t][j] = 0u;
+    }
+  };
+  auto load_b = [&](int s) {
+    const int k = min(kbeg + 32 * s + br, kend - 1);
+    const float4* p = reinterpret_cast<const float4*>(bcol + (uint64_t)k * ldb);
+    braw[0] = p[0];
+    braw[1] = p[1];
+    if constexpr (BMASK) {
+      const float4* px = reinterpret_cast<const float4*>(xcol + (uint64_t)k * ex.ldbx);
+      xraw[0] = px[0];
+      xraw[1] = px[1];
+    }
+    brs = ex.rs[AMAP ? (uint64_t)ex.amap[k] : (uint64_t)k];
+  };
+  auto store_b = [&](int s, int buf) {
+    const bool ok = bok && kbeg + 32 * s + br < kend;
+    float v[8] = {braw[0].x, braw[0].y, braw[0].z, braw[0].w,
+                  braw[1].x, braw[1].y, braw[1].z, braw[1].w};
+    if constexpr (BMASK) {
+      const float xs[8] = {xraw[0].x, xraw[0].y, xraw[0].z, xraw[0].w,
+                           xraw[1].x, xraw[1].y, xraw[1].z, xraw[1].w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xs[u] > 0.f ? v[u] * ex.bscale : 0.f;
+    }
+    uint32_t w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = ok ? h2_pair(ldexpf(v[u] * brs, bexp[u])) : 0u;
+    f16x8 q0, q1;
+    h2_unpack(w, q0, q1);
+    char* dst = h2tn + buf * 2 * kH2TnImg + h2_tr_off(br, bc / 8);
+    *reinterpret_cast<f16x8*>(dst) = q0;
+    *reinterpret_cast<f16x8*>(dst + kH2TnImg) = q1;
+  };
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int off_lo = h2_tr_off(8 * g + tq, tp >> 1) + 8 * (tp & 1);
+  const int off_hi = h2_tr_off(8 * g + 4 + tq, tp >> 1) + 8 * (tp & 1);
+  auto read_b = [&](int buf, int ct, f16x8 (&b)[2]) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const char* img = h2tn + (buf * 2 + pc) * kH2TnImg;
+      const s16x4h lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)(img + (off_lo ^ (32 * ct))));
+      const s16x4h hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)(img + (off_hi ^ (32 * ct))));
+      const s16x8h c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      b[pc] = __builtin_bit_cast(f16x8, c);
+    }
+  };
+
+  if (nsteps > 0) {
+    load_ids(0, rid[0]);
+    if (nsteps > 1) load_ids(1, rid[1]);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) load_x(0, rid[0], t);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) h2_unpack(xa[t], pa[t][0], pa[t][1]);
+    if (nsteps > 1)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) load_x(1, rid[1], t);
+    if (nsteps > 2) load_ids(2, rid[0]);
+    load_b(0);
+    store_b(0, 0);
+    if (nsteps > 1) load_b(1);
+  }
+  auto step = [&](int s, auto par) {
+    constexpr int P = decltype(par)::value;
+    __syncthreads();
+    if (s + 1 < nsteps) store_b(s + 1, 1 - P);
+    if (s + 2 < nsteps) load_b(s + 2);
+    if (s + 3 < nsteps) load_ids(s + 3, rid[1 - P]);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        f16x8 b[2];
+        read_b(P, ct, b);
+        acc[t][ct] = mfma3(pa[t], b, acc[t][ct]);
+      }
+      if (s + 1 < nsteps) h2_unpack(xa[t], pa[t][0], pa[t][1]);
+      if (s + 2 < nsteps) load_x(s + 2, rid[P], t);
+    }
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    step(s, std::integral_constant<int, 0>());
+    if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>());
+  }
+  float* Cb = C + (uint64_t)split * split_stride;
+  float cs[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) {
+    const int col = n0 + 16 * ct + i;
+    cs[ct] = col < N ? ldexpf(1.f, -col_exp(col)) : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (w_lo + t >= w_hi) continue;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 16 * (w_lo + t) + 4 * g + v;
+      if (row >= M) continue;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const int col = n0 + 16 * ct + i;
+        if (col < N) Cb[(uint64_t)row * ldc + col] = acc[t][ct][v] * cs[ct];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// v2 kernels (NTS_H2_NN=2 / NTS_H2_TN=2 select them; see the launchers):
+// every global load is compiler-visible and runs several k-steps ahead of
+// its use.  On the gathered C2 shapes the v1 kernels wait on row reads whose
+// latency under load exceeds their two-step prefetch (one step ~ 1 us of MFMA
+// work vs several us of random-row latency).
+//
+// NN v2: block = 8 waves, 2 row tiles per wave per round (as v1).  Lane (i, g)
+// loads its A fragment words A[row i][32 s + 8 g .. +7] (two 16-byte loads
+// per tile) into a ring of D register sets, D steps ahead; the B image of
+// step s (16 KB) is copied 32 bytes per thread through registers, loaded two
+// steps ahead and written to one of two LDS stages one step ahead.  One
+// barrier per step.
+template <bool EPI, bool AMAP>
+__device__ __forceinline__ void h2_nn_store(const f32x4h (&acc)[2][8], int nt, int64_t tile0, int n0,
+                                            int i, int g, int M, int N, float* __restrict__ C,
+                                            uint64_t ldc, const H2Extra& ex) {
+  float cs[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) {
+    const int col = n0 + 16 * ct + i;
+    cs[ct] = col < N ? ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[col]))) : 0.f;
+  }
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    if (rt >= nt) continue;
+    const int64_t r4 = (tile0 + rt) * 16 + 4 * g;
+    float rsv[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const uint64_t rr = (uint64_t)(r4 + v < M ? r4 + v : M - 1);
+      rsv[v] = ex.rs[AMAP ? (uint64_t)ex.amap[rr] : rr];
+    }
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+      if ((int)col >= N) continue;
+      float o[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) o[v] = acc[rt][ct][v] * cs[ct] * rsv[v];
+      if constexpr (EPI) {
+        const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
+        const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+    }
+  }
+}
+
+constexpr int kH2Nn2D = 3;  // A and B prefetch depth (steps); B's LDS stages
+
+template <bool EPI, bool AMAP>
+__global__ __launch_bounds__(kH2NnThreads, 1) void k_h2_nn2(int M, int N, int K,
+                                                           const uint32_t* __restrict__ A, uint64_t lda,
+                                                           const char* __restrict__ bimg,
+                                                           float* __restrict__ C, uint64_t ldc, int rounds,
+                                                           H2Extra ex) {
+  constexpr int D = kH2Nn2D;
+  __shared__ __attribute__((aligned(16))) char sb[D][kH2Img];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * 128;
+  const int T = (M + 15) / 16;
+  const int64_t W = (int64_t)gridDim.x * 8;
+  const int64_t gw = (int64_t)blockIdx.x * 8 + wv;
+  const int t_lo = (int)(gw * T / W), t_hi = (int)((gw + 1) * T / W);
+  const int nsteps = K / 32;
+  const size_t bstride = (size_t)gridDim.y * kH2Img;
+  const char* bsrc = bimg + (size_t)blockIdx.y * kH2Img + 32 * tid;
+  uint4 breg[D][2];  // B image pieces, D steps ahead like A (equal distances: a wait
+                     // for one stream never forces the other's younger loads)
+  uint4 areg[D][2][2];
+  const uint32_t* arow[2];
+  f32x4h acc[2][8];
+  auto load_b = [&](int s, uint4 (&r)[2]) {
+    const uint4* p = reinterpret_cast<const uint4*>(bsrc + (size_t)min(s, nsteps - 1) * bstride);
+    r[0] = p[0];
+    r[1] = p[1];
+  };
+  auto write_b = [&](int buf, const uint4 (&r)[2]) {
+    uint4* d = reinterpret_cast<uint4*>(&sb[buf][32 * tid]);
+    d[0] = r[0];
+    d[1] = r[1];
+  };
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int t = min(t_lo + 2 * rd + rt, T - 1);
+      const int64_t row = (int64_t)t * 16 + i;
+      const uint64_t rr = (uint64_t)(row < M ? row : M - 1);
+      arow[rt] = A + (AMAP ? (uint64_t)ex.amap[rr] : rr) * lda + 8 * g;
+    }
+    // every load is unconditional (clamped step / tile): the compiler then
+    // counts the loads in flight exactly and waits only for the ones it uses
+    auto load_a = [&](int s, uint4 (&r)[2][2]) {
+      s = min(s, nsteps - 1);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const uint4* p = reinterpret_cast<const uint4*>(arow[rt] + 32 * s);
+        r[rt][0] = p[0];
+        r[rt][1] = p[1];
+      }
+    };
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      load_b(d, breg[d]);
+      load_a(d, areg[d]);
+    }
+    write_b(0, breg[0]);
+    // step s (j = s % D: B(s) in LDS stage j); steps past nsteps (the loop
+    // runs a multiple of D) only keep the load stream uniform
+    auto step = [&](int s, auto jc) {
+      constexpr int j = decltype(jc)::value;
+      __syncthreads();
+      write_b((j + 1) % D, breg[(j + 1) % D]);
+      load_b(s + D, breg[j]);
+      f16x8 a[2][2];
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        const uint32_t w[8] = {areg[j][rt][0].x, areg[j][rt][0].y, areg[j][rt][0].z, areg[j][rt][0].w,
+                               areg[j][rt][1].x, areg[j][rt][1].y, areg[j][rt][1].z, areg[j][rt][1].w};
+        h2_unpack(w, a[rt][0], a[rt][1]);
+      }
+      load_a(s + D, areg[j]);
+      if (s >= nsteps || nt == 0) return;
+      const char* img = sb[j];
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        f16x8 b[2];
+        b[0] = *reinterpret_cast<const f16x8*>(img + ct * 2 * kH2Frag + 16 * lane);
+        b[1] = *reinterpret_cast<const f16x8*>(img + ct * 2 * kH2Frag + kH2Frag + 16 * lane);
+        acc[0][ct] = mfma3(a[0], b, acc[0][ct]);
+        if (nt == 2) acc[1][ct] = mfma3(a[1], b, acc[1][ct]);
+      }
+    };
+    static_assert(kH2Nn2D == 3, "the step loop below unrolls by 3");
+    for (int s = 0; s < nsteps; s += 3) {
+      step(s, std::integral_constant<int, 0>());
+      step(s + 1, std::integral_constant<int, 1>());
+      step(s + 2, std::integral_constant<int, 2>());
+    }
+    __syncthreads();  // every wave is done with sb before the next round's first write
+    h2_nn_store<EPI, AMAP>(acc, nt, (int64_t)(t_lo + 2 * rd), n0, i, g, M, N, C, ldc, ex);
+  }
+}
+
+// TN v2: k_h2_tn with three-deep register rings: a tile's A^T words are
+// loaded three steps before its MFMAs (and unpacked just before them), the
+// row ids of a step two steps before its loads, B rows two steps before they
+// are split into LDS; B's row scales come pre-gathered (ex.rsg, written by
+// the column-max pass).  TPW = 2 tiles per wave keeps the rings in registers.
+template <int TPW, bool BMASK, bool AMAP>
+__global__ __launch_bounds__(kH2TnThreads, 1) void k_h2_tn2(int M, int N, int K,
+                                                           const uint32_t* __restrict__ A, uint64_t lda,
+                                                           const float* __restrict__ B, uint64_t ldb,
+                                                           float* __restrict__ C, uint64_t ldc, int kchunk,
+                                                           uint64_t split_stride, int nmb, int nnb,
+                                                           H2Extra ex) {
+  // [2][2][kH2TnImg] B pieces, then the chunk's row ids and B row scales
+  extern __shared__ __attribute__((aligned(16))) char h2tn2[];
+  uint32_t* const sid = reinterpret_cast<uint32_t*>(h2tn2 + kH2TnLds);
+  float* const ssc = reinterpret_cast<float*>(sid + kchunk);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int mb = blockIdx.x % nmb;
+  const int nb = (blockIdx.x / nmb) % nnb;
+  const int split = blockIdx.x / (nmb * nnb);
+  const int n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int b_lo = mb * T / nmb, b_cnt = (mb + 1) * T / nmb - b_lo;
+  const int w_lo = b_lo + wv * b_cnt / 8, w_hi = b_lo + (wv + 1) * b_cnt / 8;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nsteps = kbeg < kend ? (kend - kbeg + 31) / 32 : 0;
+  const int ntile = w_hi - w_lo;
+
+  int acol[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acol[t] = min(16 * min(w_lo + t, max(w_hi - 1, w_lo)) + i, M - 1);
+  const int br = tid >> 4, bc = 8 * (tid & 15);
+  const bool bok = n0 + bc < N;
+  const float* bcol = B + (bok ? n0 + bc : 0);
+  const float* xcol = BMASK ? ex.bx + (bok ? n0 + bc : 0) : nullptr;
+  auto col_exp = [&](int col) {
+    float m = __uint_as_float(ex.cmax[col]);
+    if constexpr (BMASK) m *= ex.bscale;
+    return h2_exp(m);
+  };
+  int bexp[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) bexp[u] = bok ? col_exp(n0 + bc + u) : 0;
+
+  f32x4h acc[TPW][8];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[t][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
+  uint32_t xa[3][TPW][8];
+  float4 braw[3][2], xraw[3][BMASK ? 2 : 1];
+  float bsc[3];
+  // the chunk's row ids and B row scales to LDS once: the per-step reads then
+  // count in lgkmcnt, and the only vmcnt streams (A words, B rows) run the
+  // same three steps ahead
+  for (int k = tid; k < kend - kbeg; k += kH2TnThreads) {
+    sid[k] = AMAP ? ex.amap[kbeg + k] : (uint32_t)(kbeg + k);
+    ssc[k] = ex.rsg[kbeg + k];
+  }
+  __syncthreads();
+
+  // every load is unconditional with a clamped address (rows past the chunk
+  // are zeroed where the words are consumed): the compiler then counts the
+  // loads in flight exactly and waits only for the ones it uses
+  const int klast = kend - kbeg - 1;
+  auto load_x = [&](int s, uint32_t (&x)[TPW][8]) {
+    const int k0 = 32 * s + 8 * g;
+    uint32_t r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = sid[min(k0 + j, klast)];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[t][j] = A[(uint64_t)r[j] * lda + acol[t]];
+  };
+  auto load_b = [&](int s, float4 (&b)[2], float4 (&x)[BMASK ? 2 : 1], float& sc) {
+    const int kl = min(32 * s + br, klast);
+    const int k = kbeg + kl;
+    const float4* p = reinterpret_cast<const float4*>(bcol + (uint64_t)k * ldb);
+    b[0] = p[0];
+    b[1] = p[1];
+    if constexpr (BMASK) {
+      const float4* px = reinterpret_cast<const float4*>(xcol + (uint64_t)k * ex.ldbx);
+      x[0] = px[0];
+      x[1] = px[1];
+    }
+    sc = ssc[kl];
+  };
+  auto store_b = [&](int s, int buf, const float4 (&b)[2], const float4 (&x)[BMASK ? 2 : 1], float sc) {
+    const bool ok = bok && kbeg + 32 * s + br < kend;
+    float v[8] = {b[0].x, b[0].y, b[0].z, b[0].w, b[1].x, b[1].y, b[1].z, b[1].w};
+    if constexpr (BMASK) {
+      const float xs[8] = {x[0].x, x[0].y, x[0].z, x[0].w, x[1].x, x[1].y, x[1].z, x[1].w};
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xs[u] > 0.f ? v[u] * ex.bscale : 0.f;
+    }
+    uint32_t w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = ok ? h2_pair(ldexpf(v[u] * sc, bexp[u])) : 0u;
+    f16x8 q0, q1;
+    h2_unpack(w, q0, q1);
+    char* dst = h2tn2 + buf * 2 * kH2TnImg + h2_tr_off(br, bc / 8);
+    *reinterpret_cast<f16x8*>(dst) = q0;
+    *reinterpret_cast<f16x8*>(dst + kH2TnImg) = q1;
+  };
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int off_lo = h2_tr_off(8 * g + tq, tp >> 1) + 8 * (tp & 1);
+  const int off_hi = h2_tr_off(8 * g + 4 + tq, tp >> 1) + 8 * (tp & 1);
+  auto read_b = [&](int buf, int ct, f16x8 (&b)[2]) {
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const char* img = h2tn2 + (buf * 2 + pc) * kH2TnImg;
+      const s16x4h lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)(img + (off_lo ^ (32 * ct))));
+      const s16x4h hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)(img + (off_hi ^ (32 * ct))));
+      const s16x8h c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      b[pc] = __builtin_bit_cast(f16x8, c);
+    }
+  };
+
+  if (nsteps == 0) return;  // (never launched: every split has >= 1 step)
+  // prologue: B and A of steps 0..2 (B(0) to LDS)
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    load_b(d, braw[d], xraw[d], bsc[d]);
+    load_x(d, xa[d]);
+  }
+  store_b(0, 0, braw[0], xraw[0], bsc[0]);
+  // step s (j = s % 3): B(s) in LDS buffer s & 1, B(s+1) and B(s+2) raw in
+  // braw[j+1], braw[j+2]; A(s) raw in xa[j].  Issued: B(s+3) into braw[j]
+  // (B(s) went to LDS last step), then A(s+3) into xa[j] once A(s) is read.
+  auto step = [&](int s, auto jc) {
+    constexpr int j = decltype(jc)::value;
+    constexpr int j1 = (j + 1) % 3;
+    __syncthreads();
+    store_b(s + 1, (s + 1) & 1, braw[j1], xraw[j1], bsc[j1]);
+    load_b(s + 3, braw[j], xraw[j], bsc[j]);
+    // rows of step s past the chunk: zero words (the pad may hold anything)
+    const int kl = kend - (kbeg + 32 * s + 8 * g);
+    uint32_t w[TPW][8];
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w[t][q] = q < kl ? xa[j][t][q] : 0u;
+    load_x(s + 3, xa[j]);
+    if (s < nsteps) {
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        if (t >= ntile) continue;
+        f16x8 pa[2];
+        h2_unpack(w[t], pa[0], pa[1]);
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) {
+          f16x8 b[2];
+          read_b(s & 1, ct, b);
+          acc[t][ct] = mfma3(pa, b, acc[t][ct]);
+        }
+      }
+    }
+  };
+  // steps past nsteps (the loop runs a multiple of 3) only keep the load
+  // stream uniform; their B rows are masked off by store_b's bounds check
+  for (int s = 0; s < nsteps; s += 3) {
+    step(s, std::integral_constant<int, 0>());
+    step(s + 1, std::integral_constant<int, 1>());
+    step(s + 2, std::integral_constant<int, 2>());
+  }
+  float* Cb = C + (uint64_t)split * split_stride;
+  float cs[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) {
+    const int col = n0 + 16 * ct + i;
+    cs[ct] = col < N ? ldexpf(1.f, -col_exp(col)) : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (t >= ntile) continue;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 16 * (w_lo + t) + 4 * g + v;
+      if (row >= M) continue;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const int col = n0 + 16 * ct + i;
+        if (col < N) Cb[(uint64_t)row * ldc + col] = acc[t][ct][v] * cs[ct];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernel generation per GEMM (A/B): NTS_H2_NN=1|2, NTS_H2_TN=1|2
+static int h2_gen(const char* var, int dflt) {
+  const char* e = getenv(var);
+  return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : dflt;
+}
+static bool h2_nn_v1() {
+  static const bool v = h2_gen("NTS_H2_NN", 1) == 1;
+  return v;
+}
+static bool h2_tn_v1() {
+  static const bool v = h2_gen("NTS_H2_TN", 2) == 1;
+  return v;
+}
+
+static int colmax(nts_hip_ctx* ctx, const float* B, uint64_t ldb, uint64_t K, int N, const float* rs,
+                  const uint32_t* amap, uint32_t* out, float* rsg = nullptr) {
+  NTS_HIP_TRY(hipMemsetAsync(out, 0, (size_t)N * sizeof(uint32_t), ctx->stream));
+  if (K == 0) return NTS_OK;
+  const uint64_t blocks = std::min<uint64_t>(1024, (K + 63) / 64);
+  const uint64_t per = (K + blocks - 1) / blocks;
+  hipLaunchKernelGGL(k_colmax, dim3((uint32_t)((K + per - 1) / per)), dim3(256), 0, ctx->stream, B, ldb,
+                     K, N, rs, amap, per, out, rsg);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+}  // namespace nts_hip
+
+using namespace nts_hip;
+
+extern "C" int nts_hip_h2_split_rows(nts_hip_ctx* ctx, uint64_t R, uint32_t K, const float* X,
+                                     uint64_t ldx, uint32_t Kp, uint32_t* P, uint64_t ldp, float* rs) {
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(Kp >= K && Kp % 32 == 0 && ldp >= Kp && ldp % 4 == 0, "Kp / ldp");
+  NTS_CHECK_ARG(ldx >= K, "ldx < K");
+  NTS_CHECK_ARG(R == 0 || (X && P && rs), "NULL buffer");
+  NTS_CHECK_ARG((uintptr_t)P % 16 == 0, "P must be 16-byte aligned");
+  if (R == 0) return NTS_OK;
+  hipLaunchKernelGGL(k_h2_split_rows, dim3((uint32_t)((R + 3) / 4)), dim3(256), 0, ctx->stream, R, K, X,
+                     ldx, Kp, P, ldp, rs);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+// scratch: [column max bits (N words, padded)][...]
+extern "C" int nts_hip_gemm_h2_gather(nts_hip_ctx* ctx, int relu_dropout, int M, int N, int Kp,
+                                      const uint32_t* P, uint64_t ldp, const float* rs,
+                                      const uint32_t* a_rows, const float* W, uint64_t ldw, int K,
+                                      float* C, uint64_t ldc, float p, uint64_t seed, uint64_t offset) {
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(M >= 0 && N > 0 && N % 16 == 0 && K > 0 && Kp >= K && Kp % 32 == 0, "shape");
+  NTS_CHECK_ARG(ldp >= (uint64_t)Kp && ldp % 4 == 0 && (uintptr_t)P % 16 == 0, "pair table layout");
+  NTS_CHECK_ARG(ldw >= (uint64_t)N && ldc >= (uint64_t)N, "ld");
+  NTS_CHECK_ARG(M == 0 || (P && rs && W && C), "NULL buffer");
+  NTS_CHECK_ARG(p >= 0.f && p < 1.f, "p must be in [0, 1)");
+  if (M == 0) return NTS_OK;
+  const int ncb = (N + 127) / 128, nsteps = Kp / 32;
+  const size_t cm_bytes = ((size_t)N * 4 + 255) / 256 * 256;
+  const size_t img = (size_t)nsteps * ncb * kH2Img;
+  NTS_RET(ensure_scratch(ctx, cm_bytes + img + 256));
+  uint32_t* cmax = (uint32_t*)ctx->scratch;
+  char* bimg = (char*)ctx->scratch + cm_bytes;
+  NTS_RET(colmax(ctx, W, ldw, (uint64_t)K, N, nullptr, nullptr, cmax));
+  const int total = nsteps * ncb * 512;
+  hipLaunchKernelGGL(k_h2_split_b, dim3((total + 255) / 256), dim3(256), 0, ctx->stream, W, ldw, K, N,
+                     total, ncb, cmax, bimg);
+  NTS_LAUNCH_CHECK();
+  H2Extra ex;
+  ex.keep_threshold = dropout_threshold(p);
+  ex.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  ex.seed = seed;
+  ex.offset = offset;
+  ex.amap = a_rows;
+  ex.rs = rs;
+  ex.cmax = cmax;
+  const int T = (M + 15) / 16;
+  int gx = std::max(8, (256 / ncb) / 8 * 8);
+  gx = std::min(gx, std::max(8, ((T + 15) / 16 + 7) / 8 * 8));
+  const int64_t Wv = (int64_t)gx * 8;
+  const int max_tiles = (int)((T + Wv - 1) / Wv);
+  const int rounds = (max_tiles + 1) / 2;
+  const dim3 grid(gx, ncb);
+#define NTS_H2NN(E, MP)                                                                          \
+  do {                                                                                           \
+    if (h2_nn_v1()) {                                                                            \
+      NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn<E, MP>),            \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kH2NnLds));    \
+      hipLaunchKernelGGL((k_h2_nn<E, MP>), grid, dim3(kH2NnThreads), kH2NnLds, ctx->stream, M, N, \
+                         Kp, P, ldp, bimg, C, ldc, rounds, ex);                                  \
+    } else {                                                                                     \
+      hipLaunchKernelGGL((k_h2_nn2<E, MP>), grid, dim3(kH2NnThreads), 0, ctx->stream, M, N, Kp, P, \
+                         ldp, bimg, C, ldc, rounds, ex);                                         \
+    }                                                                                            \
+  } while (0)
+  if (relu_dropout) {
+    if (a_rows) NTS_H2NN(true, true); else NTS_H2NN(true, false);
+  } else {
+    if (a_rows) NTS_H2NN(false, true); else NTS_H2NN(false, false);
+  }
+#undef NTS_H2NN
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+extern "C" int nts_hip_gemm_h2_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint32_t* P,
+                                         uint64_t ldp, const float* rs, const uint32_t* a_rows,
+                                         const float* B, uint64_t ldb, const float* X, uint64_t ldx,
+                                         float bscale, float* C, uint64_t ldc) {
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(M > 0 && N > 0 && N % 16 == 0 && N <= 1024 && K >= 0, "shape");
+  NTS_CHECK_ARG(ldp >= (uint64_t)M && (uintptr_t)P % 4 == 0, "pair table layout");
+  NTS_CHECK_ARG(ldb >= (uint64_t)N && ldb % 4 == 0 && (uintptr_t)B % 16 == 0, "B layout");
+  NTS_CHECK_ARG(!X || (ldx >= (uint64_t)N && ldx % 4 == 0 && (uintptr_t)X % 16 == 0), "X layout");
+  NTS_CHECK_ARG(!a_rows || (uintptr_t)a_rows % 16 == 0, "a_rows must be 16-byte aligned");
+  NTS_CHECK_ARG(ldc >= (uint64_t)N, "ldc");
+  NTS_CHECK_ARG(K == 0 || (P && rs && B && C), "NULL buffer");
+  if (K == 0) {
+    NTS_HIP_TRY(hipMemset2DAsync(C, ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M,
+                                 ctx->stream));
+    return NTS_OK;
+  }
+  // v2 (TPW 2) keeps the chunk's row ids + scales in LDS (8 B per row): past
+  // 8192-row chunks (a reduction > ~700 K rows at this N) the v1 kernel runs
+  bool v1 = h2_tn_v1();
+  int TPW = 0, nmb = 0, splits = 0, kchunk = 0;
+  const int T = (M + 15) / 16, nnb = (N + 127) / 128, ksteps = (K + 31) / 32;
+  for (int pass = 0; pass < 2; ++pass) {
+    TPW = v1 ? 3 : 2;
+    nmb = (T + 8 * TPW - 1) / (8 * TPW);
+    splits = std::max(1, std::min(256 / (nmb * nnb), ksteps / 4));
+    kchunk = ((ksteps + splits - 1) / splits) * 32;
+    splits = (K + kchunk - 1) / kchunk;
+    if (v1 || kchunk <= 8192) break;
+    v1 = true;
+  }
+  const int tn2_lds = kH2TnLds + 8 * kchunk;
+  const uint64_t stride = (uint64_t)M * N;
+  const size_t cm_bytes = ((size_t)N * 4 + 255) / 256 * 256;
+  const size_t rsg_bytes = ((size_t)K * 4 + 255) / 256 * 256;
+  const size_t part_bytes = splits > 1 ? stride * splits * sizeof(float) : 0;
+  NTS_RET(ensure_scratch(ctx, cm_bytes + rsg_bytes + part_bytes + 256));
+  uint32_t* cmax = (uint32_t*)ctx->scratch;
+  float* rsg = (float*)((char*)ctx->scratch + cm_bytes);
+  float* out = C;
+  uint64_t ldo = ldc;
+  if (splits > 1) {
+    out = (float*)((char*)ctx->scratch + cm_bytes + rsg_bytes);
+    ldo = N;
+  }
+  // column max of rs[row] * op(B) (bounded by the unmasked B * bscale), and
+  // the B rows' scales gathered for the kernel
+  NTS_RET(colmax(ctx, B, ldb, (uint64_t)K, N, rs, a_rows, cmax, rsg));
+  H2Extra ex;
+  ex.amap = a_rows;
+  ex.rs = rs;
+  ex.rsg = rsg;
+  ex.cmax = cmax;
+  ex.bx = X;
+  ex.ldbx = ldx;
+  ex.bscale = bscale;
+  NTS_CHECK_ARG(!X || bscale > 0.f, "bscale must be > 0");
+  const dim3 grid(nmb * nnb * splits);
+#define NTS_H2TN(BM, MP)                                                                         \
+  do {                                                                                           \
+    if (v1) {                                                                                    \
+      NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn<3, BM, MP>),        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kH2TnLds));    \
+      hipLaunchKernelGGL((k_h2_tn<3, BM, MP>), grid, dim3(kH2TnThreads), kH2TnLds, ctx->stream, M, \
+                         N, K, P, ldp, B, ldb, out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, \
+                         nmb, nnb, ex);                                                          \
+    } else {                                                                                     \
+      NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn2<2, BM, MP>),       \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, tn2_lds));     \
+      hipLaunchKernelGGL((k_h2_tn2<2, BM, MP>), grid, dim3(kH2TnThreads), tn2_lds, ctx->stream, M, \
+                         N, K, P, ldp, B, ldb, out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, \
+                         nmb, nnb, ex);                                                          \
+    }                                                                                            \
+  } while (0)
+  if (X) {
+    if (a_rows) NTS_H2TN(true, true); else NTS_H2TN(true, false);
+  } else {
+    if (a_rows) NTS_H2TN(false, true); else NTS_H2TN(false, false);
+  }
+#undef NTS_H2TN
+  NTS_LAUNCH_CHECK();
+  if (splits == 1) return NTS_OK;
+  return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+}

@@ -218,6 +218,35 @@ class HipContext:
         check(self.lib.nts_hip_gemm_tn_gather_f32(self.h, M, N, K, ptr(A), A.stride(0), ptr(rows),
                                                   ptr(B), B.stride(0), ptr(C), C.stride(0)))
 
+    # ---- two-piece f16 pair tables (csrc/gemmh2.hip) ---------------------------
+    def h2_split_rows(self, X, pad_to=32):
+        """X [R, K] fp32 -> (P int32 [R, Kp] pair words, rs fp32 [R] row scales)."""
+        R, K = X.shape
+        Kp = (K + pad_to - 1) // pad_to * pad_to
+        P = torch.empty(R, Kp, dtype=torch.int32, device=X.device)
+        rs = torch.empty(R, dtype=torch.float32, device=X.device)
+        check(self.lib.nts_hip_h2_split_rows(self.h, R, K, ptr(X), X.stride(0), Kp, ptr(P),
+                                             P.stride(0), ptr(rs)))
+        return P, rs
+
+    def gemm_h2_gather(self, P, rs, rows, W, C, relu_dropout=False, p=0.0, seed=0, offset=0):
+        """C = act(X[rows] @ W), X given as its pair table (rows None: all rows)."""
+        K, N = W.shape
+        M = rows.numel() if rows is not None else P.shape[0]
+        check(self.lib.nts_hip_gemm_h2_gather(self.h, int(relu_dropout), M, N, P.shape[1], ptr(P),
+                                              P.stride(0), ptr(rs), ptr(rows), ptr(W), W.stride(0),
+                                              K, ptr(C), C.stride(0), float(p), int(seed),
+                                              int(offset)))
+
+    def gemm_h2_tn_gather(self, P, rs, rows, B, C, M, X=None, bscale=1.0):
+        """C = X[rows, :M].T @ op(B), op(B) = B or B * (X_mask > 0) * bscale."""
+        N = B.shape[1]
+        Kr = rows.numel() if rows is not None else B.shape[0]
+        check(self.lib.nts_hip_gemm_h2_tn_gather(self.h, M, N, Kr, ptr(P), P.stride(0), ptr(rs),
+                                                 ptr(rows), ptr(B), B.stride(0), ptr(X),
+                                                 X.stride(0) if X is not None else 0, float(bscale),
+                                                 ptr(C), C.stride(0)))
+
     def gemm_relu_dropout(self, A, B, C, p=0.0, seed=0, offset=0):
         """C = dropout(relu(A @ B), p) with the Philox mask of (seed, offset)."""
         M, K = A.shape

@@ -39,7 +39,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                early_aggregate=True, sampler_priority=True, fuse_activation=True,
                fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0,
                up_degree=False, gat=False, pd_cache=False, pd_rate=0.2, pd_super_batch=4,
-               gemm="split3", overlap_allreduce=-1):
+               gemm="split3", overlap_allreduce=-1, pair_table=1):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -60,6 +60,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.transform_first = int(transform_first)
     c.gemm_mode = {"f32": _abi.NTS_GEMM_F32, "split3": _abi.NTS_GEMM_SPLIT3}[gemm]
     c.overlap_allreduce = int(overlap_allreduce)
+    c.pair_table = int(pair_table)
     c.early_aggregate = bool(early_aggregate)
     c.sampler_priority = bool(sampler_priority)
     c.fuse_activation = bool(fuse_activation)

@@ -159,6 +159,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("pipeline", &GCNConfig::pipeline)
       .def_readwrite("transform_first", &GCNConfig::transform_first)
       .def_readwrite("gemm_mode", &GCNConfig::gemm_mode)
+      .def_readwrite("pair_table", &GCNConfig::pair_table)
       .def_readwrite("overlap_allreduce", &GCNConfig::overlap_allreduce)
       .def_readwrite("pd_cache", &GCNConfig::pd_cache)
       .def_readwrite("pd_rate", &GCNConfig::pd_rate)

@@ -731,7 +731,8 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
 struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, int64_t sg_ptr,
                         int64_t cs_ptr, double p, int64_t seed, int64_t offset, int64_t prof_ptr,
-                        int64_t h_out) {
+                        int64_t h_out, int64_t pairs_ptr) {
+    const auto* pairs = reinterpret_cast<const PairTable*>(pairs_ptr);
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     auto* sg = reinterpret_cast<sampCSC*>(sg_ptr);
     auto* prof = reinterpret_cast<KernelProfiler*>(prof_ptr);
@@ -744,10 +745,18 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     NtsVar H = h_out ? NtsVar() : torch::empty({std::max<int64_t>(s, 1), N}, f32_opts(dev));
     float* hp = h_out ? reinterpret_cast<float*>(h_out) : H.data_ptr<float>();
     if (prof) prof->begin(KernelProfiler::GATHER_GEMM, st);
-    hip_check(nts_hip_gemm_gather_f32(cs->ctx(), (int)s, (int)N, (int)F, table.data_ptr<float>(),
-                                      (uint64_t)table.stride(0), sg->dev_src(),
-                                      Wc.data_ptr<float>(), (uint64_t)N, hp, (uint64_t)N),
-              "nts_hip_gemm_gather_f32");
+    if (pairs)
+      hip_check(nts_hip_gemm_h2_gather(cs->ctx(), 0, (int)s, (int)N, (int)pairs->P.size(1),
+                                       reinterpret_cast<const uint32_t*>(pairs->P.data_ptr<int32_t>()),
+                                       (uint64_t)pairs->P.stride(0), pairs->rs.data_ptr<float>(),
+                                       sg->dev_src(), Wc.data_ptr<float>(), (uint64_t)N, (int)F, hp,
+                                       (uint64_t)N, 0.f, 0, 0),
+                "nts_hip_gemm_h2_gather");
+    else
+      hip_check(nts_hip_gemm_gather_f32(cs->ctx(), (int)s, (int)N, (int)F, table.data_ptr<float>(),
+                                        (uint64_t)table.stride(0), sg->dev_src(),
+                                        Wc.data_ptr<float>(), (uint64_t)N, hp, (uint64_t)N),
+                "nts_hip_gemm_gather_f32");
     if (prof) prof->end(KernelProfiler::GATHER_GEMM, st, 2.0 * (double)s * F * N);
     NtsVar X1 = torch::empty({v, N}, f32_opts(dev));
     if (prof) prof->begin(KernelProfiler::BOTTOM_AGG, st);
@@ -764,6 +773,7 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     ctx->saved_data["sg"] = sg_ptr;
     ctx->saved_data["cs"] = cs_ptr;
     ctx->saved_data["prof"] = prof_ptr;
+    ctx->saved_data["pairs"] = pairs_ptr;
     ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
     return X1;
   }
@@ -812,14 +822,24 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                   4.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
     }
     NtsVar dW = torch::empty({F, N}, W.options());
+    const auto* pairs = reinterpret_cast<const PairTable*>(ctx->saved_data["pairs"].toInt());
     if (prof) prof->begin(KernelProfiler::GATHER_GEMM_TN, st);
-    hip_check(nts_hip_gemm_tn_gather_f32(cs->ctx(), (int)F, (int)N, (int)s, table.data_ptr<float>(),
-                                         (uint64_t)table.stride(0), sg->dev_src(),
-                                         dH.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
-                                         (uint64_t)N),
-              "nts_hip_gemm_tn_gather_f32");
+    if (pairs && pairs->tn)
+      hip_check(nts_hip_gemm_h2_tn_gather(cs->ctx(), (int)F, (int)N, (int)s,
+                                          reinterpret_cast<const uint32_t*>(pairs->P.data_ptr<int32_t>()),
+                                          (uint64_t)pairs->P.stride(0), pairs->rs.data_ptr<float>(),
+                                          sg->dev_src(), dH.data_ptr<float>(), (uint64_t)N, nullptr, 0,
+                                          1.f, dW.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_gemm_h2_tn_gather");
+    else
+      hip_check(nts_hip_gemm_tn_gather_f32(cs->ctx(), (int)F, (int)N, (int)s, table.data_ptr<float>(),
+                                           (uint64_t)table.stride(0), sg->dev_src(),
+                                           dH.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
+                                           (uint64_t)N),
+                "nts_hip_gemm_tn_gather_f32");
     if (prof) prof->end(KernelProfiler::GATHER_GEMM_TN, st, 2.0 * (double)s * F * N);
-    return {NtsVar(), dW, NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar()};
+    return {NtsVar(), dW,       NtsVar(), NtsVar(), NtsVar(), NtsVar(),
+            NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
 // Output layer + loss in fused kernels (nts_hip.h).  Under grad mode the
@@ -929,10 +949,11 @@ NtsVar hip_relu_dropout(const NtsVar& x, double p, uint64_t seed, uint64_t offse
 
 NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,
                             uint64_t seed, uint64_t offset, NtsStream* cs, KernelProfiler* prof,
-                            float* h_out) {
+                            float* h_out, const PairTable* pairs) {
   return HipBottomTFFn::apply(table, W, reinterpret_cast<int64_t>(sg),
                               reinterpret_cast<int64_t>(cs), p, (int64_t)seed, (int64_t)offset,
-                              reinterpret_cast<int64_t>(prof), reinterpret_cast<int64_t>(h_out));
+                              reinterpret_cast<int64_t>(prof), reinterpret_cast<int64_t>(h_out),
+                              reinterpret_cast<int64_t>(pairs));
 }
 
 // ---------------------------------------------------------------------------

@@ -72,6 +72,19 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     TORCH_CHECK(tf_ok, "transform_first needs >= 2 layers, the MFMA GEMMs with the fused "
                        "activation, no GAT and no feature cache");
   tf_ = tf_ok && cfg.transform_first == 1;
+  if (tf_ && cfg.pair_table > 0) {
+    // the feature table is static: its rows are split into f16 pairs once
+    const int64_t V = F.size(0), K = F.size(1), Kp = (K + 31) / 32 * 32;
+    pairs_ = std::make_unique<PairTable>();
+    pairs_->P = torch::empty({V, Kp}, torch::TensorOptions().dtype(torch::kInt32).device(F.device()));
+    pairs_->rs = torch::empty({V}, f32_opts(graph->device));
+    pairs_->tn = cfg.pair_table >= 2;
+    hip_check(nts_hip_h2_split_rows(cs->ctx(), (uint64_t)V, (uint32_t)K, F.data_ptr<float>(),
+                                    (uint64_t)F.stride(0), (uint32_t)Kp,
+                                    reinterpret_cast<uint32_t*>(pairs_->P.data_ptr<int32_t>()),
+                                    (uint64_t)Kp, pairs_->rs.data_ptr<float>()),
+              "nts_hip_h2_split_rows");
+  }
   // CSR transposes only where a graph-op backward runs (every hop but the
   // outermost, whose backward the context skips — unless the bottom layer is
   // transform-first: its aggregation then has a backward, dH = A^T dZ)
@@ -319,7 +332,7 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
             return hip_bottom_transform(t, P[0]->W, s, p,
                                         (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1, off,
                                         cs.get(), profiler(),
-                                        keep ? h.data_ptr<float>() : nullptr);
+                                        keep ? h.data_ptr<float>() : nullptr, pairs_.get());
           },
           F);
       if (keep) {

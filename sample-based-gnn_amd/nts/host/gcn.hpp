@@ -34,6 +34,10 @@ struct GCNConfig {
   // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode): NTS_GEMM_F32 (fp32-input
   // MFMA) or NTS_GEMM_SPLIT3 (fp32-accurate three-piece bf16 split)
   int gemm_mode = NTS_GEMM_SPLIT3;
+  // transform-first GEMMs on the feature table's f16 pair table (csrc/gemmh2.hip,
+  // built once at construction): 0 = off (gemm_mode), 1 = the forward GEMM,
+  // 2 = the forward and the weight-gradient GEMMs
+  int pair_table = 1;
   // data parallel: the gradient all-reduce of step k runs on a stream of its
   // own and the optimizer step waits for it only where step k+1 first reads
   // W (after its bottom aggregation, which does not depend on W): -1 = on with
@@ -172,6 +176,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   bool pd_active_ = false;
   std::vector<std::pair<const char*, hipEvent_t>> tl_;  // NTS_TIMELINE events
   bool tf_ = false;  // transform-first bottom layer (cfg.transform_first)
+  std::unique_ptr<PairTable> pairs_;  // the feature table's f16 pair table (cfg.pair_table)
   // early aggregation: per sampler slot, the bottom graph op's output and the
   // event after which it (and the slot's sampled graph) is ready
   static constexpr int kSlots = 3;  // sampler slots when pipelined (see the constructor)

@@ -426,9 +426,17 @@ NtsVar hip_relu_dropout(const NtsVar& x, double p, uint64_t seed, uint64_t offse
 // on the layer's sampled block `sg` (its CSR is needed for the backward);
 // autograd returns dW = X[source]^T (A^T (dX1 ⊙ mask)).  h_out != NULL: H =
 // X[source] W is written there ([src_size, F_out], eval / tests).
+// pairs != NULL: the table's f16 pair table (nts_hip_h2_split_rows, built once
+// by the driver) — the forward GEMM runs on it, and the weight-gradient GEMM
+// too when pairs->tn.
+struct PairTable {
+  NtsVar P;   // int32 [V, Kp] pair words
+  NtsVar rs;  // fp32 [V] row scales
+  bool tn = true;
+};
 NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,
                             uint64_t seed, uint64_t offset, NtsStream* cs, KernelProfiler* prof,
-                            float* h_out = nullptr);
+                            float* h_out = nullptr, const PairTable* pairs = nullptr);
 
 struct Parameter {
   NtsVar W, M, V;

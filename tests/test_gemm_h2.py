@@ -1,0 +1,186 @@
+"""Two-piece f16 pair-table GEMMs (NTS_GEMM_H2, csrc/gemmh2.hip) vs fp64 and vs
+the fp32-input MFMA path.
+
+Bar: on the transform-first bottom layer's shapes (row-gathered NN with and
+without the relu/dropout epilogue, row-gathered TN with and without the
+relu/dropout backward) the pair-table path's error against an fp64 GEMM of the
+same fp32 operands, normalised by |A| |B| per element, is at most 2x the fp32
+MFMA path's (plus 1e-7) and below 1e-6 — rows spanning twelve decades of
+magnitude and gradients of 1e-7 included (the per-row / per-column power-of-two
+scales); the dropout keep mask is the fp32 path's; results are deterministic.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from nts.hip import HipContext
+    return HipContext(0, seed=2000)
+
+
+def _check(got32, goth2, ref, scale, factor=2.0):
+    e32 = ((got32.double() - ref).abs() / scale).max().item()
+    eh2 = ((goth2.double() - ref).abs() / scale).max().item()
+    print(f"[h2] fp32 MFMA {e32:.3e}  h2 {eh2:.3e}")
+    assert eh2 <= factor * e32 + 1e-7, (eh2, e32)
+    assert eh2 < 1e-6, eh2
+
+
+def _table(V, K, g, decades=0.0):
+    ld = (K + 31) // 32 * 32 + 32
+    X = torch.full((V, ld), float("nan"), device=DEV)[:, :K]
+    X.copy_(torch.randn(V, K, device=DEV, generator=g))
+    if decades:
+        X.mul_(10.0 ** ((torch.rand(V, 1, device=DEV, generator=g) - 0.5) * decades))
+    X[3].zero_()  # an all-zero row (scale 1)
+    return X
+
+
+def test_split_rows_roundtrip(ctx):
+    g = torch.Generator(device=DEV).manual_seed(7)
+    X = _table(5000, 602, g, decades=12)
+    P, rs = ctx.h2_split_rows(X)
+    torch.cuda.synchronize()
+    assert P.shape == (5000, 608) and (P[:, 602:] == 0).all()
+    w = P.view(torch.int16).view(5000, 608, 2)
+    y = w[..., 0].view(torch.float16).float() + w[..., 1].view(torch.float16).float()
+    rec = y[:, :602].double() * rs.double()[:, None]
+    # rs is a power of two; the row max lands in [2^14, 2^15)
+    assert torch.equal(torch.frexp(rs).mantissa[rs != 0], torch.full_like(rs[rs != 0], 0.5))
+    m = y[:, :602].abs().max(1).values
+    nz = m > 0
+    assert ((m[nz] >= 2 ** 14) & (m[nz] < 2 ** 15)).all()
+    rmax = X.double().abs().max(1).values[:, None] + 1e-300
+    assert ((rec - X.double()).abs() <= 2.0 ** -23 * X.double().abs() + 2.0 ** -38 * rmax).all()
+
+
+@pytest.mark.parametrize("M,N,K,decades", [(228656, 128, 602, 0), (3000, 128, 602, 12),
+                                           (2500, 256, 100, 6), (300, 16, 64, 0)])
+def test_h2_gemm_gather(ctx, M, N, K, decades):
+    g = torch.Generator(device=DEV).manual_seed(M + K + N)
+    V = M + M // 3 + 11
+    X = _table(V, K, g, decades)
+    rows = torch.randperm(V, device=DEV, generator=g)[:M].to(torch.int32)
+    rows[5] = 3  # the zero row
+    W = torch.randn(K, N, device=DEV, generator=g) * 0.05
+    P, rs = ctx.h2_split_rows(X)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.full((M, N), float("nan"), device=DEV)
+    ctx.gemm_gather(X, rows, W, C32)
+    ctx.gemm_h2_gather(P, rs, rows, W, Ch)
+    Xg = X[rows.long()].double()
+    ref = Xg @ W.double()
+    scale = Xg.abs() @ W.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ch).any()
+    _check(C32, Ch, ref, scale)
+    Ch2 = torch.empty_like(Ch)
+    ctx.gemm_h2_gather(P, rs, rows, W, Ch2)
+    torch.cuda.synchronize()
+    assert torch.equal(Ch, Ch2)
+
+
+def test_h2_gemm_all_rows(ctx):
+    g = torch.Generator(device=DEV).manual_seed(11)
+    X = _table(4099, 301, g)
+    W = torch.randn(301, 128, device=DEV, generator=g)
+    P, rs = ctx.h2_split_rows(X)
+    C32 = torch.empty(4099, 128, device=DEV)
+    Ch = torch.empty(4099, 128, device=DEV)
+    ctx.gemm(X, W, C32)
+    ctx.gemm_h2_gather(P, rs, None, W, Ch)
+    ref = X.double() @ W.double()
+    scale = X.double().abs() @ W.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    _check(C32, Ch, ref, scale)
+
+
+@pytest.mark.parametrize("M,N,K,p", [(136076, 128, 602, 0.5), (2050, 64, 77, 0.2), (1000, 128, 128, 0.0)])
+def test_h2_relu_dropout_epilogue(ctx, M, N, K, p):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + 1)
+    X = _table(M, K, g)
+    W = torch.randn(K, N, device=DEV, generator=g)
+    P, rs = ctx.h2_split_rows(X)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.empty(M, N, device=DEV)
+    seed, offset = 0x1234_5678_9ABC, 77
+    ctx.gemm_relu_dropout(X, W, C32, p=p, seed=seed, offset=offset)
+    ctx.gemm_h2_gather(P, rs, None, W, Ch, relu_dropout=True, p=p, seed=seed, offset=offset)
+    Z = X.double() @ W.double()
+    scale = X.double().abs() @ W.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    clear = Z.abs() > 1e-5 * scale
+    assert torch.equal((C32 != 0) & clear, (Ch != 0) & clear)
+    s = 1.0 / (1.0 - p)
+    ref = torch.where(C32 != 0, torch.relu(Z) * s, torch.zeros_like(Z))
+    e32 = ((C32.double() - ref).abs() / (scale * s))[clear].max().item()
+    eh = ((Ch.double() - ref).abs() / (scale * s))[clear].max().item()
+    assert eh <= 2.0 * e32 + 1e-7 and eh < 1e-6, (eh, e32)
+
+
+@pytest.mark.parametrize("M,N,K,gscale", [(602, 128, 228656, 1e-7), (602, 128, 5000, 1.0),
+                                          (100, 256, 3000, 1e3), (41, 64, 300, 1.0)])
+def test_h2_gemm_tn_gather(ctx, M, N, K, gscale):
+    g = torch.Generator(device=DEV).manual_seed(M * N + K + 9)
+    V = K + K // 2 + 5
+    X = _table(V, M, g, decades=6)
+    rows = torch.randint(0, V, (K,), device=DEV, generator=g).to(torch.int32)
+    G = torch.randn(K, N, device=DEV, generator=g) * gscale
+    G[:, 5] *= 1e-9  # a column far below the others
+    P, rs = ctx.h2_split_rows(X)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.full((M, N), float("nan"), device=DEV)
+    ctx.gemm_tn_gather(X, rows, G, C32)
+    ctx.gemm_h2_tn_gather(P, rs, rows, G, Ch, M)
+    Xg = X[rows.long()].double()
+    ref = Xg.t() @ G.double()
+    scale = Xg.abs().t() @ G.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ch).any()
+    _check(C32, Ch, ref, scale)
+    Ch2 = torch.empty_like(Ch)
+    ctx.gemm_h2_tn_gather(P, rs, rows, G, Ch2, M)
+    torch.cuda.synchronize()
+    assert torch.equal(Ch, Ch2)
+
+
+@pytest.mark.parametrize("M,N,K", [(602, 128, 135758), (602, 128, 5000)])
+def test_h2_gemm_tn_masked(ctx, M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M * 3 + N + K)
+    A = _table(K, M, g)
+    G = torch.randn(K, N, device=DEV, generator=g) * 1e-5
+    Xm = torch.relu(torch.randn(K, N, device=DEV, generator=g))
+    P, rs = ctx.h2_split_rows(A)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.empty(M, N, device=DEV)
+    ctx.gemm_tn_masked(A, G, Xm, C32, scale=2.0)
+    ctx.gemm_h2_tn_gather(P, rs, None, G, Ch, M, X=Xm, bscale=2.0)
+    Bm = G.double() * (Xm > 0).double() * 2.0
+    ref = A.double().t() @ Bm
+    scale = A.double().abs().t() @ Bm.abs() + 1e-300
+    torch.cuda.synchronize()
+    _check(C32, Ch, ref, scale)
+
+
+def test_h2_error_distribution_report(ctx):
+    """C2 transform-first shape: mean and max normalised error of both paths."""
+    g = torch.Generator(device=DEV).manual_seed(42)
+    X = torch.rand(228656, 608, device=DEV, generator=g)[:, :602]
+    W = torch.randn(602, 128, device=DEV, generator=g) * 0.05
+    P, rs = ctx.h2_split_rows(X)
+    C32 = torch.empty(228656, 128, device=DEV)
+    Ch = torch.empty_like(C32)
+    ctx.gemm(X, W, C32)
+    ctx.gemm_h2_gather(P, rs, None, W, Ch)
+    ref = X.double() @ W.double()
+    scale = X.double().abs() @ W.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    r32 = (C32.double() - ref).abs() / scale
+    rh = (Ch.double() - ref).abs() / scale
+    print(f"\n[h2] fp32 MFMA: mean {r32.mean().item():.3e} max {r32.max().item():.3e}; "
+          f"h2: mean {rh.mean().item():.3e} max {rh.max().item():.3e}")
