@@ -35,6 +35,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TF = 157.3  # MI355X fp32 matrix peak (MI355X_MICROARCH.md)
+F16_MFMA_PEAK_TF = 2500.0  # MI355X dense f16/bf16 matrix peak (MI355X_MICROARCH.md)
 SHAPE_NAMES = {"reddit": "Reddit", "products": "ogbn-products", "papers100m": "ogbn-papers100M",
                "tiny": "tiny"}
 
@@ -71,9 +72,10 @@ def parse():
                    help="layer GEMM arithmetic: f32 = fp32-input MFMA; split3 = fp32 operands "
                         "split exactly into three bf16 pieces, six piece products on the bf16 "
                         "MFMA (fp32-accurate, csrc/gemm3.hip)")
-    p.add_argument("--pair-table", type=int, default=1, choices=[0, 1, 2],
+    p.add_argument("--pair-table", type=int, default=3, choices=[0, 1, 2, 3],
                    help="transform-first GEMMs on the feature table's f16 pair table "
-                        "(csrc/gemmh2.hip): 0 off, 1 forward GEMM, 2 forward + weight gradient")
+                        "(csrc/gemmh2.hip): 0 off, 1 forward GEMM, 2 forward + weight gradient, "
+                        "3 = 2 with the weight gradient on the whole-row planar kernel")
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
@@ -361,12 +363,36 @@ def roofline(prof: dict, args, layers, world) -> dict:
     stream that launches it), its algorithmic units / average launch time vs
     the MI355X peak; every profiled kernel listed under `kernels`."""
     kernels = {}
+    F, N = layers[0], layers[1]
+    Kp = (F + 31) // 32 * 32
     for name, st in prof.items():
         if not st["calls"]:
             continue
         avg_s = st["ms"] / st["calls"] * 1e-3
         gemm = name.startswith("gather_gemm")
         per = st["units"] / st["calls"]
+        pair = gemm and (args.pair_table >= (1 if name == "gather_gemm" else 2))
+        if pair:
+            # f16 pair-table GEMM (csrc/gemmh2.hip): three f16 MFMA products per
+            # fp32 product, against the dense f16 peak; and its algorithmic
+            # bytes (each gathered pair-table row once, the fp32 B rows / output
+            # rows once, W once) against HBM — the binding roof is reported
+            rows = per / (2.0 * F * N)
+            byt = rows * (4.0 * Kp + 4.0 * N) + 4.0 * Kp * N
+            mf = 3.0 * per / avg_s / 1e12
+            hb = byt / avg_s / 1e9
+            k_m = {"bound": "mfma", "unit": "TFLOP/s", "achieved": mf, "peak": F16_MFMA_PEAK_TF,
+                   "frac": mf / F16_MFMA_PEAK_TF}
+            k_h = {"bound": "hbm", "unit": "GB/s", "achieved": hb, "peak": HBM_PEAK_GBS,
+                   "frac": hb / HBM_PEAK_GBS}
+            k = dict(max(k_m, k_h, key=lambda d: d["frac"]))
+            k.update({"avg_launch_ms": avg_s * 1e3, "flops_per_launch": per,
+                      "f16_mfma_flops_per_launch": 3.0 * per, "algorithmic_bytes_per_launch": byt,
+                      "mfma_frac": k_m["frac"], "hbm_frac": k_h["frac"],
+                      "arithmetic": "f16 pair table (3 f16 MFMAs per fp32 product)",
+                      "calls": st["calls"], "share_of_timed_ms": st["ms"]})
+            kernels[name] = k
+            continue
         ach = per / avg_s / (1e12 if gemm else 1e9)
         peak = FP32_MFMA_PEAK_TF if gemm else HBM_PEAK_GBS
         kernels[name] = {

@@ -450,6 +450,15 @@ int nts_hip_gemm_h2_gather(nts_hip_ctx *ctx, int relu_dropout, int M, int N, int
 int nts_hip_gemm_h2_tn_gather(nts_hip_ctx *ctx, int M, int N, int K, const uint32_t *P, uint64_t ldp,
                               const float *rs, const uint32_t *a_rows, const float *B, uint64_t ldb,
                               const float *Xm, uint64_t ldx, float bscale, float *C, uint64_t ldc);
+/* The same weight gradient on a "planar" pair table (per row the y0 plane of
+ * Kp f16, then the y1 plane; row scales as above), whole rows streamed once by
+ * LDS DMA, every output row in one block (csrc/gemmh2.hip k_h2_tn3):
+ * N % 128 == 0, M <= 640, M <= Kp <= 640. */
+int nts_hip_h2_split_rows_planar(nts_hip_ctx *ctx, uint64_t R, uint32_t K, const float *X,
+                                 uint64_t ldx, uint32_t Kp, uint16_t *Q, uint64_t ldq, float *rs);
+int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx *ctx, int M, int N, int K, const uint16_t *Q, uint64_t ldq,
+                               int Kp, const float *rs, const uint32_t *a_rows, const float *B,
+                               uint64_t ldb, float *C, uint64_t ldc);
 
 /* Hidden-layer forward with its activation fused into the GEMM epilogue:
  *   C = dropout(relu(A B), p)   — vertexForward's

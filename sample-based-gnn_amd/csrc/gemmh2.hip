@@ -103,6 +103,28 @@ __global__ __launch_bounds__(256) void k_h2_split_rows(uint64_t R, uint32_t K, c
   if (lane == 0) rs[r] = ldexpf(1.f, -e);
 }
 
+// planar pair table: per row the y0 plane (Kp f16), then the y1 plane
+__global__ __launch_bounds__(256) void k_h2_split_rows_planar(uint64_t R, uint32_t K, const float* __restrict__ X,
+                                                             uint64_t ldx, uint32_t Kp, uint16_t* __restrict__ Q,
+                                                             uint64_t ldq, float* __restrict__ rs) {
+  const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= R) return;
+  const float* x = X + r * ldx;
+  float m = 0.f;
+  for (uint32_t k = lane; k < K; k += 64) m = fmaxf(m, fabsf(x[k]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const int e = h2_exp(m);
+  uint16_t* q = Q + r * ldq;
+  for (uint32_t k = lane; k < Kp; k += 64) {
+    const uint32_t w = k < K ? h2_pair(ldexpf(x[k], e)) : 0u;
+    q[k] = (uint16_t)(w & 0xFFFFu);
+    q[Kp + k] = (uint16_t)(w >> 16);
+  }
+  if (lane == 0) rs[r] = ldexpf(1.f, -e);
+}
+
 // out[c] = max(out[c], max over rows k of |B[k, c]| * (rs ? rs[amap ? amap[k] : k] : 1)) as
 // float bits (non-negative floats order like their bit patterns); out zeroed
 // by the caller; rsg != NULL: rsg[k] = that row scale.  Thread t: column quad
@@ -118,14 +140,24 @@ __global__ __launch_bounds__(256) void k_colmax(const float* __restrict__ B, uin
   const uint64_t k0 = (uint64_t)blockIdx.x * rows_per_block;
   const uint64_t k1 = k0 + rows_per_block < K ? k0 + rows_per_block : K;
   if (rl < RL) {
-    for (uint64_t k = k0 + rl; k < k1; k += RL) {
-      const float4 v = *reinterpret_cast<const float4*>(B + k * ldb + 4 * q);
-      const float s = rs ? fabsf(rs[amap ? amap[k] : k]) : 1.f;
-      if (rsg && q == 0) rsg[k] = s;  // the row's scale, gathered once for the TN kernel
-      m[0] = fmaxf(m[0], fabsf(v.x) * s);
-      m[1] = fmaxf(m[1], fabsf(v.y) * s);
-      m[2] = fmaxf(m[2], fabsf(v.z) * s);
-      m[3] = fmaxf(m[3], fabsf(v.w) * s);
+    // four rows in flight per thread (the id -> scale gathers are dependent loads)
+    for (uint64_t k = k0 + rl; k < k1; k += 4 * (uint64_t)RL) {
+      float4 v[4];
+      float sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t kk = k + (uint64_t)u * RL < k1 ? k + (uint64_t)u * RL : k1 - 1;
+        v[u] = *reinterpret_cast<const float4*>(B + kk * ldb + 4 * q);
+        sv[u] = rs ? fabsf(rs[amap ? amap[kk] : kk]) : 1.f;
+        if (rsg && q == 0) rsg[kk] = sv[u];  // the row's scale, gathered once for the TN kernel
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        m[0] = fmaxf(m[0], fabsf(v[u].x) * sv[u]);
+        m[1] = fmaxf(m[1], fabsf(v[u].y) * sv[u]);
+        m[2] = fmaxf(m[2], fabsf(v[u].z) * sv[u]);
+        m[3] = fmaxf(m[3], fabsf(v[u].w) * sv[u]);
+      }
     }
   }
 #pragma unroll
@@ -887,6 +919,400 @@ __global__ __launch_bounds__(kH2TnThreads, 1) void k_h2_tn2(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
+// TN v3 (NTS_H2_TN=3, the default where it applies): the weight gradient of
+// the transform-first bottom layer, dW = X[src]^T dH, with whole rows of the
+// "planar" pair table (per row: the y0 plane of Kp f16, then the y1 plane)
+// streamed by LDS DMA.  One block per k-chunk covers EVERY output row (up to
+// 8 waves x TPW 16-row tiles) and 128 columns, so X rows and dH rows are each
+// read once (v1/v2 split the output rows over 2-3 blocks and re-read dH).
+//   per 16-row step: X rows -> an LDS stage (rows padded to a 512-byte
+//   multiple, 16-byte chunks XOR-swizzled by row: conflict-free transposed
+//   reads), raw fp32 dH rows -> an LDS stage; both two steps ahead (three
+//   stages, counted vmcnt, raw barriers); then the block splits the 16 dH
+//   rows (times their row scale and 2^e(col)) into two f16 planes, and each
+//   wave reads its A^T fragments (ds_read_b64_tr_b16, 16 x 4 per plane) and
+//   the 8 x 2 B fragments and runs TPW x 8 x 3 v_mfma_f32_16x16x16_f16.
+constexpr int kH2Tn3Threads = 512;
+constexpr int kH2Tn3BRaw = 16 * 512;  // one step of fp32 dH rows (N = 128)
+constexpr int kH2Tn3BPl = 16 * 256;   // one plane of the split step
+
+__device__ __forceinline__ uint32_t h2_swz(int row) { return (uint32_t)(2 * (row & 7)); }
+
+template <int TPW>
+__global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn3(int M, int K, const char* __restrict__ Q,
+                                                            uint64_t ldq, int pitch, int plane_bytes,
+                                                            const float* __restrict__ B, uint64_t ldb,
+                                                            float* __restrict__ C, uint64_t ldc, int kchunk,
+                                                            uint64_t split_stride, int nnb, H2Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char h2tn3[];
+  const int xstage = 16 * pitch;
+  char* const sx = h2tn3;                          // [3][16][pitch]
+  char* const sbr = sx + 3 * xstage;               // [3][kH2Tn3BRaw]
+  char* const sbp = sbr + 3 * kH2Tn3BRaw;          // [2 planes][kH2Tn3BPl]
+  int* const sce = reinterpret_cast<int*>(sbp + 2 * kH2Tn3BPl);  // [128] column exponents
+  uint32_t* const sid = reinterpret_cast<uint32_t*>(sce + 128);
+  float* const ssc = reinterpret_cast<float*>(sid + kchunk);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int nb = blockIdx.x % nnb, split = blockIdx.x / nnb;
+  const int n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int w_lo = wv * T / 8, w_hi = (wv + 1) * T / 8, ntile = w_hi - w_lo;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk), klast = kend - kbeg - 1;
+  const int nsteps = (kend - kbeg + 15) / 16;
+  for (int k = tid; k <= klast; k += kH2Tn3Threads) {
+    const uint32_t id = ex.amap ? ex.amap[kbeg + k] : (uint32_t)(kbeg + k);
+    sid[k] = id;
+    ssc[k] = ex.rs[id];
+  }
+  __syncthreads();
+  // the chunk's column scales: max |rs[row] B[row, c]| over the chunk's rows
+  // (the partial of this chunk is scaled back by its own 2^-e(col))
+  // thread t: columns 4 (t & 31) .. +3 (the B split role below), rows t >> 5 + 16 j
+  const int sr = tid >> 5, sc = 4 * (tid & 31);
+  int bexp[4];
+  {
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* bp = B + (uint64_t)kbeg * ldb + n0 + sc;
+    for (int k = sr; k <= klast; k += 64) {
+      float4 v[4];
+      float sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kk = min(k + 16 * u, klast);
+        v[u] = *reinterpret_cast<const float4*>(bp + (uint64_t)kk * ldb);
+        sv[u] = k + 16 * u <= klast ? fabsf(ssc[kk]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        m[0] = fmaxf(m[0], fabsf(v[u].x) * sv[u]);
+        m[1] = fmaxf(m[1], fabsf(v[u].y) * sv[u]);
+        m[2] = fmaxf(m[2], fabsf(v[u].z) * sv[u]);
+        m[3] = fmaxf(m[3], fabsf(v[u].w) * sv[u]);
+      }
+    }
+    float* red = reinterpret_cast<float*>(sbp);  // 16 row lanes x 128 columns (8 KB)
+    *reinterpret_cast<float4*>(red + 128 * sr + sc) = make_float4(m[0], m[1], m[2], m[3]);
+    __syncthreads();
+    if (tid < 128) {
+      float mm = 0.f;
+      for (int l = 0; l < 16; ++l) mm = fmaxf(mm, red[128 * l + tid]);
+      sce[tid] = h2_exp(mm);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
+  }
+  const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx, lsbr = (uint32_t)(uintptr_t)(lds_ptr_h)sbr;
+  const int cpr = pitch / 16;  // 16-byte chunks per LDS row
+  const int row_chunks = 2 * plane_bytes / 16;
+  // X(s): 5 x 1 KB pieces per wave per 16-row step (16 * pitch = 40 KB for Kp 608)
+  const int xpieces = xstage / 1024 / 8;
+  auto issue = [&](int s) {
+    s = min(s, nsteps - 1);
+    const int st = s % 3;
+    for (int q = 0; q < xpieces; ++q) {
+      const int p = wv * xpieces + q;
+      const int o = 1024 * p + 16 * lane;
+      const int row = o / pitch, c = (o - row * pitch) / 16;
+      const int gc = c ^ (int)h2_swz(row);  // the global chunk this LDS slot holds
+      const uint32_t id = sid[min(16 * s + row, klast)];
+      const char* src = Q + (uint64_t)id * ldq + 16 * (gc < row_chunks ? gc : 0);
+      glds16h(src, lsx + st * xstage + 1024 * p);
+    }
+    {  // B raw: 1 KB per wave (rows 2 wv, 2 wv + 1)
+      const int row = 2 * wv + (lane >> 5);
+      const int k = kbeg + min(16 * s + row, klast);
+      glds16h(reinterpret_cast<const char*>(B + (uint64_t)k * ldb + n0) + 16 * (lane & 31),
+              lsbr + st * kH2Tn3BRaw + 1024 * wv);
+    }
+  };
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+  f32x4h acc[TPW][8];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[t][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int arow = 4 * g + tq;  // the X row this lane addresses in the transposed reads
+  const uint32_t aswz = h2_swz(arow);
+  const int boff = h2_tr_off(4 * g + tq, tp >> 1) + 8 * (tp & 1);
+  issue(0);
+  issue(1);
+  for (int s = 0; s < nsteps; ++s) {
+    // X(s), B(s) landed (X(s+1), B(s+1) may stay in flight: xpieces + 1 per step)
+    if (xpieces == 5) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_h();
+    issue(s + 2);
+    const int st = s % 3;
+    {  // split B(s): row sr, 4 columns
+      const float4 v = *reinterpret_cast<const float4*>(sbr + st * kH2Tn3BRaw + 512 * sr + 4 * sc);
+      const bool ok = 16 * s + sr <= klast;
+      const float scl = ssc[min(16 * s + sr, klast)];
+      const float x[4] = {v.x, v.y, v.z, v.w};
+      uint32_t w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = ok ? h2_pair(ldexpf(x[u] * scl, bexp[u])) : 0u;
+      const uint32_t lo0 = __builtin_amdgcn_perm(w[1], w[0], 0x05040100u);
+      const uint32_t lo1 = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
+      const uint32_t hi0 = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);
+      const uint32_t hi1 = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
+      const int off = h2_tr_off(sr, sc / 8) + 8 * ((sc / 4) & 1);
+      *reinterpret_cast<uint2*>(sbp + off) = make_uint2(lo0, lo1);
+      *reinterpret_cast<uint2*>(sbp + kH2Tn3BPl + off) = make_uint2(hi0, hi1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the planes are written before the barrier
+    raw_barrier_h();
+    f16x4 bf[8][2];
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct)
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc)
+        bf[ct][pc] = __builtin_bit_cast(
+            f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)(sbp + pc * kH2Tn3BPl + (boff ^ (32 * ct)))));
+    const char* xs = sx + st * xstage + arow * pitch;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (t >= ntile) continue;
+      f16x4 af[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int c = (pc * plane_bytes + 32 * (w_lo + t) + 8 * tp) / 16;
+        af[pc] = __builtin_bit_cast(
+            f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                       (lds_s16x4h*)(xs + 16 * (c ^ (int)aswz) + 8 * (tp & 1))));
+      }
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x16f16(af[1], bf[ct][0], acc[t][ct], 0, 0, 0);
+        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x16f16(af[0], bf[ct][1], acc[t][ct], 0, 0, 0);
+        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x16f16(af[0], bf[ct][0], acc[t][ct], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+  raw_barrier_h();
+  float* Cb = C + (uint64_t)split * split_stride;
+  float cs[8];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) cs[ct] = ldexpf(1.f, -sce[16 * ct + i]);
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (t >= ntile) continue;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 16 * (w_lo + t) + 4 * g + v;
+      if (row >= M) continue;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) Cb[(uint64_t)row * ldc + n0 + 16 * ct + i] = acc[t][ct][v] * cs[ct];
+    }
+  }
+}
+
+// TN v4: k_h2_tn3 on v_mfma_f32_32x32x16_f16 (full-rate f16 MFMA at K = 16;
+// the 16x16x16 form issues at the 16x16x32 form's cycles for half the work).
+template <int TPW>
+__global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const char* __restrict__ Q,
+                                                            uint64_t ldq, int pitch, int plane_bytes,
+                                                            const float* __restrict__ B, uint64_t ldb,
+                                                            float* __restrict__ C, uint64_t ldc, int kchunk,
+                                                            uint64_t split_stride, int nnb, H2Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char h2tn4[];
+  const int xstage = 16 * pitch;
+  char* const sx = h2tn4;                          // [3][16][pitch]
+  char* const sbr = sx + 3 * xstage;               // [3][kH2Tn3BRaw]
+  char* const sbp = sbr + 3 * kH2Tn3BRaw;          // [2 planes][kH2Tn3BPl]
+  int* const sce = reinterpret_cast<int*>(sbp + 2 * kH2Tn3BPl);  // [128] column exponents
+  uint32_t* const sid = reinterpret_cast<uint32_t*>(sce + 128);
+  float* const ssc = reinterpret_cast<float*>(sid + kchunk);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int nb = blockIdx.x % nnb, split = blockIdx.x / nnb;
+  const int n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int w_lo = wv * T / 8, w_hi = (wv + 1) * T / 8, ntile = w_hi - w_lo;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk), klast = kend - kbeg - 1;
+  const int nsteps = (kend - kbeg + 15) / 16;
+  for (int k = tid; k <= klast; k += kH2Tn3Threads) {
+    const uint32_t id = ex.amap ? ex.amap[kbeg + k] : (uint32_t)(kbeg + k);
+    sid[k] = id;
+    ssc[k] = ex.rs[id];
+  }
+  __syncthreads();
+  // the chunk's column scales: max |rs[row] B[row, c]| over the chunk's rows
+  // (the partial of this chunk is scaled back by its own 2^-e(col))
+  // thread t: columns 4 (t & 31) .. +3 (the B split role below), rows t >> 5 + 16 j
+  const int sr = tid >> 5, sc = 4 * (tid & 31);
+  int bexp[4];
+  {
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* bp = B + (uint64_t)kbeg * ldb + n0 + sc;
+    for (int k = sr; k <= klast; k += 64) {
+      float4 v[4];
+      float sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int kk = min(k + 16 * u, klast);
+        v[u] = *reinterpret_cast<const float4*>(bp + (uint64_t)kk * ldb);
+        sv[u] = k + 16 * u <= klast ? fabsf(ssc[kk]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        m[0] = fmaxf(m[0], fabsf(v[u].x) * sv[u]);
+        m[1] = fmaxf(m[1], fabsf(v[u].y) * sv[u]);
+        m[2] = fmaxf(m[2], fabsf(v[u].z) * sv[u]);
+        m[3] = fmaxf(m[3], fabsf(v[u].w) * sv[u]);
+      }
+    }
+    float* red = reinterpret_cast<float*>(sbp);  // 16 row lanes x 128 columns (8 KB)
+    *reinterpret_cast<float4*>(red + 128 * sr + sc) = make_float4(m[0], m[1], m[2], m[3]);
+    __syncthreads();
+    if (tid < 128) {
+      float mm = 0.f;
+      for (int l = 0; l < 16; ++l) mm = fmaxf(mm, red[128 * l + tid]);
+      sce[tid] = h2_exp(mm);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
+  }
+  const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx, lsbr = (uint32_t)(uintptr_t)(lds_ptr_h)sbr;
+  const int cpr = pitch / 16;  // 16-byte chunks per LDS row
+  const int row_chunks = 2 * plane_bytes / 16;
+  // X(s): 5 x 1 KB pieces per wave per 16-row step (16 * pitch = 40 KB for Kp 608)
+  const int xpieces = xstage / 1024 / 8;
+  auto issue = [&](int s) {
+    s = min(s, nsteps - 1);
+    const int st = s % 3;
+    for (int q = 0; q < xpieces; ++q) {
+      const int p = wv * xpieces + q;
+      const int o = 1024 * p + 16 * lane;
+      const int row = o / pitch, c = (o - row * pitch) / 16;
+      const int gc = c ^ (int)h2_swz(row);  // the global chunk this LDS slot holds
+      const uint32_t id = sid[min(16 * s + row, klast)];
+      const char* src = Q + (uint64_t)id * ldq + 16 * (gc < row_chunks ? gc : 0);
+      glds16h(src, lsx + st * xstage + 1024 * p);
+    }
+    {  // B raw: 1 KB per wave (rows 2 wv, 2 wv + 1)
+      const int row = 2 * wv + (lane >> 5);
+      const int k = kbeg + min(16 * s + row, klast);
+      glds16h(reinterpret_cast<const char*>(B + (uint64_t)k * ldb + n0) + 16 * (lane & 31),
+              lsbr + st * kH2Tn3BRaw + 1024 * wv);
+    }
+  };
+  // waves: wn = wv & 1 takes output columns 64 wn .. +63 (two 32-column
+  // tiles), wm = wv >> 1 a quarter of the 32-row output tiles (at most TPW)
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  const int wn = wv & 1, wm = wv >> 1;
+  const int T32 = (M + 31) / 32;
+  const int m_lo = wm * T32 / 4, m_hi = (wm + 1) * T32 / 4, nmt = m_hi - m_lo;
+  f32x16 acc[TPW][2];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[t][nt][v] = 0.f;
+  // 32x32x16 fragments: lane l = (c = l & 31, h = l >> 5) holds k rows 8h .. 8h+7
+  // of column c; read as two transposed 4-row halves by its 16-lane group
+  // (lane 4 tq + tp of the group addresses row 8h + tq (+4), columns 4 tp ..)
+  const int h = lane >> 5, half = (lane >> 4) & 1;
+  const int tq = (lane & 15) >> 2, tp = lane & 3;
+  const int r0 = 8 * h + tq, r1 = r0 + 4;
+  const uint32_t sw0 = h2_swz(r0), sw1 = h2_swz(r1);
+  int boff[2][2];  // [n tile][row half]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int ch = (2 * (64 * wn + 32 * nt + 16 * half + 4 * tp)) / 16;  // 16-byte chunk of the 256-byte row
+    boff[nt][0] = h2_tr_off(r0, ch) + 8 * (tp & 1);
+    boff[nt][1] = h2_tr_off(r1, ch) + 8 * (tp & 1);
+  }
+  issue(0);
+  issue(1);
+  for (int s = 0; s < nsteps; ++s) {
+    // X(s), B(s) landed (X(s+1), B(s+1) may stay in flight: xpieces + 1 per step)
+    if (xpieces == 5) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_h();
+    issue(s + 2);
+    const int st = s % 3;
+    {  // split B(s): row sr, 4 columns
+      const float4 v = *reinterpret_cast<const float4*>(sbr + st * kH2Tn3BRaw + 512 * sr + 4 * sc);
+      const bool ok = 16 * s + sr <= klast;
+      const float scl = ssc[min(16 * s + sr, klast)];
+      const float x[4] = {v.x, v.y, v.z, v.w};
+      uint32_t w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = ok ? h2_pair(ldexpf(x[u] * scl, bexp[u])) : 0u;
+      const uint32_t lo0 = __builtin_amdgcn_perm(w[1], w[0], 0x05040100u);
+      const uint32_t lo1 = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
+      const uint32_t hi0 = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);
+      const uint32_t hi1 = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
+      const int off = h2_tr_off(sr, sc / 8) + 8 * ((sc / 4) & 1);
+      *reinterpret_cast<uint2*>(sbp + off) = make_uint2(lo0, lo1);
+      *reinterpret_cast<uint2*>(sbp + kH2Tn3BPl + off) = make_uint2(hi0, hi1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the planes are written before the barrier
+    raw_barrier_h();
+    auto tr = [&](const char* p) {
+      return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)p);
+    };
+    f16x8 bf[2][2];  // [n tile][plane]
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const s16x4h lo = tr(sbp + pc * kH2Tn3BPl + boff[nt][0]);
+        const s16x4h hi = tr(sbp + pc * kH2Tn3BPl + boff[nt][1]);
+        const s16x8h c = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bf[nt][pc] = __builtin_bit_cast(f16x8, c);
+      }
+    const char* xs0 = sx + st * xstage + r0 * pitch;
+    const char* xs1 = sx + st * xstage + r1 * pitch;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (t >= nmt) continue;
+      f16x8 af[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        const int c = (pc * plane_bytes + 2 * (32 * (m_lo + t) + 16 * half + 4 * tp)) / 16;
+        const s16x4h lo = tr(xs0 + 16 * (c ^ (int)sw0) + 8 * (tp & 1));
+        const s16x4h hi = tr(xs1 + 16 * (c ^ (int)sw1) + 8 * (tp & 1));
+        const s16x8h cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[pc] = __builtin_bit_cast(f16x8, cc);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[nt][0], acc[t][nt], 0, 0, 0);
+        acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[nt][1], acc[t][nt], 0, 0, 0);
+        acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[nt][0], acc[t][nt], 0, 0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+  raw_barrier_h();
+  // acc[t][nt][v] = C[32 (m_lo + t) + 8 (v / 4) + 4 h + v % 4][n0 + 64 wn + 32 nt + (lane & 31)]
+  float* Cb = C + (uint64_t)split * split_stride;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int cl = 64 * wn + 32 * nt + (lane & 31);
+    const float cs = ldexpf(1.f, -sce[cl]);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (t >= nmt) continue;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = 32 * (m_lo + t) + 8 * (v / 4) + 4 * h + (v % 4);
+        if (row < M) Cb[(uint64_t)row * ldc + n0 + cl] = acc[t][nt][v] * cs;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // kernel generation per GEMM (A/B): NTS_H2_NN=1|2, NTS_H2_TN=1|2
 static int h2_gen(const char* var, int dflt) {
   const char* e = getenv(var);
@@ -905,7 +1331,7 @@ static int colmax(nts_hip_ctx* ctx, const float* B, uint64_t ldb, uint64_t K, in
                   const uint32_t* amap, uint32_t* out, float* rsg = nullptr) {
   NTS_HIP_TRY(hipMemsetAsync(out, 0, (size_t)N * sizeof(uint32_t), ctx->stream));
   if (K == 0) return NTS_OK;
-  const uint64_t blocks = std::min<uint64_t>(1024, (K + 63) / 64);
+  const uint64_t blocks = std::min<uint64_t>(256, (K + 63) / 64);  // 256 x N atomics at most
   const uint64_t per = (K + blocks - 1) / blocks;
   hipLaunchKernelGGL(k_colmax, dim3((uint32_t)((K + per - 1) / per)), dim3(256), 0, ctx->stream, B, ldb,
                      K, N, rs, amap, per, out, rsg);
@@ -1071,6 +1497,79 @@ extern "C" int nts_hip_gemm_h2_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, 
     if (a_rows) NTS_H2TN(false, true); else NTS_H2TN(false, false);
   }
 #undef NTS_H2TN
+  NTS_LAUNCH_CHECK();
+  if (splits == 1) return NTS_OK;
+  return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+}
+
+extern "C" int nts_hip_h2_split_rows_planar(nts_hip_ctx* ctx, uint64_t R, uint32_t K, const float* X,
+                                            uint64_t ldx, uint32_t Kp, uint16_t* Q, uint64_t ldq,
+                                            float* rs) {
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(Kp >= K && Kp % 32 == 0 && ldq >= 2 * (uint64_t)Kp && ldq % 8 == 0, "Kp / ldq");
+  NTS_CHECK_ARG(ldx >= K, "ldx < K");
+  NTS_CHECK_ARG(R == 0 || (X && Q && rs), "NULL buffer");
+  NTS_CHECK_ARG((uintptr_t)Q % 16 == 0, "Q must be 16-byte aligned");
+  if (R == 0) return NTS_OK;
+  hipLaunchKernelGGL(k_h2_split_rows_planar, dim3((uint32_t)((R + 3) / 4)), dim3(256), 0, ctx->stream, R,
+                     K, X, ldx, Kp, Q, ldq, rs);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+// TN v3 on the planar table (k_h2_tn3): N % 128 == 0, M <= 8 * 5 * 16 = 640,
+// rows of <= 640 pair words (Kp <= 640).  Scratch: [column max][row scales][partials].
+extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
+                                          uint64_t ldq, int Kp, const float* rs, const uint32_t* a_rows,
+                                          const float* B, uint64_t ldb, float* C, uint64_t ldc) {
+  constexpr int TPW = 5;
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(M > 0 && M <= 8 * TPW * 16 && N > 0 && N % 128 == 0 && K >= 0, "shape");
+  NTS_CHECK_ARG(Kp % 32 == 0 && Kp >= M && Kp <= 640 && ldq >= 2 * (uint64_t)Kp && ldq % 8 == 0 &&
+                    (uintptr_t)Q % 16 == 0, "planar table layout");
+  NTS_CHECK_ARG(ldb >= (uint64_t)N && ldb % 4 == 0 && (uintptr_t)B % 16 == 0, "B layout");
+  NTS_CHECK_ARG(ldc >= (uint64_t)N, "ldc");
+  NTS_CHECK_ARG(K == 0 || (Q && rs && B && C), "NULL buffer");
+  if (K == 0) {
+    NTS_HIP_TRY(hipMemset2DAsync(C, ldc * sizeof(float), 0, (size_t)N * sizeof(float), (size_t)M,
+                                 ctx->stream));
+    return NTS_OK;
+  }
+  const int nnb = N / 128;
+  const int pitch = (4 * Kp + 511) / 512 * 512;
+  const int ksteps = (K + 15) / 16;
+  int splits = std::max(1, std::min(256 / nnb, ksteps / 8));
+  int kchunk = ((ksteps + splits - 1) / splits) * 16;
+  if (kchunk > 960) kchunk = 960;  // the chunk's ids + row scales in LDS (8 B per row)
+  splits = (K + kchunk - 1) / kchunk;
+  const int lds = 3 * 16 * pitch + 3 * kH2Tn3BRaw + 2 * kH2Tn3BPl + 512 + 8 * kchunk;
+  NTS_CHECK_ARG(lds <= 160 * 1024, "LDS");
+  const uint64_t stride = (uint64_t)M * N;
+  const size_t part_bytes = splits > 1 ? stride * splits * sizeof(float) : 0;
+  float* out = C;
+  uint64_t ldo = ldc;
+  if (splits > 1) {
+    NTS_RET(ensure_scratch(ctx, part_bytes + 256));
+    out = (float*)ctx->scratch;
+    ldo = N;
+  }
+  H2Extra ex;  // the column scales are per chunk, computed in the kernel
+  ex.amap = a_rows;
+  ex.rs = rs;
+  static const bool v3 = h2_gen("NTS_H2_TN", 2) == 1;  // NTS_H2_TN=1: the 16x16x16 form (A/B)
+  if (v3) {
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn3<TPW>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL((k_h2_tn3<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
+                       reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, B, ldb,
+                       out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, nnb, ex);
+  } else {
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL((k_h2_tn4<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
+                       reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, B, ldb,
+                       out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, nnb, ex);
+  }
   NTS_LAUNCH_CHECK();
   if (splits == 1) return NTS_OK;
   return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);

@@ -229,6 +229,24 @@ class HipContext:
                                              P.stride(0), ptr(rs)))
         return P, rs
 
+    def h2_split_rows_planar(self, X, pad_to=32):
+        """X [R, K] fp32 -> (Q int16 [R, 2 Kp]: y0 plane then y1 plane per row, rs [R])."""
+        R, K = X.shape
+        Kp = (K + pad_to - 1) // pad_to * pad_to
+        Q = torch.empty(R, 2 * Kp, dtype=torch.int16, device=X.device)
+        rs = torch.empty(R, dtype=torch.float32, device=X.device)
+        check(self.lib.nts_hip_h2_split_rows_planar(self.h, R, K, ptr(X), X.stride(0), Kp, ptr(Q),
+                                                    Q.stride(0), ptr(rs)))
+        return Q, rs
+
+    def gemm_h2p_tn_gather(self, Q, rs, rows, B, C, M):
+        """C = X[rows, :M].T @ B with X given as its planar pair table."""
+        N = B.shape[1]
+        Kr = rows.numel() if rows is not None else B.shape[0]
+        check(self.lib.nts_hip_gemm_h2p_tn_gather(self.h, M, N, Kr, ptr(Q), Q.stride(0),
+                                                  Q.shape[1] // 2, ptr(rs), ptr(rows), ptr(B),
+                                                  B.stride(0), ptr(C), C.stride(0)))
+
     def gemm_h2_gather(self, P, rs, rows, W, C, relu_dropout=False, p=0.0, seed=0, offset=0):
         """C = act(X[rows] @ W), X given as its pair table (rows None: all rows)."""
         K, N = W.shape

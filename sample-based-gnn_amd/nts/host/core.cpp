@@ -824,7 +824,15 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     NtsVar dW = torch::empty({F, N}, W.options());
     const auto* pairs = reinterpret_cast<const PairTable*>(ctx->saved_data["pairs"].toInt());
     if (prof) prof->begin(KernelProfiler::GATHER_GEMM_TN, st);
-    if (pairs && pairs->tn)
+    if (pairs && pairs->tn && pairs->Q.defined())
+      hip_check(nts_hip_gemm_h2p_tn_gather(cs->ctx(), (int)F, (int)N, (int)s,
+                                           reinterpret_cast<const uint16_t*>(pairs->Q.data_ptr<int16_t>()),
+                                           (uint64_t)pairs->Q.stride(0), (int)(pairs->Q.size(1) / 2),
+                                           pairs->rs.data_ptr<float>(), sg->dev_src(),
+                                           dH.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
+                                           (uint64_t)N),
+                "nts_hip_gemm_h2p_tn_gather");
+    else if (pairs && pairs->tn)
       hip_check(nts_hip_gemm_h2_tn_gather(cs->ctx(), (int)F, (int)N, (int)s,
                                           reinterpret_cast<const uint32_t*>(pairs->P.data_ptr<int32_t>()),
                                           (uint64_t)pairs->P.stride(0), pairs->rs.data_ptr<float>(),

@@ -71,7 +71,12 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   if (cfg.transform_first == 1)
     TORCH_CHECK(tf_ok, "transform_first needs >= 2 layers, the MFMA GEMMs with the fused "
                        "activation, no GAT and no feature cache");
-  tf_ = tf_ok && cfg.transform_first == 1;
+  // auto (-1): transform first where the first layer narrows the rows at
+  // least 4x and its GEMMs run on the f16 pair tables (C2: 602 -> 128,
+  // 0.87 vs 0.99 ms/step); the reference's order elsewhere
+  tf_ = tf_ok && (cfg.transform_first == 1 ||
+                  (cfg.transform_first < 0 && cfg.pair_table >= 3 &&
+                   cfg.layer_size[0] >= 4 * cfg.layer_size[1]));
   if (tf_ && cfg.pair_table > 0) {
     // the feature table is static: its rows are split into f16 pairs once
     const int64_t V = F.size(0), K = F.size(1), Kp = (K + 31) / 32 * 32;
@@ -84,6 +89,18 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                     reinterpret_cast<uint32_t*>(pairs_->P.data_ptr<int32_t>()),
                                     (uint64_t)Kp, pairs_->rs.data_ptr<float>()),
               "nts_hip_h2_split_rows");
+    // the weight gradient on the planar form where k_h2_tn3 takes the shape
+    // (every output row in one block: K <= 640, N % 128 == 0)
+    const int64_t Nh = cfg.layer_size[1];
+    if (cfg.pair_table >= 3 && Kp <= 640 && Nh % 128 == 0) {
+      pairs_->Q = torch::empty({V, 2 * Kp},
+                               torch::TensorOptions().dtype(torch::kInt16).device(F.device()));
+      hip_check(nts_hip_h2_split_rows_planar(cs->ctx(), (uint64_t)V, (uint32_t)K, F.data_ptr<float>(),
+                                             (uint64_t)F.stride(0), (uint32_t)Kp,
+                                             reinterpret_cast<uint16_t*>(pairs_->Q.data_ptr<int16_t>()),
+                                             (uint64_t)(2 * Kp), pairs_->rs.data_ptr<float>()),
+                "nts_hip_h2_split_rows_planar");
+    }
   }
   // CSR transposes only where a graph-op backward runs (every hop but the
   // outermost, whose backward the context skips — unless the bottom layer is

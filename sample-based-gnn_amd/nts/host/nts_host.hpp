@@ -433,6 +433,7 @@ struct PairTable {
   NtsVar P;   // int32 [V, Kp] pair words
   NtsVar rs;  // fp32 [V] row scales
   bool tn = true;
+  NtsVar Q;   // int16 [V, 2 Kp] planar form (defined: the weight gradient on k_h2_tn3)
 };
 NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,
                             uint64_t seed, uint64_t offset, NtsStream* cs, KernelProfiler* prof,

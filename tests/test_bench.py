@@ -24,7 +24,7 @@ def bench():
 def _args(**kw):
     base = dict(shape="reddit", batch=10000, fanout="25-10", weight="sum", transform_first=-1,
                 model="gcn", cache_rate=-1.0, gemm="split3", no_hip_gemm=False, no_pipeline=False,
-                pd_cache=False, pd_rate=0.2, pd_super_batch=4)
+                pd_cache=False, pd_rate=0.2, pd_super_batch=4, pair_table=0)
     base.update(kw)
     return types.SimpleNamespace(**base)
 
@@ -41,6 +41,14 @@ def test_roofline_dominant_kernel_and_units(bench, monkeypatch):
     assert rl["frac"] == pytest.approx(rl["achieved"] / bench.HBM_PEAK_GBS)
     assert rl["kernels"]["gather_gemm"]["bound"] == "mfma"
     assert "gat_forward" not in rl["kernels"]
+    # f16 pair-table GEMM: three f16 MFMA products per fp32 product vs the f16
+    # peak, its algorithmic bytes vs HBM; the larger fraction is the bound
+    g = bench.roofline(prof, _args(pair_table=3), [602, 128, 41], 1)["kernels"]["gather_gemm"]
+    rows = 35e9 / (2 * 602 * 128)
+    assert g["f16_mfma_flops_per_launch"] == pytest.approx(3 * 35e9)
+    assert g["algorithmic_bytes_per_launch"] == pytest.approx(rows * (4 * 608 + 4 * 128) + 4 * 608 * 128)
+    assert g["mfma_frac"] == pytest.approx(3 * 35e9 / 0.1e-3 / 1e12 / bench.F16_MFMA_PEAK_TF)
+    assert g["bound"] == "hbm" and g["frac"] == pytest.approx(max(g["mfma_frac"], g["hbm_frac"]))
 
 
 def test_pmc_attached_only_for_the_same_build_and_workload(bench, monkeypatch, tmp_path):

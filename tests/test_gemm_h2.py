@@ -184,3 +184,42 @@ def test_h2_error_distribution_report(ctx):
     rh = (Ch.double() - ref).abs() / scale
     print(f"\n[h2] fp32 MFMA: mean {r32.mean().item():.3e} max {r32.max().item():.3e}; "
           f"h2: mean {rh.mean().item():.3e} max {rh.max().item():.3e}")
+
+
+def test_split_rows_planar_matches_pairs(ctx):
+    g = torch.Generator(device=DEV).manual_seed(8)
+    X = _table(3000, 602, g, decades=8)
+    P, rs = ctx.h2_split_rows(X)
+    Q, rs2 = ctx.h2_split_rows_planar(X)
+    torch.cuda.synchronize()
+    assert torch.equal(rs, rs2)
+    w = P.view(torch.int16).view(3000, 608, 2)
+    assert torch.equal(Q[:, :608], w[..., 0]) and torch.equal(Q[:, 608:], w[..., 1])
+
+
+@pytest.mark.parametrize("M,N,K,gscale", [(602, 128, 228656, 1e-7), (602, 128, 5003, 1.0),
+                                          (100, 256, 3000, 1e3), (600, 128, 100, 1.0),
+                                          (41, 128, 17, 1.0)])
+def test_h2p_gemm_tn_gather(ctx, M, N, K, gscale):
+    """TN v3 on the planar table: whole rows by LDS DMA, every output row in one block."""
+    g = torch.Generator(device=DEV).manual_seed(M * N + K + 19)
+    V = K + K // 2 + 5
+    X = _table(V, M, g, decades=6)
+    rows = torch.randint(0, V, (K,), device=DEV, generator=g).to(torch.int32)
+    G = torch.randn(K, N, device=DEV, generator=g) * gscale
+    G[:, 5] *= 1e-9
+    Q, rs = ctx.h2_split_rows_planar(X)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.full((M, N), float("nan"), device=DEV)
+    ctx.gemm_tn_gather(X, rows, G, C32)
+    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch, M)
+    Xg = X[rows.long()].double()
+    ref = Xg.t() @ G.double()
+    scale = Xg.abs().t() @ G.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ch).any()
+    _check(C32, Ch, ref, scale)
+    Ch2 = torch.empty_like(Ch)
+    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch2, M)
+    torch.cuda.synchronize()
+    assert torch.equal(Ch, Ch2)

@@ -69,13 +69,14 @@ def _driver(E, graph, F, C, layers, fanout, batch, drop=0.0, seed=2000, comm=Non
 
 
 @pytest.mark.parametrize("F,tf,pt", [(602, 0, 1), (128, 0, 1), (602, 1, 0), (602, 1, 1),
-                                     (128, 1, 2), (48, 1, 1)])
+                                     (128, 1, 2), (48, 1, 1), (602, 1, 3)])
 def test_gcn_forward_activations_match_gcn_cpu_sample(E, graph, F, tf, pt):
     """tf = 0: aggregate first, the reference's order (Y0 bit-exact);
     tf = 1: transform first, A (X W0): H = X W0 and every later activation
     within the north-star's 1e-4 of the GCN_CPU_SAMPLE chain (pt: the
     forward GEMM on the fp32 table (0) or on its f16 pair table (1, 2))."""
-    drv, feat, labels, _ = _driver(E, graph, F, 41, [F, 64, 41], [25, 10], 256, transform_first=tf,
+    H = 128 if pt == 3 else 64
+    drv, feat, labels, _ = _driver(E, graph, F, 41, [F, H, 41], [25, 10], 256, transform_first=tf,
                                    pair_table=pt)
     assert drv.transform_first == bool(tf)
     seeds = torch.arange(7, 7 + 256, dtype=torch.int32)
@@ -154,14 +155,15 @@ def test_one_rank_communicator_is_identical(E, graph, overlap, tf):
         assert torch.equal(x, y)
 
 
-@pytest.mark.parametrize("tf,pt", [(0, 1), (1, 0), (1, 1), (1, 2)])
+@pytest.mark.parametrize("tf,pt", [(0, 1), (1, 0), (1, 1), (1, 2), (1, 3)])
 def test_training_step_matches_oracle_step(E, graph, tf, pt):
     """One train_batch: sample -> forward -> NLL -> self_backward (graph-op
     backward through the CSR) -> learn_local_with_decay_Adam, vs the oracle
     (tf = 1: the bottom layer transform-first, its backward through the bottom
     layer's CSR and the row-gathered weight-gradient GEMM)."""
     F, C, B = 64, 7, 200
-    drv, feat, labels, train = _driver(E, graph, F, C, [F, 32, C], [10, 5], B, transform_first=tf,
+    H = 128 if pt == 3 else 32  # pt 3: the planar weight-gradient kernel takes N % 128 == 0
+    drv, feat, labels, train = _driver(E, graph, F, C, [F, H, C], [10, 5], B, transform_first=tf,
                                        pair_table=pt)
     W0 = [w.cpu().clone() for w in drv.weights()]
     drv.train_batch()
