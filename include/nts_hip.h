@@ -459,6 +459,13 @@ int nts_hip_h2_split_rows_planar(nts_hip_ctx *ctx, uint64_t R, uint32_t K, const
 int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx *ctx, int M, int N, int K, const uint16_t *Q, uint64_t ldq,
                                int Kp, const float *rs, const uint32_t *a_rows, const float *B,
                                uint64_t ldb, float *C, uint64_t ldc);
+/* The forward GEMM on the planar table (k_h2_nn3: W's 16-column slices held
+ * in registers, 16-row tiles of whole rows by LDS DMA): N % 128 == 0,
+ * K <= Kp <= 640; arguments as nts_hip_gemm_h2_gather. */
+int nts_hip_gemm_h2p_gather(nts_hip_ctx *ctx, int relu_dropout, int M, int N, int Kp, const uint16_t *Q,
+                            uint64_t ldq, const float *rs, const uint32_t *a_rows, const float *W,
+                            uint64_t ldw, int K, float *C, uint64_t ldc, float p, uint64_t seed,
+                            uint64_t offset);
 
 /* Hidden-layer forward with its activation fused into the GEMM epilogue:
  *   C = dropout(relu(A B), p)   — vertexForward's

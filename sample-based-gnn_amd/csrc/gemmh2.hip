@@ -1313,6 +1313,113 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
 }
 
 // ---------------------------------------------------------------------------
+// NN v3 (planar table, NTS_H2_NN default where it applies): H = diag(rs) X[amap] W
+// with W stationary: wave wv holds the f16 fragments of W's 16-column slice
+// n0 + 16 wv .. +15 for EVERY k-step in registers (<= 20 steps x 2 pieces),
+// loaded once; the block streams 16-row tiles of whole planar rows by LDS DMA
+// (the TN v4 stage: rows padded to a 512-byte multiple, 16-byte chunks
+// XOR-swizzled by row), two tiles ahead, and per tile each wave runs
+// nks x 3 v_mfma_f32_16x16x32_f16 on A fragments read from the stage.
+constexpr int kH2Nn3KS = 20;  // k-steps held in registers (Kp <= 640)
+
+template <bool EPI, bool AMAP>
+__global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const char* __restrict__ Q,
+                                                  uint64_t ldq, int pitch, int plane_bytes,
+                                                  const char* __restrict__ bimg, float* __restrict__ C,
+                                                  uint64_t ldc, H2Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char h2nn3[];
+  const int xstage = 16 * pitch;
+  char* const sx = h2nn3;  // [3][16][pitch]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int nb = blockIdx.y, n0 = nb * 128;
+  const int nks = Kp / 32;
+  const int T = (M + 15) / 16;
+  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
+  const int nt = t1 - t0;
+  if (nt <= 0) return;
+  uint32_t* const sid = reinterpret_cast<uint32_t*>(sx + 3 * xstage);  // [16 nt] row ids
+  float* const srs = reinterpret_cast<float*>(sid + 16 * nt);           // [16 nt] row scales
+  for (int r = tid; r < 16 * nt; r += 512) {
+    const int64_t row = min((int64_t)t0 * 16 + r, (int64_t)M - 1);
+    const uint32_t id = AMAP ? ex.amap[row] : (uint32_t)row;
+    sid[r] = id;
+    srs[r] = ex.rs[id];
+  }
+  // W: img[s][cb][ct][piece][lane] (k_h2_split_b) — this wave's ct = wv
+  f16x8 wf[kH2Nn3KS][2];
+#pragma unroll
+  for (int s = 0; s < kH2Nn3KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      wf[s][p] = s < nks ? *reinterpret_cast<const f16x8*>(
+                               bimg + ((size_t)s * gridDim.y + nb) * kH2Img + wv * 2 * kH2Frag +
+                               p * kH2Frag + 16 * lane)
+                         : f16x8{};
+  const float cs = ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[n0 + 16 * wv + i])));
+  __syncthreads();  // (waits for every load above: the LDS DMA counts below start from zero)
+  const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx;
+  const int xpieces = xstage / 1024 / 8;
+  const int row_chunks = 2 * plane_bytes / 16;
+#define NTS_NN3_ISSUE(R_)                                                                        \
+  do {                                                                                           \
+    const int r_ = min((R_), nt - 1);                                                            \
+    for (int q = 0; q < xpieces; ++q) {                                                          \
+      const int p = wv * xpieces + q;                                                            \
+      const int o = 1024 * p + 16 * lane;                                                        \
+      const int row = o / pitch, c = (o - row * pitch) / 16;                                     \
+      const int gc = c ^ (row & 15); /* the global chunk this LDS slot holds */                  \
+      const char* src = Q + (uint64_t)sid[16 * r_ + row] * ldq + 16 * (gc < row_chunks ? gc : 0); \
+      glds16h(src, lsx + (r_ % 3) * xstage + 1024 * p);                                          \
+    }                                                                                            \
+  } while (0)
+  const int pch = plane_bytes / 16;  // chunks per plane
+  const int iswz = i;                 // row i's swizzle (i < 16)
+  NTS_NN3_ISSUE(0);
+  NTS_NN3_ISSUE(1);
+  for (int r = 0; r < nt; ++r) {
+    // tile r landed; younger: round r-2's 4 stores, tile r+1's pieces, round r-1's 4 stores
+    if (xpieces == 5) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier_h();
+    NTS_NN3_ISSUE(r + 2);
+    const char* xs = sx + (r % 3) * xstage + i * pitch;
+    f32x4h acc = f32x4h{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kH2Nn3KS; ++s) {
+      if (s < nks) {
+        const f16x8 a1 = *reinterpret_cast<const f16x8*>(xs + 16 * ((pch + 4 * s + g) ^ iswz));
+        const f16x8 a0 = *reinterpret_cast<const f16x8*>(xs + 16 * ((4 * s + g) ^ iswz));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, wf[s][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][0], acc, 0, 0, 0);
+      }
+    }
+    // acc[v] = H[16 (t0 + r) + 4 g + v][n0 + 16 wv + i]
+    const int64_t r4 = (int64_t)(t0 + r) * 16 + 4 * g;
+    const uint32_t col = (uint32_t)(n0 + 16 * wv + i);
+    float o[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) o[v] = acc[v] * cs * srs[16 * r + 4 * g + v];
+    if constexpr (EPI) {
+      const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
+      const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+  raw_barrier_h();
+#undef NTS_NN3_ISSUE
+}
+
+// ---------------------------------------------------------------------------
 // kernel generation per GEMM (A/B): NTS_H2_NN=1|2, NTS_H2_TN=1|2
 static int h2_gen(const char* var, int dflt) {
   const char* e = getenv(var);
@@ -1573,4 +1680,62 @@ extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K,
   NTS_LAUNCH_CHECK();
   if (splits == 1) return NTS_OK;
   return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+}
+
+// NN v3 on the planar table (k_h2_nn3): N % 128 == 0, Kp <= 640.  The W image
+// and its column maxima in scratch, as nts_hip_gemm_h2_gather.
+extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M, int N, int Kp,
+                                       const uint16_t* Q, uint64_t ldq, const float* rs,
+                                       const uint32_t* a_rows, const float* W, uint64_t ldw, int K,
+                                       float* C, uint64_t ldc, float p, uint64_t seed, uint64_t offset) {
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(M >= 0 && N > 0 && N % 128 == 0 && K > 0 && Kp >= K && Kp % 32 == 0 &&
+                    Kp <= 32 * kH2Nn3KS, "shape");
+  NTS_CHECK_ARG(ldq >= 2 * (uint64_t)Kp && ldq % 8 == 0 && (uintptr_t)Q % 16 == 0, "planar table layout");
+  NTS_CHECK_ARG(ldw >= (uint64_t)N && ldc >= (uint64_t)N, "ld");
+  NTS_CHECK_ARG(M == 0 || (Q && rs && W && C), "NULL buffer");
+  NTS_CHECK_ARG(p >= 0.f && p < 1.f, "p must be in [0, 1)");
+  if (M == 0) return NTS_OK;
+  const int ncb = N / 128, nsteps = Kp / 32;
+  const size_t cm_bytes = ((size_t)N * 4 + 255) / 256 * 256;
+  const size_t img = (size_t)nsteps * ncb * kH2Img;
+  NTS_RET(ensure_scratch(ctx, cm_bytes + img + 256));
+  uint32_t* cmax = (uint32_t*)ctx->scratch;
+  char* bimg = (char*)ctx->scratch + cm_bytes;
+  NTS_RET(colmax(ctx, W, ldw, (uint64_t)K, N, nullptr, nullptr, cmax));
+  const int total = nsteps * ncb * 512;
+  hipLaunchKernelGGL(k_h2_split_b, dim3((total + 255) / 256), dim3(256), 0, ctx->stream, W, ldw, K, N,
+                     total, ncb, cmax, bimg);
+  NTS_LAUNCH_CHECK();
+  H2Extra ex;
+  ex.keep_threshold = dropout_threshold(p);
+  ex.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  ex.seed = seed;
+  ex.offset = offset;
+  ex.amap = a_rows;
+  ex.rs = rs;
+  ex.cmax = cmax;
+  const int pitch = (4 * Kp + 511) / 512 * 512;
+  const int T = (M + 15) / 16;
+  const int gx = std::max(1, std::min(256 / ncb, T));
+  const int max_tiles = (T + gx - 1) / gx;
+  const int lds = 3 * 16 * pitch + 2 * 4 * 16 * max_tiles;
+  NTS_CHECK_ARG(lds <= 160 * 1024, "too many rows for the row-id stage (use nts_hip_gemm_h2_gather)");
+  const dim3 grid(gx, ncb);
+#define NTS_H2NN3(E, MP)                                                                          \
+  do {                                                                                            \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn3<E, MP>),              \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));            \
+    hipLaunchKernelGGL((k_h2_nn3<E, MP>), grid, dim3(512), lds, ctx->stream, M, N, Kp,            \
+                       reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, bimg, C, \
+                       ldc, ex);                                                                  \
+  } while (0)
+  if (relu_dropout) {
+    if (a_rows) NTS_H2NN3(true, true); else NTS_H2NN3(true, false);
+  } else {
+    if (a_rows) NTS_H2NN3(false, true); else NTS_H2NN3(false, false);
+  }
+#undef NTS_H2NN3
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
 }

@@ -48,7 +48,7 @@ EXPORTED = (
     "nts_hip_host_device_pointer", "nts_hip_gather_rows_cached", "nts_hip_spmm_csc_fwd_cached",
     "nts_hip_stage_uncached_rows", "nts_hip_gat_forward", "nts_hip_gat_backward",
     "nts_hip_h2_split_rows", "nts_hip_gemm_h2_gather", "nts_hip_gemm_h2_tn_gather",
-    "nts_hip_h2_split_rows_planar", "nts_hip_gemm_h2p_tn_gather",
+    "nts_hip_h2_split_rows_planar", "nts_hip_gemm_h2p_tn_gather", "nts_hip_gemm_h2p_gather",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -124,6 +124,7 @@ def lib() -> C.CDLL:
         "nts_hip_gemm_h2_tn_gather": ([P, I, I, I, P, U64, P, P, P, U64, P, U64, F, P, U64], I),
         "nts_hip_h2_split_rows_planar": ([P, U64, U32, P, U64, U32, P, U64, P], I),
         "nts_hip_gemm_h2p_tn_gather": ([P, I, I, I, P, U64, I, P, P, P, U64, P, U64], I),
+        "nts_hip_gemm_h2p_gather": ([P, I, I, I, I, P, U64, P, P, P, U64, I, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),

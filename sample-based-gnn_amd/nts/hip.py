@@ -239,6 +239,14 @@ class HipContext:
                                                     Q.stride(0), ptr(rs)))
         return Q, rs
 
+    def gemm_h2p_gather(self, Q, rs, rows, W, C, relu_dropout=False, p=0.0, seed=0, offset=0):
+        """C = act(X[rows] @ W), X given as its planar pair table (rows None: all rows)."""
+        K, N = W.shape
+        M = rows.numel() if rows is not None else Q.shape[0]
+        check(self.lib.nts_hip_gemm_h2p_gather(self.h, int(relu_dropout), M, N, Q.shape[1] // 2, ptr(Q),
+                                               Q.stride(0), ptr(rs), ptr(rows), ptr(W), W.stride(0), K,
+                                               ptr(C), C.stride(0), float(p), int(seed), int(offset)))
+
     def gemm_h2p_tn_gather(self, Q, rs, rows, B, C, M):
         """C = X[rows, :M].T @ B with X given as its planar pair table."""
         N = B.shape[1]

@@ -745,7 +745,14 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     NtsVar H = h_out ? NtsVar() : torch::empty({std::max<int64_t>(s, 1), N}, f32_opts(dev));
     float* hp = h_out ? reinterpret_cast<float*>(h_out) : H.data_ptr<float>();
     if (prof) prof->begin(KernelProfiler::GATHER_GEMM, st);
-    if (pairs)
+    if (pairs && pairs->Q.defined())
+      hip_check(nts_hip_gemm_h2p_gather(cs->ctx(), 0, (int)s, (int)N, (int)(pairs->Q.size(1) / 2),
+                                        reinterpret_cast<const uint16_t*>(pairs->Q.data_ptr<int16_t>()),
+                                        (uint64_t)pairs->Q.stride(0), pairs->rs.data_ptr<float>(),
+                                        sg->dev_src(), Wc.data_ptr<float>(), (uint64_t)N, (int)F, hp,
+                                        (uint64_t)N, 0.f, 0, 0),
+                "nts_hip_gemm_h2p_gather");
+    else if (pairs)
       hip_check(nts_hip_gemm_h2_gather(cs->ctx(), 0, (int)s, (int)N, (int)pairs->P.size(1),
                                        reinterpret_cast<const uint32_t*>(pairs->P.data_ptr<int32_t>()),
                                        (uint64_t)pairs->P.stride(0), pairs->rs.data_ptr<float>(),

@@ -58,6 +58,7 @@ def main():
     res["h2_nn"] = timeit(lambda: h2.gemm_h2_gather(P, rs, rows, W, C), a.iters)
     res["h2_tn"] = timeit(lambda: h2.gemm_h2_tn_gather(P, rs, rows, G, dW, a.K), a.iters)
     Q, rs2 = h2.h2_split_rows_planar(X)
+    res["h2p_nn"] = timeit(lambda: h2.gemm_h2p_gather(Q, rs2, rows, W, C), a.iters)
     res["h2p_tn"] = timeit(lambda: h2.gemm_h2p_tn_gather(Q, rs2, rows, G, dW, a.K), a.iters)
     res["h2_split_rows"] = timeit(lambda: h2.h2_split_rows(X), 3)
     for k, us in res.items():

@@ -223,3 +223,48 @@ def test_h2p_gemm_tn_gather(ctx, M, N, K, gscale):
     ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch2, M)
     torch.cuda.synchronize()
     assert torch.equal(Ch, Ch2)
+
+
+@pytest.mark.parametrize("M,N,K,decades", [(228656, 128, 602, 0), (3001, 128, 602, 12),
+                                           (2500, 256, 100, 6), (17, 128, 64, 0)])
+def test_h2p_gemm_gather(ctx, M, N, K, decades):
+    """NN v3 on the planar table (W slices in registers, whole rows by LDS DMA)."""
+    g = torch.Generator(device=DEV).manual_seed(M + K + N + 3)
+    V = M + M // 3 + 11
+    X = _table(V, K, g, decades)
+    rows = torch.randperm(V, device=DEV, generator=g)[:M].to(torch.int32)
+    rows[min(5, M - 1)] = 3
+    W = torch.randn(K, N, device=DEV, generator=g) * 0.05
+    Q, rs = ctx.h2_split_rows_planar(X)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.full((M, N), float("nan"), device=DEV)
+    ctx.gemm_gather(X, rows, W, C32)
+    ctx.gemm_h2p_gather(Q, rs, rows, W, Ch)
+    Xg = X[rows.long()].double()
+    ref = Xg @ W.double()
+    scale = Xg.abs() @ W.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ch).any()
+    _check(C32, Ch, ref, scale)
+    P, rs1 = ctx.h2_split_rows(X)
+    Ci = torch.empty_like(Ch)
+    ctx.gemm_h2_gather(P, rs1, rows, W, Ci)  # the interleaved kernel: same products, same sums
+    torch.cuda.synchronize()
+    assert torch.equal(Ch, Ci)
+
+
+@pytest.mark.parametrize("p", [0.5, 0.0])
+def test_h2p_relu_dropout_epilogue(ctx, p):
+    M, N, K = 20000, 128, 602
+    g = torch.Generator(device=DEV).manual_seed(99)
+    X = _table(M, K, g)
+    W = torch.randn(K, N, device=DEV, generator=g)
+    Q, rs = ctx.h2_split_rows_planar(X)
+    P, rs1 = ctx.h2_split_rows(X)
+    Ch = torch.empty(M, N, device=DEV)
+    Ci = torch.empty(M, N, device=DEV)
+    seed, offset = 0x1234_5678_9ABC, 77
+    ctx.gemm_h2p_gather(Q, rs, None, W, Ch, relu_dropout=True, p=p, seed=seed, offset=offset)
+    ctx.gemm_h2_gather(P, rs1, None, W, Ci, relu_dropout=True, p=p, seed=seed, offset=offset)
+    torch.cuda.synchronize()
+    assert torch.equal(Ch, Ci)
