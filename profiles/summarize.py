@@ -44,6 +44,10 @@ def profiler_kernel(name: str):
         return "gather_gemm_tn"                  # X[src]^T dH (no mask)
     if k == "k_s3_tn" and targs[1:] == ["false", "true"]:
         return "gather_gemm_tn"                  # split-bf16 X[src]^T dH
+    if k in ("k_h2_nn", "k_h2_nn2", "k_h2_nn3") and targs == ["false", "true"]:
+        return "gather_gemm"                     # f16 pair table X[src] W0
+    if k in ("k_h2_tn2", "k_h2_tn3", "k_h2_tn4"):
+        return "gather_gemm_tn"                  # f16 pair table X[src]^T dH
     return None
 
 
