@@ -315,7 +315,10 @@ def main():
             "host_train_issue_s_per_step": train_host_s / args.steps,
             "bottom_layer": "transform-first A(X W)" if tf else "aggregate-first (A X) W",
             "gemm": {"f32": "fp32-input MFMA",
-                     "split3": "fp32 split into 3 bf16 pieces, 6 products, fp32 accumulate"}[args.gemm],
+                     "split3": "fp32 split into 3 bf16 pieces, 6 products, fp32 accumulate"}[args.gemm]
+                    + ("; bottom layer: the feature table's f16 pair tables (two f16 pieces + "
+                       "power-of-two row scale, 3 f16 MFMA products, fp32 accumulate)"
+                       if tf and args.pair_table >= 1 else ""),
             "layer_sizes_top_down": layer_sizes,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
                              "workload": pmc_workload(args, layers, world)},
@@ -344,8 +347,9 @@ def workload_name(args, layers, V, En, tf) -> str:
     s = (f"{kind}-style {len(layers) - 1}-layer {model} {'-'.join(map(str, layers))}, fanout "
          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic (V={V}, E={En}); "
          f"GPU sampler (Philox{', pipelined' if not args.no_pipeline else ''}) + "
-         + ("transform-first bottom layer (row-gathered MFMA GEMM, aggregation + relu/dropout)"
-            if tf else "fused gather/aggregation")
+         + (("transform-first bottom layer (row-gathered "
+             + ("f16 pair-table" if args.pair_table >= 1 else "MFMA")
+             + " GEMMs, aggregation + relu/dropout)") if tf else "fused gather/aggregation")
          + " + " + ("torch" if args.no_hip_gemm else
                     {"f32": "fp32-input MFMA", "split3": "fp32-accurate split-bf16 MFMA"}[args.gemm])
          + " GEMMs + fused loss + fused Adam")
