@@ -200,6 +200,45 @@ __global__ __launch_bounds__(256) void k_h2_split_b(const float* __restrict__ B,
   *reinterpret_cast<f16x8*>(dst + kH2Frag) = p1;
 }
 
+// W's column maxima and its two-piece fragment image in one launch (the
+// NN kernels' per-step weight preparation: one k-step x 128 columns per
+// block; every block takes its columns' maxima over all K rows itself, block
+// (0, cb) also stores them for the epilogue's column scales)
+__global__ __launch_bounds__(512) void k_h2_prep_w(const float* __restrict__ B, uint64_t ldb, int K,
+                                                  int N, uint32_t* __restrict__ cmax,
+                                                  char* __restrict__ out) {
+  __shared__ float red[4][128];
+  __shared__ int sexp[128];
+  const int s = blockIdx.x, cb = blockIdx.y, ncb = gridDim.y, tid = threadIdx.x;
+  {
+    const int c = tid & 127, rl = tid >> 7, col = cb * 128 + c;
+    float m = 0.f;
+    if (col < N)
+      for (int k = rl; k < K; k += 4) m = fmaxf(m, fabsf(B[(uint64_t)k * ldb + col]));
+    red[rl][c] = m;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const float m = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+    sexp[tid] = h2_exp(m);
+    if (s == 0 && cb * 128 + tid < N) cmax[cb * 128 + tid] = __float_as_uint(m);
+  }
+  __syncthreads();
+  const int lane = tid & 63, ct = tid >> 6;
+  const int cl = ct * 16 + (lane & 15), col = cb * 128 + cl;
+  const int k0 = 32 * s + 8 * (lane >> 4);
+  const int e = sexp[cl];
+  uint32_t w[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    w[j] = (col < N && k0 + j < K) ? h2_pair(ldexpf(B[(uint64_t)(k0 + j) * ldb + col], e)) : 0u;
+  f16x8 p0, p1;
+  h2_unpack(w, p0, p1);
+  char* dst = out + ((size_t)s * ncb + cb) * kH2Img + ct * 2 * kH2Frag + 16 * lane;
+  *reinterpret_cast<f16x8*>(dst) = p0;
+  *reinterpret_cast<f16x8*>(dst + kH2Frag) = p1;
+}
+
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lds_addr_h(const void* p) {
   return (uint32_t)(uintptr_t)(lds_ptr_h)p;
@@ -1005,7 +1044,6 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn3(int M, int K, const
     for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
   }
   const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx, lsbr = (uint32_t)(uintptr_t)(lds_ptr_h)sbr;
-  const int cpr = pitch / 16;  // 16-byte chunks per LDS row
   const int row_chunks = 2 * plane_bytes / 16;
   // X(s): 5 x 1 KB pieces per wave per 16-row step (16 * pitch = 40 KB for Kp 608)
   const int xpieces = xstage / 1024 / 8;
@@ -1129,11 +1167,8 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
   float* const ssc = reinterpret_cast<float*>(sid + kchunk);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i = lane & 15, g = lane >> 4;
   const int nb = blockIdx.x % nnb, split = blockIdx.x / nnb;
   const int n0 = nb * 128;
-  const int T = (M + 15) / 16;
-  const int w_lo = wv * T / 8, w_hi = (wv + 1) * T / 8, ntile = w_hi - w_lo;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk), klast = kend - kbeg - 1;
   const int nsteps = (kend - kbeg + 15) / 16;
   for (int k = tid; k <= klast; k += kH2Tn3Threads) {
@@ -1180,7 +1215,6 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
     for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
   }
   const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx, lsbr = (uint32_t)(uintptr_t)(lds_ptr_h)sbr;
-  const int cpr = pitch / 16;  // 16-byte chunks per LDS row
   const int row_chunks = 2 * plane_bytes / 16;
   // X(s): 5 x 1 KB pieces per wave per 16-row step (16 * pitch = 40 KB for Kp 608)
   const int xpieces = xstage / 1024 / 8;
@@ -1482,10 +1516,7 @@ extern "C" int nts_hip_gemm_h2_gather(nts_hip_ctx* ctx, int relu_dropout, int M,
   NTS_RET(ensure_scratch(ctx, cm_bytes + img + 256));
   uint32_t* cmax = (uint32_t*)ctx->scratch;
   char* bimg = (char*)ctx->scratch + cm_bytes;
-  NTS_RET(colmax(ctx, W, ldw, (uint64_t)K, N, nullptr, nullptr, cmax));
-  const int total = nsteps * ncb * 512;
-  hipLaunchKernelGGL(k_h2_split_b, dim3((total + 255) / 256), dim3(256), 0, ctx->stream, W, ldw, K, N,
-                     total, ncb, cmax, bimg);
+  hipLaunchKernelGGL(k_h2_prep_w, dim3(nsteps, ncb), dim3(512), 0, ctx->stream, W, ldw, K, N, cmax, bimg);
   NTS_LAUNCH_CHECK();
   H2Extra ex;
   ex.keep_threshold = dropout_threshold(p);
@@ -1702,10 +1733,7 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   NTS_RET(ensure_scratch(ctx, cm_bytes + img + 256));
   uint32_t* cmax = (uint32_t*)ctx->scratch;
   char* bimg = (char*)ctx->scratch + cm_bytes;
-  NTS_RET(colmax(ctx, W, ldw, (uint64_t)K, N, nullptr, nullptr, cmax));
-  const int total = nsteps * ncb * 512;
-  hipLaunchKernelGGL(k_h2_split_b, dim3((total + 255) / 256), dim3(256), 0, ctx->stream, W, ldw, K, N,
-                     total, ncb, cmax, bimg);
+  hipLaunchKernelGGL(k_h2_prep_w, dim3(nsteps, ncb), dim3(512), 0, ctx->stream, W, ldw, K, N, cmax, bimg);
   NTS_LAUNCH_CHECK();
   H2Extra ex;
   ex.keep_threshold = dropout_threshold(p);
