@@ -178,7 +178,8 @@ template size_t scan_tmp_elems<uint64_t>(uint64_t);
 // 4096-item tiles.  Per pass: per-tile digit counts (digit-major), one
 // exclusive scan over them, then a scatter in which each wave ranks its 1,024
 // contiguous items against a running per-wave digit count in LDS (match-any by
-// ballots, no barrier inside the item loop) — three barriers per tile.
+// ballots, no barrier inside the item loop), the tile is reordered by digit in
+// LDS and written out in runs (coalesced stores).
 // Tiles past the device-side count n exit at once.
 // ============================================================================
 constexpr int kRadixThreads = 256;
@@ -216,6 +217,9 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     uint64_t n_cap, uint32_t shift, uint32_t dbits, const uint32_t* __restrict__ hist,
     uint32_t nb) {
   __shared__ uint32_t wh[kRadixThreads / kWave][kRadixMaxBins];  // per-wave counts -> offsets
+  __shared__ uint32_t gstart[kRadixMaxBins];  // digit d's global start for this tile
+  __shared__ uint32_t lstart[kRadixMaxBins];  // ... and its start in the tile's digit order
+  __shared__ uint32_t sk[kRadixTile], sv[kRadixTile];  // the tile in digit order
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
@@ -253,24 +257,61 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     if (valid && before == 0) wh[w][d] = prev + (uint32_t)__popcll(peers);
   }
   __syncthreads();
-  // digit d's slice of this tile starts at the scanned count; waves follow in order
+  // per digit: the waves' counts -> their offsets within the digit's slice
+  // (wh), the tile's count of the digit (lstart, scanned below) and its
+  // global start (gstart, from the scanned histogram)
   for (uint32_t d = t; d < bins; d += kRadixThreads) {
-    uint32_t run = hist[(uint64_t)d * nb + blockIdx.x];
+    uint32_t run = 0;
 #pragma unroll
     for (int ww = 0; ww < kRadixThreads / kWave; ++ww) {
       const uint32_t c = wh[ww][d];
       wh[ww][d] = run;
       run += c;
     }
+    lstart[d] = run;
+    gstart[d] = hist[(uint64_t)d * nb + blockIdx.x];
   }
   __syncthreads();
+  {  // exclusive scan of the tile's digit counts: thread t owns digits 2t, 2t + 1
+    __shared__ uint32_t wsum[kRadixThreads / kWave];
+    static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");
+    const uint32_t c0 = 2u * t < bins ? lstart[2 * t] : 0u;
+    const uint32_t c1 = 2u * t + 1 < bins ? lstart[2 * t + 1] : 0u;
+    uint32_t inc = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (lane == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+#pragma unroll
+    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) before += ww < w ? wsum[ww] : 0u;
+    const uint32_t ex = before + inc - (c0 + c1);
+    if (2u * t < bins) lstart[2 * t] = ex;
+    if (2u * t + 1 < bins) lstart[2 * t + 1] = ex + c0;
+  }
+  __syncthreads();
+  // the tile in digit order through LDS, then written out in index order:
+  // consecutive LDS slots of one digit go to consecutive global positions
+  // (coalesced runs instead of one scattered 4-byte store per item)
 #pragma unroll
   for (int k = 0; k < kRadixItems; ++k) {
     if (wbase + (uint64_t)k * kWave + lane < n) {
-      const uint32_t pos = wh[w][(key[k] >> shift) & mask] + rank[k];
-      keys_out[pos] = key[k];
-      vals_out[pos] = val[k];
+      const uint32_t d = (key[k] >> shift) & mask;
+      const uint32_t loc = lstart[d] + wh[w][d] + rank[k];
+      sk[loc] = key[k];
+      sv[loc] = val[k];
     }
+  }
+  __syncthreads();
+  const uint32_t cnt = (uint32_t)(n - base < (uint64_t)kRadixTile ? n - base : (uint64_t)kRadixTile);
+  for (uint32_t i = t; i < cnt; i += kRadixThreads) {
+    const uint32_t k = sk[i], d = (k >> shift) & mask;
+    const uint32_t pos = gstart[d] + (i - lstart[d]);
+    keys_out[pos] = k;
+    vals_out[pos] = sv[i];
   }
 }
 
