@@ -207,19 +207,37 @@ __global__ __launch_bounds__(256) void k_h2_split_b(const float* __restrict__ B,
 __global__ __launch_bounds__(512) void k_h2_prep_w(const float* __restrict__ B, uint64_t ldb, int K,
                                                   int N, uint32_t* __restrict__ cmax,
                                                   char* __restrict__ out) {
-  __shared__ float red[4][128];
+  __shared__ float red[16][128];
   __shared__ int sexp[128];
   const int s = blockIdx.x, cb = blockIdx.y, ncb = gridDim.y, tid = threadIdx.x;
-  {
-    const int c = tid & 127, rl = tid >> 7, col = cb * 128 + c;
-    float m = 0.f;
-    if (col < N)
-      for (int k = rl; k < K; k += 4) m = fmaxf(m, fabsf(B[(uint64_t)k * ldb + col]));
-    red[rl][c] = m;
+  {  // thread: 4 columns (one float4), rows rl + 16 j, four rows in flight
+    const int q = tid & 31, rl = tid >> 5, col = cb * 128 + 4 * q;
+    float m[4] = {0.f, 0.f, 0.f, 0.f};
+    if (col < N) {  // N % 16 == 0: the float4 is whole
+      for (int k = rl; k < K; k += 64) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = min(k + 16 * u, K - 1);  // a clamped duplicate does not change a max
+          v[u] = *reinterpret_cast<const float4*>(B + (uint64_t)kk * ldb + col);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          m[0] = fmaxf(m[0], fabsf(v[u].x));
+          m[1] = fmaxf(m[1], fabsf(v[u].y));
+          m[2] = fmaxf(m[2], fabsf(v[u].z));
+          m[3] = fmaxf(m[3], fabsf(v[u].w));
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[rl][4 * q + u] = m[u];
   }
   __syncthreads();
   if (tid < 128) {
-    const float m = fmaxf(fmaxf(red[0][tid], red[1][tid]), fmaxf(red[2][tid], red[3][tid]));
+    float m = 0.f;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) m = fmaxf(m, red[l][tid]);
     sexp[tid] = h2_exp(m);
     if (s == 0 && cb * 128 + tid < N) cmax[cb * 128 + tid] = __float_as_uint(m);
   }
@@ -1507,6 +1525,7 @@ extern "C" int nts_hip_gemm_h2_gather(nts_hip_ctx* ctx, int relu_dropout, int M,
   NTS_CHECK_ARG(M >= 0 && N > 0 && N % 16 == 0 && K > 0 && Kp >= K && Kp % 32 == 0, "shape");
   NTS_CHECK_ARG(ldp >= (uint64_t)Kp && ldp % 4 == 0 && (uintptr_t)P % 16 == 0, "pair table layout");
   NTS_CHECK_ARG(ldw >= (uint64_t)N && ldc >= (uint64_t)N, "ld");
+  NTS_CHECK_ARG(ldw % 4 == 0 && (uintptr_t)W % 16 == 0, "W rows must be float4-aligned");
   NTS_CHECK_ARG(M == 0 || (P && rs && W && C), "NULL buffer");
   NTS_CHECK_ARG(p >= 0.f && p < 1.f, "p must be in [0, 1)");
   if (M == 0) return NTS_OK;
@@ -1724,6 +1743,7 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
                     Kp <= 32 * kH2Nn3KS, "shape");
   NTS_CHECK_ARG(ldq >= 2 * (uint64_t)Kp && ldq % 8 == 0 && (uintptr_t)Q % 16 == 0, "planar table layout");
   NTS_CHECK_ARG(ldw >= (uint64_t)N && ldc >= (uint64_t)N, "ld");
+  NTS_CHECK_ARG(ldw % 4 == 0 && (uintptr_t)W % 16 == 0, "W rows must be float4-aligned");
   NTS_CHECK_ARG(M == 0 || (Q && rs && W && C), "NULL buffer");
   NTS_CHECK_ARG(p >= 0.f && p < 1.f, "p must be in [0, 1)");
   if (M == 0) return NTS_OK;
