@@ -130,7 +130,24 @@ def test_c2_reddit_shaped_full_batch(E):
                          v1, H, X1, p=0.0)
     ref_x1 = torch.relu(torch.from_numpy(Y0).to(DEV).double() @ W.double())
     torch.testing.assert_close(X1.double(), ref_x1, rtol=1e-4, atol=1e-4)
-    del fs, got, feat, y, H, X1, G
+    # the benched arithmetic: the same layer on the f16 pair table (planar), and
+    # its weight gradient X[src]^T dH, at full size (src ~229 K rows)
+    Q, rs = hip.h2_split_rows_planar(feat)
+    H2 = torch.empty_like(H)
+    hip.gemm_h2p_gather(Q, rs, l1["source"], W, H2)
+    X1b = torch.empty_like(X1)
+    hip.spmm_csc_fwd_act(l1["column_offset"], l1["row_indices"], l1["edge_weight_forward"], None,
+                         v1, H2, X1b, p=0.0)
+    torch.testing.assert_close(X1b.double(), ref_x1, rtol=1e-4, atol=1e-4)
+    gH = torch.randn(l1["src_size"], 128, device=DEV,
+                     generator=torch.Generator(device=DEV).manual_seed(2)) * 1e-4
+    dW = torch.full((F, 128), float("nan"), device=DEV)
+    hip.gemm_h2p_tn_gather(Q, rs, l1["source"], gH, dW, F)
+    Xs = feat[l1["source"].long()].double()
+    ref_dw = Xs.t() @ gH.double()
+    nerr = ((dW.double() - ref_dw).abs() / (Xs.abs().t() @ gH.double().abs() + 1e-300)).max().item()
+    assert nerr < 1e-6, nerr
+    del fs, got, feat, y, H, X1, G, Q, rs, H2, X1b, gH, dW, Xs, ref_dw
     _free()
 
 
