@@ -313,6 +313,15 @@ int nts_hip_spmm_csr_bwd_masked(nts_hip_ctx *ctx, const uint32_t *row_offset,
                                 const uint32_t *s, uint32_t s_cap, const float *g_out,
                                 uint64_t ld_gout, const float *x_act, uint64_t ld_act, float scale,
                                 uint32_t feature_size, float *g_in, uint64_t ld_gin);
+/* A graph-op backward whose result feeds that activation's backward:
+ *   G_in[s,:] = (sum_j w_b[j] * G_out[ci[j],:]) ⊙ [X_act[s,:] > 0] * scale
+ * — nts_hip_spmm_csr_bwd followed by nts_hip_act_backward on its output, in
+ * one pass, the same arithmetic (the mask is read once per output row). */
+int nts_hip_spmm_csr_bwd_postmask(nts_hip_ctx *ctx, const uint32_t *row_offset,
+                                  const uint32_t *column_indices, const float *weight_backward,
+                                  const uint32_t *s, uint32_t s_cap, const float *g_out,
+                                  uint64_t ld_gout, const float *x_act, uint64_t ld_act, float scale,
+                                  uint32_t feature_size, float *g_in, uint64_t ld_gin);
 /* The activation's backward alone: out = g ⊙ [x_act > 0] * scale ([rows x
  * feature_size], each with its leading dimension) — what libtorch's relu and
  * dropout backward compute for vertexForward (toolkits/GCN_SAMPLE_GPU.hpp:252-266),

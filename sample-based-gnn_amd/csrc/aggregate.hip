@@ -99,7 +99,10 @@ constexpr uint32_t kHostBit = 0x80000000u;
 //              nts_hip_gemm_relu_dropout_f32 (dropout_words(row, col, seed, offset))
 //   kAggMask:  y = A (x ⊙ [mx > 0] · scale) — that activation's backward fused
 //              into the row loads (mx = the forward activation, same shape as x)
-enum { kAggPlain = 0, kAggAct = 1, kAggMask = 2 };
+//   kAggPostMask: y = (A x) ⊙ [mx > 0] · scale with mx indexed by the OUTPUT
+//              row (the activation backward applied to the gathered sum: the
+//              graph-op backward feeding a transform-first bottom layer)
+enum { kAggPlain = 0, kAggAct = 1, kAggMask = 2, kAggPostMask = 3 };
 struct AggExtra {
   const float* mx = nullptr;
   uint64_t ldm = 0;
@@ -213,6 +216,21 @@ __device__ __forceinline__ void store_row(typename VT<VEC>::T (&acc)[NCH], uint3
           const uint32_t col = f0 + 2 * q2 + h;
           float& v = vcomp<VEC>(acc[c], 2 * q2 + h);
           v = (dropout_bits(wd, col) >= ax.keep_threshold && v > 0.f) ? v * ax.scale : 0.f;
+        }
+      }
+    }
+  }
+  if constexpr (MODE == kAggPostMask) {  // dZ = dX ⊙ [X > 0] · scale, X row d
+    const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)d * ax.ldm);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const uint32_t col = c0 + sl + c * LPD;
+      if (col < nv) {
+        const T m = mrow[col];
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          float& v = vcomp<VEC>(acc[c], q);
+          v = vcomp<VEC>(m, q) > 0.f ? v * ax.scale : 0.f;
         }
       }
     }
@@ -510,7 +528,7 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
                          Tier tier = Tier{nullptr, nullptr, 0, 0}, AggExtra ax = AggExtra()) {
   int vec = pick_vec(F, ldx, ldy, x, y);
   if (TIER) vec = std::min(vec, pick_vec(F, tier.ldh, ldx, tier.host, x));
-  if (MODE == kAggMask) vec = std::min(vec, pick_vec(F, ax.ldm, ldx, ax.mx, x));
+  if (MODE == kAggMask || MODE == kAggPostMask) vec = std::min(vec, pick_vec(F, ax.ldm, ldx, ax.mx, x));
   // rows padded to a 16-byte multiple (the 128-byte feature / output pitch):
   // float4 loads, the partial last vector reads pitch padding and stores only
   // its valid floats
@@ -618,6 +636,26 @@ int nts_hip_spmm_csr_bwd_masked(nts_hip_ctx* ctx, const uint32_t* row_offset,
                                                weight_backward, s, s_cap, g_out, ld_gout, nullptr,
                                                feature_size, g_in, ld_gin,
                                                Tier{nullptr, nullptr, 0, 0}, ax);
+}
+
+int nts_hip_spmm_csr_bwd_postmask(nts_hip_ctx* ctx, const uint32_t* row_offset,
+                                  const uint32_t* column_indices, const float* weight_backward,
+                                  const uint32_t* s, uint32_t s_cap, const float* g_out,
+                                  uint64_t ld_gout, const float* x_act, uint64_t ld_act, float scale,
+                                  uint32_t feature_size, float* g_in, uint64_t ld_gin) {
+  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && x_act && g_in, "NULL argument");
+  NTS_CHECK_ARG(ld_gout >= feature_size && ld_act >= feature_size && ld_gin >= feature_size,
+                "leading dimension < feature_size");
+  if (s_cap == 0 || feature_size == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  AggExtra ax;
+  ax.mx = x_act;
+  ax.ldm = ld_act;
+  ax.scale = scale;
+  return launch_gather<false, false, kAggPostMask, true>(ctx->stream, row_offset, column_indices,
+                                                         weight_backward, s, s_cap, g_out, ld_gout,
+                                                         nullptr, feature_size, g_in, ld_gin,
+                                                         Tier{nullptr, nullptr, 0, 0}, ax);
 }
 
 int nts_hip_spmm_csc_bwd_atomic(nts_hip_ctx* ctx, const uint32_t* column_offset,

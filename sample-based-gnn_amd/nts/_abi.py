@@ -49,6 +49,7 @@ EXPORTED = (
     "nts_hip_stage_uncached_rows", "nts_hip_gat_forward", "nts_hip_gat_backward",
     "nts_hip_h2_split_rows", "nts_hip_gemm_h2_gather", "nts_hip_gemm_h2_tn_gather",
     "nts_hip_h2_split_rows_planar", "nts_hip_gemm_h2p_tn_gather", "nts_hip_gemm_h2p_gather",
+    "nts_hip_spmm_csr_bwd_postmask",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -111,6 +112,7 @@ def lib() -> C.CDLL:
         "nts_hip_spmm_csc_fwd": ([P, P, P, P, P, U32, P, U64, P, U32, P, U64], I),
         "nts_hip_spmm_csc_fwd_act": ([P, P, P, P, P, U32, P, U64, U32, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd_masked": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
+        "nts_hip_spmm_csr_bwd_postmask": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
         "nts_hip_act_backward": ([P, U32, U32, P, U64, P, U64, F, P, U64], I),
         "nts_hip_presample_counts": ([P, C.POINTER(GraphDev), P, U32, I, P, P], I),
         "nts_hip_presample_select": ([P, P, U64, F, P, P], I),

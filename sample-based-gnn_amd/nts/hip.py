@@ -146,6 +146,14 @@ class HipContext:
                                                 ptr(x), x.stride(0), F, ptr(y), y.stride(0),
                                                 float(p), int(seed), int(offset)))
 
+    def spmm_csr_bwd_postmask(self, ro, ci, wb, s_dev, s_cap, g_out, x_act, g_in, scale=1.0):
+        """g_in = (A^T g_out) ⊙ (x_act > 0) * scale, x_act indexed by g_in's rows."""
+        F = g_out.shape[1]
+        check(self.lib.nts_hip_spmm_csr_bwd_postmask(self.h, ptr(ro), ptr(ci), ptr(wb), ptr(s_dev),
+                                                     s_cap, ptr(g_out), g_out.stride(0), ptr(x_act),
+                                                     x_act.stride(0), float(scale), F, ptr(g_in),
+                                                     g_in.stride(0)))
+
     def spmm_csr_bwd_masked(self, ro, ci, wb, s_dev, s_cap, g_out, x_act, g_in, scale=1.0):
         """g_in = A^T (g_out * (x_act > 0) * scale) over the CSR."""
         F = g_out.shape[1]

@@ -506,12 +506,21 @@ NtsVar SingleGPUAllSampleGraphOp::backward(NtsVar& g) {
   TORCH_CHECK(go.size(0) == (int64_t)sg->v_size, "output grad rows != v_size");
   if (sg->has_csr) {
     NtsVar gi = torch::empty({(int64_t)sg->src_size, F}, f32_opts(cuda_stream->device()));
-    hip_check(nts_hip_spmm_csr_bwd(cuda_stream->ctx(), sg->dev_r_o(), sg->dev_c_i(),
-                                   sg->dev_e_w_b(), nullptr, sg->src_size, go.data_ptr<float>(),
-                                   (uint64_t)F, (uint32_t)F, gi.data_ptr<float>(), (uint64_t)F),
-              "nts_hip_spmm_csr_bwd");
+    if (sg->post_mask)  // the transform-first bottom layer's activation backward fused
+      hip_check(nts_hip_spmm_csr_bwd_postmask(cuda_stream->ctx(), sg->dev_r_o(), sg->dev_c_i(),
+                                              sg->dev_e_w_b(), nullptr, sg->src_size,
+                                              go.data_ptr<float>(), (uint64_t)F, sg->post_mask,
+                                              sg->post_mask_ld, sg->post_mask_scale, (uint32_t)F,
+                                              gi.data_ptr<float>(), (uint64_t)F),
+                "nts_hip_spmm_csr_bwd_postmask");
+    else
+      hip_check(nts_hip_spmm_csr_bwd(cuda_stream->ctx(), sg->dev_r_o(), sg->dev_c_i(),
+                                     sg->dev_e_w_b(), nullptr, sg->src_size, go.data_ptr<float>(),
+                                     (uint64_t)F, (uint32_t)F, gi.data_ptr<float>(), (uint64_t)F),
+                "nts_hip_spmm_csr_bwd");
     return gi;
   }
+  TORCH_CHECK(!sg->post_mask, "a fused activation backward needs the CSR backward");
   NtsVar gi = torch::zeros({(int64_t)sg->src_size, F}, f32_opts(cuda_stream->device()));
   hip_check(nts_hip_spmm_csc_bwd_atomic(cuda_stream->ctx(), sg->dev_c_o(), sg->dev_r_i(),
                                         sg->dev_e_w_f(), nullptr, sg->v_size, go.data_ptr<float>(),
@@ -802,7 +811,7 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     // nts_hip_spmm_csr_bwd_masked reads two rows per edge); NTS_TF_MASKED_BWD=1
     // selects the fused form
     static const bool fused_mask = getenv("NTS_TF_MASKED_BWD") != nullptr;
-    if (fused_mask) {
+    if (fused_mask && !sg->grad_premasked) {
       if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
       hip_check(nts_hip_spmm_csr_bwd_masked(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(),
                                             sg->dev_e_w_b(), nullptr, (uint32_t)s,
@@ -814,11 +823,13 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
         prof->end(KernelProfiler::BOTTOM_BWD, st,
                   8.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
     } else {
-      NtsVar dZ = torch::empty({std::max<int64_t>(v, 1), N}, f32_opts(dev));
-      hip_check(nts_hip_act_backward(cs->ctx(), (uint32_t)v, (uint32_t)N, g.data_ptr<float>(),
-                                     (uint64_t)N, X1.data_ptr<float>(), (uint64_t)N, scale,
-                                     dZ.data_ptr<float>(), (uint64_t)N),
-                "nts_hip_act_backward");
+      // the graph op above applied the activation backward already (post_mask)
+      NtsVar dZ = sg->grad_premasked ? g : torch::empty({std::max<int64_t>(v, 1), N}, f32_opts(dev));
+      if (!sg->grad_premasked)
+        hip_check(nts_hip_act_backward(cs->ctx(), (uint32_t)v, (uint32_t)N, g.data_ptr<float>(),
+                                       (uint64_t)N, X1.data_ptr<float>(), (uint64_t)N, scale,
+                                       dZ.data_ptr<float>(), (uint64_t)N),
+                  "nts_hip_act_backward");
       if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
       hip_check(nts_hip_spmm_csr_bwd(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(),
                                      nullptr, (uint32_t)s, dZ.data_ptr<float>(), (uint64_t)N,

@@ -352,6 +352,19 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
                                         keep ? h.data_ptr<float>() : nullptr, pairs_.get());
           },
           F);
+      // training: the graph op above applies this layer's relu/dropout
+      // backward to its own backward output (one CSR pass instead of the CSR
+      // gather + nts_hip_act_backward; same arithmetic); NTS_TF_MASKED_BWD=1
+      // keeps the unfused masked gather for A/B
+      static const bool masked_env = getenv("NTS_TF_MASKED_BWD") != nullptr;
+      const bool fuse = ctx.is_train() && !masked_env && hop >= 1;
+      if (hop >= 1) {
+        sampCSC* up = sg->sampled_sgs[hop - 1];
+        up->post_mask = fuse ? X.data_ptr<float>() : nullptr;
+        up->post_mask_ld = (uint64_t)X.stride(0);
+        up->post_mask_scale = p < 1.0 ? 1.0f / (1.0f - (float)p) : 0.f;
+      }
+      s->grad_premasked = fuse;
       if (keep) {
         acts.push_back(h.narrow(0, 0, (int64_t)s->src_size));
         acts.push_back(X.detach());

@@ -123,6 +123,14 @@ class sampCSC {
   torch::Tensor dst_local_id, csr_edge_id;
   // PD cache (sampled with an omit map): per dst its cache row or NTS_NOT_CACHED
   torch::Tensor omit_row;
+  // transform-first training: this layer's graph-op backward also applies the
+  // bottom layer's relu/dropout backward to its output (rows of post_mask =
+  // the bottom activation X1, > 0 kept, times post_mask_scale), and the
+  // bottom layer then receives dZ instead of dX1 (grad_premasked on it)
+  const float* post_mask = nullptr;
+  uint64_t post_mask_ld = 0;
+  float post_mask_scale = 1.f;
+  bool grad_premasked = false;
 
   sampCSC(int device, VertexId v_cap, VertexId e_cap, VertexId s_cap, bool csr, bool weights);
   void set_merge_src_dst();  // core/coocsc.hpp:405-411

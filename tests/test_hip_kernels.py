@@ -453,6 +453,32 @@ def test_spmm_csr_bwd_masked(hip, cora, F):
     assert torch.isnan(gin[s:]).all()
 
 
+@pytest.mark.parametrize("F", [1, 41, 128, 602])
+def test_spmm_csr_bwd_postmask(hip, cora, F):
+    """The graph-op backward with the next layer's activation backward fused on
+    its output rows == the CSR backward followed by act_backward, bit for bit."""
+    V, src, dst = cora
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    l0, _ = o.sample(np.arange(4, V, 11, dtype=np.uint32))
+    rng = np.random.default_rng(F + 3)
+    v, s = l0["v_size"], l0["src_size"]
+    G = _t(rng.standard_normal((v, F)).astype(np.float32))
+    Xa = _t((np.maximum(rng.standard_normal((s, F)), 0) * 2).astype(np.float32))
+    sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
+    ro, ci, wb = _t(l0["row_offset"]), _t(l0["column_indices"]), _t(l0["edge_weight_backward"])
+    plain = torch.empty(s, F, device=DEV)
+    hip.spmm_csr_bwd(ro, ci, wb, sdev, s, G, plain)
+    ref = torch.empty(s, F, device=DEV)
+    hip.act_backward(plain, Xa, ref, scale=2.0)
+    got = torch.full((s + 2, F), float("nan"), device=DEV)
+    hip.spmm_csr_bwd_postmask(ro, ci, wb, sdev, s + 2, G, Xa, got, scale=2.0)
+    torch.cuda.synchronize()
+    assert torch.equal(got[:s], ref)
+    assert torch.isnan(got[s:]).all()
+
+
 @pytest.mark.parametrize("M,N,K", [(3000, 128, 602), (2500, 64, 100), (500, 41, 100), (37, 7, 13)])
 def test_gemm_gather_rows(hip, M, N, K):
     """C = table[rows] @ W with the rows gathered inside the GEMM: bit-identical
