@@ -98,8 +98,12 @@ __global__ void k_count(const uint64_t* __restrict__ goff, const uint32_t* __res
   }
 }
 
-__global__ void k_finish_count(const uint32_t* co, uint32_t e_cap, uint32_t* sizes) {
-  uint32_t e = co[sizes[0]];
+// e_size = co[v] (clamped to e_cap, overflow flagged): done by the first
+// thread of the selection kernel, which runs after the scan of co — one
+// dependent launch less per layer than a kernel of its own.
+__device__ __forceinline__ void finish_count(const uint32_t* co, uint32_t e_cap, uint32_t* sizes) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const uint32_t e = co[sizes[0]];
   sizes[1] = min(e, e_cap);
   if (e > e_cap) sizes[3] = 1u;
 }
@@ -109,7 +113,7 @@ struct SelectArgs {
   const uint32_t* grows;
   const uint32_t* dst;
   const uint32_t* co;
-  const uint32_t* sizes;
+  uint32_t* sizes;  // reads [0]; the first thread writes [1] and the overflow flag
   uint32_t* ans;
   uint32_t* edst;
   uint8_t* marks;
@@ -187,6 +191,7 @@ __device__ __forceinline__ uint32_t select_distinct(const SelectArgs& a, uint32_
 __global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
   __shared__ uint32_t sets[kSelWaves][kSetCap];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  finish_count(a.co, a.e_cap, a.sizes);
   const uint32_t v = a.sizes[0];
   uint32_t* set = sets[w];
   const uint32_t nw = gridDim.x * kSelWaves;
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
     const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
     const uint32_t c = a.co[i];
     const uint32_t n = a.co[i + 1] - c;
-    if (c + n > a.e_cap) continue;  // capacity overflow (flagged in k_finish_count)
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by finish_count)
     if (n == deg) {
       copy_all(a, i, beg, deg, c, lane);
     } else if (n > 0) {
@@ -228,6 +233,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a)
   uint32_t* set = sets[gib];
   const uint32_t gshift = kGrp * grp;
   const uint32_t lt16 = (1u << gl) - 1u;
+  finish_count(a.co, a.e_cap, a.sizes);
   const uint32_t v = a.sizes[0];
   const uint32_t ng = gridDim.x * kSelWaves * kGrpPerWave;
   for (uint32_t i = blockIdx.x * kSelWaves * kGrpPerWave + gib; i < v; i += ng) {
@@ -236,7 +242,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a)
     const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
     const uint32_t c = a.co[i];
     const uint32_t n = a.co[i + 1] - c;
-    if (c + n > a.e_cap) continue;  // capacity overflow (flagged in k_finish_count)
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by finish_count)
     if (n == deg) {
       for (uint32_t k = gl; k < deg; k += kGrp) {
         const uint32_t g = a.grows[beg + k];
@@ -322,6 +328,7 @@ __global__ __launch_bounds__(kWave) void k_select_mt(SelectArgs a, uint32_t* mt_
   __shared__ uint32_t blk[2][624];
   __shared__ uint32_t set[kSetCap];
   const int lane = threadIdx.x;
+  finish_count(a.co, a.e_cap, a.sizes);
   for (int k = lane; k < 624; k += kWave) blk[0][k] = mt_state[k];
   uint32_t q0 = mt_state[624];
   int cur = 0;
@@ -665,16 +672,13 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
 
-  // 1) per-dst counts -> column_offset, e_size
+  // 1) per-dst counts -> column_offset (e_size: the selection's first thread)
   hipLaunchKernelGGL(k_count, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
                      o->v_size, o->v_cap, fanout, o->column_offset, o->sizes, o->omit_map,
                      o->omit_key, o->omit_loc, o->omit_row);
   NTS_LAUNCH_CHECK();
   NTS_RET(scan_exclusive<uint32_t>(o->column_offset, o->column_offset, o->sizes, o->v_cap,
                                    t_scan_co, st));
-  hipLaunchKernelGGL(k_finish_count, dim3(1), dim3(1), 0, st, o->column_offset, o->e_cap,
-                     o->sizes);
-  NTS_LAUNCH_CHECK();
 
   // 2) selection (marks the frontier; the byte map is all zeros here: it is
   // zeroed when allocated and k_mark_write clears what each layer set)
