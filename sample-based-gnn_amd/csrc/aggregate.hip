@@ -288,9 +288,30 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
       T acc[NCH];
 #pragma unroll
       for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
+      // kAggPostMask: the output row's mask is known before the edges are —
+      // load it first, so its latency overlaps the gather instead of following it
+      T pm[MODE == kAggPostMask ? NCH : 1];
+      if constexpr (MODE == kAggPostMask) {
+        const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)d * ax.ldm);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          const uint32_t col = c0 + sl + c * LPD;
+          pm[c] = col < nv ? mrow[col] : V::zero();
+        }
+      }
       gather_edges<VEC, LPD, NCH, MAP, U, TIER, MODE>(acc, beg, end, c0, sl, idx, w, x, ldx, map,
                                                       nv, tier, ax);
-      store_row<VEC, LPD, NCH, MODE>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
+      if constexpr (MODE == kAggPostMask) {  // same arithmetic as store_row's
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            float& v = vcomp<VEC>(acc[c], q);
+            v = vcomp<VEC>(pm[c], q) > 0.f ? v * ax.scale : 0.f;
+          }
+      }
+      store_row<VEC, LPD, NCH, MODE == kAggPostMask ? kAggPlain : MODE>(acc, d, c0, sl, nv,
+                                                                        last_valid, y, ldy, ax);
     }
   }
   if constexpr (COOP) {
