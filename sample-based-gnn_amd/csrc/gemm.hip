@@ -850,12 +850,64 @@ __global__ __launch_bounds__(256) void k_sum_splits_tree(const float* __restrict
   }
 }
 
+// Many splits (the row-split weight-gradient GEMMs: 256 slabs): wave w of a
+// 16-wave block sums splits w, w + 16, ... of 64 consecutive float4 elements
+// (one lane each: every load a coalesced 1 KB row piece of one slab, 8 in
+// flight), then wave 0 adds the 16 wave sums in wave order through LDS.
+// Deterministic (a fixed order per split count).
+constexpr int kSsWaves = 16;
+__global__ __launch_bounds__(kSsWaves * 64) void k_sum_splits_rows(const float4* __restrict__ part,
+                                                                   int splits, uint64_t st4,
+                                                                   uint64_t total, int N4,
+                                                                   float* __restrict__ C,
+                                                                   uint64_t ldc) {
+  constexpr int B = 8;
+  __shared__ float4 red[kSsWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t e = (uint64_t)blockIdx.x * 64 + lane;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e < total) {
+    for (int z = w; z < splits; z += B * kSsWaves) {
+      float4 v[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+        v[u] = z + kSsWaves * u < splits ? part[(uint64_t)(z + kSsWaves * u) * st4 + e]
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int u = 0; u < B; ++u)
+        if (z + kSsWaves * u < splits) {
+          acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+        }
+    }
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && e < total) {
+    float4 r = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < kSsWaves; ++k) {
+      const float4 q = red[k][lane];
+      r.x += q.x; r.y += q.y; r.z += q.z; r.w += q.w;
+    }
+    const uint64_t row = e / N4, col = (e % N4) * 4;
+    *reinterpret_cast<float4*>(C + row * ldc + col) = r;
+  }
+}
+
 // Sum `splits` partial slabs (stride floats apart, ld N) into C.
 int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, int M, int N,
                float* C, uint64_t ldc) {
   const bool v4 = N % 4 == 0 && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
   const bool wide = splits > 256;  // 64 lanes per element, else 16
   const uint64_t elems = stride / (v4 ? 4 : 1);
+  if (v4 && splits >= 64 && stride % 4 == 0 && (uintptr_t)part % 16 == 0) {
+    const uint64_t total = (uint64_t)M * N / 4;
+    hipLaunchKernelGGL(k_sum_splits_rows, dim3(std::max(1u, ceil_div(total, 64))),
+                       dim3(kSsWaves * 64), 0, st, reinterpret_cast<const float4*>(part), splits,
+                       stride / 4, total, N / 4, C, ldc);
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   const uint32_t g = std::max(1u, ceil_div(elems, wide ? 4 : 16));
 #define NTS_SS(V, T)                                                                         \
   hipLaunchKernelGGL((k_sum_splits_tree<V, T>), dim3(g), dim3(256), 0, st, part, splits, stride, \
