@@ -221,6 +221,20 @@ void GCN_SAMPLE_ALLGPU_impl::issue(int slot, NtsStream& st) {
   sampler->issue_gpu_sample(cfg.batch_size, slot, st,
                             cfg.gat ? WeightType::None : cfg.weight_type);
   sampler->omit_map = nullptr;
+  {  // load_label_gpu for this batch, on the sampling stream next to its
+     // subgraph (off the training stream; ordered by ready_[slot] below)
+    SampledSubgraph* q = sampler->ssgs[slot];
+    const int64_t n = q->pending_batch;
+    NtsVar& t = lbl_[slot];
+    if (!t.defined() || t.size(0) < n)
+      t = torch::empty({std::max<int64_t>(n, cfg.batch_size)},
+                       torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, graph->device));
+    if (n > 0)
+      hip_check(nts_hip_gather_labels(st.ctx(), L_GT.data_ptr<int64_t>(),
+                                      q->sampled_sgs[0]->dev_dst(), nullptr, (uint32_t)n,
+                                      t.data_ptr<int64_t>()),
+                "nts_hip_gather_labels");
+  }
   if (early_) {
     auto guard = st.guard();
     const int L = (int)P.size();
@@ -557,7 +571,7 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   double t1 = now_s();
   if (cfg.pd_cache) pd_train(slot);
   mark("T<", *cs);
-  sampler->load_label_gpu(*cs, sg, target, L_GT);
+  target = lbl_[slot].narrow(0, 0, (int64_t)sg->sampled_sgs[0]->v_size);
   ctx.train();
   if (early_ && cfg.profile) prof.add_units(KernelProfiler::BOTTOM_AGG, bottom_bytes(sg, true));
   const int L = (int)P.size();

@@ -183,6 +183,7 @@ class GCN_SAMPLE_ALLGPU_impl {
   static constexpr int kSlots = 3;  // sampler slots when pipelined (see the constructor)
   int nslots_ = 1;
   NtsVar pre_y_[kSlots];
+  NtsVar lbl_[kSlots];  // each slot's batch labels, gathered on the sampling stream
   NtsVar stage_[kSlots];  // early aggregation + feature cache: staged spill rows
   hipEvent_t ready_[kSlots] = {nullptr, nullptr, nullptr};
   bool early_ = false;
