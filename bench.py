@@ -45,11 +45,44 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_quota():
+    """CPUs this job may use by its cgroup's CFS quota (v2 cpu.max, v1
+    cfs_quota_us / cfs_period_us); None when there is no quota."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_share() -> dict:
+    """The inputs of the CPU-baseline thread rule, recorded in the bench line."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_quota": cpu_quota(),
+            "omp_num_threads": int(omp) if omp and omp.isdigit() else None}
+
+
 def default_cpu_threads() -> int:
-    """The reference's sampler uses nproc-1 threads (core/FullyRepGraph.hpp:49);
-    capped by the CPU share this job has (OMP_NUM_THREADS, 16 on the GPU box)."""
-    share = int(os.environ.get("OMP_NUM_THREADS") or 16)
-    return max(1, min((os.cpu_count() or 2) - 1, share))
+    """The reference's sampler uses nproc-1 threads (core/FullyRepGraph.hpp:49),
+    capped by what this job may use: the affinity mask, the cgroup CPU quota
+    and the job's declared CPU share (OMP_NUM_THREADS; 16 per GPU on the GPU
+    box, where nproc shows the whole machine)."""
+    s = cpu_share()
+    n = (s["nproc"] or 2) - 1
+    for cap in (s["affinity_cpus"], s["cpu_quota"], s["omp_num_threads"]):
+        if cap:
+            n = min(n, max(1, int(cap)))
+    return max(1, n)
 
 
 def parse():
@@ -116,7 +149,14 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=default_cpu_threads())
     p.add_argument("--scale", type=float, default=1.0)
+    p.add_argument("--rng", default="philox", choices=["philox", "mt", "mt-div"],
+                   help="sampler stream: philox (per-dst counter streams, parallel) or mt: the "
+                        "reference's single std::mt19937(2000) stream + uniform_int_distribution "
+                        "(Lemire, libstdc++ 11; mt-div: libstdc++ <= 10), replayed bit-exactly")
     return p.parse_args()
+
+
+RNG_MODES = {"philox": 0, "mt": 1, "mt-div": 2}
 
 
 def metric_name(args, layers) -> str:
@@ -185,7 +225,7 @@ def main():
         raise SystemExit(f"--layers must start at the feature width {F_dim} and have one more "
                          f"entry than --fanout")
     cfg = host.gcn_config(layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4,
-                          drop_rate=0.5, rng_mode=_abi.NTS_RNG_PHILOX, weight=args.weight,
+                          drop_rate=0.5, rng_mode=RNG_MODES[args.rng], weight=args.weight,
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
                           transform_first=args.transform_first, early_aggregate=args.early_agg,
@@ -280,7 +320,7 @@ def main():
         csr = [not args.atomic_backward] * (L - 1) + [tf]
         wt = {"sum": E.WeightType.Sum, "mean": E.WeightType.Mean,
               "mean-sampled": E.WeightType.MeanSampled}[args.weight]
-        r = E.sampler_throughput(G, train, args.batch, fan, wt, _abi.NTS_RNG_PHILOX,
+        r = E.sampler_throughput(G, train, args.batch, fan, wt, RNG_MODES[args.rng],
                                  args.sampler_batches, csr)
         sampler_only = {"value": sum_over_ranks(r["edges"]) / max_over_ranks(r["seconds"]),
                         "unit": "sampled-edges/s", "batches_per_gpu": int(r["batches"]),
@@ -346,7 +386,7 @@ def workload_name(args, layers, V, En, tf) -> str:
                  "mean-sampled": "GraphSAGE (mean by sampled count, GPU kernel formula)"}[args.weight]
     s = (f"{kind}-style {len(layers) - 1}-layer {model} {'-'.join(map(str, layers))}, fanout "
          f"{args.fanout}, batch {args.batch}/GPU, {args.shape}-shaped synthetic (V={V}, E={En}); "
-         f"GPU sampler (Philox{', pipelined' if not args.no_pipeline else ''}) + "
+         f"GPU sampler ({RNG_NAMES[args.rng]}{', pipelined' if not args.no_pipeline else ''}) + "
          + (("transform-first bottom layer (row-gathered "
              + ("f16 pair-table" if args.pair_table >= 1 else "MFMA")
              + " GEMMs, aggregation + relu/dropout)") if tf else "fused gather/aggregation")
@@ -360,6 +400,10 @@ def workload_name(args, layers, V, En, tf) -> str:
         s += (f"; NeutronOrch PD cache (GS_SAMPLE_PD_CACHE): {args.pd_rate:.0%} hot vertices per "
               f"super-batch of {args.pd_super_batch} batches, their bottom layer shared")
     return s
+
+
+RNG_NAMES = {"philox": "Philox", "mt": "MT19937 reference stream, Lemire",
+             "mt-div": "MT19937 reference stream, DIV"}
 
 
 def roofline(prof: dict, args, layers, world) -> dict:
@@ -419,7 +463,8 @@ def roofline(prof: dict, args, layers, world) -> dict:
 def pmc_workload(args, layers, world) -> str:
     return (f"{args.shape}/{args.batch}/{args.fanout}/{'-'.join(map(str, layers))}/{args.weight}/"
             f"w{world}/tf{args.transform_first}/{args.model}/c{args.cache_rate}/{args.gemm}"
-            + (f"/pd{args.pd_rate}x{args.pd_super_batch}" if args.pd_cache else ""))
+            + (f"/pd{args.pd_rate}x{args.pd_super_batch}" if args.pd_cache else "")
+            + (f"/rng-{args.rng}" if args.rng != "philox" else ""))
 
 
 def attach_pmc(rl, dom, args, layers, world):
@@ -462,11 +507,7 @@ def cpu_info() -> dict:
                 break
     except OSError:
         pass
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except Exception:
-        aff = None
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+    return {**cpu_share(), "cpu_model": model}
 
 
 def cpu_baseline(args, G, feat, labels, train, fan, layers, V):
@@ -557,7 +598,9 @@ def cpu_baseline(args, G, feat, labels, train, fan, layers, V):
         "epoch_time_s": t_all / steps * n_batches,
         "epoch_time_kind": ("measured: one full epoch" if steps == n_batches
                             else f"estimate: per-step time of {steps} steps x {n_batches} batches"),
-        "threads_rule": "min(nproc - 1 (reference default), this job's CPU share)",
+        "threads_rule": ("min(nproc - 1 (the reference's default, core/FullyRepGraph.hpp:49), "
+                         "affinity_cpus, cpu_quota (cgroup CFS), omp_num_threads (the job's "
+                         "declared CPU share)); --cpu-threads overrides"),
         **cpu_info(),
     }
     if args.cpu_o0_steps > 0:

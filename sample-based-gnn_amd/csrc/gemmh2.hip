@@ -1765,10 +1765,14 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   ex.cmax = cmax;
   const int pitch = (4 * Kp + 511) / 512 * 512;
   const int T = (M + 15) / 16;
-  const int gx = std::max(1, std::min(256 / ncb, T));
+  // one block per CU; past the row-id stage's LDS room (8 B per row) more
+  // blocks, each with fewer tiles (large bottom frontiers, e.g. C5)
+  const int tile_cap = (160 * 1024 - 3 * 16 * pitch) / (2 * 4 * 16);
+  NTS_CHECK_ARG(tile_cap >= 1, "row pitch too large for the NN stage");
+  const int gx = std::max({1, std::min(256 / ncb, T), (T + tile_cap - 1) / tile_cap});
   const int max_tiles = (T + gx - 1) / gx;
   const int lds = 3 * 16 * pitch + 2 * 4 * 16 * max_tiles;
-  NTS_CHECK_ARG(lds <= 160 * 1024, "too many rows for the row-id stage (use nts_hip_gemm_h2_gather)");
+  NTS_CHECK_ARG(lds <= 160 * 1024, "row-id stage");
   const dim3 grid(gx, ncb);
 #define NTS_H2NN3(E, MP)                                                                          \
   do {                                                                                            \

@@ -86,7 +86,7 @@ std::vector<size_t> line_cuts(const char* p, size_t n, int parts) {
   std::vector<size_t> cut(parts + 1, n);
   cut[0] = 0;
   for (int i = 1; i < parts; ++i) {
-    size_t o = n / parts * i;
+    size_t o = std::min(std::max<size_t>(n / parts * i, 1), n);  // p[o - 1] stays in the text
     while (o < n && p[o - 1] != '\n') ++o;
     cut[i] = std::max(o, cut[i - 1]);
   }

@@ -320,98 +320,357 @@ __device__ __forceinline__ void mt_twist(const uint32_t* cur, uint32_t* nxt, int
   }
 }
 
-// One wave replays the reference's sequential generator over all dsts in order.
-// blk[cur] is the current 624-word block (std::mt19937::_M_x) and q0 the read
-// position in it (_M_p); blk[cur^1] is the next block, twisted on demand.
-__global__ __launch_bounds__(kWave) void k_select_mt(SelectArgs a, uint32_t* mt_state,
-                                                     int lemire) {
-  __shared__ uint32_t blk[2][624];
-  __shared__ uint32_t set[kSetCap];
-  const int lane = threadIdx.x;
-  finish_count(a.co, a.e_cap, a.sizes);
-  for (int k = lane; k < 624; k += kWave) blk[0][k] = mt_state[k];
-  uint32_t q0 = mt_state[624];
-  int cur = 0;
-  bool have_next = false;
-  __syncthreads();
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint32_t v = a.sizes[0];
-  for (uint32_t i = 0; i < v; ++i) {
-    const uint32_t d = a.dst[i];
-    const uint64_t beg = a.goff[d];
-    const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
-    const uint32_t c = a.co[i];
-    const uint32_t n = a.co[i + 1] - c;
-    if (c + n > a.e_cap) continue;
-    if (n == deg) {  // deg <= fanout: no draws (core/ntsFastSampler.hpp:1040-1048)
-      copy_all(a, i, beg, deg, c, lane);
-      continue;
-    }
-    if (n == 0) continue;
-    Draw dr;
-    dr.init(deg, lemire != 0);
-    uint32_t count = 0;
-    while (count < n) {
-      if (q0 + kWave > 624 && !have_next) {
-        mt_twist(blk[cur], blk[cur ^ 1], lane);
-        have_next = true;
-      }
-      if (q0 >= 624) {  // window slides: next block becomes current
+// The reference draws from ONE sequential generator (random_uniform_int,
+// core/ntsFastSampler.hpp:200-205) over the dsts in order, and a dst's word
+// count is data dependent (rejections, repeated positions), so the stream
+// positions form a serial chain.  Two kernels split the work:
+//   k_mt_prep    (parallel) per-dst {c, n, deg, thr}: n = 0 for dsts that draw
+//                nothing (copy path, omitted, overflow);
+//   k_mt_serial  (ONE wave) resolves only the chain: which stream words each
+//                dst consumes, and the positions it keeps (written into `ans`);
+//   k_mt_rows    (parallel) positions -> row ids, edge dsts, frontier marks.
+// k_mt_serial speculates: the wave is cut into K = 64/G groups of G lanes and
+// evaluates K consecutive dsts at once, dst k at the stream position it would
+// start at if every dst before it consumed exactly n words (no rejection, no
+// repeat).  Within a group the first n distinct accepted draws are found in
+// one shot: each accepted lane stores a sentinel, then ds_min's its lane id
+// into an LDS table indexed by the drawn position (direct for deg <= TAB,
+// hashed above it — a hash collision is detected and sent to the exact path),
+// and reads back the earliest lane that drew the same position.  The first
+// group always starts at the true position; group k+1 is kept iff groups
+// 0..k consumed exactly their n words.  A dst whose draws do not complete
+// inside its G-word window goes to the exact full-wave path (rounds of 64
+// words, cross-round dedup through `set`).
+struct MtInfo {
+  uint32_t c, n, deg, thr;  // column offset, draws (0: none), range, Lemire threshold
+};
+
+__global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
+                          const uint32_t* __restrict__ co, uint32_t* sizes, uint32_t e_cap,
+                          int lemire, uint4* __restrict__ info) {
+  finish_count(co, e_cap, sizes);
+  const uint32_t v = sizes[0];
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < v; i += gridDim.x * blockDim.x) {
+    const uint32_t d = dst[i];
+    const uint32_t deg = (uint32_t)(goff[d + 1] - goff[d]);
+    const uint32_t c = co[i];
+    const uint32_t n = co[i + 1] - c;
+    const bool draw = n > 0 && n < deg && (uint64_t)c + n <= e_cap;
+    uint32_t thr = 0;
+    if (draw) thr = lemire ? (0u - deg) % deg : 0xFFFFFFFFu / deg;  // DIV: `scaling`
+    info[i] = make_uint4(c, draw ? n : 0u, deg, thr);
+  }
+}
+
+// word r (relative to block `cur`) of the tempered two-block window
+__device__ __forceinline__ uint32_t mt_word(const uint32_t* tw, int cur, uint32_t r) {
+  uint32_t k = (uint32_t)cur * 624u + r;
+  if (k >= 1248u) k -= 1248u;
+  return tw[k];
+}
+
+struct MtStream {
+  uint32_t* raw;  // [2][624] std::mt19937::_M_x of the current / next block
+  uint32_t* tw;   // [2][624] tempered copies
+  int cur;
+  uint32_t q0;    // _M_p within block `cur`
+  bool have_next;
+  // make words [q0, q0 + 64) available (twists the next block on demand)
+  __device__ __forceinline__ void ensure(int lane) {
+    for (;;) {
+      if (q0 >= 624) {
+        if (!have_next) {
+          mt_twist(raw + cur * 624, raw + (cur ^ 1) * 624, lane);
+          for (int k = lane; k < 624; k += kWave)
+            tw[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
+          __syncthreads();
+        }
         cur ^= 1;
         q0 -= 624;
         have_next = false;
         continue;
       }
-      const uint32_t remaining = n - count;
-      const int R = remaining <= 12 ? 16 : (remaining <= 28 ? 32 : 64);
-      uint32_t val = 0;
-      bool ok = false;
-      if (lane < R) {
-        const uint32_t q = q0 + lane;
-        const uint32_t x = q < 624 ? mt_temper(blk[cur][q]) : mt_temper(blk[cur ^ 1][q - 624]);
-        ok = dr.apply(x, val);
+      if (q0 + kWave > 624 && !have_next) {
+        mt_twist(raw + cur * 624, raw + (cur ^ 1) * 624, lane);
+        for (int k = lane; k < 624; k += kWave)
+          tw[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
+        __syncthreads();
+        have_next = true;
       }
-      bool dup = false;
-      for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
-      const uint64_t okmask = __ballot(ok);
-      for (int j = 0; j < R; ++j) {
-        uint32_t vj = __shfl(val, j, kWave);
-        dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
-      }
-      const bool isnew = ok && !dup;
-      const uint64_t newmask = __ballot(isnew);
-      const uint32_t nnew = __popcll(newmask);
-      uint64_t take = newmask;
-      if (nnew >= remaining) {
-        uint64_t m = newmask;
-        for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
-        const int last = __ffsll((long long)m) - 1;
-        take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
-        q0 += (uint32_t)last + 1u;
-      } else {
-        q0 += (uint32_t)R;
-      }
-      if ((take >> lane) & 1ull) {
-        const uint32_t slot = count + (uint32_t)__popcll(take & lt_mask);
-        set[slot] = val;
-        const uint32_t pos = c + slot;
-        const uint32_t g = a.grows[beg + val];
-        a.ans[pos] = g;
-        a.edst[pos] = i;
-        a.marks[g] = 1;
-      }
-      count += (uint32_t)__popcll(take);
-      __syncthreads();
+      return;
     }
   }
-  if (q0 >= 624 && have_next) {
-    cur ^= 1;
-    q0 -= 624;
+};
+
+__device__ __forceinline__ bool mt_apply(uint32_t x, uint32_t deg, uint32_t thr, bool lemire,
+                                         uint32_t& v) {
+  if (lemire) {
+    const uint64_t m = (uint64_t)x * deg;
+    v = (uint32_t)(m >> 32);
+    return (uint32_t)m >= thr;
+  }
+  v = x / thr;                 // thr = scaling
+  return x < deg * thr;        // past = range * scaling
+}
+
+// Exact path, whole wave: the first n distinct accepted draws of one dst in
+// rounds of up to 64 words; positions -> ans[c + slot].
+__device__ void mt_exact(MtStream& s, uint32_t* set, uint32_t* ans, uint32_t c, uint32_t n,
+                         uint32_t deg, uint32_t thr, bool lemire, int lane) {
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t count = 0;
+  while (count < n) {
+    s.ensure(lane);
+    const uint32_t remaining = n - count;
+    const int R = remaining <= 12 ? 16 : (remaining <= 28 ? 32 : 64);
+    uint32_t val = 0;
+    bool ok = false;
+    if (lane < R) ok = mt_apply(mt_word(s.tw, s.cur, s.q0 + lane), deg, thr, lemire, val);
+    bool dup = false;
+    for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
+    const uint64_t okmask = __ballot(ok);
+    for (int j = 0; j < R; ++j) {
+      const uint32_t vj = __shfl(val, j, kWave);
+      dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
+    }
+    const bool isnew = ok && !dup;
+    const uint64_t newmask = __ballot(isnew);
+    uint64_t take = newmask;
+    if ((uint32_t)__popcll(newmask) >= remaining) {
+      uint64_t m = newmask;
+      for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+      const int last = __ffsll((long long)m) - 1;
+      take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
+      s.q0 += (uint32_t)last + 1u;
+    } else {
+      s.q0 += (uint32_t)R;
+    }
+    if ((take >> lane) & 1ull) {
+      const uint32_t slot = count + (uint32_t)__popcll(take & lt_mask);
+      set[slot] = val;
+      ans[c + slot] = val;
+    }
+    count += (uint32_t)__popcll(take);
+    __syncthreads();
+  }
+}
+
+constexpr uint32_t kMtTab = 16384;  // LDS dedup table entries (all groups)
+constexpr uint32_t kMtTaken = 0xFFFFFFFEu;  // exact path: position already kept
+
+// Exact path for deg <= kMtTab, whole wave: the table is direct-mapped by
+// position over all groups' regions.  Per round of 64 words: a position is
+// new iff it is accepted, not marked kept by an earlier round, and no earlier
+// lane of the round drew it (sentinel + ds_min of lane ids, as the fast
+// path).  Kept positions are marked, and unmarked when the dst is done, so
+// the table holds no marks between dsts.
+__device__ void mt_exact_tab(MtStream& s, uint32_t* tab, uint32_t* set, uint32_t* out, uint32_t n,
+                             uint32_t deg, uint32_t thr, bool lemire, int lane) {
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t count = 0;
+  while (count < n) {
+    s.ensure(lane);
+    const uint32_t remaining = n - count;
+    uint32_t val = 0;
+    bool ok = mt_apply(mt_word(s.tw, s.cur, s.q0 + lane), deg, thr, lemire, val);
+    if (ok) ok = tab[val] != kMtTaken;
+    if (ok) tab[val] = 0xFFFFFFFFu;
+    if (ok) atomicMin(&tab[val], (uint32_t)lane);
+    const bool isnew = ok && tab[val] == (uint32_t)lane;
+    const uint64_t newmask = __ballot(isnew);
+    uint64_t take = newmask;
+    if ((uint32_t)__popcll(newmask) >= remaining) {
+      uint64_t m = newmask;
+      for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+      const int last = __ffsll((long long)m) - 1;
+      take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
+      s.q0 += (uint32_t)last + 1u;
+    } else {
+      s.q0 += (uint32_t)kWave;
+    }
+    if ((take >> lane) & 1ull) {
+      const uint32_t slot = count + (uint32_t)__popcll(take & lt_mask);
+      tab[val] = kMtTaken;
+      set[slot] = val;
+      out[slot] = val;
+    }
+    count += (uint32_t)__popcll(take);
+  }
+  for (uint32_t k = lane; k < n; k += kWave) tab[set[k]] = 0u;
+}
+constexpr uint32_t kMtInfo = 2048;  // per-dst info staged in LDS
+constexpr uint32_t kMtPos = 8192;   // kept positions staged in LDS before the flush
+
+// The hot loop issues no vector-memory instruction: on gfx9 one vmcnt counter
+// covers loads and stores, so a loop-carried global load (the next dsts'
+// info) would wait for every position store of the iteration before it.
+// Per-dst info arrives in 2048-dst chunks and kept positions leave in
+// ~7 K-word flushes, both through LDS.
+template <int G>
+__global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ info,
+                                                     const uint32_t* sizes,
+                                                     uint32_t* __restrict__ ans,
+                                                     uint32_t* mt_state, int lemire_i, int dbg) {
+  constexpr int K = kWave / G;
+  uint64_t st_it = 0, st_ex = 0, st_cyc_ex = 0, st_commit = 0;
+  const uint64_t st_t0 = __builtin_readcyclecounter();
+  constexpr uint32_t TAB = kMtTab / K;
+  constexpr uint64_t GM = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
+  __shared__ uint32_t raw[2 * 624];
+  __shared__ uint32_t tw[2 * 624];
+  __shared__ uint32_t tab[kMtTab];
+  __shared__ uint32_t set[kSetCap];
+  __shared__ uint4 inf[kMtInfo];
+  __shared__ uint32_t pbuf[kMtPos];
+  const int lane = threadIdx.x;
+  const int grp = lane / G, gl = lane % G;
+  const bool lemire = lemire_i != 0;
+  for (int k = lane; k < 624; k += kWave) {
+    const uint32_t x = mt_state[k];
+    raw[k] = x;
+    tw[k] = mt_temper(x);
+  }
+  MtStream s{raw, tw, 0, mt_state[624], false};
+  for (uint32_t k = lane; k < kMtTab; k += kWave) tab[k] = 0u;  // no stale kMtTaken marks
+  const uint32_t v = sizes[0];
+  const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t ibase = 0;  // inf[k] = info[ibase + k]
+  for (uint32_t k = lane; k < kMtInfo && k < v; k += kWave) inf[k] = info[k];
+  uint32_t cbase = 0, chi = 0;  // pbuf[k] -> ans[cbase + k]; chi: end of the kept range
+  __syncthreads();
+  uint32_t i = 0;
+  while (i < v) {
+    if (i + K > ibase + kMtInfo) {  // next info chunk
+      __syncthreads();
+      ibase = i;
+      for (uint32_t k = lane; k < kMtInfo && ibase + k < v; k += kWave) inf[k] = info[ibase + k];
+      __syncthreads();
+    }
+    const uint32_t ci = inf[i - ibase].x;
+    if (ci - cbase + kSetCap + kWave > kMtPos) {  // flush kept positions
+      __syncthreads();
+      for (uint32_t k = lane; k < chi - cbase; k += kWave) ans[cbase + k] = pbuf[k];
+      cbase = ci;
+      __syncthreads();
+    }
+    s.ensure(lane);
+    // the K dsts i .. i+K-1, speculative start of each
+    uint4 mine = (i + grp < v) ? inf[i - ibase + grp] : zero;
+    uint32_t n_k[K];
+    uint32_t my_sp = s.q0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      n_k[k] = __builtin_amdgcn_readlane(mine.y, k * G);
+      if (k < grp) my_sp += n_k[k];
+    }
+    const uint32_t deg = mine.z;
+    const bool active = mine.y > 0;
+    uint32_t val = 0;
+    bool ok = false;
+    if (active) ok = mt_apply(mt_word(tw, s.cur, my_sp + gl), deg, mine.w, lemire, val);
+    const uint32_t slot_idx = (uint32_t)grp * TAB + (deg <= TAB ? val : (val & (TAB - 1)));
+    if (ok) tab[slot_idx] = 0xFFFFFFFFu;
+    if (ok) atomicMin(&tab[slot_idx], (uint32_t)gl);
+    const uint32_t w = ok ? tab[slot_idx] : (uint32_t)gl;
+    bool dup = w != (uint32_t)gl;
+    uint64_t collm = 0;
+    if (__ballot(dup && deg > TAB)) {  // hashed: the earlier lane may hold another position
+      const uint32_t wv = __shfl(val, grp * G + (int)(w & (G - 1)), kWave);
+      const bool coll = dup && deg > TAB && wv != val;
+      collm = __ballot(coll);
+    }
+    // rank of each new lane among its group's new lanes; the lane of rank
+    // n-1 ends the dst's draws (its word is the last one consumed)
+    const uint64_t newm = __ballot(ok && !dup);
+    const uint64_t gnew = (newm >> (grp * G)) & GM;
+    const uint32_t rank = (uint32_t)__popcll(gnew & ((1ull << gl) - 1ull));
+    const bool isnew = ok && !dup;
+    const uint64_t lastm = __ballot(isnew && rank + 1 == mine.y);
+    // per group, at its first lane: committable (its n-th new draw inside the
+    // window, no hash collision; or nothing to draw) and clean (consumed
+    // exactly n words, so the next group's speculative start was right)
+    const uint64_t gl_last = (lastm >> (grp * G)) & GM;
+    const bool can = mine.y == 0 || (gl_last != 0 && ((collm >> (grp * G)) & GM) == 0);
+    const uint32_t cons = gl_last ? (uint32_t)__ffsll((long long)gl_last) : 0u;  // last + 1
+    const bool clean = can && (mine.y == 0 || cons == mine.y);
+    const bool inb = i + grp < v;
+    constexpr uint64_t LEAD = (G == 16) ? 0x0001000100010001ull
+                                        : ((G == 32) ? 0x0000000100000001ull : 1ull);
+    const uint64_t canm = __ballot(gl == 0 && inb && can) & LEAD;
+    const uint64_t dirtym = ~__ballot(gl == 0 && inb && clean) & LEAD;
+    // first group that is not clean (or past v): groups before it commit,
+    // and it commits too when committable
+    const int f = dirtym ? (__ffsll((long long)dirtym) - 1) / G : K;
+    const uint32_t commit = (uint32_t)f + ((f < K && ((canm >> (f * G)) & 1ull)) ? 1u : 0u);
+    // words consumed: the speculative start of the last committed group
+    // (relative) + its own consumption
+    uint32_t adv = 0;
+    if (commit) {
+      const int lc = (int)commit - 1;
+      adv = __builtin_amdgcn_readlane(my_sp, lc * G) - s.q0 +
+            __builtin_amdgcn_readlane(mine.y == 0 ? 0u : cons, lc * G);
+    }
+    if (isnew && rank < mine.y && (uint32_t)grp < commit) pbuf[mine.x - cbase + rank] = val;
+    // column offsets ascend with the dst, so the last committed dst ends the
+    // kept range (copy-path ranges inside it are rewritten by k_mt_rows)
+    if (commit) chi = __builtin_amdgcn_readlane(mine.x + mine.y, (commit - 1) * G);
+    s.q0 += adv;
+    i += commit;
+    ++st_it;
+    st_commit += commit;
+    if (commit == 0) {  // dst i: exact path
+      const uint64_t te = __builtin_readcyclecounter();
+      ++st_ex;
+      const uint4 fi = inf[i - ibase];
+      if (fi.z <= kMtTab)
+        mt_exact_tab(s, tab, set, pbuf + (fi.x - cbase), fi.y, fi.z, fi.w, lemire, lane);
+      else
+        mt_exact(s, set, pbuf + (fi.x - cbase), 0, fi.y, fi.z, fi.w, lemire, lane);
+      chi = fi.x + fi.y;
+      ++i;
+      st_cyc_ex += __builtin_readcyclecounter() - te;
+    }
+  }
+  if (dbg && lane == 0)
+    printf("[mt G=%d] v=%u it=%llu commit=%llu exact=%llu cyc=%llu cyc_exact=%llu\n", G, v,
+           (unsigned long long)st_it, (unsigned long long)st_commit, (unsigned long long)st_ex,
+           (unsigned long long)(__builtin_readcyclecounter() - st_t0),
+           (unsigned long long)st_cyc_ex);
+  __syncthreads();
+  for (uint32_t k = lane; k < chi - cbase && chi > cbase; k += kWave) ans[cbase + k] = pbuf[k];
+  // persist the generator state as std::mt19937 holds it: (_M_x, _M_p) with
+  // _M_p == 624 kept as is (libstdc++ twists lazily on the next call)
+  if (s.q0 > 624) {
+    s.cur ^= 1;
+    s.q0 -= 624;
   }
   __syncthreads();
-  // persist generator state: std::mt19937 keeps (_M_x = current block, _M_p)
-  for (int k = lane; k < 624; k += kWave) mt_state[k] = blk[cur][k];
-  if (lane == 0) mt_state[624] = q0;
+  for (int k = lane; k < 624; k += kWave) mt_state[k] = raw[s.cur * 624 + k];
+  if (lane == 0) mt_state[624] = s.q0;
+}
+
+// positions -> neighbour ids (16-lane group per dst); copy-path dsts take
+// every neighbour in CSC order (core/ntsFastSampler.hpp:1040-1048)
+__global__ __launch_bounds__(kSelThreads) void k_mt_rows(SelectArgs a) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gl = lane & (kGrp - 1), grp = lane >> 4;
+  const uint32_t v = a.sizes[0];
+  const uint32_t ng = gridDim.x * kSelWaves * kGrpPerWave;
+  for (uint32_t i = blockIdx.x * kSelWaves * kGrpPerWave + w * kGrpPerWave + grp; i < v; i += ng) {
+    const uint32_t d = a.dst[i];
+    const uint64_t beg = a.goff[d];
+    const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
+    const uint32_t c = a.co[i];
+    const uint32_t n = a.co[i + 1] - c;
+    if ((uint64_t)c + n > a.e_cap) continue;
+    const bool copy = n == deg;
+    for (uint32_t k = gl; k < n; k += kGrp) {
+      const uint32_t g = a.grows[beg + (copy ? k : a.ans[c + k])];
+      a.ans[c + k] = g;
+      a.edst[c + k] = i;
+      a.marks[g] = 1;
+    }
+  }
 }
 
 // ---- frontier compaction --------------------------------------------------
@@ -657,8 +916,9 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
-  const size_t need =
-      (scan_co + blk + scan_blk + sort_k + sort_v + up_n) * sizeof(uint32_t) + sort_tmp + 256;
+  const uint64_t mt_n = rng_mode != NTS_RNG_PHILOX ? al((uint64_t)o->v_cap * 4) : 0;
+  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n) *
+                          sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
   uint32_t* w0 = (uint32_t*)ctx->scratch;
   uint32_t* t_scan_co = w0;
@@ -667,7 +927,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   uint32_t* t_skey = t_scan_blk + scan_blk;
   uint32_t* t_seid = t_skey + sort_k;
   uint32_t* t_up = t_seid + sort_v;
-  void* t_sort = (void*)(t_up + up_n);
+  uint32_t* t_mt = t_up + up_n;  // MT19937 modes: per-dst MtInfo (16-byte aligned)
+  void* t_sort = (void*)(t_mt + mt_n);
 
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
@@ -706,8 +967,24 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
       hipLaunchKernelGGL(k_select_philox, dim3(gs), dim3(kSelThreads), 0, st, a);
     }
   } else {
-    hipLaunchKernelGGL(k_select_mt, dim3(1), dim3(kWave), 0, st, a, ctx->mt_state,
-                       rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0);
+    const int lem = rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0;
+    static const int mt_dbg = getenv("NTS_MT_DEBUG") ? 1 : 0;
+    uint4* info = reinterpret_cast<uint4*>(t_mt);
+    hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
+                       o->column_offset, o->sizes, o->e_cap, lem, info);
+    NTS_LAUNCH_CHECK();
+    if (fanout >= 0 && fanout <= 16)
+      hipLaunchKernelGGL(k_mt_serial<16>, dim3(1), dim3(kWave), 0, st, info, o->sizes,
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg);
+    else if (fanout >= 0 && fanout <= 32)
+      hipLaunchKernelGGL(k_mt_serial<32>, dim3(1), dim3(kWave), 0, st, info, o->sizes,
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg);
+    else
+      hipLaunchKernelGGL(k_mt_serial<64>, dim3(1), dim3(kWave), 0, st, info, o->sizes,
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg);
+    NTS_LAUNCH_CHECK();
+    const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
+    hipLaunchKernelGGL(k_mt_rows, dim3(gs), dim3(kSelThreads), 0, st, a);
   }
   NTS_LAUNCH_CHECK();
 

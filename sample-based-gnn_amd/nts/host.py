@@ -39,7 +39,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                early_aggregate=True, sampler_priority=True, fuse_activation=True,
                fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0,
                up_degree=False, gat=False, pd_cache=False, pd_rate=0.2, pd_super_batch=4,
-               gemm="split3", overlap_allreduce=-1, pair_table=3):
+               gemm="split3", overlap_allreduce=-1, pair_table=3, sample_gpu=False):
     E = ext()
     c = E.GCNConfig()
     c.layer_size = list(layers)
@@ -49,6 +49,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.weight_decay = float(weight_decay)
     c.drop_rate = float(drop_rate)
     c.rng_mode = int(rng_mode)
+    c.sample_gpu = bool(sample_gpu)
     c.weight_type = {"sum": E.WeightType.Sum, "mean": E.WeightType.Mean,
                      "mean-sampled": E.WeightType.MeanSampled,
                      "none": getattr(E.WeightType, "None")}[weight]

@@ -96,6 +96,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("batch_size"), py::arg("weight_type") = WeightType::Sum)
       .def("sample_not_finished", [](PySampler& p) { return p.s->sample_not_finished(); })
       .def("restart", [](PySampler& p) { p.s->restart(); })
+      .def("rng_state",
+           [](PySampler& p) {
+             // the MT19937 modes' generator (624 words + _M_p), as std::mt19937 holds it
+             auto out = torch::empty({625}, torch::kInt32);
+             p.cs->synchronize();
+             TORCH_CHECK(nts_hip_rng_state(p.cs->ctx(), (uint32_t*)out.data_ptr<int32_t>()) == 0,
+                         nts_hip_last_error());
+             return out;
+           })
       .def_property("batch_seq", [](PySampler& p) { return p.s->batch_seq; },
                     [](PySampler& p, uint64_t v) { p.s->batch_seq = v; })
       .def_property_readonly("work_offset", [](PySampler& p) { return p.s->work_offset; })
@@ -151,6 +160,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("beta2", &GCNConfig::beta2)
       .def_readwrite("epsilon", &GCNConfig::epsilon)
       .def_readwrite("rng_mode", &GCNConfig::rng_mode)
+      .def_readwrite("sample_gpu", &GCNConfig::sample_gpu)
       .def_readwrite("weight_type", &GCNConfig::weight_type)
       .def_readwrite("fused_gather", &GCNConfig::fused_gather)
       .def_readwrite("bias_correction", &GCNConfig::bias_correction)

@@ -761,7 +761,7 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                                         sg->dev_src(), Wc.data_ptr<float>(), (uint64_t)N, (int)F, hp,
                                         (uint64_t)N, 0.f, 0, 0),
                 "nts_hip_gemm_h2p_gather");
-    else if (pairs)
+    else if (pairs && pairs->P.defined())
       hip_check(nts_hip_gemm_h2_gather(cs->ctx(), 0, (int)s, (int)N, (int)pairs->P.size(1),
                                        reinterpret_cast<const uint32_t*>(pairs->P.data_ptr<int32_t>()),
                                        (uint64_t)pairs->P.stride(0), pairs->rs.data_ptr<float>(),
@@ -850,7 +850,7 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                                            dH.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
                                            (uint64_t)N),
                 "nts_hip_gemm_h2p_tn_gather");
-    else if (pairs && pairs->tn)
+    else if (pairs && pairs->tn && pairs->P.defined())
       hip_check(nts_hip_gemm_h2_tn_gather(cs->ctx(), (int)F, (int)N, (int)s,
                                           reinterpret_cast<const uint32_t*>(pairs->P.data_ptr<int32_t>()),
                                           (uint64_t)pairs->P.stride(0), pairs->rs.data_ptr<float>(),

@@ -31,6 +31,12 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   TORCH_CHECK(cfg.fanout.size() == cfg.layer_size.size() - 1, "fanout per layer");
   TORCH_CHECK(F.is_cuda() && F.dtype() == torch::kFloat32 && F.size(1) == cfg.layer_size[0],
               "feature table must be fp32 [V, layer_size[0]] on the GPU");
+  if (cfg.sample_gpu) {
+    TORCH_CHECK(!cfg.gat && !cfg.pd_cache, "GCN_SAMPLE_GPU: GCN / GraphSAGE layers");
+    TORCH_CHECK(cfg.rng_mode != NTS_RNG_PHILOX,
+                "GCN_SAMPLE_GPU samples with the reference's mt19937 stream (rng_mode MT19937)");
+    cfg.deterministic_backward = true;  // the CSR exists for every graph-op backward
+  }
   if (cfg.pipeline && cfg.sampler_cus > 0)
     cs = std::make_unique<NtsStream>(graph->device,
                                      cu_mask_spread(graph->device, cfg.sampler_cus, true),
@@ -78,20 +84,15 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                   (cfg.transform_first < 0 && cfg.pair_table >= 3 &&
                    cfg.layer_size[0] >= 4 * cfg.layer_size[1]));
   if (tf_ && cfg.pair_table > 0) {
-    // the feature table is static: its rows are split into f16 pairs once
+    // the feature table is static: its rows are split into f16 pairs once,
+    // in ONE layout — planar where the planar kernels take the shape (both
+    // GEMMs: every dW output row in one block, K <= 640, N % 128 == 0),
+    // interleaved otherwise
     const int64_t V = F.size(0), K = F.size(1), Kp = (K + 31) / 32 * 32;
+    const int64_t Nh = cfg.layer_size[1];
     pairs_ = std::make_unique<PairTable>();
-    pairs_->P = torch::empty({V, Kp}, torch::TensorOptions().dtype(torch::kInt32).device(F.device()));
     pairs_->rs = torch::empty({V}, f32_opts(graph->device));
     pairs_->tn = cfg.pair_table >= 2;
-    hip_check(nts_hip_h2_split_rows(cs->ctx(), (uint64_t)V, (uint32_t)K, F.data_ptr<float>(),
-                                    (uint64_t)F.stride(0), (uint32_t)Kp,
-                                    reinterpret_cast<uint32_t*>(pairs_->P.data_ptr<int32_t>()),
-                                    (uint64_t)Kp, pairs_->rs.data_ptr<float>()),
-              "nts_hip_h2_split_rows");
-    // the weight gradient on the planar form where k_h2_tn3 takes the shape
-    // (every output row in one block: K <= 640, N % 128 == 0)
-    const int64_t Nh = cfg.layer_size[1];
     if (cfg.pair_table >= 3 && Kp <= 640 && Nh % 128 == 0) {
       pairs_->Q = torch::empty({V, 2 * Kp},
                                torch::TensorOptions().dtype(torch::kInt16).device(F.device()));
@@ -100,6 +101,13 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                              reinterpret_cast<uint16_t*>(pairs_->Q.data_ptr<int16_t>()),
                                              (uint64_t)(2 * Kp), pairs_->rs.data_ptr<float>()),
                 "nts_hip_h2_split_rows_planar");
+    } else {
+      pairs_->P = torch::empty({V, Kp}, torch::TensorOptions().dtype(torch::kInt32).device(F.device()));
+      hip_check(nts_hip_h2_split_rows(cs->ctx(), (uint64_t)V, (uint32_t)K, F.data_ptr<float>(),
+                                      (uint64_t)F.stride(0), (uint32_t)Kp,
+                                      reinterpret_cast<uint32_t*>(pairs_->P.data_ptr<int32_t>()),
+                                      (uint64_t)Kp, pairs_->rs.data_ptr<float>()),
+                "nts_hip_h2_split_rows");
     }
   }
   // CSR transposes only where a graph-op backward runs (every hop but the
@@ -370,8 +378,11 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       // backward to its own backward output (one CSR pass instead of the CSR
       // gather + nts_hip_act_backward; same arithmetic); NTS_TF_MASKED_BWD=1
       // keeps the unfused masked gather for A/B
+      // (only over a CSR: with the atomic CSC backward the layer above has
+      // none, and this layer then runs nts_hip_act_backward itself)
       static const bool masked_env = getenv("NTS_TF_MASKED_BWD") != nullptr;
-      const bool fuse = ctx.is_train() && !masked_env && hop >= 1;
+      const bool fuse = ctx.is_train() && !masked_env && hop >= 1 &&
+                        sg->sampled_sgs[hop - 1]->has_csr;
       if (hop >= 1) {
         sampCSC* up = sg->sampled_sgs[hop - 1];
         up->post_mask = fuse ? X.data_ptr<float>() : nullptr;
@@ -386,7 +397,12 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       continue;
     }
     if (bottom && cfg.profile) prof.begin(KernelProfiler::BOTTOM_AGG, (hipStream_t)cs->stream());
-    if (bottom && cfg.fused_gather)
+    if (cfg.sample_gpu && bottom && cfg.fused_gather)
+      Y = ctx.runGraphOp<op::SingleGPUSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true,
+                                                     fcache.get());
+    else if (cfg.sample_gpu)
+      Y = ctx.runGraphOp<op::SingleGPUSampleGraphOp>(X, sg, graph.get(), hop, cs.get(), false);
+    else if (bottom && cfg.fused_gather)
       Y = ctx.runGraphOp<op::SingleGPUAllSampleGraphOp>(F, sg, graph.get(), hop, cs.get(), true,
                                                         fcache.get());
     else
@@ -768,6 +784,11 @@ void GCN_SAMPLE_ALLGPU_impl::set_presample(const std::vector<uint32_t>& counts,
   pd_offset_.assign(counts.size() + 1, 0);
   for (size_t i = 0; i < counts.size(); ++i) pd_offset_[i + 1] = pd_offset_[i] + counts[i];
   TORCH_CHECK(pd_offset_.back() == ids.size(), "PD cache: ids must hold sum(counts) vertices");
+  // the ids index cache_map / cache_location on the device: a stale or
+  // mismatched PRE_SAMPLE_FILE must not write past them
+  for (uint32_t id : ids)
+    TORCH_CHECK(id < graph->global_vertices, "PD cache: hot vertex id ", id,
+                " >= vertex count ", graph->global_vertices, " (stale PRE_SAMPLE_FILE?)");
   uint32_t mx = 1;
   for (uint32_t c : counts) mx = std::max(mx, c);
   std::vector<VertexId> hot(ids.begin(), ids.end());

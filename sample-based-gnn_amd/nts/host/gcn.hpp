@@ -12,6 +12,11 @@ struct GCNConfig {
   float learn_rate = 0.01f, weight_decay = 1e-4f, drop_rate = 0.5f;
   float beta1 = 0.9f, beta2 = 0.999f, epsilon = 1e-9f;  // toolkits/GCN_SAMPLE_GPU.hpp:115-117
   int rng_mode = NTS_RNG_PHILOX;
+  // GCN_SAMPLE_GPU (toolkits/GCN_SAMPLE_GPU.hpp:289-394): the CPU sampler's
+  // blocks (sample_fast: the reference's mt19937 stream, here replayed on the
+  // device, NTS_RNG_MT19937_LEMIRE) through SingleGPUSampleGraphOp, whose
+  // backward always runs over the sampled CSR (Gather_By_Src_From_Dst_Spmm)
+  bool sample_gpu = false;
   WeightType weight_type = WeightType::Sum;  // GraphSAGE toolkits: Mean
   bool up_degree = false;             // UP_DEGREE cfg key (core/GraphSegment.cpp:273-276)
   bool gat = false;                   // GAT_SAMPLE_ALL_GPU model (attention layers)

@@ -47,7 +47,9 @@ from . import dataloader
 ALGORITHMS = {
     # name: (model, weight, rng, bias_correction, feature placement)
     "GCNSAMPLESINGLE": ("gcn", "sum", "mt", True, None),
-    "GCNSAMPLEGPU": ("gcn", "sum", "philox", False, None),
+    # GCN_SAMPLE_GPU: sample_fast's mt19937 stream (replayed on the device) ->
+    # SingleGPUSampleGraphOp (CSR backward), GPU Adam (toolkits/GCN_SAMPLE_GPU.hpp:289-394)
+    "GCNSAMPLEGPU": ("gcn", "sum", "mt", False, "sample_gpu"),
     "GCNSAMPLEALLGPU": ("gcn", "sum", "philox", False, None),
     "GSSAMPLEALLGPU": ("gcn", "mean", "philox", False, None),
     "GCNSAMPLEALLMULTI": ("gcn", "sum", "philox", False, None),
@@ -103,17 +105,21 @@ def build_driver(E, info: dataloader.InputInfo, G, feat, labels, train_ids, devi
         weight="none" if model == "gat" else weight, bias_correction=bias,
         pipeline=info.pipeline_num > 1, up_degree=info.up_degree, gat=model == "gat",
         cache_rate=cache_rate, shuffle=True, pd_cache=pd, pd_rate=info.cache_rate,
-        pd_super_batch=max(info.pipeline_num, 1))
+        pd_super_batch=max(info.pipeline_num, 1), sample_gpu=place == "sample_gpu")
     return E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train_ids, cfg, comm)
 
 
-def pd_presample_file(drv, info, base, out=print):
+def pd_presample_file(drv, info, base, out=print, rank=0, world=1):
     """PRE_SAMPLE_FILE (core/ntsBaseOp.hpp:427-497): read the hot vertices of
     every super-batch if the file exists, else keep the device preSample the
-    driver ran and write it (default name when the key is unset)."""
+    driver ran and write it (default name when the key is unset).  Under
+    WORLD_SIZE > 1 each rank has its own train shard and so its own file
+    (`.rank<r>` appended): no two ranks write one path."""
     name = info.pre_sample_file or dataloader.presample_file_name(
         _path(base, info.edge_file), info.batch_size, info.fanout_string, info.pipeline_num)
     path = _path(base, name)
+    if world > 1:
+        path = path.with_name(path.name + f".rank{rank}")
     counts, ids = drv.presample()
     if path.exists():
         kc, kids = dataloader.read_presample_file(path, len(counts))
@@ -157,7 +163,7 @@ def run(cfg_path, epochs=None, device=0, out=print) -> dict:
     comm = ndist.make_communicator(E, world, rank, device)
     drv = build_driver(E, info, G, feat, lab, train, dev, comm)
     if ALGORITHMS.get(info.algorithm.upper(), ("",) * 5)[4] == "pd":
-        pd_presample_file(drv, info, base, out if rank == 0 else (lambda s: None))
+        pd_presample_file(drv, info, base, out if rank == 0 else (lambda s: None), rank, world)
     if rank == 0:
         out(f"GNNmini::Engine[MI355X.GPU.{info.algorithm}] running [{epochs}] Epochs "
             f"(V={info.vertices}, E={n_edges}, layers {info.layer_string}, fanout "

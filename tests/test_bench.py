@@ -24,7 +24,7 @@ def bench():
 def _args(**kw):
     base = dict(shape="reddit", batch=10000, fanout="25-10", weight="sum", transform_first=-1,
                 model="gcn", cache_rate=-1.0, gemm="split3", no_hip_gemm=False, no_pipeline=False,
-                pd_cache=False, pd_rate=0.2, pd_super_batch=4, pair_table=0)
+                pd_cache=False, pd_rate=0.2, pd_super_batch=4, pair_table=0, rng="philox")
     base.update(kw)
     return types.SimpleNamespace(**base)
 

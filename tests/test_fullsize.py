@@ -151,6 +151,57 @@ def test_c2_reddit_shaped_full_batch(E):
     _free()
 
 
+def _sets_equal(got_layer, ref_layer):
+    """Per-dst neighbour multisets equal (the reference emits std::unordered_map
+    order inside a dst, core/ntsFastSampler.hpp:1026-1038)."""
+    co = _np(got_layer["column_offset"]).astype(np.int64)
+    d_of_e = np.repeat(np.arange(co.size - 1, dtype=np.int64), np.diff(co))
+    a = _np(got_layer["sample_ans"]).astype(np.int64)
+    b = ref_layer["sample_ans"].astype(np.int64)
+    ka = np.sort(d_of_e * (1 << 32) + a)
+    kb = np.sort(d_of_e * (1 << 32) + b)
+    return np.array_equal(ka, kb)
+
+
+def test_c2_mt19937_reference_stream_full_batch(E):
+    """The reference's own generator at the benched size: std::mt19937(2000) +
+    uniform_int_distribution (Lemire, libstdc++ 11) consumed over the dsts in
+    order (core/ntsFastSampler.hpp:200-205,962-1140).  Two consecutive C2
+    batches (B=10,000, 25-10): every array bit-exact vs the oracle in draw
+    order, per-dst sets equal to the reference's unordered_map order, and the
+    generator state (624 words + position) identical after each batch."""
+    from nts import synthetic
+    g, F, C = synthetic.shaped("reddit", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    fan, B = [25, 10], 10_000
+    rng = np.random.default_rng(15)
+    perm = rng.permutation(V).astype(np.int32)[:2 * B]
+    fs = E.FastSampler(G, torch.from_numpy(perm), 2, B, fan, rng_mode=1, seed=2000)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    od, idg = _np(G.out_degree), _np(G.in_degree)
+    o = orc.Sampler(col, rows, idg, od, fan, seed=2000, rng_mode=orc.RNG_MT_LEMIRE,
+                    order_mode=orc.ORDER_DRAW)
+    o_map = orc.Sampler(col, rows, idg, od, fan, seed=2000, rng_mode=orc.RNG_MT_LEMIRE,
+                        order_mode=orc.ORDER_UNORDERED_MAP)
+    for b in range(2):
+        got = fs.sample_gpu_fast(B)
+        _properties(G, got, fan, V)
+        assert got[1]["e_size"] > 1_000_000
+        seeds = perm[b * B:(b + 1) * B].view(np.uint32)
+        ref = o.sample(seeds, b)
+        _compare_oracle(got, ref)
+        assert np.array_equal(_np(fs.rng_state()), o.mt_state()), f"generator state, batch {b}"
+        ref_map = o_map.sample(seeds, b)
+        for a, r in zip(got, ref_map):
+            assert np.array_equal(_np(a["source"]), r["source"])
+            assert _sets_equal(a, r)
+    del fs, got, G
+    _free()
+
+
 def test_c3_products_shaped_three_layers_mean(E):
     from nts import synthetic
     g, F, C = synthetic.shaped("products", device=DEV)

@@ -194,6 +194,83 @@ def test_training_step_matches_oracle_step(E, graph, tf, pt):
         torch.testing.assert_close(w1, ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("tf", [0, 1])
+def test_atomic_backward_trains_like_the_csr_backward(E, graph, tf):
+    """deterministic_backward=False (graph-op backward by atomic CSC scatter,
+    no CSR in the sampler) — with the transform-first bottom layer too, where
+    the layer above then has no CSR to fuse the activation backward into:
+    the same step as the CSR-gather backward, up to fp32 summation order."""
+    a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5, transform_first=tf,
+                    deterministic_backward=False)
+    b, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=0.5, transform_first=tf)
+    assert a.transform_first == bool(tf)
+    for _ in range(2):
+        a.train_batch()
+        b.train_batch()
+    a.synchronize()
+    b.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-4)
+
+
+def _gcn_cpu_sample_forward(graph, feat, W, l0, l1):
+    """GCN_CPU_SAMPLE forward (toolkits/GCN_CPU_SAMPLE.hpp:214-233), eval mode."""
+    X0 = orc.get_feature(l1["source"], feat.cpu().numpy())
+    Y0 = orc.fuse_fwd(l1, X0, graph["od"], graph["idg"])
+    X1 = torch.relu(torch.from_numpy(Y0) @ W[0])
+    Y1 = orc.fuse_fwd(l0, X1.numpy(), graph["od"], graph["idg"])
+    X2 = (torch.from_numpy(Y1) @ W[1]).log_softmax(1)
+    return [torch.from_numpy(Y0), X1, torch.from_numpy(Y1), X2]
+
+
+@pytest.mark.parametrize("tf", [0, 1])
+def test_gcn_sample_gpu_reference_stream(E, graph, tf):
+    """GCN_SAMPLE_GPU (toolkits/GCN_SAMPLE_GPU.hpp:289-394): blocks of the
+    reference's own sampler stream (sample_fast, std::mt19937(2000), replayed
+    on the device) through SingleGPUSampleGraphOp (CSR backward).  Forward
+    activations vs the GCN_CPU_SAMPLE chain on the oracle's blocks in the
+    reference's own emission order (std::unordered_map per dst) within the
+    north star's 1e-4; then one training step vs the oracle's step."""
+    from nts import _abi
+    F, C, B = 96, 7, 200
+    kw = dict(rng_mode=_abi.NTS_RNG_MT19937_LEMIRE, sample_gpu=True, transform_first=tf)
+    drv, feat, labels, train = _driver(E, graph, F, C, [F, 32, C], [10, 5], B, **kw)
+    seeds = torch.arange(11, 11 + 256, dtype=torch.int32)
+    acts = drv.forward_eval(seeds, 0)
+    W = [w.cpu() for w in drv.weights()]
+    o = orc.Sampler(graph["col"], graph["rows"], graph["idg"], graph["od"], [10, 5], seed=2000,
+                    rng_mode=orc.RNG_MT_LEMIRE, order_mode=orc.ORDER_UNORDERED_MAP)
+    l0, l1 = o.sample(seeds.numpy().astype(np.uint32), 0)
+    ref = _gcn_cpu_sample_forward(graph, feat, W, l0, l1)
+    for got, r in zip(acts[1:], ref[1:]):
+        torch.testing.assert_close(got.cpu(), r, rtol=1e-4, atol=1e-4)
+    if not tf:
+        torch.testing.assert_close(acts[0].cpu(), ref[0], rtol=1e-5, atol=1e-6)
+    # one training step on a fresh driver (fresh generator) vs the oracle
+    drv, feat, labels, train = _driver(E, graph, F, C, [F, 32, C], [10, 5], B, **kw)
+    W0 = [w.cpu().clone() for w in drv.weights()]
+    drv.train_batch()
+    drv.synchronize()
+    W1 = [w.cpu() for w in drv.weights()]
+    o = orc.Sampler(graph["col"], graph["rows"], graph["idg"], graph["od"], [10, 5], seed=2000,
+                    rng_mode=orc.RNG_MT_LEMIRE, order_mode=orc.ORDER_UNORDERED_MAP)
+    l0, l1 = o.sample(train.numpy()[:B].astype(np.uint32), 0)
+    Wg = [w.clone().requires_grad_() for w in W0]
+    X0 = orc.get_feature(l1["source"], feat.cpu().numpy())
+    Y0 = torch.from_numpy(orc.fuse_fwd(l1, X0, graph["od"], graph["idg"]))
+    X1 = torch.relu(Y0 @ Wg[0])
+    Y1 = torch.from_numpy(orc.fuse_fwd(l0, X1.detach().numpy(), graph["od"],
+                                       graph["idg"])).requires_grad_()
+    X2 = (Y1 @ Wg[1]).log_softmax(1)
+    tgt = labels.cpu()[torch.from_numpy(l0["destination"].astype(np.int64))]
+    torch.nn.functional.nll_loss(X2.log_softmax(1), tgt).backward()
+    X1.backward(torch.from_numpy(orc.fuse_bwd(l0, Y1.grad.numpy(), graph["od"], graph["idg"])))
+    for w0, w, w1 in zip(W0, Wg, W1):
+        wg = w0 * 1e-4 + w.grad
+        ref_w = w0 - (0.01 * (0.1 * wg)) / (torch.sqrt((0.001 * wg) * wg) + 1e-9)
+        torch.testing.assert_close(w1, ref_w, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("drop", [0.0, 0.5])
 def test_training_is_deterministic_and_learns(E, graph, drop):
     a, *_ = _driver(E, graph, 64, 7, [64, 32, 7], [10, 5], 200, drop=drop)

@@ -67,6 +67,21 @@ def test_text_reader_lock_step_semantics(tmp_path):
         dataloader.read_feature_label_mask(tmp_path / "f3", tmp_path / "l", tmp_path / "m", 5, 2)
 
 
+def test_text_reader_files_smaller_than_the_thread_count(tmp_path):
+    """Files of a few bytes cut for 16 threads: no cut may look before the text."""
+    (tmp_path / "f").write_text("1 2\n")
+    (tmp_path / "l").write_text("1 3\n")
+    (tmp_path / "m").write_text("1 val\n")
+    f, l, m = dataloader.read_feature_label_mask(tmp_path / "f", tmp_path / "l", tmp_path / "m",
+                                                 2, 1, threads=16)
+    assert f[1].tolist() == [2.0] and l.tolist() == [0, 3]
+    assert m.tolist() == [dataloader.MASK_UNLISTED, dataloader.MASK_VAL]
+    (tmp_path / "e").write_text("")
+    f, l, m = dataloader.read_feature_label_mask(tmp_path / "e", tmp_path / "e", tmp_path / "e",
+                                                 2, 1, threads=16)
+    assert l.tolist() == [0, 0]
+
+
 def test_text_reader_many_threads_large(tmp_path):
     rng = np.random.default_rng(3)
     V, F = 20_000, 16
