@@ -178,8 +178,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # NTS_BENCH_SHARE_GPU=1: every rank on device 0 — a rehearsal of the
     # multi-rank control flow on a one-GPU box (RCCL refuses two ranks on one
-    # device, so the ranks then talk over gloo and train without the gradient
-    # all-reduce; the numbers are not a scaling measurement)
+    # device, so the ranks talk over gloo: the timing collectives and the
+    # gradient all-reduce, through the Communicator's host transport; the
+    # numbers are not a scaling measurement)
     shared = os.environ.get("NTS_BENCH_SHARE_GPU") == "1"
     if shared:
         local_rank = 0
@@ -217,7 +218,10 @@ def main():
     dst_host = g.dst.cpu().numpy().view(np.uint32) if want_cpu else None
     del g
 
-    comm = None if shared else ndist.make_communicator(E, world, rank, local_rank)
+    if shared:
+        comm = ndist.make_host_communicator(E, world, rank) if world > 1 else None
+    else:
+        comm = ndist.make_communicator(E, world, rank, local_rank)
 
     fan = [int(x) for x in args.fanout.split("-")]
     layers = ([int(x) for x in args.layers.split("-")] if args.layers else [F_dim, args.hidden, C])
@@ -344,7 +348,7 @@ def main():
         "config": {
             "workload": workload_name(args, layers, V, En, tf),
             "global_batch": args.batch * world,
-            "parallelism": f"dp{world}" + ("-shared-gpu-rehearsal (gloo, no all-reduce)" if shared and world > 1 else ""),
+            "parallelism": f"dp{world}" + ("-shared-gpu-rehearsal (gloo all-reduce through host copies)" if shared and world > 1 else ""),
             "fanout": args.fanout,
             "epoch_time_s": epoch_s,
             "epoch_time_kind": epoch_kind,

@@ -8,7 +8,11 @@ GCN_SAMPLE_ALL_MULTI (toolkits/GCN_SAMPLE_ALL_MULTI.hpp:89-113, 564-587):
     gets the same count and the remainder is dropped;
   * communicator: one RCCL communicator per process, bootstrapped with a
     unique id that rank 0 creates and torch.distributed broadcasts (any
-    backend: nccl on the GPU box, gloo in CPU tests).
+    backend: nccl on the GPU box, gloo in CPU tests);
+  * host transport: the same Communicator with its two collectives carried
+    by torch.distributed over gloo (host copies) — for ranks that share one
+    GPU, where RCCL refuses two ranks on one device (tests, and the
+    one-GPU rehearsal `NTS_BENCH_SHARE_GPU=1 bench.py --gpus N`).
 """
 from __future__ import annotations
 
@@ -44,6 +48,25 @@ def make_communicator(ext, world: int, rank: int, local_rank: int):
         return None
     uid = broadcast_unique_id(ext.Communicator.unique_id, rank)
     return ext.Communicator(world, rank, uid, local_rank)
+
+
+def gloo_collective(tensor, op: int, root: int) -> None:
+    """Communicator host transport over the default torch.distributed group:
+    op 0 = SUM all-reduce in place, op 1 = broadcast from `root`."""
+    import torch
+    import torch.distributed as dist
+    c = tensor.detach().cpu()
+    if op == 0:
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    else:
+        dist.broadcast(c, src=root)
+    tensor.copy_(c)
+    torch.cuda.synchronize()
+
+
+def make_host_communicator(ext, world: int, rank: int, collective=gloo_collective):
+    """The C++ driver's Communicator with a host transport (see module doc)."""
+    return ext.Communicator.host(world, rank, collective)
 
 
 def global_grad_sum(local_grads, all_reduce) -> list:

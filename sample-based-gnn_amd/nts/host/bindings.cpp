@@ -135,6 +135,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         std::string s = uid;
         return std::make_shared<Communicator>(n, r, std::vector<uint8_t>(s.begin(), s.end()), dev);
       }))
+      .def_static(
+          "host",
+          [](int n, int r, py::function fn) {
+            // the Python callable runs with the GIL (pybind11's std::function
+            // wrapper acquires it); train_batch releases it
+            HostCollective h = [fn](torch::Tensor t, int op, int root) {
+              py::gil_scoped_acquire g;
+              fn(t, op, root);
+            };
+            return std::make_shared<Communicator>(n, r, h);
+          },
+          py::arg("nranks"), py::arg("rank"), py::arg("collective"))
+      .def_property_readonly("host_transport", &Communicator::host_transport)
       .def_static("unique_id",
                   []() {
                     auto v = Communicator::unique_id();

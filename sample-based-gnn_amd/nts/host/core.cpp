@@ -1207,11 +1207,26 @@ Communicator::Communicator(int n, int r, const std::vector<uint8_t>& uid, int de
   TORCH_CHECK(uid.size() == 128, "RCCL unique id must be 128 bytes");
   hip_check(nts_hip_comm_init(&comm_, n, r, uid.data(), device), "nts_hip_comm_init");
 }
-Communicator::~Communicator() { nts_hip_comm_destroy(comm_); }
+Communicator::Communicator(int n, int r, HostCollective host)
+    : nranks(n), rank(r), host_(std::move(host)) {
+  TORCH_CHECK(host_ && n >= 1 && r >= 0 && r < n, "host collective: ranks");
+}
+Communicator::~Communicator() {
+  if (comm_) nts_hip_comm_destroy(comm_);
+}
+void Communicator::host_call(float* buf, uint64_t n, void* stream, int op, int root) {
+  TORCH_CHECK(hipStreamSynchronize((hipStream_t)stream) == hipSuccess, "hipStreamSynchronize");
+  int dev = 0;
+  TORCH_CHECK(hipGetDevice(&dev) == hipSuccess, "hipGetDevice");
+  host_(torch::from_blob(buf, {(int64_t)n}, f32_opts(dev)), op, root);
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+}
 void Communicator::allreduce_sum(float* buf, uint64_t n, void* stream) {
+  if (host_) return host_call(buf, n, stream, 0, 0);
   hip_check(nts_hip_allreduce_sum_f32(comm_, buf, n, stream), "nts_hip_allreduce_sum_f32");
 }
 void Communicator::broadcast(float* buf, uint64_t n, int root, void* stream) {
+  if (host_) return host_call(buf, n, stream, 1, root);
   hip_check(nts_hip_broadcast_f32(comm_, buf, n, root, stream), "nts_hip_broadcast_f32");
 }
 std::vector<uint8_t> Communicator::unique_id() {

@@ -468,17 +468,28 @@ struct Parameter {
 };
 
 // RCCL communicator (NCCL_Communicator replacement) — one per process.
+// Host transport for the same two collectives (tests and the one-GPU
+// rehearsal of the multi-rank path): called with a tensor viewing the device
+// buffer after its stream is synchronised; op 0 = SUM all-reduce in place,
+// op 1 = broadcast from `root`.  The result must be in the buffer when it
+// returns.
+using HostCollective = std::function<void(torch::Tensor, int op, int root)>;
+
 class Communicator {
  public:
   Communicator(int nranks, int rank, const std::vector<uint8_t>& uid, int device);
+  Communicator(int nranks, int rank, HostCollective host);
   ~Communicator();
   void allreduce_sum(float* buf, uint64_t n, void* stream);
   void broadcast(float* buf, uint64_t n, int root, void* stream);
   static std::vector<uint8_t> unique_id();
+  bool host_transport() const { return (bool)host_; }
   int nranks, rank;
 
  private:
+  void host_call(float* buf, uint64_t n, void* stream, int op, int root);
   nts_hip_comm* comm_ = nullptr;
+  HostCollective host_;
 };
 
 }  // namespace nts
