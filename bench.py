@@ -149,6 +149,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=default_cpu_threads())
     p.add_argument("--scale", type=float, default=1.0)
+    p.add_argument("--train-limit", type=int, default=0,
+                   help="train on the first N seeds of this rank's shard only (0: all).  PD "
+                        "cache on papers100M-shaped graphs: preSample keeps every "
+                        "super-batch's hot ids (~0.7 M per super-batch there)")
     p.add_argument("--rng", default="philox", choices=["philox", "mt", "mt-div"],
                    help="sampler stream: philox (per-dst counter streams, parallel) or mt: the "
                         "reference's single std::mt19937(2000) stream + uniform_int_distribution "
@@ -212,6 +216,8 @@ def main():
     # toolkits/GCN_SAMPLE_ALL_MULTI.hpp:564-575)
     from nts import dist as ndist
     train = ndist.shard_nids(train_all, world, rank)
+    if args.train_limit > 0:
+        train = train[:args.train_limit]
     log(f"[bench] graph {args.shape}: V={V} E={En} F={F_dim} C={C}  ready in {time.time()-t0:.1f}s")
     want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
     src_host = g.src.cpu().numpy().view(np.uint32) if want_cpu else None
@@ -354,6 +360,7 @@ def main():
             "epoch_time_kind": epoch_kind,
             "epoch_times_s": epoch_times,
             "batches_per_epoch_per_gpu": batches_per_epoch,
+            "train_seeds_per_gpu": int(train.numel()),
             "gpu_sampler_only": sampler_only,
             "host_sampler_wait_s_per_step": sample_s / args.steps,
             "host_train_issue_s_per_step": train_host_s / args.steps,

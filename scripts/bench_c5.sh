@@ -14,4 +14,4 @@ d=json.loads(open('$O/$tag.json').read().strip().splitlines()[-1]); c=d['config'
 print('$tag', round(d['ms_per_step'],4), 'ms/step', '%.3g edges/s' % d['value'], 'epoch-est', round(c['epoch_time_s'],1), 'sampler-only %.3g' % c['gpu_sampler_only']['value'], d['roofline'].get('kernel'), round(d['roofline'].get('frac') or 0, 3))"
 }
 run hbm
-run pd_cache --cache-rate 0.3 --pd-cache --pd-rate 0.2 --pd-super-batch 4
+run pd_cache --cache-rate 0.3 --pd-cache --pd-rate 0.2 --pd-super-batch 4 --train-limit 40960

@@ -234,6 +234,112 @@ def test_c3_products_shaped_three_layers_mean(E):
     _free()
 
 
+def test_c4_products_shaped_two_layer_gcn(E):
+    """C4's per-GPU workload (GCN_SAMPLE_ALL_MULTI, products-shaped, 100-256-47,
+    fanout 25-10, B=1,024 per GPU): the sampled batch bit-exact vs the
+    oracle's PHILOX restatement, with the size-independent properties, and the
+    bottom aggregation (fused gather) bit-exact vs MiniBatchFuseOp."""
+    from nts import synthetic
+    from nts.hip import HipContext
+    g, F, C = synthetic.shaped("products", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    fan, B = [25, 10], 1024
+    seeds = torch.from_numpy(np.random.default_rng(44).choice(V, B, replace=False).astype(np.int32))
+    fs = E.FastSampler(G, seeds, 2, B, fan)
+    got = fs.sample_gpu_fast(B)
+    _properties(G, got, fan, V)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    od, idg = _np(G.out_degree), _np(G.in_degree)
+    o = orc.Sampler(col, rows, idg, od, fan, rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    ref = o.sample(seeds.numpy().astype(np.uint32), 0)
+    _compare_oracle(got, ref)
+    hip = HipContext(0)
+    feat = synthetic.features(V, F, device=DEV)
+    l1 = got[1]
+    y = torch.empty(l1["v_size"], F, device=DEV)
+    hip.spmm_csc_fwd(l1["column_offset"], l1["row_indices"], l1["edge_weight_forward"], None,
+                     l1["v_size"], feat, y, row_map=l1["source"])
+    Y0 = orc.fuse_fwd(ref[1], orc.get_feature(ref[1]["source"], feat.cpu().numpy(), threads=8),
+                      od, idg, threads=8)
+    torch.cuda.synchronize()
+    assert np.array_equal(y.cpu().numpy(), Y0)
+    del fs, got, feat, y, G
+    _free()
+
+
+def test_c5_papers_shaped_pd_cache_with_feature_spill(E):
+    """C5 as BASELINE.json states it, at one GPU: GS_SAMPLE_PD_CACHE
+    (toolkits/GS_SAMPLE_PD_CACHE.hpp:673-1112) on the papers100M-shaped graph
+    (V=111 M, E=3.34 B, 128-wide features, 128-256-256-172, 15-10-5, B=1,024,
+    GraphSAGE mean weights), the feature table in pinned host memory with 30 %
+    of its rows (highest degree) cached in HBM, and the NeutronOrch PD cache
+    (hot vertices of each super-batch of 4 batches, rate 0.2).  The training
+    seeds are the first 8 batches' worth: preSample over all 17.6 K
+    super-batches would keep ~10^10 hot ids (the reference allocates
+    cache_rate * V * super_batches of them, core/ntsBaseOp.hpp:424).
+    Checked at full size: super-batch 0's hot set == the oracle's
+    get_most_neighbor; the first trained batch == the oracle sampler with
+    those dsts omitted (every array, bit-exact; sample_gpu_fast_omit,
+    core/ntsFastSampler.hpp:711-915); no capacity overflow; source strictly
+    ascending; every sampled id a real neighbour; and finite training."""
+    from nts import host, synthetic
+    g, F, C = synthetic.shaped("papers100m", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    _free()
+    fan, B, sb = [15, 10, 5], 1024, 4
+    rng = np.random.default_rng(55)
+    train = torch.from_numpy(rng.choice(V, 8 * B, replace=False).astype(np.int32))
+    feat = synthetic.features(V, F, device=DEV)
+    labels = torch.randint(0, C, (V,), device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
+    cfg = host.gcn_config([F, 256, 256, C], fan, B, weight="mean", learn_rate=0.01, drop_rate=0.0,
+                          shuffle=False, pd_cache=True, pd_rate=0.2, pd_super_batch=sb,
+                          cache_rate=0.3)
+    drv = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg)
+    del feat
+    _free()
+    counts, ids = drv.presample()
+    assert len(counts) == 2
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    t = train.numpy().astype(np.uint32)
+    _, hot_ref = orc.presample(col, rows, t[:sb * B], len(fan), 0.2)
+    hot = np.array(ids[:counts[0]], np.uint32)
+    assert np.array_equal(hot, hot_ref) and hot.size > 1000
+    drv.train_batch()
+    drv.synchronize()
+    assert torch.isfinite(drv.loss).item()
+    got = drv.last_layers
+    # the first batch: the bottom layer sampled with super-batch 0's hot dsts omitted
+    od, idg = _np(G.out_degree), _np(G.in_degree)
+    omap = np.full(V, 0xFFFFFFFF, np.uint32)
+    omap[hot] = 1
+    o = orc.Sampler(col, rows, idg, od, fan, rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    o.set_omit(omap, 1)
+    ref = o.sample(t[:B], 0, orc.W_MEAN)
+    _compare_oracle(got, ref)
+    bottom = ref[-1]
+    cnt = np.diff(bottom["column_offset"].astype(np.int64))
+    om = np.isin(bottom["destination"], hot)
+    assert om.sum() > 100 and (cnt[om] == 0).all()
+    for ly in got:
+        src = ly["source"].long() & 0xFFFFFFFF
+        assert bool((src[1:] > src[:-1]).all())
+        assert bool(((ly["row_indices"].long() & 0xFFFFFFFF) < ly["src_size"]).all())
+    # every sampled id of the top two layers is a real neighbour (distinct positions)
+    _properties(G, got[:2], fan[:2], V)
+    for _ in range(5):  # through super-batch 1 (new hot set, shared embedding re-made)
+        drv.train_batch()
+    drv.synchronize()
+    assert torch.isfinite(drv.loss).item()
+    del drv, got, G, rows, col
+    _free()
+
+
 def test_c5_class_past_2e31_edges(E):
     """u64 CSC offsets: 2.3 x 10^9 edges on 2M vertices; seeds whose neighbour
     lists start past 2^31 are sampled bit-exactly vs the oracle."""
