@@ -153,6 +153,9 @@ def parse():
                    help="train on the first N seeds of this rank's shard only (0: all).  PD "
                         "cache on papers100M-shaped graphs: preSample keeps every "
                         "super-batch's hot ids (~0.7 M per super-batch there)")
+    p.add_argument("--no-secondary-af", action="store_true",
+                   help="skip the secondary measurement of the reference's bottom-layer order "
+                        "(aggregate-first, fp32 aggregation) beside a transform-first headline")
     p.add_argument("--rng", default="philox", choices=["philox", "mt", "mt-div"],
                    help="sampler stream: philox (per-dst counter streams, parallel) or mt: the "
                         "reference's single std::mt19937(2000) stream + uniform_int_distribution "
@@ -336,6 +339,39 @@ def main():
                         "unit": "sampled-edges/s", "batches_per_gpu": int(r["batches"]),
                         "note": "GPU sampler alone on its stream (3 batches in flight), all ranks"}
 
+    # ---- the reference's bottom-layer order on the same workload ------------------
+    secondary = None
+    if tf and args.model == "gcn" and not args.no_secondary_af and args.steps > 0:
+        cfg_af = host.gcn_config(layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4,
+                                 drop_rate=0.5, rng_mode=RNG_MODES[args.rng], weight=args.weight,
+                                 pipeline=not args.no_pipeline, transform_first=0,
+                                 gemm=args.gemm, deterministic_backward=not args.atomic_backward)
+        drv_af = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg_af, comm)
+
+        def step_af():
+            if not drv_af.sample_not_finished():
+                drv_af.restart()
+            drv_af.train_batch()
+
+        for _ in range(args.warmup):
+            step_af()
+        drv_af.synchronize()
+        drv_af.reset_stats()
+        barrier()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            step_af()
+        drv_af.synchronize()
+        barrier()
+        el_af = max_over_ranks(time.perf_counter() - ta)
+        secondary = {
+            "bottom_layer": "aggregate-first (A X) W, the reference's order: fp32 aggregation "
+                            "bit-exact vs MiniBatchFuseOp, split-bf16 GEMMs (fp32-accurate)",
+            "value": sum_over_ranks(float(drv_af.batch_edges)) / el_af,
+            "unit": "sampled-edges/s", "ms_per_step": el_af / args.steps * 1e3,
+            "steps": args.steps, "warmup": args.warmup}
+        del drv_af
+
     value = edges / elapsed
     rl = roofline(prof, args, layers, world)
     result = {
@@ -349,7 +385,9 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": ("fp32 (bottom-layer GEMMs on the feature table's f16 pair tables: 22-bit "
+                  "significand inputs, 3 f16 MFMA products, fp32 accumulate)"
+                  if tf and args.pair_table >= 1 else "fp32"),
         "data": "synthetic Chung-Lu power-law graph (seed 2024), N(0,1) fp32 features (seed 7), uniform labels",
         "config": {
             "workload": workload_name(args, layers, V, En, tf),
@@ -371,6 +409,7 @@ def main():
                        "power-of-two row scale, 3 f16 MFMA products, fp32 accumulate)"
                        if tf and args.pair_table >= 1 else ""),
             "layer_sizes_top_down": layer_sizes,
+            "reference_order_secondary": secondary,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
                              "workload": pmc_workload(args, layers, world)},
         },

@@ -628,162 +628,9 @@ __global__ __launch_bounds__(kH2TnThreads, 1) void k_h2_tn(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
-// v2 kernels (NTS_H2_NN=2 / NTS_H2_TN=2 select them; see the launchers):
-// every global load is compiler-visible and runs several k-steps ahead of
-// its use.  On the gathered C2 shapes the v1 kernels wait on row reads whose
-// latency under load exceeds their two-step prefetch (one step ~ 1 us of MFMA
-// work vs several us of random-row latency).
-//
-// NN v2: block = 8 waves, 2 row tiles per wave per round (as v1).  Lane (i, g)
-// loads its A fragment words A[row i][32 s + 8 g .. +7] (two 16-byte loads
-// per tile) into a ring of D register sets, D steps ahead; the B image of
-// step s (16 KB) is copied 32 bytes per thread through registers, loaded two
-// steps ahead and written to one of two LDS stages one step ahead.  One
-// barrier per step.
-template <bool EPI, bool AMAP>
-__device__ __forceinline__ void h2_nn_store(const f32x4h (&acc)[2][8], int nt, int64_t tile0, int n0,
-                                            int i, int g, int M, int N, float* __restrict__ C,
-                                            uint64_t ldc, const H2Extra& ex) {
-  float cs[8];
-#pragma unroll
-  for (int ct = 0; ct < 8; ++ct) {
-    const int col = n0 + 16 * ct + i;
-    cs[ct] = col < N ? ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[col]))) : 0.f;
-  }
-#pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
-    if (rt >= nt) continue;
-    const int64_t r4 = (tile0 + rt) * 16 + 4 * g;
-    float rsv[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const uint64_t rr = (uint64_t)(r4 + v < M ? r4 + v : M - 1);
-      rsv[v] = ex.rs[AMAP ? (uint64_t)ex.amap[rr] : rr];
-    }
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct) {
-      const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
-      if ((int)col >= N) continue;
-      float o[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) o[v] = acc[rt][ct][v] * cs[ct] * rsv[v];
-      if constexpr (EPI) {
-        const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
-        const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
-#pragma unroll
-        for (int v = 0; v < 4; ++v)
-          o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
-      }
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-        if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
-    }
-  }
-}
-
-constexpr int kH2Nn2D = 3;  // A and B prefetch depth (steps); B's LDS stages
-
-template <bool EPI, bool AMAP>
-__global__ __launch_bounds__(kH2NnThreads, 1) void k_h2_nn2(int M, int N, int K,
-                                                           const uint32_t* __restrict__ A, uint64_t lda,
-                                                           const char* __restrict__ bimg,
-                                                           float* __restrict__ C, uint64_t ldc, int rounds,
-                                                           H2Extra ex) {
-  constexpr int D = kH2Nn2D;
-  __shared__ __attribute__((aligned(16))) char sb[D][kH2Img];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.y * 128;
-  const int T = (M + 15) / 16;
-  const int64_t W = (int64_t)gridDim.x * 8;
-  const int64_t gw = (int64_t)blockIdx.x * 8 + wv;
-  const int t_lo = (int)(gw * T / W), t_hi = (int)((gw + 1) * T / W);
-  const int nsteps = K / 32;
-  const size_t bstride = (size_t)gridDim.y * kH2Img;
-  const char* bsrc = bimg + (size_t)blockIdx.y * kH2Img + 32 * tid;
-  uint4 breg[D][2];  // B image pieces, D steps ahead like A (equal distances: a wait
-                     // for one stream never forces the other's younger loads)
-  uint4 areg[D][2][2];
-  const uint32_t* arow[2];
-  f32x4h acc[2][8];
-  auto load_b = [&](int s, uint4 (&r)[2]) {
-    const uint4* p = reinterpret_cast<const uint4*>(bsrc + (size_t)min(s, nsteps - 1) * bstride);
-    r[0] = p[0];
-    r[1] = p[1];
-  };
-  auto write_b = [&](int buf, const uint4 (&r)[2]) {
-    uint4* d = reinterpret_cast<uint4*>(&sb[buf][32 * tid]);
-    d[0] = r[0];
-    d[1] = r[1];
-  };
-  for (int rd = 0; rd < rounds; ++rd) {
-    const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const int t = min(t_lo + 2 * rd + rt, T - 1);
-      const int64_t row = (int64_t)t * 16 + i;
-      const uint64_t rr = (uint64_t)(row < M ? row : M - 1);
-      arow[rt] = A + (AMAP ? (uint64_t)ex.amap[rr] : rr) * lda + 8 * g;
-    }
-    // every load is unconditional (clamped step / tile): the compiler then
-    // counts the loads in flight exactly and waits only for the ones it uses
-    auto load_a = [&](int s, uint4 (&r)[2][2]) {
-      s = min(s, nsteps - 1);
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const uint4* p = reinterpret_cast<const uint4*>(arow[rt] + 32 * s);
-        r[rt][0] = p[0];
-        r[rt][1] = p[1];
-      }
-    };
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      load_b(d, breg[d]);
-      load_a(d, areg[d]);
-    }
-    write_b(0, breg[0]);
-    // step s (j = s % D: B(s) in LDS stage j); steps past nsteps (the loop
-    // runs a multiple of D) only keep the load stream uniform
-    auto step = [&](int s, auto jc) {
-      constexpr int j = decltype(jc)::value;
-      __syncthreads();
-      write_b((j + 1) % D, breg[(j + 1) % D]);
-      load_b(s + D, breg[j]);
-      f16x8 a[2][2];
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        const uint32_t w[8] = {areg[j][rt][0].x, areg[j][rt][0].y, areg[j][rt][0].z, areg[j][rt][0].w,
-                               areg[j][rt][1].x, areg[j][rt][1].y, areg[j][rt][1].z, areg[j][rt][1].w};
-        h2_unpack(w, a[rt][0], a[rt][1]);
-      }
-      load_a(s + D, areg[j]);
-      if (s >= nsteps || nt == 0) return;
-      const char* img = sb[j];
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-        f16x8 b[2];
-        b[0] = *reinterpret_cast<const f16x8*>(img + ct * 2 * kH2Frag + 16 * lane);
-        b[1] = *reinterpret_cast<const f16x8*>(img + ct * 2 * kH2Frag + kH2Frag + 16 * lane);
-        acc[0][ct] = mfma3(a[0], b, acc[0][ct]);
-        if (nt == 2) acc[1][ct] = mfma3(a[1], b, acc[1][ct]);
-      }
-    };
-    static_assert(kH2Nn2D == 3, "the step loop below unrolls by 3");
-    for (int s = 0; s < nsteps; s += 3) {
-      step(s, std::integral_constant<int, 0>());
-      step(s + 1, std::integral_constant<int, 1>());
-      step(s + 2, std::integral_constant<int, 2>());
-    }
-    __syncthreads();  // every wave is done with sb before the next round's first write
-    h2_nn_store<EPI, AMAP>(acc, nt, (int64_t)(t_lo + 2 * rd), n0, i, g, M, N, C, ldc, ex);
-  }
-}
-
+// TN v2 (interleaved table): every global load is compiler-visible and runs
+// several k-steps ahead of its use (the v1 kernel waits on row reads whose
+// latency under load exceeds its two-step prefetch).
 // TN v2: k_h2_tn with three-deep register rings: a tile's A^T words are
 // loaded three steps before its MFMAs (and unpacked just before them), the
 // row ids of a step two steps before its loads, B rows two steps before they
@@ -976,7 +823,7 @@ __global__ __launch_bounds__(kH2TnThreads, 1) void k_h2_tn2(int M, int N, int K,
 }
 
 // ---------------------------------------------------------------------------
-// TN v3 (NTS_H2_TN=3, the default where it applies): the weight gradient of
+// TN v4 (the default where it applies): the weight gradient of
 // the transform-first bottom layer, dW = X[src]^T dH, with whole rows of the
 // "planar" pair table (per row: the y0 plane of Kp f16, then the y1 plane)
 // streamed by LDS DMA.  One block per k-chunk covers EVERY output row (up to
@@ -995,180 +842,9 @@ constexpr int kH2Tn3BPl = 16 * 256;   // one plane of the split step
 
 __device__ __forceinline__ uint32_t h2_swz(int row) { return (uint32_t)(2 * (row & 7)); }
 
-template <int TPW>
-__global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn3(int M, int K, const char* __restrict__ Q,
-                                                            uint64_t ldq, int pitch, int plane_bytes,
-                                                            const float* __restrict__ B, uint64_t ldb,
-                                                            float* __restrict__ C, uint64_t ldc, int kchunk,
-                                                            uint64_t split_stride, int nnb, H2Extra ex) {
-  extern __shared__ __attribute__((aligned(16))) char h2tn3[];
-  const int xstage = 16 * pitch;
-  char* const sx = h2tn3;                          // [3][16][pitch]
-  char* const sbr = sx + 3 * xstage;               // [3][kH2Tn3BRaw]
-  char* const sbp = sbr + 3 * kH2Tn3BRaw;          // [2 planes][kH2Tn3BPl]
-  int* const sce = reinterpret_cast<int*>(sbp + 2 * kH2Tn3BPl);  // [128] column exponents
-  uint32_t* const sid = reinterpret_cast<uint32_t*>(sce + 128);
-  float* const ssc = reinterpret_cast<float*>(sid + kchunk);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int i = lane & 15, g = lane >> 4;
-  const int nb = blockIdx.x % nnb, split = blockIdx.x / nnb;
-  const int n0 = nb * 128;
-  const int T = (M + 15) / 16;
-  const int w_lo = wv * T / 8, w_hi = (wv + 1) * T / 8, ntile = w_hi - w_lo;
-  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk), klast = kend - kbeg - 1;
-  const int nsteps = (kend - kbeg + 15) / 16;
-  for (int k = tid; k <= klast; k += kH2Tn3Threads) {
-    const uint32_t id = ex.amap ? ex.amap[kbeg + k] : (uint32_t)(kbeg + k);
-    sid[k] = id;
-    ssc[k] = ex.rs[id];
-  }
-  __syncthreads();
-  // the chunk's column scales: max |rs[row] B[row, c]| over the chunk's rows
-  // (the partial of this chunk is scaled back by its own 2^-e(col))
-  // thread t: columns 4 (t & 31) .. +3 (the B split role below), rows t >> 5 + 16 j
-  const int sr = tid >> 5, sc = 4 * (tid & 31);
-  int bexp[4];
-  {
-    float m[4] = {0.f, 0.f, 0.f, 0.f};
-    const float* bp = B + (uint64_t)kbeg * ldb + n0 + sc;
-    for (int k = sr; k <= klast; k += 64) {
-      float4 v[4];
-      float sv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int kk = min(k + 16 * u, klast);
-        v[u] = *reinterpret_cast<const float4*>(bp + (uint64_t)kk * ldb);
-        sv[u] = k + 16 * u <= klast ? fabsf(ssc[kk]) : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        m[0] = fmaxf(m[0], fabsf(v[u].x) * sv[u]);
-        m[1] = fmaxf(m[1], fabsf(v[u].y) * sv[u]);
-        m[2] = fmaxf(m[2], fabsf(v[u].z) * sv[u]);
-        m[3] = fmaxf(m[3], fabsf(v[u].w) * sv[u]);
-      }
-    }
-    float* red = reinterpret_cast<float*>(sbp);  // 16 row lanes x 128 columns (8 KB)
-    *reinterpret_cast<float4*>(red + 128 * sr + sc) = make_float4(m[0], m[1], m[2], m[3]);
-    __syncthreads();
-    if (tid < 128) {
-      float mm = 0.f;
-      for (int l = 0; l < 16; ++l) mm = fmaxf(mm, red[128 * l + tid]);
-      sce[tid] = h2_exp(mm);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
-  }
-  const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx, lsbr = (uint32_t)(uintptr_t)(lds_ptr_h)sbr;
-  const int row_chunks = 2 * plane_bytes / 16;
-  // X(s): 5 x 1 KB pieces per wave per 16-row step (16 * pitch = 40 KB for Kp 608)
-  const int xpieces = xstage / 1024 / 8;
-  auto issue = [&](int s) {
-    s = min(s, nsteps - 1);
-    const int st = s % 3;
-    for (int q = 0; q < xpieces; ++q) {
-      const int p = wv * xpieces + q;
-      const int o = 1024 * p + 16 * lane;
-      const int row = o / pitch, c = (o - row * pitch) / 16;
-      const int gc = c ^ (int)h2_swz(row);  // the global chunk this LDS slot holds
-      const uint32_t id = sid[min(16 * s + row, klast)];
-      const char* src = Q + (uint64_t)id * ldq + 16 * (gc < row_chunks ? gc : 0);
-      glds16h(src, lsx + st * xstage + 1024 * p);
-    }
-    {  // B raw: 1 KB per wave (rows 2 wv, 2 wv + 1)
-      const int row = 2 * wv + (lane >> 5);
-      const int k = kbeg + min(16 * s + row, klast);
-      glds16h(reinterpret_cast<const char*>(B + (uint64_t)k * ldb + n0) + 16 * (lane & 31),
-              lsbr + st * kH2Tn3BRaw + 1024 * wv);
-    }
-  };
-  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-  f32x4h acc[TPW][8];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t)
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct) acc[t][ct] = f32x4h{0.f, 0.f, 0.f, 0.f};
-  const int tq = (lane & 15) >> 2, tp = lane & 3;
-  const int arow = 4 * g + tq;  // the X row this lane addresses in the transposed reads
-  const uint32_t aswz = h2_swz(arow);
-  const int boff = h2_tr_off(4 * g + tq, tp >> 1) + 8 * (tp & 1);
-  issue(0);
-  issue(1);
-  for (int s = 0; s < nsteps; ++s) {
-    // X(s), B(s) landed (X(s+1), B(s+1) may stay in flight: xpieces + 1 per step)
-    if (xpieces == 5) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    raw_barrier_h();
-    issue(s + 2);
-    const int st = s % 3;
-    {  // split B(s): row sr, 4 columns
-      const float4 v = *reinterpret_cast<const float4*>(sbr + st * kH2Tn3BRaw + 512 * sr + 4 * sc);
-      const bool ok = 16 * s + sr <= klast;
-      const float scl = ssc[min(16 * s + sr, klast)];
-      const float x[4] = {v.x, v.y, v.z, v.w};
-      uint32_t w[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = ok ? h2_pair(ldexpf(x[u] * scl, bexp[u])) : 0u;
-      const uint32_t lo0 = __builtin_amdgcn_perm(w[1], w[0], 0x05040100u);
-      const uint32_t lo1 = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
-      const uint32_t hi0 = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);
-      const uint32_t hi1 = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
-      const int off = h2_tr_off(sr, sc / 8) + 8 * ((sc / 4) & 1);
-      *reinterpret_cast<uint2*>(sbp + off) = make_uint2(lo0, lo1);
-      *reinterpret_cast<uint2*>(sbp + kH2Tn3BPl + off) = make_uint2(hi0, hi1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the planes are written before the barrier
-    raw_barrier_h();
-    f16x4 bf[8][2];
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct)
-#pragma unroll
-      for (int pc = 0; pc < 2; ++pc)
-        bf[ct][pc] = __builtin_bit_cast(
-            f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4h*)(sbp + pc * kH2Tn3BPl + (boff ^ (32 * ct)))));
-    const char* xs = sx + st * xstage + arow * pitch;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      if (t >= ntile) continue;
-      f16x4 af[2];
-#pragma unroll
-      for (int pc = 0; pc < 2; ++pc) {
-        const int c = (pc * plane_bytes + 32 * (w_lo + t) + 8 * tp) / 16;
-        af[pc] = __builtin_bit_cast(
-            f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                       (lds_s16x4h*)(xs + 16 * (c ^ (int)aswz) + 8 * (tp & 1))));
-      }
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x16f16(af[1], bf[ct][0], acc[t][ct], 0, 0, 0);
-        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x16f16(af[0], bf[ct][1], acc[t][ct], 0, 0, 0);
-        acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x16f16(af[0], bf[ct][0], acc[t][ct], 0, 0, 0);
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
-  raw_barrier_h();
-  float* Cb = C + (uint64_t)split * split_stride;
-  float cs[8];
-#pragma unroll
-  for (int ct = 0; ct < 8; ++ct) cs[ct] = ldexpf(1.f, -sce[16 * ct + i]);
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    if (t >= ntile) continue;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int row = 16 * (w_lo + t) + 4 * g + v;
-      if (row >= M) continue;
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) Cb[(uint64_t)row * ldc + n0 + 16 * ct + i] = acc[t][ct][v] * cs[ct];
-    }
-  }
-}
-
-// TN v4: k_h2_tn3 on v_mfma_f32_32x32x16_f16 (full-rate f16 MFMA at K = 16;
-// the 16x16x16 form issues at the 16x16x32 form's cycles for half the work).
+// TN v4: the structure above on v_mfma_f32_32x32x16_f16 (full-rate f16 MFMA
+// at K = 16; the 16x16x16 form issues at the 16x16x32 form's cycles for half
+// the work: 232 vs 183 us at C2, measured and dropped).
 template <int TPW>
 __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const char* __restrict__ Q,
                                                             uint64_t ldq, int pitch, int plane_bytes,
@@ -1471,20 +1147,6 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 #undef NTS_NN3_ISSUE
 }
 
-// ---------------------------------------------------------------------------
-// kernel generation per GEMM (A/B): NTS_H2_NN=1|2, NTS_H2_TN=1|2
-static int h2_gen(const char* var, int dflt) {
-  const char* e = getenv(var);
-  return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : dflt;
-}
-static bool h2_nn_v1() {
-  static const bool v = h2_gen("NTS_H2_NN", 1) == 1;
-  return v;
-}
-static bool h2_tn_v1() {
-  static const bool v = h2_gen("NTS_H2_TN", 2) == 1;
-  return v;
-}
 
 static int colmax(nts_hip_ctx* ctx, const float* B, uint64_t ldb, uint64_t K, int N, const float* rs,
                   const uint32_t* amap, uint32_t* out, float* rsg = nullptr) {
@@ -1554,15 +1216,10 @@ extern "C" int nts_hip_gemm_h2_gather(nts_hip_ctx* ctx, int relu_dropout, int M,
   const dim3 grid(gx, ncb);
 #define NTS_H2NN(E, MP)                                                                          \
   do {                                                                                           \
-    if (h2_nn_v1()) {                                                                            \
-      NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn<E, MP>),            \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kH2NnLds));    \
-      hipLaunchKernelGGL((k_h2_nn<E, MP>), grid, dim3(kH2NnThreads), kH2NnLds, ctx->stream, M, N, \
-                         Kp, P, ldp, bimg, C, ldc, rounds, ex);                                  \
-    } else {                                                                                     \
-      hipLaunchKernelGGL((k_h2_nn2<E, MP>), grid, dim3(kH2NnThreads), 0, ctx->stream, M, N, Kp, P, \
-                         ldp, bimg, C, ldc, rounds, ex);                                         \
-    }                                                                                            \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn<E, MP>),              \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kH2NnLds));      \
+    hipLaunchKernelGGL((k_h2_nn<E, MP>), grid, dim3(kH2NnThreads), kH2NnLds, ctx->stream, M, N,   \
+                       Kp, P, ldp, bimg, C, ldc, rounds, ex);                                    \
   } while (0)
   if (relu_dropout) {
     if (a_rows) NTS_H2NN(true, true); else NTS_H2NN(true, false);
@@ -1593,7 +1250,7 @@ extern "C" int nts_hip_gemm_h2_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, 
   }
   // v2 (TPW 2) keeps the chunk's row ids + scales in LDS (8 B per row): past
   // 8192-row chunks (a reduction > ~700 K rows at this N) the v1 kernel runs
-  bool v1 = h2_tn_v1();
+  bool v1 = false;
   int TPW = 0, nmb = 0, splits = 0, kchunk = 0;
   const int T = (M + 15) / 16, nnb = (N + 127) / 128, ksteps = (K + 31) / 32;
   for (int pass = 0; pass < 2; ++pass) {
@@ -1674,7 +1331,7 @@ extern "C" int nts_hip_h2_split_rows_planar(nts_hip_ctx* ctx, uint64_t R, uint32
   return NTS_OK;
 }
 
-// TN v3 on the planar table (k_h2_tn3): N % 128 == 0, M <= 8 * 5 * 16 = 640,
+// TN v4 on the planar table (k_h2_tn4): N % 128 == 0, M <= 8 * 5 * 16 = 640,
 // rows of <= 640 pair words (Kp <= 640).  Scratch: [column max][row scales][partials].
 extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
                                           uint64_t ldq, int Kp, const float* rs, const uint32_t* a_rows,
@@ -1713,20 +1370,11 @@ extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K,
   H2Extra ex;  // the column scales are per chunk, computed in the kernel
   ex.amap = a_rows;
   ex.rs = rs;
-  static const bool v3 = h2_gen("NTS_H2_TN", 2) == 1;  // NTS_H2_TN=1: the 16x16x16 form (A/B)
-  if (v3) {
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn3<TPW>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL((k_h2_tn3<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
-                       reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, B, ldb,
-                       out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, nnb, ex);
-  } else {
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL((k_h2_tn4<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
-                       reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, B, ldb,
-                       out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, nnb, ex);
-  }
+  NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  hipLaunchKernelGGL((k_h2_tn4<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
+                     reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, B, ldb,
+                     out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, nnb, ex);
   NTS_LAUNCH_CHECK();
   if (splits == 1) return NTS_OK;
   return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
