@@ -102,13 +102,21 @@ constexpr uint32_t kHostBit = 0x80000000u;
 //   kAggPostMask: y = (A x) ⊙ [mx > 0] · scale with mx indexed by the OUTPUT
 //              row (the activation backward applied to the gathered sum: the
 //              graph-op backward feeding a transform-first bottom layer)
-enum { kAggPlain = 0, kAggAct = 1, kAggMask = 2, kAggPostMask = 3 };
+//   kAggColmax: kAggPlain, and the output's column maxima |y[d,:]|·cm_rs[cm_map[d]]
+//     into ax.cm_out (the f16 pair-table TN GEMM's per-column scales)
+enum { kAggPlain = 0, kAggAct = 1, kAggMask = 2, kAggPostMask = 3, kAggColmax = 4 };
 struct AggExtra {
   const float* mx = nullptr;
   uint64_t ldm = 0;
   float scale = 1.f;
   uint32_t keep_threshold = 0;
   uint64_t seed = 0, offset = 0;
+  // column maxima of the output (nts_hip_spmm_csr_bwd_colmax): cm_out[col] =
+  // max over rows d of |y[d, col]| * cm_rs[cm_map[d]], as float bits
+  // (atomicMax on the bits of non-negative floats); one pass over the columns
+  const float* cm_rs = nullptr;
+  const uint32_t* cm_map = nullptr;
+  uint32_t* cm_out = nullptr;
 };
 
 template <int VEC>
@@ -269,6 +277,8 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
   using V = VT<VEC>;
   using T = typename V::T;
   static_assert(MODE == kAggPlain || (!MAP && !TIER), "activation modes gather local rows only");
+  constexpr bool CM = MODE == kAggColmax;
+  constexpr int EM = CM ? kAggPlain : MODE;  // the gather and store proper
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
   constexpr int GPB = kAggThreads / LPD;
   const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
@@ -278,6 +288,17 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     if (threadIdx.x == 0) n_long = 0;
     __syncthreads();
   }
+  T cmv[CM ? NCH : 1];  // this lane's running column maxima (kAggColmax)
+#pragma unroll
+  for (int c = 0; c < (CM ? NCH : 1); ++c) cmv[c] = V::zero();
+  auto colmax_row = [&](const T (&acc)[NCH], uint32_t d) {
+    const float r = fabsf(ax.cm_rs[ax.cm_map[d]]);
+#pragma unroll
+    for (int c = 0; c < (CM ? NCH : 1); ++c)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        vcomp<VEC>(cmv[c], q) = fmaxf(vcomp<VEC>(cmv[c], q), fabsf(vcomp<VEC>(acc[c], q)) * r);
+  };
   for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
     const uint32_t beg = off[d], end = off[d + 1];
     if (COOP && end - beg > kLongRow<U>()) {  // summed by the whole block below
@@ -299,7 +320,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
           pm[c] = col < nv ? mrow[col] : V::zero();
         }
       }
-      gather_edges<VEC, LPD, NCH, MAP, U, TIER, MODE>(acc, beg, end, c0, sl, idx, w, x, ldx, map,
+      gather_edges<VEC, LPD, NCH, MAP, U, TIER, EM>(acc, beg, end, c0, sl, idx, w, x, ldx, map,
                                                       nv, tier, ax);
       if constexpr (MODE == kAggPostMask) {  // same arithmetic as store_row's
 #pragma unroll
@@ -310,8 +331,9 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
             v = vcomp<VEC>(pm[c], q) > 0.f ? v * ax.scale : 0.f;
           }
       }
-      store_row<VEC, LPD, NCH, MODE == kAggPostMask ? kAggPlain : MODE>(acc, d, c0, sl, nv,
-                                                                        last_valid, y, ldy, ax);
+      store_row<VEC, LPD, NCH, MODE == kAggPostMask ? kAggPlain : EM>(acc, d, c0, sl, nv,
+                                                                      last_valid, y, ldy, ax);
+      if constexpr (CM) colmax_row(acc, d);
     }
   }
   if constexpr (COOP) {
@@ -327,7 +349,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
         T acc[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; ++c) acc[c] = V::zero();
-        gather_edges<VEC, LPD, NCH, MAP, U, TIER, MODE>(acc, pb, pe, c0, sl, idx, w, x, ldx, map,
+        gather_edges<VEC, LPD, NCH, MAP, U, TIER, EM>(acc, pb, pe, c0, sl, idx, w, x, ldx, map,
                                                         nv, tier, ax);
 #pragma unroll
         for (int c = 0; c < NCH; ++c) part[(grp * NCH + c) * LPD + sl] = acc[c];
@@ -343,11 +365,33 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
             }
             acc[c] = s;
           }
-          store_row<VEC, LPD, NCH, MODE>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
+          store_row<VEC, LPD, NCH, EM>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
+          if constexpr (CM) colmax_row(acc, d);
         }
         __syncthreads();
       }
     }
+  }
+  if constexpr (CM) {
+    // the wave's column maxima (lane groups of a wave differ in the lane bits
+    // >= LPD), then an atomic only where this wave beats the running global
+    // maximum: after the first few waves almost none does.  A stale read only
+    // costs an extra atomic; the max is monotone, so the result is exact.
+    static_assert(LPD <= 64, "lane groups within one wave");
+    const uint32_t ncol = (nv - 1) * VEC + last_valid;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        float m = vcomp<VEC>(cmv[c], q);
+        for (int o = LPD; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+        const uint32_t col = (sl + c * LPD) * VEC + q;
+        if ((threadIdx.x & 63) < LPD && col < ncol && m > 0.f) {
+          const uint32_t mb = __float_as_uint(m);
+          if (__hip_atomic_load(ax.cm_out + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mb)
+            __hip_atomic_fetch_max(ax.cm_out + col, mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
   }
 }
 
@@ -554,7 +598,7 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   // float4 loads, the partial last vector reads pitch padding and stores only
   // its valid floats
   const uint32_t F4 = (F + 3) / 4 * 4;
-  if (MODE == kAggPlain && vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
+  if ((MODE == kAggPlain || MODE == kAggColmax) && vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
       (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
       (!TIER || (F4 <= tier.ldh && tier.ldh % 4 == 0 && (uintptr_t)tier.host % 16 == 0)))
     vec = 4;
@@ -618,6 +662,30 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
   return launch_gather<false, false, kAggPlain, true>(ctx->stream, row_offset, column_indices,
                                                       weight_backward, s, s_cap,
                               g_out, ld_gout, nullptr, feature_size, g_in, ld_gin);
+}
+
+int nts_hip_spmm_csr_bwd_colmax(nts_hip_ctx* ctx, const uint32_t* row_offset,
+                                const uint32_t* column_indices, const float* weight_backward,
+                                const uint32_t* s, uint32_t s_cap, const float* g_out,
+                                uint64_t ld_gout, uint32_t feature_size, float* g_in,
+                                uint64_t ld_gin, const float* rs, const uint32_t* row_map,
+                                uint32_t* colmax_bits) {
+  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && g_in && rs && row_map &&
+                    colmax_bits, "NULL argument");
+  NTS_CHECK_ARG(ld_gout >= feature_size && ld_gin >= feature_size,
+                "leading dimension < feature_size");
+  NTS_CHECK_ARG(feature_size <= 512, "column maxima: one pass over at most 512 columns");
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  NTS_HIP_TRY(hipMemsetAsync(colmax_bits, 0, (size_t)feature_size * sizeof(uint32_t), ctx->stream));
+  if (s_cap == 0 || feature_size == 0) return NTS_OK;
+  AggExtra ax;
+  ax.cm_rs = rs;
+  ax.cm_map = row_map;
+  ax.cm_out = colmax_bits;
+  return launch_gather<false, false, kAggColmax, true>(ctx->stream, row_offset, column_indices,
+                                                       weight_backward, s, s_cap, g_out, ld_gout,
+                                                       nullptr, feature_size, g_in, ld_gin,
+                                                       Tier{nullptr, nullptr, 0, 0}, ax);
 }
 
 int nts_hip_spmm_csc_fwd_act(nts_hip_ctx* ctx, const uint32_t* column_offset,

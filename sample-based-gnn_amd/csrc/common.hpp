@@ -111,6 +111,9 @@ struct nts_hip_ctx {
   void* scratch = nullptr;         // scans / radix sort temporaries
   size_t scratch_bytes = 0;
   uint32_t* mt_state = nullptr;    // 624 words + position (device)
+  uint64_t* scan_state = nullptr;  // single-pass scan tile states (epoch-tagged)
+  uint64_t scan_state_elems = 0;
+  uint32_t scan_epoch = 0;
   int gemm_mode = NTS_GEMM_F32;    // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode)
 };
 
@@ -129,12 +132,37 @@ int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T
 template <typename T>
 size_t scan_tmp_elems(uint64_t n_cap);
 
+// Single-pass exclusive scan (u32, decoupled look-back; primitives.hip):
+// out[i] = sum(in[0..i)) for i in [0, n], n = *n_dev (or n_cap).  One kernel.
+int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const uint32_t* n_dev,
+                    uint64_t n_cap, hipStream_t stream);
+int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems);
+size_t scan1_state_elems(uint64_t n_cap);
+
+// The sampler's per-dst counts fused into that scan: co[i] = min(deg(dst[i]),
+// fanout) (0 for an omitted dst), exclusive-scanned; sizes[0] = v,
+// sizes[1] = min(co[v], e_cap), overflow flags in sizes[3].
+struct CountArgs {
+  const uint64_t* goff;
+  const uint32_t* dst;
+  const uint32_t* v_in;
+  uint32_t v_cap;
+  int fanout;
+  uint32_t* sizes;
+  uint32_t e_cap;
+  const uint32_t* omit_map;
+  uint32_t omit_key;
+  const uint32_t* omit_loc;
+  uint32_t* omit_row;
+};
+int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream);
+
 // Stable LSD radix sort of (key, value) pairs on the low `bits` key bits.
 // n = *n_dev (or n_cap).  vals_in == nullptr means values = 0..n-1.
 // Result lands in keys_out/vals_out.  tmp: radix_tmp_bytes(n_cap).
 int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap,
-                     uint32_t bits, void* tmp, hipStream_t stream);
+                     uint32_t bits, void* tmp, hipStream_t stream, nts_hip_ctx* ctx = nullptr);
 size_t radix_tmp_bytes(uint64_t n_cap);
 
 // C[M x N] = sum of `splits` partial slabs [M x N] (ld N, `stride` floats

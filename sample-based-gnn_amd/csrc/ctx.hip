@@ -44,6 +44,19 @@ int ensure_scratch(nts_hip_ctx* ctx, size_t bytes) {
   return NTS_OK;
 }
 
+// Tile states of the single-pass scan: zeroed once (epoch 0 is never issued).
+int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems) {
+  if (elems <= ctx->scan_state_elems) return NTS_OK;
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (ctx->scan_state) NTS_HIP_TRY(hipFree(ctx->scan_state));
+  ctx->scan_state = nullptr;
+  const uint64_t n = elems + elems / 4 + 64;
+  NTS_HIP_TRY(hipMalloc(&ctx->scan_state, n * sizeof(uint64_t)));
+  NTS_HIP_TRY(hipMemset(ctx->scan_state, 0, n * sizeof(uint64_t)));
+  ctx->scan_state_elems = n;
+  return NTS_OK;
+}
+
 // std::mt19937 seeding (init_genrand): sequential, done on the host.
 static void mt_seed_host(uint64_t seed, uint32_t* st) {
   st[0] = (uint32_t)seed;
@@ -91,6 +104,7 @@ int nts_hip_ctx_destroy(nts_hip_ctx* ctx) {
   if (ctx->src_index) (void)hipFree(ctx->src_index);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->mt_state) (void)hipFree(ctx->mt_state);
+  if (ctx->scan_state) (void)hipFree(ctx->scan_state);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return NTS_OK;
@@ -127,6 +141,8 @@ int nts_hip_ctx_reserve(nts_hip_ctx* ctx, uint64_t n_vertices, uint64_t max_item
   size_t need = radix_tmp_bytes(items);
   size_t s64 = scan_tmp_elems<uint64_t>(items + 1) * sizeof(uint64_t) + 256;
   if (s64 > need) need = s64;
+  // the radix sort's histogram scan is the largest single-pass scan
+  NTS_RET(ensure_scan_state(ctx, scan1_state_elems(512 * (items / 4096 + 1))));
   return ensure_scratch(ctx, need);
 }
 

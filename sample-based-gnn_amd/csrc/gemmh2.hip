@@ -876,7 +876,12 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
   // thread t: columns 4 (t & 31) .. +3 (the B split role below), rows t >> 5 + 16 j
   const int sr = tid >> 5, sc = 4 * (tid & 31);
   int bexp[4];
-  {
+  if (ex.cmax) {  // global column maxima from dH's producer (nts_hip_spmm_csr_bwd_colmax)
+    if (tid < 128) sce[tid] = h2_exp(__uint_as_float(ex.cmax[n0 + tid]));
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
+  } else {
     float m[4] = {0.f, 0.f, 0.f, 0.f};
     const float* bp = B + (uint64_t)kbeg * ldb + n0 + sc;
     for (int k = sr; k <= klast; k += 64) {
@@ -1333,9 +1338,9 @@ extern "C" int nts_hip_h2_split_rows_planar(nts_hip_ctx* ctx, uint64_t R, uint32
 
 // TN v4 on the planar table (k_h2_tn4): N % 128 == 0, M <= 8 * 5 * 16 = 640,
 // rows of <= 640 pair words (Kp <= 640).  Scratch: [column max][row scales][partials].
-extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
-                                          uint64_t ldq, int Kp, const float* rs, const uint32_t* a_rows,
-                                          const float* B, uint64_t ldb, float* C, uint64_t ldc) {
+static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q, uint64_t ldq, int Kp,
+                         const float* rs, const uint32_t* a_rows, const float* B, uint64_t ldb, float* C,
+                         uint64_t ldc, const uint32_t* colmax_bits) {
   constexpr int TPW = 5;
   NTS_CHECK_ARG(ctx, "NULL context");
   NTS_CHECK_ARG(M > 0 && M <= 8 * TPW * 16 && N > 0 && N % 128 == 0 && K >= 0, "shape");
@@ -1367,9 +1372,10 @@ extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K,
     out = (float*)ctx->scratch;
     ldo = N;
   }
-  H2Extra ex;  // the column scales are per chunk, computed in the kernel
+  H2Extra ex;  // column scales: the producer's global maxima, else per chunk in the kernel
   ex.amap = a_rows;
   ex.rs = rs;
+  ex.cmax = colmax_bits;
   NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   hipLaunchKernelGGL((k_h2_tn4<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
@@ -1378,6 +1384,23 @@ extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K,
   NTS_LAUNCH_CHECK();
   if (splits == 1) return NTS_OK;
   return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+}
+
+extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
+                                          uint64_t ldq, int Kp, const float* rs, const uint32_t* a_rows,
+                                          const float* B, uint64_t ldb, float* C, uint64_t ldc) {
+  return h2p_tn_gather(ctx, M, N, K, Q, ldq, Kp, rs, a_rows, B, ldb, C, ldc, nullptr);
+}
+
+// as nts_hip_gemm_h2p_tn_gather with B's column maxima precomputed (the bits of
+// max_k |rs[a_rows[k]] B[k, c]|, N words, e.g. by nts_hip_spmm_csr_bwd_colmax):
+// the kernel skips its per-chunk pre-pass over B (one read of B instead of two)
+extern "C" int nts_hip_gemm_h2p_tn_gather_cm(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
+                                             uint64_t ldq, int Kp, const float* rs,
+                                             const uint32_t* a_rows, const float* B, uint64_t ldb,
+                                             float* C, uint64_t ldc, const uint32_t* colmax_bits) {
+  NTS_CHECK_ARG(colmax_bits, "NULL column maxima");
+  return h2p_tn_gather(ctx, M, N, K, Q, ldq, Kp, rs, a_rows, B, ldb, C, ldc, colmax_bits);
 }
 
 // NN v3 on the planar table (k_h2_nn3): N % 128 == 0, Kp <= 640.  The W image

@@ -12,7 +12,7 @@
 //   k_pd_set_cache             — set_cache_index (cache_map, cache_location)
 //   k_pd_load_share            — dev_load_share_embedding_kernel
 //   k_relu_dropout             — vertexForward's activation after the overwrite
-// The omitted sampling itself is k_count's omit_map (sampler.hip).
+// The omitted sampling itself is count_scan's omit_map (primitives.hip, sampler.hip).
 #include "common.hpp"
 
 namespace nts_hip {

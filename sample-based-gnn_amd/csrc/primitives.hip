@@ -166,6 +166,198 @@ int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T
   return NTS_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Single-pass exclusive scan (u32) with decoupled look-back: one kernel where
+// scan_exclusive needs two.  Tile t publishes its aggregate, then its
+// inclusive prefix once the look-back over tiles t-1, t-2, ... has found an
+// inclusive prefix; tile states are 64-bit words {epoch:30 | kind:2 |
+// value:32} written and read with RELAXED agent-scope atomics: each word
+// carries its own value, so no other data needs ordering (acquire/release
+// would add an L2 invalidate / write-back per access — buffer_inv sc1 and
+// buffer_wbl2 sc1 — which cost the whole XCD its L2, measured 34 us a call).  The epoch (a per-call
+// sequence number) makes states of earlier calls invalid, so nothing is reset
+// between calls.  A tile only waits on lower-numbered tiles; workgroups are
+// dispatched in index order on each XCD, so the lowest unfinished tile is
+// always resident and the chain completes.
+// COUNT: the input is not read from memory but computed per item as the
+// sampler's per-dst count min(deg(dst[i]), fanout) (init_co_only,
+// core/FullyRepGraph.hpp:530-539), with the omit map of sample_gpu_fast_omit
+// (core/ntsFastSampler.hpp:711-915) — k_count fused into the scan.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kTileAgg = 1, kTileIncl = 2;
+
+__device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint64_t kind, uint32_t v) {
+  return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | (kind << 32) | v;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restrict__ in,
+                                                        uint32_t* __restrict__ out,
+                                                        const uint32_t* n_dev, uint64_t n_cap,
+                                                        uint64_t* __restrict__ state,
+                                                        uint32_t epoch, CountArgs ca) {
+  __shared__ uint32_t tile[kScanTile + kScanTile / 16];
+  __shared__ uint32_t wsum[kScanThreads / kWave];
+  __shared__ uint32_t s_prefix;
+  const int t = threadIdx.x, lane = t & 63;
+  uint64_t n;
+  if (COUNT) {
+    const uint32_t v_req = *ca.v_in;
+    n = min(v_req, ca.v_cap);
+    if (blockIdx.x == 0 && t == 0) {
+      ca.sizes[0] = (uint32_t)n;
+      ca.sizes[3] = v_req > ca.v_cap ? 1u : 0u;
+    }
+  } else {
+    n = n_dev ? (uint64_t)*n_dev : n_cap;
+  }
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  if (base > n) return;  // every tile up to the one holding out[n] runs the chain
+  if constexpr (COUNT) {
+    // three rounds of independent loads (dst ids, their offsets, the omit
+    // map) instead of one dependent chain per item
+    uint32_t d[kScanItems];
+    uint64_t lo[kScanItems], hi[kScanItems];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+      d[k] = i < n ? ca.dst[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+      lo[k] = i < n ? ca.goff[d[k]] : 0u;
+      hi[k] = i < n ? ca.goff[d[k] + 1] : 0u;
+    }
+    uint32_t x[kScanItems];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const uint32_t deg = (uint32_t)(hi[k] - lo[k]);
+      x[k] = ca.fanout < 0 ? deg : min(deg, (uint32_t)ca.fanout);
+    }
+    if (ca.omit_map) {
+#pragma unroll
+      for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+        if (i < n) {
+          const bool om = ca.omit_map[d[k]] == ca.omit_key;
+          if (om) x[k] = 0;
+          if (ca.omit_row) ca.omit_row[i] = om ? ca.omit_loc[d[k]] : 0xFFFFFFFFu;
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) tile[pad_idx(k * kScanThreads + t)] = x[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const uint32_t j = k * kScanThreads + t;
+      const uint64_t i = base + j;
+      tile[pad_idx(j)] = i < n ? in[i] : 0u;
+    }
+  }
+  __syncthreads();
+  uint32_t v[kScanItems];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    v[k] = tile[pad_idx(t * kScanItems + k)];
+    s += v[k];
+  }
+  uint32_t agg;
+  const uint32_t ex = block_excl_scan(s, wsum, &agg);
+  // publish, look back (wave 0, lanes over 64 predecessors at a time)
+  if (t < kWave) {
+    if (blockIdx.x == 0) {
+      if (t == 0) {
+        __hip_atomic_store(state, tile_word(epoch, kTileIncl, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = 0;
+      }
+    } else {
+      if (t == 0)
+        __hip_atomic_store(state + blockIdx.x, tile_word(epoch, kTileAgg, agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t prefix = 0;
+      int64_t top = (int64_t)blockIdx.x - 1;  // highest tile not yet folded in
+      for (;;) {
+        const int64_t p = top - lane;
+        uint64_t w = 0;
+        uint32_t kind = 0;
+        if (p >= 0) {
+          for (;;) {  // this lane's tile has published (under this epoch)
+            w = __hip_atomic_load(state + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(w >> 34) == (epoch & 0x3FFFFFFFu)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          kind = (uint32_t)((w >> 32) & 3u);
+        }
+        // lanes 0.. up to (and including) the first inclusive one
+        const uint64_t inc = __ballot(p >= 0 && kind == kTileIncl);
+        const int stop = inc ? __ffsll((long long)inc) - 1 : kWave;
+        uint32_t add = (lane <= stop && p >= 0) ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, kWave);
+        prefix += add;
+        if (inc || top - kWave < 0) break;
+        top -= kWave;
+      }
+      if (t == 0) {
+        __hip_atomic_store(state + blockIdx.x, tile_word(epoch, kTileIncl, prefix + agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = prefix;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t run = ex + s_prefix;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    tile[pad_idx(t * kScanItems + k)] = run;
+    run += v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint32_t j = k * kScanThreads + t;
+    const uint64_t i = base + j;
+    if (i <= n) out[i] = tile[pad_idx(j)];
+    if (COUNT && i == n) {  // e_size = co[v], clamped to the edge capacity
+      const uint32_t e = tile[pad_idx(j)];
+      ca.sizes[1] = min(e, ca.e_cap);
+      if (e > ca.e_cap) atomicOr(&ca.sizes[3], 1u);
+    }
+  }
+}
+
+size_t scan1_state_elems(uint64_t n_cap) { return (n_cap / kScanTile + 1 + 63) / 64 * 64; }
+
+static uint32_t next_epoch(nts_hip_ctx* ctx) {
+  ctx->scan_epoch = (ctx->scan_epoch + 1) & 0x3FFFFFFFu;
+  if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;  // 0: the state words' initial value
+  return ctx->scan_epoch;
+}
+
+int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const uint32_t* n_dev,
+                    uint64_t n_cap, hipStream_t stream) {
+  const uint64_t nb = n_cap / kScanTile + 1;
+  NTS_RET(ensure_scan_state(ctx, scan1_state_elems(n_cap)));
+  hipLaunchKernelGGL(k_scan1<false>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, in, out,
+                     n_dev, n_cap, ctx->scan_state, next_epoch(ctx), CountArgs{});
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream) {
+  const uint64_t nb = (uint64_t)ca.v_cap / kScanTile + 1;
+  NTS_RET(ensure_scan_state(ctx, scan1_state_elems(ca.v_cap)));
+  hipLaunchKernelGGL(k_scan1<true>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, nullptr,
+                     co, nullptr, (uint64_t)ca.v_cap, ctx->scan_state, next_epoch(ctx), ca);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
 template int scan_exclusive<uint32_t>(const uint32_t*, uint32_t*, const uint32_t*, uint64_t,
                                       uint32_t*, hipStream_t);
 template int scan_exclusive<uint64_t>(const uint64_t*, uint64_t*, const uint32_t*, uint64_t,
@@ -326,7 +518,7 @@ size_t radix_tmp_bytes(uint64_t n_cap) {
 
 int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t bits,
-                     void* tmp, hipStream_t stream) {
+                     void* tmp, hipStream_t stream, nts_hip_ctx* ctx) {
   if (n_cap == 0) return NTS_OK;
   uint32_t nb = ceil_div(n_cap, kRadixTile);
   uint64_t n_al = (n_cap + 63) / 64 * 64;
@@ -349,7 +541,10 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev,
                        n_cap, shift, mask, hist, nb);
     NTS_LAUNCH_CHECK();
-    NTS_RET(scan_exclusive<uint32_t>(hist, hist, nullptr, hist_n, stmp, stream));
+    if (ctx)  // one kernel (single-pass look-back scan on the context's tile states)
+      NTS_RET(scan1_exclusive(ctx, hist, hist, nullptr, hist_n, stream));
+    else
+      NTS_RET(scan_exclusive<uint32_t>(hist, hist, nullptr, hist_n, stmp, stream));
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc,
                        kdst, vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb);
     NTS_LAUNCH_CHECK();

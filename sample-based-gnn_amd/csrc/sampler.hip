@@ -71,49 +71,12 @@ struct Draw {
 // ---------------------------------------------------------------------------
 // per-layer kernels
 // ---------------------------------------------------------------------------
-// omit_map (sample_gpu_fast_omit, core/ntsFastSampler.hpp:711-915, kernel
-// sample_processing_get_co_gpu_kernel_omit cuda/ntsCUDATransferKernel.cuh:795-818):
-// a dst with omit_map[dst] == omit_key samples no neighbours (its bottom-layer
-// embedding comes from the PD cache)
-__global__ void k_count(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
-                        const uint32_t* v_in, uint32_t v_cap, int fanout,
-                        uint32_t* __restrict__ co, uint32_t* sizes,
-                        const uint32_t* __restrict__ omit_map, uint32_t omit_key,
-                        const uint32_t* __restrict__ omit_loc, uint32_t* __restrict__ omit_row) {
-  const uint32_t v_req = *v_in;
-  const uint32_t v = min(v_req, v_cap);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    sizes[0] = v;
-    sizes[3] = (v_req > v_cap) ? 1u : 0u;
-  }
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < v; i += gridDim.x * blockDim.x) {
-    uint32_t d = dst[i];
-    uint32_t deg = (uint32_t)(goff[d + 1] - goff[d]);
-    if (omit_map) {
-      const bool om = omit_map[d] == omit_key;
-      if (om) deg = 0;
-      if (omit_row) omit_row[i] = om ? omit_loc[d] : 0xFFFFFFFFu;
-    }
-    co[i] = (fanout < 0) ? deg : min(deg, (uint32_t)fanout);
-  }
-}
-
-// e_size = co[v] (clamped to e_cap, overflow flagged): done by the first
-// thread of the selection kernel, which runs after the scan of co — one
-// dependent launch less per layer than a kernel of its own.
-__device__ __forceinline__ void finish_count(const uint32_t* co, uint32_t e_cap, uint32_t* sizes) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  const uint32_t e = co[sizes[0]];
-  sizes[1] = min(e, e_cap);
-  if (e > e_cap) sizes[3] = 1u;
-}
-
 struct SelectArgs {
   const uint64_t* goff;
   const uint32_t* grows;
   const uint32_t* dst;
   const uint32_t* co;
-  uint32_t* sizes;  // reads [0]; the first thread writes [1] and the overflow flag
+  uint32_t* sizes;  // [0] v, [1] e (count_scan wrote them)
   uint32_t* ans;
   uint32_t* edst;
   uint8_t* marks;
@@ -187,11 +150,121 @@ __device__ __forceinline__ uint32_t select_distinct(const SelectArgs& a, uint32_
   return consumed;
 }
 
+// ---- fanout > kSetCap: distinct positions through an LDS hash set --------
+// The reference CPU sampler takes any fanout (core/ntsFastSampler.hpp:1028-1048;
+// its GPU path falls back to the first k neighbours past 1024,
+// cuda/ntsCUDATransferKernel.cuh:852-881).  Same result as select_distinct —
+// the first `need` distinct accepted draws, in draw order — with the kept
+// positions in an open-addressing set (key = position + 1, 0 = empty, linear
+// probing, capacity a power of two >= 2 x need) instead of a list scanned per
+// candidate; repeats inside one 64-word round by lane shuffles.
+constexpr uint32_t kBigFanoutMax = 16384;  // hash capacity 32 K words = 128 KB of LDS
+
+__device__ __forceinline__ uint32_t pos_hash(uint32_t v, uint32_t mask) {
+  return (v * 0x9E3779B1u) >> 7 & mask;
+}
+__device__ __forceinline__ bool hset_has(const uint32_t* h, uint32_t mask, uint32_t v) {
+  for (uint32_t s = pos_hash(v, mask);; s = (s + 1) & mask) {
+    const uint32_t k = h[s];
+    if (k == v + 1) return true;
+    if (k == 0) return false;
+  }
+}
+__device__ __forceinline__ void hset_put(uint32_t* h, uint32_t mask, uint32_t v) {
+  for (uint32_t s = pos_hash(v, mask);; s = (s + 1) & mask) {
+    const uint32_t old = atomicCAS(&h[s], 0u, v + 1);
+    if (old == 0 || old == v + 1) return;
+  }
+}
+
+// draws for one dst into out[0 .. need) (positions), whole wave; returns the
+// words consumed.  The set (cap words) must be all zeros; it is zeroed again.
+template <typename WordFn>
+__device__ uint32_t select_distinct_hashed(uint32_t need, uint32_t* hset, uint32_t cap, int lane,
+                                           uint32_t deg, uint32_t thr, bool lemire, uint32_t* out,
+                                           WordFn word) {
+  const uint32_t mask = cap - 1;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t count = 0, consumed = 0;
+  while (count < need) {
+    const uint32_t remaining = need - count;
+    uint32_t val = 0;
+    bool ok;
+    const uint32_t x = word(consumed + lane);
+    if (lemire) {
+      const uint64_t m = (uint64_t)x * deg;
+      val = (uint32_t)(m >> 32);
+      ok = (uint32_t)m >= thr;
+    } else {
+      val = x / thr;
+      ok = x < deg * thr;
+    }
+    bool dup = ok && hset_has(hset, mask, val);
+    const uint64_t okmask = __ballot(ok);
+    for (int j = 0; j < kWave; ++j) {
+      const uint32_t vj = __shfl(val, j, kWave);
+      dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
+    }
+    const uint64_t newmask = __ballot(ok && !dup);
+    uint64_t take = newmask;
+    if ((uint32_t)__popcll(newmask) >= remaining) {
+      uint64_t m = newmask;
+      for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+      const int last = __ffsll((long long)m) - 1;
+      take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
+      consumed += (uint32_t)last + 1u;
+    } else {
+      consumed += (uint32_t)kWave;
+    }
+    if ((take >> lane) & 1ull) {
+      hset_put(hset, mask, val);
+      out[count + (uint32_t)__popcll(take & lt_mask)] = val;
+    }
+    count += (uint32_t)__popcll(take);
+    __syncthreads();  // the puts land before the next round's probes
+  }
+  for (uint32_t k = lane; k < cap; k += kWave) hset[k] = 0u;
+  __syncthreads();
+  return consumed;
+}
+
+// PHILOX, fanout > kSetCap: one wave per block (the hash set takes the LDS).
+// Positions go to ans first (in place), then to neighbour ids.
+__global__ __launch_bounds__(kWave) void k_select_philox_big(SelectArgs a, uint32_t cap) {
+  extern __shared__ uint32_t hset[];
+  const int lane = threadIdx.x;
+  for (uint32_t k = lane; k < cap; k += kWave) hset[k] = 0u;
+  __syncthreads();
+  const uint32_t v = a.sizes[0];
+  for (uint32_t i = blockIdx.x; i < v; i += gridDim.x) {
+    const uint32_t d = a.dst[i];
+    const uint64_t beg = a.goff[d];
+    const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
+    const uint32_t c = a.co[i];
+    const uint32_t n = a.co[i + 1] - c;
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by count_scan)
+    if (n == deg) {
+      copy_all(a, i, beg, deg, c, lane);
+      continue;
+    }
+    if (n == 0) continue;
+    const uint64_t seed = a.seed, bs = a.batch_seq;
+    const uint32_t layer = a.layer;
+    select_distinct_hashed(n, hset, cap, lane, deg, (0u - deg) % deg, true, a.ans + c,
+                           [&](uint32_t j) { return philox_word(seed, d, layer, bs, j); });
+    for (uint32_t k = lane; k < n; k += kWave) {
+      const uint32_t g = a.grows[beg + a.ans[c + k]];
+      a.ans[c + k] = g;
+      a.edst[c + k] = i;
+      a.marks[g] = 1;
+    }
+  }
+}
+
 // PHILOX: one wave per destination, grid-stride.
 __global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
   __shared__ uint32_t sets[kSelWaves][kSetCap];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  finish_count(a.co, a.e_cap, a.sizes);
   const uint32_t v = a.sizes[0];
   uint32_t* set = sets[w];
   const uint32_t nw = gridDim.x * kSelWaves;
@@ -201,7 +274,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
     const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
     const uint32_t c = a.co[i];
     const uint32_t n = a.co[i + 1] - c;
-    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by finish_count)
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by count_scan)
     if (n == deg) {
       copy_all(a, i, beg, deg, c, lane);
     } else if (n > 0) {
@@ -233,7 +306,6 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a)
   uint32_t* set = sets[gib];
   const uint32_t gshift = kGrp * grp;
   const uint32_t lt16 = (1u << gl) - 1u;
-  finish_count(a.co, a.e_cap, a.sizes);
   const uint32_t v = a.sizes[0];
   const uint32_t ng = gridDim.x * kSelWaves * kGrpPerWave;
   for (uint32_t i = blockIdx.x * kSelWaves * kGrpPerWave + gib; i < v; i += ng) {
@@ -242,7 +314,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a)
     const uint32_t deg = (uint32_t)(a.goff[d + 1] - beg);
     const uint32_t c = a.co[i];
     const uint32_t n = a.co[i + 1] - c;
-    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by finish_count)
+    if (c + n > a.e_cap) continue;  // capacity overflow (flagged by count_scan)
     if (n == deg) {
       for (uint32_t k = gl; k < deg; k += kGrp) {
         const uint32_t g = a.grows[beg + k];
@@ -345,10 +417,16 @@ struct MtInfo {
   uint32_t c, n, deg, thr;  // column offset, draws (0: none), range, Lemire threshold
 };
 
+// nn / cstat (chunked resolver, may be null): the draws per dst, and per
+// chunk of kMtChunkP dsts the expected extra words (repeats) and their
+// variance: drawing the k-th distinct of `deg` positions takes a geometric
+// number of words with success (deg - k) / deg — mean extra k / (deg - k),
+// variance k deg / (deg - k)^2 (rejections, p < deg / 2^32, neglected).
+constexpr uint32_t kMtChunkP = 256;
 __global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
                           const uint32_t* __restrict__ co, uint32_t* sizes, uint32_t e_cap,
-                          int lemire, uint4* __restrict__ info) {
-  finish_count(co, e_cap, sizes);
+                          int lemire, uint4* __restrict__ info, uint32_t* __restrict__ nn,
+                          float2* __restrict__ cstat) {
   const uint32_t v = sizes[0];
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < v; i += gridDim.x * blockDim.x) {
     const uint32_t d = dst[i];
@@ -359,6 +437,20 @@ __global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __r
     uint32_t thr = 0;
     if (draw) thr = lemire ? (0u - deg) % deg : 0xFFFFFFFFu / deg;  // DIV: `scaling`
     info[i] = make_uint4(c, draw ? n : 0u, deg, thr);
+    if (nn) {
+      nn[i] = draw ? n : 0u;
+      if (draw) {
+        float m = 0.f, var = 0.f;
+        const float fd = (float)deg;
+        for (uint32_t k = 1; k < n; ++k) {
+          const float r = fd - (float)k;
+          m += (float)k / r;
+          var += (float)k * fd / (r * r);
+        }
+        atomicAdd(&cstat[i / kMtChunkP].x, m);
+        atomicAdd(&cstat[i / kMtChunkP].y, var);
+      }
+    }
   }
 }
 
@@ -369,20 +461,30 @@ __device__ __forceinline__ uint32_t mt_word(const uint32_t* tw, int cur, uint32_
   return tw[k];
 }
 
+// The word source of the MT19937 walks: either the generator itself (raw
+// != nullptr: two 624-word blocks in LDS, the next one twisted on demand) or
+// a flat array of already tempered words (raw == nullptr: the chunked
+// resolver's words, generated in bulk by k_mtp_gen), word r at tw[r].
 struct MtStream {
   uint32_t* raw;  // [2][624] std::mt19937::_M_x of the current / next block
-  uint32_t* tw;   // [2][624] tempered copies
+  const uint32_t* tw;  // [2][624] tempered copies (flat: every word of the walk)
   int cur;
-  uint32_t q0;    // _M_p within block `cur`
+  uint32_t q0;    // _M_p within block `cur` (flat: the next word's index)
   bool have_next;
+  __device__ __forceinline__ uint32_t word(uint32_t r) const {
+    if (!raw) return tw[r];
+    return mt_word(tw, cur, r);
+  }
   // make words [q0, q0 + 64) available (twists the next block on demand)
   __device__ __forceinline__ void ensure(int lane) {
+    if (!raw) return;
+    uint32_t* twm = const_cast<uint32_t*>(tw);
     for (;;) {
       if (q0 >= 624) {
         if (!have_next) {
           mt_twist(raw + cur * 624, raw + (cur ^ 1) * 624, lane);
           for (int k = lane; k < 624; k += kWave)
-            tw[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
+            twm[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
           __syncthreads();
         }
         cur ^= 1;
@@ -393,7 +495,7 @@ struct MtStream {
       if (q0 + kWave > 624 && !have_next) {
         mt_twist(raw + cur * 624, raw + (cur ^ 1) * 624, lane);
         for (int k = lane; k < 624; k += kWave)
-          tw[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
+          twm[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
         __syncthreads();
         have_next = true;
       }
@@ -425,7 +527,7 @@ __device__ void mt_exact(MtStream& s, uint32_t* set, uint32_t* ans, uint32_t c, 
     const int R = remaining <= 12 ? 16 : (remaining <= 28 ? 32 : 64);
     uint32_t val = 0;
     bool ok = false;
-    if (lane < R) ok = mt_apply(mt_word(s.tw, s.cur, s.q0 + lane), deg, thr, lemire, val);
+    if (lane < R) ok = mt_apply(s.word(s.q0 + lane), deg, thr, lemire, val);
     bool dup = false;
     for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
     const uint64_t okmask = __ballot(ok);
@@ -464,15 +566,15 @@ constexpr uint32_t kMtTaken = 0xFFFFFFFEu;  // exact path: position already kept
 // lane of the round drew it (sentinel + ds_min of lane ids, as the fast
 // path).  Kept positions are marked, and unmarked when the dst is done, so
 // the table holds no marks between dsts.
-__device__ void mt_exact_tab(MtStream& s, uint32_t* tab, uint32_t* set, uint32_t* out, uint32_t n,
-                             uint32_t deg, uint32_t thr, bool lemire, int lane) {
+__device__ void mt_exact_tab(MtStream& s, uint32_t* tab, uint32_t* out, uint32_t n, uint32_t deg,
+                             uint32_t thr, bool lemire, int lane) {
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t count = 0;
   while (count < n) {
     s.ensure(lane);
     const uint32_t remaining = n - count;
     uint32_t val = 0;
-    bool ok = mt_apply(mt_word(s.tw, s.cur, s.q0 + lane), deg, thr, lemire, val);
+    bool ok = mt_apply(s.word(s.q0 + lane), deg, thr, lemire, val);
     if (ok) ok = tab[val] != kMtTaken;
     if (ok) tab[val] = 0xFFFFFFFFu;
     if (ok) atomicMin(&tab[val], (uint32_t)lane);
@@ -489,61 +591,137 @@ __device__ void mt_exact_tab(MtStream& s, uint32_t* tab, uint32_t* set, uint32_t
       s.q0 += (uint32_t)kWave;
     }
     if ((take >> lane) & 1ull) {
-      const uint32_t slot = count + (uint32_t)__popcll(take & lt_mask);
       tab[val] = kMtTaken;
-      set[slot] = val;
-      out[slot] = val;
+      out[count + (uint32_t)__popcll(take & lt_mask)] = val;
     }
     count += (uint32_t)__popcll(take);
   }
-  for (uint32_t k = lane; k < n; k += kWave) tab[set[k]] = 0u;
+  __syncthreads();  // out (LDS or global) written before it is read back
+  for (uint32_t k = lane; k < n; k += kWave) tab[out[k]] = 0u;
+  __syncthreads();
 }
+
+// Exact path for deg > kMtTab and n > kSetCap: the kept positions in `tab`
+// used as an open-addressing set (select_distinct_hashed's), n <= kMtTab / 2.
+__device__ void mt_exact_hashed(MtStream& s, uint32_t* tab, uint32_t* out, uint32_t n,
+                                uint32_t deg, uint32_t thr, bool lemire, int lane) {
+  const uint32_t mask = kMtTab - 1;
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (uint32_t k = lane; k < kMtTab; k += kWave) tab[k] = 0u;
+  __syncthreads();
+  uint32_t count = 0;
+  while (count < n) {
+    s.ensure(lane);
+    const uint32_t remaining = n - count;
+    uint32_t val = 0;
+    const bool ok = mt_apply(s.word(s.q0 + lane), deg, thr, lemire, val);
+    bool dup = ok && hset_has(tab, mask, val);
+    const uint64_t okmask = __ballot(ok);
+    for (int j = 0; j < kWave; ++j) {
+      const uint32_t vj = __shfl(val, j, kWave);
+      dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
+    }
+    const uint64_t newmask = __ballot(ok && !dup);
+    uint64_t take = newmask;
+    if ((uint32_t)__popcll(newmask) >= remaining) {
+      uint64_t m = newmask;
+      for (uint32_t t = 1; t < remaining; ++t) m &= m - 1;
+      const int last = __ffsll((long long)m) - 1;
+      take = newmask & ((last == 63) ? ~0ull : ((2ull << last) - 1ull));
+      s.q0 += (uint32_t)last + 1u;
+    } else {
+      s.q0 += (uint32_t)kWave;
+    }
+    if ((take >> lane) & 1ull) {
+      hset_put(tab, mask, val);
+      out[count + (uint32_t)__popcll(take & lt_mask)] = val;
+    }
+    count += (uint32_t)__popcll(take);
+    __syncthreads();
+  }
+  for (uint32_t k = lane; k < kMtTab; k += kWave) tab[k] = 0u;
+  __syncthreads();
+}
+
 constexpr uint32_t kMtInfo = 2048;  // per-dst info staged in LDS
 constexpr uint32_t kMtPos = 8192;   // kept positions staged in LDS before the flush
+// chunked resolver (fanout <= 32): dsts per chunk, words staged per chunk
+constexpr uint32_t kMtChunk = 256;
+constexpr uint32_t kMtStage = 12288;
 
 // The hot loop issues no vector-memory instruction: on gfx9 one vmcnt counter
 // covers loads and stores, so a loop-carried global load (the next dsts'
 // info) would wait for every position store of the iteration before it.
 // Per-dst info arrives in 2048-dst chunks and kept positions leave in
 // ~7 K-word flushes, both through LDS.
-template <int G>
+// FLAT (the chunked resolver's replay, one block per chunk of kMtChunk dsts):
+// the chunk's exact entry word is known (k_mtp_resolve), its words come from
+// the bulk-generated stream (staged in LDS when they fit), and no generator
+// state is kept.
+struct MtChunked {
+  const uint32_t* words;    // tempered words of the layer (k_mtp_gen)
+  const uint32_t* base;     // [v + 1] exclusive scan of the draws n
+  const uint32_t* entries;  // [chunks + 1] extra words consumed before each chunk
+};
+
+template <int G, bool FLAT>
 __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ info,
                                                      const uint32_t* sizes,
                                                      uint32_t* __restrict__ ans,
-                                                     uint32_t* mt_state, int lemire_i, int dbg) {
+                                                     uint32_t* mt_state, int lemire_i, int dbg,
+                                                     MtChunked ch) {
   constexpr int K = kWave / G;
   uint64_t st_it = 0, st_ex = 0, st_cyc_ex = 0, st_commit = 0;
   const uint64_t st_t0 = __builtin_readcyclecounter();
   constexpr uint32_t TAB = kMtTab / K;
-  constexpr uint64_t GM = (G == 64) ? ~0ull : ((1ull << G) - 1ull);
-  __shared__ uint32_t raw[2 * 624];
-  __shared__ uint32_t tw[2 * 624];
+  constexpr uint64_t GM = (G == 64) ? ~0ull : ((1ull << (G & 63)) - 1ull);
+  constexpr uint32_t NINF = FLAT ? kMtChunk : kMtInfo;
+  __shared__ uint32_t wl[FLAT ? kMtStage : 4 * 624];  // FLAT: staged words; else raw + tempered
   __shared__ uint32_t tab[kMtTab];
   __shared__ uint32_t set[kSetCap];
-  __shared__ uint4 inf[kMtInfo];
+  __shared__ uint4 inf[NINF];
   __shared__ uint32_t pbuf[kMtPos];
   const int lane = threadIdx.x;
   const int grp = lane / G, gl = lane % G;
   const bool lemire = lemire_i != 0;
-  for (int k = lane; k < 624; k += kWave) {
-    const uint32_t x = mt_state[k];
-    raw[k] = x;
-    tw[k] = mt_temper(x);
+  uint32_t vv = sizes[0], i0 = 0;
+  MtStream s{nullptr, nullptr, 0, 0u, false};
+  if constexpr (FLAT) {
+    i0 = blockIdx.x * kMtChunk;
+    if (i0 >= vv) return;
+    vv = min(vv, i0 + kMtChunk);
+    const uint32_t e0 = ch.base[i0] + ch.entries[blockIdx.x];
+    const uint32_t nw = ch.base[vv] + ch.entries[blockIdx.x + 1] - e0;
+    if (nw <= kMtStage) {
+      for (uint32_t k = lane; k < nw; k += kWave) wl[k] = ch.words[e0 + k];
+      s.tw = wl;
+    } else {
+      s.tw = ch.words + e0;  // (rare) read the chunk's words in place
+    }
+  } else {
+    uint32_t* raw = wl;
+    uint32_t* tw = wl + 2 * 624;
+    for (int k = lane; k < 624; k += kWave) {
+      const uint32_t x = mt_state[k];
+      raw[k] = x;
+      tw[k] = mt_temper(x);
+    }
+    s = MtStream{raw, tw, 0, mt_state[624], false};
   }
-  MtStream s{raw, tw, 0, mt_state[624], false};
   for (uint32_t k = lane; k < kMtTab; k += kWave) tab[k] = 0u;  // no stale kMtTaken marks
-  const uint32_t v = sizes[0];
+  const uint32_t v = vv;
   const uint4 zero = make_uint4(0u, 0u, 0u, 0u);
-  uint32_t ibase = 0;  // inf[k] = info[ibase + k]
-  for (uint32_t k = lane; k < kMtInfo && k < v; k += kWave) inf[k] = info[k];
-  uint32_t cbase = 0, chi = 0;  // pbuf[k] -> ans[cbase + k]; chi: end of the kept range
+  uint32_t ibase = i0;  // inf[k] = info[ibase + k]
+  for (uint32_t k = lane; k < NINF && i0 + k < v; k += kWave) inf[k] = info[i0 + k];
   __syncthreads();
-  uint32_t i = 0;
+  uint32_t cbase = inf[0].x, chi = cbase;  // pbuf[k] -> ans[cbase + k]; chi: end of the kept range
+  __syncthreads();
+  uint32_t i = i0;
   while (i < v) {
-    if (i + K > ibase + kMtInfo) {  // next info chunk
+    if (i + K > ibase + NINF) {  // next info chunk
       __syncthreads();
       ibase = i;
-      for (uint32_t k = lane; k < kMtInfo && ibase + k < v; k += kWave) inf[k] = info[ibase + k];
+      for (uint32_t k = lane; k < NINF && ibase + k < v; k += kWave) inf[k] = info[ibase + k];
       __syncthreads();
     }
     const uint32_t ci = inf[i - ibase].x;
@@ -567,7 +745,7 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
     const bool active = mine.y > 0;
     uint32_t val = 0;
     bool ok = false;
-    if (active) ok = mt_apply(mt_word(tw, s.cur, my_sp + gl), deg, mine.w, lemire, val);
+    if (active) ok = mt_apply(s.word(my_sp + gl), deg, mine.w, lemire, val);
     const uint32_t slot_idx = (uint32_t)grp * TAB + (deg <= TAB ? val : (val & (TAB - 1)));
     if (ok) tab[slot_idx] = 0xFFFFFFFFu;
     if (ok) atomicMin(&tab[slot_idx], (uint32_t)gl);
@@ -622,31 +800,359 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
       const uint64_t te = __builtin_readcyclecounter();
       ++st_ex;
       const uint4 fi = inf[i - ibase];
-      if (fi.z <= kMtTab)
-        mt_exact_tab(s, tab, set, pbuf + (fi.x - cbase), fi.y, fi.z, fi.w, lemire, lane);
-      else
-        mt_exact(s, set, pbuf + (fi.x - cbase), 0, fi.y, fi.z, fi.w, lemire, lane);
-      chi = fi.x + fi.y;
+      if (fi.y <= kSetCap) {
+        if (fi.z <= kMtTab)
+          mt_exact_tab(s, tab, pbuf + (fi.x - cbase), fi.y, fi.z, fi.w, lemire, lane);
+        else
+          mt_exact(s, set, pbuf + (fi.x - cbase), 0, fi.y, fi.z, fi.w, lemire, lane);
+        chi = fi.x + fi.y;
+      } else {  // fanout > kSetCap: flush, then straight to the global positions
+        __syncthreads();
+        for (uint32_t k = lane; k < chi - cbase && chi > cbase; k += kWave) ans[cbase + k] = pbuf[k];
+        if (fi.z <= kMtTab)
+          mt_exact_tab(s, tab, ans + fi.x, fi.y, fi.z, fi.w, lemire, lane);
+        else
+          mt_exact_hashed(s, tab, ans + fi.x, fi.y, fi.z, fi.w, lemire, lane);
+        cbase = chi = fi.x + fi.y;
+      }
       ++i;
       st_cyc_ex += __builtin_readcyclecounter() - te;
     }
   }
-  if (dbg && lane == 0)
-    printf("[mt G=%d] v=%u it=%llu commit=%llu exact=%llu cyc=%llu cyc_exact=%llu\n", G, v,
+  if (dbg && lane == 0 && (!FLAT || blockIdx.x == 0))
+    printf("[mt G=%d%s] v=%u it=%llu commit=%llu exact=%llu cyc=%llu cyc_exact=%llu\n", G,
+           FLAT ? " chunk0" : "", v - i0,
            (unsigned long long)st_it, (unsigned long long)st_commit, (unsigned long long)st_ex,
            (unsigned long long)(__builtin_readcyclecounter() - st_t0),
            (unsigned long long)st_cyc_ex);
   __syncthreads();
   for (uint32_t k = lane; k < chi - cbase && chi > cbase; k += kWave) ans[cbase + k] = pbuf[k];
-  // persist the generator state as std::mt19937 holds it: (_M_x, _M_p) with
-  // _M_p == 624 kept as is (libstdc++ twists lazily on the next call)
-  if (s.q0 > 624) {
-    s.cur ^= 1;
-    s.q0 -= 624;
+  if constexpr (!FLAT) {
+    // persist the generator state as std::mt19937 holds it: (_M_x, _M_p) with
+    // _M_p == 624 kept as is (libstdc++ twists lazily on the next call)
+    if (s.q0 > 624) {
+      s.cur ^= 1;
+      s.q0 -= 624;
+    }
+    __syncthreads();
+    for (int k = lane; k < 624; k += kWave) mt_state[k] = wl[s.cur * 624 + k];
+    if (lane == 0) mt_state[624] = s.q0;
+  }
+}
+
+// ---- chunked MT19937 resolver (fanout <= 32) -----------------------------
+// The single wave above walks the whole layer.  Here the layer's words are
+// generated in bulk first (the stream does not depend on the data), the dsts
+// are cut into chunks of kMtChunk, and for every chunk and every plausible
+// number of extra words consumed before it (a window of +-6 sigma around the
+// expected count) one lane walks the chunk and records the count after it —
+// a table per chunk.  One wave then chains the tables (Delta_{k+1} =
+// T_k[Delta_k]; a Delta outside the window is walked out serially), and each
+// chunk is replayed from its exact entry word by k_mt_serial<FLAT>.  Every
+// position is the one the sequential generator yields.
+constexpr uint32_t kMtWmax = 2048;  // window entries per chunk
+constexpr uint32_t kMtChunkedMinV = 32768;  // dst capacity from which a layer is chunked
+
+// words consumed by one dst whose draws start at word p (lane-private):
+// n when its first n words are accepted and pairwise distinct, else the
+// sequential count; `lst` holds up to NMAX distinct positions of this lane.
+template <int NMAX>
+__device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W, uint32_t nw,
+                                                 uint32_t p, uint32_t n, uint32_t deg,
+                                                 uint32_t thr, bool lemire, uint32_t* lst,
+                                                 uint32_t lstride) {
+  uint32_t val[NMAX];
+  bool clean = true;
+#pragma unroll
+  for (int t = 0; t < NMAX; ++t) {
+    if ((uint32_t)t < n) {
+      const uint32_t q = p + t;
+      clean &= mt_apply(q < nw ? W[q] : 0u, deg, thr, lemire, val[t]);
+    }
+  }
+#pragma unroll
+  for (int a = 1; a < NMAX; ++a)
+#pragma unroll
+    for (int b = 0; b < a; ++b)
+      if ((uint32_t)a < n) clean &= val[a] != val[b];
+  if (clean) return n;
+  uint32_t cnt = 0, q = p;
+  while (cnt < n) {
+    uint32_t x;
+    const bool ok = mt_apply(q < nw ? W[q] : 0u, deg, thr, lemire, x);
+    ++q;
+    if (!ok) continue;
+    bool dup = false;
+    for (uint32_t k = 0; k < cnt; ++k) dup |= lst[k * lstride] == x;
+    if (!dup) lst[(cnt++) * lstride] = x;
+    if (q - p > 1u << 20) break;  // (unreachable for deg > n) keep every lane finite
+  }
+  return q - p;
+}
+
+// bulk generation: W[t] = the tempered word at _M_p + t of the stream in
+// mt_state, t < nw (written to *nw_out); rb[b] = raw block b (b = 0: the
+// state's own).  nw = draws + expected extras + 10 sigma + 4096 (<= w_cap).
+constexpr int kGenThreads = 256;
+__global__ __launch_bounds__(kGenThreads) void k_mtp_gen(const uint32_t* __restrict__ mt_state,
+                                                        const uint32_t* base, const uint32_t* sizes,
+                                                        const float2* cstat, uint32_t w_cap,
+                                                        uint32_t* __restrict__ W,
+                                                        uint32_t* __restrict__ rb,
+                                                        uint32_t* nw_out) {
+  __shared__ uint32_t blk[2][624];
+  __shared__ float red[2][kGenThreads / kWave];
+  const int t = threadIdx.x;
+  const uint32_t v = sizes[0];
+  const uint32_t nch = (v + kMtChunkP - 1) / kMtChunkP;
+  float m = 0.f, var = 0.f;
+  for (uint32_t k = t; k < nch; k += kGenThreads) {
+    m += cstat[k].x;
+    var += cstat[k].y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m += __shfl_down(m, o, kWave);
+    var += __shfl_down(var, o, kWave);
+  }
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = m;
+    red[1][t >> 6] = var;
+  }
+  for (int k = t; k < 624; k += kGenThreads) {
+    blk[0][k] = mt_state[k];
+    rb[k] = mt_state[k];
   }
   __syncthreads();
-  for (int k = lane; k < 624; k += kWave) mt_state[k] = raw[s.cur * 624 + k];
-  if (lane == 0) mt_state[624] = s.q0;
+  float mm = 0.f, vv = 0.f;
+  for (int w = 0; w < kGenThreads / kWave; ++w) {
+    mm += red[0][w];
+    vv += red[1][w];
+  }
+  const double want = (double)base[v] + (double)mm + 10.0 * sqrt((double)vv) + 4096.0;
+  const uint32_t nw = (uint32_t)fmin(want, (double)w_cap);
+  const uint32_t q0 = mt_state[624];
+  if (t == 0) *nw_out = nw;
+  for (uint32_t a = q0 + t; a < 624; a += kGenThreads)
+    if (a - q0 < nw) W[a - q0] = mt_temper(blk[0][a]);
+  const uint32_t U = 0x80000000u, L = 0x7fffffffu, A = 0x9908b0dfu;
+  for (uint32_t b = 1; 624u * b - q0 < nw; ++b) {
+    const uint32_t* cur = blk[(b - 1) & 1];
+    uint32_t* nxt = blk[b & 1];
+    // _M_gen_rand in three dependent pieces: [0,227) from the current block,
+    // [227,454) and [454,624) from the words just made
+    if (t < 227) {
+      const uint32_t y = (cur[t] & U) | (cur[t + 1] & L);
+      nxt[t] = cur[t + 397] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    __syncthreads();
+    if (t < 227) {
+      const int k = t + 227;
+      const uint32_t y = (cur[k] & U) | (cur[k + 1] & L);
+      nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    __syncthreads();
+    if (t < 170) {
+      const int k = t + 454;
+      const uint32_t y = (cur[k] & U) | ((k < 623 ? cur[k + 1] : nxt[0]) & L);
+      nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    __syncthreads();
+    const uint32_t o = 624u * b - q0;
+    for (int k = t; k < 624; k += kGenThreads) {
+      const uint32_t x = nxt[k];
+      rb[(uint64_t)b * 624 + k] = x;
+      if (o + k < nw) W[o + k] = mt_temper(x);
+    }
+  }
+}
+
+// the window tables: block (x, k) = entries lo_k + 256 x + t of chunk k
+template <int NMAX>
+__global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ info,
+                                                   const uint32_t* __restrict__ base,
+                                                   const uint32_t* sizes, const float2* cstat,
+                                                   const uint32_t* __restrict__ W,
+                                                   const uint32_t* nw_dev, int lemire_i,
+                                                   uint2* __restrict__ win,
+                                                   uint32_t* __restrict__ tabs) {
+  __shared__ uint4 inf[kMtChunk];
+  __shared__ uint32_t bs[kMtChunk];
+  __shared__ uint32_t lst[NMAX * 256];
+  __shared__ float red[2][4];
+  const int t = threadIdx.x;
+  const uint32_t k = blockIdx.y, v = sizes[0];
+  const uint32_t i0 = k * kMtChunk;
+  if (i0 >= v) return;
+  const uint32_t i1 = min(v, i0 + kMtChunk);
+  float m = 0.f, var = 0.f;
+  for (uint32_t j = t; j < k; j += 256) {
+    m += cstat[j].x;
+    var += cstat[j].y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m += __shfl_down(m, o, kWave);
+    var += __shfl_down(var, o, kWave);
+  }
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = m;
+    red[1][t >> 6] = var;
+  }
+  for (uint32_t j = t; j < i1 - i0; j += 256) {
+    inf[j] = info[i0 + j];
+    bs[j] = base[i0 + j];
+  }
+  __syncthreads();
+  const float mm = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const float vv = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  const float h = ceilf(6.f * sqrtf(vv)) + 8.f;
+  const uint32_t lo = (uint32_t)fmaxf(0.f, floorf(mm - h));
+  const uint32_t wn = min(kMtWmax, (uint32_t)(mm + h - (float)lo) + 1u);
+  if (blockIdx.x == 0 && t == 0) win[k] = make_uint2(lo, wn);
+  if (blockIdx.x * 256u >= wn) return;
+  const uint32_t slot = blockIdx.x * 256u + t;
+  const uint32_t nw = *nw_dev;
+  const bool lemire = lemire_i != 0;
+  uint32_t dl = lo + slot;
+  // software pipeline: the words of the next drawing dst are fetched while
+  // this one is checked, at the start it would have if this one is clean
+  // (the common case); a lane whose Delta moved fetches again
+  const uint32_t cnt = i1 - i0;
+  auto next_draw = [&](uint32_t j) {
+    while (j < cnt && inf[j].y == 0) ++j;
+    return j;
+  };
+  uint32_t j = next_draw(0);
+  uint32_t wv[NMAX];
+  uint32_t pf = j < cnt ? bs[j] + dl : 0u;
+#pragma unroll
+  for (int q = 0; q < NMAX; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
+  while (j < cnt) {
+    const uint4 f = inf[j];
+    const uint32_t p = bs[j] + dl;
+    uint32_t cur[NMAX];
+#pragma unroll
+    for (int q = 0; q < NMAX; ++q) cur[q] = wv[q];
+    if (p != pf) {  // (the previous dst consumed extra words)
+#pragma unroll
+      for (int q = 0; q < NMAX; ++q) cur[q] = p + q < nw ? W[p + q] : 0u;
+    }
+    const uint32_t jn = next_draw(j + 1);
+    pf = jn < cnt ? bs[jn] + dl : 0u;
+#pragma unroll
+    for (int q = 0; q < NMAX; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
+    // first n words accepted and pairwise distinct: n words; else walk
+    uint32_t val[NMAX];
+    bool clean = true;
+#pragma unroll
+    for (int q = 0; q < NMAX; ++q)
+      if ((uint32_t)q < f.y) clean &= mt_apply(cur[q], f.z, f.w, lemire, val[q]);
+#pragma unroll
+    for (int a2 = 1; a2 < NMAX; ++a2)
+#pragma unroll
+      for (int b2 = 0; b2 < a2; ++b2)
+        if ((uint32_t)a2 < f.y) clean &= val[a2] != val[b2];
+    if (!clean) dl += lane_consume<NMAX>(W, nw, p, f.y, f.z, f.w, lemire, lst + t, 256) - f.y;
+    j = jn;
+  }
+  if (slot < wn) tabs[(uint64_t)k * kMtWmax + slot] = dl;
+}
+
+// chain the tables: entries[k] = extra words before chunk k (one wave).  The
+// windows of the next kRing chunks are fetched ahead into LDS by LDS DMA
+// (16 B per lane per instruction; no other vector-memory op in the loop, so
+// the hand-counted vmcnt below is exact).  A Delta outside its chunk's window
+// is walked out by lane 0.  Also leaves the generator state after the layer.
+constexpr int kRing = 5;
+constexpr uint32_t kMtMaxChunks = 4096;  // the host keeps v_cap <= kMtMaxChunks * kMtChunk
+constexpr int kRingOps = kMtWmax * 4 / (16 * kWave);  // LDS-DMA instructions per window
+
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+template <int NMAX>
+__global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__ info,
+                                                      const uint32_t* __restrict__ base,
+                                                      const uint32_t* sizes, const uint32_t* W,
+                                                      const uint32_t* nw_dev, int lemire_i,
+                                                      const uint2* __restrict__ win,
+                                                      const uint32_t* __restrict__ tabs,
+                                                      uint32_t* __restrict__ entries,
+                                                      const uint32_t* __restrict__ rb,
+                                                      uint32_t* __restrict__ mt_state,
+                                                      uint32_t* __restrict__ ovf,
+                                                      uint32_t* __restrict__ nfallback) {
+  __shared__ __attribute__((aligned(16))) uint32_t ring[kRing][kMtWmax];
+  __shared__ uint32_t ent[kMtMaxChunks];
+  __shared__ uint2 wins[kMtMaxChunks];
+  __shared__ uint32_t lst[NMAX];
+  const int lane = threadIdx.x;
+  const uint32_t v = sizes[0];
+  const uint32_t nch = min((v + kMtChunk - 1) / kMtChunk, kMtMaxChunks);
+  for (uint32_t k = lane; k < nch; k += kWave) wins[k] = win[k];  // before any LDS DMA
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bool lemire = lemire_i != 0;
+  const uint32_t nw = *nw_dev;
+  auto fetch = [&](uint32_t k) {  // window of chunk min(k, nch - 1) -> ring slot k % kRing
+    const uint32_t kk = nch ? min(k, nch - 1) : 0u;
+    const char* src = reinterpret_cast<const char*>(tabs + (uint64_t)kk * kMtWmax);
+    const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)ring[k % kRing];
+#pragma unroll
+    for (int q = 0; q < kRingOps; ++q) glds16(src + 1024 * q + 16 * lane, dst + 1024 * q);
+  };
+  for (uint32_t k = 0; k < (uint32_t)kRing; ++k) fetch(k);
+  uint32_t dl = 0, fallbacks = 0;
+  for (uint32_t k = 0; k < nch; ++k) {
+    ent[k] = dl;  // (lane-uniform store)
+    // the window of chunk k landed: (kRing - 1) windows issued after it
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kRing - 1) * kRingOps) : "memory");
+    const uint2 w = wins[k];
+    if (dl >= w.x && dl < w.x + w.y) {
+      dl = ring[k % kRing][dl - w.x];
+    } else {  // outside the window: walk the chunk
+      ++fallbacks;
+      uint32_t d2 = dl;
+      if (lane == 0) {
+        const uint32_t i0 = k * kMtChunk, i1 = min(v, i0 + kMtChunk);
+        for (uint32_t j = i0; j < i1; ++j) {
+          const uint4 f = info[j];
+          if (f.y == 0) continue;
+          d2 += lane_consume<NMAX>(W, nw, base[j] + d2, f.y, f.z, f.w, lemire, lst, 1) - f.y;
+        }
+      }
+      dl = __builtin_amdgcn_readfirstlane(d2);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // the slot is read before it is refilled
+    fetch(k + kRing);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (uint32_t k = lane; k < nch; k += kWave) entries[k] = ent[k];
+  if (lane == 0) {
+    entries[nch] = dl;
+    if (dl + base[v] > nw) *ovf |= 4u;  // the stream generated fell short
+    *nfallback = fallbacks;
+  }
+  // the generator after the layer: _M_p + consumed words from the state's block
+  const uint32_t a = mt_state[624] + base[v] + dl;
+  uint32_t b = a / 624, off = a % 624;
+  if (off == 0 && b > 0) {  // libstdc++ keeps the exhausted block until the next call
+    --b;
+    off = 624;
+  }
+  __syncthreads();
+  for (int k = lane; k < 624; k += kWave) mt_state[k] = rb[(uint64_t)b * 624 + k];
+  if (lane == 0) mt_state[624] = off;
 }
 
 // positions -> neighbour ids (16-lane group per dst); copy-path dsts take
@@ -897,7 +1403,9 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
                 "weights requested without buffers/degrees");
   const bool up = up_degree && weight_type != NTS_WEIGHT_NONE;
   NTS_CHECK_ARG(rng_mode >= NTS_RNG_PHILOX && rng_mode <= NTS_RNG_MT19937_DIV, "rng_mode");
-  NTS_CHECK_ARG(fanout <= kSetCap, "fanout above the rejection-path capacity (1024)");
+  NTS_CHECK_ARG(fanout <= (int)kBigFanoutMax, "fanout above 16384 (the distinct-position hash set)");
+  NTS_CHECK_ARG(rng_mode == NTS_RNG_PHILOX || fanout <= (int)(kMtTab / 2),
+                "MT19937 modes: fanout above 8192 (the exact path's hash set)");
   NTS_CHECK_ARG(g->n_vertices <= 0xFFFFFFFFull, "vertex count exceeds uint32 ids");
   const bool csr = o->row_offset != nullptr;
   NTS_CHECK_ARG(!csr || o->column_indices, "CSR requested without column_indices");
@@ -916,7 +1424,30 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
-  const uint64_t mt_n = rng_mode != NTS_RNG_PHILOX ? al((uint64_t)o->v_cap * 4) : 0;
+  // MT19937 modes: per-dst info; the chunked resolver (fanout 1..32) adds the
+  // draws' scan, chunk stats, the bulk word stream + raw blocks, the window
+  // tables and the chunk entries
+  const bool mt_serial_env = getenv("NTS_MT_SERIAL") != nullptr;  // (read per call: tests A/B)
+  // (small layers — e.g. the seed layer — stay on the single walker: the
+  // tables' cost grows with the layer's length times its window, while the
+  // walker's chain is short)
+  const bool mt_chunked_env = getenv("NTS_MT_CHUNKED") != nullptr;
+  const bool mt_chunked = rng_mode != NTS_RNG_PHILOX && !mt_serial_env && fanout >= 1 &&
+                          fanout <= 32 && (uint64_t)o->v_cap <= (uint64_t)kMtMaxChunks * kMtChunk &&
+                          (mt_chunked_env || o->v_cap >= kMtChunkedMinV);
+  const uint64_t nch_cap = (uint64_t)o->v_cap / kMtChunk + 1;
+  const uint64_t w_cap = (uint64_t)o->e_cap + o->e_cap / 4 + 131072;
+  const uint64_t mt_info_n = rng_mode != NTS_RNG_PHILOX ? al((uint64_t)o->v_cap * 4) : 0;
+  const uint64_t mt_base_n = mt_chunked ? al((uint64_t)o->v_cap + 1) : 0;
+  const uint64_t mt_stat_n = mt_chunked ? al(2 * nch_cap) : 0;
+  const uint64_t mt_w_n = mt_chunked ? al(w_cap + 256) : 0;  // + the walks' look-ahead
+  const uint64_t mt_rb_n = mt_chunked ? al((w_cap / 624 + 3) * 624) : 0;
+  const uint64_t mt_win_n = mt_chunked ? al(2 * nch_cap) : 0;
+  const uint64_t mt_tab_n = mt_chunked ? al(nch_cap * kMtWmax) : 0;
+  const uint64_t mt_ent_n = mt_chunked ? al(nch_cap + 1) : 0;
+  const uint64_t mt_misc_n = mt_chunked ? 64 : 0;
+  const uint64_t mt_n = mt_info_n + mt_base_n + mt_stat_n + mt_w_n + mt_rb_n + mt_win_n +
+                        mt_tab_n + mt_ent_n + mt_misc_n;
   const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n) *
                           sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
@@ -933,13 +1464,24 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
 
-  // 1) per-dst counts -> column_offset (e_size: the selection's first thread)
-  hipLaunchKernelGGL(k_count, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                     o->v_size, o->v_cap, fanout, o->column_offset, o->sizes, o->omit_map,
-                     o->omit_key, o->omit_loc, o->omit_row);
-  NTS_LAUNCH_CHECK();
-  NTS_RET(scan_exclusive<uint32_t>(o->column_offset, o->column_offset, o->sizes, o->v_cap,
-                                   t_scan_co, st));
+  // 1) per-dst counts -> column_offset, v_size, e_size: one single-pass
+  // count + scan kernel
+  {
+    CountArgs ca;
+    ca.goff = g->column_offset;
+    ca.dst = o->destination;
+    ca.v_in = o->v_size;
+    ca.v_cap = o->v_cap;
+    ca.fanout = fanout;
+    ca.sizes = o->sizes;
+    ca.e_cap = o->e_cap;
+    ca.omit_map = o->omit_map;
+    ca.omit_key = o->omit_key;
+    ca.omit_loc = o->omit_loc;
+    ca.omit_row = o->omit_row;
+    NTS_RET(count_scan(ctx, ca, o->column_offset, st));
+  }
+  (void)t_scan_co;
 
   // 2) selection (marks the frontier; the byte map is all zeros here: it is
   // zeroed when allocated and k_mark_write clears what each layer set)
@@ -962,32 +1504,86 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
       const uint32_t gs =
           std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
       hipLaunchKernelGGL(k_select_philox_g16, dim3(gs), dim3(kSelThreads), 0, st, a);
-    } else {
+    } else if (fanout < 0 || fanout <= kSetCap) {
       const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves), 4096u));
       hipLaunchKernelGGL(k_select_philox, dim3(gs), dim3(kSelThreads), 0, st, a);
+    } else {
+      uint32_t cap = 1;
+      while (cap < 2u * (uint32_t)fanout) cap <<= 1;
+      const size_t lds = (size_t)cap * sizeof(uint32_t);
+      NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_philox_big),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      const uint32_t gs = std::max(1u, std::min(o->v_cap, 2048u));
+      hipLaunchKernelGGL(k_select_philox_big, dim3(gs), dim3(kWave), lds, st, a, cap);
     }
   } else {
     const int lem = rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0;
     static const int mt_dbg = getenv("NTS_MT_DEBUG") ? 1 : 0;
     uint4* info = reinterpret_cast<uint4*>(t_mt);
+    if (mt_chunked) {
+      uint32_t* base = t_mt + mt_info_n;
+      float2* cstat = reinterpret_cast<float2*>(base + mt_base_n);
+      uint32_t* W = base + mt_base_n + mt_stat_n;
+      uint32_t* rb = W + mt_w_n;
+      uint2* win = reinterpret_cast<uint2*>(rb + mt_rb_n);
+      uint32_t* tabs = rb + mt_rb_n + mt_win_n;
+      uint32_t* entries = tabs + mt_tab_n;
+      uint32_t* misc = entries + mt_ent_n;  // [0] words generated, [1] fallbacks
+      NTS_HIP_TRY(hipMemsetAsync(cstat, 0, mt_stat_n * sizeof(uint32_t), st));
+      hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
+                         o->column_offset, o->sizes, o->e_cap, lem, info, base, cstat);
+      NTS_LAUNCH_CHECK();
+      NTS_RET(scan1_exclusive(ctx, base, base, o->sizes, o->v_cap, st));
+      hipLaunchKernelGGL(k_mtp_gen, dim3(1), dim3(kGenThreads), 0, st, ctx->mt_state, base,
+                         o->sizes, cstat, (uint32_t)w_cap, W, rb, misc);
+      NTS_LAUNCH_CHECK();
+      const dim3 tgrid(kMtWmax / 256, (uint32_t)nch_cap);
+      const MtChunked chunked{W, base, entries};
+      if (fanout <= 16) {
+        hipLaunchKernelGGL(k_mtp_tables<16>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
+                           W, misc, lem, win, tabs);
+        NTS_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_mtp_resolve<16>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes, W,
+                           misc, lem, win, tabs, entries, rb, ctx->mt_state, o->sizes + 3, misc + 1);
+        NTS_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_mt_serial<16, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
+                           info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
+      } else {
+        hipLaunchKernelGGL(k_mtp_tables<32>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
+                           W, misc, lem, win, tabs);
+        NTS_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_mtp_resolve<32>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes, W,
+                           misc, lem, win, tabs, entries, rb, ctx->mt_state, o->sizes + 3, misc + 1);
+        NTS_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_mt_serial<32, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
+                           info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
+      }
+      NTS_LAUNCH_CHECK();
+      const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
+      hipLaunchKernelGGL(k_mt_rows, dim3(gs), dim3(kSelThreads), 0, st, a);
+      NTS_LAUNCH_CHECK();
+      goto frontier;
+    }
     hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                       o->column_offset, o->sizes, o->e_cap, lem, info);
+                       o->column_offset, o->sizes, o->e_cap, lem, info, nullptr, nullptr);
     NTS_LAUNCH_CHECK();
+    const MtChunked none{nullptr, nullptr, nullptr};
     if (fanout >= 0 && fanout <= 16)
-      hipLaunchKernelGGL(k_mt_serial<16>, dim3(1), dim3(kWave), 0, st, info, o->sizes,
-                         o->sample_ans, ctx->mt_state, lem, mt_dbg);
+      hipLaunchKernelGGL((k_mt_serial<16, false>), dim3(1), dim3(kWave), 0, st, info, o->sizes,
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg, none);
     else if (fanout >= 0 && fanout <= 32)
-      hipLaunchKernelGGL(k_mt_serial<32>, dim3(1), dim3(kWave), 0, st, info, o->sizes,
-                         o->sample_ans, ctx->mt_state, lem, mt_dbg);
+      hipLaunchKernelGGL((k_mt_serial<32, false>), dim3(1), dim3(kWave), 0, st, info, o->sizes,
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg, none);
     else
-      hipLaunchKernelGGL(k_mt_serial<64>, dim3(1), dim3(kWave), 0, st, info, o->sizes,
-                         o->sample_ans, ctx->mt_state, lem, mt_dbg);
+      hipLaunchKernelGGL((k_mt_serial<64, false>), dim3(1), dim3(kWave), 0, st, info, o->sizes,
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg, none);
     NTS_LAUNCH_CHECK();
     const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
     hipLaunchKernelGGL(k_mt_rows, dim3(gs), dim3(kSelThreads), 0, st, a);
   }
   NTS_LAUNCH_CHECK();
 
+frontier:
   if (o->dst_local_id) {
     hipLaunchKernelGGL(k_mark_dst, dim3(gv), dim3(256), 0, st, o->destination, o->sizes,
                        ctx->marks);
@@ -1032,7 +1628,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   // 5) CSR transpose (stable in edge order = ascending local dst)
   if (csr) {
     NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
-                             ceil_log2((uint64_t)o->s_cap + 1), t_sort, st));
+                             ceil_log2((uint64_t)o->s_cap + 1), t_sort, st, ctx));
     hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
                        weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
                        o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,

@@ -225,6 +225,37 @@ def test_h2p_gemm_tn_gather(ctx, M, N, K, gscale):
     assert torch.equal(Ch, Ch2)
 
 
+@pytest.mark.parametrize("M,N,K,gscale", [(602, 128, 228656, 1e-7), (602, 128, 5003, 1.0),
+                                          (100, 256, 3000, 1e3), (41, 128, 17, 1.0)])
+def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale):
+    """TN v4 with B's column maxima given (the CSR backward's epilogue) instead
+    of its per-chunk pre-pass over B: the same error bar vs fp64, deterministic."""
+    g = torch.Generator(device=DEV).manual_seed(M * N + K + 23)
+    V = K + K // 2 + 5
+    X = _table(V, M, g, decades=6)
+    rows = torch.randint(0, V, (K,), device=DEV, generator=g).to(torch.int32)
+    G = torch.randn(K, N, device=DEV, generator=g) * gscale
+    G[:, 5] *= 1e-9
+    G[:, 9] = 0.0  # an all-zero column (max 0)
+    Q, rs = ctx.h2_split_rows_planar(X)
+    cm = (G.abs() * rs[rows.long()][:, None]).max(0).values.contiguous().view(torch.int32)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.full((M, N), float("nan"), device=DEV)
+    ctx.gemm_tn_gather(X, rows, G, C32)
+    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch, M, colmax=cm)
+    Xg = X[rows.long()].double()
+    ref = Xg.t() @ G.double()
+    scale = Xg.abs().t() @ G.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ch).any()
+    assert (Ch[:, 9] == 0).all()
+    _check(C32, Ch, ref, scale)
+    Ch2 = torch.empty_like(Ch)
+    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch2, M, colmax=cm)
+    torch.cuda.synchronize()
+    assert torch.equal(Ch, Ch2)
+
+
 @pytest.mark.parametrize("M,N,K,decades", [(228656, 128, 602, 0), (3001, 128, 602, 12),
                                            (2500, 256, 100, 6), (17, 128, 64, 0)])
 def test_h2p_gemm_gather(ctx, M, N, K, decades):

@@ -126,11 +126,15 @@ def _assert_layers_equal(gl, ol):
                 assert np.array_equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("walker", ["serial", "chunked"])
 @pytest.mark.parametrize("fanouts", [(25, 10), (3, 2), (-1, 4), (5, 5, 5)])
-def test_sampler_mt19937_is_reference_stream(hip, cora, fanouts):
+def test_sampler_mt19937_is_reference_stream(hip, cora, fanouts, walker, monkeypatch):
     """MT19937 mode reproduces the reference generator: identical arrays to the
     oracle in draw order, identical per-dst sets to the reference's
-    unordered_map order, identical generator state afterwards."""
+    unordered_map order, identical generator state afterwards — with the
+    single-wave walker and with the chunked resolver (bulk words, window
+    tables, chained entries, per-chunk replay) forced on every layer."""
+    monkeypatch.setenv("NTS_MT_SERIAL" if walker == "serial" else "NTS_MT_CHUNKED", "1")
     V, src, dst = cora
     g = _graph(hip, V, src, dst)
     col, rows = orc.build_csc(V, src, dst)
@@ -165,6 +169,50 @@ def test_sampler_mt19937_div_mode(hip, cora):
                     order_mode=orc.ORDER_DRAW)
     gl = [_gpu_layer_np(l) for l in _sample_gpu(hip, g, seeds, [10, 5], 2)]
     _assert_layers_equal(gl, o.sample(seeds))
+
+
+def _hub_graph(seed):
+    """Degrees past the 1024 rejection-set cap and past the MT exact path's
+    16 K direct table: 48 hub dsts of 20,000 in-edges, 400 of 1,500-3,000,
+    and a sparse rest."""
+    rng = np.random.default_rng(seed)
+    V = 60_000
+    parts_s, parts_d = [], []
+    for d in range(48):
+        parts_s.append(rng.integers(0, V, 20_000))
+        parts_d.append(np.full(20_000, d))
+    for d in range(48, 448):
+        k = int(rng.integers(1_500, 3_000))
+        parts_s.append(rng.integers(0, V, k))
+        parts_d.append(np.full(k, d))
+    parts_s.append(rng.integers(0, V, 300_000))
+    parts_d.append(rng.integers(0, V, 300_000))
+    return V, np.concatenate(parts_s).astype(np.uint32), np.concatenate(parts_d).astype(np.uint32)
+
+
+@pytest.mark.parametrize("rng_mode", [0, 1])
+def test_sampler_fanout_above_1024(hip, rng_mode):
+    """Fanout 2,000 (> the 1,024-entry rejection set): the LDS hash-set path
+    (Philox) and the MT exact paths (direct table, hashed past 16 K degree)
+    give the oracle's arrays in draw order (std::unordered_map semantics,
+    core/ntsFastSampler.hpp:1028-1048), and the MT generator state matches."""
+    V, src, dst = _hub_graph(12)
+    g = _graph(hip, V, src, dst)
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    seeds = np.concatenate([np.arange(0, 448, 3), np.arange(1000, 1200)]).astype(np.uint32)
+    fan = [2000, 3]
+    hip.rng_seed(2000)
+    o = orc.Sampler(col, rows, in_d, out_d, fan, seed=2000,
+                    rng_mode=orc.RNG_PHILOX if rng_mode == 0 else orc.RNG_MT_LEMIRE,
+                    order_mode=orc.ORDER_DRAW)
+    for bs in range(2):
+        gl = [_gpu_layer_np(l) for l in _sample_gpu(hip, g, seeds, fan, rng_mode, bs)]
+        ol = o.sample(seeds, bs)
+        assert ol[0]["e_size"] > 100 * 2000
+        _assert_layers_equal(gl, ol)
+    if rng_mode == 1:
+        assert np.array_equal(hip.rng_state().numpy().view(np.uint32), o.mt_state())
 
 
 @pytest.mark.parametrize("case", ["cora", "random"])
@@ -215,9 +263,10 @@ def test_sampler_edge_cases(hip):
     col, rows = orc.build_csc(V, src, dst)
     out_d, in_d = orc.degrees(V, src, dst)
     for seeds, fan in [(np.array([], np.uint32), [4, 4]), (np.array([0, 2999, 5], np.uint32), [0, 3]),
-                       (np.array([0], np.uint32), [1500, 2]), (np.array([0, 7], np.uint32), [-1, -1])]:
+                       (np.array([0], np.uint32), [1500, 2]), (np.array([0, 7], np.uint32), [-1, -1]),
+                       (np.array([0], np.uint32), [20000, 2])]:
         o = orc.Sampler(col, rows, in_d, out_d, fan, rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
-        if any(f > 1024 for f in fan):
+        if any(f > 16384 for f in fan):  # past the distinct-position hash set
             with pytest.raises(RuntimeError):
                 _sample_gpu(hip, g, seeds, fan, 0)
             continue
@@ -477,6 +526,34 @@ def test_spmm_csr_bwd_postmask(hip, cora, F):
     torch.cuda.synchronize()
     assert torch.equal(got[:s], ref)
     assert torch.isnan(got[s:]).all()
+
+
+@pytest.mark.parametrize("F", [1, 41, 128, 512])
+def test_spmm_csr_bwd_colmax(hip, cora, F):
+    """The CSR backward that also emits its output's column maxima (scaled by
+    rs[row_map[row]]) for the pair-table TN GEMM: the rows bit-identical to
+    spmm_csr_bwd's, the maxima exact (hub rows summed cooperatively included)."""
+    V, src, dst = cora
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    l0, _ = o.sample(np.arange(4, V, 11, dtype=np.uint32))
+    rng = np.random.default_rng(F + 5)
+    v, s = l0["v_size"], l0["src_size"]
+    G = _t(rng.standard_normal((v, F)).astype(np.float32))
+    rs = _t(np.ldexp(1.0, rng.integers(-20, 20, V)).astype(np.float32))
+    rmap = _t(l0["source"].astype(np.uint32))
+    sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
+    ro, ci, wb = _t(l0["row_offset"]), _t(l0["column_indices"]), _t(l0["edge_weight_backward"])
+    plain = torch.empty(s, F, device=DEV)
+    hip.spmm_csr_bwd(ro, ci, wb, sdev, s, G, plain)
+    got = torch.full((s + 2, F), float("nan"), device=DEV)
+    cm = torch.full((F,), -1, dtype=torch.int32, device=DEV)
+    hip.spmm_csr_bwd_colmax(ro, ci, wb, sdev, s + 2, G, got, rs, rmap, cm)
+    torch.cuda.synchronize()
+    assert torch.equal(got[:s], plain)
+    want = (plain.abs() * rs[rmap.long()][:, None]).max(0).values
+    assert torch.equal(cm.view(torch.float32), want)
 
 
 @pytest.mark.parametrize("M,N,K", [(3000, 128, 602), (2500, 64, 100), (500, 41, 100), (37, 7, 13)])
