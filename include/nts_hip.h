@@ -34,12 +34,14 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 6  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 7  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
                                      accuracy counts in the fused loss;
                                   4: PD cache entry points + omit fields, GEMM mode;
                                   5: two-piece f16 pair-table GEMMs (nts_hip_h2_*);
-                                  6: nts_hip_spmm_csr_bwd_colmax + nts_hip_gemm_h2p_tn_gather_cm */
+                                  6: nts_hip_spmm_csr_bwd_colmax + nts_hip_gemm_h2p_tn_gather_cm;
+                                  7: the column maxima per part of rows (no row scales in
+                                     the backward), nts_hip_csr_bwd_colmax_rows_per_part */
 
 /* status codes */
 #define NTS_OK 0
@@ -291,17 +293,19 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx *ctx, const uint32_t *row_offset,
                          const uint32_t *s, uint32_t s_cap, const float *g_out,
                          uint64_t ld_gout, uint32_t feature_size, float *g_in,
                          uint64_t ld_gin);
-/* nts_hip_spmm_csr_bwd that also leaves the output's column maxima in
- * colmax_bits[0..feature_size): the float bits of max_s |G_in[s,c]| *
- * |rs[row_map[s]]| (zeroed first; exact — an unordered max).  The operand
- * scales of nts_hip_gemm_h2p_tn_gather_cm when G_in is its B and row_map its
- * a_rows, so the GEMM reads G_in once.  feature_size <= 512. */
+/* nts_hip_spmm_csr_bwd that also leaves its output's column maxima per part
+ * of R = nts_hip_csr_bwd_colmax_rows_per_part(feature_size) rows:
+ * part_max[p * feature_size + c] = the float bits of max |G_in[s, c]| over
+ * s in [p R, (p+1) R) (0 past the live rows; exact — an unordered max),
+ * ceil(s_cap / R) parts.  The operand scales of nts_hip_gemm_h2p_tn_gather_cm
+ * when G_in is its B, so that GEMM reads G_in once.  feature_size <= 512,
+ * G rows 16-byte aligned with ld % 4 == 0. */
+uint32_t nts_hip_csr_bwd_colmax_rows_per_part(uint32_t feature_size);
 int nts_hip_spmm_csr_bwd_colmax(nts_hip_ctx *ctx, const uint32_t *row_offset,
                                 const uint32_t *column_indices, const float *weight_backward,
                                 const uint32_t *s, uint32_t s_cap, const float *g_out,
                                 uint64_t ld_gout, uint32_t feature_size, float *g_in,
-                                uint64_t ld_gin, const float *rs, const uint32_t *row_map,
-                                uint32_t *colmax_bits);
+                                uint64_t ld_gin, uint32_t *part_max);
 /* Transform-first bottom layer: when the layer narrows the rows
  * (F_in > F_out), A (X W) replaces (A X) W — the reference aggregates first
  * (SingleGPUAllSampleGraphOp::forward then Parameter::forward,
@@ -480,14 +484,15 @@ int nts_hip_h2_split_rows_planar(nts_hip_ctx *ctx, uint64_t R, uint32_t K, const
 int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx *ctx, int M, int N, int K, const uint16_t *Q, uint64_t ldq,
                                int Kp, const float *rs, const uint32_t *a_rows, const float *B,
                                uint64_t ldb, float *C, uint64_t ldc);
-/* The same with B's column maxima given (colmax_bits[N], the float bits of
- * max_k |rs[a_rows[k]] B[k,c]| — nts_hip_spmm_csr_bwd_colmax's output): one
- * scale per column instead of one per column and 960-row chunk, and no
- * pre-pass over B in the kernel. */
+/* The same with per-part column maxima of |B| given (part p = B rows
+ * [p R, (p+1) R), N words per part — nts_hip_spmm_csr_bwd_colmax's output,
+ * R = rows_per_part): each k-chunk's column scales come from the parts that
+ * cover its rows times the chunk's largest row scale, with no pre-pass over B
+ * in the kernel. */
 int nts_hip_gemm_h2p_tn_gather_cm(nts_hip_ctx *ctx, int M, int N, int K, const uint16_t *Q,
                                   uint64_t ldq, int Kp, const float *rs, const uint32_t *a_rows,
                                   const float *B, uint64_t ldb, float *C, uint64_t ldc,
-                                  const uint32_t *colmax_bits);
+                                  const uint32_t *part_max, uint32_t rows_per_part);
 /* The forward GEMM on the planar table (k_h2_nn3: W's 16-column slices held
  * in registers, 16-row tiles of whole rows by LDS DMA): N % 128 == 0,
  * K <= Kp <= 640; arguments as nts_hip_gemm_h2_gather. */

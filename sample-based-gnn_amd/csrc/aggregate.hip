@@ -102,8 +102,9 @@ constexpr uint32_t kHostBit = 0x80000000u;
 //   kAggPostMask: y = (A x) ⊙ [mx > 0] · scale with mx indexed by the OUTPUT
 //              row (the activation backward applied to the gathered sum: the
 //              graph-op backward feeding a transform-first bottom layer)
-//   kAggColmax: kAggPlain, and the output's column maxima |y[d,:]|·cm_rs[cm_map[d]]
-//     into ax.cm_out (the f16 pair-table TN GEMM's per-column scales)
+//   kAggColmax: kAggPlain, and per block the column maxima of |y| over the
+//     block's output rows into row blockIdx.x of ax.cm_out (the f16
+//     pair-table TN GEMM's per-chunk column scales, nts_hip_spmm_csr_bwd_colmax)
 enum { kAggPlain = 0, kAggAct = 1, kAggMask = 2, kAggPostMask = 3, kAggColmax = 4 };
 struct AggExtra {
   const float* mx = nullptr;
@@ -111,11 +112,8 @@ struct AggExtra {
   float scale = 1.f;
   uint32_t keep_threshold = 0;
   uint64_t seed = 0, offset = 0;
-  // column maxima of the output (nts_hip_spmm_csr_bwd_colmax): cm_out[col] =
-  // max over rows d of |y[d, col]| * cm_rs[cm_map[d]], as float bits
-  // (atomicMax on the bits of non-negative floats); one pass over the columns
-  const float* cm_rs = nullptr;
-  const uint32_t* cm_map = nullptr;
+  // per-block column maxima of the output (nts_hip_spmm_csr_bwd_colmax):
+  // cm_out[b * F + col] = max over block b's rows d of |y[d, col]|, float bits
   uint32_t* cm_out = nullptr;
 };
 
@@ -288,16 +286,23 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     if (threadIdx.x == 0) n_long = 0;
     __syncthreads();
   }
-  T cmv[CM ? NCH : 1];  // this lane's running column maxima (kAggColmax)
+  // kAggColmax: the block's column maxima in LDS (float bits; non-negative
+  // floats order as their bits), one LDS atomic per lane and column per row
+  const uint32_t ncol = (nv - 1) * VEC + last_valid;
+  __shared__ uint32_t smax[CM ? 512 : 1];
+  if constexpr (CM) {
+    for (uint32_t c = threadIdx.x; c < ncol; c += kAggThreads) smax[c] = 0u;
+    __syncthreads();
+  }
+  auto colmax_row = [&](const T (&acc)[NCH], uint32_t c0) {
 #pragma unroll
-  for (int c = 0; c < (CM ? NCH : 1); ++c) cmv[c] = V::zero();
-  auto colmax_row = [&](const T (&acc)[NCH], uint32_t d) {
-    const float r = fabsf(ax.cm_rs[ax.cm_map[d]]);
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
-    for (int c = 0; c < (CM ? NCH : 1); ++c)
-#pragma unroll
-      for (int q = 0; q < VEC; ++q)
-        vcomp<VEC>(cmv[c], q) = fmaxf(vcomp<VEC>(cmv[c], q), fabsf(vcomp<VEC>(acc[c], q)) * r);
+      for (int q = 0; q < VEC; ++q) {
+        const uint32_t col = (c0 + sl + c * LPD) * VEC + q;
+        if (col < ncol)
+          atomicMax(&smax[col], __float_as_uint(fabsf(vcomp<VEC>(acc[c], q))));
+      }
   };
   for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
     const uint32_t beg = off[d], end = off[d + 1];
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
       }
       store_row<VEC, LPD, NCH, MODE == kAggPostMask ? kAggPlain : EM>(acc, d, c0, sl, nv,
                                                                       last_valid, y, ldy, ax);
-      if constexpr (CM) colmax_row(acc, d);
+      if constexpr (CM) colmax_row(acc, c0);
     }
   }
   if constexpr (COOP) {
@@ -366,32 +371,16 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
             acc[c] = s;
           }
           store_row<VEC, LPD, NCH, EM>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
-          if constexpr (CM) colmax_row(acc, d);
+          if constexpr (CM) colmax_row(acc, c0);
         }
         __syncthreads();
       }
     }
   }
-  if constexpr (CM) {
-    // the wave's column maxima (lane groups of a wave differ in the lane bits
-    // >= LPD), then an atomic only where this wave beats the running global
-    // maximum: after the first few waves almost none does.  A stale read only
-    // costs an extra atomic; the max is monotone, so the result is exact.
-    static_assert(LPD <= 64, "lane groups within one wave");
-    const uint32_t ncol = (nv - 1) * VEC + last_valid;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) {
-        float m = vcomp<VEC>(cmv[c], q);
-        for (int o = LPD; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
-        const uint32_t col = (sl + c * LPD) * VEC + q;
-        if ((threadIdx.x & 63) < LPD && col < ncol && m > 0.f) {
-          const uint32_t mb = __float_as_uint(m);
-          if (__hip_atomic_load(ax.cm_out + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < mb)
-            __hip_atomic_fetch_max(ax.cm_out + col, mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
+  if constexpr (CM) {  // the block's maxima -> its row of the per-block buffer
+    __syncthreads();
+    uint32_t* row = ax.cm_out + (uint64_t)blockIdx.x * ncol;
+    for (uint32_t c = threadIdx.x; c < ncol; c += kAggThreads) row[c] = smax[c];
   }
 }
 
@@ -536,6 +525,18 @@ static Shape pick_shape(uint32_t nv) {
   return {64, (int)std::min<uint32_t>(nch, 8)};
 }
 
+// the vector width launch_gather picks for a local-row gather (no tier, no
+// mask operand): rows padded to a 16-byte multiple take float4 loads, the
+// partial last vector reading pitch padding and storing only its valid floats
+static int plain_vec(uint32_t F, uint64_t ldx, uint64_t ldy, const void* x, const void* y) {
+  int vec = pick_vec(F, ldx, ldy, x, y);
+  const uint32_t F4 = (F + 3) / 4 * 4;
+  if (vec < 4 && F4 <= ldx && F4 <= ldy && ldx % 4 == 0 && ldy % 4 == 0 &&
+      (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0)
+    vec = 4;
+  return vec;
+}
+
 static int gather_u_env() {
   static const int u = [] {
     const char* e = getenv("NTS_GATHER_U");
@@ -590,7 +591,8 @@ template <bool MAP, bool TIER = false, int MODE = kAggPlain, bool COOP = false>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
                          const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
                          uint64_t ldx, const uint32_t* map, uint32_t F, float* y, uint64_t ldy,
-                         Tier tier = Tier{nullptr, nullptr, 0, 0}, AggExtra ax = AggExtra()) {
+                         Tier tier = Tier{nullptr, nullptr, 0, 0}, AggExtra ax = AggExtra(),
+                         uint32_t expect_grid = 0) {
   int vec = pick_vec(F, ldx, ldy, x, y);
   if (TIER) vec = std::min(vec, pick_vec(F, tier.ldh, ldx, tier.host, x));
   if (MODE == kAggMask || MODE == kAggPostMask) vec = std::min(vec, pick_vec(F, ax.ldm, ldx, ax.mx, x));
@@ -617,6 +619,8 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   }();
   // COOP needs one row per lane group
   const uint32_t grid = std::max(1u, COOP ? ceil_div(n_cap, gpb) : std::min(ceil_div(n_cap, gpb), cap));
+  // kAggColmax: the per-block buffer was sized for this grid
+  NTS_CHECK_ARG(expect_grid == 0 || expect_grid == grid, "aggregation grid != the sized one");
   if (vec == 4)
     return launch_gather_vec<4, MAP, TIER, MODE, COOP>(st, grid, last_valid, s, off, idx, w, n_dev,
                                                  n_cap, x, ldx, map, nv, y, ldy, tier, ax);
@@ -664,28 +668,34 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
                               g_out, ld_gout, nullptr, feature_size, g_in, ld_gin);
 }
 
+uint32_t nts_hip_csr_bwd_colmax_rows_per_part(uint32_t feature_size) {
+  if (feature_size == 0) return 0;
+  return (uint32_t)(kAggThreads / pick_shape((feature_size + 3) / 4).lpd);
+}
+
 int nts_hip_spmm_csr_bwd_colmax(nts_hip_ctx* ctx, const uint32_t* row_offset,
                                 const uint32_t* column_indices, const float* weight_backward,
                                 const uint32_t* s, uint32_t s_cap, const float* g_out,
                                 uint64_t ld_gout, uint32_t feature_size, float* g_in,
-                                uint64_t ld_gin, const float* rs, const uint32_t* row_map,
-                                uint32_t* colmax_bits) {
-  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && g_in && rs && row_map &&
-                    colmax_bits, "NULL argument");
+                                uint64_t ld_gin, uint32_t* part_max) {
+  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && g_in && part_max, "NULL argument");
   NTS_CHECK_ARG(ld_gout >= feature_size && ld_gin >= feature_size,
                 "leading dimension < feature_size");
-  NTS_CHECK_ARG(feature_size <= 512, "column maxima: one pass over at most 512 columns");
-  NTS_HIP_TRY(hipSetDevice(ctx->device));
-  NTS_HIP_TRY(hipMemsetAsync(colmax_bits, 0, (size_t)feature_size * sizeof(uint32_t), ctx->stream));
+  NTS_CHECK_ARG(feature_size <= 512, "column maxima: at most 512 columns");
   if (s_cap == 0 || feature_size == 0) return NTS_OK;
+  // the parts follow the COOP grid (one output row per lane group): the
+  // float4 row shape nts_hip_csr_bwd_colmax_rows_per_part assumes
+  NTS_CHECK_ARG(plain_vec(feature_size, ld_gout, ld_gin, g_out, g_in) == 4,
+                "column maxima: 16-byte aligned rows with ld % 4 == 0");
+  const uint32_t rpp = nts_hip_csr_bwd_colmax_rows_per_part(feature_size);
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
   AggExtra ax;
-  ax.cm_rs = rs;
-  ax.cm_map = row_map;
-  ax.cm_out = colmax_bits;
+  ax.cm_out = part_max;
   return launch_gather<false, false, kAggColmax, true>(ctx->stream, row_offset, column_indices,
                                                        weight_backward, s, s_cap, g_out, ld_gout,
                                                        nullptr, feature_size, g_in, ld_gin,
-                                                       Tier{nullptr, nullptr, 0, 0}, ax);
+                                                       Tier{nullptr, nullptr, 0, 0}, ax,
+                                                       ceil_div(s_cap, rpp));
 }
 
 int nts_hip_spmm_csc_fwd_act(nts_hip_ctx* ctx, const uint32_t* column_offset,

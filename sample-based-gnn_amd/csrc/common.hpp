@@ -155,7 +155,12 @@ struct CountArgs {
   const uint32_t* omit_loc;
   uint32_t* omit_row;
 };
-int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream);
+// tmp: count_scan_tmp_elems(v_cap) words for the two-kernel form
+// (NTS_SCAN1=0; the default and tmp == nullptr: the single-pass kernel)
+int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream,
+               uint32_t* tmp);
+size_t count_scan_tmp_elems(uint64_t v_cap);
+bool scan1_enabled();
 
 // Stable LSD radix sort of (key, value) pairs on the low `bits` key bits.
 // n = *n_dev (or n_cap).  vals_in == nullptr means values = 0..n-1.

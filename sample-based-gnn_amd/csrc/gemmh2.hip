@@ -286,6 +286,11 @@ struct H2Extra {
   const float* rs = nullptr;       // row scales of the pair table
   const uint32_t* cmax = nullptr;  // column max bits (W for NN, rs * op(B) for TN)
   const float* rsg = nullptr;      // TN v2: the B rows' scales rs[amap[k]], gathered
+  // TN v4: per-part column maxima of |B| (part p = B rows [p rpp, (p+1) rpp),
+  // N words per part; nts_hip_spmm_csr_bwd_colmax) instead of the pre-pass
+  const uint32_t* cparts = nullptr;
+  uint32_t rpp = 0;
+  uint64_t nparts_ld = 0;  // words per part (>= N)
   const float* bx = nullptr;       // TN BMASK: op(B) = B * bscale where X > 0
   uint64_t ldbx = 0;
   float bscale = 1.f;
@@ -876,8 +881,32 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
   // thread t: columns 4 (t & 31) .. +3 (the B split role below), rows t >> 5 + 16 j
   const int sr = tid >> 5, sc = 4 * (tid & 31);
   int bexp[4];
-  if (ex.cmax) {  // global column maxima from dH's producer (nts_hip_spmm_csr_bwd_colmax)
-    if (tid < 128) sce[tid] = h2_exp(__uint_as_float(ex.cmax[n0 + tid]));
+  if (ex.cparts) {
+    // the chunk's column scales from dH's producer (nts_hip_spmm_csr_bwd_colmax):
+    // max |B[k, c]| over the parts covering the chunk's rows (a superset at the
+    // chunk edges) times max |rs| over the chunk's rows (powers of two), so
+    // every |rs B| 2^e(col) < 2^15; dH is read once, by the main loop
+    float* red = reinterpret_cast<float*>(sbp);  // [4][128] column maxima, [8] rs maxima
+    {
+      const int cl = tid & 127, j = tid >> 7;
+      const uint32_t p0 = (uint32_t)kbeg / ex.rpp, p1 = (uint32_t)(kbeg + klast) / ex.rpp;
+      uint32_t m = 0;
+      for (uint32_t p = p0 + j; p <= p1; p += 4) m = max(m, ex.cparts[(uint64_t)p * ex.nparts_ld + n0 + cl]);
+      red[128 * j + cl] = __uint_as_float(m);
+      float r = 0.f;
+      for (int k = tid; k <= klast; k += kH2Tn3Threads) r = fmaxf(r, fabsf(ssc[k]));
+      for (int o = 32; o > 0; o >>= 1) r = fmaxf(r, __shfl_xor(r, o));
+      if (lane == 0) red[512 + wv] = r;
+    }
+    __syncthreads();
+    if (tid < 128) {
+      float rm = 0.f;
+      for (int w = 0; w < 8; ++w) rm = fmaxf(rm, red[512 + w]);
+      const float m = fmaxf(fmaxf(red[tid], red[128 + tid]), fmaxf(red[256 + tid], red[384 + tid]));
+      // 2^e (m rm) in [2^13, 2^15): e = h2_exp(m) + h2_exp(rm) - 15, with no
+      // product formed (it may overflow)
+      sce[tid] = (m > 0.f && rm > 0.f) ? h2_exp(m) + h2_exp(rm) - 15 : 0;
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 4; ++u) bexp[u] = sce[sc + u];
@@ -1340,7 +1369,7 @@ extern "C" int nts_hip_h2_split_rows_planar(nts_hip_ctx* ctx, uint64_t R, uint32
 // rows of <= 640 pair words (Kp <= 640).  Scratch: [column max][row scales][partials].
 static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q, uint64_t ldq, int Kp,
                          const float* rs, const uint32_t* a_rows, const float* B, uint64_t ldb, float* C,
-                         uint64_t ldc, const uint32_t* colmax_bits) {
+                         uint64_t ldc, const uint32_t* part_max, uint32_t rows_per_part) {
   constexpr int TPW = 5;
   NTS_CHECK_ARG(ctx, "NULL context");
   NTS_CHECK_ARG(M > 0 && M <= 8 * TPW * 16 && N > 0 && N % 128 == 0 && K >= 0, "shape");
@@ -1372,10 +1401,12 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
     out = (float*)ctx->scratch;
     ldo = N;
   }
-  H2Extra ex;  // column scales: the producer's global maxima, else per chunk in the kernel
+  H2Extra ex;  // column scales per chunk: from the producer's per-part maxima, else a pre-pass
   ex.amap = a_rows;
   ex.rs = rs;
-  ex.cmax = colmax_bits;
+  ex.cparts = part_max;
+  ex.rpp = rows_per_part;
+  ex.nparts_ld = (uint64_t)N;
   NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW>),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   hipLaunchKernelGGL((k_h2_tn4<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
@@ -1389,18 +1420,19 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
 extern "C" int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
                                           uint64_t ldq, int Kp, const float* rs, const uint32_t* a_rows,
                                           const float* B, uint64_t ldb, float* C, uint64_t ldc) {
-  return h2p_tn_gather(ctx, M, N, K, Q, ldq, Kp, rs, a_rows, B, ldb, C, ldc, nullptr);
+  return h2p_tn_gather(ctx, M, N, K, Q, ldq, Kp, rs, a_rows, B, ldb, C, ldc, nullptr, 0);
 }
 
-// as nts_hip_gemm_h2p_tn_gather with B's column maxima precomputed (the bits of
-// max_k |rs[a_rows[k]] B[k, c]|, N words, e.g. by nts_hip_spmm_csr_bwd_colmax):
+// as nts_hip_gemm_h2p_tn_gather with per-part column maxima of |B| given (part
+// p = B rows [p R, (p+1) R), N words each, e.g. by nts_hip_spmm_csr_bwd_colmax):
 // the kernel skips its per-chunk pre-pass over B (one read of B instead of two)
 extern "C" int nts_hip_gemm_h2p_tn_gather_cm(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* Q,
                                              uint64_t ldq, int Kp, const float* rs,
                                              const uint32_t* a_rows, const float* B, uint64_t ldb,
-                                             float* C, uint64_t ldc, const uint32_t* colmax_bits) {
-  NTS_CHECK_ARG(colmax_bits, "NULL column maxima");
-  return h2p_tn_gather(ctx, M, N, K, Q, ldq, Kp, rs, a_rows, B, ldb, C, ldc, colmax_bits);
+                                             float* C, uint64_t ldc, const uint32_t* part_max,
+                                             uint32_t rows_per_part) {
+  NTS_CHECK_ARG(part_max && rows_per_part > 0, "NULL column maxima");
+  return h2p_tn_gather(ctx, M, N, K, Q, ldq, Kp, rs, a_rows, B, ldb, C, ldc, part_max, rows_per_part);
 }
 
 // NN v3 on the planar table (k_h2_nn3): N % 128 == 0, Kp <= 640.  The W image

@@ -81,11 +81,14 @@ __device__ __forceinline__ T block_prefix_of(const T* partials, uint32_t count, 
 // computed here — no separate scan of the partials (and no single-workgroup
 // kernel, which stalls for tens of microseconds behind a concurrent stream's
 // large kernels).  Otherwise partials[blockIdx.x] is already the offset.
-template <typename T, bool DIRECT>
+// CNT: the input is the sampler's counts (k_count_reduce) and out[n] is also
+// e_size: sizes[1] = min(out[n], e_cap), overflow flagged in sizes[3].
+template <typename T, bool DIRECT, bool CNT = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
                                                            const uint32_t* n_dev,
                                                            uint64_t n_cap,
-                                                           const T* partials) {
+                                                           const T* partials,
+                                                           uint32_t* sizes, uint32_t e_cap) {
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
   if (base > n) return;
@@ -124,6 +127,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
     uint32_t j = k * kScanThreads + t;
     uint64_t i = base + j;
     if (i <= n) out[i] = tile[pad_idx(j)];
+    if (CNT && i == n) {
+      const T e = tile[pad_idx(j)];
+      sizes[1] = (uint32_t)min(e, (T)e_cap);
+      if (e > (T)e_cap) atomicOr(&sizes[3], 1u);
+    }
   }
 }
 
@@ -144,7 +152,7 @@ int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T
   uint64_t nb = n_cap / kScanTile + 1;
   if (nb == 1) {
     hipLaunchKernelGGL((k_scan_down<T, false>), dim3(1), dim3(kScanThreads), 0, stream, in, out,
-                       n_dev, n_cap, (const T*)nullptr);
+                       n_dev, n_cap, (const T*)nullptr, nullptr, 0u);
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
@@ -155,13 +163,13 @@ int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T
   NTS_LAUNCH_CHECK();
   if (nb <= kScanDirectTiles) {
     hipLaunchKernelGGL((k_scan_down<T, true>), dim3((uint32_t)nb), dim3(kScanThreads), 0, stream,
-                       in, out, n_dev, n_cap, (const T*)partials);
+                       in, out, n_dev, n_cap, (const T*)partials, nullptr, 0u);
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
   NTS_RET(scan_exclusive<T>(partials, partials, nullptr, nb, rest, stream));
   hipLaunchKernelGGL((k_scan_down<T, false>), dim3((uint32_t)nb), dim3(kScanThreads), 0, stream,
-                     in, out, n_dev, n_cap, (const T*)partials);
+                     in, out, n_dev, n_cap, (const T*)partials, nullptr, 0u);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }
@@ -190,6 +198,46 @@ __device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint64_t kind, uin
   return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | (kind << 32) | v;
 }
 
+// The sampler's per-dst counts of the tile's items i = base + k kScanThreads + t:
+// min(deg(dst[i]), fanout) (init_co_only, core/FullyRepGraph.hpp:530-539), 0
+// for a dst of the omit map (sample_gpu_fast_omit, core/ntsFastSampler.hpp:
+// 711-915), whose cache row is recorded in omit_row.  Three rounds of
+// independent loads (dst ids, their offsets, the omit map) instead of one
+// dependent chain per item.
+__device__ __forceinline__ void count_items(const CountArgs& ca, uint64_t base, uint64_t n,
+                                            uint32_t (&x)[kScanItems]) {
+  const int t = threadIdx.x;
+  uint32_t d[kScanItems];
+  uint64_t lo[kScanItems], hi[kScanItems];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+    d[k] = i < n ? ca.dst[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+    lo[k] = i < n ? ca.goff[d[k]] : 0u;
+    hi[k] = i < n ? ca.goff[d[k] + 1] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint32_t deg = (uint32_t)(hi[k] - lo[k]);
+    x[k] = ca.fanout < 0 ? deg : min(deg, (uint32_t)ca.fanout);
+  }
+  if (ca.omit_map) {
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+      if (i < n) {
+        const bool om = ca.omit_map[d[k]] == ca.omit_key;
+        if (om) x[k] = 0;
+        if (ca.omit_row) ca.omit_row[i] = om ? ca.omit_loc[d[k]] : 0xFFFFFFFFu;
+      }
+    }
+  }
+}
+
 template <bool COUNT>
 __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restrict__ in,
                                                         uint32_t* __restrict__ out,
@@ -214,38 +262,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
   if (base > n) return;  // every tile up to the one holding out[n] runs the chain
   if constexpr (COUNT) {
-    // three rounds of independent loads (dst ids, their offsets, the omit
-    // map) instead of one dependent chain per item
-    uint32_t d[kScanItems];
-    uint64_t lo[kScanItems], hi[kScanItems];
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-      const uint64_t i = base + (uint64_t)k * kScanThreads + t;
-      d[k] = i < n ? ca.dst[i] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-      const uint64_t i = base + (uint64_t)k * kScanThreads + t;
-      lo[k] = i < n ? ca.goff[d[k]] : 0u;
-      hi[k] = i < n ? ca.goff[d[k] + 1] : 0u;
-    }
     uint32_t x[kScanItems];
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-      const uint32_t deg = (uint32_t)(hi[k] - lo[k]);
-      x[k] = ca.fanout < 0 ? deg : min(deg, (uint32_t)ca.fanout);
-    }
-    if (ca.omit_map) {
-#pragma unroll
-      for (int k = 0; k < kScanItems; ++k) {
-        const uint64_t i = base + (uint64_t)k * kScanThreads + t;
-        if (i < n) {
-          const bool om = ca.omit_map[d[k]] == ca.omit_key;
-          if (om) x[k] = 0;
-          if (ca.omit_row) ca.omit_row[i] = om ? ca.omit_loc[d[k]] : 0xFFFFFFFFu;
-        }
-      }
-    }
+    count_items(ca, base, n, x);
 #pragma unroll
     for (int k = 0; k < kScanItems; ++k) tile[pad_idx(k * kScanThreads + t)] = x[k];
   } else {
@@ -349,7 +367,76 @@ int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const u
   return NTS_OK;
 }
 
-int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream) {
+// Two-kernel count + scan (NTS_SCAN1=0): per-tile totals of the counts (the
+// counts themselves written to co), then k_scan_down over co in place (it
+// also writes e_size).  No tile waits on another tile's published state.
+// Measured against the single-pass form next to the training stream (one
+// MI355X, bench): C2 0.857 vs 0.851 ms/step, C3 0.708 vs 0.699, GPU sampler
+// alone 4.84 vs 5.07 G edges/s at C2 — the single-pass form stays the default.
+__global__ __launch_bounds__(kScanThreads) void k_count_reduce(CountArgs ca,
+                                                               uint32_t* __restrict__ co,
+                                                               uint32_t* __restrict__ partials) {
+  const int t = threadIdx.x;
+  const uint32_t v_req = *ca.v_in;
+  const uint64_t n = min(v_req, ca.v_cap);
+  if (blockIdx.x == 0 && t == 0) {
+    ca.sizes[0] = (uint32_t)n;
+    ca.sizes[3] = v_req > ca.v_cap ? 1u : 0u;
+  }
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  uint32_t s = 0;
+  if (base < n) {
+    uint32_t x[kScanItems];
+    count_items(ca, base, n, x);
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      const uint64_t i = base + (uint64_t)k * kScanThreads + t;
+      if (i < n) co[i] = x[k];
+      s += x[k];
+    }
+  }
+  __shared__ uint32_t wsum[kScanThreads / kWave];
+  uint32_t tot;
+  (void)block_excl_scan(s, wsum, &tot);
+  if (t == 0) partials[blockIdx.x] = tot;
+}
+
+size_t count_scan_tmp_elems(uint64_t v_cap) { return scan_tmp_elems<uint32_t>(v_cap) + 64; }
+
+// NTS_SCAN1=0: the two-kernel scans for count_scan and the radix histograms
+// (A/B); default the single-pass look-back scans
+bool scan1_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NTS_SCAN1");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream,
+               uint32_t* tmp) {
+  if (!scan1_enabled() && tmp) {
+    const uint64_t nb = (uint64_t)ca.v_cap / kScanTile + 1;
+    uint32_t* partials = tmp;
+    uint32_t* rest = tmp + (nb + 1 + 63) / 64 * 64;
+    hipLaunchKernelGGL(k_count_reduce, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, ca, co,
+                       partials);
+    NTS_LAUNCH_CHECK();
+    if (nb <= kScanDirectTiles) {
+      hipLaunchKernelGGL((k_scan_down<uint32_t, true, true>), dim3((uint32_t)nb),
+                         dim3(kScanThreads), 0, stream, (const uint32_t*)co, co,
+                         (const uint32_t*)ca.sizes, (uint64_t)ca.v_cap, (const uint32_t*)partials,
+                         ca.sizes, ca.e_cap);
+    } else {
+      NTS_RET(scan_exclusive<uint32_t>(partials, partials, nullptr, nb, rest, stream));
+      hipLaunchKernelGGL((k_scan_down<uint32_t, false, true>), dim3((uint32_t)nb),
+                         dim3(kScanThreads), 0, stream, (const uint32_t*)co, co,
+                         (const uint32_t*)ca.sizes, (uint64_t)ca.v_cap, (const uint32_t*)partials,
+                         ca.sizes, ca.e_cap);
+    }
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   const uint64_t nb = (uint64_t)ca.v_cap / kScanTile + 1;
   NTS_RET(ensure_scan_state(ctx, scan1_state_elems(ca.v_cap)));
   hipLaunchKernelGGL(k_scan1<true>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, nullptr,
@@ -541,7 +628,7 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev,
                        n_cap, shift, mask, hist, nb);
     NTS_LAUNCH_CHECK();
-    if (ctx)  // one kernel (single-pass look-back scan on the context's tile states)
+    if (ctx && scan1_enabled())  // one kernel (single-pass look-back scan)
       NTS_RET(scan1_exclusive(ctx, hist, hist, nullptr, hist_n, stream));
     else
       NTS_RET(scan_exclusive<uint32_t>(hist, hist, nullptr, hist_n, stmp, stream));

@@ -1418,7 +1418,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
 
   // scratch layout (u32 words)
   auto al = [](uint64_t x) { return (x + 63) / 64 * 64; };
-  const uint64_t scan_co = al(scan_tmp_elems<uint32_t>(o->v_cap) + 1);
+  const uint64_t scan_co = al(count_scan_tmp_elems(o->v_cap) + 1);
   const uint64_t blk = al(nblk_marks + 1);
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
@@ -1464,8 +1464,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
 
-  // 1) per-dst counts -> column_offset, v_size, e_size: one single-pass
-  // count + scan kernel
+  // 1) per-dst counts -> column_offset, v_size, e_size (count + scan)
   {
     CountArgs ca;
     ca.goff = g->column_offset;
@@ -1479,9 +1478,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
     ca.omit_key = o->omit_key;
     ca.omit_loc = o->omit_loc;
     ca.omit_row = o->omit_row;
-    NTS_RET(count_scan(ctx, ca, o->column_offset, st));
+    NTS_RET(count_scan(ctx, ca, o->column_offset, st, t_scan_co));
   }
-  (void)t_scan_co;
 
   // 2) selection (marks the frontier; the byte map is all zeros here: it is
   // zeroed when allocated and k_mark_write clears what each layer set)

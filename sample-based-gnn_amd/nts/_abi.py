@@ -17,7 +17,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 6  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 7  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
@@ -50,6 +50,7 @@ EXPORTED = (
     "nts_hip_h2_split_rows", "nts_hip_gemm_h2_gather", "nts_hip_gemm_h2_tn_gather",
     "nts_hip_h2_split_rows_planar", "nts_hip_gemm_h2p_tn_gather", "nts_hip_gemm_h2p_gather",
     "nts_hip_spmm_csr_bwd_postmask", "nts_hip_spmm_csr_bwd_colmax", "nts_hip_gemm_h2p_tn_gather_cm",
+    "nts_hip_csr_bwd_colmax_rows_per_part",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -126,10 +127,11 @@ def lib() -> C.CDLL:
         "nts_hip_gemm_h2_tn_gather": ([P, I, I, I, P, U64, P, P, P, U64, P, U64, F, P, U64], I),
         "nts_hip_h2_split_rows_planar": ([P, U64, U32, P, U64, U32, P, U64, P], I),
         "nts_hip_gemm_h2p_tn_gather": ([P, I, I, I, P, U64, I, P, P, P, U64, P, U64], I),
-        "nts_hip_gemm_h2p_tn_gather_cm": ([P, I, I, I, P, U64, I, P, P, P, U64, P, U64, P], I),
+        "nts_hip_gemm_h2p_tn_gather_cm": ([P, I, I, I, P, U64, I, P, P, P, U64, P, U64, P, U32], I),
         "nts_hip_gemm_h2p_gather": ([P, I, I, I, I, P, U64, P, P, P, U64, I, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
-        "nts_hip_spmm_csr_bwd_colmax": ([P, P, P, P, P, U32, P, U64, U32, P, U64, P, P, P], I),
+        "nts_hip_spmm_csr_bwd_colmax": ([P, P, P, P, P, U32, P, U64, U32, P, U64, P], I),
+        "nts_hip_csr_bwd_colmax_rows_per_part": ([U32], U32),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),
         "nts_hip_gemm_relu_dropout_f32": ([P, I, I, I, P, U64, P, U64, P, U64, F, U64, U64], I),

@@ -168,12 +168,16 @@ class HipContext:
                                             ptr(g_out), g_out.stride(0), F, ptr(g_in),
                                             g_in.stride(0)))
 
-    def spmm_csr_bwd_colmax(self, ro, ci, wb, s_dev, s_cap, g_out, g_in, rs, row_map, colmax):
-        """spmm_csr_bwd + colmax (int32 bits) = max_s |g_in[s, c]| * |rs[row_map[s]]|."""
+    def colmax_rows_per_part(self, F):
+        return int(self.lib.nts_hip_csr_bwd_colmax_rows_per_part(F))
+
+    def spmm_csr_bwd_colmax(self, ro, ci, wb, s_dev, s_cap, g_out, g_in, parts):
+        """spmm_csr_bwd + parts[p, c] (int32 bits) = max |g_in[s, c]| over the
+        part's rows s in [p R, (p+1) R), R = colmax_rows_per_part(F)."""
         F = g_out.shape[1]
         check(self.lib.nts_hip_spmm_csr_bwd_colmax(self.h, ptr(ro), ptr(ci), ptr(wb), ptr(s_dev), s_cap,
                                                    ptr(g_out), g_out.stride(0), F, ptr(g_in),
-                                                   g_in.stride(0), ptr(rs), ptr(row_map), ptr(colmax)))
+                                                   g_in.stride(0), ptr(parts)))
 
     def spmm_csc_bwd_atomic(self, co, ri, w, v_dev, v_cap, g_out, g_in):
         F = g_out.shape[1]
@@ -262,14 +266,15 @@ class HipContext:
                                                Q.stride(0), ptr(rs), ptr(rows), ptr(W), W.stride(0), K,
                                                ptr(C), C.stride(0), float(p), int(seed), int(offset)))
 
-    def gemm_h2p_tn_gather(self, Q, rs, rows, B, C, M, colmax=None):
+    def gemm_h2p_tn_gather(self, Q, rs, rows, B, C, M, parts=None, rows_per_part=0):
         """C = X[rows, :M].T @ B with X given as its planar pair table."""
         N = B.shape[1]
         Kr = rows.numel() if rows is not None else B.shape[0]
-        if colmax is not None:  # B's column maxima given (spmm_csr_bwd_colmax)
+        if parts is not None:  # B's per-part column maxima given (spmm_csr_bwd_colmax)
             check(self.lib.nts_hip_gemm_h2p_tn_gather_cm(self.h, M, N, Kr, ptr(Q), Q.stride(0),
                                                          Q.shape[1] // 2, ptr(rs), ptr(rows), ptr(B),
-                                                         B.stride(0), ptr(C), C.stride(0), ptr(colmax)))
+                                                         B.stride(0), ptr(C), C.stride(0), ptr(parts),
+                                                         rows_per_part))
             return
         check(self.lib.nts_hip_gemm_h2p_tn_gather(self.h, M, N, Kr, ptr(Q), Q.stride(0),
                                                   Q.shape[1] // 2, ptr(rs), ptr(rows), ptr(B),

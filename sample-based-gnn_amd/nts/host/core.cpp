@@ -808,7 +808,8 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     const float scale = (float)ctx->saved_data["scale"].toDouble();
     const auto* pairs = reinterpret_cast<const PairTable*>(ctx->saved_data["pairs"].toInt());
     const PairTable* pairs_q = pairs && pairs->tn && pairs->Q.defined() ? pairs : nullptr;
-    NtsVar colmax;  // dH's column maxima (int32 bits), when the gather produced them
+    NtsVar colmax;  // dH's per-part column maxima (int32 bits), when the gather produced them
+    uint32_t rpp = 0;
     // dZ = dX1 ⊙ mask once per dst row, then the plain CSR gather (measured
     // faster than applying the mask to every gathered row:
     // nts_hip_spmm_csr_bwd_masked reads two rows per edge); NTS_TF_MASKED_BWD=1
@@ -834,16 +835,17 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                                        dZ.data_ptr<float>(), (uint64_t)N),
                   "nts_hip_act_backward");
       if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
-      // the planar-table TN GEMM takes dH's column maxima from this gather's
-      // epilogue (one read of dH instead of two); NTS_TN_CHUNK_SCALES=1 keeps
-      // its own per-chunk pre-pass
+      // the planar-table TN GEMM takes dH's column maxima per part of rows
+      // from this gather's epilogue (one read of dH instead of two);
+      // NTS_TN_CHUNK_SCALES=1 keeps its own per-chunk pre-pass
       static const bool chunk_scales = getenv("NTS_TN_CHUNK_SCALES") != nullptr;
-      if (pairs_q && !chunk_scales && N <= 512) {
-        colmax = torch::empty({N}, torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, dev));
+      if (pairs_q && !chunk_scales && N <= 512 && N % 4 == 0) {
+        rpp = nts_hip_csr_bwd_colmax_rows_per_part((uint32_t)N);
+        const int64_t nparts = (std::max<int64_t>(s, 1) + rpp - 1) / rpp;
+        colmax = torch::empty({nparts, N}, torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, dev));
         hip_check(nts_hip_spmm_csr_bwd_colmax(
                       cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(), nullptr, (uint32_t)s,
                       dZ.data_ptr<float>(), (uint64_t)N, (uint32_t)N, dH.data_ptr<float>(), (uint64_t)N,
-                      pairs_q->rs.data_ptr<float>(), sg->dev_src(),
                       reinterpret_cast<uint32_t*>(colmax.data_ptr<int32_t>())),
                   "nts_hip_spmm_csr_bwd_colmax");
       } else {
@@ -865,7 +867,8 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                                               pairs->rs.data_ptr<float>(), sg->dev_src(),
                                               dH.data_ptr<float>(), (uint64_t)N, dW.data_ptr<float>(),
                                               (uint64_t)N,
-                                              reinterpret_cast<const uint32_t*>(colmax.data_ptr<int32_t>())),
+                                              reinterpret_cast<const uint32_t*>(colmax.data_ptr<int32_t>()),
+                                              rpp),
                 "nts_hip_gemm_h2p_tn_gather_cm");
     else if (pairs_q)
       hip_check(nts_hip_gemm_h2p_tn_gather(cs->ctx(), (int)F, (int)N, (int)s,

@@ -228,8 +228,9 @@ def test_h2p_gemm_tn_gather(ctx, M, N, K, gscale):
 @pytest.mark.parametrize("M,N,K,gscale", [(602, 128, 228656, 1e-7), (602, 128, 5003, 1.0),
                                           (100, 256, 3000, 1e3), (41, 128, 17, 1.0)])
 def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale):
-    """TN v4 with B's column maxima given (the CSR backward's epilogue) instead
-    of its per-chunk pre-pass over B: the same error bar vs fp64, deterministic."""
+    """TN v4 with B's per-part column maxima given (the CSR backward's
+    epilogue) instead of its per-chunk pre-pass over B: the same error bar vs
+    fp64, deterministic."""
     g = torch.Generator(device=DEV).manual_seed(M * N + K + 23)
     V = K + K // 2 + 5
     X = _table(V, M, g, decades=6)
@@ -238,11 +239,15 @@ def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale):
     G[:, 5] *= 1e-9
     G[:, 9] = 0.0  # an all-zero column (max 0)
     Q, rs = ctx.h2_split_rows_planar(X)
-    cm = (G.abs() * rs[rows.long()][:, None]).max(0).values.contiguous().view(torch.int32)
+    R = 8  # rows per part (the CSR backward's for N = 128)
+    nparts = (K + R - 1) // R
+    pad = torch.zeros(nparts * R, N, device=DEV)
+    pad[:K] = G.abs()
+    cm = pad.view(nparts, R, N).max(1).values.contiguous().view(torch.int32)
     C32 = torch.empty(M, N, device=DEV)
     Ch = torch.full((M, N), float("nan"), device=DEV)
     ctx.gemm_tn_gather(X, rows, G, C32)
-    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch, M, colmax=cm)
+    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch, M, parts=cm, rows_per_part=R)
     Xg = X[rows.long()].double()
     ref = Xg.t() @ G.double()
     scale = Xg.abs().t() @ G.double().abs() + 1e-300
@@ -251,7 +256,7 @@ def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale):
     assert (Ch[:, 9] == 0).all()
     _check(C32, Ch, ref, scale)
     Ch2 = torch.empty_like(Ch)
-    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch2, M, colmax=cm)
+    ctx.gemm_h2p_tn_gather(Q, rs, rows, G, Ch2, M, parts=cm, rows_per_part=R)
     torch.cuda.synchronize()
     assert torch.equal(Ch, Ch2)
 

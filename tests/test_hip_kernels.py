@@ -528,11 +528,12 @@ def test_spmm_csr_bwd_postmask(hip, cora, F):
     assert torch.isnan(got[s:]).all()
 
 
-@pytest.mark.parametrize("F", [1, 41, 128, 512])
+@pytest.mark.parametrize("F", [4, 40, 128, 512])
 def test_spmm_csr_bwd_colmax(hip, cora, F):
-    """The CSR backward that also emits its output's column maxima (scaled by
-    rs[row_map[row]]) for the pair-table TN GEMM: the rows bit-identical to
-    spmm_csr_bwd's, the maxima exact (hub rows summed cooperatively included)."""
+    """The CSR backward that also emits its output's column maxima per part of
+    R rows for the pair-table TN GEMM: the rows bit-identical to
+    spmm_csr_bwd's, every part's maxima exact (hub rows summed cooperatively
+    included), parts past the live rows zero."""
     V, src, dst = cora
     col, rows = orc.build_csc(V, src, dst)
     out_d, in_d = orc.degrees(V, src, dst)
@@ -541,19 +542,22 @@ def test_spmm_csr_bwd_colmax(hip, cora, F):
     rng = np.random.default_rng(F + 5)
     v, s = l0["v_size"], l0["src_size"]
     G = _t(rng.standard_normal((v, F)).astype(np.float32))
-    rs = _t(np.ldexp(1.0, rng.integers(-20, 20, V)).astype(np.float32))
-    rmap = _t(l0["source"].astype(np.uint32))
     sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
     ro, ci, wb = _t(l0["row_offset"]), _t(l0["column_indices"]), _t(l0["edge_weight_backward"])
     plain = torch.empty(s, F, device=DEV)
     hip.spmm_csr_bwd(ro, ci, wb, sdev, s, G, plain)
-    got = torch.full((s + 2, F), float("nan"), device=DEV)
-    cm = torch.full((F,), -1, dtype=torch.int32, device=DEV)
-    hip.spmm_csr_bwd_colmax(ro, ci, wb, sdev, s + 2, G, got, rs, rmap, cm)
+    cap = s + 37
+    R = hip.colmax_rows_per_part(F)
+    nparts = (cap + R - 1) // R
+    got = torch.full((cap, F), float("nan"), device=DEV)
+    parts = torch.full((nparts, F), -1, dtype=torch.int32, device=DEV)
+    hip.spmm_csr_bwd_colmax(ro, ci, wb, sdev, cap, G, got, parts)
     torch.cuda.synchronize()
     assert torch.equal(got[:s], plain)
-    want = (plain.abs() * rs[rmap.long()][:, None]).max(0).values
-    assert torch.equal(cm.view(torch.float32), want)
+    pad = torch.zeros(nparts * R, F, device=DEV)
+    pad[:s] = plain.abs()
+    want = pad.view(nparts, R, F).max(1).values
+    assert torch.equal(parts.view(torch.float32), want)
 
 
 @pytest.mark.parametrize("M,N,K", [(3000, 128, 602), (2500, 64, 100), (500, 41, 100), (37, 7, 13)])
