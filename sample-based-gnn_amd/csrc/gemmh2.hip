@@ -850,7 +850,10 @@ __device__ __forceinline__ uint32_t h2_swz(int row) { return (uint32_t)(2 * (row
 // TN v4: the structure above on v_mfma_f32_32x32x16_f16 (full-rate f16 MFMA
 // at K = 16; the 16x16x16 form issues at the 16x16x32 form's cycles for half
 // the work: 232 vs 183 us at C2, measured and dropped).
-template <int TPW>
+// DIAG (timing probes only, NTS_TN4_DIAG; results are garbage): bit 0 skips
+// the MFMAs, bit 1 stops streaming after the first two steps, bit 2 skips the
+// partial-slab stores
+template <int TPW, int DIAG = 0>
 __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const char* __restrict__ Q,
                                                             uint64_t ldq, int pitch, int plane_bytes,
                                                             const float* __restrict__ B, uint64_t ldb,
@@ -999,7 +1002,7 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
     if (xpieces == 5) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier_h();
-    issue(s + 2);
+    if (!(DIAG & 2)) issue(s + 2);
     const int st = s % 3;
     {  // split B(s): row sr, 4 columns
       const float4 v = *reinterpret_cast<const float4*>(sbr + st * kH2Tn3BRaw + 512 * sr + 4 * sc);
@@ -1034,10 +1037,10 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
       }
     const char* xs0 = sx + st * xstage + r0 * pitch;
     const char* xs1 = sx + st * xstage + r1 * pitch;
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      if (t >= nmt) continue;
-      f16x8 af[2];
+    // A^T fragments of tile t + 1 read while tile t's MFMAs run (the
+    // sched_barriers keep that order; without them each tile's reads were
+    // waited on right before its MFMAs)
+    auto load_af = [&](int t, f16x8 (&af)[2]) {
 #pragma unroll
       for (int pc = 0; pc < 2; ++pc) {
         const int c = (pc * plane_bytes + 2 * (32 * (m_lo + t) + 16 * half + 4 * tp)) / 16;
@@ -1046,12 +1049,29 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
         const s16x8h cc = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         af[pc] = __builtin_bit_cast(f16x8, cc);
       }
+    };
+    // (the reads are unconditional, past the wave's last tile its last tile
+    // again: a conditional read leaves the waitcnt pass only lgkmcnt(0))
+    f16x8 afr[2][2];  // ring: [t % 2][plane]
+    if (nmt > 0) {
+    load_af(0, afr[0]);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (t + 1 < TPW) load_af(min(t + 1, nmt - 1), afr[(t + 1) % 2]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t >= nmt) continue;
+      const f16x8(&af)[2] = afr[t % 2];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[nt][0], acc[t][nt], 0, 0, 0);
-        acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[nt][1], acc[t][nt], 0, 0, 0);
-        acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[nt][0], acc[t][nt], 0, 0, 0);
+        if constexpr (DIAG & 1) {
+          acc[t][nt][0] += (float)af[1][0] + (float)af[0][0] + (float)bf[nt][0][0] + (float)bf[nt][1][0];
+        } else {
+          acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[1], bf[nt][0], acc[t][nt], 0, 0, 0);
+          acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[nt][1], acc[t][nt], 0, 0, 0);
+          acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[0], bf[nt][0], acc[t][nt], 0, 0, 0);
+        }
       }
+    }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
@@ -1068,7 +1088,7 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int row = 32 * (m_lo + t) + 8 * (v / 4) + 4 * h + (v % 4);
-        if (row < M) Cb[(uint64_t)row * ldc + n0 + cl] = acc[t][nt][v] * cs;
+        if (row < M && (!(DIAG & 4) || acc[t][nt][v] == 1234.5f)) Cb[(uint64_t)row * ldc + n0 + cl] = acc[t][nt][v] * cs;
       }
     }
   }
@@ -1084,7 +1104,13 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
 // nks x 3 v_mfma_f32_16x16x32_f16 on A fragments read from the stage.
 constexpr int kH2Nn3KS = 20;  // k-steps held in registers (Kp <= 640)
 
-template <bool EPI, bool AMAP>
+// NKS > 0: the k-step count fixed at compile time (Kp = 32 NKS): the step loop
+// fully unrolled with the A fragments read from LDS two steps ahead of their
+// MFMAs (with a runtime count each step's reads were waited on right before
+// its MFMAs: one exposed LDS latency per step).
+// DIAG (timing probes only, NTS_NN3_DIAG; results are garbage): bit 0 skips
+// the MFMAs, bit 1 stops streaming tiles after the first two
+template <bool EPI, bool AMAP, int NKS = 0, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const char* __restrict__ Q,
                                                   uint64_t ldq, int pitch, int plane_bytes,
                                                   const char* __restrict__ bimg, float* __restrict__ C,
@@ -1142,22 +1168,53 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
   NTS_NN3_ISSUE(0);
   NTS_NN3_ISSUE(1);
   for (int r = 0; r < nt; ++r) {
-    // tile r landed; younger: round r-2's 4 stores, tile r+1's pieces, round r-1's 4 stores
-    if (xpieces == 5) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // tile r landed.  Younger VMEM ops: r = 0: tile 1's 5 pieces; r = 1:
+    // tile 2's pieces and round 0's 4 stores; r >= 2: round r-2's 4 stores,
+    // tile r+1's pieces, round r-1's 4 stores
+    if (xpieces == 5) {
+      if (r == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else if (r == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     raw_barrier_h();
-    NTS_NN3_ISSUE(r + 2);
+    if (!(DIAG & 2)) NTS_NN3_ISSUE(r + 2);
     const char* xs = sx + (r % 3) * xstage + i * pitch;
     f32x4h acc = f32x4h{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < kH2Nn3KS; ++s) {
-      if (s < nks) {
-        const f16x8 a1 = *reinterpret_cast<const f16x8*>(xs + 16 * ((pch + 4 * s + g) ^ iswz));
-        const f16x8 a0 = *reinterpret_cast<const f16x8*>(xs + 16 * ((4 * s + g) ^ iswz));
+    auto step = [&](int s, const f16x8& a1, const f16x8& a0) {
+      if constexpr (DIAG & 1) {
+        acc[0] += (float)a1[0] + (float)a0[0] + (float)wf[s][0][0] + (float)wf[s][1][0];
+      } else {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, wf[s][0], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][1], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][0], acc, 0, 0, 0);
       }
+    };
+    auto ld1 = [&](int s) { return *reinterpret_cast<const f16x8*>(xs + 16 * ((pch + 4 * s + g) ^ iswz)); };
+    auto ld0 = [&](int s) { return *reinterpret_cast<const f16x8*>(xs + 16 * ((4 * s + g) ^ iswz)); };
+    if constexpr (NKS > 0) {
+      f16x8 b1[3], b0[3];  // fragments of steps s, s+1, s+2 (ring of three)
+      b1[0] = ld1(0);
+      b0[0] = ld0(0);
+      if (NKS > 1) {
+        b1[1] = ld1(1);
+        b0[1] = ld0(1);
+      }
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        if (s + 2 < NKS) {
+          b1[(s + 2) % 3] = ld1(s + 2);
+          b0[(s + 2) % 3] = ld0(s + 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads two steps ahead
+        step(s, b1[s % 3], b0[s % 3]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < kH2Nn3KS; ++s)
+        if (s < nks) step(s, ld1(s), ld0(s));
     }
     // acc[v] = H[16 (t0 + r) + 4 g + v][n0 + 16 wv + i]
     const int64_t r4 = (int64_t)(t0 + r) * 16 + 4 * g;
@@ -1407,11 +1464,24 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
   ex.cparts = part_max;
   ex.rpp = rows_per_part;
   ex.nparts_ld = (uint64_t)N;
-  NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  hipLaunchKernelGGL((k_h2_tn4<TPW>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, ctx->stream, M, K,
-                     reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, B, ldb,
-                     out, ldo, kchunk, splits > 1 ? stride : (uint64_t)0, nnb, ex);
+  static const int diag = [] {
+    const char* e = getenv("NTS_TN4_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+#define NTS_TN4(D)                                                                                 \
+  do {                                                                                             \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW, D>),              \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));             \
+    hipLaunchKernelGGL((k_h2_tn4<TPW, D>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds,           \
+                       ctx->stream, M, K, reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), \
+                       pitch, 2 * Kp, B, ldb, out, ldo, kchunk,                                    \
+                       splits > 1 ? stride : (uint64_t)0, nnb, ex);                                \
+  } while (0)
+  if (diag == 1) NTS_TN4(1);
+  else if (diag == 2) NTS_TN4(2);
+  else if (diag == 4) NTS_TN4(4);
+  else NTS_TN4(0);
+#undef NTS_TN4
   NTS_LAUNCH_CHECK();
   if (splits == 1) return NTS_OK;
   return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
@@ -1477,16 +1547,30 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   const int lds = 3 * 16 * pitch + 2 * 4 * 16 * max_tiles;
   NTS_CHECK_ARG(lds <= 160 * 1024, "row-id stage");
   const dim3 grid(gx, ncb);
-#define NTS_H2NN3(E, MP)                                                                          \
+#define NTS_H2NN3(E, MP, ...)                                                                     \
   do {                                                                                            \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn3<E, MP>),              \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn3<E, MP, ##__VA_ARGS__>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));            \
-    hipLaunchKernelGGL((k_h2_nn3<E, MP>), grid, dim3(512), lds, ctx->stream, M, N, Kp,            \
+    hipLaunchKernelGGL((k_h2_nn3<E, MP, ##__VA_ARGS__>), grid, dim3(512), lds, ctx->stream, M, N, Kp,            \
                        reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, bimg, C, \
                        ldc, ex);                                                                  \
   } while (0)
+  static const int diag = [] {
+    const char* e = getenv("NTS_NN3_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  // compile-time step counts for the feature widths the driver meets
+  // (C2: 602 -> Kp 608); NTS_NN3_DIAG=4 forces the runtime-count loop
   if (relu_dropout) {
     if (a_rows) NTS_H2NN3(true, true); else NTS_H2NN3(true, false);
+  } else if (a_rows && diag == 1) {
+    NTS_H2NN3(false, true, 19, 1);
+  } else if (a_rows && diag == 2) {
+    NTS_H2NN3(false, true, 19, 2);
+  } else if (a_rows && nsteps == 19 && diag != 4) {
+    NTS_H2NN3(false, true, 19);
+  } else if (a_rows && nsteps == 20 && diag != 4) {
+    NTS_H2NN3(false, true, 20);
   } else {
     if (a_rows) NTS_H2NN3(false, true); else NTS_H2NN3(false, false);
   }
