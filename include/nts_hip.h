@@ -501,6 +501,20 @@ int nts_hip_gemm_h2p_gather(nts_hip_ctx *ctx, int relu_dropout, int M, int N, in
                             uint64_t ldw, int K, float *C, uint64_t ldc, float p, uint64_t seed,
                             uint64_t offset);
 
+/* Layer forward on a dynamic fp32 input with at most 128 columns (the
+ * aggregate-first layer of the products / papers-shaped configs, 100 or 128
+ * -> 256): C = act(A W), A split into f16 pairs with power-of-two row scales
+ * inside the kernel, W into pairs with column scales, 3 f16 MFMA products,
+ * fp32 accumulate (the pair-table arithmetic of nts_hip_gemm_h2p_gather).
+ * relu_dropout: the activation of nts_hip_gemm_relu_dropout_f32 (same Philox
+ * keys, so the same elements are dropped).  K <= 128 with K % 4 == 0, A rows
+ * 16-byte aligned, N 128 or 256.  Q != NULL: A's planar pair table
+ * (rows of 2 Kp f16, Kp = K rounded up to 32) and row scales rs[M] are also
+ * written (the weight gradient's operand). */
+int nts_hip_gemm_h2d_act(nts_hip_ctx *ctx, int relu_dropout, int M, int N, int K, const float *A,
+                         uint64_t lda, const float *W, uint64_t ldw, float *C, uint64_t ldc, float p,
+                         uint64_t seed, uint64_t offset, uint16_t *Q, uint64_t ldq, float *rs);
+
 /* Hidden-layer forward with its activation fused into the GEMM epilogue:
  *   C = dropout(relu(A B), p)   — vertexForward's
  *   torch::dropout(torch::relu(x.matmul(W)), drop_rate, training)

@@ -1239,6 +1239,177 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 }
 
 
+// ---------------------------------------------------------------------------
+// NN with a DYNAMIC fp32 A of at most 128 columns (the aggregate-first layer
+// of the products / papers-shaped configs: ~140K aggregated rows x 100 ->
+// 256, where the fp32 and split-bf16 MFMA kernels run at ~1.8 TB/s on a
+// memory-bound shape): C = act(A W) with A split into f16 pairs INSIDE the
+// kernel.  Per 32-row tile: the raw fp32 rows by LDS DMA (three stages, two
+// tiles ahead), one thread per row and 8 columns splits them (row max over 16
+// lanes -> power-of-two row scale, y0 = f16(y), y1 = f16(y - y0)) into two
+// swizzled f16 planes, then each wave runs its W-stationary column tiles
+// (NTW x 16 columns, W's fragments in registers as k_h2_nn3) over the two
+// 16-row halves: 3 v_mfma_f32_16x16x32_f16 per 32-deep step.  Epilogue:
+// rs(row) 2^-e(col) acc, relu/dropout with the Philox keys of
+// nts_hip_gemm_relu_dropout_f32.  QOUT: the planes and row scales are also
+// written out as A's planar pair table (the weight gradient's operand).
+constexpr int kH2dTM = 32;
+
+template <int NKS, int NTW, bool EPI, bool QOUT>
+__global__ __launch_bounds__(512) void k_h2_nnd(int M, int K, const float* __restrict__ A, uint64_t lda,
+                                                const char* __restrict__ bimg, int ncb,
+                                                const uint32_t* __restrict__ cmax, float* __restrict__ C,
+                                                uint64_t ldc, uint16_t* __restrict__ Qo, uint64_t ldq,
+                                                float* __restrict__ rso, H2Extra ex) {
+  constexpr int TM = kH2dTM, KP = 32 * NKS;
+  constexpr int CPR = KP / 4;                 // 16-byte fp32 chunks per raw row
+  constexpr int PCH = KP / 8;                 // 16-byte f16 chunks of a row's k range
+  constexpr int PRB = 256;                    // plane row pitch: 16 chunks (XOR-swizzled by row)
+  constexpr int PL = TM * PRB;                // one plane
+  constexpr int NPC = (TM * CPR + 511) / 512; // LDS-DMA pieces per thread and tile
+  constexpr int RAW = NPC * 512 * 16;         // one raw stage (row-major [TM][KP] fp32 + padding)
+  constexpr int NS = 2 * NTW * 4;             // epilogue stores per wave and tile
+  constexpr int NQ = QOUT ? 3 : 0;            // pair-table stores per wave and tile
+  static_assert(NKS >= 1 && NKS <= 4, "shape");
+  __shared__ __attribute__((aligned(16))) char smem[3 * RAW + 2 * PL + TM * 4];
+  char* const raw = smem;
+  char* const pl = smem + 3 * RAW;
+  float* const srs = reinterpret_cast<float*>(pl + 2 * PL);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int T = (M + TM - 1) / TM;
+  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
+  const int nt = t1 - t0;
+  if (nt <= 0) return;
+  f16x8 wf[NKS][NTW][2];
+  float cs[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int gct = wv * NTW + j, cb = gct >> 3, ct = gct & 7;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        wf[s][j][p] = *reinterpret_cast<const f16x8*>(bimg + ((size_t)s * ncb + cb) * kH2Img +
+                                                      ct * 2 * kH2Frag + p * kH2Frag + 16 * lane);
+    cs[j] = ldexpf(1.f, -h2_exp(__uint_as_float(cmax[16 * gct + i])));
+  }
+  __syncthreads();  // every load above done: the counted waits below start from zero
+  const uint32_t lraw = (uint32_t)(uintptr_t)(lds_ptr_h)raw;
+  // tile r's rows -> raw stage r % 3 (row-major [TM][KP] fp32); chunks past
+  // the row's K load the row's first chunk (zeroed by the split), rows past M
+  // the last row
+  auto issue = [&](int r) {
+    r = min(r, nt - 1);
+#pragma unroll
+    for (int q = 0; q < NPC; ++q) {
+      const int pc = q * 512 + wv * 64 + lane;
+      const int row = pc / CPR, c = pc - row * CPR;
+      const int64_t grow = min((int64_t)(t0 + r) * TM + row, (int64_t)M - 1);
+      // (pieces past the tile land in the stage's padding: any valid address)
+      const float* src = pc < TM * CPR ? A + (uint64_t)grow * lda + (4 * c < K ? 4 * c : 0) : A;
+      glds16h(src, lraw + (r % 3) * RAW + 16 * (q * 512 + wv * 64));
+    }
+  };
+  issue(0);
+  issue(1);
+  const int sr = tid >> 4, sc = tid & 15;  // split role: row, 8-column group
+  for (int r = 0; r < nt; ++r) {
+    // raw tile r landed.  Younger VMEM ops: r = 0: tile 1's pieces; r = 1:
+    // tile 2's pieces + round 0's stores; r >= 2: round r-2's stores, tile
+    // r+1's pieces, round r-1's stores
+    if (r == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NPC) : "memory");
+    else if (r == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NPC + NQ + NS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NPC + 2 * (NQ + NS)) : "memory");
+    raw_barrier_h();  // also: every wave is past tile r-1's plane reads
+    issue(r + 2);
+    const int64_t row0 = (int64_t)(t0 + r) * TM;
+    {  // split: row sr, columns 8 sc .. 8 sc + 7 (16 lanes per row; sc >= PCH: zeros)
+      float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (sc < PCH) {
+        const float* xr = reinterpret_cast<const float*>(raw + (r % 3) * RAW + sr * KP * 4) + 8 * sc;
+        const float4 u0 = *reinterpret_cast<const float4*>(xr);
+        const float4 u1 = *reinterpret_cast<const float4*>(xr + 4);
+        x[0] = u0.x; x[1] = u0.y; x[2] = u0.z; x[3] = u0.w;
+        x[4] = u1.x; x[5] = u1.y; x[6] = u1.z; x[7] = u1.w;
+      }
+      float m = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (8 * sc + k >= K) x[k] = 0.f;
+        m = fmaxf(m, fabsf(x[k]));
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const int e = h2_exp(m);
+      uint32_t w[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) w[k] = h2_pair(ldexpf(x[k], e));
+      f16x8 p0, p1;
+      h2_unpack(w, p0, p1);
+      const float rsv = ldexpf(1.f, -e);
+      if (sc == 0) srs[sr] = rsv;
+      if (sc < PCH) {
+        const int cw = sc ^ (sr & 15);
+        *reinterpret_cast<f16x8*>(pl + sr * PRB + 16 * cw) = p0;
+        *reinterpret_cast<f16x8*>(pl + PL + sr * PRB + 16 * cw) = p1;
+      }
+      if constexpr (QOUT) {  // the planar pair row (clamped duplicates rewrite row M-1 alike)
+        const int64_t grow = min(row0 + sr, (int64_t)M - 1);
+        uint16_t* q = Qo + (uint64_t)grow * ldq;
+        if (sc < PCH) {
+          *reinterpret_cast<f16x8*>(q + 8 * sc) = p0;
+          *reinterpret_cast<f16x8*>(q + KP + 8 * sc) = p1;
+        }
+        if (sc == 0) rso[grow] = rsv;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier_h();
+    f32x4h acc[2][NTW];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ar = 16 * h + i;
+      const char* a0p = pl + ar * PRB;
+      const int swz = ar & 15;
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[h][j] = f32x4h{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const int c = (4 * s + g) ^ swz;
+        const f16x8 a[2] = {*reinterpret_cast<const f16x8*>(a0p + 16 * c),
+                            *reinterpret_cast<const f16x8*>(a0p + PL + 16 * c)};
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[h][j] = mfma3(a, wf[s][j], acc[h][j]);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        const int64_t r4 = row0 + 16 * h + 4 * g;
+        const uint32_t col = (uint32_t)(16 * (wv * NTW + j) + i);
+        float o[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v] = acc[h][j][v] * cs[j] * srs[16 * h + 4 * g + v];
+        if constexpr (EPI) {
+          const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
+          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+  raw_barrier_h();
+}
+
 static int colmax(nts_hip_ctx* ctx, const float* B, uint64_t ldb, uint64_t K, int N, const float* rs,
                   const uint32_t* amap, uint32_t* out, float* rsg = nullptr) {
   NTS_HIP_TRY(hipMemsetAsync(out, 0, (size_t)N * sizeof(uint32_t), ctx->stream));
@@ -1575,6 +1746,62 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     if (a_rows) NTS_H2NN3(false, true); else NTS_H2NN3(false, false);
   }
 #undef NTS_H2NN3
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+// Dynamic-A NN (k_h2_nnd): K <= 128 with K % 4 == 0 and 16-byte rows, N 128 or
+// 256.  W's image and column maxima in scratch (as nts_hip_gemm_h2_gather).
+extern "C" int nts_hip_gemm_h2d_act(nts_hip_ctx* ctx, int relu_dropout, int M, int N, int K,
+                                    const float* A, uint64_t lda, const float* W, uint64_t ldw,
+                                    float* C, uint64_t ldc, float p, uint64_t seed, uint64_t offset,
+                                    uint16_t* Q, uint64_t ldq, float* rs) {
+  NTS_CHECK_ARG(ctx, "NULL context");
+  NTS_CHECK_ARG(M >= 0 && K > 0 && K <= 128 && K % 4 == 0 && (N == 128 || N == 256), "shape");
+  NTS_CHECK_ARG(lda >= (uint64_t)K && lda % 4 == 0 && (uintptr_t)A % 16 == 0, "A rows must be 16-byte aligned");
+  NTS_CHECK_ARG(ldw >= (uint64_t)N && ldw % 4 == 0 && (uintptr_t)W % 16 == 0 && ldc >= (uint64_t)N, "ld");
+  NTS_CHECK_ARG(p >= 0.f && p < 1.f, "p must be in [0, 1)");
+  const int nks = (K + 31) / 32;
+  NTS_CHECK_ARG(!Q || (rs && ldq >= 2 * (uint64_t)(32 * nks) && ldq % 8 == 0 && (uintptr_t)Q % 16 == 0),
+                "pair table output");
+  if (M == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  const int ncb = N / 128;
+  const size_t cm_bytes = ((size_t)N * 4 + 255) / 256 * 256;
+  const size_t img = (size_t)nks * ncb * kH2Img;
+  NTS_RET(ensure_scratch(ctx, cm_bytes + img + 256));
+  uint32_t* cmax = (uint32_t*)ctx->scratch;
+  char* bimg = (char*)ctx->scratch + cm_bytes;
+  hipLaunchKernelGGL(k_h2_prep_w, dim3(nks, ncb), dim3(512), 0, ctx->stream, W, ldw, K, N, cmax, bimg);
+  NTS_LAUNCH_CHECK();
+  H2Extra ex;
+  ex.keep_threshold = relu_dropout ? dropout_threshold(p) : 0u;
+  ex.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  ex.seed = seed;
+  ex.offset = offset;
+  const int T = (M + kH2dTM - 1) / kH2dTM;
+  const dim3 grid(std::max(1, std::min(256, T)));  // one block per CU (~156 VGPRs)
+#define NTS_H2D(NK, NT, E, QO)                                                                   \
+  hipLaunchKernelGGL((k_h2_nnd<NK, NT, E, QO>), grid, dim3(512), 0, ctx->stream, M, K, A, lda,   \
+                     bimg, ncb, cmax, C, ldc, Q, ldq, rs, ex)
+#define NTS_H2D_NK(NK)                                                                           \
+  do {                                                                                           \
+    if (N == 256) {                                                                              \
+      if (relu_dropout) { if (Q) NTS_H2D(NK, 2, true, true); else NTS_H2D(NK, 2, true, false); } \
+      else { if (Q) NTS_H2D(NK, 2, false, true); else NTS_H2D(NK, 2, false, false); }            \
+    } else {                                                                                     \
+      if (relu_dropout) { if (Q) NTS_H2D(NK, 1, true, true); else NTS_H2D(NK, 1, true, false); } \
+      else { if (Q) NTS_H2D(NK, 1, false, true); else NTS_H2D(NK, 1, false, false); }            \
+    }                                                                                            \
+  } while (0)
+  switch (nks) {
+    case 1: NTS_H2D_NK(1); break;
+    case 2: NTS_H2D_NK(2); break;
+    case 3: NTS_H2D_NK(3); break;
+    default: NTS_H2D_NK(4);
+  }
+#undef NTS_H2D_NK
+#undef NTS_H2D
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }

@@ -50,7 +50,7 @@ EXPORTED = (
     "nts_hip_h2_split_rows", "nts_hip_gemm_h2_gather", "nts_hip_gemm_h2_tn_gather",
     "nts_hip_h2_split_rows_planar", "nts_hip_gemm_h2p_tn_gather", "nts_hip_gemm_h2p_gather",
     "nts_hip_spmm_csr_bwd_postmask", "nts_hip_spmm_csr_bwd_colmax", "nts_hip_gemm_h2p_tn_gather_cm",
-    "nts_hip_csr_bwd_colmax_rows_per_part",
+    "nts_hip_csr_bwd_colmax_rows_per_part", "nts_hip_gemm_h2d_act",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -132,6 +132,7 @@ def lib() -> C.CDLL:
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_spmm_csr_bwd_colmax": ([P, P, P, P, P, U32, P, U64, U32, P, U64, P], I),
         "nts_hip_csr_bwd_colmax_rows_per_part": ([U32], U32),
+        "nts_hip_gemm_h2d_act": ([P, I, I, I, I, P, U64, P, U64, P, U64, F, U64, U64, P, U64, P], I),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
         "nts_hip_gemm_f32": ([P, I, I, I, I, P, U64, P, U64, P, U64], I),
         "nts_hip_gemm_relu_dropout_f32": ([P, I, I, I, P, U64, P, U64, P, U64, F, U64, U64], I),

@@ -280,6 +280,17 @@ class HipContext:
                                                   Q.shape[1] // 2, ptr(rs), ptr(rows), ptr(B),
                                                   B.stride(0), ptr(C), C.stride(0)))
 
+    def gemm_h2d_act(self, A, W, C, relu_dropout=False, p=0.0, seed=0, offset=0, Q=None, rs=None):
+        """C = act(A @ W) with A (K <= 128) split into f16 pairs in the kernel;
+        Q/rs: A's planar pair table written on the way."""
+        K, N = W.shape
+        M = A.shape[0]
+        check(self.lib.nts_hip_gemm_h2d_act(self.h, int(relu_dropout), M, N, K, ptr(A), A.stride(0),
+                                            ptr(W), W.stride(0), ptr(C), C.stride(0), float(p), int(seed),
+                                            int(offset), ptr(Q) if Q is not None else None,
+                                            Q.stride(0) if Q is not None else 0,
+                                            ptr(rs) if rs is not None else None))
+
     def gemm_h2_gather(self, P, rs, rows, W, C, relu_dropout=False, p=0.0, seed=0, offset=0):
         """C = act(X[rows] @ W), X given as its pair table (rows None: all rows)."""
         K, N = W.shape

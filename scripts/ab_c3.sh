@@ -1,16 +1,22 @@
 #!/bin/bash
-set -o pipefail
-O=gpurun_out/ab_c3_${1:-a}
+# C3 (products-shaped GraphSAGE 100-256-256-47, 15-10-5, B=1024) and C4
+# (100-256-47, 25-10) bench lines with and without an env knob:
+#   scripts/ab_c3.sh <tag> "<ENV=VAL ...>"
+O=gpurun_out/${1:-abc3}
+E=${2:-NTS_H2_DYN=1}
 mkdir -p $O
-run() {
-  local tag=$1; shift
-  timeout -k 10 300 python -u bench.py --no-cpu-baseline --sampler-batches 0 --epochs 1 --shape products --layers 100-256-256-47 --fanout 15-10-5 --batch 1024 --weight mean --steps 40 --warmup 10 "$@" > $O/$tag.json 2> $O/$tag.err || { echo "bench $tag failed"; tail -5 $O/$tag.err; exit 1; }
-  python3 -c "
-import json
-d=json.loads(open('$O/$tag.json').read().strip().splitlines()[-1]); c=d['config']
-print('$tag', round(d['ms_per_step'],4), 'ms/step', 'issue', round(c['host_train_issue_s_per_step']*1e3,3), 'wait', round(c['host_sampler_wait_s_per_step']*1e3,3))"
-}
-run split3
-run f32 --gemm f32
-NTS_DIAG_REUSE_SAMPLE=1 run reuse_split3 --epochs 0
-run nopipe --no-pipeline
+C3="--shape products --layers 100-256-256-47 --fanout 15-10-5 --batch 1024 --weight mean"
+C4="--shape products --layers 100-256-47 --fanout 25-10 --batch 1024"
+i=0
+for e in "" "$E" "" "$E"; do
+  i=$((i+1))
+  env $e timeout -k 10 300 python -u bench.py $C3 --steps 40 --warmup 10 --no-cpu-baseline --no-secondary-af --epochs 0 --sampler-batches 0 > $O/c3_$i.json 2> $O/c3_$i.err || { echo "c3 failed ($e)"; tail -20 $O/c3_$i.err; exit 1; }
+  env $e timeout -k 10 300 python -u bench.py $C4 --steps 40 --warmup 10 --no-cpu-baseline --no-secondary-af --epochs 0 --sampler-batches 0 > $O/c4_$i.json 2> $O/c4_$i.err || { echo "c4 failed ($e)"; tail -20 $O/c4_$i.err; exit 1; }
+  python3 - "$O" $i "$e" <<'PY'
+import json, sys
+o, i, e = sys.argv[1], sys.argv[2], sys.argv[3]
+for c in ("c3", "c4"):
+    d = json.loads(open(f"{o}/{c}_{i}.json").read().strip().splitlines()[-1])
+    print(c, repr(e), round(d["ms_per_step"], 4), "ms/step", "%.4g" % d["value"])
+PY
+done

@@ -304,3 +304,54 @@ def test_h2p_relu_dropout_epilogue(ctx, p):
     ctx.gemm_h2_gather(P, rs1, None, W, Ci, relu_dropout=True, p=p, seed=seed, offset=offset)
     torch.cuda.synchronize()
     assert torch.equal(Ch, Ci)
+
+
+@pytest.mark.parametrize("M,N,K,decades", [(140156, 256, 100, 0), (5003, 128, 128, 12),
+                                           (4099, 256, 96, 6), (777, 256, 4, 0), (33, 128, 64, 3)])
+def test_h2d_gemm_dynamic_input(ctx, M, N, K, decades):
+    """The narrow dynamic-input NN (k_h2_nnd: A split into pairs in the
+    kernel): the pair-table error bar vs fp64, deterministic, and the pair
+    table it writes on the way equal to h2_split_rows_planar's bit for bit."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + 41)
+    X = _table(M, K, g, decades)
+    W = torch.randn(K, N, device=DEV, generator=g) * 0.05
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.full((M, N), float("nan"), device=DEV)
+    ctx.gemm(X, W, C32)
+    Kp = (K + 31) // 32 * 32
+    Q = torch.full((M, 2 * Kp), -1, dtype=torch.int16, device=DEV)
+    rs = torch.full((M,), float("nan"), device=DEV)
+    ctx.gemm_h2d_act(X, W, Ch, Q=Q, rs=rs)
+    ref = X.double() @ W.double()
+    scale = X.double().abs() @ W.double().abs() + 1e-300
+    Q0, rs0 = ctx.h2_split_rows_planar(X)
+    Ch2 = torch.empty_like(Ch)
+    ctx.gemm_h2d_act(X, W, Ch2)
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ch).any()
+    _check(C32, Ch, ref, scale)
+    assert torch.equal(Ch, Ch2)
+    assert torch.equal(Q, Q0[:, :2 * Kp]) and torch.equal(rs, rs0)
+
+
+@pytest.mark.parametrize("M,N,K,p", [(140156, 256, 100, 0.5), (2050, 128, 64, 0.2), (1000, 256, 128, 0.0)])
+def test_h2d_relu_dropout_epilogue(ctx, M, N, K, p):
+    """k_h2_nnd's relu/dropout epilogue drops the elements the fp32 path drops."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K + 43)
+    X = _table(M, K, g)
+    W = torch.randn(K, N, device=DEV, generator=g)
+    C32 = torch.empty(M, N, device=DEV)
+    Ch = torch.empty(M, N, device=DEV)
+    seed, offset = 0x1234_5678_9ABC, 77
+    ctx.gemm_relu_dropout(X, W, C32, p=p, seed=seed, offset=offset)
+    ctx.gemm_h2d_act(X, W, Ch, relu_dropout=True, p=p, seed=seed, offset=offset)
+    Z = X.double() @ W.double()
+    scale = X.double().abs() @ W.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    clear = Z.abs() > 1e-5 * scale
+    assert torch.equal((C32 != 0) & clear, (Ch != 0) & clear)
+    s = 1.0 / (1.0 - p)
+    ref = torch.where(C32 != 0, torch.relu(Z) * s, torch.zeros_like(Z))
+    e32 = ((C32.double() - ref).abs() / (scale * s))[clear].max().item()
+    eh = ((Ch.double() - ref).abs() / (scale * s))[clear].max().item()
+    assert eh <= 2.0 * e32 + 1e-7 and eh < 1e-6, (eh, e32)
