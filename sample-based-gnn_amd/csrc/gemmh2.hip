@@ -1385,26 +1385,48 @@ __global__ __launch_bounds__(512) void k_h2_nnd(int M, int K, const float* __res
         for (int j = 0; j < NTW; ++j) acc[h][j] = mfma3(a, wf[s][j], acc[h][j]);
       }
     }
+    // epilogue over the (half, column tile) blocks q = 2 h + j.  The keep
+    // bits of lanes i and i ^ 1 come from one Philox call (one call per 4 x 2
+    // elements): per pair of blocks (q0, q1) the even lane draws q0's words,
+    // the odd lane q1's, and they swap
+    constexpr int NB = 2 * NTW;
+    const bool drop = EPI && ex.keep_threshold != 0u;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int q0 = 0; q0 < NB; q0 += 2) {
+      uint32_t wd[2][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+      if (drop) {
+        const int qm = q0 + (i & 1);  // this lane's draw
+        const int64_t r4m = row0 + 16 * (qm / NTW) + 4 * g;
+        const uint32_t colm = (uint32_t)(16 * (wv * NTW + qm % NTW) + i);
+        const uint4 rnd = dropout_words((uint64_t)r4m, colm, ex.seed, ex.offset);
+        const uint32_t mine[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) {
+        for (int v = 0; v < 4; ++v) {
+          const uint32_t other = (uint32_t)__shfl_xor((int)mine[v], 1);
+          wd[0][v] = (i & 1) ? other : mine[v];
+          wd[1][v] = (i & 1) ? mine[v] : other;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = q0 + u, h = q / NTW, j = q % NTW;
         const int64_t r4 = row0 + 16 * h + 4 * g;
         const uint32_t col = (uint32_t)(16 * (wv * NTW + j) + i);
         float o[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) o[v] = acc[h][j][v] * cs[j] * srs[16 * h + 4 * g + v];
         if constexpr (EPI) {
-          const uint4 rnd = dropout_words((uint64_t)r4, col, ex.seed, ex.offset);
-          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
 #pragma unroll
           for (int v = 0; v < 4; ++v)
-            o[v] = (dropout_bits(wd[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+            o[v] = ((!drop || dropout_bits(wd[u][v], col) >= ex.keep_threshold) && o[v] > 0.f)
+                       ? o[v] * ex.scale
+                       : 0.f;
         }
 #pragma unroll
         for (int v = 0; v < 4; ++v)
           if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
       }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
   raw_barrier_h();

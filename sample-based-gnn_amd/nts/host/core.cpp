@@ -698,12 +698,27 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
     const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
     TORCH_CHECK(Wc.size(0) == K, "hip_linear_act: shape mismatch");
     NtsVar X = torch::empty({M, N}, xc.options());
-    hip_check(nts_hip_gemm_relu_dropout_f32(cs->ctx(), (int)M, (int)N, (int)K,
-                                            xc.data_ptr<float>(), (uint64_t)xc.stride(0),
-                                            Wc.data_ptr<float>(), (uint64_t)N, X.data_ptr<float>(),
-                                            (uint64_t)N, (float)p, (uint64_t)seed,
-                                            (uint64_t)offset),
-              "nts_hip_gemm_relu_dropout_f32");
+    // a narrow input (K <= 128, N 128 or 256: the products / papers-shaped
+    // aggregate-first bottom layer) on the in-kernel f16 pair split
+    // (nts_hip_gemm_h2d_act); NTS_H2D=0 keeps the GEMM mode's kernel
+    static const bool h2d = [] {
+      const char* e = getenv("NTS_H2D");
+      return !(e && e[0] == '0');
+    }();
+    if (h2d && K <= 128 && K % 4 == 0 && (N == 128 || N == 256) && xc.stride(0) % 4 == 0 &&
+        (uintptr_t)xc.data_ptr<float>() % 16 == 0)
+      hip_check(nts_hip_gemm_h2d_act(cs->ctx(), 1, (int)M, (int)N, (int)K, xc.data_ptr<float>(),
+                                     (uint64_t)xc.stride(0), Wc.data_ptr<float>(), (uint64_t)N,
+                                     X.data_ptr<float>(), (uint64_t)N, (float)p, (uint64_t)seed,
+                                     (uint64_t)offset, nullptr, 0, nullptr),
+                "nts_hip_gemm_h2d_act");
+    else
+      hip_check(nts_hip_gemm_relu_dropout_f32(cs->ctx(), (int)M, (int)N, (int)K,
+                                              xc.data_ptr<float>(), (uint64_t)xc.stride(0),
+                                              Wc.data_ptr<float>(), (uint64_t)N, X.data_ptr<float>(),
+                                              (uint64_t)N, (float)p, (uint64_t)seed,
+                                              (uint64_t)offset),
+                "nts_hip_gemm_relu_dropout_f32");
     ctx->save_for_backward({xc, Wc, X});
     ctx->saved_data["cs"] = cs_ptr;
     ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
@@ -727,75 +742,6 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
     }
     if (ctx->needs_input_grad(0)) dx = (g * (X > 0).to(g.dtype()) * scale).matmul(W.t());
     return {dx, dW, NtsVar(), NtsVar(), NtsVar(), NtsVar()};
-  }
-};
-
-// Aggregate-first bottom layer with a narrow input (K <= 128: the products /
-// papers-shaped configs): X = act(Y W) with Y split into f16
-// pairs inside the GEMM (nts_hip_gemm_h2d_act), which also writes Y's planar
-// pair table for the weight gradient dW = Y^T dZ (nts_hip_gemm_h2p_tn_gather,
-// the transform-first TN kernel with identity rows).  dZ = dX ⊙ [X > 0] / (1-p)
-// comes from the graph op above when it applied the mask to its own output
-// (sampCSC::post_mask, s->grad_premasked), else from nts_hip_act_backward.
-struct HipBottomNarrowFn : public torch::autograd::Function<HipBottomNarrowFn> {
-  static NtsVar forward(AutogradContext* ctx, NtsVar x, NtsVar W, double p, int64_t seed,
-                        int64_t offset, int64_t cs_ptr, int64_t s_ptr) {
-    auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
-    NtsVar xc = row_major(x), Wc = W.contiguous();
-    const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
-    TORCH_CHECK(Wc.size(0) == K, "hip_bottom_narrow: shape mismatch");
-    const int64_t Kp = (K + 31) / 32 * 32;
-    NtsVar X = torch::empty({M, N}, xc.options());
-    const bool grad = W.requires_grad() && s_ptr != 0;
-    NtsVar Q, rs;
-    if (grad) {
-      Q = torch::empty({M, 2 * Kp}, torch::TensorOptions().dtype(torch::kInt16).device(xc.device()));
-      rs = torch::empty({M}, xc.options());
-    }
-    hip_check(nts_hip_gemm_h2d_act(cs->ctx(), 1, (int)M, (int)N, (int)K, xc.data_ptr<float>(),
-                                   (uint64_t)xc.stride(0), Wc.data_ptr<float>(), (uint64_t)N,
-                                   X.data_ptr<float>(), (uint64_t)N, (float)p, (uint64_t)seed,
-                                   (uint64_t)offset,
-                                   grad ? reinterpret_cast<uint16_t*>(Q.data_ptr<int16_t>()) : nullptr,
-                                   (uint64_t)(2 * Kp), grad ? rs.data_ptr<float>() : nullptr),
-              "nts_hip_gemm_h2d_act");
-    if (grad) {
-      ctx->save_for_backward({Wc, X, Q, rs});
-      ctx->saved_data["s"] = s_ptr;
-    }
-    ctx->saved_data["cs"] = cs_ptr;
-    ctx->saved_data["K"] = K;
-    ctx->saved_data["scale"] = p < 1.0 ? (double)(1.0f / (1.0f - (float)p)) : 0.0;
-    return X;
-  }
-  static variable_list backward(AutogradContext* ctx, variable_list grads) {
-    auto saved = ctx->get_saved_variables();
-    TORCH_CHECK(saved.size() == 4, "hip_bottom_narrow: forward saved no pair table");
-    NtsVar W = saved[0], X = saved[1], Q = saved[2], rs = saved[3];
-    auto* cs = reinterpret_cast<NtsStream*>(ctx->saved_data["cs"].toInt());
-    auto* s = reinterpret_cast<sampCSC*>(ctx->saved_data["s"].toInt());
-    const float scale = (float)ctx->saved_data["scale"].toDouble();
-    const int64_t K = ctx->saved_data["K"].toInt();
-    NtsVar g = grads[0].contiguous();
-    const int64_t M = X.size(0), N = X.size(1);
-    NtsVar dZ = g;
-    if (!s->grad_premasked) {
-      dZ = torch::empty({M, N}, g.options());
-      hip_check(nts_hip_act_backward(cs->ctx(), (uint32_t)M, (uint32_t)N, g.data_ptr<float>(),
-                                     (uint64_t)N, X.data_ptr<float>(), (uint64_t)N, scale,
-                                     dZ.data_ptr<float>(), (uint64_t)N),
-                "nts_hip_act_backward");
-    }
-    NtsVar dW = torch::empty({K, N}, W.options());
-    hip_check(nts_hip_gemm_h2p_tn_gather(cs->ctx(), (int)K, (int)N, (int)M,
-                                         reinterpret_cast<const uint16_t*>(Q.data_ptr<int16_t>()),
-                                         (uint64_t)Q.stride(0), (int)(Q.size(1) / 2),
-                                         rs.data_ptr<float>(), nullptr, dZ.data_ptr<float>(),
-                                         (uint64_t)N, dW.data_ptr<float>(), (uint64_t)N),
-              "nts_hip_gemm_h2p_tn_gather");
-    NtsVar dx;
-    if (ctx->needs_input_grad(0)) dx = dZ.matmul(W.t());
-    return {dx, dW, NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
 
@@ -1031,23 +977,6 @@ NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
                       NtsStream* cs) {
   return HipLinearActFn::apply(x, W, p, (int64_t)seed, (int64_t)offset,
                                reinterpret_cast<int64_t>(cs));
-}
-
-bool bottom_narrow_ok(const NtsVar& x, const NtsVar& W) {
-  static const bool on = [] {
-    const char* e = getenv("NTS_H2D");
-    return !(e && e[0] == '0');
-  }();
-  const int64_t M = x.size(0), K = x.size(1), N = W.size(1);
-  return on && x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 4 == 0 &&
-         (uintptr_t)x.data_ptr<float>() % 16 == 0 && K <= 128 && K % 4 == 0 &&
-         (N == 128 || N == 256) && M >= 1;
-}
-
-NtsVar hip_bottom_narrow(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
-                         uint64_t offset, NtsStream* cs, sampCSC* s) {
-  return HipBottomNarrowFn::apply(x, W, p, (int64_t)seed, (int64_t)offset,
-                                  reinterpret_cast<int64_t>(cs), reinterpret_cast<int64_t>(s));
 }
 
 // dropout(relu(x)) on its own (nts_hip_relu_dropout_f32, the GEMM epilogue's

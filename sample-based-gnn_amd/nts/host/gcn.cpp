@@ -320,28 +320,6 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::weights() {
 NtsVar GCN_SAMPLE_ALLGPU_impl::vertexForward(int l, NtsVar& a) {
   const int L = (int)P.size();
   if (l == L - 1) return P[l]->forward(a).log_softmax(1);
-  if (l == 0 && cur_bottom_ && cfg.hip_gemm && cfg.fuse_activation && cfg.pair_table >= 1 &&
-      bottom_narrow_ok(a, P[0]->W)) {
-    // narrow aggregate-first bottom layer: the graph op above
-    // applies this layer's relu/dropout backward to its own output rows
-    // (post_mask, as the transform-first layer), over its CSR
-    const bool train = ctx.is_train();
-    const double p = train ? cfg.drop_rate : 0.0;
-    NtsVar X = hip_bottom_narrow(a, P[0]->W, p, (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1,
-                                 dropout_calls_++, cs.get(), train ? cur_bottom_ : nullptr);
-    const bool fuse = train && cur_up_ && cur_up_->has_csr;
-    if (cur_up_) {
-      cur_up_->post_mask = fuse ? X.data_ptr<float>() : nullptr;
-      cur_up_->post_mask_ld = (uint64_t)X.stride(0);
-      cur_up_->post_mask_scale = p < 1.0 ? 1.0f / (1.0f - (float)p) : 0.f;
-    }
-    cur_bottom_->grad_premasked = fuse;
-    return X;
-  }
-  if (l == 0 && cur_up_) {  // no fused activation backward over this batch's slot
-    cur_up_->post_mask = nullptr;
-    if (cur_bottom_) cur_bottom_->grad_premasked = false;
-  }
   if (cfg.hip_gemm && cfg.fuse_activation) {
     const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
     return hip_linear_act(a, P[l]->W, p, (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1,
@@ -355,9 +333,6 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
                                                      const NtsVar* loss_target) {
   const int L = (int)P.size();
   std::vector<NtsVar> acts;
-  // the bottom layer's sampled graph and the one above it (vertexForward(0))
-  cur_bottom_ = (!tf_ && !pd_active_ && !cfg.gat) ? sg->sampled_sgs[L - 1] : nullptr;
-  cur_up_ = cur_bottom_ && L >= 2 ? sg->sampled_sgs[L - 2] : nullptr;
   NtsVar X0;
   if (!cfg.fused_gather && !tf_) {
     if (fcache)

@@ -42,9 +42,7 @@ struct GCNConfig {
   // transform-first GEMMs on the feature table's f16 pair table (csrc/gemmh2.hip,
   // built once at construction): 0 = off (gemm_mode), 1 = the forward GEMM,
   // 2 = the forward and the weight-gradient GEMMs, 3 = 2 with the weight
-  // gradient on the planar table's whole-row kernel where the shape allows;
-  // >= 1 also runs an aggregate-first bottom layer with a narrow input
-  // (K <= 128, N 128 or 256) on the in-kernel pair split (hip_bottom_narrow)
+  // gradient on the planar table's whole-row kernel where the shape allows
   int pair_table = 3;
   // data parallel: the gradient all-reduce of step k runs on a stream of its
   // own and the optimizer step waits for it only where step k+1 first reads
@@ -195,10 +193,6 @@ class GCN_SAMPLE_ALLGPU_impl {
   hipEvent_t ready_[kSlots] = {nullptr, nullptr, nullptr};
   bool early_ = false;
   uint64_t dropout_calls_ = 0;  // Philox offset of the fused dropout masks
-  // the current batch's bottom layer and the layer above it (forward() sets
-  // them for vertexForward(0)'s narrow bottom path; nullptr: not that path)
-  sampCSC* cur_bottom_ = nullptr;
-  sampCSC* cur_up_ = nullptr;
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch
   int next_slot_ = 0;
   int reuse_slot_ = -1;  // NTS_DIAG_REUSE_SAMPLE

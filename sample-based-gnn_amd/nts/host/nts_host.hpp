@@ -391,14 +391,6 @@ NtsVar row_major(const NtsVar& x);
 NtsVar row_padded_empty(int64_t rows, int64_t F, int device);
 // dropout(relu(x W), p) in one MFMA GEMM (activation in the epilogue, Philox
 // mask of (seed, offset)); autograd: dW = x^T (dX ⊙ [X > 0] / (1-p)) fused.
-// The aggregate-first bottom layer when its input is narrow (K <= 128,
-// bottom_narrow_ok): in-kernel f16 pair split forward, pair-table weight
-// gradient (core.cpp HipBottomNarrowFn); s: the bottom layer's sampCSC, whose
-// grad_premasked says the graph op above applied the activation backward
-// (nullptr: no backward)
-bool bottom_narrow_ok(const NtsVar& x, const NtsVar& W);
-NtsVar hip_bottom_narrow(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
-                         uint64_t offset, NtsStream* cs, sampCSC* s);
 NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
                       NtsStream* cs);
 

@@ -160,9 +160,9 @@ def test_training_step_matches_oracle_step(E, graph, tf, pt):
     """One train_batch: sample -> forward -> NLL -> self_backward (graph-op
     backward through the CSR) -> learn_local_with_decay_Adam, vs the oracle
     (tf = 1: the bottom layer transform-first, its backward through the bottom
-    layer's CSR and the row-gathered weight-gradient GEMM; tf = 0, pt 3, H 128:
-    the narrow aggregate-first bottom layer on the in-kernel pair split, its
-    activation backward fused into the graph op above)."""
+    layer's CSR and the row-gathered weight-gradient GEMM; tf = 0, H 128: the
+    narrow aggregate-first bottom layer's forward on the in-kernel pair
+    split, nts_hip_gemm_h2d_act)."""
     F, C, B = 64, 7, 200
     H = 128 if pt == 3 else 32  # pt 3: the planar weight-gradient kernel takes N % 128 == 0
     drv, feat, labels, train = _driver(E, graph, F, C, [F, H, C], [10, 5], B, transform_first=tf,
