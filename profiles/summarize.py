@@ -31,8 +31,8 @@ def profiler_kernel(name: str):
         mode = targs[6] if len(targs) > 6 else "0"
         if mode == "1":
             return "bottom_aggregation"          # transform-first: A H + relu/dropout
-        if mode == "2":
-            return "bottom_backward"             # A^T (dX ⊙ mask)
+        if mode in ("2", "4"):
+            return "bottom_backward"             # A^T (dX ⊙ mask) / A^T dZ + column maxima
         if targs[3] == "true" and targs[5] == "false":
             return "bottom_aggregation"          # aggregate-first: fused gather A X
         return None
@@ -44,7 +44,7 @@ def profiler_kernel(name: str):
         return "gather_gemm_tn"                  # X[src]^T dH (no mask)
     if k == "k_s3_tn" and targs[1:] == ["false", "true"]:
         return "gather_gemm_tn"                  # split-bf16 X[src]^T dH
-    if k in ("k_h2_nn", "k_h2_nn2", "k_h2_nn3") and targs == ["false", "true"]:
+    if k in ("k_h2_nn", "k_h2_nn2", "k_h2_nn3") and targs[:2] == ["false", "true"]:
         return "gather_gemm"                     # f16 pair table X[src] W0
     if k in ("k_h2_tn2", "k_h2_tn3", "k_h2_tn4"):
         return "gather_gemm_tn"                  # f16 pair table X[src]^T dH
