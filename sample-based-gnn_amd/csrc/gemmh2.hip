@@ -853,7 +853,8 @@ __device__ __forceinline__ uint32_t h2_swz(int row) { return (uint32_t)(2 * (row
 // DIAG (timing probes only, NTS_TN4_DIAG; results are garbage): bit 0 skips
 // the MFMAs, bit 1 stops streaming after the first two steps, bit 2 skips the
 // partial-slab stores
-template <int TPW, int DIAG = 0>
+// RP (pitch 2560 only): row-aligned LDS-DMA pieces, as k_h2_nn3
+template <int TPW, int DIAG = 0, bool RP = false>
 __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const char* __restrict__ Q,
                                                             uint64_t ldq, int pitch, int plane_bytes,
                                                             const float* __restrict__ B, uint64_t ldb,
@@ -952,14 +953,27 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
   auto issue = [&](int s) {
     s = min(s, nsteps - 1);
     const int st = s % 3;
-    for (int q = 0; q < xpieces; ++q) {
-      const int p = wv * xpieces + q;
-      const int o = 1024 * p + 16 * lane;
-      const int row = o / pitch, c = (o - row * pitch) / 16;
-      const int gc = c ^ (int)h2_swz(row);  // the global chunk this LDS slot holds
-      const uint32_t id = sid[min(16 * s + row, klast)];
-      const char* src = Q + (uint64_t)id * ldq + 16 * (gc < row_chunks ? gc : 0);
-      glds16h(src, lsx + st * xstage + 1024 * p);
+    if constexpr (RP) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int p = wv * 6 + q, row = p / 3, part = p - 3 * row;
+        const int c = 64 * part + lane;  // LDS slot (16-byte chunk) of the row
+        const int gc = c ^ (int)h2_swz(row);
+        const uint32_t id = sid[min(16 * s + row, klast)];
+        const char* src = Q + (uint64_t)id * ldq + 16 * (gc < row_chunks ? gc : 0);
+        const uint32_t dst = __builtin_amdgcn_readfirstlane(lsx + st * xstage + row * 2560 + 1024 * part);
+        if (c < 160) glds16h(src, dst);
+      }
+    } else {
+      for (int q = 0; q < xpieces; ++q) {
+        const int p = wv * xpieces + q;
+        const int o = 1024 * p + 16 * lane;
+        const int row = o / pitch, c = (o - row * pitch) / 16;
+        const int gc = c ^ (int)h2_swz(row);  // the global chunk this LDS slot holds
+        const uint32_t id = sid[min(16 * s + row, klast)];
+        const char* src = Q + (uint64_t)id * ldq + 16 * (gc < row_chunks ? gc : 0);
+        glds16h(src, lsx + st * xstage + 1024 * p);
+      }
     }
     {  // B raw: 1 KB per wave (rows 2 wv, 2 wv + 1)
       const int row = 2 * wv + (lane >> 5);
@@ -999,7 +1013,8 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
   issue(1);
   for (int s = 0; s < nsteps; ++s) {
     // X(s), B(s) landed (X(s+1), B(s+1) may stay in flight: xpieces + 1 per step)
-    if (xpieces == 5) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (RP) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else if (xpieces == 5) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     raw_barrier_h();
     if (!(DIAG & 2)) issue(s + 2);
@@ -1110,7 +1125,10 @@ constexpr int kH2Nn3KS = 20;  // k-steps held in registers (Kp <= 640)
 // its MFMAs: one exposed LDS latency per step).
 // DIAG (timing probes only, NTS_NN3_DIAG; results are garbage): bit 0 skips
 // the MFMAs, bit 1 stops streaming tiles after the first two
-template <bool EPI, bool AMAP, int NKS = 0, int DIAG = 0>
+// RP (pitch 2560 only): LDS-DMA pieces cut at row boundaries — three per row
+// (1 KiB, 1 KiB, 512 B with 32 lanes), six per wave and tile — instead of
+// 1 KiB pieces that straddle rows (MI355X_MICROARCH.md, indexed rows into LDS)
+template <bool EPI, bool AMAP, int NKS = 0, int DIAG = 0, bool RP = false>
 __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const char* __restrict__ Q,
                                                   uint64_t ldq, int pitch, int plane_bytes,
                                                   const char* __restrict__ bimg, float* __restrict__ C,
@@ -1154,13 +1172,24 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 #define NTS_NN3_ISSUE(R_)                                                                        \
   do {                                                                                           \
     const int r_ = min((R_), nt - 1);                                                            \
-    for (int q = 0; q < xpieces; ++q) {                                                          \
-      const int p = wv * xpieces + q;                                                            \
-      const int o = 1024 * p + 16 * lane;                                                        \
-      const int row = o / pitch, c = (o - row * pitch) / 16;                                     \
-      const int gc = c ^ (row & 15); /* the global chunk this LDS slot holds */                  \
-      const char* src = Q + (uint64_t)sid[16 * r_ + row] * ldq + 16 * (gc < row_chunks ? gc : 0); \
-      glds16h(src, lsx + (r_ % 3) * xstage + 1024 * p);                                          \
+    if constexpr (RP) {                                                                          \
+      _Pragma("unroll") for (int q = 0; q < 6; ++q) {                                            \
+        const int p = wv * 6 + q, row = p / 3, part = p - 3 * row;                               \
+        const int c = 64 * part + lane; /* LDS slot (16-byte chunk) of the row */               \
+        const int gc = c ^ (row & 15);                                                           \
+        const char* src = Q + (uint64_t)sid[16 * r_ + row] * ldq + 16 * (gc < row_chunks ? gc : 0); \
+        const uint32_t dst_ = __builtin_amdgcn_readfirstlane(lsx + (r_ % 3) * xstage + row * 2560 + 1024 * part); \
+        if (c < 160) glds16h(src, dst_);                                                         \
+      }                                                                                          \
+    } else {                                                                                     \
+      for (int q = 0; q < xpieces; ++q) {                                                        \
+        const int p = wv * xpieces + q;                                                          \
+        const int o = 1024 * p + 16 * lane;                                                      \
+        const int row = o / pitch, c = (o - row * pitch) / 16;                                   \
+        const int gc = c ^ (row & 15); /* the global chunk this LDS slot holds */                \
+        const char* src = Q + (uint64_t)sid[16 * r_ + row] * ldq + 16 * (gc < row_chunks ? gc : 0); \
+        glds16h(src, lsx + (r_ % 3) * xstage + 1024 * p);                                        \
+      }                                                                                          \
     }                                                                                            \
   } while (0)
   const int pch = plane_bytes / 16;  // chunks per plane
@@ -1171,7 +1200,11 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
     // tile r landed.  Younger VMEM ops: r = 0: tile 1's 5 pieces; r = 1:
     // tile 2's pieces and round 0's 4 stores; r >= 2: round r-2's 4 stores,
     // tile r+1's pieces, round r-1's 4 stores
-    if (xpieces == 5) {
+    if (RP) {  // six pieces per wave and tile
+      if (r == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (r == 1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+    } else if (xpieces == 5) {
       if (r == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       else if (r == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
@@ -1661,11 +1694,15 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
     const char* e = getenv("NTS_TN4_DIAG");
     return e ? atoi(e) : 0;
   }();
-#define NTS_TN4(D)                                                                                 \
+  static const bool rp = [] {  // row-aligned DMA pieces (A/B: NTS_TN4_RP=0)
+    const char* e = getenv("NTS_TN4_RP");
+    return !(e && e[0] == '0');
+  }();
+#define NTS_TN4(D, ...)                                                                            \
   do {                                                                                             \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW, D>),              \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW, D, ##__VA_ARGS__>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));             \
-    hipLaunchKernelGGL((k_h2_tn4<TPW, D>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds,           \
+    hipLaunchKernelGGL((k_h2_tn4<TPW, D, ##__VA_ARGS__>), dim3(nnb * splits), dim3(kH2Tn3Threads), lds, \
                        ctx->stream, M, K, reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), \
                        pitch, 2 * Kp, B, ldb, out, ldo, kchunk,                                    \
                        splits > 1 ? stride : (uint64_t)0, nnb, ex);                                \
@@ -1673,6 +1710,7 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
   if (diag == 1) NTS_TN4(1);
   else if (diag == 2) NTS_TN4(2);
   else if (diag == 4) NTS_TN4(4);
+  else if (rp && pitch == 2560) NTS_TN4(0, true);
   else NTS_TN4(0);
 #undef NTS_TN4
   NTS_LAUNCH_CHECK();
@@ -1752,6 +1790,11 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     const char* e = getenv("NTS_NN3_DIAG");
     return e ? atoi(e) : 0;
   }();
+  // row-aligned LDS-DMA pieces (A/B: NTS_NN3_RP=0 keeps the row-straddling ones)
+  static const bool rp = [] {
+    const char* e = getenv("NTS_NN3_RP");
+    return !(e && e[0] == '0');
+  }();
   // compile-time step counts for the feature widths the driver meets
   // (C2: 602 -> Kp 608); NTS_NN3_DIAG=4 forces the runtime-count loop
   if (relu_dropout) {
@@ -1760,8 +1803,12 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     NTS_H2NN3(false, true, 19, 1);
   } else if (a_rows && diag == 2) {
     NTS_H2NN3(false, true, 19, 2);
+  } else if (a_rows && nsteps == 19 && diag != 4 && pitch == 2560 && rp) {
+    NTS_H2NN3(false, true, 19, 0, true);
   } else if (a_rows && nsteps == 19 && diag != 4) {
     NTS_H2NN3(false, true, 19);
+  } else if (a_rows && nsteps == 20 && diag != 4 && pitch == 2560 && rp) {
+    NTS_H2NN3(false, true, 20, 0, true);
   } else if (a_rows && nsteps == 20 && diag != 4) {
     NTS_H2NN3(false, true, 20);
   } else {
