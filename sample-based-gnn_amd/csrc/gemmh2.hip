@@ -1128,7 +1128,10 @@ constexpr int kH2Nn3KS = 20;  // k-steps held in registers (Kp <= 640)
 // RP (pitch 2560 only): LDS-DMA pieces cut at row boundaries — three per row
 // (1 KiB, 1 KiB, 512 B with 32 lanes), six per wave and tile — instead of
 // 1 KiB pieces that straddle rows (MI355X_MICROARCH.md, indexed rows into LDS)
-template <bool EPI, bool AMAP, int NKS = 0, int DIAG = 0, bool RP = false>
+// TR (no epilogue activation, NKS > 0): the MFMA operands swapped so that
+// each lane holds four consecutive columns of one row — one 16-byte store per
+// lane and tile instead of four 4-byte stores
+template <bool EPI, bool AMAP, int NKS = 0, int DIAG = 0, bool RP = false, bool TR = false>
 __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const char* __restrict__ Q,
                                                   uint64_t ldq, int pitch, int plane_bytes,
                                                   const char* __restrict__ bimg, float* __restrict__ C,
@@ -1165,6 +1168,10 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
                                p * kH2Frag + 16 * lane)
                          : f16x8{};
   const float cs = ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[n0 + 16 * wv + i])));
+  float cs4[4];  // TR: the scales of this lane's columns n0 + 16 wv + 4 g + v
+#pragma unroll
+  for (int v = 0; v < 4; ++v)
+    cs4[v] = TR ? ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[n0 + 16 * wv + 4 * g + v]))) : 0.f;
   __syncthreads();  // (waits for every load above: the LDS DMA counts below start from zero)
   const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx;
   const int xpieces = xstage / 1024 / 8;
@@ -1200,10 +1207,15 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
     // tile r landed.  Younger VMEM ops: r = 0: tile 1's 5 pieces; r = 1:
     // tile 2's pieces and round 0's 4 stores; r >= 2: round r-2's 4 stores,
     // tile r+1's pieces, round r-1's 4 stores
+    constexpr int NST = TR ? 1 : 4;  // stores per wave and tile
     if (RP) {  // six pieces per wave and tile
       if (r == 0) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else if (r == 1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+      else if (r == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + 2 * NST) : "memory");
+    } else if (TR && xpieces == 5) {
+      if (r == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else if (r == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 + NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(5 + 2 * NST) : "memory");
     } else if (xpieces == 5) {
       if (r == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       else if (r == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
@@ -1218,6 +1230,10 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
     auto step = [&](int s, const f16x8& a1, const f16x8& a0) {
       if constexpr (DIAG & 1) {
         acc[0] += (float)a1[0] + (float)a0[0] + (float)wf[s][0][0] + (float)wf[s][1][0];
+      } else if constexpr (TR) {  // D^T: rows of W^T (columns) x columns of X^T (rows)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][0], a1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][1], a0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][0], a0, acc, 0, 0, 0);
       } else {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, wf[s][0], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][1], acc, 0, 0, 0);
@@ -1248,6 +1264,14 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 #pragma unroll
       for (int s = 0; s < kH2Nn3KS; ++s)
         if (s < nks) step(s, ld1(s), ld0(s));
+    }
+    if constexpr (TR) {  // acc[v] = H[16 (t0 + r) + i][n0 + 16 wv + 4 g + v]
+      const int64_t row = (int64_t)(t0 + r) * 16 + i;
+      const float rsr = srs[16 * r + i];
+      const float4 o4 = make_float4(acc[0] * cs4[0] * rsr, acc[1] * cs4[1] * rsr,
+                                    acc[2] * cs4[2] * rsr, acc[3] * cs4[3] * rsr);
+      if (row < M) *reinterpret_cast<float4*>(C + (uint64_t)row * ldc + n0 + 16 * wv + 4 * g) = o4;
+      continue;
     }
     // acc[v] = H[16 (t0 + r) + 4 g + v][n0 + 16 wv + i]
     const int64_t r4 = (int64_t)(t0 + r) * 16 + 4 * g;
@@ -1795,6 +1819,13 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     const char* e = getenv("NTS_NN3_RP");
     return !(e && e[0] == '0');
   }();
+  // 16-byte row stores from swapped MFMA operands (NTS_NN3_TR=1; measured:
+  // alone 174-178 -> 168-170 us, in the C2 bench no gain — off by default)
+  static const bool tr = [] {
+    const char* e = getenv("NTS_NN3_TR");
+    return e && e[0] == '1';
+  }();
+  const bool tr_ok = tr && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
   // compile-time step counts for the feature widths the driver meets
   // (C2: 602 -> Kp 608); NTS_NN3_DIAG=4 forces the runtime-count loop
   if (relu_dropout) {
@@ -1803,12 +1834,14 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     NTS_H2NN3(false, true, 19, 1);
   } else if (a_rows && diag == 2) {
     NTS_H2NN3(false, true, 19, 2);
+  } else if (a_rows && nsteps == 19 && diag != 4 && pitch == 2560 && rp && tr_ok) {
+    NTS_H2NN3(false, true, 19, 0, true, true);
   } else if (a_rows && nsteps == 19 && diag != 4 && pitch == 2560 && rp) {
     NTS_H2NN3(false, true, 19, 0, true);
   } else if (a_rows && nsteps == 19 && diag != 4) {
     NTS_H2NN3(false, true, 19);
-  } else if (a_rows && nsteps == 20 && diag != 4 && pitch == 2560 && rp) {
-    NTS_H2NN3(false, true, 20, 0, true);
+  } else if (a_rows && nsteps == 20 && diag != 4 && pitch == 2560 && rp && tr_ok) {
+    NTS_H2NN3(false, true, 20, 0, true, true);
   } else if (a_rows && nsteps == 20 && diag != 4) {
     NTS_H2NN3(false, true, 20);
   } else {
