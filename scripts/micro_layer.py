@@ -46,7 +46,8 @@ def main():
     X = torch.empty(a.M, a.N, device=dev)
     dW = torch.empty(a.K, a.N, device=dev)
     out = {"shape": [a.M, a.K, a.N]}
-    for name, mode in (("f32", _abi.NTS_GEMM_F32), ("split3", _abi.NTS_GEMM_SPLIT3)):
+    for name, mode in (("f32", _abi.NTS_GEMM_F32), ("split3", _abi.NTS_GEMM_SPLIT3),
+                       ("split3all", _abi.NTS_GEMM_SPLIT3_ALL)):
         c = HipContext(0)
         c.set_gemm_mode(mode)
         out[name + "_fwd_act_us"] = timeit(lambda: c.gemm_relu_dropout(A, W, X, p=0.5, seed=1, offset=2), a.iters)
