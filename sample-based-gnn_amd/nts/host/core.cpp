@@ -740,7 +740,22 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
                                            dW.data_ptr<float>(), (uint64_t)N),
                 "nts_hip_gemm_tn_masked_f32");
     }
-    if (ctx->needs_input_grad(0)) dx = (g * (X > 0).to(g.dtype()) * scale).matmul(W.t());
+    if (ctx->needs_input_grad(0)) {
+      // dx = (g ⊙ [X > 0] / (1-p)) W^T: the activation backward
+      // (nts_hip_act_backward) and the layer GEMM, not three torch
+      // elementwise kernels and a library GEMM
+      NtsVar dZ = torch::empty({M, N}, g.options());
+      hip_check(nts_hip_act_backward(cs->ctx(), (uint32_t)M, (uint32_t)N, g.data_ptr<float>(),
+                                     (uint64_t)N, X.data_ptr<float>(), (uint64_t)N, scale,
+                                     dZ.data_ptr<float>(), (uint64_t)N),
+                "nts_hip_act_backward");
+      NtsVar Wt = W.t().contiguous();
+      dx = torch::empty({M, K}, g.options());
+      hip_check(nts_hip_gemm_f32(cs->ctx(), 0, (int)M, (int)K, (int)N, dZ.data_ptr<float>(),
+                                 (uint64_t)N, Wt.data_ptr<float>(), (uint64_t)K,
+                                 dx.data_ptr<float>(), (uint64_t)K),
+                "nts_hip_gemm_f32(dx)");
+    }
     return {dx, dW, NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
