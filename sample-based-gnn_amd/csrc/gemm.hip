@@ -607,12 +607,16 @@ __global__ __launch_bounds__(wres_threads<NCOL>()) void k_gemm_wres(
 // Pitches make both reads conflict-free: LDY = 656 (rows of 4 lane groups
 // land on disjoint b32 banks at stride 5), LDG = 132.  Partial tiles of the
 // k-chunks are summed in a fixed order (k_sum_splits_tree).
+// RT = 1 (a 128 x 128 tile, the narrow layers' weight gradient: 100 or 128
+// output rows): LDY = 160 puts the two lane groups of a b32 read on disjoint
+// bank halves.
 constexpr int kTbWaves = 8;
-constexpr int kTbRT = 5;
-constexpr int kTbRows = kTbWaves * 16 * kTbRT;  // 640
 constexpr int kTbKS = 16;                       // k rows per step
-constexpr int kTbLDY = 656;
 constexpr int kTbLDG = 132;
+template <int RT>
+constexpr int tb_rows() { return kTbWaves * 16 * RT; }  // 640 at RT = 5
+template <int RT>
+constexpr int tb_ldy() { return RT == 5 ? 656 : RT == 1 ? 160 : tb_rows<RT>() + 16; }
 
 // NB = 3 (STAGGER): waves 4-7 run half a k-step behind waves 0-3 (they
 // finish step st-1's second half after the barrier that ends step st-1), so
@@ -620,20 +624,21 @@ constexpr int kTbLDG = 132;
 // stores (MI355X_MICROARCH.md, workgroup rule 9).  A third LDS buffer keeps
 // step st-1 readable while step st+1 is stored.  Every output element keeps
 // the same k order: results are bit-identical to NB = 2.
-template <int NB>
+template <int NB, int RT>
 struct TbSmem {
-  float y[NB][kTbKS * kTbLDY];
+  float y[NB][kTbKS * tb_ldy<RT>()];
   float g[NB][kTbKS * kTbLDG];
 };
 
-template <bool BMASK, int AVEC, bool STAGGER>
+template <bool BMASK, int AVEC, bool STAGGER, int RT = 5>
 __global__ __launch_bounds__(kTbWaves * 64, 1) void k_gemm_tn_big(
     int M, int N, int K, const float* __restrict__ A, uint64_t lda, const float* __restrict__ B,
     uint64_t ldb, float* __restrict__ C, uint64_t ldc, int kchunk, uint64_t split_stride,
     int nrg, int ncb, GemmExtra ex) {
   extern __shared__ __attribute__((aligned(16))) float smem_raw[];
   constexpr int NB = STAGGER ? 3 : 2;
-  TbSmem<NB>& sm = *reinterpret_cast<TbSmem<NB>*>(smem_raw);
+  constexpr int kTbRT = RT, kTbRows = tb_rows<RT>(), kTbLDY = tb_ldy<RT>();
+  TbSmem<NB, RT>& sm = *reinterpret_cast<TbSmem<NB, RT>*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int rg = blockIdx.x % nrg;
@@ -923,7 +928,12 @@ int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, i
 }
 
 static bool tn_big_ok(int M, int N, const float* B, uint64_t ldb, const GemmExtra& ex, bool bmask) {
-  if (M < 320 || N % 128 != 0 || ldb % 4 != 0 || (uintptr_t)B % 16 != 0) return false;
+  static const bool narrow = [] {  // RT = 1 for <= 128 output rows (A/B: NTS_TN_NARROW=0)
+    const char* e = getenv("NTS_TN_NARROW");
+    return !(e && e[0] == '0');
+  }();
+  if (!(M >= 320 || (narrow && M <= 128)) || N % 128 != 0 || ldb % 4 != 0 || (uintptr_t)B % 16 != 0)
+    return false;
   if (bmask && (ex.ldbx % 4 != 0 || (uintptr_t)ex.bx % 16 != 0)) return false;
   return true;
 }
@@ -933,7 +943,9 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
                          const float* B, uint64_t ldb, float* C, uint64_t ldc,
                          const GemmExtra& ex) {
   hipStream_t st = ctx->stream;
-  const int nrg = (M + kTbRows - 1) / kTbRows, ncb = N / 128;
+  const bool rt1 = M <= 128;
+  const int nrg = (M + (rt1 ? tb_rows<1>() : tb_rows<5>()) - 1) / (rt1 ? tb_rows<1>() : tb_rows<5>());
+  const int ncb = N / 128;
   int splits = std::max(1, std::min(256 / (nrg * ncb), (K + 4 * kTbKS - 1) / (4 * kTbKS)));
   const int kchunk = ((K + splits - 1) / splits + kTbKS - 1) / kTbKS * kTbKS;
   splits = (K + kchunk - 1) / kchunk;
@@ -942,7 +954,8 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
     const char* e = getenv("NTS_TN_STAGGER");
     return !(e && e[0] == '0');
   }();
-  const size_t lds = stagger ? sizeof(TbSmem<3>) : sizeof(TbSmem<2>);
+  const size_t lds = rt1 ? (stagger ? sizeof(TbSmem<3, 1>) : sizeof(TbSmem<2, 1>))
+                        : (stagger ? sizeof(TbSmem<3, 5>) : sizeof(TbSmem<2, 5>));
   const bool a4 = lda % 4 == 0 && lda >= (uint64_t)(M + 3) / 4 * 4 && (uintptr_t)A % 16 == 0;
   const bool a2 = M % 2 == 0 && lda % 2 == 0 && (uintptr_t)A % 8 == 0;
   const bool direct = splits == 1;
@@ -954,13 +967,18 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
     out = (float*)ctx->scratch;
     ldo = N;
   }
-#define NTS_TB_S(AV, SG)                                                                        \
+#define NTS_TB_R(AV, SG, R)                                                                     \
   do {                                                                                          \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_big<BMASK, AV, SG>), \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_tn_big<BMASK, AV, SG, R>), \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
-    hipLaunchKernelGGL((k_gemm_tn_big<BMASK, AV, SG>), grid, dim3(kTbWaves * 64), lds, st, M, N, \
+    hipLaunchKernelGGL((k_gemm_tn_big<BMASK, AV, SG, R>), grid, dim3(kTbWaves * 64), lds, st, M, N, \
                        K, A, lda, B, ldb, out, ldo, kchunk, direct ? (uint64_t)0 : stride, nrg, \
                        ncb, ex);                                                                \
+  } while (0)
+#define NTS_TB_S(AV, SG)                  \
+  do {                                    \
+    if (rt1) NTS_TB_R(AV, SG, 1);         \
+    else NTS_TB_R(AV, SG, 5);             \
   } while (0)
 #define NTS_TB(AV)                               \
   do {                                           \
@@ -970,6 +988,7 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
   if (a4) NTS_TB(4); else if (a2) NTS_TB(2); else NTS_TB(1);
 #undef NTS_TB
 #undef NTS_TB_S
+#undef NTS_TB_R
   NTS_LAUNCH_CHECK();
   if (direct) return NTS_OK;
   return sum_splits(st, out, splits, stride, M, N, C, ldc);
