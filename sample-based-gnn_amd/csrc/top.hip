@@ -33,7 +33,11 @@
 namespace nts_hip {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-constexpr int kTopWaves = 4;
+// waves (16-row tiles) per block; a build-time knob for A/B builds
+#ifndef NTS_TOP_WAVES
+#define NTS_TOP_WAVES 4
+#endif
+constexpr int kTopWaves = NTS_TOP_WAVES;
 constexpr int kTopThreads = kTopWaves * 64;
 constexpr int kTopRowsPerWave = 16;
 constexpr int kTopRows = kTopWaves * kTopRowsPerWave;  // rows per block

@@ -14,7 +14,8 @@ import pathlib
 import torch  # noqa: F401  (must be loaded first: its HIP runtime is the one we share)
 
 _HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = _HERE / "lib" / "libnts_hip.so"
+# NTS_HIP_LIB: another build of the same ABI (A/B builds of a tuning knob)
+LIB_PATH = pathlib.Path(os.environ["NTS_HIP_LIB"]) if os.environ.get("NTS_HIP_LIB") else _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
 ABI_VERSION = 7  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
