@@ -946,7 +946,14 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
   const bool rt1 = M <= 128;
   const int nrg = (M + (rt1 ? tb_rows<1>() : tb_rows<5>()) - 1) / (rt1 ? tb_rows<1>() : tb_rows<5>());
   const int ncb = N / 128;
-  int splits = std::max(1, std::min(256 / (nrg * ncb), (K + 4 * kTbKS - 1) / (4 * kTbKS)));
+  // narrow tiles hold ~55 KB of LDS and ~70 VGPRs: two blocks fit a CU, and
+  // the second doubles the gathered rows in flight (A/B: NTS_TN_NARROW_BLOCKS)
+  static const int narrow_blocks = [] {
+    const char* e = getenv("NTS_TN_NARROW_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 512;
+  }();
+  const int target = rt1 ? narrow_blocks : 256;
+  int splits = std::max(1, std::min(target / (nrg * ncb), (K + 4 * kTbKS - 1) / (4 * kTbKS)));
   const int kchunk = ((K + splits - 1) / splits + kTbKS - 1) / kTbKS * kTbKS;
   splits = (K + kchunk - 1) / kchunk;
   const dim3 grid(nrg * ncb * splits);
