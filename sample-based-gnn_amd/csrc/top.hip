@@ -67,22 +67,51 @@ __device__ __forceinline__ float grp_sum(float v) {
 }
 
 // Stage W into LDS as sW[k][Cp] (zero columns >= C): coalesced loads of the
-// contiguous [K x C] matrix, 8 in flight per thread.
+// contiguous [K x C] matrix.  K % 16 == 0 makes K x C a multiple of 4: with a
+// 16-byte aligned W the whole matrix goes as float4s, up to 16 per thread in
+// flight (one memory round trip for C3's 256 x 47; the scalar form took six
+// dependent rounds of 8 loads, most of the kernel at 16 blocks).
 template <int CP>
 __device__ __forceinline__ void stage_w(const TopArgs& a, float* sW) {
   const int C = a.C, KC = a.K * C;
-  constexpr int B = 8;
-  for (int e0 = threadIdx.x; e0 < KC; e0 += B * kTopThreads) {
-    float v[B];
+  if (((uintptr_t)a.W & 15) == 0) {
+    const float4* W4 = reinterpret_cast<const float4*>(a.W);
+    const int nq = KC / 4;
+    constexpr int B = 16;
+    for (int q0 = threadIdx.x; q0 < nq; q0 += B * kTopThreads) {
+      float4 v[B];
 #pragma unroll
-    for (int u = 0; u < B; ++u) {
-      const int e = e0 + u * kTopThreads;
-      v[u] = e < KC ? a.W[e] : 0.f;
+      for (int u = 0; u < B; ++u) {
+        const int q = q0 + u * kTopThreads;
+        v[u] = q < nq ? W4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int q = q0 + u * kTopThreads;
+        if (q < nq) {
+          const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int e = 4 * q + c;
+            sW[(e / C) * CP + e % C] = x[c];
+          }
+        }
+      }
     }
+  } else {
+    constexpr int B = 8;
+    for (int e0 = threadIdx.x; e0 < KC; e0 += B * kTopThreads) {
+      float v[B];
 #pragma unroll
-    for (int u = 0; u < B; ++u) {
-      const int e = e0 + u * kTopThreads;
-      if (e < KC) sW[(e / C) * CP + e % C] = v[u];
+      for (int u = 0; u < B; ++u) {
+        const int e = e0 + u * kTopThreads;
+        v[u] = e < KC ? a.W[e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int e = e0 + u * kTopThreads;
+        if (e < KC) sW[(e / C) * CP + e % C] = v[u];
+      }
     }
   }
   const int pad = CP - C;
@@ -95,7 +124,7 @@ __device__ __forceinline__ void stage_w(const TopArgs& a, float* sW) {
 template <bool VEC4>
 __device__ __forceinline__ void stage_y(const TopArgs& a, float* sY, int r0, int lane) {
   const int K = a.K, P = K + 4;
-  constexpr int B = 8;  // loads in flight per lane
+  constexpr int B = VEC4 ? 16 : 8;  // loads in flight per lane (K = 256: one round)
   if (VEC4) {
     const int kq = K / 4, it = K / 16;  // float4 per row; per lane (16 rows x kq / 64)
     for (int j0 = 0; j0 < it; j0 += B) {
