@@ -204,26 +204,38 @@ __global__ __launch_bounds__(256) void k_h2_split_b(const float* __restrict__ B,
 // W's column maxima and its two-piece fragment image in one launch (the
 // NN kernels' per-step weight preparation: one k-step x 128 columns per
 // block; every block takes its columns' maxima over all K rows itself, block
-// (0, cb) also stores them for the epilogue's column scales)
+// (0, cb) also stores them for the epilogue's column scales).  The fragment's
+// own 8 values are loaded first (they do not depend on the maxima) and the
+// maxima scan keeps 16 row loads in flight per thread: one memory round trip
+// at K <= 256, three at K = 602 (was one per 64 rows plus one for the
+// fragment: 19 us a call at C2, 15 us at C3's K = 100)
 __global__ __launch_bounds__(512) void k_h2_prep_w(const float* __restrict__ B, uint64_t ldb, int K,
                                                   int N, uint32_t* __restrict__ cmax,
                                                   char* __restrict__ out) {
   __shared__ float red[16][128];
   __shared__ int sexp[128];
   const int s = blockIdx.x, cb = blockIdx.y, ncb = gridDim.y, tid = threadIdx.x;
-  {  // thread: 4 columns (one float4), rows rl + 16 j, four rows in flight
+  const int lane = tid & 63, ct = tid >> 6;
+  const int cl = ct * 16 + (lane & 15), fcol = cb * 128 + cl;
+  const int k0 = 32 * s + 8 * (lane >> 4);
+  float raw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    raw[j] = (fcol < N && k0 + j < K) ? B[(uint64_t)(k0 + j) * ldb + fcol] : 0.f;
+  {  // thread: 4 columns (one float4), rows rl + 16 j, sixteen rows in flight
+    constexpr int RF = 16;
     const int q = tid & 31, rl = tid >> 5, col = cb * 128 + 4 * q;
     float m[4] = {0.f, 0.f, 0.f, 0.f};
     if (col < N) {  // N % 16 == 0: the float4 is whole
-      for (int k = rl; k < K; k += 64) {
-        float4 v[4];
+      for (int k = rl; k < K; k += 16 * RF) {
+        float4 v[RF];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < RF; ++u) {
           const int kk = min(k + 16 * u, K - 1);  // a clamped duplicate does not change a max
           v[u] = *reinterpret_cast<const float4*>(B + (uint64_t)kk * ldb + col);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < RF; ++u) {
           m[0] = fmaxf(m[0], fabsf(v[u].x));
           m[1] = fmaxf(m[1], fabsf(v[u].y));
           m[2] = fmaxf(m[2], fabsf(v[u].z));
@@ -243,14 +255,10 @@ __global__ __launch_bounds__(512) void k_h2_prep_w(const float* __restrict__ B, 
     if (s == 0 && cb * 128 + tid < N) cmax[cb * 128 + tid] = __float_as_uint(m);
   }
   __syncthreads();
-  const int lane = tid & 63, ct = tid >> 6;
-  const int cl = ct * 16 + (lane & 15), col = cb * 128 + cl;
-  const int k0 = 32 * s + 8 * (lane >> 4);
   const int e = sexp[cl];
   uint32_t w[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
-    w[j] = (col < N && k0 + j < K) ? h2_pair(ldexpf(B[(uint64_t)(k0 + j) * ldb + col], e)) : 0u;
+  for (int j = 0; j < 8; ++j) w[j] = (fcol < N && k0 + j < K) ? h2_pair(ldexpf(raw[j], e)) : 0u;
   f16x8 p0, p1;
   h2_unpack(w, p0, p1);
   char* dst = out + ((size_t)s * ncb + cb) * kH2Img + ct * 2 * kH2Frag + 16 * lane;

@@ -90,10 +90,14 @@ __device__ __forceinline__ void stage_w(const TopArgs& a, float* sW) {
         const int q = q0 + u * kTopThreads;
         if (q < nq) {
           const float x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          int r = 4 * q / C, cc = 4 * q - r * C;  // one division per float4
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const int e = 4 * q + c;
-            sW[(e / C) * CP + e % C] = x[c];
+            sW[r * CP + cc] = x[c];
+            if (++cc == C) {
+              cc = 0;
+              ++r;
+            }
           }
         }
       }
@@ -318,43 +322,79 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's dZ stores landed
     __builtin_amdgcn_wave_barrier();
-    // dY [16 x K] = dZ [16 x CP] W^T: A lane (i,g) = dZ[i][c], B = W[k = 16 kt + i][c]
-    for (int kt = 0; kt < K / 16; ++kt) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dY [16 x K] = dZ [16 x CP] W^T: A lane (i,g) = dZ[i][c], B = W[k = 16 kt + i][c].
+    // Four k tiles at a time: four independent MFMA chains share each dZ read
+    // (one chain per tile was a serial LDS-read -> MFMA latency chain, and a
+    // block of 4 waves has one wave per SIMD to hide it).  Tiles past K/16
+    // repeat the last one and are not stored; each chain's order is unchanged.
+    const int nkt = K / 16;
+    constexpr int KT = 4;
+    for (int kt0 = 0; kt0 < nkt; kt0 += KT) {
+      f32x4 acc[KT];
+      int ktu[KT];
 #pragma unroll
-      for (int c0 = 0; c0 < CP; c0 += 4)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dz[i * CP + c0 + g],
-                                                   sW[(16 * kt + i) * CP + c0 + g], acc, 0, 0, 0);
+      for (int u = 0; u < KT; ++u) {
+        acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ktu[u] = min(kt0 + u, nkt - 1);
+      }
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int r = r0 + 4 * g + v;
-        if (r < a.n) a.dY[(uint64_t)r * K + 16 * kt + i] = acc[v];
+      for (int c0 = 0; c0 < CP; c0 += 4) {
+        const float av = dz[i * CP + c0 + g];
+#pragma unroll
+        for (int u = 0; u < KT; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW[(16 * ktu[u] + i) * CP + c0 + g], acc[u],
+                                                        0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        if (kt0 + u >= nkt) break;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int r = r0 + 4 * g + v;
+          if (r < a.n) a.dY[(uint64_t)r * K + 16 * (kt0 + u) + i] = acc[u][v];
+        }
       }
     }
     // dW partial [K x CP] = Y^T [K x 16] dZ [16 x CP]:
     //   A lane (i,g) = Y[r0 + 4s + g][16 kt + i], B = dZ[4s + g][16 ct + i]
+    // two k tiles at a time (2 NCT chains sharing the dZ reads)
     const uint64_t nslab = (uint64_t)gridDim.x * kTopWaves;
     const uint64_t slab = (uint64_t)blockIdx.x * kTopWaves + w;
-    for (int kt = 0; kt < K / 16; ++kt) {
-      f32x4 acc[NCT];
+    constexpr int KW = 2;
+    for (int kt0 = 0; kt0 < nkt; kt0 += KW) {
+      f32x4 acc[KW][NCT];
+      int ktu[KW];
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int u = 0; u < KW; ++u) {
+        ktu[u] = min(kt0 + u, nkt - 1);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const float av = sY[(4 * s + g) * (K + 4) + 16 * kt + i];
+        float bv[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) bv[ct] = dz[(4 * s + g) * CP + 16 * ct + i];
+#pragma unroll
+        for (int u = 0; u < KW; ++u) {
+          const float av = sY[(4 * s + g) * (K + 4) + 16 * ktu[u] + i];
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct)
+            acc[u][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[ct], acc[u][ct], 0, 0, 0);
+        }
+      }
+      // acc[u][ct][v] = dW[16 kt + 4 g + v][16 ct + i] -> chunk (k, ct), lane i
+#pragma unroll
+      for (int u = 0; u < KW; ++u) {
+        if (kt0 + u >= nkt) break;
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct)
-          acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, dz[(4 * s + g) * CP + 16 * ct + i],
-                                                         acc[ct], 0, 0, 0);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const uint64_t q = (uint64_t)(16 * (kt0 + u) + 4 * g + v) * NCT + ct;
+            a.part[(q * nslab + slab) * 16 + i] = acc[u][ct][v];
+          }
       }
-      // acc[ct][v] = dW[16 kt + 4 g + v][16 ct + i] -> chunk (k, ct), lane i
-#pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const uint64_t q = (uint64_t)(16 * kt + 4 * g + v) * NCT + ct;
-          a.part[(q * nslab + slab) * 16 + i] = acc[ct][v];
-        }
     }
   }
   if (LOSS) {
@@ -368,6 +408,251 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
       }
       a.lpart[blockIdx.x] = s;
       if (a.cpart) a.cpart[blockIdx.x] = c;
+    }
+  }
+}
+
+// K-split form (the default): one block of kTopWaves waves per 16-row tile,
+// wave w taking the k tiles kt = w, w + kTopWaves, ... of every product.
+// The per-wave form above runs a whole tile's three products on one wave —
+// ~600 dependent v_mfma_f32_16x16x4_f32 at K = 256 with one wave per SIMD,
+// 35 us however few rows (C3: 1,024 rows, 64 waves on 256 CUs).  Here the
+// logits are four partial chains summed in a fixed order (w = 0..3) through
+// LDS; every wave then holds the same Z and log-softmax, wave 0 writes dZ
+// and the loss; dY and dW run on each wave's k tiles (two at a time).  One dW
+// slab per block.  Deterministic; the logits' summation order differs from
+// the per-wave form (NTS_TOP_KSPLIT=0) by rounding only.
+static inline size_t top_ks_lds(int K, int Cp) {
+  return ((size_t)K * Cp + (size_t)16 * (K + 4) + (size_t)(kTopWaves + 1) * 16 * Cp) * sizeof(float);
+}
+
+template <int NCT, bool LOSS, bool GRAD, bool VEC4>
+__global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
+  constexpr int CP = 16 * NCT, NW = kTopWaves;
+  extern __shared__ float smem[];
+  __shared__ float wl;
+  __shared__ uint32_t wc;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int K = a.K, P = K + 4, nkt = K / 16;
+  float* sW = smem;                // [K][CP]
+  float* sY = sW + K * CP;         // [16][K + 4]
+  float* zp = sY + 16 * P;         // [NW][16][CP] partial logits
+  float* dz = zp + NW * 16 * CP;   // [16][CP]
+  const int r0 = blockIdx.x * 16;
+  {  // the tile's 16 rows, all threads (rows >= n are zero)
+    constexpr int B = 8;
+    if (VEC4) {
+      const int kq = K / 4, tot = 16 * kq;
+      for (int q0 = threadIdx.x; q0 < tot; q0 += B * kTopThreads) {
+        float4 v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const int q = q0 + u * kTopThreads, rr = q / kq, r = r0 + rr;
+          v[u] = (q < tot && r < a.n) ? *reinterpret_cast<const float4*>(a.Y + (uint64_t)r * a.ldy + 4 * (q % kq))
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const int q = q0 + u * kTopThreads;
+          if (q < tot) *reinterpret_cast<float4*>(sY + (q / kq) * P + 4 * (q % kq)) = v[u];
+        }
+      }
+    } else {
+      const int tot = 16 * K;
+      for (int q0 = threadIdx.x; q0 < tot; q0 += B * kTopThreads) {
+        float v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const int q = q0 + u * kTopThreads, r = r0 + q / K;
+          v[u] = (q < tot && r < a.n) ? a.Y[(uint64_t)r * a.ldy + q % K] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const int q = q0 + u * kTopThreads;
+          if (q < tot) sY[(q / K) * P + q % K] = v[u];
+        }
+      }
+    }
+  }
+  stage_w<CP>(a, sW);
+  __syncthreads();
+  f32x4 z[NCT];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct) z[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    const float* yr = sY + i * P;
+    for (int kt = w; kt < nkt; kt += NW) {
+#pragma unroll
+      for (int k0 = 16 * kt; k0 < 16 * kt + 16; k0 += 4) {
+        const float av = yr[k0 + g];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          z[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW[(k0 + g) * CP + 16 * ct + i], z[ct], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) zp[(w * 16 + 4 * g + v) * CP + 16 * ct + i] = z[ct][v];
+  __syncthreads();
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      float t = zp[(4 * g + v) * CP + 16 * ct + i];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) t += zp[(q * 16 + 4 * g + v) * CP + 16 * ct + i];
+      z[ct][v] = t;
+    }
+  float lp[NCT][4], lp2[NCT][4];
+  log_softmax2<NCT>(z, a.C, i, lp, lp2);
+  int tgt[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int r = r0 + 4 * g + v;
+    tgt[v] = r < a.n ? (int)a.labels[r] : -1;
+  }
+  if (LOSS && w == 0) {
+    float l = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (16 * ct + i == tgt[v]) l -= lp2[ct][v];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, kWave);
+    if (lane == 0) wl = l;
+    if (a.cpart) {  // getCorrect (toolkits/GCN_SAMPLE_ALLGPU.hpp:166-172), as k_top_xent
+      uint32_t ok = 0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+          if (16 * ct + i < a.C && lp[ct][v] > best) {
+            best = lp[ct][v];
+            bi = 16 * ct + i;
+          }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          const float ob = __shfl_xor(best, o, kWave);
+          const int oi = __shfl_xor(bi, o, kWave);
+          if (ob > best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+          }
+        }
+        ok += (i == 0 && tgt[v] >= 0 && bi == tgt[v]) ? 1u : 0u;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) ok += __shfl_down(ok, o, kWave);
+      if (lane == 0) wc = ok;
+    }
+  }
+  if (GRAD) {
+    if (w == 0) {
+      const float gl = (a.grad ? *a.grad : 1.0f) / (float)a.n;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int r = r0 + 4 * g + v;
+        float d2[NCT], s2 = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          d2[ct] = (16 * ct + i == tgt[v]) ? -gl : 0.f;
+          s2 += d2[ct];
+        }
+        s2 = grp_sum(s2);
+        float d1[NCT], s1 = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const bool on = 16 * ct + i < a.C;
+          d1[ct] = on ? d2[ct] - expf(lp2[ct][v]) * s2 : 0.f;
+          s1 += d1[ct];
+        }
+        s1 = grp_sum(s1);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const bool on = 16 * ct + i < a.C && r < a.n;
+          dz[(4 * g + v) * CP + 16 * ct + i] = on ? d1[ct] - expf(lp[ct][v]) * s1 : 0.f;
+        }
+      }
+    }
+    __syncthreads();
+    // dY [16 x K] = dZ W^T on this wave's k tiles, two at a time
+    constexpr int KT = 2;
+    for (int j0 = w; j0 < nkt; j0 += KT * NW) {
+      f32x4 acc[KT];
+      int ktu[KT];
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ktu[u] = min(j0 + u * NW, nkt - 1);
+      }
+#pragma unroll
+      for (int c0 = 0; c0 < CP; c0 += 4) {
+        const float av = dz[i * CP + c0 + g];
+#pragma unroll
+        for (int u = 0; u < KT; ++u)
+          acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, sW[(16 * ktu[u] + i) * CP + c0 + g], acc[u],
+                                                        0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        const int kt = j0 + u * NW;
+        if (kt >= nkt) break;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int r = r0 + 4 * g + v;
+          if (r < a.n) a.dY[(uint64_t)r * K + 16 * kt + i] = acc[u][v];
+        }
+      }
+    }
+    // dW slab of this block [K x CP] = Y^T dZ, rows of this wave's k tiles
+    const uint64_t nslab = gridDim.x, slab = blockIdx.x;
+    for (int j0 = w; j0 < nkt; j0 += KT * NW) {
+      f32x4 acc[KT][NCT];
+      int ktu[KT];
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        ktu[u] = min(j0 + u * NW, nkt - 1);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[u][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        float bv[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) bv[ct] = dz[(4 * s4 + g) * CP + 16 * ct + i];
+#pragma unroll
+        for (int u = 0; u < KT; ++u) {
+          const float av = sY[(4 * s4 + g) * P + 16 * ktu[u] + i];
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct)
+            acc[u][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[ct], acc[u][ct], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < KT; ++u) {
+        const int kt = j0 + u * NW;
+        if (kt >= nkt) break;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const uint64_t q = (uint64_t)(16 * kt + 4 * g + v) * NCT + ct;
+            a.part[(q * nslab + slab) * 16 + i] = acc[u][ct][v];
+          }
+      }
+    }
+  }
+  if (LOSS) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      a.lpart[blockIdx.x] = wl;
+      if (a.cpart) a.cpart[blockIdx.x] = wc;
     }
   }
 }
@@ -433,8 +718,34 @@ __global__ __launch_bounds__(256) void k_top_finish(const float* __restrict__ pa
   (void)K;
 }
 
+static bool top_ksplit() {  // A/B: NTS_TOP_KSPLIT=0 runs the per-wave form
+  static const bool on = [] {
+    const char* e = getenv("NTS_TOP_KSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int NCT, bool LOSS, bool GRAD>
+static int launch_top_ks(hipStream_t st, int nblk, const TopArgs& a) {
+  const size_t lds = top_ks_lds(a.K, 16 * NCT);
+  const bool v4 = a.ldy % 4 == 0 && (uintptr_t)a.Y % 16 == 0;
+  const void* f = v4 ? reinterpret_cast<const void*>(&k_top_xent_ks<NCT, LOSS, GRAD, true>)
+                     : reinterpret_cast<const void*>(&k_top_xent_ks<NCT, LOSS, GRAD, false>);
+  NTS_HIP_TRY(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (v4)
+    hipLaunchKernelGGL((k_top_xent_ks<NCT, LOSS, GRAD, true>), dim3(nblk), dim3(kTopThreads), lds,
+                       st, a);
+  else
+    hipLaunchKernelGGL((k_top_xent_ks<NCT, LOSS, GRAD, false>), dim3(nblk), dim3(kTopThreads), lds,
+                       st, a);
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
 template <int NCT, bool LOSS, bool GRAD>
 static int launch_top(hipStream_t st, int nblk, const TopArgs& a) {
+  if (top_ksplit()) return launch_top_ks<NCT, LOSS, GRAD>(st, nblk, a);
   const size_t lds = top_lds(a.K, 16 * NCT);
   const bool v4 = a.ldy % 4 == 0 && (uintptr_t)a.Y % 16 == 0;
   const void* f = v4 ? reinterpret_cast<const void*>(&k_top_xent<NCT, LOSS, GRAD, true>)
@@ -500,8 +811,9 @@ static int top_run(nts_hip_ctx* ctx, bool loss_on, bool grad_on, const float* Y,
                    const float* grad_loss, float* loss, float* dY, float* dW, uint32_t* correct) {
   NTS_RET(top_check(ctx, n, K, C, ldy));
   const int Cp = (C + 15) / 16 * 16;
-  const int nblk = (n + kTopRows - 1) / kTopRows;
-  const int nslab = nblk * kTopWaves;
+  const bool ks = top_ksplit();
+  const int nblk = ks ? (n + 15) / 16 : (n + kTopRows - 1) / kTopRows;
+  const int nslab = ks ? nblk : nblk * kTopWaves;
   const size_t lp = ((size_t)nblk + 63) / 64 * 64;
   NTS_RET(ensure_scratch(
       ctx, (2 * lp + (grad_on ? (size_t)nslab * K * Cp : 0)) * sizeof(float)));
