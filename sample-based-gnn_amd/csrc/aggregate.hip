@@ -516,20 +516,10 @@ static int pick_vec(uint32_t F, uint64_t ld1, uint64_t ld2, const void* p1, cons
 struct Shape {
   int lpd, nch;
 };
-// NTS_AGG_HALF=1 (A/B): rows of 17..32 vectors on 16-lane groups with two
-// vectors per lane — twice the rows in flight per wave (same per-row order)
-static bool agg_half() {
-  static const bool on = [] {
-    const char* e = getenv("NTS_AGG_HALF");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 static Shape pick_shape(uint32_t nv) {
   if (nv <= 8) return {8, 1};
   if (nv <= 16) return {16, 1};
-  if (nv <= 32) return agg_half() && nv > 16 ? Shape{16, 2} : Shape{32, 1};
+  if (nv <= 32) return {32, 1};
   if (nv <= 64) return {64, 1};
   uint32_t nch = (nv + 63) / 64;
   return {64, (int)std::min<uint32_t>(nch, 8)};
@@ -580,7 +570,6 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
                          nv, y, ldy, last_valid, tier, ax);                                 \
   } while (0)
   if (s.lpd == 8) NTS_G(8, 1);
-  else if (s.lpd == 16 && s.nch == 2) NTS_G(16, 2);
   else if (s.lpd == 16) NTS_G(16, 1);
   else if (s.lpd == 32) NTS_G(32, 1);
   else switch (s.nch) {
