@@ -13,8 +13,13 @@ backward (CSR transpose aggregations, gathered weight-gradient GEMM) ->
 value = sampled edges of all ranks in the K timed steps / max-over-ranks wall
 time.  Inputs are resident in HBM before the timed region.
 
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
-(one process per GPU, seeds sharded, one fused RCCL SUM all-reduce per step).
+Multi-GPU: `python bench.py --gpus N` starts `python -m torch.distributed.run
+--nproc-per-node N bench.py --gpus N ...` as a child process (before anything
+touches the GPU), relays rank 0's JSON line and exits with the child's status;
+launched that way or by the driver's own torch.distributed.run, every rank
+checks WORLD_SIZE == --gpus, and the line carries `rccl_ranks` as RCCL reports
+it (ncclCommCount).  One process per GPU, seeds sharded, one fused RCCL SUM
+all-reduce per step (toolkits/GCN_SAMPLE_ALL_MULTI.hpp:89-113,367-377).
 """
 from __future__ import annotations
 
@@ -23,6 +28,7 @@ import hashlib
 import json
 import os
 import pathlib
+import subprocess
 import sys
 import time
 
@@ -83,6 +89,83 @@ def default_cpu_threads() -> int:
         if cap:
             n = min(n, max(1, int(cap)))
     return max(1, n)
+
+
+def nts_env() -> dict:
+    """Every NTS_* variable of this run (recorded in profile_meta)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("NTS_")}
+
+
+def diag_env() -> list:
+    """NTS_*DIAG* variables: diagnostics that skip work or give wrong results;
+    a bench line measured under one is invalid, so bench.py refuses to run."""
+    return sorted(k for k in os.environ if k.startswith("NTS_") and "DIAG" in k)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv: list, n: int) -> int:
+    """`bench.py --gpus N` without a launcher: run `torch.distributed.run
+    --nproc-per-node N bench.py ...` as a CHILD process (this process has not
+    touched the GPU and never execs), relay rank 0's JSON line, and return the
+    child's exit status — non-zero also when no line came back or its n_gpus
+    is not N."""
+    shared = os.environ.get("NTS_BENCH_SHARE_GPU") == "1"
+    if not shared and "--launch-selftest" not in argv:
+        have = torch.cuda.device_count()  # counts devices without initialising HIP
+        if have < n:
+            print(f"[bench] --gpus {n} but this node has {have} GPU(s)", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           str(ROOT / "bench.py"), *argv]
+    env = dict(os.environ, PYTHONUNBUFFERED="1", MASTER_ADDR="127.0.0.1")
+    log(f"[bench] launching {n} ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for out in p.stdout:
+        try:
+            obj = json.loads(out)
+        except ValueError:
+            obj = None
+        if isinstance(obj, dict) and "metric" in obj:
+            line = obj
+        else:
+            sys.stderr.write(out)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc != 0:
+        print(f"[bench] the {n}-rank run exited with {rc}", file=sys.stderr)
+        return rc
+    if line is None or line.get("n_gpus") != n:
+        print(f"[bench] the {n}-rank run reported no line for {n} ranks: {line}", file=sys.stderr)
+        return 1
+    line.setdefault("config", {})["launcher"] = (
+        f"bench.py --gpus {n} -> child `python -m torch.distributed.run --nproc-per-node {n}`")
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def launch_selftest(world: int, rank: int) -> None:
+    """--launch-selftest: the launcher's control flow without a GPU — every
+    rank joins a gloo group and rank 0 prints a line with the ranks that
+    answered (tests/test_bench.py)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank)
+        dist.destroy_process_group()
+    else:
+        ranks = [0]
+    if rank == 0:
+        print(json.dumps({"metric": "launch-selftest", "value": 0.0, "n_gpus": world,
+                          "ranks": ranks}), flush=True)
 
 
 def parse():
@@ -160,6 +243,10 @@ def parse():
                    help="sampler stream: philox (per-dst counter streams, parallel) or mt: the "
                         "reference's single std::mt19937(2000) stream + uniform_int_distribution "
                         "(Lemire, libstdc++ 11; mt-div: libstdc++ <= 10), replayed bit-exactly")
+    p.add_argument("--no-interference-probe", action="store_true",
+                   help="skip the diagnostic training-stream-alone timing (one sampled batch "
+                        "reused, no sampler beside the training stream)")
+    p.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -180,9 +267,20 @@ def lib_sha256() -> str:
 
 def main():
     args = parse()
+    bad = diag_env()
+    if bad:
+        raise SystemExit(f"[bench] refusing to measure with diagnostic knobs set: {bad} "
+                         f"(they skip work or give wrong results)")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU "
+                         f"is required")
+    if args.launch_selftest:
+        return launch_selftest(world, rank)
     # NTS_BENCH_SHARE_GPU=1: every rank on device 0 — a rehearsal of the
     # multi-rank control flow on a one-GPU box (RCCL refuses two ranks on one
     # device, so the ranks talk over gloo: the timing collectives and the
@@ -231,6 +329,12 @@ def main():
         comm = ndist.make_host_communicator(E, world, rank) if world > 1 else None
     else:
         comm = ndist.make_communicator(E, world, rank, local_rank)
+    rccl_ranks = None  # ranks of the RCCL communicator as RCCL reports them
+    if comm is not None and not comm.host_transport:
+        rccl_ranks, my = comm.rccl_count()
+        if rccl_ranks != world or my != rank:
+            raise SystemExit(f"[bench] RCCL communicator has {rccl_ranks} ranks (this one {my}), "
+                             f"expected {world} (this one {rank})")
 
     fan = [int(x) for x in args.fanout.split("-")]
     layers = ([int(x) for x in args.layers.split("-")] if args.layers else [F_dim, args.hidden, C])
@@ -326,6 +430,27 @@ def main():
     else:
         epoch_s, epoch_kind = elapsed / args.steps * batches_per_epoch, "ms_per_step x batches/epoch"
 
+    # ---- diagnostic: the training stream without the sampler beside it -----------
+    alone = None
+    if (args.model == "gcn" and not args.no_interference_probe and args.steps > 0
+            and not args.no_pipeline):
+        drv.set_diag_reuse_sample(True)
+        for _ in range(args.warmup):
+            step()
+        drv.synchronize()
+        barrier()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        drv.synchronize()
+        barrier()
+        el_alone = max_over_ranks(time.perf_counter() - ta)
+        drv.set_diag_reuse_sample(False)
+        alone = {"ms_per_step": el_alone / args.steps * 1e3, "steps": args.steps,
+                 "interference_ms_per_step": (elapsed - el_alone) / args.steps * 1e3,
+                 "note": "diagnostic, not a throughput: one sampled batch reused every step, "
+                         "so the training stream runs without the pipelined sampler beside it"}
+
     # ---- GPU sampler alone (SURVEY §8d sampler-only rate) -------------------------
     sampler_only = None
     if args.sampler_batches > 0 and args.model == "gcn":
@@ -379,6 +504,7 @@ def main():
         "value": value,
         "unit": "sampled-edges/s",
         "n_gpus": world,
+        "rccl_ranks": rccl_ranks,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -393,6 +519,10 @@ def main():
             "workload": workload_name(args, layers, V, En, tf),
             "global_batch": args.batch * world,
             "parallelism": f"dp{world}" + ("-shared-gpu-rehearsal (gloo all-reduce through host copies)" if shared and world > 1 else ""),
+            "gradient_exchange": ("none (one rank)" if comm is None else
+                                  "gloo host transport" if comm.host_transport else
+                                  f"RCCL all-reduce, {rccl_ranks} ranks"),
+            "training_stream_alone": alone,
             "fanout": args.fanout,
             "epoch_time_s": epoch_s,
             "epoch_time_kind": epoch_kind,
@@ -411,6 +541,7 @@ def main():
             "layer_sizes_top_down": layer_sizes,
             "reference_order_secondary": secondary,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
+                             "nts_env": nts_env(),
                              "workload": pmc_workload(args, layers, world)},
         },
         "roofline": rl,

@@ -34,14 +34,15 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 7  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 8  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
                                      accuracy counts in the fused loss;
                                   4: PD cache entry points + omit fields, GEMM mode;
                                   5: two-piece f16 pair-table GEMMs (nts_hip_h2_*);
                                   6: nts_hip_spmm_csr_bwd_colmax + nts_hip_gemm_h2p_tn_gather_cm;
                                   7: the column maxima per part of rows (no row scales in
-                                     the backward), nts_hip_csr_bwd_colmax_rows_per_part */
+                                     the backward), nts_hip_csr_bwd_colmax_rows_per_part;
+                                  8: nts_hip_comm_count */
 
 /* status codes */
 #define NTS_OK 0
@@ -581,6 +582,11 @@ int nts_hip_comm_unique_id(uint8_t out_id[128]);
 int nts_hip_comm_init(nts_hip_comm **comm, int nranks, int rank, const uint8_t id[128],
                       int device);
 int nts_hip_comm_destroy(nts_hip_comm *comm);
+/* Ranks in the communicator as RCCL itself reports them (ncclCommCount) and
+ * this process's rank (ncclCommUserRank): the check that an N-process launch
+ * really built one N-rank clique (the reference's ncclCommInitAll over
+ * `device_num` GPUs, toolkits/GCN_SAMPLE_ALL_MULTI.hpp:89-113). */
+int nts_hip_comm_count(nts_hip_comm *comm, int *nranks, int *rank);
 /* In-place float SUM all-reduce (NCCL_Communicator::AllReduce, cuda/ntsCUDAGraphOP.cu:180-186). */
 int nts_hip_allreduce_sum_f32(nts_hip_comm *comm, float *buf, uint64_t count, void *stream);
 /* In-place broadcast from root (NCCL_Communicator::Bcast, cuda/ntsCUDAGraphOP.cu:188-193). */

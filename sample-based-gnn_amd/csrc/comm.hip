@@ -62,6 +62,13 @@ int nts_hip_comm_destroy(nts_hip_comm* c) {
   return NTS_OK;
 }
 
+int nts_hip_comm_count(nts_hip_comm* c, int* nranks, int* rank) {
+  NTS_CHECK_ARG(c && c->comm && nranks && rank, "NULL argument");
+  NTS_RCCL_TRY(ncclCommCount(c->comm, nranks));
+  NTS_RCCL_TRY(ncclCommUserRank(c->comm, rank));
+  return NTS_OK;
+}
+
 int nts_hip_allreduce_sum_f32(nts_hip_comm* c, float* buf, uint64_t count, void* stream) {
   NTS_CHECK_ARG(c && c->comm && (buf || count == 0), "NULL argument");
   NTS_RCCL_TRY(ncclAllReduce(buf, buf, (size_t)count, ncclFloat, ncclSum, c->comm,

@@ -85,8 +85,12 @@ struct Gemm3Extra {
   uint64_t ldbx = 0;
   float bscale = 1.f;
   const uint32_t* amap = nullptr;  // gathered A rows (NN: M rows, TN: K rows)
+#ifdef NTS_PROBE_BUILD
   int diag = 0;  // NTS_S3_DIAG timing probes (results invalid): 1 no global loads,
                  // 2 no split, 4 no barrier, 8 no MFMA, 16 no B fragment reads
+#else
+  static constexpr int diag = 0;  // the product library has no timing probes
+#endif
 };
 
 // ---------------------------------------------------------------------------
@@ -728,11 +732,13 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
   ex.seed = seed;
   ex.offset = offset;
   ex.amap = amap;
+#ifdef NTS_PROBE_BUILD
   static const int diag = [] {
     const char* e = getenv("NTS_S3_DIAG");
     return e ? atoi(e) : 0;
   }();
   ex.diag = diag;
+#endif
   const int ncb = (N + 127) / 128;
   const int nsteps = (K + 31) / 32;
   // the weight's fragment image (scratch: the NN call uses no other scratch)
@@ -773,11 +779,13 @@ int gemm3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda
              const uint32_t* amap, const float* B, uint64_t ldb, const float* X, uint64_t ldx,
              float bscale, float* C, uint64_t ldc) {
   Gemm3Extra ex;
+#ifdef NTS_PROBE_BUILD
   static const int diag = [] {
     const char* e = getenv("NTS_S3_DIAG");
     return e ? atoi(e) : 0;
   }();
   ex.diag = diag;
+#endif
   ex.amap = amap;
   ex.bx = X;
   ex.ldbx = ldx;

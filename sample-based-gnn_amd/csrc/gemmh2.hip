@@ -1740,10 +1740,12 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
   ex.cparts = part_max;
   ex.rpp = rows_per_part;
   ex.nparts_ld = (uint64_t)N;
+#ifdef NTS_PROBE_BUILD  // timing probes (scripts/probe): results are garbage
   static const int diag = [] {
     const char* e = getenv("NTS_TN4_DIAG");
     return e ? atoi(e) : 0;
   }();
+#endif
   static const bool rp = [] {  // row-aligned DMA pieces (A/B: NTS_TN4_RP=0)
     const char* e = getenv("NTS_TN4_RP");
     return !(e && e[0] == '0');
@@ -1757,10 +1759,13 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
                        pitch, 2 * Kp, B, ldb, out, ldo, kchunk,                                    \
                        splits > 1 ? stride : (uint64_t)0, nnb, ex);                                \
   } while (0)
+#ifdef NTS_PROBE_BUILD
   if (diag == 1) NTS_TN4(1);
   else if (diag == 2) NTS_TN4(2);
   else if (diag == 4) NTS_TN4(4);
-  else if (rp && pitch == 2560) NTS_TN4(0, true);
+  else
+#endif
+  if (rp && pitch == 2560) NTS_TN4(0, true);
   else NTS_TN4(0);
 #undef NTS_TN4
   NTS_LAUNCH_CHECK();
@@ -1836,10 +1841,14 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
                        reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), pitch, 2 * Kp, bimg, C, \
                        ldc, ex);                                                                  \
   } while (0)
+#ifdef NTS_PROBE_BUILD  // timing probes (scripts/probe): results are garbage
   static const int diag = [] {
     const char* e = getenv("NTS_NN3_DIAG");
     return e ? atoi(e) : 0;
   }();
+#else
+  constexpr int diag = 0;
+#endif
   // row-aligned LDS-DMA pieces (A/B: NTS_NN3_RP=0 keeps the row-straddling ones)
   static const bool rp = [] {
     const char* e = getenv("NTS_NN3_RP");
@@ -1856,10 +1865,12 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   // (C2: 602 -> Kp 608); NTS_NN3_DIAG=4 forces the runtime-count loop
   if (relu_dropout) {
     if (a_rows) NTS_H2NN3(true, true); else NTS_H2NN3(true, false);
+#ifdef NTS_PROBE_BUILD
   } else if (a_rows && diag == 1) {
     NTS_H2NN3(false, true, 19, 1);
   } else if (a_rows && diag == 2) {
     NTS_H2NN3(false, true, 19, 2);
+#endif
   } else if (a_rows && nsteps == 19 && diag != 4 && pitch == 2560 && rp && tr_ok) {
     NTS_H2NN3(false, true, 19, 0, true, true);
   } else if (a_rows && nsteps == 19 && diag != 4 && pitch == 2560 && rp) {

@@ -18,7 +18,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ["NTS_HIP_LIB"]) if os.environ.get("NTS_HIP_LIB") else _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 7  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 8  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
@@ -44,6 +44,7 @@ EXPORTED = (
     "nts_hip_relu_dropout_f32",
     "nts_hip_gemm_f32", "nts_hip_gemm_relu_dropout_f32", "nts_hip_gemm_tn_masked_f32",
     "nts_hip_linear_xent_fwd", "nts_hip_linear_xent_bwd", "nts_hip_linear_xent_train", "nts_hip_adam", "nts_hip_comm_unique_id", "nts_hip_comm_init", "nts_hip_comm_destroy",
+    "nts_hip_comm_count",
     "nts_hip_allreduce_sum_f32", "nts_hip_broadcast_f32",
     "nts_hip_cache_select", "nts_hip_host_alloc", "nts_hip_host_free",
     "nts_hip_host_device_pointer", "nts_hip_gather_rows_cached", "nts_hip_spmm_csc_fwd_cached",
@@ -145,6 +146,7 @@ def lib() -> C.CDLL:
         "nts_hip_comm_unique_id": ([P], I),
         "nts_hip_comm_init": ([C.POINTER(P), I, I, P, I], I),
         "nts_hip_comm_destroy": ([P], I),
+        "nts_hip_comm_count": ([P, C.POINTER(I), C.POINTER(I)], I),
         "nts_hip_allreduce_sum_f32": ([P, P, U64, P], I),
         "nts_hip_broadcast_f32": ([P, P, U64, I, P], I),
         "nts_hip_cache_select": ([P, P, U64, U64, P, P], I),

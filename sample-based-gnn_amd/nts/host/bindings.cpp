@@ -148,6 +148,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           },
           py::arg("nranks"), py::arg("rank"), py::arg("collective"))
       .def_property_readonly("host_transport", &Communicator::host_transport)
+      .def("rccl_count", &Communicator::rccl_count)
       .def_static("unique_id",
                   []() {
                     auto v = Communicator::unique_id();
@@ -231,6 +232,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("nids"))
       .def("weights", &GCN_SAMPLE_ALLGPU_impl::weights)
       .def("reset_stats", &GCN_SAMPLE_ALLGPU_impl::reset_stats)
+      .def("set_diag_reuse_sample", &GCN_SAMPLE_ALLGPU_impl::set_diag_reuse_sample)
       .def("resolve_profile",
            [](GCN_SAMPLE_ALLGPU_impl& d) {
              // {kernel: {"ms": total device ms, "calls": n, "units": algorithmic

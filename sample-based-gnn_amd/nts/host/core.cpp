@@ -1287,6 +1287,12 @@ void Communicator::broadcast(float* buf, uint64_t n, int root, void* stream) {
   if (host_) return host_call(buf, n, stream, 1, root);
   hip_check(nts_hip_broadcast_f32(comm_, buf, n, root, stream), "nts_hip_broadcast_f32");
 }
+std::pair<int, int> Communicator::rccl_count() const {
+  if (host_) return {-1, -1};
+  int n = 0, r = 0;
+  hip_check(nts_hip_comm_count(comm_, &n, &r), "nts_hip_comm_count");
+  return {n, r};
+}
 std::vector<uint8_t> Communicator::unique_id() {
   std::vector<uint8_t> id(128);
   hip_check(nts_hip_comm_unique_id(id.data()), "nts_hip_comm_unique_id");

@@ -544,10 +544,10 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   auto guard = cs->guard();
   double t0 = now_s();
   NtsStream& sst = ss ? *ss : *cs;
-  // NTS_DIAG_REUSE_SAMPLE=1 (diagnostic only, not a valid measurement): sample
+  // set_diag_reuse_sample (diagnostic only, not a valid measurement): sample
   // once and train every step on that batch — the training stream's time
   // without the sampler beside it
-  static const bool diag_reuse = getenv("NTS_DIAG_REUSE_SAMPLE") != nullptr;
+  const bool diag_reuse = diag_reuse_;
   int slot;
   SampledSubgraph* sg;
   if (diag_reuse && reuse_slot_ >= 0) {

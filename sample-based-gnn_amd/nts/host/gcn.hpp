@@ -90,6 +90,13 @@ class GCN_SAMPLE_ALLGPU_impl {
   void init_nn();
   float train_batch();
   float run_epoch();
+  // Diagnostic (bench.py's training-stream-alone probe, never the headline):
+  // on = sample one batch and train every later step on it, so the training
+  // stream runs without the sampler beside it; off = back to sampling.
+  void set_diag_reuse_sample(bool on) {
+    diag_reuse_ = on;
+    reuse_slot_ = -1;
+  }
   bool has_batch() const {
     return prefetched_ >= 0 || (!pass_done_ && sampler->sample_not_finished());
   }
@@ -195,7 +202,8 @@ class GCN_SAMPLE_ALLGPU_impl {
   uint64_t dropout_calls_ = 0;  // Philox offset of the fused dropout masks
   int prefetched_ = -1;  // slot holding an issued, not yet trained batch
   int next_slot_ = 0;
-  int reuse_slot_ = -1;  // NTS_DIAG_REUSE_SAMPLE
+  bool diag_reuse_ = false;
+  int reuse_slot_ = -1;  // set_diag_reuse_sample
   // pass boundary: the next pass's first batch is issued behind the current
   // pass's last one (carry_), handed over by restart()
   int carry_ = -1;

@@ -484,6 +484,9 @@ class Communicator {
   void broadcast(float* buf, uint64_t n, int root, void* stream);
   static std::vector<uint8_t> unique_id();
   bool host_transport() const { return (bool)host_; }
+  // (ranks, this rank) as RCCL reports them (ncclCommCount / ncclCommUserRank);
+  // (-1, -1) for the host transport
+  std::pair<int, int> rccl_count() const;
   int nranks, rank;
 
  private:

@@ -85,3 +85,45 @@ def test_metric_and_workload_labels(bench):
         _args(shape="products", weight="mean"), [100, 256, 256, 47])
     w = bench.workload_name(_args(), [602, 128, 41], 232965, 114848857, False)
     assert "split-bf16" in w and "fused gather/aggregation" in w
+
+
+def _run_bench(args, **env_extra):
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")
+           and not k.startswith("NTS_")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True,
+                          text=True, env=env, timeout=300)
+
+
+def test_gpus_n_launches_n_ranks_itself():
+    """bench.py --gpus 2 with no launcher starts torch.distributed.run as a
+    child, every rank joins, and the parent relays rank 0's line."""
+    r = _run_bench(["--gpus", "2", "--launch-selftest"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    obj = json.loads(lines[0])
+    assert obj["n_gpus"] == 2 and sorted(obj["ranks"]) == [0, 1]
+    assert "torch.distributed.run" in obj["config"]["launcher"]
+
+
+def test_world_size_must_match_gpus():
+    r = _run_bench(["--gpus", "1", "--launch-selftest"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert r.returncode != 0 and "WORLD_SIZE=2 but --gpus 1" in r.stderr
+
+
+def test_diagnostic_knobs_are_refused():
+    r = _run_bench(["--launch-selftest"], NTS_NN3_DIAG="1")
+    assert r.returncode != 0 and "NTS_NN3_DIAG" in r.stderr
+    r = _run_bench(["--launch-selftest"], NTS_DIAG_REUSE_SAMPLE="1")
+    assert r.returncode != 0 and "NTS_DIAG_REUSE_SAMPLE" in r.stderr
+
+
+def test_nts_env_is_recorded(bench, monkeypatch):
+    monkeypatch.setenv("NTS_SCAN1", "0")
+    assert bench.nts_env()["NTS_SCAN1"] == "0"
+    assert bench.diag_env() == []
