@@ -42,7 +42,8 @@ extern "C" {
                                   6: nts_hip_spmm_csr_bwd_colmax + nts_hip_gemm_h2p_tn_gather_cm;
                                   7: the column maxima per part of rows (no row scales in
                                      the backward), nts_hip_csr_bwd_colmax_rows_per_part;
-                                  8: nts_hip_comm_count */
+                                  8: nts_hip_comm_count; the CSR-backward column maxima scaled by
+                                     the pair table's row scales (exact TN operand maxima) */
 
 /* status codes */
 #define NTS_OK 0
@@ -296,17 +297,20 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx *ctx, const uint32_t *row_offset,
                          uint64_t ld_gin);
 /* nts_hip_spmm_csr_bwd that also leaves its output's column maxima per part
  * of R = nts_hip_csr_bwd_colmax_rows_per_part(feature_size) rows:
- * part_max[p * feature_size + c] = the float bits of max |G_in[s, c]| over
- * s in [p R, (p+1) R) (0 past the live rows; exact — an unordered max),
- * ceil(s_cap / R) parts.  The operand scales of nts_hip_gemm_h2p_tn_gather_cm
- * when G_in is its B, so that GEMM reads G_in once.  feature_size <= 512,
- * G rows 16-byte aligned with ld % 4 == 0. */
+ * part_max[p * feature_size + c] = the float bits of max |rs(s) G_in[s, c]|
+ * over s in [p R, (p+1) R) (0 past the live rows; exact — an unordered max),
+ * ceil(s_cap / R) parts, with the row scale rs(s) = row_scale[row_map[s]]
+ * (row_map NULL: row_scale[s]; row_scale NULL: 1).  With the pair table's row
+ * scales and the GEMM's row map these are exactly the operand maxima
+ * nts_hip_gemm_h2p_tn_gather_cm takes when G_in is its B, so that GEMM reads
+ * G_in once.  feature_size <= 512, G rows 16-byte aligned with ld % 4 == 0. */
 uint32_t nts_hip_csr_bwd_colmax_rows_per_part(uint32_t feature_size);
 int nts_hip_spmm_csr_bwd_colmax(nts_hip_ctx *ctx, const uint32_t *row_offset,
                                 const uint32_t *column_indices, const float *weight_backward,
                                 const uint32_t *s, uint32_t s_cap, const float *g_out,
                                 uint64_t ld_gout, uint32_t feature_size, float *g_in,
-                                uint64_t ld_gin, uint32_t *part_max);
+                                uint64_t ld_gin, uint32_t *part_max, const float *row_scale,
+                                const uint32_t *row_map);
 /* Transform-first bottom layer: when the layer narrows the rows
  * (F_in > F_out), A (X W) replaces (A X) W — the reference aggregates first
  * (SingleGPUAllSampleGraphOp::forward then Parameter::forward,
@@ -485,11 +489,11 @@ int nts_hip_h2_split_rows_planar(nts_hip_ctx *ctx, uint64_t R, uint32_t K, const
 int nts_hip_gemm_h2p_tn_gather(nts_hip_ctx *ctx, int M, int N, int K, const uint16_t *Q, uint64_t ldq,
                                int Kp, const float *rs, const uint32_t *a_rows, const float *B,
                                uint64_t ldb, float *C, uint64_t ldc);
-/* The same with per-part column maxima of |B| given (part p = B rows
- * [p R, (p+1) R), N words per part — nts_hip_spmm_csr_bwd_colmax's output,
- * R = rows_per_part): each k-chunk's column scales come from the parts that
- * cover its rows times the chunk's largest row scale, with no pre-pass over B
- * in the kernel. */
+/* The same with per-part column maxima of |rs[a_rows[k]] B[k, c]| given
+ * (part p = B rows [p R, (p+1) R), N words per part —
+ * nts_hip_spmm_csr_bwd_colmax's output with row_scale = rs and row_map =
+ * a_rows, R = rows_per_part): each k-chunk's column scales come from the
+ * parts that cover its rows, with no pre-pass over B in the kernel. */
 int nts_hip_gemm_h2p_tn_gather_cm(nts_hip_ctx *ctx, int M, int N, int K, const uint16_t *Q,
                                   uint64_t ldq, int Kp, const float *rs, const uint32_t *a_rows,
                                   const float *B, uint64_t ldb, float *C, uint64_t ldc,

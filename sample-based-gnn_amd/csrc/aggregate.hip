@@ -113,8 +113,11 @@ struct AggExtra {
   uint32_t keep_threshold = 0;
   uint64_t seed = 0, offset = 0;
   // per-block column maxima of the output (nts_hip_spmm_csr_bwd_colmax):
-  // cm_out[b * F + col] = max over block b's rows d of |y[d, col]|, float bits
+  // cm_out[b * F + col] = max over block b's rows d of |rs(d) y[d, col]|, float
+  // bits, rs(d) = cm_rs[cm_map[d]] (cm_map NULL: cm_rs[d]; cm_rs NULL: 1)
   uint32_t* cm_out = nullptr;
+  const float* cm_rs = nullptr;
+  const uint32_t* cm_map = nullptr;
 };
 
 template <int VEC>
@@ -294,14 +297,17 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
     for (uint32_t c = threadIdx.x; c < ncol; c += kAggThreads) smax[c] = 0u;
     __syncthreads();
   }
-  auto colmax_row = [&](const T (&acc)[NCH], uint32_t c0) {
+  auto colmax_row = [&](const T (&acc)[NCH], uint32_t c0, uint32_t d) {
+    // the row's scale (a power of two: the product is exact unless it leaves
+    // the float range)
+    const float rsd = ax.cm_rs ? ax.cm_rs[ax.cm_map ? ax.cm_map[d] : d] : 1.f;
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
         const uint32_t col = (c0 + sl + c * LPD) * VEC + q;
         if (col < ncol)
-          atomicMax(&smax[col], __float_as_uint(fabsf(vcomp<VEC>(acc[c], q))));
+          atomicMax(&smax[col], __float_as_uint(fabsf(vcomp<VEC>(acc[c], q) * rsd)));
       }
   };
   for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
@@ -338,7 +344,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
       }
       store_row<VEC, LPD, NCH, MODE == kAggPostMask ? kAggPlain : EM>(acc, d, c0, sl, nv,
                                                                       last_valid, y, ldy, ax);
-      if constexpr (CM) colmax_row(acc, c0);
+      if constexpr (CM) colmax_row(acc, c0, d);
     }
   }
   if constexpr (COOP) {
@@ -371,7 +377,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
             acc[c] = s;
           }
           store_row<VEC, LPD, NCH, EM>(acc, d, c0, sl, nv, last_valid, y, ldy, ax);
-          if constexpr (CM) colmax_row(acc, c0);
+          if constexpr (CM) colmax_row(acc, c0, d);
         }
         __syncthreads();
       }
@@ -677,8 +683,10 @@ int nts_hip_spmm_csr_bwd_colmax(nts_hip_ctx* ctx, const uint32_t* row_offset,
                                 const uint32_t* column_indices, const float* weight_backward,
                                 const uint32_t* s, uint32_t s_cap, const float* g_out,
                                 uint64_t ld_gout, uint32_t feature_size, float* g_in,
-                                uint64_t ld_gin, uint32_t* part_max) {
+                                uint64_t ld_gin, uint32_t* part_max, const float* row_scale,
+                                const uint32_t* row_map) {
   NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && g_in && part_max, "NULL argument");
+  NTS_CHECK_ARG(row_scale || !row_map, "row_map without row_scale");
   NTS_CHECK_ARG(ld_gout >= feature_size && ld_gin >= feature_size,
                 "leading dimension < feature_size");
   NTS_CHECK_ARG(feature_size <= 512, "column maxima: at most 512 columns");
@@ -691,6 +699,8 @@ int nts_hip_spmm_csr_bwd_colmax(nts_hip_ctx* ctx, const uint32_t* row_offset,
   NTS_HIP_TRY(hipSetDevice(ctx->device));
   AggExtra ax;
   ax.cm_out = part_max;
+  ax.cm_rs = row_scale;
+  ax.cm_map = row_map;
   return launch_gather<false, false, kAggColmax, true>(ctx->stream, row_offset, column_indices,
                                                        weight_backward, s, s_cap, g_out, ld_gout,
                                                        nullptr, feature_size, g_in, ld_gin,

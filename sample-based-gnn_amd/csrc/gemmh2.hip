@@ -895,30 +895,23 @@ __global__ __launch_bounds__(kH2Tn3Threads, 1) void k_h2_tn4(int M, int K, const
   const int sr = tid >> 5, sc = 4 * (tid & 31);
   int bexp[4];
   if (ex.cparts) {
-    // the chunk's column scales from dH's producer (nts_hip_spmm_csr_bwd_colmax):
-    // max |B[k, c]| over the parts covering the chunk's rows (a superset at the
-    // chunk edges) times max |rs| over the chunk's rows (powers of two), so
-    // every |rs B| 2^e(col) < 2^15; dH is read once, by the main loop
-    float* red = reinterpret_cast<float*>(sbp);  // [4][128] column maxima, [8] rs maxima
+    // the chunk's column scales from dH's producer (nts_hip_spmm_csr_bwd_colmax
+    // with the row scales): max |rs[row] B[row, c]| over the parts covering
+    // the chunk's rows (a superset at the chunk edges: a scale at most that
+    // much smaller), so every |rs B| 2^e(col) < 2^15; dH is read once, by the
+    // main loop
+    float* red = reinterpret_cast<float*>(sbp);  // [4][128] column maxima
     {
       const int cl = tid & 127, j = tid >> 7;
       const uint32_t p0 = (uint32_t)kbeg / ex.rpp, p1 = (uint32_t)(kbeg + klast) / ex.rpp;
       uint32_t m = 0;
       for (uint32_t p = p0 + j; p <= p1; p += 4) m = max(m, ex.cparts[(uint64_t)p * ex.nparts_ld + n0 + cl]);
       red[128 * j + cl] = __uint_as_float(m);
-      float r = 0.f;
-      for (int k = tid; k <= klast; k += kH2Tn3Threads) r = fmaxf(r, fabsf(ssc[k]));
-      for (int o = 32; o > 0; o >>= 1) r = fmaxf(r, __shfl_xor(r, o));
-      if (lane == 0) red[512 + wv] = r;
     }
     __syncthreads();
     if (tid < 128) {
-      float rm = 0.f;
-      for (int w = 0; w < 8; ++w) rm = fmaxf(rm, red[512 + w]);
       const float m = fmaxf(fmaxf(red[tid], red[128 + tid]), fmaxf(red[256 + tid], red[384 + tid]));
-      // 2^e (m rm) in [2^13, 2^15): e = h2_exp(m) + h2_exp(rm) - 15, with no
-      // product formed (it may overflow)
-      sce[tid] = (m > 0.f && rm > 0.f) ? h2_exp(m) + h2_exp(rm) - 15 : 0;
+      sce[tid] = h2_exp(m);  // 2^e m in [2^14, 2^15)
     }
     __syncthreads();
 #pragma unroll

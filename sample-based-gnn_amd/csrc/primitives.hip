@@ -249,13 +249,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   __shared__ uint32_t s_prefix;
   const int t = threadIdx.x, lane = t & 63;
   uint64_t n;
+  uint32_t v_req = 0;
   if (COUNT) {
-    const uint32_t v_req = *ca.v_in;
+    v_req = *ca.v_in;
     n = min(v_req, ca.v_cap);
-    if (blockIdx.x == 0 && t == 0) {
-      ca.sizes[0] = (uint32_t)n;
-      ca.sizes[3] = v_req > ca.v_cap ? 1u : 0u;
-    }
+    if (blockIdx.x == 0 && t == 0) ca.sizes[0] = (uint32_t)n;
   } else {
     n = n_dev ? (uint64_t)*n_dev : n_cap;
   }
@@ -342,9 +340,11 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
     const uint64_t i = base + j;
     if (i <= n) out[i] = tile[pad_idx(j)];
     if (COUNT && i == n) {  // e_size = co[v], clamped to the edge capacity
+      // the overflow flag has ONE writer, this item's thread, for both
+      // capacities: a store from another workgroup could land after it
       const uint32_t e = tile[pad_idx(j)];
       ca.sizes[1] = min(e, ca.e_cap);
-      if (e > ca.e_cap) atomicOr(&ca.sizes[3], 1u);
+      ca.sizes[3] = (v_req > ca.v_cap ? 1u : 0u) | (e > ca.e_cap ? 1u : 0u);
     }
   }
 }

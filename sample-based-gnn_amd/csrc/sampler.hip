@@ -1144,6 +1144,9 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
     *nfallback = fallbacks;
   }
   // the generator after the layer: _M_p + consumed words from the state's block
+  // (only when the words consumed are inside the generated stream: past it the
+  // block index leaves rb, and the host reports the short stream)
+  if (dl + base[v] > nw) return;
   const uint32_t a = mt_state[624] + base[v] + dl;
   uint32_t b = a / 624, off = a % 624;
   if (off == 0 && b > 0) {  // libstdc++ keeps the exhausted block until the next call

@@ -132,7 +132,7 @@ def lib() -> C.CDLL:
         "nts_hip_gemm_h2p_tn_gather_cm": ([P, I, I, I, P, U64, I, P, P, P, U64, P, U64, P, U32], I),
         "nts_hip_gemm_h2p_gather": ([P, I, I, I, I, P, U64, P, P, P, U64, I, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),
-        "nts_hip_spmm_csr_bwd_colmax": ([P, P, P, P, P, U32, P, U64, U32, P, U64, P], I),
+        "nts_hip_spmm_csr_bwd_colmax": ([P, P, P, P, P, U32, P, U64, U32, P, U64, P, P, P], I),
         "nts_hip_csr_bwd_colmax_rows_per_part": ([U32], U32),
         "nts_hip_gemm_h2d_act": ([P, I, I, I, I, P, U64, P, U64, P, U64, F, U64, U64, P, U64, P], I),
         "nts_hip_spmm_csc_bwd_atomic": ([P, P, P, P, P, U32, P, U64, U32, P, U64], I),

@@ -171,13 +171,15 @@ class HipContext:
     def colmax_rows_per_part(self, F):
         return int(self.lib.nts_hip_csr_bwd_colmax_rows_per_part(F))
 
-    def spmm_csr_bwd_colmax(self, ro, ci, wb, s_dev, s_cap, g_out, g_in, parts):
-        """spmm_csr_bwd + parts[p, c] (int32 bits) = max |g_in[s, c]| over the
-        part's rows s in [p R, (p+1) R), R = colmax_rows_per_part(F)."""
+    def spmm_csr_bwd_colmax(self, ro, ci, wb, s_dev, s_cap, g_out, g_in, parts, rs=None,
+                            rows=None):
+        """spmm_csr_bwd + parts[p, c] (int32 bits) = max |rs(s) g_in[s, c]| over
+        the part's rows s in [p R, (p+1) R), R = colmax_rows_per_part(F),
+        rs(s) = rs[rows[s]] (rows None: rs[s]; rs None: 1)."""
         F = g_out.shape[1]
         check(self.lib.nts_hip_spmm_csr_bwd_colmax(self.h, ptr(ro), ptr(ci), ptr(wb), ptr(s_dev), s_cap,
                                                    ptr(g_out), g_out.stride(0), F, ptr(g_in),
-                                                   g_in.stride(0), ptr(parts)))
+                                                   g_in.stride(0), ptr(parts), ptr(rs), ptr(rows)))
 
     def spmm_csc_bwd_atomic(self, co, ri, w, v_dev, v_cap, g_out, g_in):
         F = g_out.shape[1]

@@ -359,6 +359,9 @@ SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
     s->v_size = (VertexId)hs[4 * l];
     s->e_size = (VertexId)hs[4 * l + 1];
     s->src_size = (VertexId)hs[4 * l + 2];
+    TORCH_CHECK((hs[4 * l + 3] & 4) == 0, "sampled layer ", l,
+                ": the MT19937 word stream generated for the layer fell short of the words "
+                "its rejection draws consumed (the generator state is not advanced)");
     TORCH_CHECK(hs[4 * l + 3] == 0, "sampled layer ", l, " exceeded its capacity");
     sampled_edges += s->e_size;
   }
@@ -692,7 +695,7 @@ struct HipLinearFn : public torch::autograd::Function<HipLinearFn> {
 // backward in the weight-gradient GEMM's operand load (nts_hip.h).
 struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar x, NtsVar W, double p, int64_t seed,
-                        int64_t offset, int64_t cs_ptr) {
+                        int64_t offset, int64_t cs_ptr, bool pair_split) {
     auto* cs = reinterpret_cast<NtsStream*>(cs_ptr);
     NtsVar xc = row_major(x), Wc = W.contiguous();
     const int64_t M = xc.size(0), K = xc.size(1), N = Wc.size(1);
@@ -700,12 +703,9 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
     NtsVar X = torch::empty({M, N}, xc.options());
     // a narrow input (K <= 128, N 128 or 256: the products / papers-shaped
     // aggregate-first bottom layer) on the in-kernel f16 pair split
-    // (nts_hip_gemm_h2d_act); NTS_H2D=0 keeps the GEMM mode's kernel
-    static const bool h2d = [] {
-      const char* e = getenv("NTS_H2D");
-      return !(e && e[0] == '0');
-    }();
-    if (h2d && K <= 128 && K % 4 == 0 && (N == 128 || N == 256) && xc.stride(0) % 4 == 0 &&
+    // (nts_hip_gemm_h2d_act) when the config allows pair-split
+    // arithmetic (GCNConfig::pair_table > 0); otherwise the GEMM mode's kernel
+    if (pair_split && K <= 128 && K % 4 == 0 && (N == 128 || N == 256) && xc.stride(0) % 4 == 0 &&
         (uintptr_t)xc.data_ptr<float>() % 16 == 0)
       hip_check(nts_hip_gemm_h2d_act(cs->ctx(), 1, (int)M, (int)N, (int)K, xc.data_ptr<float>(),
                                      (uint64_t)xc.stride(0), Wc.data_ptr<float>(), (uint64_t)N,
@@ -756,7 +756,7 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
                                  dx.data_ptr<float>(), (uint64_t)K),
                 "nts_hip_gemm_f32(dx)");
     }
-    return {dx, dW, NtsVar(), NtsVar(), NtsVar(), NtsVar()};
+    return {dx, dW, NtsVar(), NtsVar(), NtsVar(), NtsVar(), NtsVar()};
   }
 };
 
@@ -869,14 +869,18 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
       // from this gather's epilogue (one read of dH instead of two);
       // NTS_TN_CHUNK_SCALES=1 keeps its own per-chunk pre-pass
       static const bool chunk_scales = getenv("NTS_TN_CHUNK_SCALES") != nullptr;
-      if (pairs_q && !chunk_scales && N <= 512 && N % 4 == 0) {
+      // (its float4 rows need 16-byte aligned dZ / dH rows: else the plain gather)
+      const bool cm_rows = N <= 512 && N % 4 == 0 && (uintptr_t)dZ.data_ptr<float>() % 16 == 0 &&
+                           (uintptr_t)dH.data_ptr<float>() % 16 == 0;
+      if (pairs_q && !chunk_scales && cm_rows) {
         rpp = nts_hip_csr_bwd_colmax_rows_per_part((uint32_t)N);
         const int64_t nparts = (std::max<int64_t>(s, 1) + rpp - 1) / rpp;
         colmax = torch::empty({nparts, N}, torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, dev));
         hip_check(nts_hip_spmm_csr_bwd_colmax(
                       cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(), nullptr, (uint32_t)s,
                       dZ.data_ptr<float>(), (uint64_t)N, (uint32_t)N, dH.data_ptr<float>(), (uint64_t)N,
-                      reinterpret_cast<uint32_t*>(colmax.data_ptr<int32_t>())),
+                      reinterpret_cast<uint32_t*>(colmax.data_ptr<int32_t>()),
+                      pairs_q->rs.data_ptr<float>(), sg->dev_src()),
                   "nts_hip_spmm_csr_bwd_colmax");
       } else {
         hip_check(nts_hip_spmm_csr_bwd(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(),
@@ -989,9 +993,9 @@ struct HipLinearXentFn : public torch::autograd::Function<HipLinearXentFn> {
 }  // namespace
 
 NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
-                      NtsStream* cs) {
+                      NtsStream* cs, bool pair_split) {
   return HipLinearActFn::apply(x, W, p, (int64_t)seed, (int64_t)offset,
-                               reinterpret_cast<int64_t>(cs));
+                               reinterpret_cast<int64_t>(cs), pair_split);
 }
 
 // dropout(relu(x)) on its own (nts_hip_relu_dropout_f32, the GEMM epilogue's

@@ -323,7 +323,7 @@ NtsVar GCN_SAMPLE_ALLGPU_impl::vertexForward(int l, NtsVar& a) {
   if (cfg.hip_gemm && cfg.fuse_activation) {
     const double p = ctx.is_train() ? cfg.drop_rate : 0.0;
     return hip_linear_act(a, P[l]->W, p, (uint64_t)cfg.seed * 0x9E3779B97F4A7C15ull + 1,
-                          dropout_calls_++, cs.get());
+                          dropout_calls_++, cs.get(), cfg.pair_table > 0);
   }
   return torch::dropout(torch::relu(P[l]->forward(a)), cfg.drop_rate, ctx.is_train());
 }

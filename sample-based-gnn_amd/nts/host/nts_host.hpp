@@ -391,8 +391,10 @@ NtsVar row_major(const NtsVar& x);
 NtsVar row_padded_empty(int64_t rows, int64_t F, int device);
 // dropout(relu(x W), p) in one MFMA GEMM (activation in the epilogue, Philox
 // mask of (seed, offset)); autograd: dW = x^T (dX ⊙ [X > 0] / (1-p)) fused.
+// pair_split: narrow inputs (K <= 128, N 128 | 256) may use the in-kernel f16
+// pair split (nts_hip_gemm_h2d_act) instead of the GEMM mode's kernel.
 NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed, uint64_t offset,
-                      NtsStream* cs);
+                      NtsStream* cs, bool pair_split);
 
 // Device time of selected kernels on the stream that launches them (HIP
 // events; resolve() synchronises — call outside timed regions).  `units` are

@@ -225,24 +225,32 @@ def test_h2p_gemm_tn_gather(ctx, M, N, K, gscale):
     assert torch.equal(Ch, Ch2)
 
 
-@pytest.mark.parametrize("M,N,K,gscale", [(602, 128, 228656, 1e-7), (602, 128, 5003, 1.0),
-                                          (100, 256, 3000, 1e3), (41, 128, 17, 1.0)])
-def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale):
-    """TN v4 with B's per-part column maxima given (the CSR backward's
-    epilogue) instead of its per-chunk pre-pass over B: the same error bar vs
-    fp64, deterministic."""
+@pytest.mark.parametrize("M,N,K,gscale,anti", [(602, 128, 228656, 1e-7, False),
+                                               (602, 128, 5003, 1.0, False),
+                                               (100, 256, 3000, 1e3, False), (41, 128, 17, 1.0, False),
+                                               (602, 128, 5003, 1.0, True),
+                                               (602, 128, 228656, 1e-3, True)])
+def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale, anti):
+    """TN v4 with the per-part column maxima of |rs[row] B| given (the CSR
+    backward's epilogue) instead of its per-chunk pre-pass over B: the same
+    error bar vs fp64, deterministic.  anti: B's rows scaled inversely to the
+    magnitudes of their X rows (6 decades), where max |rs| x max |B| would
+    overstate the operand maxima by ~2^20."""
     g = torch.Generator(device=DEV).manual_seed(M * N + K + 23)
     V = K + K // 2 + 5
     X = _table(V, M, g, decades=6)
     rows = torch.randint(0, V, (K,), device=DEV, generator=g).to(torch.int32)
     G = torch.randn(K, N, device=DEV, generator=g) * gscale
+    if anti:
+        amax = X[rows.long()].abs().amax(1, keepdim=True)
+        G *= torch.where(amax > 0, 1.0 / amax.clamp_min(1e-30), torch.ones_like(amax))
     G[:, 5] *= 1e-9
     G[:, 9] = 0.0  # an all-zero column (max 0)
     Q, rs = ctx.h2_split_rows_planar(X)
     R = 8  # rows per part (the CSR backward's for N = 128)
     nparts = (K + R - 1) // R
     pad = torch.zeros(nparts * R, N, device=DEV)
-    pad[:K] = G.abs()
+    pad[:K] = G.abs() * rs[rows.long()][:, None]  # maxima of |rs[row] G[k, c]|
     cm = pad.view(nparts, R, N).max(1).values.contiguous().view(torch.int32)
     C32 = torch.empty(M, N, device=DEV)
     Ch = torch.full((M, N), float("nan"), device=DEV)

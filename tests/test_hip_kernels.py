@@ -558,6 +558,17 @@ def test_spmm_csr_bwd_colmax(hip, cora, F):
     pad[:s] = plain.abs()
     want = pad.view(nparts, R, F).max(1).values
     assert torch.equal(parts.view(torch.float32), want)
+    # scaled by power-of-two row scales through a row map (the pair table's
+    # rs[source[s]], the TN GEMM's exact operand maxima)
+    rsv = torch.pow(2.0, torch.randint(-30, 30, (V,), device=DEV).float())
+    rmap = _t(l0["source"])
+    parts2 = torch.full((nparts, F), -1, dtype=torch.int32, device=DEV)
+    got2 = torch.empty_like(got)
+    hip.spmm_csr_bwd_colmax(ro, ci, wb, sdev, cap, G, got2, parts2, rs=rsv, rows=rmap)
+    torch.cuda.synchronize()
+    assert torch.equal(got2[:s], plain)
+    pad[:s] = plain.abs() * rsv[rmap.long()][:, None]
+    assert torch.equal(parts2.view(torch.float32), pad.view(nparts, R, F).max(1).values)
 
 
 @pytest.mark.parametrize("M,N,K", [(3000, 128, 602), (2500, 64, 100), (500, 41, 100), (37, 7, 13)])
@@ -959,3 +970,37 @@ def test_act_backward(hip, rows, F, pad):
     torch.cuda.synchronize()
     ref = torch.where(X > 0, G * 2.0, torch.zeros_like(G))
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("rng_mode", [0])
+def test_capacity_overflow_flag_survives_multi_tile_scan(hip, rng_mode):
+    """The fused count scan sets the overflow flag from ONE thread (the item
+    at n), for the edge capacity and the dst capacity alike, with the dsts
+    spanning several 4,096-item scan tiles: a truncated layer is always
+    reported (a block-0 clear racing an atomicOr from another
+    tile could lose it)."""
+    from nts.hip import LayerBuffers
+    V, src, dst = _random_graph(30000, 600000, 11)
+    g = _graph(hip, V, src, dst)
+    seeds = np.arange(0, 14000, dtype=np.uint32)  # 4 scan tiles
+    hip.reserve(V, 14000 * 10)
+    dst_t = _t(seeds)
+    vsz = torch.tensor([seeds.size], dtype=torch.int32, device=DEV)
+    for rep in range(8):
+        # edge capacity exceeded
+        lay = LayerBuffers(14000, 5000, 14000 * 10, dst_t, vsz, torch.device(DEV))
+        hip.sample_layer(g, lay, 10, 0, rep, rng_mode, 0)
+        torch.cuda.synchronize()
+        v, e, s, ovf = lay.sizes_host()
+        assert v == 14000 and e == 5000 and (ovf & 1), (rep, v, e, ovf)
+        # dst capacity exceeded (v_req = 14000 > v_cap = 9000)
+        lay = LayerBuffers(9000, 9000 * 10, 9000 * 10, dst_t, vsz, torch.device(DEV))
+        hip.sample_layer(g, lay, 10, 0, rep, rng_mode, 0)
+        torch.cuda.synchronize()
+        v, e, s, ovf = lay.sizes_host()
+        assert v == 9000 and (ovf & 1), (rep, v, e, ovf)
+        # in capacity: no flag
+        lay = LayerBuffers(14000, 14000 * 10, 14000 * 10, dst_t, vsz, torch.device(DEV))
+        hip.sample_layer(g, lay, 10, 0, rep, rng_mode, 0)
+        torch.cuda.synchronize()
+        assert lay.sizes_host()[3] == 0
