@@ -236,6 +236,9 @@ def parse():
                    help="train on the first N seeds of this rank's shard only (0: all).  PD "
                         "cache on papers100M-shaped graphs: preSample keeps every "
                         "super-batch's hot ids (~0.7 M per super-batch there)")
+    p.add_argument("--no-secondary-exact", action="store_true",
+                   help="skip the secondary measurement of the headline order with fp32-exact "
+                        "GEMM inputs (split-bf16 on the gathered rows instead of the pair tables)")
     p.add_argument("--no-secondary-af", action="store_true",
                    help="skip the secondary measurement of the reference's bottom-layer order "
                         "(aggregate-first, fp32 aggregation) beside a transform-first headline")
@@ -464,38 +467,53 @@ def main():
                         "unit": "sampled-edges/s", "batches_per_gpu": int(r["batches"]),
                         "note": "GPU sampler alone on its stream (3 batches in flight), all ranks"}
 
-    # ---- the reference's bottom-layer order on the same workload ------------------
-    secondary = None
-    if tf and args.model == "gcn" and not args.no_secondary_af and args.steps > 0:
-        cfg_af = host.gcn_config(layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4,
-                                 drop_rate=0.5, rng_mode=RNG_MODES[args.rng], weight=args.weight,
-                                 pipeline=not args.no_pipeline, transform_first=0,
-                                 gemm=args.gemm, deterministic_backward=not args.atomic_backward)
-        drv_af = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg_af, comm)
+    # ---- secondary orders / arithmetic on the same workload ----------------------
+    def time_secondary(cfg2):
+        drv2 = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg2, comm)
 
-        def step_af():
-            if not drv_af.sample_not_finished():
-                drv_af.restart()
-            drv_af.train_batch()
+        def step2():
+            if not drv2.sample_not_finished():
+                drv2.restart()
+            drv2.train_batch()
 
         for _ in range(args.warmup):
-            step_af()
-        drv_af.synchronize()
-        drv_af.reset_stats()
+            step2()
+        drv2.synchronize()
+        drv2.reset_stats()
         barrier()
         ta = time.perf_counter()
         for _ in range(args.steps):
-            step_af()
-        drv_af.synchronize()
+            step2()
+        drv2.synchronize()
         barrier()
-        el_af = max_over_ranks(time.perf_counter() - ta)
-        secondary = {
-            "bottom_layer": "aggregate-first (A X) W, the reference's order: fp32 aggregation "
-                            "bit-exact vs MiniBatchFuseOp, split-bf16 GEMMs (fp32-accurate)",
-            "value": sum_over_ranks(float(drv_af.batch_edges)) / el_af,
-            "unit": "sampled-edges/s", "ms_per_step": el_af / args.steps * 1e3,
-            "steps": args.steps, "warmup": args.warmup}
-        del drv_af
+        el2 = max_over_ranks(time.perf_counter() - ta)
+        out = {"value": sum_over_ranks(float(drv2.batch_edges)) / el2, "unit": "sampled-edges/s",
+               "ms_per_step": el2 / args.steps * 1e3, "steps": args.steps, "warmup": args.warmup}
+        del drv2
+        return out
+
+    secondary = None  # the reference's bottom-layer order
+    exact_tf = None   # the headline order with fp32-exact GEMM inputs
+    if tf and args.model == "gcn" and args.steps > 0:
+        if not args.no_secondary_af:
+            secondary = {
+                "bottom_layer": "aggregate-first (A X) W, the reference's order: fp32 aggregation "
+                                "bit-exact vs MiniBatchFuseOp, split-bf16 GEMMs (fp32-accurate)",
+                **time_secondary(host.gcn_config(
+                    layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
+                    rng_mode=RNG_MODES[args.rng], weight=args.weight,
+                    pipeline=not args.no_pipeline, transform_first=0, gemm=args.gemm,
+                    deterministic_backward=not args.atomic_backward))}
+        if args.pair_table > 0 and not args.no_secondary_exact:
+            exact_tf = {
+                "bottom_layer": "transform-first A (X W) with fp32-exact GEMM inputs: the gathered "
+                                "fp32 feature rows split in the kernel into three bf16 pieces, six "
+                                "products, fp32 accumulate (no pair table)",
+                **time_secondary(host.gcn_config(
+                    layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
+                    rng_mode=RNG_MODES[args.rng], weight=args.weight,
+                    pipeline=not args.no_pipeline, transform_first=1, gemm="split3", pair_table=0,
+                    deterministic_backward=not args.atomic_backward))}
 
     value = edges / elapsed
     rl = roofline(prof, args, layers, world)
@@ -540,6 +558,7 @@ def main():
                        if tf and args.pair_table >= 1 else ""),
             "layer_sizes_top_down": layer_sizes,
             "reference_order_secondary": secondary,
+            "fp32_exact_inputs_secondary": exact_tf,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
                              "nts_env": nts_env(),
                              "workload": pmc_workload(args, layers, world)},
