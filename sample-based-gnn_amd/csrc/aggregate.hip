@@ -510,6 +510,309 @@ __global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float
 }
 
 // ---------------------------------------------------------------------------
+// LDS-staged aggregation of 128-float rows (k_agg_lds): the same sums as
+// k_spmm_gather (per output row, its edges in edge order, acc + x * w with
+// contraction off — bit-identical for every row k_spmm_gather sums serially;
+// the long CSR rows it splits into pieces are summed serially here, i.e. in
+// MiniBatchFuseOp's order), but the neighbour rows are gathered into LDS by
+// LDS DMA (global_load_lds_dwordx4, per-lane row bases) instead of registers:
+// the gather form MI355X_MICROARCH.md measures at 7.4-8.6 TB/s against
+// 5.5-5.8 for register gathers (§ Indexed rows: gather into LDS).
+//
+// Block = 1 loader wave + 4 consumer waves (8 groups of 32 lanes, one float4
+// of the row per lane).  Output rows are cut into parts of kLdsR rows; block
+// b takes parts b, b + G, ... and streams each part's edges in stages of
+// kLdsSE rows through a ring of kLdsNS LDS slots:
+//   loader  per stage k: wait until the consumers freed slot k % NS (stage
+//           k - NS done), put the stage's weights, its part's offsets and its
+//           descriptor into the slot (loaded two stages ahead), issue the 16
+//           row DMAs, then (counted vmcnt, in-order completion) mark stage
+//           k - 3 full.  Only the loader issues vector-memory loads, so its
+//           vmcnt counts are static; three stages stay in flight.
+//   groups  group g owns rows pR + g + 8 j of part p and sums each row's
+//           edges that fall in the stage, stores a row when its last edge is
+//           in, and carries a row that continues into the next stage.
+// Output modes as k_spmm_gather's: plain, relu/dropout epilogue (kAggAct),
+// post-mask (kAggPostMask), column maxima per part (kAggColmax; part p's
+// maxima row = max over its rows of |rs(row) y|, the TN GEMM's operand
+// scales), all written by store_row.
+constexpr int kLdsR = 128;                       // output rows per part
+constexpr int kLdsSE = 32;                       // edges (rows of x) per stage
+constexpr int kLdsNS = 4;                        // ring slots
+constexpr int kLdsCons = 4;                      // consumer waves
+constexpr int kLdsThreads = kWave * (kLdsCons + 1);
+constexpr int kLdsRowB = 512;                    // 128 floats
+constexpr int kLdsMaxParts = 64;                 // parts per block (lane-held bounds)
+constexpr int kLdsCmSlots = 8;                   // colmax part ring
+constexpr int kLdsF = 128;                       // floats per row
+
+struct LdsAggShared {
+  float4 rows[kLdsNS][kLdsSE][32];               // 64 KB
+  float w[kLdsNS][kLdsSE];
+  uint32_t offs[kLdsNS][kLdsR];                  // the stage's part: off[pR + j]
+  uint4 meta[kLdsNS];                            // {part, sb, se, flags | total << 8}
+  uint32_t pend[kLdsNS];                         // the part's edge end off[min(pR + R, n)]
+  uint32_t full[kLdsNS], freed[kLdsNS];
+  // loader staging, three stages ahead of the ring: [0, 32) row ids, [32, 64)
+  // weights, then the part's offsets 0..127 (global_load_lds_dword)
+  uint32_t stg[3][64 + kLdsR];
+  uint4 stgd[3];                                 // staged descriptors {part i, sb, se, flags}
+  uint32_t cm[kLdsCmSlots][kLdsF];               // kAggColmax: part maxima ring
+  uint32_t cm_cnt[kLdsCmSlots];
+};
+
+// 16 (or 4) bytes per lane from `src` to LDS (wave-uniform base `lds`) + 16 (4)
+// * lane.  Inline asm: the compiler neither counts these loads nor waits for
+// them — the loader's s_waitcnt vmcnt(N) are the only waits, with N counted by
+// hand (every load the loader issues is one of these).
+__device__ __forceinline__ void glds16a(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+__device__ __forceinline__ void glds4a(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// bounded spin (a hang would take the GPU with it): gives up after ~2^22 polls
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
+  for (uint32_t it = 0; lds_ld(p) < v && it < (1u << 22); ++it) __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
+    const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
+    const float* __restrict__ x, uint64_t ldx, float* __restrict__ y, uint64_t ldy, AggExtra ax) {
+  constexpr bool CM = MODE == kAggColmax;
+  constexpr int EM = CM ? kAggPlain : MODE;
+  __shared__ LdsAggShared sh;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t parts = (n + kLdsR - 1) / kLdsR;
+  const uint32_t parts_cap = (n_cap + kLdsR - 1) / kLdsR;
+  const uint32_t my_parts = parts > b ? (parts - b + G - 1) / G : 0u;  // <= kLdsMaxParts (host)
+  for (int i = tid; i < kLdsNS; i += kLdsThreads) {
+    sh.full[i] = 0u;
+    sh.freed[i] = 0u;
+  }
+  if (CM) {
+    for (int i = tid; i < kLdsCmSlots * kLdsF; i += kLdsThreads) (&sh.cm[0][0])[i] = 0u;
+    for (int i = tid; i < kLdsCmSlots; i += kLdsThreads) sh.cm_cnt[i] = 0u;
+    // parts past the live rows: zero maxima (as k_spmm_gather's per-block rows)
+    for (uint32_t p = parts + (b + G - parts % G) % G; p < parts_cap; p += G)
+      for (int c = tid; c < kLdsF; c += kLdsThreads) ax.cm_out[(uint64_t)p * kLdsF + c] = 0u;
+  }
+  __syncthreads();
+  if (my_parts == 0) return;
+
+  if (wv == kLdsCons) {
+    // ---------------- loader wave ----------------
+    // lane i holds part i's edge bounds and stage count
+    uint32_t pe0 = 0, pe1 = 0, nst = 0;
+    if ((uint32_t)lane < my_parts) {
+      const uint32_t p = b + (uint32_t)lane * G;
+      pe0 = off[(uint64_t)p * kLdsR];
+      pe1 = off[min((uint64_t)(p + 1) * kLdsR, (uint64_t)n)];
+      nst = max(1u, (pe1 - pe0 + kLdsSE - 1) / kLdsSE);
+    }
+    uint32_t total = nst;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o);
+    // stage descriptors in order (cursor: part i, stage s of it); past the end
+    // the last stage again (dummy loads that nothing reads)
+    uint32_t cur_i = 0, cur_s = 0;
+    const uint32_t lstg = lds_u32(&sh.stg[0][0]);
+    // ids (lanes 0-31) and weights (32-63) of stage q's edges, the part's
+    // offsets: three global_load_lds_dword into staging entry q % 3
+    auto load_ids = [&](uint32_t q) {
+      const uint32_t i = min(cur_i, my_parts - 1);
+      const uint32_t e0 = __shfl(pe0, (int)i), e1 = __shfl(pe1, (int)i), ns = __shfl(nst, (int)i);
+      const uint32_t st = cur_i < my_parts ? cur_s : ns - 1;
+      const int qq = (int)(q % 3);
+      const uint32_t sb = e0 + st * kLdsSE, se = min(sb + kLdsSE, e1);
+      if (lane == 0)  // (read back after this entry's loads landed: ordered by the vmcnt wait)
+        sh.stgd[qq] = make_uint4(i, sb, se, (st == 0 ? 1u : 0u) | (st + 1 == ns ? 2u : 0u));
+      if (cur_i < my_parts && ++cur_s == ns) {
+        cur_s = 0;
+        ++cur_i;
+      }
+      const uint32_t e = sb + (uint32_t)(lane & 31);
+      const uint32_t ec = e < se ? e : sb < se ? sb : 0u;
+      const void* src = lane < 32 || !w ? (const void*)(idx + ec) : (const void*)(w + ec);
+      glds4a(src, lstg + (uint32_t)(qq * (64 + kLdsR) * 4));
+      const uint64_t p = b + i * G;
+      glds4a(off + min(p * kLdsR + lane, (uint64_t)n), lstg + (uint32_t)((qq * (64 + kLdsR) + 64) * 4));
+      glds4a(off + min(p * kLdsR + 64 + lane, (uint64_t)n),
+             lstg + (uint32_t)((qq * (64 + kLdsR) + 128) * 4));
+    };
+    const uint32_t lrows = lds_u32(&sh.rows[0][0][0]);
+    load_ids(0);
+    load_ids(1);
+    for (uint32_t k = 0; k < total; ++k) {
+      const uint32_t slot = k % kLdsNS;
+      const int qq = (int)(k % 3);
+      if (k >= (uint32_t)kLdsNS) lds_wait_ge(&sh.freed[slot], (uint32_t)kLdsCons * (k / kLdsNS));
+      // staging of stage k landed.  Younger: k = 0: ids(1); k = 1: ids(2),
+      // rows(0); k >= 2: rows(k-2), ids(k+1), rows(k-1) — 3 + 16 + 3 + 16
+      // loads; so the rows of stage k-3 (older than ids(k)) have landed too
+      if (k == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (k == 1) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(35)" ::: "memory");
+      if (k >= 3) lds_st(&sh.full[(k - 3) % kLdsNS], k - 2);
+      // staging -> the slot (weights, offsets, descriptor)
+      const uint32_t id = sh.stg[qq][lane & 31];
+      const uint4 dsc = sh.stgd[qq];
+      const uint32_t sb = dsc.y, se = dsc.z;
+      const uint32_t pend = __shfl(pe1, (int)dsc.x);
+      if (lane >= 32) sh.w[slot][lane - 32] = w ? __uint_as_float(sh.stg[qq][lane]) : 1.f;
+      sh.offs[slot][lane] = sh.stg[qq][64 + lane];
+      sh.offs[slot][64 + lane] = sh.stg[qq][128 + lane];
+      if (lane == 0) {
+        sh.meta[slot] = make_uint4(b + dsc.x * G, sb, se, dsc.w | (total << 8));
+        sh.pend[slot] = pend;
+      }
+      load_ids(k + 2);  // staging entry (k + 2) % 3 held stage k - 1: copied out already
+      // 16 row DMAs: instruction j moves rows 2j (lanes 0-31) and 2j + 1
+      const uint32_t nrow = se - sb;
+      const uint32_t id0 = __shfl(id, 0);
+#pragma unroll
+      for (int jj = 0; jj < kLdsSE / 2; ++jj) {
+        const int r = 2 * jj + (lane >> 5);
+        uint32_t rid = __shfl(id, r);
+        rid = (uint32_t)r < nrow ? rid : (nrow ? id0 : 0u);
+        const char* src = reinterpret_cast<const char*>(x + (uint64_t)rid * ldx) + 16 * (lane & 31);
+        glds16a(src, lrows + (uint32_t)((slot * kLdsSE + 2 * jj) * kLdsRowB));
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t k = total > 3 ? total - 3 : 0; k < total; ++k) lds_st(&sh.full[k % kLdsNS], k + 1);
+    return;
+  }
+
+  // ---------------- consumer waves: 8 groups of 32 lanes ----------------
+  const int g = 2 * wv + (lane >> 5), l = lane & 31;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 cmx = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t j = 0, pcount = 0;                    // local row of the part, rows in the part
+  uint32_t e_beg = 0, e_end = 0, part = 0, part_ord = 0;
+  float4 pm = make_float4(0.f, 0.f, 0.f, 0.f);  // kAggPostMask: the row's mask
+  float rsd = 1.f;                               // kAggColmax: the row's scale
+  auto row_ctx = [&](uint32_t d) {  // per-row operands known before its edges
+    if constexpr (MODE == kAggPostMask)
+      pm = *reinterpret_cast<const float4*>(ax.mx + (uint64_t)d * ax.ldm + 4 * l);
+    if constexpr (CM) rsd = ax.cm_rs ? ax.cm_rs[ax.cm_map ? ax.cm_map[d] : d] : 1.f;
+  };
+  uint32_t total = 1;
+  for (uint32_t k = 0; k < total; ++k) {
+    const uint32_t slot = k % kLdsNS;
+    lds_wait_ge(&sh.full[slot], k + 1);
+    const uint4 mt = sh.meta[slot];
+    total = mt.w >> 8;
+    const uint32_t sb = mt.y, se = mt.z, fl = mt.w & 255u;
+    if (fl & 1u) {  // first stage of part mt.x: this group's first row
+      part = mt.x;
+      pcount = min((uint32_t)kLdsR, n - part * kLdsR);
+      j = (uint32_t)g;
+      if (j < pcount) {
+        e_beg = sh.offs[slot][j];
+        e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
+        row_ctx(part * kLdsR + j);
+      }
+      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      cmx = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const float4* srow = &sh.rows[slot][0][l];
+    const float* sw = sh.w[slot];
+    // rows whose edges start in this stage (a row without edges at the
+    // stage's end included): sum their edges here, store the complete ones
+    while (j < pcount && (e_beg < se || (e_beg == e_end && e_beg <= se))) {
+      uint32_t e = max(e_beg, sb);
+      const uint32_t hi = min(e_end, se);
+      for (; e + 4 <= hi; e += 4) {  // four rows of x in flight
+        float4 xv[4];
+        float wv4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          xv[u] = srow[(e + u - sb) * 32];
+          wv4[u] = sw[e + u - sb];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc = VT<4>::madd(acc, xv[u], wv4[u]);
+      }
+      for (; e < hi; ++e) acc = VT<4>::madd(acc, srow[(e - sb) * 32], sw[e - sb]);
+      if (e_end > se) break;  // continues in the next stage
+      const uint32_t d = part * kLdsR + j;
+      float4 a1[1] = {acc};
+      if constexpr (MODE == kAggPostMask)
+        a1[0] = make_float4(pm.x > 0.f ? a1[0].x * ax.scale : 0.f, pm.y > 0.f ? a1[0].y * ax.scale : 0.f,
+                            pm.z > 0.f ? a1[0].z * ax.scale : 0.f, pm.w > 0.f ? a1[0].w * ax.scale : 0.f);
+      store_row<4, 32, 1, MODE == kAggPostMask ? kAggPlain : EM>(a1, d, 0, l, 32, 4, y, ldy, ax);
+      if constexpr (CM) {
+        cmx.x = fmaxf(cmx.x, fabsf(a1[0].x * rsd));
+        cmx.y = fmaxf(cmx.y, fabsf(a1[0].y * rsd));
+        cmx.z = fmaxf(cmx.z, fabsf(a1[0].z * rsd));
+        cmx.w = fmaxf(cmx.w, fabsf(a1[0].w * rsd));
+      }
+      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      j += 8;
+      if (j < pcount) {
+        e_beg = sh.offs[slot][j];
+        e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
+        row_ctx(part * kLdsR + j);
+      }
+    }
+    if (CM && (fl & 2u)) {
+      // part done for this group: fold its maxima into the part's ring slot;
+      // the eighth group to arrive writes the part's row and clears the slot
+      // (a group can be at most a few parts ahead: every stage of a part is
+      // consumed by every wave before the ring moves NS stages on)
+      const uint32_t cs = part_ord % kLdsCmSlots;
+      atomicMax(&sh.cm[cs][4 * l + 0], __float_as_uint(cmx.x));
+      atomicMax(&sh.cm[cs][4 * l + 1], __float_as_uint(cmx.y));
+      atomicMax(&sh.cm[cs][4 * l + 2], __float_as_uint(cmx.z));
+      atomicMax(&sh.cm[cs][4 * l + 3], __float_as_uint(cmx.w));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint32_t arrived = 0;
+      if (l == 0) arrived = atomicAdd(&sh.cm_cnt[cs], 1u);
+      arrived = __shfl(arrived, lane & 32);
+      if (arrived == 7u) {
+        const uint4 m4 = *reinterpret_cast<const uint4*>(&sh.cm[cs][4 * l]);
+        *reinterpret_cast<uint4*>(ax.cm_out + (uint64_t)part * kLdsF + 4 * l) = m4;
+        *reinterpret_cast<uint4*>(&sh.cm[cs][4 * l]) = make_uint4(0u, 0u, 0u, 0u);
+        if (l == 0) sh.cm_cnt[cs] = 0u;
+      }
+    }
+    if (fl & 2u) ++part_ord;
+    // this wave is done reading the slot
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_fetch_add(&sh.freed[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
 static int pick_vec(uint32_t F, uint64_t ld1, uint64_t ld2, const void* p1, const void* p2) {
@@ -593,6 +896,21 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
   return NTS_OK;
 }
 
+// the LDS-staged gather (k_agg_lds) takes 128-float rows gathered by local id
+// (no row map, no host tier, no per-edge mask rows) in 16-byte vectors;
+// NTS_AGG_LDS=0 keeps k_spmm_gather (A/B)
+static bool agg_lds_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NTS_AGG_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+template <bool MAP, bool TIER, int MODE>
+static bool agg_lds_applies(int vec, uint32_t F) {
+  return !MAP && !TIER && MODE != kAggMask && vec == 4 && F == (uint32_t)kLdsF && agg_lds_enabled();
+}
+
 template <bool MAP, bool TIER = false, int MODE = kAggPlain, bool COOP = false>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
                          const float* w, const uint32_t* n_dev, uint32_t n_cap, const float* x,
@@ -612,6 +930,16 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
     vec = 4;
   const uint32_t nv = (F + vec - 1) / vec;
   const uint32_t last_valid = F - (nv - 1) * vec;
+  if (agg_lds_applies<MAP, TIER, MODE>(vec, F)) {
+    // 128-float rows: the LDS-staged gather (k_agg_lds)
+    const uint32_t parts_cap = ceil_div(n_cap, kLdsR);
+    const uint32_t grid = std::max(std::min(parts_cap, 512u), ceil_div(parts_cap, kLdsMaxParts));
+    if (grid == 0) return NTS_OK;
+    hipLaunchKernelGGL((k_agg_lds<MODE>), dim3(grid), dim3(kLdsThreads), 0, st, off, idx, w, n_dev,
+                       n_cap, x, ldx, y, ldy, ax);
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   const Shape s = pick_shape(nv);
   const uint32_t gpb = kAggThreads / s.lpd;
   // one destination per lane group: every row's dependent loads (offsets ->
@@ -676,6 +1004,8 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
 
 uint32_t nts_hip_csr_bwd_colmax_rows_per_part(uint32_t feature_size) {
   if (feature_size == 0) return 0;
+  // (the colmax gather always runs on float4 rows: vec 4)
+  if (agg_lds_applies<false, false, kAggColmax>(4, feature_size)) return (uint32_t)kLdsR;
   return (uint32_t)(kAggThreads / pick_shape((feature_size + 3) / 4).lpd);
 }
 
