@@ -1,8 +1,22 @@
 #!/bin/bash
-# Round-4 GPU round trip: suite + smoke + bench (scripts/gpu_check.sh), then the
-# wave-state PMC passes of the C2 bench kernels (scripts/pmc_stalls.sh).
+# Round-4 GPU round trip: aggregation kernel tests first (fast fail), suite +
+# smoke + bench (scripts/gpu_check.sh), an A/B bench of the register gather
+# (NTS_AGG_LDS=0), then the wave-state PMC passes (scripts/pmc_stalls.sh).
 set -o pipefail
 T=${1:-r04}
+O=gpurun_out/$T
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_hip_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -k "spmm or csr or agg" > $O/agg_tests.log 2>&1 || { echo "agg tests failed"; tail -30 $O/agg_tests.log; exit 1; }
+tail -2 $O/agg_tests.log
 bash scripts/gpu_check.sh $T || exit 1
-bash scripts/pmc_stalls.sh $T > gpurun_out/$T/stalls.txt 2>&1 || { tail -5 gpurun_out/$T/stalls.txt; exit 1; }
-cat gpurun_out/$T/stalls.txt
+B="--no-cpu-baseline --no-secondary-af --no-secondary-exact --epochs 0 --sampler-batches 0"
+NTS_AGG_LDS=0 timeout -k 10 300 python -u bench.py $B > $O/bench_reg.json 2> $O/bench_reg.err || { echo "bench reg failed"; tail -5 $O/bench_reg.err; exit 1; }
+timeout -k 10 300 python -u bench.py $B > $O/bench_lds.json 2> $O/bench_lds.err || { echo "bench lds failed"; tail -5 $O/bench_lds.err; exit 1; }
+python - <<PY
+import json
+for f in ("$O/bench_reg.json", "$O/bench_lds.json"):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f, round(d["ms_per_step"], 4), "ms/step", {k: (round(v["avg_launch_ms"]*1e3,1), round(v["frac"],3)) for k, v in d["roofline"].get("kernels", {}).items()}, d["config"].get("training_stream_alone"))
+PY
+bash scripts/pmc_stalls.sh $T > $O/stalls.txt 2>&1 || { tail -5 $O/stalls.txt; exit 1; }
+cat $O/stalls.txt
