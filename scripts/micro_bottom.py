@@ -1,8 +1,11 @@
 """Micro benchmark of the transform-first bottom layer's planar pair-table GEMMs
 at C2 size, alone on the GPU: k_h2_nn3 (H = X[src] W) and k_h2_tn4 (dW =
 X[src]^T dH, per-part column maxima given) — time per call and effective
-rate on the algorithmic bytes.  Timing probes: NTS_NN3_DIAG / NTS_TN4_DIAG.
+rate on the algorithmic bytes.  Timing probes (NTS_NN3_DIAG / NTS_TN4_DIAG)
+exist only in the probe build of the library:
 
+  make -C sample-based-gnn_amd/csrc probe
+  NTS_HIP_LIB=scripts/probe/lib/libnts_hip.so NTS_NN3_DIAG=1 python scripts/micro_bottom.py
   python scripts/micro_bottom.py [--iters 20]
 """
 import argparse
@@ -52,7 +55,7 @@ def main():
     R = h2.colmax_rows_per_part(a.N)
     nparts = (a.M + R - 1) // R
     pad = torch.zeros(nparts * R, a.N, device=dev)
-    pad[:a.M] = G.abs()
+    pad[:a.M] = G.abs() * rs[rows.long()][:, None]  # maxima of |rs[row] G|
     parts = pad.view(nparts, R, a.N).max(1).values.contiguous().view(torch.int32)
     Kp = Q.shape[1] // 2
     row_bytes = 4 * Kp
