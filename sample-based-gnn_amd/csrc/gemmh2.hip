@@ -123,7 +123,15 @@ __global__ __launch_bounds__(256) void k_h2_split_rows_planar(uint64_t R, uint32
     q[k] = (uint16_t)(w & 0xFFFFu);
     q[Kp + k] = (uint16_t)(w >> 16);
   }
-  if (lane == 0) rs[r] = ldexpf(1.f, -e);
+  if (lane == 0) {
+    const float sc = ldexpf(1.f, -e);
+    rs[r] = sc;
+    if (ldq >= 2 * (uint64_t)Kp + 8) {  // a row tail: the scale rides along with the row
+      const uint32_t b = __float_as_uint(sc);
+      q[2 * Kp] = (uint16_t)(b & 0xFFFFu);
+      q[2 * Kp + 1] = (uint16_t)(b >> 16);
+    }
+  }
 }
 
 // out[c] = max(out[c], max over rows k of |B[k, c]| * (rs ? rs[amap ? amap[k] : k] : 1)) as
@@ -1298,6 +1306,126 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 }
 
 
+// NN v4 (k_h2_nn4): k_h2_nn3 with FOUR LDS stages, three 16-row tiles in
+// flight per block instead of two (the 160 KB of LDS hold exactly four
+// 16 x 2560-byte stages): the row ids move to registers (lane t of each wave
+// holds its two rows of tile t, read with readlane) and the row scales ride in
+// the planar table's row tails (ldq = 1280 halves: the scale at half 2 Kp,
+// nts_hip_h2_split_rows_planar), so the stages take the whole LDS.  RP pieces
+// (three per row, six per wave and tile), planar rows swizzled by row as in
+// k_h2_nn3; the tail chunk (global chunk 2 Kp / 8) lands in LDS slot
+// 2Kp/8 ^ (row & 15).  No epilogue activation (the transform-first forward).
+template <int NKS>
+__global__ __launch_bounds__(512, 1) void k_h2_nn4(int M, int N, const char* __restrict__ Q,
+                                                  uint64_t ldq, int plane_bytes,
+                                                  const char* __restrict__ bimg, float* __restrict__ C,
+                                                  uint64_t ldc, H2Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char h2nn4[];
+  constexpr int kPitch = 2560, kStage = 16 * kPitch;
+  char* const sx = h2nn4;  // [4][16][2560]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, g = lane >> 4;
+  const int nb = blockIdx.y, n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int t0 = (int)((int64_t)blockIdx.x * T / gridDim.x);
+  const int t1 = (int)((int64_t)(blockIdx.x + 1) * T / gridDim.x);
+  const int nt = t1 - t0;  // <= 64 (host)
+  if (nt <= 0) return;
+  // lane t: the ids of rows 2 wv and 2 wv + 1 of tile t (this wave's DMA rows)
+  uint32_t id0 = 0, id1 = 0;
+  if (lane < nt) {
+    const int64_t r0 = min((int64_t)(t0 + lane) * 16 + 2 * wv, (int64_t)M - 1);
+    const int64_t r1 = min((int64_t)(t0 + lane) * 16 + 2 * wv + 1, (int64_t)M - 1);
+    id0 = ex.amap[r0];
+    id1 = ex.amap[r1];
+  }
+  f16x8 wf[kH2Nn3KS][2];
+#pragma unroll
+  for (int s = 0; s < kH2Nn3KS; ++s)
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      wf[s][p] = s < NKS ? *reinterpret_cast<const f16x8*>(
+                               bimg + ((size_t)s * gridDim.y + nb) * kH2Img + wv * 2 * kH2Frag +
+                               p * kH2Frag + 16 * lane)
+                         : f16x8{};
+  const float cs = ldexpf(1.f, -h2_exp(__uint_as_float(ex.cmax[n0 + 16 * wv + i])));
+  __syncthreads();  // (waits for every load above: the LDS DMA counts below start from zero)
+  const uint32_t lsx = (uint32_t)(uintptr_t)(lds_ptr_h)sx;
+  auto issue = [&](int r) {
+    const int rr = min(r, nt - 1);
+    const uint32_t ida = __builtin_amdgcn_readlane(id0, rr), idb = __builtin_amdgcn_readlane(id1, rr);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int row = q / 3, part = q - 3 * row;  // this wave's rows 2 wv + row
+      const int grow = 2 * wv + row;
+      const int c = 64 * part + lane;              // LDS slot (16-byte chunk) of the row
+      const int gc = c ^ (grow & 15);               // the global chunk it holds (tail included)
+      const char* src = Q + (uint64_t)(row ? idb : ida) * ldq + 16 * gc;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lsx + (rr & 3) * kStage + grow * kPitch + 1024 * part);
+      if (c < 160) glds16h(src, dst);
+    }
+  };
+  const int pch = plane_bytes / 16;  // chunks per plane
+  const int tail = 2 * pch;          // the row-scale chunk
+  issue(0);
+  issue(1);
+  issue(2);
+  for (int r = 0; r < nt; ++r) {
+    // tile r landed.  Younger VMEM ops (6 DMA pieces per tile, 4 stores per
+    // round): r = 0: tiles 1, 2; r = 1: tile 2, tile 3 + round 0's stores;
+    // r = 2: + tile 4 + round 1's stores; r >= 3: round r-3's stores, then
+    // (tile, stores) of rounds r-2 and r-1
+    if (r == 0) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (r == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (r == 2) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    raw_barrier_h();  // also: every wave is past tile r-1 (its stage takes tile r+3)
+    issue(r + 3);
+    const char* st = sx + (r & 3) * kStage;
+    const char* xs = st + i * kPitch;
+    // the row scales of this lane's output rows 4 g + v (row tails)
+    float rsr[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int row = 4 * g + v;
+      rsr[v] = *reinterpret_cast<const float*>(st + row * kPitch + 16 * (tail ^ row));
+    }
+    f32x4h acc = f32x4h{0.f, 0.f, 0.f, 0.f};
+    auto ld1 = [&](int s) { return *reinterpret_cast<const f16x8*>(xs + 16 * ((pch + 4 * s + g) ^ i)); };
+    auto ld0 = [&](int s) { return *reinterpret_cast<const f16x8*>(xs + 16 * ((4 * s + g) ^ i)); };
+    f16x8 b1[3], b0[3];  // fragments of steps s, s+1, s+2 (ring of three)
+    b1[0] = ld1(0);
+    b0[0] = ld0(0);
+    b1[1] = ld1(1);
+    b0[1] = ld0(1);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      if (s + 2 < NKS) {
+        b1[(s + 2) % 3] = ld1(s + 2);
+        b0[(s + 2) % 3] = ld0(s + 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads two steps ahead
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(b1[s % 3], wf[s][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0[s % 3], wf[s][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(b0[s % 3], wf[s][0], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // acc[v] = H[16 (t0 + r) + 4 g + v][n0 + 16 wv + i]
+    const int64_t r4 = (int64_t)(t0 + r) * 16 + 4 * g;
+    const uint32_t col = (uint32_t)(n0 + 16 * wv + i);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float o = acc[v] * cs * rsr[v];
+      // (four stores per round, as the counted waits assume: only the last
+      // tile of the last block can lose lanes, and no counted wait follows it)
+      if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+  raw_barrier_h();
+}
+
 // ---------------------------------------------------------------------------
 // NN with a DYNAMIC fp32 A of at most 128 columns (the aggregate-first layer
 // of the products / papers-shaped configs: ~140K aggregated rows x 100 ->
@@ -1821,7 +1949,7 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   // blocks, each with fewer tiles (large bottom frontiers, e.g. C5)
   const int tile_cap = (160 * 1024 - 3 * 16 * pitch) / (2 * 4 * 16);
   NTS_CHECK_ARG(tile_cap >= 1, "row pitch too large for the NN stage");
-  const int gx = std::max({1, std::min(256 / ncb, T), (T + tile_cap - 1) / tile_cap});
+  int gx = std::max({1, std::min(256 / ncb, T), (T + tile_cap - 1) / tile_cap});
   const int max_tiles = (T + gx - 1) / gx;
   const int lds = 3 * 16 * pitch + 2 * 4 * 16 * max_tiles;
   NTS_CHECK_ARG(lds <= 160 * 1024, "row-id stage");
@@ -1854,6 +1982,22 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     return e && e[0] == '1';
   }();
   const bool tr_ok = tr && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+  // four stages (k_h2_nn4) where the table rows carry their scales in a tail
+  // (ldq >= 1280 halves: 2560-byte rows) and the step count is compiled in;
+  // NTS_H2_NN4=0 keeps k_h2_nn3 (A/B)
+  static const bool nn4 = [] {
+    const char* e = getenv("NTS_H2_NN4");
+    return !(e && e[0] == '0');
+  }();
+  if (nn4 && !relu_dropout && a_rows && pitch == 2560 && ldq >= 1280 && (nsteps == 19 || nsteps == 20)) {
+    gx = std::max(gx, (T + 63) / 64);  // <= 64 tiles per block (lane-held row ids)
+    constexpr int lds4 = 4 * 16 * 2560;
+#define NTS_H2NN4(NK)                                                                                 do {                                                                                                  NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn4<NK>),                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds4));                 hipLaunchKernelGGL((k_h2_nn4<NK>), dim3(gx, ncb), dim3(512), lds4, ctx->stream, M, N,                                    reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), 2 * Kp, bimg, C, ldc, ex);   } while (0)
+    if (nsteps == 19) NTS_H2NN4(19); else NTS_H2NN4(20);
+#undef NTS_H2NN4
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   // compile-time step counts for the feature widths the driver meets
   // (C2: 602 -> Kp 608); NTS_NN3_DIAG=4 forces the runtime-count loop
   if (relu_dropout) {

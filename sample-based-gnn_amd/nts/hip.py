@@ -250,11 +250,16 @@ class HipContext:
                                              P.stride(0), ptr(rs)))
         return P, rs
 
-    def h2_split_rows_planar(self, X, pad_to=32):
-        """X [R, K] fp32 -> (Q int16 [R, 2 Kp]: y0 plane then y1 plane per row, rs [R])."""
+    def h2_split_rows_planar(self, X, pad_to=32, tail=False):
+        """X [R, K] fp32 -> (Q int16 [R, 2 Kp]: y0 plane then y1 plane per row, rs [R]).
+        tail: rows padded to 2560 bytes (Q a view of them) with the row scale in
+        the tail, as the driver builds the table (the four-stage forward GEMM)."""
         R, K = X.shape
         Kp = (K + pad_to - 1) // pad_to * pad_to
-        Q = torch.empty(R, 2 * Kp, dtype=torch.int16, device=X.device)
+        if tail and 4 * Kp + 8 <= 2560:
+            Q = torch.empty(R, 1280, dtype=torch.int16, device=X.device)[:, :2 * Kp]
+        else:
+            Q = torch.empty(R, 2 * Kp, dtype=torch.int16, device=X.device)
         rs = torch.empty(R, dtype=torch.float32, device=X.device)
         check(self.lib.nts_hip_h2_split_rows_planar(self.h, R, K, ptr(X), X.stride(0), Kp, ptr(Q),
                                                     Q.stride(0), ptr(rs)))

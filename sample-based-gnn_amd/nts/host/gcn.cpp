@@ -94,12 +94,16 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     pairs_->rs = torch::empty({V}, f32_opts(graph->device));
     pairs_->tn = cfg.pair_table >= 2;
     if (cfg.pair_table >= 3 && Kp <= 640 && Nh % 128 == 0) {
-      pairs_->Q = torch::empty({V, 2 * Kp},
-                               torch::TensorOptions().dtype(torch::kInt16).device(F.device()));
+      // rows padded to 2560 bytes where that leaves a tail for the row scale
+      // (the four-stage forward GEMM reads it with the row); Q is the [V, 2 Kp]
+      // view of the padded rows
+      const int64_t ldq = 4 * Kp + 8 <= 2560 ? 1280 : 2 * Kp;
+      pairs_->Q = torch::empty({V, ldq}, torch::TensorOptions().dtype(torch::kInt16).device(F.device()))
+                      .narrow(1, 0, 2 * Kp);
       hip_check(nts_hip_h2_split_rows_planar(cs->ctx(), (uint64_t)V, (uint32_t)K, F.data_ptr<float>(),
                                              (uint64_t)F.stride(0), (uint32_t)Kp,
                                              reinterpret_cast<uint16_t*>(pairs_->Q.data_ptr<int16_t>()),
-                                             (uint64_t)(2 * Kp), pairs_->rs.data_ptr<float>()),
+                                             (uint64_t)ldq, pairs_->rs.data_ptr<float>()),
                 "nts_hip_h2_split_rows_planar");
     } else {
       pairs_->P = torch::empty({V, Kp}, torch::TensorOptions().dtype(torch::kInt32).device(F.device()));

@@ -269,21 +269,32 @@ def test_h2p_gemm_tn_gather_given_column_maxima(ctx, M, N, K, gscale, anti):
     assert torch.equal(Ch, Ch2)
 
 
-@pytest.mark.parametrize("M,N,K,decades", [(228656, 128, 602, 0), (3001, 128, 602, 12),
-                                           (2500, 256, 100, 6), (17, 128, 64, 0)])
-def test_h2p_gemm_gather(ctx, M, N, K, decades):
-    """NN v3 on the planar table (W slices in registers, whole rows by LDS DMA)."""
+@pytest.mark.parametrize("M,N,K,decades,tail", [(228656, 128, 602, 0, False), (3001, 128, 602, 12, False),
+                                                (2500, 256, 100, 6, False), (17, 128, 64, 0, False),
+                                                (228656, 128, 602, 0, True), (3001, 128, 602, 12, True),
+                                                (17, 128, 602, 3, True), (5000, 256, 640, 6, True)])
+def test_h2p_gemm_gather(ctx, M, N, K, decades, tail):
+    """NN v3 on the planar table (W slices in registers, whole rows by LDS DMA);
+    tail: rows padded to 2560 bytes with the row scale in the tail — the
+    four-stage NN v4 (K 602 / 640: 19 / 20 steps), bit-identical to v3."""
     g = torch.Generator(device=DEV).manual_seed(M + K + N + 3)
     V = M + M // 3 + 11
     X = _table(V, K, g, decades)
     rows = torch.randperm(V, device=DEV, generator=g)[:M].to(torch.int32)
     rows[min(5, M - 1)] = 3
     W = torch.randn(K, N, device=DEV, generator=g) * 0.05
-    Q, rs = ctx.h2_split_rows_planar(X)
+    Q, rs = ctx.h2_split_rows_planar(X, tail=tail)
     C32 = torch.empty(M, N, device=DEV)
     Ch = torch.full((M, N), float("nan"), device=DEV)
     ctx.gemm_gather(X, rows, W, C32)
     ctx.gemm_h2p_gather(Q, rs, rows, W, Ch)
+    if tail:  # v4 (row scales from the tails) == v3 (row scales from rs), bit for bit
+        Q3, rs3 = ctx.h2_split_rows_planar(X)
+        assert torch.equal(Q3, Q) and torch.equal(rs3, rs)
+        C3 = torch.full((M, N), float("nan"), device=DEV)
+        ctx.gemm_h2p_gather(Q3, rs3, rows, W, C3)
+        torch.cuda.synchronize()
+        assert torch.equal(C3, Ch)
     Xg = X[rows.long()].double()
     ref = Xg @ W.double()
     scale = Xg.abs() @ W.double().abs() + 1e-300
