@@ -520,7 +520,7 @@ __global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float
 // 5.5-5.8 for register gathers (§ Indexed rows: gather into LDS).
 //
 // Block = 1 loader wave + 4 consumer waves (8 groups of 32 lanes, one float4
-// of the row per lane).  Output rows are cut into parts of kLdsR rows; block
+// of the row per lane).  Output rows are cut into parts of R <= kLdsR rows; block
 // b takes parts b, b + G, ... and streams each part's edges in stages of
 // kLdsSE rows through a ring of kLdsNS LDS slots:
 //   loader  per stage k: wait until the consumers freed slot k % NS (stage
@@ -602,7 +602,8 @@ template <int MODE>
 __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
-    const float* __restrict__ x, uint64_t ldx, float* __restrict__ y, uint64_t ldy, AggExtra ax) {
+    const float* __restrict__ x, uint64_t ldx, float* __restrict__ y, uint64_t ldy, uint32_t R,
+    AggExtra ax) {
   constexpr bool CM = MODE == kAggColmax;
   constexpr int EM = CM ? kAggPlain : MODE;
   __shared__ LdsAggShared sh;
@@ -610,8 +611,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t parts = (n + kLdsR - 1) / kLdsR;
-  const uint32_t parts_cap = (n_cap + kLdsR - 1) / kLdsR;
+  const uint32_t parts = (n + R - 1) / R;
+  const uint32_t parts_cap = (n_cap + R - 1) / R;
   const uint32_t my_parts = parts > b ? (parts - b + G - 1) / G : 0u;  // <= kLdsMaxParts (host)
   for (int i = tid; i < kLdsNS; i += kLdsThreads) {
     sh.full[i] = 0u;
@@ -633,8 +634,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     uint32_t pe0 = 0, pe1 = 0, nst = 0;
     if ((uint32_t)lane < my_parts) {
       const uint32_t p = b + (uint32_t)lane * G;
-      pe0 = off[(uint64_t)p * kLdsR];
-      pe1 = off[min((uint64_t)(p + 1) * kLdsR, (uint64_t)n)];
+      pe0 = off[(uint64_t)p * R];
+      pe1 = off[min((uint64_t)(p + 1) * R, (uint64_t)n)];
       nst = max(1u, (pe1 - pe0 + kLdsSE - 1) / kLdsSE);
     }
     uint32_t total = nst;
@@ -663,8 +664,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       const void* src = lane < 32 || !w ? (const void*)(idx + ec) : (const void*)(w + ec);
       glds4a(src, lstg + (uint32_t)(qq * (64 + kLdsR) * 4));
       const uint64_t p = b + i * G;
-      glds4a(off + min(p * kLdsR + lane, (uint64_t)n), lstg + (uint32_t)((qq * (64 + kLdsR) + 64) * 4));
-      glds4a(off + min(p * kLdsR + 64 + lane, (uint64_t)n),
+      glds4a(off + min(p * R + lane, (uint64_t)n), lstg + (uint32_t)((qq * (64 + kLdsR) + 64) * 4));
+      glds4a(off + min(p * R + 64 + lane, (uint64_t)n),
              lstg + (uint32_t)((qq * (64 + kLdsR) + 128) * 4));
     };
     const uint32_t lrows = lds_u32(&sh.rows[0][0][0]);
@@ -733,12 +734,12 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     const uint32_t sb = mt.y, se = mt.z, fl = mt.w & 255u;
     if (fl & 1u) {  // first stage of part mt.x: this group's first row
       part = mt.x;
-      pcount = min((uint32_t)kLdsR, n - part * kLdsR);
+      pcount = min(R, n - part * R);
       j = (uint32_t)g;
       if (j < pcount) {
         e_beg = sh.offs[slot][j];
         e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
-        row_ctx(part * kLdsR + j);
+        row_ctx(part * R + j);
       }
       acc = make_float4(0.f, 0.f, 0.f, 0.f);
       cmx = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -763,7 +764,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       }
       for (; e < hi; ++e) acc = VT<4>::madd(acc, srow[(e - sb) * 32], sw[e - sb]);
       if (e_end > se) break;  // continues in the next stage
-      const uint32_t d = part * kLdsR + j;
+      const uint32_t d = part * R + j;
       float4 a1[1] = {acc};
       if constexpr (MODE == kAggPostMask)
         a1[0] = make_float4(pm.x > 0.f ? a1[0].x * ax.scale : 0.f, pm.y > 0.f ? a1[0].y * ax.scale : 0.f,
@@ -780,7 +781,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       if (j < pcount) {
         e_beg = sh.offs[slot][j];
         e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
-        row_ctx(part * kLdsR + j);
+        row_ctx(part * R + j);
       }
     }
     if (CM && (fl & 2u)) {
@@ -932,11 +933,17 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
   const uint32_t last_valid = F - (nv - 1) * vec;
   if (agg_lds_applies<MAP, TIER, MODE>(vec, F)) {
     // 128-float rows: the LDS-staged gather (k_agg_lds)
-    const uint32_t parts_cap = ceil_div(n_cap, kLdsR);
-    const uint32_t grid = std::max(std::min(parts_cap, 512u), ceil_div(parts_cap, kLdsMaxParts));
+    // rows per part: kLdsR for the column maxima (the parts the TN GEMM reads,
+    // nts_hip_csr_bwd_colmax_rows_per_part), else smaller parts for small
+    // layers (~1,000 parts: enough blocks for the chip)
+    uint32_t R = (uint32_t)kLdsR;
+    if (MODE != kAggColmax)
+      while (R > 8 && (uint64_t)R * 1024 > n_cap) R /= 2;
+    const uint32_t parts_cap = ceil_div(n_cap, R);
+    const uint32_t grid = std::max(std::min(parts_cap, 1024u), ceil_div(parts_cap, kLdsMaxParts));
     if (grid == 0) return NTS_OK;
     hipLaunchKernelGGL((k_agg_lds<MODE>), dim3(grid), dim3(kLdsThreads), 0, st, off, idx, w, n_dev,
-                       n_cap, x, ldx, y, ldy, ax);
+                       n_cap, x, ldx, y, ldy, R, ax);
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
