@@ -510,7 +510,7 @@ __global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float
 }
 
 // ---------------------------------------------------------------------------
-// LDS-staged aggregation of 128-float rows (k_agg_lds): the same sums as
+// LDS-staged aggregation of 128- and 256-float rows (k_agg_lds): the same sums as
 // k_spmm_gather (per output row, its edges in edge order, acc + x * w with
 // contraction off — bit-identical for every row k_spmm_gather sums serially;
 // the long CSR rows it splits into pieces are summed serially here, i.e. in
@@ -520,7 +520,7 @@ __global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float
 // 5.5-5.8 for register gathers (§ Indexed rows: gather into LDS).
 //
 // Block = 1 loader wave + 4 consumer waves (8 groups of 32 lanes, one float4
-// of the row per lane).  Output rows are cut into parts of R <= kLdsR rows; block
+// of the row per lane, two for 256-float rows).  Output rows are cut into parts of R <= kLdsR rows; block
 // b takes parts b, b + G, ... and streams each part's edges in stages of
 // kLdsSE rows through a ring of kLdsNS LDS slots:
 //   loader  per stage k: wait until the consumers freed slot k % NS (stage
@@ -547,7 +547,7 @@ constexpr int kLdsCmSlots = 8;                   // colmax part ring
 constexpr int kLdsF = 128;                       // floats per row
 
 struct LdsAggShared {
-  float4 rows[kLdsNS][kLdsSE][32];               // 64 KB
+  float4 rows[kLdsNS][kLdsSE * 32];              // 64 KB: 16 KB per slot (32 or 16 rows)
   float w[kLdsNS][kLdsSE];
   uint32_t offs[kLdsNS][kLdsR];                  // the stage's part: off[pR + j]
   uint4 meta[kLdsNS];                            // {part, sb, se, flags | total << 8}
@@ -598,7 +598,7 @@ __device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
   asm volatile("" ::: "memory");
 }
 
-template <int MODE>
+template <int MODE, int NCH>
 __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
@@ -606,6 +606,9 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     AggExtra ax) {
   constexpr bool CM = MODE == kAggColmax;
   constexpr int EM = CM ? kAggPlain : MODE;
+  constexpr int RF4 = 32 * NCH;         // float4s per row (128 or 256 floats)
+  constexpr int SE = kLdsSE / NCH;      // rows per stage (16 KB)
+  static_assert(!CM || NCH == 1, "column maxima: 128-float rows");
   __shared__ LdsAggShared sh;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -636,7 +639,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       const uint32_t p = b + (uint32_t)lane * G;
       pe0 = off[(uint64_t)p * R];
       pe1 = off[min((uint64_t)(p + 1) * R, (uint64_t)n)];
-      nst = max(1u, (pe1 - pe0 + kLdsSE - 1) / kLdsSE);
+      nst = max(1u, (pe1 - pe0 + SE - 1) / SE);
     }
     uint32_t total = nst;
 #pragma unroll
@@ -652,7 +655,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       const uint32_t e0 = __shfl(pe0, (int)i), e1 = __shfl(pe1, (int)i), ns = __shfl(nst, (int)i);
       const uint32_t st = cur_i < my_parts ? cur_s : ns - 1;
       const int qq = (int)(q % 3);
-      const uint32_t sb = e0 + st * kLdsSE, se = min(sb + kLdsSE, e1);
+      const uint32_t sb = e0 + st * SE, se = min(sb + SE, e1);
       if (lane == 0)  // (read back after this entry's loads landed: ordered by the vmcnt wait)
         sh.stgd[qq] = make_uint4(i, sb, se, (st == 0 ? 1u : 0u) | (st + 1 == ns ? 2u : 0u));
       if (cur_i < my_parts && ++cur_s == ns) {
@@ -668,7 +671,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       glds4a(off + min(p * R + 64 + lane, (uint64_t)n),
              lstg + (uint32_t)((qq * (64 + kLdsR) + 128) * 4));
     };
-    const uint32_t lrows = lds_u32(&sh.rows[0][0][0]);
+    const uint32_t lrows = lds_u32(&sh.rows[0][0]);
     load_ids(0);
     load_ids(1);
     for (uint32_t k = 0; k < total; ++k) {
@@ -695,16 +698,17 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
         sh.pend[slot] = pend;
       }
       load_ids(k + 2);  // staging entry (k + 2) % 3 held stage k - 1: copied out already
-      // 16 row DMAs: instruction j moves rows 2j (lanes 0-31) and 2j + 1
+      // 16 row DMAs of 1 KB: instruction jj moves float4s 64 jj + lane of the
+      // stage (rows 2 jj and 2 jj + 1 of 128 floats, or row jj of 256)
       const uint32_t nrow = se - sb;
       const uint32_t id0 = __shfl(id, 0);
 #pragma unroll
-      for (int jj = 0; jj < kLdsSE / 2; ++jj) {
-        const int r = 2 * jj + (lane >> 5);
+      for (int jj = 0; jj < 16; ++jj) {
+        const int fl4 = 64 * jj + lane, r = fl4 / RF4, c16 = fl4 % RF4;
         uint32_t rid = __shfl(id, r);
         rid = (uint32_t)r < nrow ? rid : (nrow ? id0 : 0u);
-        const char* src = reinterpret_cast<const char*>(x + (uint64_t)rid * ldx) + 16 * (lane & 31);
-        glds16a(src, lrows + (uint32_t)((slot * kLdsSE + 2 * jj) * kLdsRowB));
+        const char* src = reinterpret_cast<const char*>(x + (uint64_t)rid * ldx) + 16 * c16;
+        glds16a(src, lrows + (uint32_t)(slot * kLdsSE * kLdsRowB + 1024 * jj));
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -714,15 +718,22 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
 
   // ---------------- consumer waves: 8 groups of 32 lanes ----------------
   const int g = 2 * wv + (lane >> 5), l = lane & 31;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc[NCH];
   float4 cmx = make_float4(0.f, 0.f, 0.f, 0.f);
   uint32_t j = 0, pcount = 0;                    // local row of the part, rows in the part
   uint32_t e_beg = 0, e_end = 0, part = 0, part_ord = 0;
-  float4 pm = make_float4(0.f, 0.f, 0.f, 0.f);  // kAggPostMask: the row's mask
+  float4 pm[NCH];                                // kAggPostMask: the row's mask
   float rsd = 1.f;                               // kAggColmax: the row's scale
+  auto zero = [&]() {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  zero();
   auto row_ctx = [&](uint32_t d) {  // per-row operands known before its edges
     if constexpr (MODE == kAggPostMask)
-      pm = *reinterpret_cast<const float4*>(ax.mx + (uint64_t)d * ax.ldm + 4 * l);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+        pm[c] = *reinterpret_cast<const float4*>(ax.mx + (uint64_t)d * ax.ldm + 4 * (l + 32 * c));
     if constexpr (CM) rsd = ax.cm_rs ? ax.cm_rs[ax.cm_map ? ax.cm_map[d] : d] : 1.f;
   };
   uint32_t total = 1;
@@ -741,10 +752,10 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
         e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
         row_ctx(part * R + j);
       }
-      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      zero();
       cmx = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float4* srow = &sh.rows[slot][0][l];
+    const float4* srow = &sh.rows[slot][l];
     const float* sw = sh.w[slot];
     // rows whose edges start in this stage (a row without edges at the
     // stage's end included): sum their edges here, store the complete ones
@@ -752,31 +763,37 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       uint32_t e = max(e_beg, sb);
       const uint32_t hi = min(e_end, se);
       for (; e + 4 <= hi; e += 4) {  // four rows of x in flight
-        float4 xv[4];
+        float4 xv[4][NCH];
         float wv4[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          xv[u] = srow[(e + u - sb) * 32];
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) xv[u][c] = srow[(e + u - sb) * RF4 + 32 * c];
           wv4[u] = sw[e + u - sb];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) acc = VT<4>::madd(acc, xv[u], wv4[u]);
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) acc[c] = VT<4>::madd(acc[c], xv[u][c], wv4[u]);
       }
-      for (; e < hi; ++e) acc = VT<4>::madd(acc, srow[(e - sb) * 32], sw[e - sb]);
+      for (; e < hi; ++e)
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) acc[c] = VT<4>::madd(acc[c], srow[(e - sb) * RF4 + 32 * c], sw[e - sb]);
       if (e_end > se) break;  // continues in the next stage
       const uint32_t d = part * R + j;
-      float4 a1[1] = {acc};
       if constexpr (MODE == kAggPostMask)
-        a1[0] = make_float4(pm.x > 0.f ? a1[0].x * ax.scale : 0.f, pm.y > 0.f ? a1[0].y * ax.scale : 0.f,
-                            pm.z > 0.f ? a1[0].z * ax.scale : 0.f, pm.w > 0.f ? a1[0].w * ax.scale : 0.f);
-      store_row<4, 32, 1, MODE == kAggPostMask ? kAggPlain : EM>(a1, d, 0, l, 32, 4, y, ldy, ax);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+          acc[c] = make_float4(pm[c].x > 0.f ? acc[c].x * ax.scale : 0.f, pm[c].y > 0.f ? acc[c].y * ax.scale : 0.f,
+                               pm[c].z > 0.f ? acc[c].z * ax.scale : 0.f, pm[c].w > 0.f ? acc[c].w * ax.scale : 0.f);
+      store_row<4, 32, NCH, MODE == kAggPostMask ? kAggPlain : EM>(acc, d, 0, l, RF4, 4, y, ldy, ax);
       if constexpr (CM) {
-        cmx.x = fmaxf(cmx.x, fabsf(a1[0].x * rsd));
-        cmx.y = fmaxf(cmx.y, fabsf(a1[0].y * rsd));
-        cmx.z = fmaxf(cmx.z, fabsf(a1[0].z * rsd));
-        cmx.w = fmaxf(cmx.w, fabsf(a1[0].w * rsd));
+        cmx.x = fmaxf(cmx.x, fabsf(acc[0].x * rsd));
+        cmx.y = fmaxf(cmx.y, fabsf(acc[0].y * rsd));
+        cmx.z = fmaxf(cmx.z, fabsf(acc[0].z * rsd));
+        cmx.w = fmaxf(cmx.w, fabsf(acc[0].w * rsd));
       }
-      acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      zero();
       j += 8;
       if (j < pcount) {
         e_beg = sh.offs[slot][j];
@@ -909,7 +926,8 @@ static bool agg_lds_enabled() {
 }
 template <bool MAP, bool TIER, int MODE>
 static bool agg_lds_applies(int vec, uint32_t F) {
-  return !MAP && !TIER && MODE != kAggMask && vec == 4 && F == (uint32_t)kLdsF && agg_lds_enabled();
+  return !MAP && !TIER && MODE != kAggMask && vec == 4 && agg_lds_enabled() &&
+         (F == (uint32_t)kLdsF || (F == 2u * kLdsF && MODE != kAggColmax));
 }
 
 template <bool MAP, bool TIER = false, int MODE = kAggPlain, bool COOP = false>
@@ -942,8 +960,15 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
     const uint32_t parts_cap = ceil_div(n_cap, R);
     const uint32_t grid = std::max(std::min(parts_cap, 1024u), ceil_div(parts_cap, kLdsMaxParts));
     if (grid == 0) return NTS_OK;
-    hipLaunchKernelGGL((k_agg_lds<MODE>), dim3(grid), dim3(kLdsThreads), 0, st, off, idx, w, n_dev,
-                       n_cap, x, ldx, y, ldy, R, ax);
+    if constexpr (MODE == kAggColmax)
+      hipLaunchKernelGGL((k_agg_lds<MODE, 1>), dim3(grid), dim3(kLdsThreads), 0, st, off, idx, w, n_dev,
+                         n_cap, x, ldx, y, ldy, R, ax);
+    else if (F == (uint32_t)kLdsF)
+      hipLaunchKernelGGL((k_agg_lds<MODE, 1>), dim3(grid), dim3(kLdsThreads), 0, st, off, idx, w, n_dev,
+                         n_cap, x, ldx, y, ldy, R, ax);
+    else
+      hipLaunchKernelGGL((k_agg_lds<MODE, 2>), dim3(grid), dim3(kLdsThreads), 0, st, off, idx, w, n_dev,
+                         n_cap, x, ldx, y, ldy, R, ax);
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }

@@ -329,7 +329,7 @@ def _assert_csr_rows(got, ref, row_offset):
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("F", [16, 41, 128, 602])
+@pytest.mark.parametrize("F", [16, 41, 128, 256, 602])
 def test_spmm_backward_csr_bitexact_and_atomic(hip, cora, F):
     V, src, dst = cora
     col, rows = orc.build_csc(V, src, dst)
@@ -502,7 +502,7 @@ def test_spmm_csr_bwd_masked(hip, cora, F):
     assert torch.isnan(gin[s:]).all()
 
 
-@pytest.mark.parametrize("F", [1, 41, 128, 602])
+@pytest.mark.parametrize("F", [1, 41, 128, 256, 602])
 def test_spmm_csr_bwd_postmask(hip, cora, F):
     """The graph-op backward with the next layer's activation backward fused on
     its output rows == the CSR backward followed by act_backward, bit for bit."""
@@ -918,7 +918,7 @@ def test_gat_layer_matches_torch(hip, cora, F):
     assert torch.equal(dH, dH2)
 
 
-@pytest.mark.parametrize("F,mask", [(128, False), (128, True), (602, False), (7, True)])
+@pytest.mark.parametrize("F,mask", [(128, False), (128, True), (256, False), (602, False), (7, True)])
 def test_csr_bwd_long_rows_cooperative(hip, F, mask):
     """A hub sampled by thousands of destinations gives one CSR row of thousands
     of edges (the power-law case): summed by the whole workgroup in GPB in-order
