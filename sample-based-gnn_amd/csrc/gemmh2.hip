@@ -295,6 +295,19 @@ __device__ __forceinline__ void raw_barrier_h() {
   asm volatile("" ::: "memory");
 }
 
+// CUs the one-block-per-CU pair-table GEMMs spread over (k_h2_nn3/4 row
+// tiles, k_h2_tn4 k-chunks, k_h2_nnd tiles): 256, or NTS_GEMM_CUS (A/B: a grid
+// below the CU count leaves CUs to the pipelined sampler's blocks instead of
+// waiting for them)
+static int gemm_cus() {
+  static const int n = [] {
+    const char* e = getenv("NTS_GEMM_CUS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v <= 256 ? v : 256;
+  }();
+  return n;
+}
+
 struct H2Extra {
   uint32_t keep_threshold = 0;  // EPI: relu + inverted dropout (common.hpp dropout_*)
   float scale = 1.f;
@@ -1840,7 +1853,7 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
   const int nnb = N / 128;
   const int pitch = (4 * Kp + 511) / 512 * 512;
   const int ksteps = (K + 15) / 16;
-  int splits = std::max(1, std::min(256 / nnb, ksteps / 8));
+  int splits = std::max(1, std::min(gemm_cus() / nnb, ksteps / 8));
   int kchunk = ((ksteps + splits - 1) / splits) * 16;
   if (kchunk > 960) kchunk = 960;  // the chunk's ids + row scales in LDS (8 B per row)
   splits = (K + kchunk - 1) / kchunk;
@@ -1949,7 +1962,7 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   // blocks, each with fewer tiles (large bottom frontiers, e.g. C5)
   const int tile_cap = (160 * 1024 - 3 * 16 * pitch) / (2 * 4 * 16);
   NTS_CHECK_ARG(tile_cap >= 1, "row pitch too large for the NN stage");
-  int gx = std::max({1, std::min(256 / ncb, T), (T + tile_cap - 1) / tile_cap});
+  int gx = std::max({1, std::min(gemm_cus() / ncb, T), (T + tile_cap - 1) / tile_cap});
   const int max_tiles = (T + gx - 1) / gx;
   const int lds = 3 * 16 * pitch + 2 * 4 * 16 * max_tiles;
   NTS_CHECK_ARG(lds <= 160 * 1024, "row-id stage");
@@ -2056,7 +2069,7 @@ extern "C" int nts_hip_gemm_h2d_act(nts_hip_ctx* ctx, int relu_dropout, int M, i
   ex.seed = seed;
   ex.offset = offset;
   const int T = (M + kH2dTM - 1) / kH2dTM;
-  const dim3 grid(std::max(1, std::min(256, T)));  // one block per CU (~156 VGPRs)
+  const dim3 grid(std::max(1, std::min(gemm_cus(), T)));  // one block per CU (~156 VGPRs)
 #define NTS_H2D(NK, NT, E, QO)                                                                   \
   hipLaunchKernelGGL((k_h2_nnd<NK, NT, E, QO>), grid, dim3(512), 0, ctx->stream, M, K, A, lda,   \
                      bimg, ncb, cmax, C, ldc, Q, ldq, rs, ex)

@@ -20,9 +20,10 @@ B="--no-cpu-baseline --no-secondary-af --no-secondary-exact --epochs 0 --sampler
 NTS_AGG_LDS=0 timeout -k 10 300 python -u bench.py $B > $O/bench_reg.json 2> $O/bench_reg.err || { echo "bench reg failed"; tail -5 $O/bench_reg.err; exit 1; }
 timeout -k 10 300 python -u bench.py $B > $O/bench_lds.json 2> $O/bench_lds.err || { echo "bench lds failed"; tail -5 $O/bench_lds.err; exit 1; }
 NTS_H2_NN4=1 timeout -k 10 300 python -u bench.py $B > $O/bench_nn4.json 2> $O/bench_nn4.err || { echo "bench nn4 failed"; tail -5 $O/bench_nn4.err; exit 1; }
+NTS_GEMM_CUS=232 timeout -k 10 300 python -u bench.py $B > $O/bench_cus232.json 2> $O/bench_cus232.err || { echo "bench cus failed"; tail -5 $O/bench_cus232.err; exit 1; }
 python - <<PY
 import json
-for f in ("$O/bench.json", "$O/bench_reg.json", "$O/bench_lds.json", "$O/bench_nn4.json"):
+for f in ("$O/bench.json", "$O/bench_reg.json", "$O/bench_lds.json", "$O/bench_nn4.json", "$O/bench_cus232.json"):
     d = json.loads(open(f).read().strip().splitlines()[-1])
     print(f, round(d["ms_per_step"], 4), "ms/step", {k: (round(v["avg_launch_ms"]*1e3,1), round(v["frac"],3)) for k, v in d["roofline"].get("kernels", {}).items()}, d["config"].get("training_stream_alone"))
 PY
