@@ -82,7 +82,8 @@ __device__ __forceinline__ T block_prefix_of(const T* partials, uint32_t count, 
 // kernel, which stalls for tens of microseconds behind a concurrent stream's
 // large kernels).  Otherwise partials[blockIdx.x] is already the offset.
 // CNT: the input is the sampler's counts (k_count_reduce) and out[n] is also
-// e_size: sizes[1] = min(out[n], e_cap), overflow flagged in sizes[3].
+// e_size: sizes[1] = out[n], or past e_cap the offset of the first dst whose
+// edges do not fit (overflow flagged in sizes[3]).
 template <typename T, bool DIRECT, bool CNT = false>
 __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
                                                            const uint32_t* n_dev,
@@ -119,6 +120,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     tile[pad_idx(t * kScanItems + k)] = run;
+    // CNT: the item whose edges cross the capacity truncates the layer at
+    // its first edge (never inside a destination: the selection skips a dst
+    // that does not fit whole, so no edge array holds unwritten slots)
+    if (CNT && run <= (T)e_cap && run + v[k] > (T)e_cap) sizes[1] = (uint32_t)run;
     run += v[k];
   }
   __syncthreads();
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_down(const T* in, T* out,
     if (i <= n) out[i] = tile[pad_idx(j)];
     if (CNT && i == n) {
       const T e = tile[pad_idx(j)];
-      sizes[1] = (uint32_t)min(e, (T)e_cap);
+      if (e <= (T)e_cap) sizes[1] = (uint32_t)e;
       if (e > (T)e_cap) atomicOr(&sizes[3], 1u);
     }
   }
@@ -331,6 +336,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     tile[pad_idx(t * kScanItems + k)] = run;
+    // COUNT: the dst whose edges cross the edge capacity truncates the layer
+    // at its first edge — the selection skips a dst that does not fit whole,
+    // so e_size never covers unwritten edge slots (their ids are garbage)
+    if (COUNT && run <= ca.e_cap && run + v[k] > ca.e_cap) ca.sizes[1] = run;
     run += v[k];
   }
   __syncthreads();
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
       // the overflow flag has ONE writer, this item's thread, for both
       // capacities: a store from another workgroup could land after it
       const uint32_t e = tile[pad_idx(j)];
-      ca.sizes[1] = min(e, ca.e_cap);
+      if (e <= ca.e_cap) ca.sizes[1] = e;  // (else the crossing dst above wrote it)
       ca.sizes[3] = (v_req > ca.v_cap ? 1u : 0u) | (e > ca.e_cap ? 1u : 0u);
     }
   }
