@@ -677,14 +677,21 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     for (uint32_t k = 0; k < total; ++k) {
       const uint32_t slot = k % kLdsNS;
       const int qq = (int)(k % 3);
+      // per iteration j the loader issues ids(j + 2) (3 loads) then rows(j)
+      // (16 LDS DMAs).  Stage k-3 is marked full as soon as its rows landed
+      // (younger: ids(k), rows(k-2), ids(k+1), rows(k-1) = 38 loads) — before
+      // waiting for the consumers, so that they never wait on the loader's
+      // own wait for a free slot
+      if (k >= 3) {
+        asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+        lds_st(&sh.full[(k - 3) % kLdsNS], k - 2);
+      }
       if (k >= (uint32_t)kLdsNS) lds_wait_ge(&sh.freed[slot], (uint32_t)kLdsCons * (k / kLdsNS));
       // staging of stage k landed.  Younger: k = 0: ids(1); k = 1: ids(2),
-      // rows(0); k >= 2: rows(k-2), ids(k+1), rows(k-1) — 3 + 16 + 3 + 16
-      // loads; so the rows of stage k-3 (older than ids(k)) have landed too
+      // rows(0); k >= 2: rows(k-2), ids(k+1), rows(k-1)
       if (k == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       else if (k == 1) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(35)" ::: "memory");
-      if (k >= 3) lds_st(&sh.full[(k - 3) % kLdsNS], k - 2);
       // staging -> the slot (weights, offsets, descriptor)
       const uint32_t id = sh.stg[qq][lane & 31];
       const uint4 dsc = sh.stgd[qq];
@@ -722,19 +729,27 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
   float4 cmx = make_float4(0.f, 0.f, 0.f, 0.f);
   uint32_t j = 0, pcount = 0;                    // local row of the part, rows in the part
   uint32_t e_beg = 0, e_end = 0, part = 0, part_ord = 0;
-  float4 pm[NCH];                                // kAggPostMask: the row's mask
-  float rsd = 1.f;                               // kAggColmax: the row's scale
+  // per-row operands known before the row's edges (kAggPostMask: the row's
+  // mask, kAggColmax: its scale), loaded one row ahead: a global load used
+  // right away would make the compiler wait for every older store as well
+  float4 pm[NCH], pm_n[NCH];
+  float rsd = 1.f, rsd_n = 1.f;
   auto zero = [&]() {
 #pragma unroll
     for (int c = 0; c < NCH; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   };
   zero();
-  auto row_ctx = [&](uint32_t d) {  // per-row operands known before its edges
+  auto row_ctx = [&](uint32_t d) {  // -> the "next" registers
     if constexpr (MODE == kAggPostMask)
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
-        pm[c] = *reinterpret_cast<const float4*>(ax.mx + (uint64_t)d * ax.ldm + 4 * (l + 32 * c));
-    if constexpr (CM) rsd = ax.cm_rs ? ax.cm_rs[ax.cm_map ? ax.cm_map[d] : d] : 1.f;
+        pm_n[c] = *reinterpret_cast<const float4*>(ax.mx + (uint64_t)d * ax.ldm + 4 * (l + 32 * c));
+    if constexpr (CM) rsd_n = ax.cm_rs ? ax.cm_rs[ax.cm_map ? ax.cm_map[d] : d] : 1.f;
+  };
+  auto take_ctx = [&]() {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) pm[c] = pm_n[c];
+    rsd = rsd_n;
   };
   uint32_t total = 1;
   for (uint32_t k = 0; k < total; ++k) {
@@ -751,6 +766,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
         e_beg = sh.offs[slot][j];
         e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
         row_ctx(part * R + j);
+        take_ctx();
+        if (j + 8 < pcount) row_ctx(part * R + j + 8);
       }
       zero();
       cmx = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -762,17 +779,18 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     while (j < pcount && (e_beg < se || (e_beg == e_end && e_beg <= se))) {
       uint32_t e = max(e_beg, sb);
       const uint32_t hi = min(e_end, se);
-      for (; e + 4 <= hi; e += 4) {  // four rows of x in flight
-        float4 xv[4][NCH];
-        float wv4[4];
+      constexpr int UL = 8 / NCH;  // rows of x read ahead of their adds
+      for (; e + UL <= hi; e += UL) {
+        float4 xv[UL][NCH];
+        float wv4[UL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < UL; ++u) {
 #pragma unroll
           for (int c = 0; c < NCH; ++c) xv[u][c] = srow[(e + u - sb) * RF4 + 32 * c];
           wv4[u] = sw[e + u - sb];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < UL; ++u)
 #pragma unroll
           for (int c = 0; c < NCH; ++c) acc[c] = VT<4>::madd(acc[c], xv[u][c], wv4[u]);
       }
@@ -798,7 +816,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       if (j < pcount) {
         e_beg = sh.offs[slot][j];
         e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
-        row_ctx(part * R + j);
+        take_ctx();
+        if (j + 8 < pcount) row_ctx(part * R + j + 8);
       }
     }
     if (CM && (fl & 2u)) {
@@ -916,11 +935,11 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
 
 // the LDS-staged gather (k_agg_lds) takes 128-float rows gathered by local id
 // (no row map, no host tier, no per-edge mask rows) in 16-byte vectors;
-// NTS_AGG_LDS=0 keeps k_spmm_gather (A/B)
+// opt-in (NTS_AGG_LDS=1) until measured faster than k_spmm_gather
 static bool agg_lds_enabled() {
   static const bool on = [] {
     const char* e = getenv("NTS_AGG_LDS");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

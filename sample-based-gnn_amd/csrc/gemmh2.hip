@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 
 // NN v4 (k_h2_nn4): k_h2_nn3 with FOUR LDS stages, three 16-row tiles in
 // flight per block instead of two (the 160 KB of LDS hold exactly four
-// 16 x 2560-byte stages): the row ids move to registers (lane t of each wave
+// 16 x 2560-byte stages; Kp = 608, 19 k-steps): the row ids move to registers (lane t of each wave
 // holds its two rows of tile t, read with readlane) and the row scales ride in
 // the planar table's row tails (ldq = 1280 halves: the scale at half 2 Kp,
 // nts_hip_h2_split_rows_planar), so the stages take the whole LDS.  RP pieces
@@ -2002,11 +2002,11 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
     const char* e = getenv("NTS_H2_NN4");
     return e && e[0] == '1';
   }();
-  if (nn4 && !relu_dropout && a_rows && pitch == 2560 && ldq >= 1280 && (nsteps == 19 || nsteps == 20)) {
+  if (nn4 && !relu_dropout && a_rows && pitch == 2560 && ldq >= 2 * (uint64_t)Kp + 8 && nsteps == 19) {
     gx = std::max(gx, (T + 63) / 64);  // <= 64 tiles per block (lane-held row ids)
     constexpr int lds4 = 4 * 16 * 2560;
 #define NTS_H2NN4(NK)                                                                                 do {                                                                                                  NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn4<NK>),                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds4));                 hipLaunchKernelGGL((k_h2_nn4<NK>), dim3(gx, ncb), dim3(512), lds4, ctx->stream, M, N,                                    reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), 2 * Kp, bimg, C, ldc, ex);   } while (0)
-    if (nsteps == 19) NTS_H2NN4(19); else NTS_H2NN4(20);
+    NTS_H2NN4(19);
 #undef NTS_H2NN4
     NTS_LAUNCH_CHECK();
     return NTS_OK;
