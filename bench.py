@@ -441,6 +441,7 @@ def main():
         for _ in range(args.warmup):
             step()
         drv.synchronize()
+        drv.reset_stats()
         barrier()
         ta = time.perf_counter()
         for _ in range(args.steps):
@@ -448,9 +449,14 @@ def main():
         drv.synchronize()
         barrier()
         el_alone = max_over_ranks(time.perf_counter() - ta)
+        prof_alone = drv.resolve_profile()
         drv.set_diag_reuse_sample(False)
         alone = {"ms_per_step": el_alone / args.steps * 1e3, "steps": args.steps,
                  "interference_ms_per_step": (elapsed - el_alone) / args.steps * 1e3,
+                 "kernel_avg_us": {k: {"alone": round(v["ms"] / v["calls"] * 1e3, 1),
+                                       "pipelined": round(prof[k]["ms"] / prof[k]["calls"] * 1e3, 1)}
+                                   for k, v in prof_alone.items()
+                                   if v["calls"] and k in prof and prof[k]["calls"]},
                  "note": "diagnostic, not a throughput: one sampled batch reused every step, "
                          "so the training stream runs without the pipelined sampler beside it"}
 

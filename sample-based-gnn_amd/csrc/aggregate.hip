@@ -519,19 +519,21 @@ __global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float
 // the gather form MI355X_MICROARCH.md measures at 7.4-8.6 TB/s against
 // 5.5-5.8 for register gathers (§ Indexed rows: gather into LDS).
 //
-// Block = 1 loader wave + 4 consumer waves (8 groups of 32 lanes, one float4
-// of the row per lane, two for 256-float rows).  Output rows are cut into parts of R <= kLdsR rows; block
-// b takes parts b, b + G, ... and streams each part's edges in stages of
-// kLdsSE rows through a ring of kLdsNS LDS slots:
-//   loader  per stage k: wait until the consumers freed slot k % NS (stage
-//           k - NS done), put the stage's weights, its part's offsets and its
-//           descriptor into the slot (loaded two stages ahead), issue the 16
-//           row DMAs, then (counted vmcnt, in-order completion) mark stage
-//           k - 3 full.  Only the loader issues vector-memory loads, so its
-//           vmcnt counts are static; three stages stay in flight.
-//   groups  group g owns rows pR + g + 8 j of part p and sums each row's
-//           edges that fall in the stage, stores a row when its last edge is
-//           in, and carries a row that continues into the next stage.
+// Block = an id loader wave, a row loader wave and 4 consumer waves (8 groups
+// of 32 lanes, one float4 of the row per lane, two for 256-float rows).
+// Output rows are cut into parts of R <= kLdsR rows; block b takes parts b,
+// b + G, ... and streams each part's edges in 16 KB stages (kLdsSE rows of 128
+// floats, or 16 of 256) through a ring of kLdsNS LDS slots:
+//   id loader   per stage: the stage's row ids, weights and its part's
+//               offsets by LDS DMA into an id ring, 8 stages ahead (the id
+//               loads' latency never sits in front of a row DMA)
+//   row loader  per stage: once its ids are in and its slot is free (stage
+//               k - NS consumed), 16 row DMAs; stage k-2 is marked full when
+//               it lands — three stages in flight.  Each loader issues only
+//               its own LDS DMAs, so its vmcnt counts are static.
+//   groups      group g owns rows pR + g + 8 j of part p, sums each row's
+//               edges that fall in the stage, stores a row when its last edge
+//               is in, and carries a row that continues into the next stage.
 // Output modes as k_spmm_gather's: plain, relu/dropout epilogue (kAggAct),
 // post-mask (kAggPostMask), column maxima per part (kAggColmax; part p's
 // maxima row = max over its rows of |rs(row) y|, the TN GEMM's operand
@@ -540,7 +542,9 @@ constexpr int kLdsR = 128;                       // output rows per part
 constexpr int kLdsSE = 32;                       // edges (rows of x) per stage
 constexpr int kLdsNS = 4;                        // ring slots
 constexpr int kLdsCons = 4;                      // consumer waves
-constexpr int kLdsThreads = kWave * (kLdsCons + 1);
+constexpr int kLdsThreads = kWave * (kLdsCons + 2);  // + row loader + id loader
+constexpr int kLdsID = 12;                       // id-ring entries (stages ahead of the rows)
+constexpr int kLdsIdAhead = 8;                   // id loads in flight (3 LDS DMAs each)
 constexpr int kLdsRowB = 512;                    // 128 floats
 constexpr int kLdsMaxParts = 64;                 // parts per block (lane-held bounds)
 constexpr int kLdsCmSlots = 8;                   // colmax part ring
@@ -548,15 +552,14 @@ constexpr int kLdsF = 128;                       // floats per row
 
 struct LdsAggShared {
   float4 rows[kLdsNS][kLdsSE * 32];              // 64 KB: 16 KB per slot (32 or 16 rows)
-  float w[kLdsNS][kLdsSE];
-  uint32_t offs[kLdsNS][kLdsR];                  // the stage's part: off[pR + j]
-  uint4 meta[kLdsNS];                            // {part, sb, se, flags | total << 8}
-  uint32_t pend[kLdsNS];                         // the part's edge end off[min(pR + R, n)]
-  uint32_t full[kLdsNS], freed[kLdsNS];
-  // loader staging, three stages ahead of the ring: [0, 32) row ids, [32, 64)
-  // weights, then the part's offsets 0..127 (global_load_lds_dword)
-  uint32_t stg[3][64 + kLdsR];
-  uint4 stgd[3];                                 // staged descriptors {part i, sb, se, flags}
+  uint32_t full[kLdsNS], freed[kLdsNS];          // row slots: stages landed / waves done
+  // id ring (kLdsID stages, filled kLdsIdAhead stages ahead by the id loader's
+  // LDS DMAs): per stage [0, 32) row ids, [32, 64) weights, [64, 192) the
+  // part's offsets off[pR + j]; its descriptor and the part's edge end
+  uint32_t ids[kLdsID][64 + kLdsR];
+  uint4 meta[kLdsID];                            // {part, sb, se, flags | total << 8}
+  uint32_t pend[kLdsID];                         // off[min(pR + R, n)]
+  uint32_t ids_ready;                            // stages whose id entries landed
   uint32_t cm[kLdsCmSlots][kLdsF];               // kAggColmax: part maxima ring
   uint32_t cm_cnt[kLdsCmSlots];
 };
@@ -621,6 +624,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     sh.full[i] = 0u;
     sh.freed[i] = 0u;
   }
+  if (tid == 0) sh.ids_ready = 0u;
   if (CM) {
     for (int i = tid; i < kLdsCmSlots * kLdsF; i += kLdsThreads) (&sh.cm[0][0])[i] = 0u;
     for (int i = tid; i < kLdsCmSlots; i += kLdsThreads) sh.cm_cnt[i] = 0u;
@@ -631,9 +635,16 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
   __syncthreads();
   if (my_parts == 0) return;
 
-  if (wv == kLdsCons) {
-    // ---------------- loader wave ----------------
-    // lane i holds part i's edge bounds and stage count
+  // stage k consumed by every consumer wave
+  auto consumed = [&](uint32_t k) {
+    return lds_ld(&sh.freed[k % kLdsNS]) >= (uint32_t)kLdsCons * (k / kLdsNS + 1);
+  };
+  if (wv == kLdsCons + 1) {
+    // ---------------- id loader ----------------
+    // lane i holds part i's edge bounds and stage count; per stage three LDS
+    // DMAs (ids | weights, the part's offsets) into id-ring entry k % kLdsID,
+    // kLdsIdAhead stages in flight; entry k is refilled once stage k - kLdsID
+    // is consumed.  (The only vector-memory ops of this wave: counted waits.)
     uint32_t pe0 = 0, pe1 = 0, nst = 0;
     if ((uint32_t)lane < my_parts) {
       const uint32_t p = b + (uint32_t)lane * G;
@@ -644,70 +655,61 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
     uint32_t total = nst;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o);
-    // stage descriptors in order (cursor: part i, stage s of it); past the end
-    // the last stage again (dummy loads that nothing reads)
-    uint32_t cur_i = 0, cur_s = 0;
-    const uint32_t lstg = lds_u32(&sh.stg[0][0]);
-    // ids (lanes 0-31) and weights (32-63) of stage q's edges, the part's
-    // offsets: three global_load_lds_dword into staging entry q % 3
-    auto load_ids = [&](uint32_t q) {
-      const uint32_t i = min(cur_i, my_parts - 1);
-      const uint32_t e0 = __shfl(pe0, (int)i), e1 = __shfl(pe1, (int)i), ns = __shfl(nst, (int)i);
-      const uint32_t st = cur_i < my_parts ? cur_s : ns - 1;
-      const int qq = (int)(q % 3);
-      const uint32_t sb = e0 + st * SE, se = min(sb + SE, e1);
-      if (lane == 0)  // (read back after this entry's loads landed: ordered by the vmcnt wait)
-        sh.stgd[qq] = make_uint4(i, sb, se, (st == 0 ? 1u : 0u) | (st + 1 == ns ? 2u : 0u));
-      if (cur_i < my_parts && ++cur_s == ns) {
-        cur_s = 0;
-        ++cur_i;
+    const uint32_t lids = lds_u32(&sh.ids[0][0]);
+    uint32_t cur_i = 0, cur_s = 0;  // cursor: part, stage within the part
+    for (uint32_t k = 0; k < total + kLdsIdAhead - 1; ++k) {
+      if (k < total) {
+        const int q = (int)(k % kLdsID);
+        if (k >= (uint32_t)kLdsID)
+          for (uint32_t it = 0; !consumed(k - kLdsID) && it < (1u << 22); ++it) __builtin_amdgcn_s_sleep(1);
+        const uint32_t i = cur_i;
+        const uint32_t e0 = __shfl(pe0, (int)i), e1 = __shfl(pe1, (int)i), ns = __shfl(nst, (int)i);
+        const uint32_t sb = e0 + cur_s * SE, se = min(sb + SE, e1);
+        if (lane == 0) {
+          sh.meta[q] = make_uint4(b + i * G, sb, se,
+                                  (cur_s == 0 ? 1u : 0u) | (cur_s + 1 == ns ? 2u : 0u) | (total << 8));
+          sh.pend[q] = e1;
+        }
+        if (++cur_s == ns) {
+          cur_s = 0;
+          ++cur_i;
+        }
+        const uint32_t e = sb + (uint32_t)(lane & 31);
+        const uint32_t ec = e < se ? e : sb < se ? sb : 0u;
+        const void* src = lane < 32 || !w ? (const void*)(idx + ec) : (const void*)(w + ec);
+        glds4a(src, lids + (uint32_t)(q * (64 + kLdsR) * 4));
+        const uint64_t p = b + i * G;
+        glds4a(off + min(p * R + lane, (uint64_t)n), lids + (uint32_t)((q * (64 + kLdsR) + 64) * 4));
+        glds4a(off + min(p * R + 64 + lane, (uint64_t)n), lids + (uint32_t)((q * (64 + kLdsR) + 128) * 4));
       }
-      const uint32_t e = sb + (uint32_t)(lane & 31);
-      const uint32_t ec = e < se ? e : sb < se ? sb : 0u;
-      const void* src = lane < 32 || !w ? (const void*)(idx + ec) : (const void*)(w + ec);
-      glds4a(src, lstg + (uint32_t)(qq * (64 + kLdsR) * 4));
-      const uint64_t p = b + i * G;
-      glds4a(off + min(p * R + lane, (uint64_t)n), lstg + (uint32_t)((qq * (64 + kLdsR) + 64) * 4));
-      glds4a(off + min(p * R + 64 + lane, (uint64_t)n),
-             lstg + (uint32_t)((qq * (64 + kLdsR) + 128) * 4));
-    };
+      // entry k - (kLdsIdAhead - 1) landed: younger are the 3 (kLdsIdAhead - 1)
+      // loads of the stages after it (fewer at the end: then wait for all)
+      if (k + 1 >= (uint32_t)kLdsIdAhead) {
+        if (k < total) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(3 * (kLdsIdAhead - 1)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) lds_st(&sh.ids_ready, min(k + 2 - kLdsIdAhead, total));
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) lds_st(&sh.ids_ready, total);
+    return;
+  }
+  if (wv == kLdsCons) {
+    // ---------------- row loader ----------------
+    // per stage 16 LDS DMAs of 1 KB into row slot k % kLdsNS once its ids are
+    // in and stage k - kLdsNS is consumed; stage k-2 is marked full when it
+    // lands (younger: the 32 DMAs of k-1 and k), three stages in flight
     const uint32_t lrows = lds_u32(&sh.rows[0][0]);
-    load_ids(0);
-    load_ids(1);
+    uint32_t total = 1;
     for (uint32_t k = 0; k < total; ++k) {
       const uint32_t slot = k % kLdsNS;
-      const int qq = (int)(k % 3);
-      // per iteration j the loader issues ids(j + 2) (3 loads) then rows(j)
-      // (16 LDS DMAs).  Stage k-3 is marked full as soon as its rows landed
-      // (younger: ids(k), rows(k-2), ids(k+1), rows(k-1) = 38 loads) — before
-      // waiting for the consumers, so that they never wait on the loader's
-      // own wait for a free slot
-      if (k >= 3) {
-        asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
-        lds_st(&sh.full[(k - 3) % kLdsNS], k - 2);
-      }
+      const int q = (int)(k % kLdsID);
+      lds_wait_ge(&sh.ids_ready, k + 1);
       if (k >= (uint32_t)kLdsNS) lds_wait_ge(&sh.freed[slot], (uint32_t)kLdsCons * (k / kLdsNS));
-      // staging of stage k landed.  Younger: k = 0: ids(1); k = 1: ids(2),
-      // rows(0); k >= 2: rows(k-2), ids(k+1), rows(k-1)
-      if (k == 0) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else if (k == 1) asm volatile("s_waitcnt vmcnt(19)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(35)" ::: "memory");
-      // staging -> the slot (weights, offsets, descriptor)
-      const uint32_t id = sh.stg[qq][lane & 31];
-      const uint4 dsc = sh.stgd[qq];
-      const uint32_t sb = dsc.y, se = dsc.z;
-      const uint32_t pend = __shfl(pe1, (int)dsc.x);
-      if (lane >= 32) sh.w[slot][lane - 32] = w ? __uint_as_float(sh.stg[qq][lane]) : 1.f;
-      sh.offs[slot][lane] = sh.stg[qq][64 + lane];
-      sh.offs[slot][64 + lane] = sh.stg[qq][128 + lane];
-      if (lane == 0) {
-        sh.meta[slot] = make_uint4(b + dsc.x * G, sb, se, dsc.w | (total << 8));
-        sh.pend[slot] = pend;
-      }
-      load_ids(k + 2);  // staging entry (k + 2) % 3 held stage k - 1: copied out already
-      // 16 row DMAs of 1 KB: instruction jj moves float4s 64 jj + lane of the
-      // stage (rows 2 jj and 2 jj + 1 of 128 floats, or row jj of 256)
-      const uint32_t nrow = se - sb;
+      const uint4 mt = sh.meta[q];
+      total = mt.w >> 8;
+      const uint32_t nrow = mt.z - mt.y;
+      const uint32_t id = sh.ids[q][lane & 31];
       const uint32_t id0 = __shfl(id, 0);
 #pragma unroll
       for (int jj = 0; jj < 16; ++jj) {
@@ -717,9 +719,13 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
         const char* src = reinterpret_cast<const char*>(x + (uint64_t)rid * ldx) + 16 * c16;
         glds16a(src, lrows + (uint32_t)(slot * kLdsSE * kLdsRowB + 1024 * jj));
       }
+      if (k >= 2) {
+        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+        lds_st(&sh.full[(k - 2) % kLdsNS], k - 1);
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (uint32_t k = total > 3 ? total - 3 : 0; k < total; ++k) lds_st(&sh.full[k % kLdsNS], k + 1);
+    for (uint32_t k = total > 2 ? total - 2 : 0; k < total; ++k) lds_st(&sh.full[k % kLdsNS], k + 1);
     return;
   }
 
@@ -754,8 +760,9 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
   uint32_t total = 1;
   for (uint32_t k = 0; k < total; ++k) {
     const uint32_t slot = k % kLdsNS;
+    const int q = (int)(k % kLdsID);
     lds_wait_ge(&sh.full[slot], k + 1);
-    const uint4 mt = sh.meta[slot];
+    const uint4 mt = sh.meta[q];
     total = mt.w >> 8;
     const uint32_t sb = mt.y, se = mt.z, fl = mt.w & 255u;
     if (fl & 1u) {  // first stage of part mt.x: this group's first row
@@ -763,8 +770,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       pcount = min(R, n - part * R);
       j = (uint32_t)g;
       if (j < pcount) {
-        e_beg = sh.offs[slot][j];
-        e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
+        e_beg = sh.ids[q][64 + j];
+        e_end = j + 1 < pcount ? sh.ids[q][64 + j + 1] : sh.pend[q];
         row_ctx(part * R + j);
         take_ctx();
         if (j + 8 < pcount) row_ctx(part * R + j + 8);
@@ -773,7 +780,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       cmx = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const float4* srow = &sh.rows[slot][l];
-    const float* sw = sh.w[slot];
+    const float* sw = reinterpret_cast<const float*>(&sh.ids[q][32]);
     // rows whose edges start in this stage (a row without edges at the
     // stage's end included): sum their edges here, store the complete ones
     while (j < pcount && (e_beg < se || (e_beg == e_end && e_beg <= se))) {
@@ -787,7 +794,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
         for (int u = 0; u < UL; ++u) {
 #pragma unroll
           for (int c = 0; c < NCH; ++c) xv[u][c] = srow[(e + u - sb) * RF4 + 32 * c];
-          wv4[u] = sw[e + u - sb];
+          wv4[u] = w ? sw[e + u - sb] : 1.f;
         }
 #pragma unroll
         for (int u = 0; u < UL; ++u)
@@ -796,7 +803,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       }
       for (; e < hi; ++e)
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) acc[c] = VT<4>::madd(acc[c], srow[(e - sb) * RF4 + 32 * c], sw[e - sb]);
+        for (int c = 0; c < NCH; ++c)
+          acc[c] = VT<4>::madd(acc[c], srow[(e - sb) * RF4 + 32 * c], w ? sw[e - sb] : 1.f);
       if (e_end > se) break;  // continues in the next stage
       const uint32_t d = part * R + j;
       if constexpr (MODE == kAggPostMask)
@@ -814,8 +822,8 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       zero();
       j += 8;
       if (j < pcount) {
-        e_beg = sh.offs[slot][j];
-        e_end = j + 1 < pcount ? sh.offs[slot][j + 1] : sh.pend[slot];
+        e_beg = sh.ids[q][64 + j];
+        e_end = j + 1 < pcount ? sh.ids[q][64 + j + 1] : sh.pend[q];
         take_ctx();
         if (j + 8 < pcount) row_ctx(part * R + j + 8);
       }

@@ -20,15 +20,16 @@ for e in NTS_H2_NN4=0 NTS_H2_NN4=1; do
   echo "$e $(cat $O/micro_bottom_$e.json)"
 done
 B="--no-cpu-baseline --no-secondary-af --no-secondary-exact --epochs 0 --sampler-batches 0"
-for e in NTS_NONE=0 NTS_AGG_LDS=1 NTS_H2_NN4=1 NTS_GEMM_CUS=232; do
+for e in NTS_NONE=0 NTS_AGG_LDS=1 NTS_H2_NN4=0; do
   env $e timeout -k 10 300 python -u bench.py $B > $O/bench_$e.json 2> $O/bench_$e.err || { echo "bench $e failed"; tail -5 $O/bench_$e.err; exit 1; }
   python3 - $O/bench_$e.json "$e" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 a = d["config"].get("training_stream_alone") or {}
 print(sys.argv[2], round(d["ms_per_step"], 4), "ms/step; alone", round(a.get("ms_per_step", 0), 4),
-      {k: (round(v["avg_launch_ms"] * 1e3, 1), round(v["frac"], 3)) for k, v in d["roofline"].get("kernels", {}).items()})
+      {k: (round(v["avg_launch_ms"] * 1e3, 1), round(v["frac"], 3)) for k, v in d["roofline"].get("kernels", {}).items()},
+      a.get("kernel_avg_us"))
 PY
 done
-bash scripts/pmc_stalls.sh $T > $O/stalls.txt 2>&1 || { tail -5 $O/stalls.txt; exit 1; }
-cat $O/stalls.txt
+NTS_AGG_LDS=1 bash scripts/pmc_stalls.sh $T > $O/stalls.txt 2>&1 || { tail -5 $O/stalls.txt; exit 1; }
+grep -E "k_agg_lds|k_h2_nn4" $O/stalls.txt
