@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-samp1}
 mkdir -p $O
 shift || true
-timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tr -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --epochs 0 --sampler-batches 32 --no-secondary-af "$@" > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tr -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --epochs 0 --sampler-batches 32 --no-secondary-af --no-secondary-exact --no-interference-probe "$@" > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 python3 - "$O" <<'PY'
 import csv, glob, sys, collections
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
