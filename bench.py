@@ -198,6 +198,8 @@ def parse():
     p.add_argument("--early-agg", action="store_true",
                    help="aggregate-first: issue the bottom aggregation behind the sampler")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
+    p.add_argument("--training-priority", action="store_true",
+                   help="the training stream at high priority, the sampler's at normal")
     p.add_argument("--model", default="gcn", choices=["gcn", "gat"],
                    help="gcn (headline) or gat (GAT_SAMPLE_ALL_GPU-style attention layers)")
     p.add_argument("--atomic-backward", action="store_true",
@@ -349,7 +351,8 @@ def main():
                           fused_gather=not args.no_fused_gather, profile=True,
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
                           transform_first=args.transform_first, early_aggregate=args.early_agg,
-                          sampler_priority=not args.no_priority,
+                          sampler_priority=(-1 if args.training_priority else
+                                            0 if args.no_priority else 1),
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,

@@ -138,6 +138,58 @@ int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const u
                     uint64_t n_cap, hipStream_t stream);
 int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems);
 size_t scan1_state_elems(uint64_t n_cap);
+// the next per-call epoch of the look-back tile states (never 0)
+uint32_t scan_next_epoch(nts_hip_ctx* ctx);
+
+// Decoupled look-back (one wave, every lane calls): tile `tile` publishes its
+// aggregate, sums its predecessors' states (RELAXED agent-scope atomics: each
+// 64-bit word {epoch:30 | kind:2 | value:32} carries its own value) up to the
+// first inclusive one, publishes its inclusive prefix and returns the
+// exclusive one.  Tiles only wait on lower-numbered tiles, which the
+// dispatcher places first, so the chain completes.
+__device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint64_t kind, uint32_t v) {
+  return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | (kind << 32) | v;
+}
+__device__ __forceinline__ uint32_t lookback_exclusive(uint64_t* state, uint32_t tile,
+                                                       uint32_t epoch, uint32_t agg) {
+  constexpr uint64_t kAgg = 1, kIncl = 2;
+  const int lane = threadIdx.x & 63;
+  if (tile == 0) {
+    if (lane == 0)
+      __hip_atomic_store(state, lb_word(epoch, kIncl, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0u;
+  }
+  if (lane == 0)
+    __hip_atomic_store(state + tile, lb_word(epoch, kAgg, agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t prefix = 0;
+  int64_t top = (int64_t)tile - 1;
+  for (;;) {
+    const int64_t p = top - lane;
+    uint64_t wd = 0;
+    uint32_t kind = 0;
+    if (p >= 0) {
+      for (;;) {
+        wd = __hip_atomic_load(state + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(wd >> 34) == (epoch & 0x3FFFFFFFu)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      kind = (uint32_t)((wd >> 32) & 3u);
+    }
+    const uint64_t inc = __ballot(p >= 0 && kind == kIncl);
+    const int stop = inc ? __ffsll((long long)inc) - 1 : 64;
+    uint32_t add = (lane <= stop && p >= 0) ? (uint32_t)wd : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
+    prefix += add;
+    if (inc || top - 64 < 0) break;
+    top -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store(state + tile, lb_word(epoch, kIncl, prefix + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return prefix;
+}
 
 // The sampler's per-dst counts fused into that scan: co[i] = min(deg(dst[i]),
 // fanout) (0 for an omitted dst), exclusive-scanned; sizes[0] = v,

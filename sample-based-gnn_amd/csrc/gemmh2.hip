@@ -1997,11 +1997,11 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   const bool tr_ok = tr && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
   // four stages (k_h2_nn4) where the table rows carry their scales in a tail
   // (ldq >= 2 Kp + 8 halves: 2560-byte rows) and the step count is compiled
-  // in (measured, C2 alone: 163.5 vs 167.3 us; in the bench 163 vs 172 us);
-  // NTS_H2_NN4=0 keeps k_h2_nn3 (A/B)
+  // in.  Opt-in (NTS_H2_NN4=1): measured no faster than k_h2_nn3 in the C2
+  // bench (r04d: 152.6 vs ~158 us alone, 164.9 vs 170.9 us pipelined)
   static const bool nn4 = [] {
     const char* e = getenv("NTS_H2_NN4");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (nn4 && !relu_dropout && a_rows && pitch == 2560 && ldq >= 2 * (uint64_t)Kp + 8 && nsteps == 19) {
     gx = std::max(gx, (T + 63) / 64);  // <= 64 tiles per block (lane-held row ids)

@@ -358,13 +358,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   }
 }
 
-size_t scan1_state_elems(uint64_t n_cap) { return (n_cap / kScanTile + 1 + 63) / 64 * 64; }
-
 static uint32_t next_epoch(nts_hip_ctx* ctx) {
   ctx->scan_epoch = (ctx->scan_epoch + 1) & 0x3FFFFFFFu;
   if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;  // 0: the state words' initial value
   return ctx->scan_epoch;
 }
+uint32_t scan_next_epoch(nts_hip_ctx* ctx) { return next_epoch(ctx); }
+
+size_t scan1_state_elems(uint64_t n_cap) { return (n_cap / kScanTile + 1 + 63) / 64 * 64; }
+
+
 
 int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const uint32_t* n_dev,
                     uint64_t n_cap, hipStream_t stream) {

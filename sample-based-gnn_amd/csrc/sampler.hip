@@ -1210,6 +1210,66 @@ __global__ __launch_bounds__(kMarkThreads) void k_mark_count(const uint8_t* __re
   }
 }
 
+// Single-pass frontier compaction (the default): each 4096-vertex tile counts
+// its marks, takes its offset by decoupled look-back over the tiles before it
+// (lookback_exclusive) and writes `source` / `src_index` in ascending vertex
+// order — k_mark_count + k_mark_write in one launch.  Clears the marks it
+// read; the last tile writes src_size (and the s_cap overflow flag, this
+// kernel's only writer of it).
+__global__ __launch_bounds__(kMarkThreads) void k_mark_fused(
+    uint8_t* __restrict__ marks, uint32_t nblk, uint64_t n_vertices, uint32_t s_cap,
+    uint32_t* __restrict__ source, uint32_t* __restrict__ src_index, uint32_t* sizes,
+    uint64_t* __restrict__ state, uint32_t epoch) {
+  const uint64_t tid = (uint64_t)blockIdx.x * kMarkThreads + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ uint32_t ws[kMarkThreads / kWave];
+  __shared__ uint32_t s_prefix;
+  const uint4 m = reinterpret_cast<const uint4*>(marks)[tid];
+  if (m.x | m.y | m.z | m.w) reinterpret_cast<uint4*>(marks)[tid] = make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t c = count16(m);
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t agg = 0, off = 0;
+  for (int i = 0; i < kMarkThreads / kWave; ++i) {
+    off += i < w ? ws[i] : 0u;
+    agg += ws[i];
+  }
+  if (w == 0) {
+    const uint32_t pre = lookback_exclusive(state, blockIdx.x, epoch, agg);
+    if (lane == 0) s_prefix = pre;
+  }
+  __syncthreads();
+  uint32_t pos = s_prefix + off + inc - c;
+  if (blockIdx.x == nblk - 1 && threadIdx.x == 0) {
+    const uint32_t total = s_prefix + agg;
+    sizes[2] = min(total, s_cap);
+    if (total > s_cap) atomicOr(&sizes[3], 2u);
+  }
+  if (c == 0) return;
+  const uint32_t words[4] = {m.x, m.y, m.z, m.w};
+  const uint64_t v0 = tid * 16;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if ((words[q] >> (8 * b)) & 0xffu) {
+        const uint64_t vtx = v0 + q * 4 + b;
+        if (vtx < n_vertices && pos < s_cap) {
+          source[pos] = (uint32_t)vtx;
+          src_index[vtx] = pos;
+        }
+        ++pos;
+      }
+    }
+  }
+}
+
 // Also clears the byte map it consumed, so the next layer starts from zeros
 // without a memset (the map is zeroed once when allocated).
 // DIRECT: blk holds the per-tile counts and each block sums the ones before
@@ -1591,21 +1651,30 @@ frontier:
     NTS_LAUNCH_CHECK();
   }
 
-  // 3) frontier: ascending compaction of the byte map
-  hipLaunchKernelGGL(k_mark_count, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
-                     t_blk);
-  NTS_LAUNCH_CHECK();
-  if (nblk_marks <= kMarkDirectTiles) {  // up to 8M vertices: no scan kernel
-    hipLaunchKernelGGL(k_mark_write<true>, dim3(nblk_marks), dim3(kMarkThreads), 0, st,
-                       ctx->marks, t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index,
-                       o->sizes);
+  // 3) frontier: ascending compaction of the byte map (single pass; the
+  // two-kernel form with the two-kernel scans, NTS_SCAN1=0)
+  if (scan1_enabled()) {
+    NTS_RET(ensure_scan_state(ctx, scan1_state_elems((uint64_t)nblk_marks * 4096)));
+    hipLaunchKernelGGL(k_mark_fused, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
+                       nblk_marks, V, o->s_cap, o->source, ctx->src_index, o->sizes,
+                       ctx->scan_state, scan_next_epoch(ctx));
+    NTS_LAUNCH_CHECK();
   } else {
-    NTS_RET(scan_exclusive<uint32_t>(t_blk, t_blk, nullptr, nblk_marks, t_scan_blk, st));
-    hipLaunchKernelGGL(k_mark_write<false>, dim3(nblk_marks), dim3(kMarkThreads), 0, st,
-                       ctx->marks, t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index,
-                       o->sizes);
+    hipLaunchKernelGGL(k_mark_count, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
+                       t_blk);
+    NTS_LAUNCH_CHECK();
+    if (nblk_marks <= kMarkDirectTiles) {  // up to 8M vertices: no scan kernel
+      hipLaunchKernelGGL(k_mark_write<true>, dim3(nblk_marks), dim3(kMarkThreads), 0, st,
+                         ctx->marks, t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index,
+                         o->sizes);
+    } else {
+      NTS_RET(scan_exclusive<uint32_t>(t_blk, t_blk, nullptr, nblk_marks, t_scan_blk, st));
+      hipLaunchKernelGGL(k_mark_write<false>, dim3(nblk_marks), dim3(kMarkThreads), 0, st,
+                         ctx->marks, t_blk, nblk_marks, V, o->s_cap, o->source, ctx->src_index,
+                         o->sizes);
+    }
+    NTS_LAUNCH_CHECK();
   }
-  NTS_LAUNCH_CHECK();
 
   if (o->dst_local_id) {
     hipLaunchKernelGGL(k_dst_local, dim3(gv), dim3(256), 0, st, o->destination, ctx->src_index,

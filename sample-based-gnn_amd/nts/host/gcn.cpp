@@ -42,7 +42,8 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                      cu_mask_spread(graph->device, cfg.sampler_cus, true),
                                      (uint64_t)cfg.seed);
   else
-    cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed);
+    cs = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed,
+                                     cfg.pipeline && cfg.sampler_priority < 0);
   hip_check(nts_hip_ctx_set_gemm_mode(cs->ctx(), cfg.gemm_mode), "nts_hip_ctx_set_gemm_mode");
   // inputs were produced on other streams: order them before our stream
   TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
@@ -138,7 +139,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                      (uint64_t)cfg.seed);
   else if (cfg.pipeline)
     ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed,
-                                     cfg.sampler_priority);
+                                     cfg.sampler_priority > 0);
   // size the scratch arenas once so the training loop never allocates
   uint64_t items = graph->global_vertices;
   for (auto* s : sampler->ssg->sampled_sgs) items = std::max<uint64_t>({items, s->e_cap, s->v_cap});

@@ -27,7 +27,10 @@ struct GCNConfig {
   bool pipeline = true;               // sample batch i+1 on its own stream while i trains
   bool fuse_activation = true;        // hidden layers: relu + dropout in the MFMA GEMM
   bool fuse_loss = true;              // training: output layer + log_softmax x2 + nll in 2 kernels
-  bool sampler_priority = true;       // pipelined sampler on a high-priority stream
+  // pipelined sampler's stream priority: 1 = sampler stream high, 0 = both
+  // normal, -1 = the training stream high (the sampler's blocks dispatched
+  // after the training stream's)
+  int sampler_priority = 1;
   int sampler_cus = 0;
   bool pad_features = true;           // copy wide feature tables to a 128-byte row pitch
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
