@@ -890,6 +890,33 @@ __device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W,
   return q - p;
 }
 
+// words consumed by one dst whose draws start at the first of the NW words in
+// `cur` (lane-private, registers only): the index after the n-th distinct
+// accepted draw, or 0 when it lies past the NW words (then lane_consume walks
+// the stream).  A draw is new iff it is accepted and no earlier accepted draw
+// has its value — the reference's rejection loop (ntsFastSampler.hpp:1026-1038).
+template <int NW>
+__device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint32_t n,
+                                                 uint32_t deg, uint32_t thr, bool lemire) {
+  constexpr uint32_t kRej = 0xFFFFFFFFu;  // a rejected word (positions are < deg)
+  uint32_t val[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    uint32_t x;
+    val[q] = mt_apply(cur[q], deg, thr, lemire, x) ? x : kRej;
+  }
+  uint32_t cnt = 0, used = 0;
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    bool dup = val[t] == kRej;
+#pragma unroll
+    for (int b = 0; b < t; ++b) dup |= val[b] == val[t];
+    cnt += dup ? 0u : 1u;
+    used = (used == 0 && cnt == n) ? (uint32_t)t + 1u : used;
+  }
+  return used;
+}
+
 // bulk generation: W[t] = the tempered word at _M_p + t of the stream in
 // mt_state, t < nw (written to *nw_out); rb[b] = raw block b (b = 0: the
 // state's own).  nw = draws + expected extras + 10 sigma + 4096 (<= w_cap).
@@ -1023,37 +1050,31 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
     while (j < cnt && inf[j].y == 0) ++j;
     return j;
   };
+  // NW words per dst in registers: the n-th distinct draw is found there
+  // unless it needs more than NW - n extra words
+  constexpr int NW = NMAX + 8;
   uint32_t j = next_draw(0);
-  uint32_t wv[NMAX];
+  uint32_t wv[NW];
   uint32_t pf = j < cnt ? bs[j] + dl : 0u;
 #pragma unroll
-  for (int q = 0; q < NMAX; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
+  for (int q = 0; q < NW; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
   while (j < cnt) {
     const uint4 f = inf[j];
     const uint32_t p = bs[j] + dl;
-    uint32_t cur[NMAX];
+    uint32_t cur[NW];
 #pragma unroll
-    for (int q = 0; q < NMAX; ++q) cur[q] = wv[q];
+    for (int q = 0; q < NW; ++q) cur[q] = wv[q];
     if (p != pf) {  // (the previous dst consumed extra words)
 #pragma unroll
-      for (int q = 0; q < NMAX; ++q) cur[q] = p + q < nw ? W[p + q] : 0u;
+      for (int q = 0; q < NW; ++q) cur[q] = p + q < nw ? W[p + q] : 0u;
     }
     const uint32_t jn = next_draw(j + 1);
     pf = jn < cnt ? bs[jn] + dl : 0u;
 #pragma unroll
-    for (int q = 0; q < NMAX; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
-    // first n words accepted and pairwise distinct: n words; else walk
-    uint32_t val[NMAX];
-    bool clean = true;
-#pragma unroll
-    for (int q = 0; q < NMAX; ++q)
-      if ((uint32_t)q < f.y) clean &= mt_apply(cur[q], f.z, f.w, lemire, val[q]);
-#pragma unroll
-    for (int a2 = 1; a2 < NMAX; ++a2)
-#pragma unroll
-      for (int b2 = 0; b2 < a2; ++b2)
-        if ((uint32_t)a2 < f.y) clean &= val[a2] != val[b2];
-    if (!clean) dl += lane_consume<NMAX>(W, nw, p, f.y, f.z, f.w, lemire, lst + t, 256) - f.y;
+    for (int q = 0; q < NW; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
+    uint32_t used = regs_consume<NW>(cur, f.y, f.z, f.w, lemire);
+    if (used == 0) used = lane_consume<NMAX>(W, nw, p, f.y, f.z, f.w, lemire, lst + t, 256);
+    dl += used - f.y;
     j = jn;
   }
   if (slot < wn) tabs[(uint64_t)k * kMtWmax + slot] = dl;
