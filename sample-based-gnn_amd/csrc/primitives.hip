@@ -5,6 +5,7 @@
 // and never synchronise with the host, so a whole sampling hop can be
 // enqueued (or graph-captured) without knowing e_size / src_size on the host.
 #include "common.hpp"
+#include "radix_tile.hpp"
 
 namespace nts_hip {
 
@@ -473,12 +474,6 @@ template size_t scan_tmp_elems<uint64_t>(uint64_t);
 // LDS and written out in runs (coalesced stores).
 // Tiles past the device-side count n exit at once.
 // ============================================================================
-constexpr int kRadixThreads = 256;
-constexpr int kRadixItems = 16;
-constexpr int kRadixTile = kRadixThreads * kRadixItems;  // 4096
-constexpr int kRadixMaxBits = 9;
-constexpr int kRadixMaxBins = 1 << kRadixMaxBits;
-
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys,
                                                               const uint32_t* n_dev,
                                                               uint64_t n_cap, uint32_t shift,
@@ -507,103 +502,14 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* n_dev,
     uint64_t n_cap, uint32_t shift, uint32_t dbits, const uint32_t* __restrict__ hist,
     uint32_t nb) {
-  __shared__ uint32_t wh[kRadixThreads / kWave][kRadixMaxBins];  // per-wave counts -> offsets
-  __shared__ uint32_t gstart[kRadixMaxBins];  // digit d's global start for this tile
-  __shared__ uint32_t lstart[kRadixMaxBins];  // ... and its start in the tile's digit order
-  __shared__ uint32_t sk[kRadixTile], sv[kRadixTile];  // the tile in digit order
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  __shared__ RadixTileLds sm;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
-  const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-  if (base >= n) return;  // whole tile past the end (uniform per block)
-  const uint32_t mask = (1u << dbits) - 1u, bins = mask + 1;
-  for (uint32_t d = t; d < bins; d += kRadixThreads)
-#pragma unroll
-    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) wh[ww][d] = 0;
-  __syncthreads();
-  // wave w ranks items base + 1024 w + 64 k + lane (index order) against its
-  // running digit counts
-  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint64_t wbase = base + (uint64_t)w * (kRadixItems * kWave);
-  uint32_t key[kRadixItems], val[kRadixItems], rank[kRadixItems];
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = wbase + (uint64_t)k * kWave + lane;
-    const bool valid = i < n;
-    key[k] = valid ? keys_in[i] : 0u;
-    val[k] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    const bool valid = wbase + (uint64_t)k * kWave + lane < n;
-    const uint32_t d = (key[k] >> shift) & mask;
-    uint64_t peers = __ballot(valid);
-    for (uint32_t b = 0; b < dbits; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t m = __ballot(bit);
-      peers &= bit ? m : ~m;
-    }
-    const uint32_t prev = wh[w][d];
-    const uint32_t before = (uint32_t)__popcll(peers & lt_mask);
-    rank[k] = prev + before;
-    if (valid && before == 0) wh[w][d] = prev + (uint32_t)__popcll(peers);
-  }
-  __syncthreads();
-  // per digit: the waves' counts -> their offsets within the digit's slice
-  // (wh), the tile's count of the digit (lstart, scanned below) and its
-  // global start (gstart, from the scanned histogram)
-  for (uint32_t d = t; d < bins; d += kRadixThreads) {
-    uint32_t run = 0;
-#pragma unroll
-    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) {
-      const uint32_t c = wh[ww][d];
-      wh[ww][d] = run;
-      run += c;
-    }
-    lstart[d] = run;
-    gstart[d] = hist[(uint64_t)d * nb + blockIdx.x];
-  }
-  __syncthreads();
-  {  // exclusive scan of the tile's digit counts: thread t owns digits 2t, 2t + 1
-    __shared__ uint32_t wsum[kRadixThreads / kWave];
-    static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");
-    const uint32_t c0 = 2u * t < bins ? lstart[2 * t] : 0u;
-    const uint32_t c1 = 2u * t + 1 < bins ? lstart[2 * t + 1] : 0u;
-    uint32_t inc = c0 + c1;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o);
-      if (lane >= o) inc += y;
-    }
-    if (lane == kWave - 1) wsum[w] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-#pragma unroll
-    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) before += ww < w ? wsum[ww] : 0u;
-    const uint32_t ex = before + inc - (c0 + c1);
-    if (2u * t < bins) lstart[2 * t] = ex;
-    if (2u * t + 1 < bins) lstart[2 * t + 1] = ex + c0;
-  }
-  __syncthreads();
-  // the tile in digit order through LDS, then written out in index order:
-  // consecutive LDS slots of one digit go to consecutive global positions
-  // (coalesced runs instead of one scattered 4-byte store per item)
-#pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
-    if (wbase + (uint64_t)k * kWave + lane < n) {
-      const uint32_t d = (key[k] >> shift) & mask;
-      const uint32_t loc = lstart[d] + wh[w][d] + rank[k];
-      sk[loc] = key[k];
-      sv[loc] = val[k];
-    }
-  }
-  __syncthreads();
-  const uint32_t cnt = (uint32_t)(n - base < (uint64_t)kRadixTile ? n - base : (uint64_t)kRadixTile);
-  for (uint32_t i = t; i < cnt; i += kRadixThreads) {
-    const uint32_t k = sk[i], d = (k >> shift) & mask;
-    const uint32_t pos = gstart[d] + (i - lstart[d]);
-    keys_out[pos] = k;
-    vals_out[pos] = sv[i];
-  }
+  if ((uint64_t)blockIdx.x * kRadixTile >= n) return;  // whole tile past the end
+  radix_scatter_tile(sm, keys_in, vals_in, n, shift, dbits, hist, nb, 0u,
+                     [&](uint32_t pos, uint32_t key, uint32_t val, bool, uint32_t) {
+                       keys_out[pos] = key;
+                       vals_out[pos] = val;
+                     });
 }
 
 size_t radix_tmp_bytes(uint64_t n_cap) {

@@ -1,0 +1,130 @@
+// One 4096-item tile of a stable LSD radix pass (shared by the generic sort
+// in primitives.hip and the sampler's CSR transpose in sampler.hip).
+// Internal, not part of the C-ABI.
+#pragma once
+#include "common.hpp"
+
+namespace nts_hip {
+
+constexpr int kRadixThreads = 256;
+constexpr int kRadixItems = 16;
+constexpr int kRadixTile = kRadixThreads * kRadixItems;  // 4096
+constexpr int kRadixMaxBits = 9;
+constexpr int kRadixMaxBins = 1 << kRadixMaxBits;
+
+struct RadixTileLds {
+  uint32_t wh[kRadixThreads / kWave][kRadixMaxBins];  // per-wave counts -> offsets
+  uint32_t gstart[kRadixMaxBins];  // digit d's global start for this tile
+  uint32_t lstart[kRadixMaxBins];  // ... and its start in the tile's digit order
+  uint32_t sk[kRadixTile], sv[kRadixTile];  // the tile in digit order
+  uint32_t wsum[kRadixThreads / kWave];
+};
+
+// Tile blockIdx.x of a pass over n items (base = blockIdx.x * kRadixTile < n):
+// each wave ranks its 1,024 contiguous items against a running per-wave digit
+// count in LDS (match-any by ballots, no barrier inside the item loop), the
+// tile is reordered by digit in LDS and handed out in runs: epi(pos, key,
+// val, run_first, prev_key) for every item, where pos = its position in the
+// pass's output (digit start from the scanned per-tile histogram `hist`,
+// digit-major [bins][nb], minus `sub`), run_first = it opens its digit's run
+// in this tile, prev_key = the key before it in the output (valid unless
+// run_first).  Consecutive items of a run go to consecutive positions.
+// vals_in == nullptr: values are the item indices.
+template <class Epi>
+__device__ __forceinline__ void radix_scatter_tile(RadixTileLds& sm, const uint32_t* __restrict__ keys_in,
+                                                   const uint32_t* __restrict__ vals_in, uint64_t n,
+                                                   uint32_t shift, uint32_t dbits,
+                                                   const uint32_t* __restrict__ hist, uint32_t nb,
+                                                   uint32_t sub, Epi&& epi) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+  const uint32_t mask = (1u << dbits) - 1u, bins = mask + 1;
+  for (uint32_t d = t; d < bins; d += kRadixThreads)
+#pragma unroll
+    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) sm.wh[ww][d] = 0;
+  __syncthreads();
+  // wave w ranks items base + 1024 w + 64 k + lane (index order) against its
+  // running digit counts
+  const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint64_t wbase = base + (uint64_t)w * (kRadixItems * kWave);
+  uint32_t key[kRadixItems], val[kRadixItems], rank[kRadixItems];
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = wbase + (uint64_t)k * kWave + lane;
+    const bool valid = i < n;
+    key[k] = valid ? keys_in[i] : 0u;
+    val[k] = valid ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    const bool valid = wbase + (uint64_t)k * kWave + lane < n;
+    const uint32_t d = (key[k] >> shift) & mask;
+    uint64_t peers = __ballot(valid);
+    for (uint32_t b = 0; b < dbits; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t prev = sm.wh[w][d];
+    const uint32_t before = (uint32_t)__popcll(peers & lt_mask);
+    rank[k] = prev + before;
+    if (valid && before == 0) sm.wh[w][d] = prev + (uint32_t)__popcll(peers);
+  }
+  __syncthreads();
+  // per digit: the waves' counts -> their offsets within the digit's slice
+  // (wh), the tile's count of the digit (lstart, scanned below) and its
+  // global start (gstart, from the scanned histogram)
+  for (uint32_t d = t; d < bins; d += kRadixThreads) {
+    uint32_t run = 0;
+#pragma unroll
+    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) {
+      const uint32_t c = sm.wh[ww][d];
+      sm.wh[ww][d] = run;
+      run += c;
+    }
+    sm.lstart[d] = run;
+    sm.gstart[d] = hist[(uint64_t)d * nb + blockIdx.x] - sub;
+  }
+  __syncthreads();
+  {  // exclusive scan of the tile's digit counts: thread t owns digits 2t, 2t + 1
+    static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");
+    const uint32_t c0 = 2u * t < bins ? sm.lstart[2 * t] : 0u;
+    const uint32_t c1 = 2u * t + 1 < bins ? sm.lstart[2 * t + 1] : 0u;
+    uint32_t inc = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (lane == kWave - 1) sm.wsum[w] = inc;
+    __syncthreads();
+    uint32_t before = 0;
+#pragma unroll
+    for (int ww = 0; ww < kRadixThreads / kWave; ++ww) before += ww < w ? sm.wsum[ww] : 0u;
+    const uint32_t ex = before + inc - (c0 + c1);
+    if (2u * t < bins) sm.lstart[2 * t] = ex;
+    if (2u * t + 1 < bins) sm.lstart[2 * t + 1] = ex + c0;
+  }
+  __syncthreads();
+  // the tile in digit order through LDS, then handed out in index order:
+  // consecutive LDS slots of one digit go to consecutive output positions
+#pragma unroll
+  for (int k = 0; k < kRadixItems; ++k) {
+    if (wbase + (uint64_t)k * kWave + lane < n) {
+      const uint32_t d = (key[k] >> shift) & mask;
+      const uint32_t loc = sm.lstart[d] + sm.wh[w][d] + rank[k];
+      sm.sk[loc] = key[k];
+      sm.sv[loc] = val[k];
+    }
+  }
+  __syncthreads();
+  const uint32_t cnt = (uint32_t)(n - base < (uint64_t)kRadixTile ? n - base : (uint64_t)kRadixTile);
+  for (uint32_t i = t; i < cnt; i += kRadixThreads) {
+    const uint32_t k = sm.sk[i], d = (k >> shift) & mask;
+    const uint32_t ls = sm.lstart[d];
+    const bool run_first = i == ls;
+    epi(sm.gstart[d] + (i - ls), k, sm.sv[i], run_first, run_first ? 0u : sm.sk[i - 1]);
+  }
+}
+
+}  // namespace nts_hip

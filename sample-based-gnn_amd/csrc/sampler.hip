@@ -22,6 +22,7 @@
 //   * CSR transpose = stable radix sort of (local src, edge id) -> identical to
 //     the reference's serial fill order (ascending dst), atomic-free.
 #include "common.hpp"
+#include "radix_tile.hpp"
 
 namespace nts_hip {
 
@@ -1384,28 +1385,118 @@ __device__ __forceinline__ float norm_degree(uint32_t out_src, uint32_t in_dst) 
 // core/ntsFastSampler.hpp:1111-1113); MEAN_SAMPLED by its sampled edge count
 // (the reference GPU kernel get_mean_weight, cuda/ntsCUDATransferKernel.cuh:319-342,
 // which its GPU toolkits never reach: SURVEY Appendix B-5).
-__global__ void k_relabel(const uint32_t* __restrict__ ans, const uint32_t* __restrict__ edst,
-                          const uint32_t* __restrict__ dst, const uint32_t* __restrict__ src_index,
-                          const uint32_t* __restrict__ out_deg, const uint32_t* __restrict__ in_deg,
-                          const uint32_t* __restrict__ co, const uint32_t* sizes,
-                          int weight_type, uint32_t* __restrict__ ri, float* __restrict__ wf,
-                          uint32_t* __restrict__ up_cnt) {
-  const uint32_t e = sizes[1];
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x) {
-    const uint32_t g = ans[k];
-    const uint32_t r = src_index[g];
-    ri[k] = r;
-    if (up_cnt) {
-      atomicAdd(up_cnt + r, 1u);
-    } else if (weight_type != NTS_WEIGHT_NONE) {
-      const uint32_t dg = dst[edst[k]];
-      const uint32_t ind = in_deg[dg];
-      float w = norm_degree(out_deg[g], ind);
-      if (weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
-      if (weight_type == NTS_WEIGHT_MEAN_SAMPLED) w = w / (float)(co[edst[k] + 1] - co[edst[k]]);
-      wf[k] = w;
+struct RelabelArgs {
+  const uint32_t* ans;
+  const uint32_t* edst;
+  const uint32_t* dst;
+  const uint32_t* src_index;
+  const uint32_t* out_deg;
+  const uint32_t* in_deg;
+  const uint32_t* co;
+  const uint32_t* sizes;
+  int weight_type;
+  uint32_t* ri;
+  float* wf;
+  uint32_t* up_cnt;
+};
+
+__device__ __forceinline__ uint32_t relabel_one(const RelabelArgs& a, uint32_t k) {
+  const uint32_t g = a.ans[k];
+  const uint32_t r = a.src_index[g];
+  a.ri[k] = r;
+  if (a.up_cnt) {
+    atomicAdd(a.up_cnt + r, 1u);
+  } else if (a.weight_type != NTS_WEIGHT_NONE) {
+    const uint32_t dg = a.dst[a.edst[k]];
+    const uint32_t ind = a.in_deg[dg];
+    float w = norm_degree(a.out_deg[g], ind);
+    if (a.weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
+    if (a.weight_type == NTS_WEIGHT_MEAN_SAMPLED) w = w / (float)(a.co[a.edst[k] + 1] - a.co[a.edst[k]]);
+    a.wf[k] = w;
+  }
+  return r;
+}
+
+__global__ void k_relabel(RelabelArgs a) {
+  const uint32_t e = a.sizes[1];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x)
+    relabel_one(a, k);
+}
+
+// The CSR transpose's first kernel (the fused sort, csr_sort_fused): one
+// 4096-edge tile per block relabels its edges (k_relabel's work) and counts
+// the local src ids' digits for each of the NP radix passes into `hist`
+// (pass-major, then digit-major [NP][bins][nb], the layout one exclusive scan
+// turns into every pass's output offsets, pass p's shifted by p * e); and
+// presets row_offset[0 .. s] = e for the final pass's atomicMin.
+template <int NP>
+__global__ __launch_bounds__(kRadixThreads) void k_relabel_tiles(RelabelArgs a, uint32_t dbits,
+                                                                 uint32_t* __restrict__ hist,
+                                                                 uint32_t nb, uint32_t* __restrict__ ro) {
+  __shared__ uint32_t h[NP][kRadixMaxBins];
+  const int t = threadIdx.x;
+  const uint32_t bins = 1u << dbits, mask = bins - 1u;
+  for (uint32_t d = t; d < bins; d += kRadixThreads)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) h[p][d] = 0;
+  __syncthreads();
+  const uint32_t e = a.sizes[1];
+  const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+#pragma unroll 4
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
+    if (i < e) {
+      const uint32_t r = relabel_one(a, (uint32_t)i);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) atomicAdd(&h[p][(r >> (p * dbits)) & mask], 1u);
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+    for (uint32_t d = t; d < bins; d += kRadixThreads)
+      hist[((uint64_t)p * bins + d) * nb + blockIdx.x] = h[p][d];
+  const uint32_t s = a.sizes[2];
+  for (uint64_t j = (uint64_t)blockIdx.x * kRadixThreads + t; j <= s;
+       j += (uint64_t)gridDim.x * kRadixThreads)
+    ro[j] = e;
+}
+
+// A pass of the fused CSR sort.  Non-final passes write (key, edge id) to
+// keys_out / vals_out; the final one writes the CSR directly: column index,
+// backward weight and edge id at the edge's CSR position, and row_offset[key]
+// = min over the key's first positions (atomicMin: a row's first edge is
+// either inside its tile's run, prev_key != key, or opens a run).
+struct CsrOut {
+  const uint32_t* edst;
+  const float* wf;
+  uint32_t* ro;
+  uint32_t* ci;
+  float* wb;
+  uint32_t* ceid;
+};
+template <bool FINAL>
+__global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* sizes,
+    uint32_t pass, uint32_t dbits, const uint32_t* __restrict__ hist, uint32_t nb, CsrOut c) {
+  __shared__ RadixTileLds sm;
+  const uint64_t n = sizes[1];
+  if ((uint64_t)blockIdx.x * kRadixTile >= n) return;
+  const uint32_t bins = 1u << dbits;
+  const uint32_t* hp = hist + (uint64_t)pass * bins * nb;
+  radix_scatter_tile(sm, keys_in, vals_in, n, pass * dbits, dbits, hp, nb, pass * (uint32_t)n,
+                     [&](uint32_t pos, uint32_t key, uint32_t val, bool first, uint32_t prev) {
+                       if (!FINAL) {
+                         keys_out[pos] = key;
+                         vals_out[pos] = val;
+                       } else {
+                         c.ci[pos] = c.edst[val];
+                         if (c.ceid) c.ceid[pos] = val;
+                         if (c.wb) c.wb[pos] = c.wf ? c.wf[val] : 0.0f;
+                         if (first || prev != key) atomicMin(c.ro + key, pos);
+                       }
+                     });
 }
 
 // UP_DEGREE weights: out = sampled edges of the src (counted by k_relabel),
@@ -1506,6 +1597,12 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t blk = al(nblk_marks + 1);
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
+  // the fused CSR sort (csr_fused below): every pass's per-tile digit counts
+  // (<= 1536 per tile: NP x 2^dbits with dbits = ceil(bits / NP)) and a
+  // second (key, edge id) buffer for the passes between the first and last
+  const uint32_t nb_csr = std::max(1u, ceil_div(o->e_cap, kRadixTile));
+  const uint64_t csr_hist_n = csr ? al(1536ull * nb_csr + 1) : 0;
+  const uint64_t sort_k2 = csr ? al(o->e_cap) : 0;
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
   // MT19937 modes: per-dst info; the chunked resolver (fanout 1..32) adds the
@@ -1532,7 +1629,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t mt_misc_n = mt_chunked ? 64 : 0;
   const uint64_t mt_n = mt_info_n + mt_base_n + mt_stat_n + mt_w_n + mt_rb_n + mt_win_n +
                         mt_tab_n + mt_ent_n + mt_misc_n;
-  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n) *
+  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n + csr_hist_n +
+                       2 * sort_k2) *
                           sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
   uint32_t* w0 = (uint32_t*)ctx->scratch;
@@ -1543,7 +1641,10 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   uint32_t* t_seid = t_skey + sort_k;
   uint32_t* t_up = t_seid + sort_v;
   uint32_t* t_mt = t_up + up_n;  // MT19937 modes: per-dst MtInfo (16-byte aligned)
-  void* t_sort = (void*)(t_mt + mt_n);
+  uint32_t* t_chist = t_mt + mt_n;
+  uint32_t* t_skey2 = t_chist + csr_hist_n;
+  uint32_t* t_seid2 = t_skey2 + sort_k2;
+  void* t_sort = (void*)(t_seid2 + sort_k2);
 
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
@@ -1703,26 +1804,74 @@ frontier:
     NTS_LAUNCH_CHECK();
   }
 
-  // 4) relabel to local ids + forward weights
+  // 4) relabel to local ids + forward weights; 5) CSR transpose: a stable
+  // radix sort of (local src, edge id) on ceil_log2(s_cap + 1) bits.  Fused
+  // (the default): the relabel kernel counts every pass's digits per tile,
+  // one scan turns them into all passes' offsets, and the last pass writes the
+  // CSR itself — NP + 2 launches instead of 3 NP + 2.  Kept on the generic
+  // sort + k_csr_finalize: the merged frontier (dst_local_id: a dst may have no
+  // out edge, an empty CSR row) and the two-kernel scans (NTS_SCAN1=0).
+  const bool csr_fused = csr && !o->dst_local_id && scan1_enabled();
+  const uint32_t sbits = std::max(1u, ceil_log2((uint64_t)o->s_cap + 1));
+  const uint32_t npass = (sbits + kRadixMaxBits - 1) / kRadixMaxBits;
+  const uint32_t dbits = (sbits + npass - 1) / npass;
+  RelabelArgs ra{o->sample_ans,      o->edge_dst, o->destination, ctx->src_index,
+                 g->out_degree,      g->in_degree, o->column_offset, o->sizes,
+                 weight_type,        o->row_indices, o->edge_weight_forward,
+                 up ? t_up : nullptr};
   if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, o->sample_ans, o->edge_dst,
-                     o->destination, ctx->src_index, g->out_degree, g->in_degree,
-                     o->column_offset, o->sizes, weight_type, o->row_indices,
-                     o->edge_weight_forward, up ? t_up : nullptr);
+  if (csr_fused) {
+    switch (npass) {
+      case 1:
+        hipLaunchKernelGGL(k_relabel_tiles<1>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+                           t_chist, nb_csr, o->row_offset);
+        break;
+      case 2:
+        hipLaunchKernelGGL(k_relabel_tiles<2>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+                           t_chist, nb_csr, o->row_offset);
+        break;
+      case 3:
+        hipLaunchKernelGGL(k_relabel_tiles<3>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+                           t_chist, nb_csr, o->row_offset);
+        break;
+      default:
+        hipLaunchKernelGGL(k_relabel_tiles<4>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+                           t_chist, nb_csr, o->row_offset);
+    }
+  } else {
+    hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, ra);
+  }
   NTS_LAUNCH_CHECK();
   if (up) {
     hipLaunchKernelGGL(k_up_weight, dim3(ge), dim3(256), 0, st, o->row_indices, o->edge_dst,
                        o->column_offset, t_up, o->sizes, weight_type, o->edge_weight_forward);
     NTS_LAUNCH_CHECK();
   }
-
-  // 5) CSR transpose (stable in edge order = ascending local dst)
-  if (csr) {
+  const float* wf_csr = weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward;
+  if (csr_fused) {
+    NTS_RET(scan1_exclusive(ctx, t_chist, t_chist, nullptr, (uint64_t)npass * (1u << dbits) * nb_csr,
+                            st));
+    const CsrOut co{o->edge_dst, wf_csr, o->row_offset, o->column_indices,
+                    o->edge_weight_backward, o->csr_edge_id};
+    const uint32_t* kin = o->row_indices;
+    const uint32_t* vin = nullptr;  // edge ids = item indices
+    for (uint32_t p = 0; p + 1 < npass; ++p) {
+      uint32_t* ko = (p & 1) ? t_skey2 : t_skey;
+      uint32_t* vo = (p & 1) ? t_seid2 : t_seid;
+      hipLaunchKernelGGL(k_csr_scatter<false>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin, vin,
+                         ko, vo, o->sizes, p, dbits, t_chist, nb_csr, co);
+      NTS_LAUNCH_CHECK();
+      kin = ko;
+      vin = vo;
+    }
+    hipLaunchKernelGGL(k_csr_scatter<true>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin, vin,
+                       nullptr, nullptr, o->sizes, npass - 1, dbits, t_chist, nb_csr, co);
+    NTS_LAUNCH_CHECK();
+  } else if (csr) {
     NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
                              ceil_log2((uint64_t)o->s_cap + 1), t_sort, st, ctx));
     hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
-                       weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
-                       o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
+                       wf_csr, o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
                        o->csr_edge_id);
     NTS_LAUNCH_CHECK();
   }

@@ -215,6 +215,9 @@ SampledSubgraph::SampledSubgraph(int device, int layers_, const std::vector<int>
                                       (VertexId)caps[l][2], c, weights));
     if (merge) sampled_sgs.back()->set_merge_src_dst();
   }
+  // every layer's sizes[4] as a view of one device array: one D2H per batch
+  dev_sizes = torch::zeros({std::max(layers, 1) * 4}, u32_opts(device));
+  for (int l = 0; l < layers; ++l) sampled_sgs[l]->sizes = dev_sizes.narrow(0, 4 * l, 4);
   host_sizes = torch::empty({layers * 4}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true));
   hip_rt(hipEventCreateWithFlags(&sampled, hipEventDisableTiming), "hipEventCreate");
   hip_rt(hipEventCreateWithFlags(&consumed, hipEventDisableTiming), "hipEventCreate");
@@ -334,10 +337,9 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   }
   // one D2H of all layer sizes per batch (the reference syncs twice per layer)
   int32_t* hs = ssg->host_sizes.data_ptr<int32_t>();
-  for (int l = 0; l < layer; ++l)
-    hip_rt(hipMemcpyAsync(hs + 4 * l, dptr<uint32_t>(ssg->sampled_sgs[l]->sizes), 16,
-                          hipMemcpyDeviceToHost, st),
-           "hipMemcpyAsync(sizes)");
+  hip_rt(hipMemcpyAsync(hs, dptr<uint32_t>(ssg->dev_sizes), 16 * (size_t)layer,
+                        hipMemcpyDeviceToHost, st),
+         "hipMemcpyAsync(sizes)");
   hip_rt(hipEventRecord(ssg->sampled, st), "hipEventRecord");
   if (host_profile()) fprintf(stderr, "[host] issue total: %.1f us\n", (now_s() - t0) * 1e6);
   ssg->pending_batch = (int)actual;

@@ -157,6 +157,7 @@ class SampledSubgraph {
   std::vector<sampCSC*> sampled_sgs;
   int layers = 0;
   std::vector<int> fanout;
+  torch::Tensor dev_sizes;   // device u32 [layers*4]: the layers' sizes (views)
   torch::Tensor host_sizes;  // pinned int32 [layers*4]
   hipEvent_t sampled = nullptr;   // recorded after the sizes copy of the last issue
   hipEvent_t consumed = nullptr;  // recorded by the trainer once it is done with the slot
