@@ -1484,6 +1484,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
   const uint64_t n = sizes[1];
   if ((uint64_t)blockIdx.x * kRadixTile >= n) return;
   const uint32_t bins = 1u << dbits;
+  const uint32_t s = sizes[2];  // (a key >= s only after a frontier overflow)
   const uint32_t* hp = hist + (uint64_t)pass * bins * nb;
   radix_scatter_tile(sm, keys_in, vals_in, n, pass * dbits, dbits, hp, nb, pass * (uint32_t)n,
                      [&](uint32_t pos, uint32_t key, uint32_t val, bool first, uint32_t prev) {
@@ -1494,7 +1495,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
                          c.ci[pos] = c.edst[val];
                          if (c.ceid) c.ceid[pos] = val;
                          if (c.wb) c.wb[pos] = c.wf ? c.wf[val] : 0.0f;
-                         if (first || prev != key) atomicMin(c.ro + key, pos);
+                         if ((first || prev != key) && key < s) atomicMin(c.ro + key, pos);
                        }
                      });
 }
