@@ -921,76 +921,85 @@ __device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint
 // bulk generation: W[t] = the tempered word at _M_p + t of the stream in
 // mt_state, t < nw (written to *nw_out); rb[b] = raw block b (b = 0: the
 // state's own).  nw = draws + expected extras + 10 sigma + 4096 (<= w_cap).
-constexpr int kGenThreads = 256;
+// One wave, the 624-word block in registers: lane l holds words 64 i + l in
+// x[i] (i < 10; lanes >= 48 of x[9] unused), and the twist's operands are
+// lane rotations of them — cur[k + 1] (x[i] from lane l + 1), cur[k + 397]
+// (x[i + 6] / x[i + 7] from lane l + 13) for k < 227 and nxt[k - 227]
+// (n[i - 4] / n[i - 3] from lane l + 29) above — no LDS and no barrier.
+constexpr int kGenThreads = kWave;
 __global__ __launch_bounds__(kGenThreads) void k_mtp_gen(const uint32_t* __restrict__ mt_state,
                                                         const uint32_t* base, const uint32_t* sizes,
                                                         const float2* cstat, uint32_t w_cap,
                                                         uint32_t* __restrict__ W,
                                                         uint32_t* __restrict__ rb,
                                                         uint32_t* nw_out) {
-  __shared__ uint32_t blk[2][624];
-  __shared__ float red[2][kGenThreads / kWave];
-  const int t = threadIdx.x;
+  const int l = threadIdx.x;
   const uint32_t v = sizes[0];
   const uint32_t nch = (v + kMtChunkP - 1) / kMtChunkP;
   float m = 0.f, var = 0.f;
-  for (uint32_t k = t; k < nch; k += kGenThreads) {
+  for (uint32_t k = l; k < nch; k += kWave) {
     m += cstat[k].x;
     var += cstat[k].y;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    m += __shfl_down(m, o, kWave);
-    var += __shfl_down(var, o, kWave);
+    m += __shfl_xor(m, o, kWave);
+    var += __shfl_xor(var, o, kWave);
   }
-  if ((t & 63) == 0) {
-    red[0][t >> 6] = m;
-    red[1][t >> 6] = var;
-  }
-  for (int k = t; k < 624; k += kGenThreads) {
-    blk[0][k] = mt_state[k];
-    rb[k] = mt_state[k];
-  }
-  __syncthreads();
-  float mm = 0.f, vv = 0.f;
-  for (int w = 0; w < kGenThreads / kWave; ++w) {
-    mm += red[0][w];
-    vv += red[1][w];
-  }
-  const double want = (double)base[v] + (double)mm + 10.0 * sqrt((double)vv) + 4096.0;
+  const double want = (double)base[v] + (double)m + 10.0 * sqrt((double)var) + 4096.0;
   const uint32_t nw = (uint32_t)fmin(want, (double)w_cap);
   const uint32_t q0 = mt_state[624];
-  if (t == 0) *nw_out = nw;
-  for (uint32_t a = q0 + t; a < 624; a += kGenThreads)
-    if (a - q0 < nw) W[a - q0] = mt_temper(blk[0][a]);
+  if (l == 0) *nw_out = nw;
+  uint32_t x[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t k = 64u * i + l;
+    x[i] = k < 624 ? mt_state[k] : 0u;
+    if (k < 624) {
+      rb[k] = x[i];
+      if (k >= q0 && k - q0 < nw) W[k - q0] = mt_temper(x[i]);
+    }
+  }
   const uint32_t U = 0x80000000u, L = 0x7fffffffu, A = 0x9908b0dfu;
+  const int l1 = (l + 1) & 63, l13 = (l + 13) & 63, l29 = (l + 29) & 63;
   for (uint32_t b = 1; 624u * b - q0 < nw; ++b) {
-    const uint32_t* cur = blk[(b - 1) & 1];
-    uint32_t* nxt = blk[b & 1];
-    // _M_gen_rand in three dependent pieces: [0,227) from the current block,
-    // [227,454) and [454,624) from the words just made
-    if (t < 227) {
-      const uint32_t y = (cur[t] & U) | (cur[t + 1] & L);
-      nxt[t] = cur[t + 397] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    uint32_t n[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const uint32_t k = 64u * i + l;
+      // cur[k + 1] (k = 623: nxt[0])
+      uint32_t c1 = __shfl(x[i], l1, kWave);
+      if (i < 9) {
+        const uint32_t h = __builtin_amdgcn_readfirstlane(x[i + 1]);  // lane 0
+        c1 = l == 63 ? h : c1;
+      } else {
+        const uint32_t h = __builtin_amdgcn_readfirstlane(n[0]);
+        c1 = l == 47 ? h : c1;
+      }
+      const uint32_t y = (x[i] & U) | (c1 & L);
+      uint32_t src = 0;
+      if (i <= 3) {  // k < 227 (i = 3: lanes < 35): cur[k + 397]
+        const uint32_t s1 = __shfl(x[i + 6], l13, kWave);
+        const uint32_t s2 = i + 7 <= 9 ? __shfl(x[i + 7 <= 9 ? i + 7 : 9], l13, kWave) : 0u;
+        src = l + 13 < 64 ? s1 : s2;
+      }
+      if (i >= 3) {  // k >= 227: nxt[k - 227]
+        const uint32_t t1 = i >= 4 ? __shfl(n[i >= 4 ? i - 4 : 0], l29, kWave) : 0u;
+        const uint32_t t2 = __shfl(n[i - 3], l29, kWave);
+        const uint32_t nx = l < 35 ? t1 : t2;
+        src = (i > 3 || l >= 35) ? nx : src;
+      }
+      n[i] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
     }
-    __syncthreads();
-    if (t < 227) {
-      const int k = t + 227;
-      const uint32_t y = (cur[k] & U) | (cur[k + 1] & L);
-      nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-    }
-    __syncthreads();
-    if (t < 170) {
-      const int k = t + 454;
-      const uint32_t y = (cur[k] & U) | ((k < 623 ? cur[k + 1] : nxt[0]) & L);
-      nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-    }
-    __syncthreads();
     const uint32_t o = 624u * b - q0;
-    for (int k = t; k < 624; k += kGenThreads) {
-      const uint32_t x = nxt[k];
-      rb[(uint64_t)b * 624 + k] = x;
-      if (o + k < nw) W[o + k] = mt_temper(x);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const uint32_t k = 64u * i + l;
+      x[i] = n[i];
+      if (k < 624) {
+        rb[(uint64_t)b * 624 + k] = n[i];
+        if (o + k < nw) W[o + k] = mt_temper(n[i]);
+      }
     }
   }
 }
