@@ -966,8 +966,7 @@ __global__ __launch_bounds__(kGenThreads) void k_mtp_gen(const uint32_t* __restr
     uint32_t n[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-      const uint32_t k = 64u * i + l;
-      // cur[k + 1] (k = 623: nxt[0])
+      // word k = 64 i + l; cur[k + 1] (k = 623: nxt[0])
       uint32_t c1 = __shfl(x[i], l1, kWave);
       if (i < 9) {
         const uint32_t h = __builtin_amdgcn_readfirstlane(x[i + 1]);  // lane 0
