@@ -25,17 +25,17 @@ struct RadixTileLds {
 // count in LDS (match-any by ballots, no barrier inside the item loop), the
 // tile is reordered by digit in LDS and handed out in runs: epi(pos, key,
 // val, run_first, prev_key) for every item, where pos = its position in the
-// pass's output (digit start from the scanned per-tile histogram `hist`,
-// digit-major [bins][nb], minus `sub`), run_first = it opens its digit's run
-// in this tile, prev_key = the key before it in the output (valid unless
-// run_first).  Consecutive items of a run go to consecutive positions.
-// vals_in == nullptr: values are the item indices.
-template <class Epi>
+// pass's output, run_first = it opens its digit's run in this tile, prev_key
+// = the key before it in the output (valid unless run_first).  Consecutive
+// items of a run go to consecutive positions.  publish(d, count) is told the
+// tile's count of every digit first, then gstart(d, count) returns where the
+// tile's run of digit d starts in the output (each digit by one thread, the
+// same thread for both).  vals_in == nullptr: values are the item indices.
+template <class Pub, class GS, class Epi>
 __device__ __forceinline__ void radix_scatter_tile(RadixTileLds& sm, const uint32_t* __restrict__ keys_in,
                                                    const uint32_t* __restrict__ vals_in, uint64_t n,
-                                                   uint32_t shift, uint32_t dbits,
-                                                   const uint32_t* __restrict__ hist, uint32_t nb,
-                                                   uint32_t sub, Epi&& epi) {
+                                                   uint32_t shift, uint32_t dbits, Pub&& publish,
+                                                   GS&& gstart, Epi&& epi) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
   const uint32_t mask = (1u << dbits) - 1u, bins = mask + 1;
@@ -73,7 +73,7 @@ __device__ __forceinline__ void radix_scatter_tile(RadixTileLds& sm, const uint3
   __syncthreads();
   // per digit: the waves' counts -> their offsets within the digit's slice
   // (wh), the tile's count of the digit (lstart, scanned below) and its
-  // global start (gstart, from the scanned histogram)
+  // start in the output (gstart)
   for (uint32_t d = t; d < bins; d += kRadixThreads) {
     uint32_t run = 0;
 #pragma unroll
@@ -83,8 +83,9 @@ __device__ __forceinline__ void radix_scatter_tile(RadixTileLds& sm, const uint3
       run += c;
     }
     sm.lstart[d] = run;
-    sm.gstart[d] = hist[(uint64_t)d * nb + blockIdx.x] - sub;
+    publish(d, run);
   }
+  for (uint32_t d = t; d < bins; d += kRadixThreads) sm.gstart[d] = gstart(d, sm.lstart[d]);
   __syncthreads();
   {  // exclusive scan of the tile's digit counts: thread t owns digits 2t, 2t + 1
     static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");

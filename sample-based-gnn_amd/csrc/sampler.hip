@@ -1470,11 +1470,17 @@ __global__ __launch_bounds__(kRadixThreads) void k_relabel_tiles(RelabelArgs a, 
     ro[j] = e;
 }
 
-// A pass of the fused CSR sort.  Non-final passes write (key, edge id) to
-// keys_out / vals_out; the final one writes the CSR directly: column index,
-// backward weight and edge id at the edge's CSR position, and row_offset[key]
-// = min over the key's first positions (atomicMin: a row's first edge is
-// either inside its tile's run, prev_key != key, or opens a run).
+// A pass of the fused CSR sort.  Pass 0's tiles are the relabelled edges,
+// whose per-tile digit counts k_relabel_tiles left; a later pass's tiles are
+// the previous pass's output, so their counts are their own: each tile
+// publishes its count of every digit and sums its predecessors' (decoupled
+// look-back per digit over epoch-tagged words, state[tile][digit]) — the
+// digit's global start is the relabel histogram's scanned entry at tile 0.
+// Non-final passes write (key, edge id) to keys_out / vals_out; the final one
+// writes the CSR directly: column index, backward weight and edge id at the
+// edge's CSR position, and row_offset[key] = min over the key's first
+// positions (atomicMin: a row's first edge either follows a different key
+// inside its tile's run, or opens a run).
 struct CsrOut {
   const uint32_t* edst;
   const float* wf;
@@ -1483,29 +1489,70 @@ struct CsrOut {
   float* wb;
   uint32_t* ceid;
 };
+// tile blockIdx.x's count of digit d, published before any look-back
+// (published as the inclusive prefix right away by tile 0)
+__device__ __forceinline__ void digit_publish(uint64_t* __restrict__ state, uint32_t bins,
+                                              uint32_t epoch, uint32_t d, uint32_t cnt) {
+  __hip_atomic_store(state + (uint64_t)blockIdx.x * bins + d,
+                     lb_word(epoch, blockIdx.x == 0 ? 2u : 1u, cnt), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// the tiles before this one: their counts of digit d summed back to the first
+// inclusive prefix; then this tile's inclusive prefix is published
+__device__ __forceinline__ uint32_t digit_lookback(uint64_t* __restrict__ state, uint32_t bins,
+                                                   uint32_t epoch, uint32_t d, uint32_t cnt) {
+  constexpr uint64_t kIncl = 2;
+  const uint32_t tile = blockIdx.x;
+  if (tile == 0) return 0u;
+  uint64_t* st = state + d;  // (tile, d) at st[tile * bins]
+  uint32_t prefix = 0;
+  for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
+    uint64_t w;
+    for (;;) {
+      w = __hip_atomic_load(st + (uint64_t)j * bins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(w >> 34) == (epoch & 0x3FFFFFFFu)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    prefix += (uint32_t)w;
+    if (((w >> 32) & 3u) == kIncl) break;
+  }
+  __hip_atomic_store(st + (uint64_t)tile * bins, lb_word(epoch, kIncl, prefix + cnt),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return prefix;
+}
 template <bool FINAL>
 __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* sizes,
-    uint32_t pass, uint32_t dbits, const uint32_t* __restrict__ hist, uint32_t nb, CsrOut c) {
+    uint32_t pass, uint32_t dbits, const uint32_t* __restrict__ hist, uint32_t nb,
+    uint64_t* __restrict__ state, uint32_t epoch, CsrOut c) {
   __shared__ RadixTileLds sm;
   const uint64_t n = sizes[1];
   if ((uint64_t)blockIdx.x * kRadixTile >= n) return;
   const uint32_t bins = 1u << dbits;
   const uint32_t s = sizes[2];  // (a key >= s only after a frontier overflow)
   const uint32_t* hp = hist + (uint64_t)pass * bins * nb;
-  radix_scatter_tile(sm, keys_in, vals_in, n, pass * dbits, dbits, hp, nb, pass * (uint32_t)n,
-                     [&](uint32_t pos, uint32_t key, uint32_t val, bool first, uint32_t prev) {
-                       if (!FINAL) {
-                         keys_out[pos] = key;
-                         vals_out[pos] = val;
-                       } else {
-                         c.ci[pos] = c.edst[val];
-                         if (c.ceid) c.ceid[pos] = val;
-                         if (c.wb) c.wb[pos] = c.wf ? c.wf[val] : 0.0f;
-                         if ((first || prev != key) && key < s) atomicMin(c.ro + key, pos);
-                       }
-                     });
+  const uint32_t sub = pass * (uint32_t)n;  // the scan ran over every pass's counts
+  radix_scatter_tile(
+      sm, keys_in, vals_in, n, pass * dbits, dbits,
+      [&](uint32_t d, uint32_t cnt) {
+        if (pass != 0) digit_publish(state, bins, epoch, d, cnt);
+      },
+      [&](uint32_t d, uint32_t cnt) {
+        if (pass == 0) return hp[(uint64_t)d * nb + blockIdx.x];
+        return hp[(uint64_t)d * nb] - sub + digit_lookback(state, bins, epoch, d, cnt);
+      },
+      [&](uint32_t pos, uint32_t key, uint32_t val, bool first, uint32_t prev) {
+        if (!FINAL) {
+          keys_out[pos] = key;
+          vals_out[pos] = val;
+        } else {
+          c.ci[pos] = c.edst[val];
+          if (c.ceid) c.ceid[pos] = val;
+          if (c.wb) c.wb[pos] = c.wf ? c.wf[val] : 0.0f;
+          if ((first || prev != key) && key < s) atomicMin(c.ro + key, pos);
+        }
+      });
 }
 
 // UP_DEGREE weights: out = sampled edges of the src (counted by k_relabel),
@@ -1864,17 +1911,20 @@ frontier:
                     o->edge_weight_backward, o->csr_edge_id};
     const uint32_t* kin = o->row_indices;
     const uint32_t* vin = nullptr;  // edge ids = item indices
+    if (npass > 1) NTS_RET(ensure_scan_state(ctx, (uint64_t)nb_csr << dbits));
     for (uint32_t p = 0; p + 1 < npass; ++p) {
       uint32_t* ko = (p & 1) ? t_skey2 : t_skey;
       uint32_t* vo = (p & 1) ? t_seid2 : t_seid;
       hipLaunchKernelGGL(k_csr_scatter<false>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin, vin,
-                         ko, vo, o->sizes, p, dbits, t_chist, nb_csr, co);
+                         ko, vo, o->sizes, p, dbits, t_chist, nb_csr, ctx->scan_state,
+                         p ? scan_next_epoch(ctx) : 0u, co);
       NTS_LAUNCH_CHECK();
       kin = ko;
       vin = vo;
     }
     hipLaunchKernelGGL(k_csr_scatter<true>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin, vin,
-                       nullptr, nullptr, o->sizes, npass - 1, dbits, t_chist, nb_csr, co);
+                       nullptr, nullptr, o->sizes, npass - 1, dbits, t_chist, nb_csr,
+                       ctx->scan_state, npass > 1 ? scan_next_epoch(ctx) : 0u, co);
     NTS_LAUNCH_CHECK();
   } else if (csr) {
     NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
