@@ -1,0 +1,10 @@
+#!/bin/bash
+# Streaming probe of the pair table's sorted sweep (scripts/probe/stream_probe.hip,
+# built in-tree beforehand) and the two pair-table GEMMs alone.
+set -o pipefail
+O=gpurun_out/${1:-r04probe}
+mkdir -p $O
+timeout -k 10 120 scripts/probe/stream_probe 10 > $O/stream.txt 2>&1 || { echo "probe failed"; tail -5 $O/stream.txt; exit 1; }
+cat $O/stream.txt
+timeout -k 10 200 python -u scripts/micro_bottom.py > $O/micro_bottom.json 2> $O/micro_bottom.err || { echo "micro_bottom failed"; tail -5 $O/micro_bottom.err; exit 1; }
+cat $O/micro_bottom.json
