@@ -310,8 +310,23 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
           atomicMax(&smax[col], __float_as_uint(fabsf(vcomp<VEC>(acc[c], q) * rsd)));
       }
   };
-  for (uint32_t d = blockIdx.x * GPB + grp; d < n; d += gridDim.x * GPB) {
-    const uint32_t beg = off[d], end = off[d + 1];
+  // the next row's offsets are loaded while this row is gathered (one
+  // dependent load fewer per row: off -> idx -> rows becomes idx -> rows)
+  uint32_t d = blockIdx.x * GPB + grp;
+  uint32_t nbeg = 0, nend = 0;
+  if (d < n) {
+    nbeg = off[d];
+    nend = off[d + 1];
+  }
+  for (; d < n; d += gridDim.x * GPB) {
+    const uint32_t beg = nbeg, end = nend;
+    {
+      const uint32_t dn = d + gridDim.x * GPB;
+      if (dn < n) {
+        nbeg = off[dn];
+        nend = off[dn + 1];
+      }
+    }
     if (COOP && end - beg > kLongRow<U>()) {  // summed by the whole block below
       if (sl == 0) long_rows[atomicAdd(&n_long, 1u)] = d;
       continue;
