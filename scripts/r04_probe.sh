@@ -12,3 +12,4 @@ timeout -k 10 200 python -u scripts/micro_agg.py > $O/micro_agg.json 2> $O/micro
 cat $O/micro_agg.json
 timeout -k 10 400 python -u -m pytest tests/test_hip_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -k "spmm or csr or agg" > $O/agg_tests.log 2>&1 || { echo "agg tests failed"; tail -30 $O/agg_tests.log; exit 1; }
 tail -1 $O/agg_tests.log
+bash scripts/bench_configs.sh r04 || exit 1
