@@ -131,6 +131,9 @@ __device__ __forceinline__ float vcomp(const typename VT<VEC>::T& v, int q) {
 
 // acc[c] += sum over the edges [beg, end) in edge order of w[e] * row(e)[col],
 // col = c0 + sl + c * LPD (one LPD-lane group, see k_spmm_gather)
+// pre: the row's first chunk of edge ids / weights was loaded by the caller
+// (lane sl: entry beg + sl, raw id before MAP/TIER) — one row ahead, so that
+// the chain per row is the row loads alone
 template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER, int MODE>
 __device__ __forceinline__ void gather_edges(typename VT<VEC>::T (&acc)[NCH], uint32_t beg,
                                              uint32_t end, uint32_t c0, int sl,
@@ -138,7 +141,9 @@ __device__ __forceinline__ void gather_edges(typename VT<VEC>::T (&acc)[NCH], ui
                                              const float* __restrict__ w,
                                              const float* __restrict__ x, uint64_t ldx,
                                              const uint32_t* __restrict__ map, uint32_t nv,
-                                             const Tier& tier, const AggExtra& ax) {
+                                             const Tier& tier, const AggExtra& ax,
+                                             bool pre = false, uint32_t pre_r = 0,
+                                             float pre_w = 0.f) {
   using V = VT<VEC>;
   using T = typename V::T;
   for (uint32_t cb = beg; cb < end; cb += LPD) {
@@ -146,8 +151,13 @@ __device__ __forceinline__ void gather_edges(typename VT<VEC>::T (&acc)[NCH], ui
     uint32_t my_r = 0;
     float my_w = 0.f;
     if ((uint32_t)sl < ne) {  // streamed once: do not keep in cache
-      my_r = __builtin_nontemporal_load(idx + cb + sl);
-      my_w = w ? __builtin_nontemporal_load(w + cb + sl) : 1.0f;
+      if (pre && cb == beg) {
+        my_r = pre_r;
+        my_w = pre_w;
+      } else {
+        my_r = __builtin_nontemporal_load(idx + cb + sl);
+        my_w = w ? __builtin_nontemporal_load(w + cb + sl) : 1.0f;
+      }
       const uint32_t loc = my_r;
       if (MAP) my_r = map[my_r];
       if (TIER) {
@@ -310,24 +320,47 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
           atomicMax(&smax[col], __float_as_uint(fabsf(vcomp<VEC>(acc[c], q) * rsd)));
       }
   };
-  // the next row's offsets are loaded while this row is gathered (one
-  // dependent load fewer per row: off -> idx -> rows becomes idx -> rows)
-  uint32_t d = blockIdx.x * GPB + grp;
-  uint32_t nbeg = 0, nend = 0;
-  if (d < n) {
-    nbeg = off[d];
-    nend = off[d + 1];
-  }
-  for (; d < n; d += gridDim.x * GPB) {
-    const uint32_t beg = nbeg, end = nend;
-    {
-      const uint32_t dn = d + gridDim.x * GPB;
-      if (dn < n) {
-        nbeg = off[dn];
-        nend = off[dn + 1];
-      }
+  // software pipeline over the group's rows: the offsets two rows ahead and
+  // the first chunk of edge ids / weights one row ahead are loaded while this
+  // row is gathered (the chain per row off -> ids -> rows becomes the rows)
+  const uint32_t stride = gridDim.x * GPB;
+  auto first_chunk = [&](uint32_t b, uint32_t e, uint32_t& r, float& wt) {
+    r = 0;
+    wt = 0.f;
+    if ((uint32_t)sl < e - b) {
+      r = __builtin_nontemporal_load(idx + b + sl);
+      wt = w ? __builtin_nontemporal_load(w + b + sl) : 1.0f;
     }
-    if (COOP && end - beg > kLongRow<U>()) {  // summed by the whole block below
+  };
+  uint32_t d = blockIdx.x * GPB + grp;
+  uint32_t beg = 0, end = 0, beg1 = 0, end1 = 0, pr = 0;
+  float pw = 0.f;
+  if (d < n) {
+    beg = off[d];
+    end = off[d + 1];
+  }
+  if (d + stride < n) {
+    beg1 = off[d + stride];
+    end1 = off[d + stride + 1];
+  }
+  first_chunk(beg, end, pr, pw);
+  for (; d < n; d += stride) {
+    uint32_t beg2 = 0, end2 = 0, pr1, dn2 = d + 2 * stride;
+    float pw1;
+    if (dn2 < n) {
+      beg2 = off[dn2];
+      end2 = off[dn2 + 1];
+    }
+    first_chunk(beg1, end1, pr1, pw1);
+    const uint32_t cbeg = beg, cend = end, cpr = pr;
+    const float cpw = pw;
+    beg = beg1;
+    end = end1;
+    beg1 = beg2;
+    end1 = end2;
+    pr = pr1;
+    pw = pw1;
+    if (COOP && cend - cbeg > kLongRow<U>()) {  // summed by the whole block below
       if (sl == 0) long_rows[atomicAdd(&n_long, 1u)] = d;
       continue;
     }
@@ -346,8 +379,8 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
           pm[c] = col < nv ? mrow[col] : V::zero();
         }
       }
-      gather_edges<VEC, LPD, NCH, MAP, U, TIER, EM>(acc, beg, end, c0, sl, idx, w, x, ldx, map,
-                                                      nv, tier, ax);
+      gather_edges<VEC, LPD, NCH, MAP, U, TIER, EM>(acc, cbeg, cend, c0, sl, idx, w, x, ldx, map,
+                                                      nv, tier, ax, true, cpr, cpw);
       if constexpr (MODE == kAggPostMask) {  // same arithmetic as store_row's
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
