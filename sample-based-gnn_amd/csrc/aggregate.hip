@@ -278,9 +278,22 @@ __device__ __forceinline__ void store_row(typename VT<VEC>::T (&acc)[NCH], uint3
 template <int U>
 constexpr uint32_t kLongRow() { return 4 * U; }
 
+// Row software pipeline of k_spmm_gather (compile-time A/B, probe builds:
+// make probe EXTRA=-DNTS_AGG_PF=n): 0 none, 1 the next row's offsets, 2 the
+// offsets two rows ahead and the first id/weight chunk one row ahead; and the
+// waves-per-SIMD floor of its single-chunk instances (0: the compiler's choice)
+#ifndef NTS_AGG_PF
+#define NTS_AGG_PF 2
+#endif
+#ifndef NTS_AGG_WPE
+#define NTS_AGG_WPE 0
+#endif
+constexpr int kAggPf = NTS_AGG_PF;
+constexpr int kAggWpe = NTS_AGG_WPE == 0 ? 1 : NTS_AGG_WPE;
+
 template <int VEC, int LPD, int NCH, bool MAP, int U, bool TIER, int MODE = kAggPlain,
           bool COOP = false>
-__global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
+__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(NCH == 1 ? kAggWpe : 1))) void k_spmm_gather(
     const uint32_t* __restrict__ off, const uint32_t* __restrict__ idx,
     const float* __restrict__ w, const uint32_t* n_dev, uint32_t n_cap,
     const float* __restrict__ x, uint64_t ldx, const uint32_t* __restrict__ map, uint32_t nv,
@@ -335,31 +348,47 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
   uint32_t d = blockIdx.x * GPB + grp;
   uint32_t beg = 0, end = 0, beg1 = 0, end1 = 0, pr = 0;
   float pw = 0.f;
-  if (d < n) {
+  if (kAggPf >= 1 && d < n) {
     beg = off[d];
     end = off[d + 1];
   }
-  if (d + stride < n) {
+  if (kAggPf >= 2 && d + stride < n) {
     beg1 = off[d + stride];
     end1 = off[d + stride + 1];
   }
-  first_chunk(beg, end, pr, pw);
+  if (kAggPf >= 2) first_chunk(beg, end, pr, pw);
   for (; d < n; d += stride) {
-    uint32_t beg2 = 0, end2 = 0, pr1, dn2 = d + 2 * stride;
-    float pw1;
-    if (dn2 < n) {
-      beg2 = off[dn2];
-      end2 = off[dn2 + 1];
+    uint32_t cbeg, cend, cpr = 0;
+    float cpw = 0.f;
+    if constexpr (kAggPf == 0) {
+      cbeg = off[d];
+      cend = off[d + 1];
+    } else if constexpr (kAggPf == 1) {
+      cbeg = beg;
+      cend = end;
+      if (d + stride < n) {
+        beg = off[d + stride];
+        end = off[d + stride + 1];
+      }
+    } else {
+      uint32_t beg2 = 0, end2 = 0, pr1, dn2 = d + 2 * stride;
+      float pw1;
+      if (dn2 < n) {
+        beg2 = off[dn2];
+        end2 = off[dn2 + 1];
+      }
+      first_chunk(beg1, end1, pr1, pw1);
+      cbeg = beg;
+      cend = end;
+      cpr = pr;
+      cpw = pw;
+      beg = beg1;
+      end = end1;
+      beg1 = beg2;
+      end1 = end2;
+      pr = pr1;
+      pw = pw1;
     }
-    first_chunk(beg1, end1, pr1, pw1);
-    const uint32_t cbeg = beg, cend = end, cpr = pr;
-    const float cpw = pw;
-    beg = beg1;
-    end = end1;
-    beg1 = beg2;
-    end1 = end2;
-    pr = pr1;
-    pw = pw1;
     if (COOP && cend - cbeg > kLongRow<U>()) {  // summed by the whole block below
       if (sl == 0) long_rows[atomicAdd(&n_long, 1u)] = d;
       continue;
@@ -380,7 +409,7 @@ __global__ __launch_bounds__(kAggThreads) void k_spmm_gather(
         }
       }
       gather_edges<VEC, LPD, NCH, MAP, U, TIER, EM>(acc, cbeg, cend, c0, sl, idx, w, x, ldx, map,
-                                                      nv, tier, ax, true, cpr, cpw);
+                                                      nv, tier, ax, kAggPf >= 2, cpr, cpw);
       if constexpr (MODE == kAggPostMask) {  // same arithmetic as store_row's
 #pragma unroll
         for (int c = 0; c < NCH; ++c)

@@ -22,20 +22,19 @@ struct RadixTileLds {
 
 // Tile blockIdx.x of a pass over n items (base = blockIdx.x * kRadixTile < n):
 // each wave ranks its 1,024 contiguous items against a running per-wave digit
-// count in LDS (match-any by ballots, no barrier inside the item loop), the
-// tile is reordered by digit in LDS and handed out in runs: epi(pos, key,
-// val, run_first, prev_key) for every item, where pos = its position in the
-// pass's output, run_first = it opens its digit's run in this tile, prev_key
-// = the key before it in the output (valid unless run_first).  Consecutive
-// items of a run go to consecutive positions.  publish(d, count) is told the
-// tile's count of every digit first, then gstart(d, count) returns where the
-// tile's run of digit d starts in the output (each digit by one thread, the
-// same thread for both).  vals_in == nullptr: values are the item indices.
-template <class Pub, class GS, class Epi>
-__device__ __forceinline__ void radix_scatter_tile(RadixTileLds& sm, const uint32_t* __restrict__ keys_in,
-                                                   const uint32_t* __restrict__ vals_in, uint64_t n,
-                                                   uint32_t shift, uint32_t dbits, Pub&& publish,
-                                                   GS&& gstart, Epi&& epi) {
+// count in LDS (match-any by ballots, no barrier inside the item loop) and the
+// tile is reordered by digit in LDS: on return sm.sk / sm.sv hold it in digit
+// order (stable), and item i of that order goes to output position
+// radix_tile_pos(sm, i, ...) — consecutive items of a digit's run to
+// consecutive positions.  publish(d, count) is told the tile's count of every
+// digit first, then gstart(d, count) returns where the tile's run of digit d
+// starts in the output (each digit by one thread, the same thread for both).
+// vals_in == nullptr: values are the item indices.
+template <class Pub, class GS>
+__device__ __forceinline__ void radix_tile_order(RadixTileLds& sm, const uint32_t* __restrict__ keys_in,
+                                                 const uint32_t* __restrict__ vals_in, uint64_t n,
+                                                 uint32_t shift, uint32_t dbits, Pub&& publish,
+                                                 GS&& gstart) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
   const uint32_t mask = (1u << dbits) - 1u, bins = mask + 1;
@@ -119,13 +118,17 @@ __device__ __forceinline__ void radix_scatter_tile(RadixTileLds& sm, const uint3
     }
   }
   __syncthreads();
-  const uint32_t cnt = (uint32_t)(n - base < (uint64_t)kRadixTile ? n - base : (uint64_t)kRadixTile);
-  for (uint32_t i = t; i < cnt; i += kRadixThreads) {
-    const uint32_t k = sm.sk[i], d = (k >> shift) & mask;
-    const uint32_t ls = sm.lstart[d];
-    const bool run_first = i == ls;
-    epi(sm.gstart[d] + (i - ls), k, sm.sv[i], run_first, run_first ? 0u : sm.sk[i - 1]);
-  }
+}
+
+// the tile's item count, and the output position of item i of the digit order
+__device__ __forceinline__ uint32_t radix_tile_count(uint64_t n) {
+  const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+  return (uint32_t)(n - base < (uint64_t)kRadixTile ? n - base : (uint64_t)kRadixTile);
+}
+__device__ __forceinline__ uint32_t radix_tile_pos(const RadixTileLds& sm, uint32_t i, uint32_t key,
+                                                   uint32_t shift, uint32_t mask) {
+  const uint32_t d = (key >> shift) & mask;
+  return sm.gstart[d] + (i - sm.lstart[d]);
 }
 
 }  // namespace nts_hip

@@ -1437,36 +1437,73 @@ __global__ void k_relabel(RelabelArgs a) {
 // (pass-major, then digit-major [NP][bins][nb], the layout one exclusive scan
 // turns into every pass's output offsets, pass p's shifted by p * e); and
 // presets row_offset[0 .. s] = e for the final pass's atomicMin.
+constexpr int kRelabelThreads = 1024;  // 4 edges per thread: 16 waves per tile in flight
 template <int NP>
-__global__ __launch_bounds__(kRadixThreads) void k_relabel_tiles(RelabelArgs a, uint32_t dbits,
-                                                                 uint32_t* __restrict__ hist,
-                                                                 uint32_t nb, uint32_t* __restrict__ ro) {
+__global__ __launch_bounds__(kRelabelThreads) void k_relabel_tiles(RelabelArgs a, uint32_t dbits,
+                                                                   uint32_t* __restrict__ hist,
+                                                                   uint32_t nb, uint32_t* __restrict__ ro) {
   __shared__ uint32_t h[NP][kRadixMaxBins];
   const int t = threadIdx.x;
   const uint32_t bins = 1u << dbits, mask = bins - 1u;
-  for (uint32_t d = t; d < bins; d += kRadixThreads)
+  for (uint32_t d = t; d < bins; d += kRelabelThreads)
 #pragma unroll
     for (int p = 0; p < NP; ++p) h[p][d] = 0;
   __syncthreads();
   const uint32_t e = a.sizes[1];
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-#pragma unroll 4
-  for (int k = 0; k < kRadixItems; ++k) {
-    const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
-    if (i < e) {
-      const uint32_t r = relabel_one(a, (uint32_t)i);
+  constexpr int kPer = kRadixTile / kRelabelThreads;
+  // relabel_one's loads for the thread's kPer edges in dependency phases (the
+  // stores of one edge would otherwise hold back the loads of the next)
+  uint32_t g[kPer], ed[kPer], r[kPer], od[kPer], dg[kPer], cnt[kPer];
+  bool ok[kPer];
+  const bool wts = a.weight_type != NTS_WEIGHT_NONE && !a.up_cnt;
 #pragma unroll
-      for (int p = 0; p < NP; ++p) atomicAdd(&h[p][(r >> (p * dbits)) & mask], 1u);
+  for (int k = 0; k < kPer; ++k) {
+    const uint64_t i = base + (uint64_t)k * kRelabelThreads + t;
+    ok[k] = i < e;
+    g[k] = ok[k] ? a.ans[i] : 0u;
+    ed[k] = ok[k] && wts ? a.edst[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    r[k] = ok[k] ? a.src_index[g[k]] : 0u;
+    od[k] = ok[k] && wts ? a.out_deg[g[k]] : 0u;
+    dg[k] = ok[k] && wts ? a.dst[ed[k]] : 0u;
+    cnt[k] = ok[k] && wts && a.weight_type == NTS_WEIGHT_MEAN_SAMPLED
+                 ? a.co[ed[k] + 1] - a.co[ed[k]]
+                 : 1u;
+  }
+  uint32_t indg[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) indg[k] = ok[k] && wts ? a.in_deg[dg[k]] : 1u;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (!ok[k]) continue;
+    const uint64_t i = base + (uint64_t)k * kRelabelThreads + t;
+    a.ri[i] = r[k];
+    if (a.up_cnt) {
+      atomicAdd(a.up_cnt + r[k], 1u);
+    } else if (wts) {  // relabel_one's arithmetic
+      const uint32_t ind = indg[k];
+      float w = norm_degree(od[k], ind);
+      if (a.weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
+      if (a.weight_type == NTS_WEIGHT_MEAN_SAMPLED) w = w / (float)cnt[k];
+      a.wf[i] = w;
     }
   }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    if (base + (uint64_t)k * kRelabelThreads + t < e)
+#pragma unroll
+      for (int p = 0; p < NP; ++p) atomicAdd(&h[p][(r[k] >> (p * dbits)) & mask], 1u);
   __syncthreads();
 #pragma unroll
   for (int p = 0; p < NP; ++p)
-    for (uint32_t d = t; d < bins; d += kRadixThreads)
+    for (uint32_t d = t; d < bins; d += kRelabelThreads)
       hist[((uint64_t)p * bins + d) * nb + blockIdx.x] = h[p][d];
   const uint32_t s = a.sizes[2];
-  for (uint64_t j = (uint64_t)blockIdx.x * kRadixThreads + t; j <= s;
-       j += (uint64_t)gridDim.x * kRadixThreads)
+  for (uint64_t j = (uint64_t)blockIdx.x * kRelabelThreads + t; j <= s;
+       j += (uint64_t)gridDim.x * kRelabelThreads)
     ro[j] = e;
 }
 
@@ -1533,7 +1570,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
   const uint32_t s = sizes[2];  // (a key >= s only after a frontier overflow)
   const uint32_t* hp = hist + (uint64_t)pass * bins * nb;
   const uint32_t sub = pass * (uint32_t)n;  // the scan ran over every pass's counts
-  radix_scatter_tile(
+  radix_tile_order(
       sm, keys_in, vals_in, n, pass * dbits, dbits,
       [&](uint32_t d, uint32_t cnt) {
         if (pass != 0) digit_publish(state, bins, epoch, d, cnt);
@@ -1541,18 +1578,52 @@ __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
       [&](uint32_t d, uint32_t cnt) {
         if (pass == 0) return hp[(uint64_t)d * nb + blockIdx.x];
         return hp[(uint64_t)d * nb] - sub + digit_lookback(state, bins, epoch, d, cnt);
-      },
-      [&](uint32_t pos, uint32_t key, uint32_t val, bool first, uint32_t prev) {
-        if (!FINAL) {
-          keys_out[pos] = key;
-          vals_out[pos] = val;
-        } else {
-          c.ci[pos] = c.edst[val];
-          if (c.ceid) c.ceid[pos] = val;
-          if (c.wb) c.wb[pos] = c.wf ? c.wf[val] : 0.0f;
-          if ((first || prev != key) && key < s) atomicMin(c.ro + key, pos);
-        }
       });
+  const uint32_t cnt = radix_tile_count(n), shift = pass * dbits, mask = bins - 1u;
+  const int t = threadIdx.x;
+  if (!FINAL) {
+    for (uint32_t i = t; i < cnt; i += kRadixThreads) {
+      const uint32_t k = sm.sk[i], pos = radix_tile_pos(sm, i, k, shift, mask);
+      keys_out[pos] = k;
+      vals_out[pos] = sm.sv[i];
+    }
+    return;
+  }
+  // final pass, in phases over the thread's items (LDS, then the edge
+  // gathers, then the stores) so that its random loads are all in flight
+  constexpr int kPer = kRadixTile / kRadixThreads;
+  uint32_t key[kPer], val[kPer], pos[kPer], cv[kPer];
+  float wv[kPer];
+  bool first[kPer];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const uint32_t i = t + q * kRadixThreads;
+    key[q] = val[q] = pos[q] = 0;
+    first[q] = false;
+    if (i < cnt) {
+      key[q] = sm.sk[i];
+      val[q] = sm.sv[i];
+      const uint32_t d = (key[q] >> shift) & mask, ls = sm.lstart[d];
+      pos[q] = sm.gstart[d] + (i - ls);
+      first[q] = i == ls || sm.sk[i - 1] != key[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const bool ok = t + q * kRadixThreads < cnt;
+    cv[q] = ok ? c.edst[val[q]] : 0u;
+    wv[q] = ok && c.wf ? c.wf[val[q]] : 0.0f;
+  }
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    if (t + q * kRadixThreads >= cnt) continue;
+    c.ci[pos[q]] = cv[q];
+    if (c.ceid) c.ceid[pos[q]] = val[q];
+    if (c.wb) c.wb[pos[q]] = wv[q];
+    // a row's first edge either follows a different key inside its tile's
+    // run or opens a run (then an earlier tile may hold the key too)
+    if (first[q] && key[q] < s) atomicMin(c.ro + key[q], pos[q]);
+  }
 }
 
 // UP_DEGREE weights: out = sampled edges of the src (counted by k_relabel),
@@ -1879,19 +1950,19 @@ frontier:
   if (csr_fused) {
     switch (npass) {
       case 1:
-        hipLaunchKernelGGL(k_relabel_tiles<1>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+        hipLaunchKernelGGL(k_relabel_tiles<1>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
                            t_chist, nb_csr, o->row_offset);
         break;
       case 2:
-        hipLaunchKernelGGL(k_relabel_tiles<2>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+        hipLaunchKernelGGL(k_relabel_tiles<2>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
                            t_chist, nb_csr, o->row_offset);
         break;
       case 3:
-        hipLaunchKernelGGL(k_relabel_tiles<3>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+        hipLaunchKernelGGL(k_relabel_tiles<3>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
                            t_chist, nb_csr, o->row_offset);
         break;
       default:
-        hipLaunchKernelGGL(k_relabel_tiles<4>, dim3(nb_csr), dim3(kRadixThreads), 0, st, ra, dbits,
+        hipLaunchKernelGGL(k_relabel_tiles<4>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
                            t_chist, nb_csr, o->row_offset);
     }
   } else {
