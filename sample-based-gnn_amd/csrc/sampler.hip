@@ -877,18 +877,29 @@ __device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W,
     for (int b = 0; b < a; ++b)
       if ((uint32_t)a < n) clean &= val[a] != val[b];
   if (clean) return n;
-  uint32_t cnt = 0, q = p;
+  // the sequential walk, its words fetched 16 at a time (one memory latency
+  // per 16 words, not per word: a dst whose degree is close to n needs many)
+  uint32_t cnt = 0, q = p, end = p;
   while (cnt < n) {
-    uint32_t x;
-    const bool ok = mt_apply(q < nw ? W[q] : 0u, deg, thr, lemire, x);
-    ++q;
-    if (!ok) continue;
-    bool dup = false;
-    for (uint32_t k = 0; k < cnt; ++k) dup |= lst[k * lstride] == x;
-    if (!dup) lst[(cnt++) * lstride] = x;
+    uint32_t buf[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) buf[j] = q + j < nw ? W[q + j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (cnt >= n) break;
+      uint32_t x;
+      if (!mt_apply(buf[j], deg, thr, lemire, x)) continue;
+      bool dup = false;
+      for (uint32_t k = 0; k < cnt; ++k) dup |= lst[k * lstride] == x;
+      if (!dup) {
+        lst[(cnt++) * lstride] = x;
+        end = q + j + 1;
+      }
+    }
+    q += 16;
     if (q - p > 1u << 20) break;  // (unreachable for deg > n) keep every lane finite
   }
-  return q - p;
+  return (cnt >= n ? end : q) - p;
 }
 
 // words consumed by one dst whose draws start at the first of the NW words in
