@@ -886,14 +886,14 @@ __device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W,
     for (int j = 0; j < 16; ++j) buf[j] = q + j < nw ? W[q + j] : 0u;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      if (cnt >= n) break;
       uint32_t x;
-      if (!mt_apply(buf[j], deg, thr, lemire, x)) continue;
-      bool dup = false;
-      for (uint32_t k = 0; k < cnt; ++k) dup |= lst[k * lstride] == x;
-      if (!dup) {
-        lst[(cnt++) * lstride] = x;
-        end = q + j + 1;
+      if (cnt < n && mt_apply(buf[j], deg, thr, lemire, x)) {
+        bool dup = false;
+        for (uint32_t k = 0; k < cnt; ++k) dup |= lst[k * lstride] == x;
+        if (!dup) {
+          lst[(cnt++) * lstride] = x;
+          end = q + j + 1;
+        }
       }
     }
     q += 16;
