@@ -278,12 +278,17 @@ __device__ __forceinline__ void store_row(typename VT<VEC>::T (&acc)[NCH], uint3
 template <int U>
 constexpr uint32_t kLongRow() { return 4 * U; }
 
-// Row software pipeline of k_spmm_gather (compile-time A/B, probe builds:
-// make probe EXTRA=-DNTS_AGG_PF=n): 0 none, 1 the next row's offsets, 2 the
-// offsets two rows ahead and the first id/weight chunk one row ahead; and the
-// waves-per-SIMD floor of its single-chunk instances (0: the compiler's choice)
+// Row software pipeline of k_spmm_gather (compile-time A/B builds, `make
+// variant`): 0 none, 1 the next row's offsets, 2 the offsets two rows ahead
+// and the first id/weight chunk one row ahead; and the waves-per-SIMD floor of
+// its single-chunk instances (0: the compiler's choice).  Measured at C2 size
+// (scripts/micro_agg.py, r04): bottom fwd / CSR bwd 103.7 / 121.7 us with 0,
+// 105.9 / 130.5 with 1, 102.3 / 130.6 with 2, 114.4 / 152.1 with 2 and a
+// floor of 6 waves (spills) — the prefetch registers cost a wave per SIMD
+// (occupancy 6 -> 5) and the gather needs the waves more than the shorter
+// chain, so 0 stays
 #ifndef NTS_AGG_PF
-#define NTS_AGG_PF 2
+#define NTS_AGG_PF 0
 #endif
 #ifndef NTS_AGG_WPE
 #define NTS_AGG_WPE 0

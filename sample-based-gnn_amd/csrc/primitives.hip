@@ -505,8 +505,11 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
   __shared__ RadixTileLds sm;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   if ((uint64_t)blockIdx.x * kRadixTile >= n) return;  // whole tile past the end
-  radix_tile_order(sm, keys_in, vals_in, n, shift, dbits, [](uint32_t, uint32_t) {},
-                   [&](uint32_t d, uint32_t) { return hist[(uint64_t)d * nb + blockIdx.x]; });
+  const uint32_t bins = 1u << dbits;
+  radix_tile_order(sm, keys_in, vals_in, n, shift, dbits, [](uint32_t, uint32_t) {}, [&] {
+    for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
+      sm.gstart[d] = hist[(uint64_t)d * nb + blockIdx.x];
+  });
   const uint32_t cnt = radix_tile_count(n), mask = (1u << dbits) - 1u;
   for (uint32_t i = threadIdx.x; i < cnt; i += kRadixThreads) {
     const uint32_t k = sm.sk[i], pos = radix_tile_pos(sm, i, k, shift, mask);

@@ -27,8 +27,9 @@ struct RadixTileLds {
 // order (stable), and item i of that order goes to output position
 // radix_tile_pos(sm, i, ...) — consecutive items of a digit's run to
 // consecutive positions.  publish(d, count) is told the tile's count of every
-// digit first, then gstart(d, count) returns where the tile's run of digit d
-// starts in the output (each digit by one thread, the same thread for both).
+// digit first (digit d by thread d % 256), then each thread's gstart() sets
+// sm.gstart[d] — where the tile's run of digit d starts in the output — for
+// its digits d = t, t + 256 (< bins), their counts in sm.lstart[d].
 // vals_in == nullptr: values are the item indices.
 template <class Pub, class GS>
 __device__ __forceinline__ void radix_tile_order(RadixTileLds& sm, const uint32_t* __restrict__ keys_in,
@@ -84,7 +85,7 @@ __device__ __forceinline__ void radix_tile_order(RadixTileLds& sm, const uint32_
     sm.lstart[d] = run;
     publish(d, run);
   }
-  for (uint32_t d = t; d < bins; d += kRadixThreads) sm.gstart[d] = gstart(d, sm.lstart[d]);
+  gstart();  // sm.gstart of this thread's digits (t, t + 256) from their counts in sm.lstart
   __syncthreads();
   {  // exclusive scan of the tile's digit counts: thread t owns digits 2t, 2t + 1
     static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");

@@ -1537,36 +1537,84 @@ struct CsrOut {
   float* wb;
   uint32_t* ceid;
 };
-// tile blockIdx.x's count of digit d, published before any look-back
-// (published as the inclusive prefix right away by tile 0)
-__device__ __forceinline__ void digit_publish(uint64_t* __restrict__ state, uint32_t bins,
+// Look-back state of the passes after the first: word (digit d, tile j) at
+// state[d * nb + j] = {epoch, kind, value}: the tile's count of the digit
+// (kind 1) or its inclusive prefix over tiles 0..j (kind 2).
+__device__ __forceinline__ void digit_publish(uint64_t* __restrict__ state, uint32_t nb,
                                               uint32_t epoch, uint32_t d, uint32_t cnt) {
-  __hip_atomic_store(state + (uint64_t)blockIdx.x * bins + d,
+  __hip_atomic_store(state + (uint64_t)d * nb + blockIdx.x,
                      lb_word(epoch, blockIdx.x == 0 ? 2u : 1u, cnt), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-// the tiles before this one: their counts of digit d summed back to the first
-// inclusive prefix; then this tile's inclusive prefix is published
-__device__ __forceinline__ uint32_t digit_lookback(uint64_t* __restrict__ state, uint32_t bins,
-                                                   uint32_t epoch, uint32_t d, uint32_t cnt) {
+// The thread's digits (t and t + 256 < bins): their exclusive prefixes over
+// the tiles before this one, eight predecessors read per step (all loads of
+// a step in flight together; a word from an older epoch is read again) back
+// to the nearest inclusive prefix; then this tile's inclusive prefixes are
+// published and sm.gstart set.
+constexpr int kLbWin = 8;
+__device__ __forceinline__ void digit_lookback(RadixTileLds& sm, uint64_t* __restrict__ state,
+                                               uint32_t nb, uint32_t bins, uint32_t epoch,
+                                               const uint32_t* __restrict__ hp, uint32_t sub) {
   constexpr uint64_t kIncl = 2;
-  const uint32_t tile = blockIdx.x;
-  if (tile == 0) return 0u;
-  uint64_t* st = state + d;  // (tile, d) at st[tile * bins]
-  uint32_t prefix = 0;
-  for (int64_t j = (int64_t)tile - 1; j >= 0; --j) {
-    uint64_t w;
-    for (;;) {
-      w = __hip_atomic_load(st + (uint64_t)j * bins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)(w >> 34) == (epoch & 0x3FFFFFFFu)) break;
+  const uint32_t t = threadIdx.x, tile = blockIdx.x, ep = epoch & 0x3FFFFFFFu;
+  const uint32_t nd = t + kRadixThreads < bins ? 2u : (t < bins ? 1u : 0u);
+  uint32_t pref[2] = {0u, 0u};
+  bool done[2] = {tile == 0 || nd < 1, tile == 0 || nd < 2};
+  int64_t top = (int64_t)tile - 1;
+  while (!(done[0] && done[1])) {
+    uint64_t w[2][kLbWin];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int k = 0; k < kLbWin; ++k) {
+        const int64_t p = top - k;
+        w[q][k] = (!done[q] && p >= 0)
+                      ? __hip_atomic_load(state + (uint64_t)(t + q * kRadixThreads) * nb + p,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : lb_word(ep, kIncl, 0u);
+      }
+    for (;;) {  // words not yet written in this epoch: read again
+      bool stale = false;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int k = 0; k < kLbWin; ++k) {
+          const int64_t p = top - k;
+          if (!done[q] && p >= 0 && (uint32_t)(w[q][k] >> 34) != ep) {
+            stale = true;
+            w[q][k] = __hip_atomic_load(state + (uint64_t)(t + q * kRadixThreads) * nb + p,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      if (!stale) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    prefix += (uint32_t)w;
-    if (((w >> 32) & 3u) == kIncl) break;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (done[q]) continue;
+#pragma unroll
+      for (int k = 0; k < kLbWin; ++k) {
+        if (done[q]) continue;
+        const int64_t p = top - k;
+        if (p < 0) {
+          done[q] = true;
+          continue;
+        }
+        pref[q] += (uint32_t)w[q][k];
+        if (((w[q][k] >> 32) & 3u) == kIncl) done[q] = true;
+      }
+    }
+    top -= kLbWin;
   }
-  __hip_atomic_store(st + (uint64_t)tile * bins, lb_word(epoch, kIncl, prefix + cnt),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return prefix;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if ((uint32_t)q >= nd) continue;
+    const uint32_t d = t + q * kRadixThreads;
+    if (tile > 0)
+      __hip_atomic_store(state + (uint64_t)d * nb + tile, lb_word(epoch, kIncl, pref[q] + sm.lstart[d]),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.gstart[d] = hp[(uint64_t)d * nb] - sub + pref[q];
+  }
 }
 template <bool FINAL>
 __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
@@ -1584,11 +1632,15 @@ __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
   radix_tile_order(
       sm, keys_in, vals_in, n, pass * dbits, dbits,
       [&](uint32_t d, uint32_t cnt) {
-        if (pass != 0) digit_publish(state, bins, epoch, d, cnt);
+        if (pass != 0) digit_publish(state, nb, epoch, d, cnt);
       },
-      [&](uint32_t d, uint32_t cnt) {
-        if (pass == 0) return hp[(uint64_t)d * nb + blockIdx.x];
-        return hp[(uint64_t)d * nb] - sub + digit_lookback(state, bins, epoch, d, cnt);
+      [&] {
+        if (pass != 0) {
+          digit_lookback(sm, state, nb, bins, epoch, hp, sub);
+        } else {
+          for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
+            sm.gstart[d] = hp[(uint64_t)d * nb + blockIdx.x];
+        }
       });
   const uint32_t cnt = radix_tile_count(n), shift = pass * dbits, mask = bins - 1u;
   const int t = threadIdx.x;
