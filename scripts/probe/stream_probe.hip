@@ -89,6 +89,35 @@ __global__ __launch_bounds__(kThreads, 1) void k_lds(const char* __restrict__ Q,
   if (reinterpret_cast<uint32_t*>(ring)[threadIdx.x] == 0x12345678u) sink[0] = 1;
 }
 
+// as k_lds, the block's row ids staged in LDS first (as k_h2_nn3 / k_h2_tn4
+// do), so no row's DMA waits on a global id load
+template <int DEPTH>
+__global__ __launch_bounds__(kThreads, 1) void k_lds_ids(const char* __restrict__ Q, const uint32_t* ids,
+                                                         uint32_t M, uint32_t chunk, uint32_t* sink) {
+  extern __shared__ __attribute__((aligned(16))) char ring[];
+  uint32_t* sid = reinterpret_cast<uint32_t*>(ring + 131072);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t r0 = blockIdx.x * chunk, r1 = min(M, r0 + chunk);
+  for (uint32_t r = r0 + threadIdx.x; r < r1; r += kThreads) sid[r - r0] = ids[r];
+  __syncthreads();
+  const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)ring + w * 16384;
+  int slot = 0;
+  for (uint32_t r = r0 + w; r < r1; r += 8) {
+    const uint32_t id = sid[r - r0];
+    const char* row = Q + (uint64_t)id * kPitch;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(base + 1024 * (slot & 15));
+      if (q < 2 || lane < 32) glds16(row + 1024 * q + 16 * lane, dst);
+      ++slot;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DEPTH) : "memory");
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (reinterpret_cast<uint32_t*>(ring)[threadIdx.x] == 0x12345678u) sink[0] = 1;
+}
+
 int main(int argc, char** argv) {
   const uint32_t V = 232965, M = 228616;
   const int iters = argc > 1 ? atoi(argv[1]) : 10;
@@ -130,6 +159,10 @@ int main(int argc, char** argv) {
   run("lds_d8", [&] { hipLaunchKernelGGL((k_lds<8, false>), dim3(blocks), dim3(kThreads), 131072, 0, Q, ids, M, chunk, sink); });
   run("lds_d12", [&] { hipLaunchKernelGGL((k_lds<12, false>), dim3(blocks), dim3(kThreads), 131072, 0, Q, ids, M, chunk, sink); });
   run("lds_d15", [&] { hipLaunchKernelGGL((k_lds<15, false>), dim3(blocks), dim3(kThreads), 131072, 0, Q, ids, M, chunk, sink); });
+  CK(hipFuncSetAttribute((const void*)k_lds_ids<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072 + 4096));
+  CK(hipFuncSetAttribute((const void*)k_lds_ids<15>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072 + 4096));
+  run("lds_ids_d12", [&] { hipLaunchKernelGGL((k_lds_ids<12>), dim3(blocks), dim3(kThreads), 131072 + 4096, 0, Q, ids, M, chunk, sink); });
+  run("lds_ids_d15", [&] { hipLaunchKernelGGL((k_lds_ids<15>), dim3(blocks), dim3(kThreads), 131072 + 4096, 0, Q, ids, M, chunk, sink); });
   run("dense_d12", [&] { hipLaunchKernelGGL((k_lds<12, true>), dim3(blocks), dim3(kThreads), 131072, 0, Q, ids, M, chunk, sink); });
   CK(hipGetLastError());
   return 0;
