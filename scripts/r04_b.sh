@@ -30,3 +30,5 @@ for r in list(csv.DictReader(open(f)))[:10]:
 PY
 bash scripts/prof_c3.sh $(basename $O)_c3 > $O/c3.txt 2>&1 || { tail -5 $O/c3.txt; exit 1; }
 head -30 $O/c3.txt
+timeout -k 10 120 scripts/probe/stream_probe 10 > $O/stream.txt 2>&1 || { echo "probe failed"; tail -5 $O/stream.txt; exit 1; }
+cat $O/stream.txt
