@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
 // The single wave above walks the whole layer.  Here the layer's words are
 // generated in bulk first (the stream does not depend on the data), the dsts
 // are cut into chunks of kMtChunk, and for every chunk and every plausible
-// number of extra words consumed before it (a window of +-6 sigma around the
+// number of extra words consumed before it (a window of +-4 sigma around the
 // expected count) one lane walks the chunk and records the count after it —
 // a table per chunk.  One wave then chains the tables (Delta_{k+1} =
 // T_k[Delta_k]; a Delta outside the window is walked out serially), and each
@@ -932,84 +932,79 @@ __device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint
 // bulk generation: W[t] = the tempered word at _M_p + t of the stream in
 // mt_state, t < nw (written to *nw_out); rb[b] = raw block b (b = 0: the
 // state's own).  nw = draws + expected extras + 10 sigma + 4096 (<= w_cap).
-// One wave, the 624-word block in registers: lane l holds words 64 i + l in
-// x[i] (i < 10; lanes >= 48 of x[9] unused), and the twist's operands are
-// lane rotations of them — cur[k + 1] (x[i] from lane l + 1), cur[k + 397]
-// (x[i + 6] / x[i + 7] from lane l + 13) for k < 227 and nxt[k - 227]
-// (n[i - 4] / n[i - 3] from lane l + 29) above — no LDS and no barrier.
-constexpr int kGenThreads = kWave;
+// (A one-wave form with the block in registers and the twist operands moved
+// by lane rotations measured slower: 1.92 vs 1.47 ms per C2 bottom layer —
+// the rotations' latency chain is longer than three barriers.)
+constexpr int kGenThreads = 256;
 __global__ __launch_bounds__(kGenThreads) void k_mtp_gen(const uint32_t* __restrict__ mt_state,
                                                         const uint32_t* base, const uint32_t* sizes,
                                                         const float2* cstat, uint32_t w_cap,
                                                         uint32_t* __restrict__ W,
                                                         uint32_t* __restrict__ rb,
                                                         uint32_t* nw_out) {
-  const int l = threadIdx.x;
+  __shared__ uint32_t blk[2][624];
+  __shared__ float red[2][kGenThreads / kWave];
+  const int t = threadIdx.x;
   const uint32_t v = sizes[0];
   const uint32_t nch = (v + kMtChunkP - 1) / kMtChunkP;
   float m = 0.f, var = 0.f;
-  for (uint32_t k = l; k < nch; k += kWave) {
+  for (uint32_t k = t; k < nch; k += kGenThreads) {
     m += cstat[k].x;
     var += cstat[k].y;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    m += __shfl_xor(m, o, kWave);
-    var += __shfl_xor(var, o, kWave);
+    m += __shfl_down(m, o, kWave);
+    var += __shfl_down(var, o, kWave);
   }
-  const double want = (double)base[v] + (double)m + 10.0 * sqrt((double)var) + 4096.0;
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = m;
+    red[1][t >> 6] = var;
+  }
+  for (int k = t; k < 624; k += kGenThreads) {
+    blk[0][k] = mt_state[k];
+    rb[k] = mt_state[k];
+  }
+  __syncthreads();
+  float mm = 0.f, vv = 0.f;
+  for (int w = 0; w < kGenThreads / kWave; ++w) {
+    mm += red[0][w];
+    vv += red[1][w];
+  }
+  const double want = (double)base[v] + (double)mm + 10.0 * sqrt((double)vv) + 4096.0;
   const uint32_t nw = (uint32_t)fmin(want, (double)w_cap);
   const uint32_t q0 = mt_state[624];
-  if (l == 0) *nw_out = nw;
-  uint32_t x[10];
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const uint32_t k = 64u * i + l;
-    x[i] = k < 624 ? mt_state[k] : 0u;
-    if (k < 624) {
-      rb[k] = x[i];
-      if (k >= q0 && k - q0 < nw) W[k - q0] = mt_temper(x[i]);
-    }
-  }
+  if (t == 0) *nw_out = nw;
+  for (uint32_t a = q0 + t; a < 624; a += kGenThreads)
+    if (a - q0 < nw) W[a - q0] = mt_temper(blk[0][a]);
   const uint32_t U = 0x80000000u, L = 0x7fffffffu, A = 0x9908b0dfu;
-  const int l1 = (l + 1) & 63, l13 = (l + 13) & 63, l29 = (l + 29) & 63;
   for (uint32_t b = 1; 624u * b - q0 < nw; ++b) {
-    uint32_t n[10];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      // word k = 64 i + l; cur[k + 1] (k = 623: nxt[0])
-      uint32_t c1 = __shfl(x[i], l1, kWave);
-      if (i < 9) {
-        const uint32_t h = __builtin_amdgcn_readfirstlane(x[i + 1]);  // lane 0
-        c1 = l == 63 ? h : c1;
-      } else {
-        const uint32_t h = __builtin_amdgcn_readfirstlane(n[0]);
-        c1 = l == 47 ? h : c1;
-      }
-      const uint32_t y = (x[i] & U) | (c1 & L);
-      uint32_t src = 0;
-      if (i <= 3) {  // k < 227 (i = 3: lanes < 35): cur[k + 397]
-        const uint32_t s1 = __shfl(x[i + 6], l13, kWave);
-        const uint32_t s2 = i + 7 <= 9 ? __shfl(x[i + 7 <= 9 ? i + 7 : 9], l13, kWave) : 0u;
-        src = l + 13 < 64 ? s1 : s2;
-      }
-      if (i >= 3) {  // k >= 227: nxt[k - 227]
-        const uint32_t t1 = i >= 4 ? __shfl(n[i >= 4 ? i - 4 : 0], l29, kWave) : 0u;
-        const uint32_t t2 = __shfl(n[i - 3], l29, kWave);
-        const uint32_t nx = l < 35 ? t1 : t2;
-        src = (i > 3 || l >= 35) ? nx : src;
-      }
-      n[i] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    const uint32_t* cur = blk[(b - 1) & 1];
+    uint32_t* nxt = blk[b & 1];
+    // _M_gen_rand in three dependent pieces: [0,227) from the current block,
+    // [227,454) and [454,624) from the words just made
+    if (t < 227) {
+      const uint32_t y = (cur[t] & U) | (cur[t + 1] & L);
+      nxt[t] = cur[t + 397] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
     }
+    __syncthreads();
+    if (t < 227) {
+      const int k = t + 227;
+      const uint32_t y = (cur[k] & U) | (cur[k + 1] & L);
+      nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    __syncthreads();
+    if (t < 170) {
+      const int k = t + 454;
+      const uint32_t y = (cur[k] & U) | ((k < 623 ? cur[k + 1] : nxt[0]) & L);
+      nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
+    }
+    __syncthreads();
     const uint32_t o = 624u * b - q0;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      const uint32_t k = 64u * i + l;
-      x[i] = n[i];
-      if (k < 624) {
-        rb[(uint64_t)b * 624 + k] = n[i];
-        if (o + k < nw) W[o + k] = mt_temper(n[i]);
-      }
+    for (int k = t; k < 624; k += kGenThreads) {
+      const uint32_t x = nxt[k];
+      rb[(uint64_t)b * 624 + k] = x;
+      if (o + k < nw) W[o + k] = mt_temper(x);
     }
   }
 }
@@ -1053,7 +1048,7 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   __syncthreads();
   const float mm = red[0][0] + red[0][1] + red[0][2] + red[0][3];
   const float vv = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-  const float h = ceilf(6.f * sqrtf(vv)) + 8.f;
+  const float h = ceilf(4.f * sqrtf(vv)) + 8.f;
   const uint32_t lo = (uint32_t)fmaxf(0.f, floorf(mm - h));
   const uint32_t wn = min(kMtWmax, (uint32_t)(mm + h - (float)lo) + 1u);
   if (blockIdx.x == 0 && t == 0) win[k] = make_uint2(lo, wn);
@@ -1442,23 +1437,27 @@ __global__ void k_relabel(RelabelArgs a) {
     relabel_one(a, k);
 }
 
-// The CSR transpose's first kernel (the fused sort, csr_sort_fused): one
-// 4096-edge tile per block relabels its edges (k_relabel's work) and counts
-// the local src ids' digits for each of the NP radix passes into `hist`
-// (pass-major, then digit-major [NP][bins][nb], the layout one exclusive scan
-// turns into every pass's output offsets, pass p's shifted by p * e); and
-// presets row_offset[0 .. s] = e for the final pass's atomicMin.
+// The CSR transpose's first kernel (the fused sort, see nts_hip_sample_layer):
+// one 4096-edge tile per block relabels its edges (k_relabel's work) and
+// counts the local src ids' first radix digit into `hist` (digit-major
+// [bins][nb], the layout one exclusive scan turns into the first pass's
+// output offsets); zeroes its share of the later passes' histograms (`zero`,
+// nzero words, counted by the passes before them); and presets
+// row_offset[0 .. s] = e for the final pass's atomicMin.
 constexpr int kRelabelThreads = 1024;  // 4 edges per thread: 16 waves per tile in flight
-template <int NP>
 __global__ __launch_bounds__(kRelabelThreads) void k_relabel_tiles(RelabelArgs a, uint32_t dbits,
                                                                    uint32_t* __restrict__ hist,
-                                                                   uint32_t nb, uint32_t* __restrict__ ro) {
+                                                                   uint32_t nb, uint32_t* __restrict__ ro,
+                                                                   uint32_t* __restrict__ zero,
+                                                                   uint64_t nzero) {
+  constexpr int NP = 1;
   __shared__ uint32_t h[NP][kRadixMaxBins];
   const int t = threadIdx.x;
   const uint32_t bins = 1u << dbits, mask = bins - 1u;
-  for (uint32_t d = t; d < bins; d += kRelabelThreads)
-#pragma unroll
-    for (int p = 0; p < NP; ++p) h[p][d] = 0;
+  for (uint32_t d = t; d < bins; d += kRelabelThreads) h[0][d] = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * kRelabelThreads + t; j < nzero;
+       j += (uint64_t)gridDim.x * kRelabelThreads)
+    zero[j] = 0;
   __syncthreads();
   const uint32_t e = a.sizes[1];
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
@@ -1518,17 +1517,14 @@ __global__ __launch_bounds__(kRelabelThreads) void k_relabel_tiles(RelabelArgs a
     ro[j] = e;
 }
 
-// A pass of the fused CSR sort.  Pass 0's tiles are the relabelled edges,
-// whose per-tile digit counts k_relabel_tiles left; a later pass's tiles are
-// the previous pass's output, so their counts are their own: each tile
-// publishes its count of every digit and sums its predecessors' (decoupled
-// look-back per digit over epoch-tagged words, state[tile][digit]) — the
-// digit's global start is the relabel histogram's scanned entry at tile 0.
-// Non-final passes write (key, edge id) to keys_out / vals_out; the final one
-// writes the CSR directly: column index, backward weight and edge id at the
-// edge's CSR position, and row_offset[key] = min over the key's first
-// positions (atomicMin: a row's first edge either follows a different key
-// inside its tile's run, or opens a run).
+// A pass of the fused CSR sort.  `hist` holds this pass's scanned per-tile
+// digit offsets (digit-major [bins][nb]).  A non-final pass writes (key, edge
+// id) to keys_out / vals_out and counts the next pass's digits per OUTPUT
+// tile into hist_next (one atomic per item: the next pass's tiles are this
+// pass's output, so their counts exist only once the positions do).  The
+// final pass writes the CSR directly: column index, backward weight and edge
+// id at the edge's CSR position, and row_offset[key] = min over the key's
+// first positions (atomicMin).
 struct CsrOut {
   const uint32_t* edst;
   const float* wf;
@@ -1537,111 +1533,21 @@ struct CsrOut {
   float* wb;
   uint32_t* ceid;
 };
-// Look-back state of the passes after the first: word (digit d, tile j) at
-// state[d * nb + j] = {epoch, kind, value}: the tile's count of the digit
-// (kind 1) or its inclusive prefix over tiles 0..j (kind 2).
-__device__ __forceinline__ void digit_publish(uint64_t* __restrict__ state, uint32_t nb,
-                                              uint32_t epoch, uint32_t d, uint32_t cnt) {
-  __hip_atomic_store(state + (uint64_t)d * nb + blockIdx.x,
-                     lb_word(epoch, blockIdx.x == 0 ? 2u : 1u, cnt), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-// The thread's digits (t and t + 256 < bins): their exclusive prefixes over
-// the tiles before this one, eight predecessors read per step (all loads of
-// a step in flight together; a word from an older epoch is read again) back
-// to the nearest inclusive prefix; then this tile's inclusive prefixes are
-// published and sm.gstart set.
-constexpr int kLbWin = 8;
-__device__ __forceinline__ void digit_lookback(RadixTileLds& sm, uint64_t* __restrict__ state,
-                                               uint32_t nb, uint32_t bins, uint32_t epoch,
-                                               const uint32_t* __restrict__ hp, uint32_t sub) {
-  constexpr uint64_t kIncl = 2;
-  const uint32_t t = threadIdx.x, tile = blockIdx.x, ep = epoch & 0x3FFFFFFFu;
-  const uint32_t nd = t + kRadixThreads < bins ? 2u : (t < bins ? 1u : 0u);
-  uint32_t pref[2] = {0u, 0u};
-  bool done[2] = {tile == 0 || nd < 1, tile == 0 || nd < 2};
-  int64_t top = (int64_t)tile - 1;
-  while (!(done[0] && done[1])) {
-    uint64_t w[2][kLbWin];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int k = 0; k < kLbWin; ++k) {
-        const int64_t p = top - k;
-        w[q][k] = (!done[q] && p >= 0)
-                      ? __hip_atomic_load(state + (uint64_t)(t + q * kRadixThreads) * nb + p,
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : lb_word(ep, kIncl, 0u);
-      }
-    for (;;) {  // words not yet written in this epoch: read again
-      bool stale = false;
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int k = 0; k < kLbWin; ++k) {
-          const int64_t p = top - k;
-          if (!done[q] && p >= 0 && (uint32_t)(w[q][k] >> 34) != ep) {
-            stale = true;
-            w[q][k] = __hip_atomic_load(state + (uint64_t)(t + q * kRadixThreads) * nb + p,
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-      if (!stale) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (done[q]) continue;
-#pragma unroll
-      for (int k = 0; k < kLbWin; ++k) {
-        if (done[q]) continue;
-        const int64_t p = top - k;
-        if (p < 0) {
-          done[q] = true;
-          continue;
-        }
-        pref[q] += (uint32_t)w[q][k];
-        if (((w[q][k] >> 32) & 3u) == kIncl) done[q] = true;
-      }
-    }
-    top -= kLbWin;
-  }
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    if ((uint32_t)q >= nd) continue;
-    const uint32_t d = t + q * kRadixThreads;
-    if (tile > 0)
-      __hip_atomic_store(state + (uint64_t)d * nb + tile, lb_word(epoch, kIncl, pref[q] + sm.lstart[d]),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.gstart[d] = hp[(uint64_t)d * nb] - sub + pref[q];
-  }
-}
 template <bool FINAL>
 __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* sizes,
-    uint32_t pass, uint32_t dbits, const uint32_t* __restrict__ hist, uint32_t nb,
-    uint64_t* __restrict__ state, uint32_t epoch, CsrOut c) {
+    uint32_t pass, uint32_t dbits, const uint32_t* __restrict__ hist,
+    uint32_t* __restrict__ hist_next, uint32_t nb, CsrOut c) {
   __shared__ RadixTileLds sm;
   const uint64_t n = sizes[1];
   if ((uint64_t)blockIdx.x * kRadixTile >= n) return;
   const uint32_t bins = 1u << dbits;
   const uint32_t s = sizes[2];  // (a key >= s only after a frontier overflow)
-  const uint32_t* hp = hist + (uint64_t)pass * bins * nb;
-  const uint32_t sub = pass * (uint32_t)n;  // the scan ran over every pass's counts
-  radix_tile_order(
-      sm, keys_in, vals_in, n, pass * dbits, dbits,
-      [&](uint32_t d, uint32_t cnt) {
-        if (pass != 0) digit_publish(state, nb, epoch, d, cnt);
-      },
-      [&] {
-        if (pass != 0) {
-          digit_lookback(sm, state, nb, bins, epoch, hp, sub);
-        } else {
-          for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
-            sm.gstart[d] = hp[(uint64_t)d * nb + blockIdx.x];
-        }
-      });
+  radix_tile_order(sm, keys_in, vals_in, n, pass * dbits, dbits, [](uint32_t, uint32_t) {}, [&] {
+    for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
+      sm.gstart[d] = hist[(uint64_t)d * nb + blockIdx.x];
+  });
   const uint32_t cnt = radix_tile_count(n), shift = pass * dbits, mask = bins - 1u;
   const int t = threadIdx.x;
   if (!FINAL) {
@@ -1649,6 +1555,7 @@ __global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
       const uint32_t k = sm.sk[i], pos = radix_tile_pos(sm, i, k, shift, mask);
       keys_out[pos] = k;
       vals_out[pos] = sm.sv[i];
+      atomicAdd(hist_next + (uint64_t)((k >> (shift + dbits)) & mask) * nb + pos / kRadixTile, 1u);
     }
     return;
   }
@@ -1787,11 +1694,12 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t blk = al(nblk_marks + 1);
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
-  // the fused CSR sort (csr_fused below): every pass's per-tile digit counts
-  // (<= 1536 per tile: NP x 2^dbits with dbits = ceil(bits / NP)) and a
-  // second (key, edge id) buffer for the passes between the first and last
+  // the fused CSR sort (csr_fused below): each pass's per-tile digit counts
+  // (<= 512 per tile, + the scan's total) and a second (key, edge id) buffer
+  // for the passes between the first and the last
   const uint32_t nb_csr = std::max(1u, ceil_div(o->e_cap, kRadixTile));
-  const uint64_t csr_hist_n = csr ? al(1536ull * nb_csr + 1) : 0;
+  const uint64_t csr_hist1 = al((uint64_t)kRadixMaxBins * nb_csr + 1);
+  const uint64_t csr_hist_n = csr ? 4 * csr_hist1 : 0;
   const uint64_t sort_k2 = csr ? al(o->e_cap) : 0;
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
@@ -1996,9 +1904,13 @@ frontier:
 
   // 4) relabel to local ids + forward weights; 5) CSR transpose: a stable
   // radix sort of (local src, edge id) on ceil_log2(s_cap + 1) bits.  Fused
-  // (the default): the relabel kernel counts every pass's digits per tile,
-  // one scan turns them into all passes' offsets, and the last pass writes the
-  // CSR itself — NP + 2 launches instead of 3 NP + 2.  Kept on the generic
+  // (the default): the relabel kernel counts the first pass's digits per
+  // tile, each non-final pass counts the next pass's per output tile, a scan
+  // before each pass, and the last pass writes the CSR itself — 2 NP + 1
+  // launches instead of 3 NP + 2 (measured and dropped: one scan over every
+  // pass's counts from the relabel with a per-digit decoupled look-back in the
+  // later passes, 48-91 us for the final pass against 17 for the first).
+  // Kept on the generic
   // sort + k_csr_finalize: the merged frontier (dst_local_id: a dst may have no
   // out edge, an empty CSR row) and the two-kernel scans (NTS_SCAN1=0).
   const bool csr_fused = csr && !o->dst_local_id && scan1_enabled();
@@ -2011,23 +1923,9 @@ frontier:
                  up ? t_up : nullptr};
   if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
   if (csr_fused) {
-    switch (npass) {
-      case 1:
-        hipLaunchKernelGGL(k_relabel_tiles<1>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
-                           t_chist, nb_csr, o->row_offset);
-        break;
-      case 2:
-        hipLaunchKernelGGL(k_relabel_tiles<2>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
-                           t_chist, nb_csr, o->row_offset);
-        break;
-      case 3:
-        hipLaunchKernelGGL(k_relabel_tiles<3>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
-                           t_chist, nb_csr, o->row_offset);
-        break;
-      default:
-        hipLaunchKernelGGL(k_relabel_tiles<4>, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
-                           t_chist, nb_csr, o->row_offset);
-    }
+    hipLaunchKernelGGL(k_relabel_tiles, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
+                       t_chist, nb_csr, o->row_offset, t_chist + csr_hist1,
+                       (uint64_t)(npass - 1) * csr_hist1);
   } else {
     hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, ra);
   }
@@ -2039,27 +1937,27 @@ frontier:
   }
   const float* wf_csr = weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward;
   if (csr_fused) {
-    NTS_RET(scan1_exclusive(ctx, t_chist, t_chist, nullptr, (uint64_t)npass * (1u << dbits) * nb_csr,
-                            st));
     const CsrOut co{o->edge_dst, wf_csr, o->row_offset, o->column_indices,
                     o->edge_weight_backward, o->csr_edge_id};
+    const uint64_t hist_n = (uint64_t)(1u << dbits) * nb_csr;
     const uint32_t* kin = o->row_indices;
     const uint32_t* vin = nullptr;  // edge ids = item indices
-    if (npass > 1) NTS_RET(ensure_scan_state(ctx, (uint64_t)nb_csr << dbits));
-    for (uint32_t p = 0; p + 1 < npass; ++p) {
-      uint32_t* ko = (p & 1) ? t_skey2 : t_skey;
-      uint32_t* vo = (p & 1) ? t_seid2 : t_seid;
-      hipLaunchKernelGGL(k_csr_scatter<false>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin, vin,
-                         ko, vo, o->sizes, p, dbits, t_chist, nb_csr, ctx->scan_state,
-                         p ? scan_next_epoch(ctx) : 0u, co);
+    for (uint32_t p = 0; p < npass; ++p) {
+      uint32_t* h = t_chist + p * csr_hist1;
+      NTS_RET(scan1_exclusive(ctx, h, h, nullptr, hist_n, st));
+      if (p + 1 < npass) {
+        uint32_t* ko = (p & 1) ? t_skey2 : t_skey;
+        uint32_t* vo = (p & 1) ? t_seid2 : t_seid;
+        hipLaunchKernelGGL(k_csr_scatter<false>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin,
+                           vin, ko, vo, o->sizes, p, dbits, h, h + csr_hist1, nb_csr, co);
+        kin = ko;
+        vin = vo;
+      } else {
+        hipLaunchKernelGGL(k_csr_scatter<true>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin,
+                           vin, nullptr, nullptr, o->sizes, p, dbits, h, nullptr, nb_csr, co);
+      }
       NTS_LAUNCH_CHECK();
-      kin = ko;
-      vin = vo;
     }
-    hipLaunchKernelGGL(k_csr_scatter<true>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin, vin,
-                       nullptr, nullptr, o->sizes, npass - 1, dbits, t_chist, nb_csr,
-                       ctx->scan_state, npass > 1 ? scan_next_epoch(ctx) : 0u, co);
-    NTS_LAUNCH_CHECK();
   } else if (csr) {
     NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
                              ceil_log2((uint64_t)o->s_cap + 1), t_sort, st, ctx));
