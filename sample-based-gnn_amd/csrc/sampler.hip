@@ -22,7 +22,6 @@
 //   * CSR transpose = stable radix sort of (local src, edge id) -> identical to
 //     the reference's serial fill order (ascending dst), atomic-free.
 #include "common.hpp"
-#include "radix_tile.hpp"
 
 namespace nts_hip {
 
@@ -912,14 +911,14 @@ __device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint
                                                  uint32_t deg, uint32_t thr, bool lemire) {
   constexpr uint32_t kRej = 0xFFFFFFFFu;  // a rejected word (positions are < deg)
   uint32_t val[NW];
-#pragma unroll
-  for (int q = 0; q < NW; ++q) {
-    uint32_t x;
-    val[q] = mt_apply(cur[q], deg, thr, lemire, x) ? x : kRej;
-  }
   uint32_t cnt = 0, used = 0;
 #pragma unroll
   for (int t = 0; t < NW; ++t) {
+    // n is the same for every lane (one dst per wave step): past the first n
+    // words, stop as soon as every lane has its n-th distinct draw
+    if ((uint32_t)t >= n && __ballot(used == 0) == 0) break;
+    uint32_t x;
+    val[t] = mt_apply(cur[t], deg, thr, lemire, x) ? x : kRej;
     bool dup = val[t] == kRej;
 #pragma unroll
     for (int b = 0; b < t; ++b) dup |= val[b] == val[t];
@@ -1437,165 +1436,6 @@ __global__ void k_relabel(RelabelArgs a) {
     relabel_one(a, k);
 }
 
-// The CSR transpose's first kernel (the fused sort, see nts_hip_sample_layer):
-// one 4096-edge tile per block relabels its edges (k_relabel's work) and
-// counts the local src ids' first radix digit into `hist` (digit-major
-// [bins][nb], the layout one exclusive scan turns into the first pass's
-// output offsets); zeroes its share of the later passes' histograms (`zero`,
-// nzero words, counted by the passes before them); and presets
-// row_offset[0 .. s] = e for the final pass's atomicMin.
-constexpr int kRelabelThreads = 1024;  // 4 edges per thread: 16 waves per tile in flight
-__global__ __launch_bounds__(kRelabelThreads) void k_relabel_tiles(RelabelArgs a, uint32_t dbits,
-                                                                   uint32_t* __restrict__ hist,
-                                                                   uint32_t nb, uint32_t* __restrict__ ro,
-                                                                   uint32_t* __restrict__ zero,
-                                                                   uint64_t nzero) {
-  constexpr int NP = 1;
-  __shared__ uint32_t h[NP][kRadixMaxBins];
-  const int t = threadIdx.x;
-  const uint32_t bins = 1u << dbits, mask = bins - 1u;
-  for (uint32_t d = t; d < bins; d += kRelabelThreads) h[0][d] = 0;
-  for (uint64_t j = (uint64_t)blockIdx.x * kRelabelThreads + t; j < nzero;
-       j += (uint64_t)gridDim.x * kRelabelThreads)
-    zero[j] = 0;
-  __syncthreads();
-  const uint32_t e = a.sizes[1];
-  const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-  constexpr int kPer = kRadixTile / kRelabelThreads;
-  // relabel_one's loads for the thread's kPer edges in dependency phases (the
-  // stores of one edge would otherwise hold back the loads of the next)
-  uint32_t g[kPer], ed[kPer], r[kPer], od[kPer], dg[kPer], cnt[kPer];
-  bool ok[kPer];
-  const bool wts = a.weight_type != NTS_WEIGHT_NONE && !a.up_cnt;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const uint64_t i = base + (uint64_t)k * kRelabelThreads + t;
-    ok[k] = i < e;
-    g[k] = ok[k] ? a.ans[i] : 0u;
-    ed[k] = ok[k] && wts ? a.edst[i] : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    r[k] = ok[k] ? a.src_index[g[k]] : 0u;
-    od[k] = ok[k] && wts ? a.out_deg[g[k]] : 0u;
-    dg[k] = ok[k] && wts ? a.dst[ed[k]] : 0u;
-    cnt[k] = ok[k] && wts && a.weight_type == NTS_WEIGHT_MEAN_SAMPLED
-                 ? a.co[ed[k] + 1] - a.co[ed[k]]
-                 : 1u;
-  }
-  uint32_t indg[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) indg[k] = ok[k] && wts ? a.in_deg[dg[k]] : 1u;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    if (!ok[k]) continue;
-    const uint64_t i = base + (uint64_t)k * kRelabelThreads + t;
-    a.ri[i] = r[k];
-    if (a.up_cnt) {
-      atomicAdd(a.up_cnt + r[k], 1u);
-    } else if (wts) {  // relabel_one's arithmetic
-      const uint32_t ind = indg[k];
-      float w = norm_degree(od[k], ind);
-      if (a.weight_type == NTS_WEIGHT_MEAN) w = w / (float)ind;
-      if (a.weight_type == NTS_WEIGHT_MEAN_SAMPLED) w = w / (float)cnt[k];
-      a.wf[i] = w;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k)
-    if (base + (uint64_t)k * kRelabelThreads + t < e)
-#pragma unroll
-      for (int p = 0; p < NP; ++p) atomicAdd(&h[p][(r[k] >> (p * dbits)) & mask], 1u);
-  __syncthreads();
-#pragma unroll
-  for (int p = 0; p < NP; ++p)
-    for (uint32_t d = t; d < bins; d += kRelabelThreads)
-      hist[((uint64_t)p * bins + d) * nb + blockIdx.x] = h[p][d];
-  const uint32_t s = a.sizes[2];
-  for (uint64_t j = (uint64_t)blockIdx.x * kRelabelThreads + t; j <= s;
-       j += (uint64_t)gridDim.x * kRelabelThreads)
-    ro[j] = e;
-}
-
-// A pass of the fused CSR sort.  `hist` holds this pass's scanned per-tile
-// digit offsets (digit-major [bins][nb]).  A non-final pass writes (key, edge
-// id) to keys_out / vals_out and counts the next pass's digits per OUTPUT
-// tile into hist_next (one atomic per item: the next pass's tiles are this
-// pass's output, so their counts exist only once the positions do).  The
-// final pass writes the CSR directly: column index, backward weight and edge
-// id at the edge's CSR position, and row_offset[key] = min over the key's
-// first positions (atomicMin).
-struct CsrOut {
-  const uint32_t* edst;
-  const float* wf;
-  uint32_t* ro;
-  uint32_t* ci;
-  float* wb;
-  uint32_t* ceid;
-};
-template <bool FINAL>
-__global__ __launch_bounds__(kRadixThreads) void k_csr_scatter(
-    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
-    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* sizes,
-    uint32_t pass, uint32_t dbits, const uint32_t* __restrict__ hist,
-    uint32_t* __restrict__ hist_next, uint32_t nb, CsrOut c) {
-  __shared__ RadixTileLds sm;
-  const uint64_t n = sizes[1];
-  if ((uint64_t)blockIdx.x * kRadixTile >= n) return;
-  const uint32_t bins = 1u << dbits;
-  const uint32_t s = sizes[2];  // (a key >= s only after a frontier overflow)
-  radix_tile_order(sm, keys_in, vals_in, n, pass * dbits, dbits, [](uint32_t, uint32_t) {}, [&] {
-    for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
-      sm.gstart[d] = hist[(uint64_t)d * nb + blockIdx.x];
-  });
-  const uint32_t cnt = radix_tile_count(n), shift = pass * dbits, mask = bins - 1u;
-  const int t = threadIdx.x;
-  if (!FINAL) {
-    for (uint32_t i = t; i < cnt; i += kRadixThreads) {
-      const uint32_t k = sm.sk[i], pos = radix_tile_pos(sm, i, k, shift, mask);
-      keys_out[pos] = k;
-      vals_out[pos] = sm.sv[i];
-      atomicAdd(hist_next + (uint64_t)((k >> (shift + dbits)) & mask) * nb + pos / kRadixTile, 1u);
-    }
-    return;
-  }
-  // final pass, in phases over the thread's items (LDS, then the edge
-  // gathers, then the stores) so that its random loads are all in flight
-  constexpr int kPer = kRadixTile / kRadixThreads;
-  uint32_t key[kPer], val[kPer], pos[kPer], cv[kPer];
-  float wv[kPer];
-  bool first[kPer];
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const uint32_t i = t + q * kRadixThreads;
-    key[q] = val[q] = pos[q] = 0;
-    first[q] = false;
-    if (i < cnt) {
-      key[q] = sm.sk[i];
-      val[q] = sm.sv[i];
-      const uint32_t d = (key[q] >> shift) & mask, ls = sm.lstart[d];
-      pos[q] = sm.gstart[d] + (i - ls);
-      first[q] = i == ls || sm.sk[i - 1] != key[q];
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const bool ok = t + q * kRadixThreads < cnt;
-    cv[q] = ok ? c.edst[val[q]] : 0u;
-    wv[q] = ok && c.wf ? c.wf[val[q]] : 0.0f;
-  }
-#pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    if (t + q * kRadixThreads >= cnt) continue;
-    c.ci[pos[q]] = cv[q];
-    if (c.ceid) c.ceid[pos[q]] = val[q];
-    if (c.wb) c.wb[pos[q]] = wv[q];
-    // a row's first edge either follows a different key inside its tile's
-    // run or opens a run (then an earlier tile may hold the key too)
-    if (first[q] && key[q] < s) atomicMin(c.ro + key[q], pos[q]);
-  }
-}
-
 // UP_DEGREE weights: out = sampled edges of the src (counted by k_relabel),
 // in = sampled edges of the dst (its CSC segment)
 __global__ void k_up_weight(const uint32_t* __restrict__ ri, const uint32_t* __restrict__ edst,
@@ -1694,13 +1534,6 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t blk = al(nblk_marks + 1);
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
-  // the fused CSR sort (csr_fused below): each pass's per-tile digit counts
-  // (<= 512 per tile, + the scan's total) and a second (key, edge id) buffer
-  // for the passes between the first and the last
-  const uint32_t nb_csr = std::max(1u, ceil_div(o->e_cap, kRadixTile));
-  const uint64_t csr_hist1 = al((uint64_t)kRadixMaxBins * nb_csr + 1);
-  const uint64_t csr_hist_n = csr ? 4 * csr_hist1 : 0;
-  const uint64_t sort_k2 = csr ? al(o->e_cap) : 0;
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
   // MT19937 modes: per-dst info; the chunked resolver (fanout 1..32) adds the
@@ -1727,8 +1560,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t mt_misc_n = mt_chunked ? 64 : 0;
   const uint64_t mt_n = mt_info_n + mt_base_n + mt_stat_n + mt_w_n + mt_rb_n + mt_win_n +
                         mt_tab_n + mt_ent_n + mt_misc_n;
-  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n + csr_hist_n +
-                       2 * sort_k2) *
+  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n) *
                           sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
   uint32_t* w0 = (uint32_t*)ctx->scratch;
@@ -1739,10 +1571,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   uint32_t* t_seid = t_skey + sort_k;
   uint32_t* t_up = t_seid + sort_v;
   uint32_t* t_mt = t_up + up_n;  // MT19937 modes: per-dst MtInfo (16-byte aligned)
-  uint32_t* t_chist = t_mt + mt_n;
-  uint32_t* t_skey2 = t_chist + csr_hist_n;
-  uint32_t* t_seid2 = t_skey2 + sort_k2;
-  void* t_sort = (void*)(t_seid2 + sort_k2);
+  void* t_sort = (void*)(t_mt + mt_n);
 
   const uint32_t gv = std::max(1u, std::min(ceil_div(o->v_cap, 256), kMaxGrid));
   const uint32_t ge = std::max(1u, std::min(ceil_div(o->e_cap, 256), kMaxGrid));
@@ -1902,67 +1731,33 @@ frontier:
     NTS_LAUNCH_CHECK();
   }
 
-  // 4) relabel to local ids + forward weights; 5) CSR transpose: a stable
-  // radix sort of (local src, edge id) on ceil_log2(s_cap + 1) bits.  Fused
-  // (the default): the relabel kernel counts the first pass's digits per
-  // tile, each non-final pass counts the next pass's per output tile, a scan
-  // before each pass, and the last pass writes the CSR itself — 2 NP + 1
-  // launches instead of 3 NP + 2 (measured and dropped: one scan over every
-  // pass's counts from the relabel with a per-digit decoupled look-back in the
-  // later passes, 48-91 us for the final pass against 17 for the first).
-  // Kept on the generic
-  // sort + k_csr_finalize: the merged frontier (dst_local_id: a dst may have no
-  // out edge, an empty CSR row) and the two-kernel scans (NTS_SCAN1=0).
-  const bool csr_fused = csr && !o->dst_local_id && scan1_enabled();
-  const uint32_t sbits = std::max(1u, ceil_log2((uint64_t)o->s_cap + 1));
-  const uint32_t npass = (sbits + kRadixMaxBits - 1) / kRadixMaxBits;
-  const uint32_t dbits = (sbits + npass - 1) / npass;
+  // 4) relabel to local ids + forward weights
   RelabelArgs ra{o->sample_ans,      o->edge_dst, o->destination, ctx->src_index,
                  g->out_degree,      g->in_degree, o->column_offset, o->sizes,
                  weight_type,        o->row_indices, o->edge_weight_forward,
                  up ? t_up : nullptr};
   if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
-  if (csr_fused) {
-    hipLaunchKernelGGL(k_relabel_tiles, dim3(nb_csr), dim3(kRelabelThreads), 0, st, ra, dbits,
-                       t_chist, nb_csr, o->row_offset, t_chist + csr_hist1,
-                       (uint64_t)(npass - 1) * csr_hist1);
-  } else {
-    hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, ra);
-  }
+  hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, ra);
   NTS_LAUNCH_CHECK();
   if (up) {
     hipLaunchKernelGGL(k_up_weight, dim3(ge), dim3(256), 0, st, o->row_indices, o->edge_dst,
                        o->column_offset, t_up, o->sizes, weight_type, o->edge_weight_forward);
     NTS_LAUNCH_CHECK();
   }
-  const float* wf_csr = weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward;
-  if (csr_fused) {
-    const CsrOut co{o->edge_dst, wf_csr, o->row_offset, o->column_indices,
-                    o->edge_weight_backward, o->csr_edge_id};
-    const uint64_t hist_n = (uint64_t)(1u << dbits) * nb_csr;
-    const uint32_t* kin = o->row_indices;
-    const uint32_t* vin = nullptr;  // edge ids = item indices
-    for (uint32_t p = 0; p < npass; ++p) {
-      uint32_t* h = t_chist + p * csr_hist1;
-      NTS_RET(scan1_exclusive(ctx, h, h, nullptr, hist_n, st));
-      if (p + 1 < npass) {
-        uint32_t* ko = (p & 1) ? t_skey2 : t_skey;
-        uint32_t* vo = (p & 1) ? t_seid2 : t_seid;
-        hipLaunchKernelGGL(k_csr_scatter<false>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin,
-                           vin, ko, vo, o->sizes, p, dbits, h, h + csr_hist1, nb_csr, co);
-        kin = ko;
-        vin = vo;
-      } else {
-        hipLaunchKernelGGL(k_csr_scatter<true>, dim3(nb_csr), dim3(kRadixThreads), 0, st, kin,
-                           vin, nullptr, nullptr, o->sizes, p, dbits, h, nullptr, nb_csr, co);
-      }
-      NTS_LAUNCH_CHECK();
-    }
-  } else if (csr) {
+
+  // 5) CSR transpose (stable in edge order = ascending local dst): radix sort
+  // of (local src, edge id), then the CSR arrays.  Measured and dropped in
+  // round 4 (C2, per layer): fusing the relabel with the first pass's digit
+  // counts (20 vs 11 + 8 us: a tile per block is fewer threads for its random
+  // gathers), the CSR writes into the last pass (45 vs 16 + 20 us), and the
+  // later passes' tile offsets by a per-digit decoupled look-back (48-91 us)
+  // or counted by the pass before with atomics (65 vs 16 us).
+  if (csr) {
     NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
                              ceil_log2((uint64_t)o->s_cap + 1), t_sort, st, ctx));
     hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
-                       wf_csr, o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
+                       weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
+                       o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
                        o->csr_edge_id);
     NTS_LAUNCH_CHECK();
   }
