@@ -35,4 +35,11 @@ PY
 done
 timeout -k 10 120 scripts/probe/stream_probe 10 > $O/stream.txt 2>&1 || { echo "probe failed"; tail -5 $O/stream.txt; exit 1; }
 cat $O/stream.txt
+for v in product nn3acc2 product nn3acc2; do
+  if [ $v = product ]; then L="NTS_NONE=0"; else L="NTS_HIP_LIB=scripts/probe/lib_$v/libnts_hip.so"; fi
+  env $L timeout -k 10 200 python -u scripts/micro_bottom.py > $O/mb_$v.json 2> $O/mb_$v.err || { echo "micro_bottom $v failed"; tail -5 $O/mb_$v.err; exit 1; }
+  echo "$v $(cat $O/mb_$v.json)"
+done
+NTS_HIP_LIB=scripts/probe/lib_nn3acc2/libnts_hip.so timeout -k 10 300 python -u -m pytest tests/test_gemm_h2.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/acc2_tests.log 2>&1 || { echo "acc2 tests failed"; tail -20 $O/acc2_tests.log; exit 1; }
+tail -1 $O/acc2_tests.log
 bash scripts/bench_configs.sh r04c || exit 1
