@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "nts_hip.h"
 
@@ -115,6 +117,23 @@ struct nts_hip_ctx {
   uint64_t scan_state_elems = 0;
   uint32_t scan_epoch = 0;
   int gemm_mode = NTS_GEMM_F32;    // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode)
+  // MT19937 modes: the generator's stream as tempered words in a device ring,
+  // generated ahead of the layers that read it on a side stream (sampler.hip,
+  // mt_ring_prepare).  Stream word a (0 = the first word after seeding) lives
+  // at mt_ring[a % kMtRingWords]; mt_done = {position after the last MT layer
+  // (40 bits) | that layer's sequence number (24 bits)}.
+  uint32_t* mt_ring = nullptr;
+  uint32_t* mt_gen_raw = nullptr;      // [624] the raw block the generator continues from
+  uint64_t* mt_done = nullptr;         // device word, and its pinned host copy:
+  uint64_t* mt_done_host = nullptr;
+  uint64_t mt_gen_blocks = 0;          // 624-word blocks generated (issued)
+  uint32_t mt_seq = 0;                 // MT layers issued since seeding
+  uint64_t mt_pos_done = 0;            // host: last position read back, and its layer
+  uint32_t mt_seq_done = 0;
+  hipStream_t mt_gen_stream = nullptr;
+  std::vector<std::pair<uint32_t, uint64_t>> mt_pending;    // (layer seq, word bound) not yet read back
+  std::vector<std::pair<uint64_t, hipEvent_t>> mt_gen_evs;  // (blocks after, event) of generation launches
+  std::vector<hipEvent_t> mt_ev_pool;
 };
 
 namespace nts_hip {
@@ -140,6 +159,9 @@ int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems);
 size_t scan1_state_elems(uint64_t n_cap);
 // the next per-call epoch of the look-back tile states (never 0)
 uint32_t scan_next_epoch(nts_hip_ctx* ctx);
+// MT19937 stream ring (sampler.hip): forget the generated stream (seeding)
+int mt_ring_reset(nts_hip_ctx* ctx);
+void mt_ring_free(nts_hip_ctx* ctx);
 
 // Decoupled look-back (one wave, every lane calls): tile `tile` publishes its
 // aggregate, sums its predecessors' states (RELAXED agent-scope atomics: each

@@ -104,6 +104,7 @@ int nts_hip_ctx_destroy(nts_hip_ctx* ctx) {
   if (ctx->src_index) (void)hipFree(ctx->src_index);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->mt_state) (void)hipFree(ctx->mt_state);
+  mt_ring_free(ctx);
   if (ctx->scan_state) (void)hipFree(ctx->scan_state);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -156,7 +157,7 @@ int nts_hip_rng_seed(nts_hip_ctx* ctx, uint64_t seed) {
   NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
   NTS_HIP_TRY(hipMemcpy(ctx->mt_state, st.data(), 625 * sizeof(uint32_t),
                         hipMemcpyHostToDevice));
-  return NTS_OK;
+  return mt_ring_reset(ctx);
 }
 
 int nts_hip_rng_state(nts_hip_ctx* ctx, uint32_t* host_state625) {

@@ -376,21 +376,49 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y;
 }
 
-// nxt = twist(cur), libstdc++ _M_gen_rand order, 64 lanes, chunk by chunk
-// (each chunk only depends on earlier chunks since m - n = -227 < -64).
-__device__ __forceinline__ void mt_twist(const uint32_t* cur, uint32_t* nxt, int lane) {
-  const uint32_t U = 0x80000000u, L = 0x7fffffffu, A = 0x9908b0dfu;
-  for (int base = 0; base < 624; base += kWave) {
-    const int k = base + lane;
-    if (k < 624) {
-      uint32_t x1 = (k < 623) ? cur[k + 1] : nxt[0];
-      uint32_t y = (cur[k] & U) | (x1 & L);
-      uint32_t src = (k < 227) ? cur[k + 397] : nxt[k - 227];
-      nxt[k] = src ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
-    }
-    __syncthreads();
-  }
+// tempering is invertible: the raw state word back from a tempered word
+__device__ __forceinline__ uint32_t mt_untemper(uint32_t y) {
+  y ^= y >> 18;
+  y ^= (y << 15) & 0xefc60000u;
+  uint32_t t = y;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t = y ^ ((t << 7) & 0x9d2c5680u);
+  y = t;
+  t = y;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) t = y ^ (t >> 11);
+  return t;
 }
+
+// The stream ring (nts_hip_ctx::mt_ring): word a of the stream since seeding
+// at mt_ring[a % kMtRingWords]; block b (624 words, b = 0 the first twist
+// after seeding) covers words [624 b, 624 b + 624).
+constexpr uint32_t kMtRingBits = 25;
+constexpr uint64_t kMtRingWords = 1ull << kMtRingBits;  // 128 MB of words
+constexpr uint32_t kMtRingMask = (uint32_t)(kMtRingWords - 1);
+constexpr uint64_t kMtPosMask = (1ull << 40) - 1;  // mt_done: position (40 bits) | seq << 40
+// a layer's view of the stream: word i = stream word a0 + i, zero past the
+// words generated for it (nw)
+struct MtWords {
+  const uint32_t* ring;
+  uint64_t a0;
+  uint32_t nw;
+  __device__ __forceinline__ uint32_t operator[](uint32_t i) const {
+    return i < nw ? ring[(uint32_t)(a0 + i) & kMtRingMask] : 0u;
+  }
+};
+// std::mt19937's state after the stream's first `a` words (a > 0): the raw
+// block holding word a - 1 (untempered from the ring) and _M_p = its index + 1
+// (624: libstdc++ twists lazily on the next call); whole wave
+__device__ __forceinline__ void mt_state_at(const uint32_t* ring, uint64_t a, uint32_t* mt_state,
+                                            int lane) {
+  const uint64_t last = a - 1, b = last / 624;
+  const uint32_t p = (uint32_t)(last - b * 624) + 1u;
+  for (int k = lane; k < 624; k += kWave)
+    mt_state[k] = mt_untemper(ring[(uint32_t)(b * 624 + k) & kMtRingMask]);
+  if (lane == 0) mt_state[624] = p;
+}
+
 
 // The reference draws from ONE sequential generator (random_uniform_int,
 // core/ntsFastSampler.hpp:200-205) over the dsts in order, and a dst's word
@@ -426,8 +454,11 @@ constexpr uint32_t kMtChunkP = 256;
 __global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
                           const uint32_t* __restrict__ co, uint32_t* sizes, uint32_t e_cap,
                           int lemire, uint4* __restrict__ info, uint32_t* __restrict__ nn,
-                          float2* __restrict__ cstat) {
+                          float2* __restrict__ cstat, const uint64_t* done, uint64_t* a0p) {
   const uint32_t v = sizes[0];
+  // the layer's first stream word, for the kernels after this one (the
+  // resolver moves mt_done on)
+  if (a0p && blockIdx.x == 0 && threadIdx.x == 0) *a0p = *done & kMtPosMask;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < v; i += gridDim.x * blockDim.x) {
     const uint32_t d = dst[i];
     const uint32_t deg = (uint32_t)(goff[d + 1] - goff[d]);
@@ -454,53 +485,16 @@ __global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __r
   }
 }
 
-// word r (relative to block `cur`) of the tempered two-block window
-__device__ __forceinline__ uint32_t mt_word(const uint32_t* tw, int cur, uint32_t r) {
-  uint32_t k = (uint32_t)cur * 624u + r;
-  if (k >= 1248u) k -= 1248u;
-  return tw[k];
-}
-
-// The word source of the MT19937 walks: either the generator itself (raw
-// != nullptr: two 624-word blocks in LDS, the next one twisted on demand) or
-// a flat array of already tempered words (raw == nullptr: the chunked
-// resolver's words, generated in bulk by k_mtp_gen), word r at tw[r].
+// The word source of the MT19937 walks: the stream ring (the layer's words,
+// generated ahead by k_mt_ring_gen) or words staged in LDS; word r at
+// tw[(fa + r) & fmask] for r < fnw, 0 past them.  q0: the next word's index.
 struct MtStream {
-  uint32_t* raw;  // [2][624] std::mt19937::_M_x of the current / next block
-  const uint32_t* tw;  // [2][624] tempered copies (flat: every word of the walk)
-  int cur;
-  uint32_t q0;    // _M_p within block `cur` (flat: the next word's index)
-  bool have_next;
+  const uint32_t* tw;
+  uint32_t q0;
+  uint64_t fa = 0;
+  uint32_t fmask = ~0u, fnw = ~0u;
   __device__ __forceinline__ uint32_t word(uint32_t r) const {
-    if (!raw) return tw[r];
-    return mt_word(tw, cur, r);
-  }
-  // make words [q0, q0 + 64) available (twists the next block on demand)
-  __device__ __forceinline__ void ensure(int lane) {
-    if (!raw) return;
-    uint32_t* twm = const_cast<uint32_t*>(tw);
-    for (;;) {
-      if (q0 >= 624) {
-        if (!have_next) {
-          mt_twist(raw + cur * 624, raw + (cur ^ 1) * 624, lane);
-          for (int k = lane; k < 624; k += kWave)
-            twm[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
-          __syncthreads();
-        }
-        cur ^= 1;
-        q0 -= 624;
-        have_next = false;
-        continue;
-      }
-      if (q0 + kWave > 624 && !have_next) {
-        mt_twist(raw + cur * 624, raw + (cur ^ 1) * 624, lane);
-        for (int k = lane; k < 624; k += kWave)
-          twm[(cur ^ 1) * 624 + k] = mt_temper(raw[(cur ^ 1) * 624 + k]);
-        __syncthreads();
-        have_next = true;
-      }
-      return;
-    }
+    return r < fnw ? tw[(uint32_t)(fa + r) & fmask] : 0u;
   }
 };
 
@@ -522,7 +516,7 @@ __device__ void mt_exact(MtStream& s, uint32_t* set, uint32_t* ans, uint32_t c, 
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t count = 0;
   while (count < n) {
-    s.ensure(lane);
+    if (s.q0 >= s.fnw) break;  // past the generated stream: the caller reports it
     const uint32_t remaining = n - count;
     const int R = remaining <= 12 ? 16 : (remaining <= 28 ? 32 : 64);
     uint32_t val = 0;
@@ -571,7 +565,7 @@ __device__ void mt_exact_tab(MtStream& s, uint32_t* tab, uint32_t* out, uint32_t
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t count = 0;
   while (count < n) {
-    s.ensure(lane);
+    if (s.q0 >= s.fnw) break;  // past the generated stream: the caller reports it
     const uint32_t remaining = n - count;
     uint32_t val = 0;
     bool ok = mt_apply(s.word(s.q0 + lane), deg, thr, lemire, val);
@@ -611,7 +605,7 @@ __device__ void mt_exact_hashed(MtStream& s, uint32_t* tab, uint32_t* out, uint3
   __syncthreads();
   uint32_t count = 0;
   while (count < n) {
-    s.ensure(lane);
+    if (s.q0 >= s.fnw) break;  // past the generated stream: the caller reports it
     const uint32_t remaining = n - count;
     uint32_t val = 0;
     const bool ok = mt_apply(s.word(s.q0 + lane), deg, thr, lemire, val);
@@ -659,9 +653,14 @@ constexpr uint32_t kMtStage = 12288;
 // the bulk-generated stream (staged in LDS when they fit), and no generator
 // state is kept.
 struct MtChunked {
-  const uint32_t* words;    // tempered words of the layer (k_mtp_gen)
-  const uint32_t* base;     // [v + 1] exclusive scan of the draws n
-  const uint32_t* entries;  // [chunks + 1] extra words consumed before each chunk
+  const uint32_t* ring;     // the stream ring (nts_hip_ctx::mt_ring)
+  const uint64_t* a0p;      // FLAT: the layer's first stream word (k_mt_prep copied it)
+  uint64_t gen_hi;          // stream words generated for the layer (absolute)
+  const uint32_t* base;     // FLAT: [v + 1] exclusive scan of the draws n
+  const uint32_t* entries;  // FLAT: [chunks + 1] extra words consumed before each chunk
+  uint64_t* done;           // !FLAT: mt_done (the layer starts at its position, ends there)
+  uint32_t seq;             // !FLAT: the layer's sequence number
+  uint32_t* ovf;            // !FLAT: sizes[3] (bit 2: the generated stream fell short)
 };
 
 template <int G, bool FLAT>
@@ -676,7 +675,7 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
   constexpr uint32_t TAB = kMtTab / K;
   constexpr uint64_t GM = (G == 64) ? ~0ull : ((1ull << (G & 63)) - 1ull);
   constexpr uint32_t NINF = FLAT ? kMtChunk : kMtInfo;
-  __shared__ uint32_t wl[FLAT ? kMtStage : 4 * 624];  // FLAT: staged words; else raw + tempered
+  __shared__ uint32_t wl[FLAT ? kMtStage : 1];  // FLAT: the chunk's words staged
   __shared__ uint32_t tab[kMtTab];
   __shared__ uint32_t set[kSetCap];
   __shared__ uint4 inf[NINF];
@@ -685,28 +684,31 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
   const int grp = lane / G, gl = lane % G;
   const bool lemire = lemire_i != 0;
   uint32_t vv = sizes[0], i0 = 0;
-  MtStream s{nullptr, nullptr, 0, 0u, false};
+  MtStream s{nullptr, 0u};
+  uint64_t a0 = 0;
   if constexpr (FLAT) {
     i0 = blockIdx.x * kMtChunk;
     if (i0 >= vv) return;
     vv = min(vv, i0 + kMtChunk);
+    a0 = *ch.a0p;
+    const MtWords W{ch.ring, a0, (uint32_t)(ch.gen_hi - a0)};
     const uint32_t e0 = ch.base[i0] + ch.entries[blockIdx.x];
     const uint32_t nw = ch.base[vv] + ch.entries[blockIdx.x + 1] - e0;
     if (nw <= kMtStage) {
-      for (uint32_t k = lane; k < nw; k += kWave) wl[k] = ch.words[e0 + k];
+      for (uint32_t k = lane; k < nw; k += kWave) wl[k] = W[e0 + k];
       s.tw = wl;
-    } else {
-      s.tw = ch.words + e0;  // (rare) read the chunk's words in place
+    } else {  // (rare) read the chunk's words in place
+      s.tw = ch.ring;
+      s.fa = a0 + e0;
+      s.fmask = kMtRingMask;
+      s.fnw = W.nw > e0 ? W.nw - e0 : 0u;
     }
-  } else {
-    uint32_t* raw = wl;
-    uint32_t* tw = wl + 2 * 624;
-    for (int k = lane; k < 624; k += kWave) {
-      const uint32_t x = mt_state[k];
-      raw[k] = x;
-      tw[k] = mt_temper(x);
-    }
-    s = MtStream{raw, tw, 0, mt_state[624], false};
+  } else {  // the whole layer, from the stream position after the last MT layer
+    a0 = *ch.done & kMtPosMask;
+    s.tw = ch.ring;
+    s.fa = a0;
+    s.fmask = kMtRingMask;
+    s.fnw = (uint32_t)(ch.gen_hi - a0);
   }
   for (uint32_t k = lane; k < kMtTab; k += kWave) tab[k] = 0u;  // no stale kMtTaken marks
   const uint32_t v = vv;
@@ -731,7 +733,6 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
       cbase = ci;
       __syncthreads();
     }
-    s.ensure(lane);
     // the K dsts i .. i+K-1, speculative start of each
     uint4 mine = (i + grp < v) ? inf[i - ibase + grp] : zero;
     uint32_t n_k[K];
@@ -828,15 +829,15 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
   __syncthreads();
   for (uint32_t k = lane; k < chi - cbase && chi > cbase; k += kWave) ans[cbase + k] = pbuf[k];
   if constexpr (!FLAT) {
-    // persist the generator state as std::mt19937 holds it: (_M_x, _M_p) with
-    // _M_p == 624 kept as is (libstdc++ twists lazily on the next call)
-    if (s.q0 > 624) {
-      s.cur ^= 1;
-      s.q0 -= 624;
+    // the stream position after the layer, and the generator state as
+    // std::mt19937 holds it there
+    const uint32_t used = s.q0;
+    if (used > s.fnw) {  // the generated stream fell short: the host reports it
+      if (lane == 0) atomicOr(ch.ovf, 4u);
+      return;
     }
-    __syncthreads();
-    for (int k = lane; k < 624; k += kWave) mt_state[k] = wl[s.cur * 624 + k];
-    if (lane == 0) mt_state[624] = s.q0;
+    if (lane == 0) *ch.done = ((a0 + used) & kMtPosMask) | ((uint64_t)ch.seq << 40);
+    if (used > 0) mt_state_at(ch.ring, a0 + used, mt_state, lane);
   }
 }
 
@@ -857,8 +858,7 @@ constexpr uint32_t kMtChunkedMinV = 32768;  // dst capacity from which a layer i
 // n when its first n words are accepted and pairwise distinct, else the
 // sequential count; `lst` holds up to NMAX distinct positions of this lane.
 template <int NMAX>
-__device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W, uint32_t nw,
-                                                 uint32_t p, uint32_t n, uint32_t deg,
+__device__ __forceinline__ uint32_t lane_consume(const MtWords& W, uint32_t p, uint32_t n, uint32_t deg,
                                                  uint32_t thr, bool lemire, uint32_t* lst,
                                                  uint32_t lstride) {
   uint32_t val[NMAX];
@@ -867,7 +867,7 @@ __device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W,
   for (int t = 0; t < NMAX; ++t) {
     if ((uint32_t)t < n) {
       const uint32_t q = p + t;
-      clean &= mt_apply(q < nw ? W[q] : 0u, deg, thr, lemire, val[t]);
+      clean &= mt_apply(W[q], deg, thr, lemire, val[t]);
     }
   }
 #pragma unroll
@@ -882,7 +882,7 @@ __device__ __forceinline__ uint32_t lane_consume(const uint32_t* __restrict__ W,
   while (cnt < n) {
     uint32_t buf[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) buf[j] = q + j < nw ? W[q + j] : 0u;
+    for (int j = 0; j < 16; ++j) buf[j] = W[q + j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       uint32_t x;
@@ -928,58 +928,25 @@ __device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint
   return used;
 }
 
-// bulk generation: W[t] = the tempered word at _M_p + t of the stream in
-// mt_state, t < nw (written to *nw_out); rb[b] = raw block b (b = 0: the
-// state's own).  nw = draws + expected extras + 10 sigma + 4096 (<= w_cap).
-// (A one-wave form with the block in registers and the twist operands moved
-// by lane rotations measured slower: 1.92 vs 1.47 ms per C2 bottom layer —
-// the rotations' latency chain is longer than three barriers.)
+// The stream ring's generator: nblk more 624-word blocks of the stream after
+// the raw block in `raw` (block blk0 - 1), tempered into the ring at words
+// 624 blk0 ...; `raw` is left holding the last one.  One workgroup (a twist is
+// three dependent pieces of 227 / 227 / 170 words); it runs on the ring's side
+// stream, ahead of the layers that read the words (mt_ring_prepare).  (A
+// one-wave form with the block in registers and the twist operands moved by
+// lane rotations measured slower: 1.92 vs 1.47 ms per C2 bottom layer.)
 constexpr int kGenThreads = 256;
-__global__ __launch_bounds__(kGenThreads) void k_mtp_gen(const uint32_t* __restrict__ mt_state,
-                                                        const uint32_t* base, const uint32_t* sizes,
-                                                        const float2* cstat, uint32_t w_cap,
-                                                        uint32_t* __restrict__ W,
-                                                        uint32_t* __restrict__ rb,
-                                                        uint32_t* nw_out) {
+__global__ __launch_bounds__(kGenThreads) void k_mt_ring_gen(uint32_t* __restrict__ raw,
+                                                            uint32_t* __restrict__ ring,
+                                                            uint64_t blk0, uint32_t nblk) {
   __shared__ uint32_t blk[2][624];
-  __shared__ float red[2][kGenThreads / kWave];
   const int t = threadIdx.x;
-  const uint32_t v = sizes[0];
-  const uint32_t nch = (v + kMtChunkP - 1) / kMtChunkP;
-  float m = 0.f, var = 0.f;
-  for (uint32_t k = t; k < nch; k += kGenThreads) {
-    m += cstat[k].x;
-    var += cstat[k].y;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    m += __shfl_down(m, o, kWave);
-    var += __shfl_down(var, o, kWave);
-  }
-  if ((t & 63) == 0) {
-    red[0][t >> 6] = m;
-    red[1][t >> 6] = var;
-  }
-  for (int k = t; k < 624; k += kGenThreads) {
-    blk[0][k] = mt_state[k];
-    rb[k] = mt_state[k];
-  }
+  for (int k = t; k < 624; k += kGenThreads) blk[0][k] = raw[k];
   __syncthreads();
-  float mm = 0.f, vv = 0.f;
-  for (int w = 0; w < kGenThreads / kWave; ++w) {
-    mm += red[0][w];
-    vv += red[1][w];
-  }
-  const double want = (double)base[v] + (double)mm + 10.0 * sqrt((double)vv) + 4096.0;
-  const uint32_t nw = (uint32_t)fmin(want, (double)w_cap);
-  const uint32_t q0 = mt_state[624];
-  if (t == 0) *nw_out = nw;
-  for (uint32_t a = q0 + t; a < 624; a += kGenThreads)
-    if (a - q0 < nw) W[a - q0] = mt_temper(blk[0][a]);
   const uint32_t U = 0x80000000u, L = 0x7fffffffu, A = 0x9908b0dfu;
-  for (uint32_t b = 1; 624u * b - q0 < nw; ++b) {
-    const uint32_t* cur = blk[(b - 1) & 1];
-    uint32_t* nxt = blk[b & 1];
+  for (uint32_t b = 0; b < nblk; ++b) {
+    const uint32_t* cur = blk[b & 1];
+    uint32_t* nxt = blk[(b + 1) & 1];
     // _M_gen_rand in three dependent pieces: [0,227) from the current block,
     // [227,454) and [454,624) from the words just made
     if (t < 227) {
@@ -999,13 +966,12 @@ __global__ __launch_bounds__(kGenThreads) void k_mtp_gen(const uint32_t* __restr
       nxt[k] = nxt[k - 227] ^ (y >> 1) ^ ((y & 1u) ? A : 0u);
     }
     __syncthreads();
-    const uint32_t o = 624u * b - q0;
-    for (int k = t; k < 624; k += kGenThreads) {
-      const uint32_t x = nxt[k];
-      rb[(uint64_t)b * 624 + k] = x;
-      if (o + k < nw) W[o + k] = mt_temper(x);
-    }
+    const uint64_t w0 = (blk0 + b) * 624;
+    for (int k = t; k < 624; k += kGenThreads)
+      ring[(uint32_t)(w0 + k) & kMtRingMask] = mt_temper(nxt[k]);
   }
+  __syncthreads();
+  for (int k = t; k < 624; k += kGenThreads) raw[k] = blk[nblk & 1][k];
 }
 
 // the window tables: block (x, k) = entries lo_k + 256 x + t of chunk k
@@ -1013,9 +979,9 @@ template <int NMAX>
 __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ info,
                                                    const uint32_t* __restrict__ base,
                                                    const uint32_t* sizes, const float2* cstat,
-                                                   const uint32_t* __restrict__ W,
-                                                   const uint32_t* nw_dev, int lemire_i,
-                                                   uint2* __restrict__ win,
+                                                   const uint32_t* __restrict__ ring,
+                                                   const uint64_t* a0p, uint64_t gen_hi,
+                                                   int lemire_i, uint2* __restrict__ win,
                                                    uint32_t* __restrict__ tabs) {
   __shared__ uint4 inf[kMtChunk];
   __shared__ uint32_t bs[kMtChunk];
@@ -1053,7 +1019,8 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   if (blockIdx.x == 0 && t == 0) win[k] = make_uint2(lo, wn);
   if (blockIdx.x * 256u >= wn) return;
   const uint32_t slot = blockIdx.x * 256u + t;
-  const uint32_t nw = *nw_dev;
+  const uint64_t a0 = *a0p;
+  const MtWords W{ring, a0, (uint32_t)(gen_hi - a0)};
   const bool lemire = lemire_i != 0;
   uint32_t dl = lo + slot;
   // software pipeline: the words of the next drawing dst are fetched while
@@ -1071,7 +1038,7 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   uint32_t wv[NW];
   uint32_t pf = j < cnt ? bs[j] + dl : 0u;
 #pragma unroll
-  for (int q = 0; q < NW; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
+  for (int q = 0; q < NW; ++q) wv[q] = W[pf + q];
   while (j < cnt) {
     const uint4 f = inf[j];
     const uint32_t p = bs[j] + dl;
@@ -1080,14 +1047,14 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
     for (int q = 0; q < NW; ++q) cur[q] = wv[q];
     if (p != pf) {  // (the previous dst consumed extra words)
 #pragma unroll
-      for (int q = 0; q < NW; ++q) cur[q] = p + q < nw ? W[p + q] : 0u;
+      for (int q = 0; q < NW; ++q) cur[q] = W[p + q];
     }
     const uint32_t jn = next_draw(j + 1);
     pf = jn < cnt ? bs[jn] + dl : 0u;
 #pragma unroll
-    for (int q = 0; q < NW; ++q) wv[q] = pf + q < nw ? W[pf + q] : 0u;
+    for (int q = 0; q < NW; ++q) wv[q] = W[pf + q];
     uint32_t used = regs_consume<NW>(cur, f.y, f.z, f.w, lemire);
-    if (used == 0) used = lane_consume<NMAX>(W, nw, p, f.y, f.z, f.w, lemire, lst + t, 256);
+    if (used == 0) used = lane_consume<NMAX>(W, p, f.y, f.z, f.w, lemire, lst + t, 256);
     dl += used - f.y;
     j = jn;
   }
@@ -1116,12 +1083,14 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
 template <int NMAX>
 __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__ info,
                                                       const uint32_t* __restrict__ base,
-                                                      const uint32_t* sizes, const uint32_t* W,
-                                                      const uint32_t* nw_dev, int lemire_i,
+                                                      const uint32_t* sizes,
+                                                      const uint32_t* __restrict__ sring,
+                                                      const uint64_t* a0p, uint64_t gen_hi,
+                                                      int lemire_i,
                                                       const uint2* __restrict__ win,
                                                       const uint32_t* __restrict__ tabs,
                                                       uint32_t* __restrict__ entries,
-                                                      const uint32_t* __restrict__ rb,
+                                                      uint64_t* __restrict__ done, uint32_t seq,
                                                       uint32_t* __restrict__ mt_state,
                                                       uint32_t* __restrict__ ovf,
                                                       uint32_t* __restrict__ nfallback) {
@@ -1136,7 +1105,9 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const bool lemire = lemire_i != 0;
-  const uint32_t nw = *nw_dev;
+  const uint64_t a0 = *a0p;
+  const MtWords W{sring, a0, (uint32_t)(gen_hi - a0)};
+  const uint32_t nw = W.nw;
   auto fetch = [&](uint32_t k) {  // window of chunk min(k, nch - 1) -> ring slot k % kRing
     const uint32_t kk = nch ? min(k, nch - 1) : 0u;
     const char* src = reinterpret_cast<const char*>(tabs + (uint64_t)kk * kMtWmax);
@@ -1161,7 +1132,7 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
         for (uint32_t j = i0; j < i1; ++j) {
           const uint4 f = info[j];
           if (f.y == 0) continue;
-          d2 += lane_consume<NMAX>(W, nw, base[j] + d2, f.y, f.z, f.w, lemire, lst, 1) - f.y;
+          d2 += lane_consume<NMAX>(W, base[j] + d2, f.y, f.z, f.w, lemire, lst, 1) - f.y;
         }
       }
       dl = __builtin_amdgcn_readfirstlane(d2);
@@ -1178,19 +1149,13 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
     if (dl + base[v] > nw) *ovf |= 4u;  // the stream generated fell short
     *nfallback = fallbacks;
   }
-  // the generator after the layer: _M_p + consumed words from the state's block
-  // (only when the words consumed are inside the generated stream: past it the
-  // block index leaves rb, and the host reports the short stream)
-  if (dl + base[v] > nw) return;
-  const uint32_t a = mt_state[624] + base[v] + dl;
-  uint32_t b = a / 624, off = a % 624;
-  if (off == 0 && b > 0) {  // libstdc++ keeps the exhausted block until the next call
-    --b;
-    off = 624;
-  }
-  __syncthreads();
-  for (int k = lane; k < 624; k += kWave) mt_state[k] = rb[(uint64_t)b * 624 + k];
-  if (lane == 0) mt_state[624] = off;
+  // the stream position after the layer, and the generator state there
+  // (only when the words consumed are inside the generated stream: the host
+  // reports a short stream)
+  const uint32_t used = base[v] + dl;
+  if (used > nw) return;
+  if (lane == 0) *done = ((a0 + used) & kMtPosMask) | ((uint64_t)seq << 40);
+  if (used > 0) mt_state_at(sring, a0 + used, mt_state, lane);
 }
 
 // positions -> neighbour ids (16-lane group per dst); copy-path dsts take
@@ -1495,6 +1460,141 @@ __global__ void k_csr_finalize(const uint32_t* __restrict__ skey, const uint32_t
 
 }  // namespace nts_hip
 
+namespace nts_hip {
+
+// ---- the stream ring, host side ----------------------------------------------
+// Words are generated in launches of up to kMtGenChunk blocks on the ring's
+// own stream, each followed by an event; a layer waits on the event that
+// covers its words.  Bound on the words a layer may consume: its w_cap (a
+// layer past it reports a short stream, sizes[3] bit 2).  The host keeps the
+// position read back after the last finished MT layer (mt_done, copied to
+// pinned memory after each layer) plus the bounds of the layers issued since,
+// generates up to that sum plus two layers' bounds ahead, and never more than
+// the ring holds beyond the oldest word a pending layer can still read.
+constexpr uint32_t kMtGenChunk = 4096;  // ~2.7 ms of generation per launch
+
+static int mt_ring_ensure(nts_hip_ctx* ctx) {
+  if (ctx->mt_ring) return NTS_OK;
+  // first MT layer since the context was created: the generator starts from
+  // the seeded state (no MT layer has moved it)
+  NTS_HIP_TRY(hipMalloc(&ctx->mt_ring, kMtRingWords * sizeof(uint32_t)));
+  NTS_HIP_TRY(hipMalloc(&ctx->mt_gen_raw, 624 * sizeof(uint32_t)));
+  NTS_HIP_TRY(hipMalloc(&ctx->mt_done, sizeof(uint64_t)));
+  NTS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->mt_done_host), sizeof(uint64_t),
+                            hipHostMallocDefault));
+  NTS_HIP_TRY(hipStreamCreateWithFlags(&ctx->mt_gen_stream, hipStreamNonBlocking));
+  return mt_ring_reset(ctx);
+}
+
+int mt_ring_reset(nts_hip_ctx* ctx) {
+  if (!ctx->mt_ring) return NTS_OK;
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->mt_gen_stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  NTS_HIP_TRY(hipMemcpy(ctx->mt_gen_raw, ctx->mt_state, 624 * sizeof(uint32_t),
+                        hipMemcpyDeviceToDevice));
+  NTS_HIP_TRY(hipMemset(ctx->mt_done, 0, sizeof(uint64_t)));
+  *ctx->mt_done_host = 0;
+  ctx->mt_gen_blocks = 0;
+  ctx->mt_seq = 0;
+  ctx->mt_pos_done = 0;
+  ctx->mt_seq_done = 0;
+  ctx->mt_pending.clear();
+  for (auto& e : ctx->mt_gen_evs) ctx->mt_ev_pool.push_back(e.second);
+  ctx->mt_gen_evs.clear();
+  return NTS_OK;
+}
+
+void mt_ring_free(nts_hip_ctx* ctx) {
+  if (ctx->mt_gen_stream) (void)hipStreamSynchronize(ctx->mt_gen_stream);
+  for (auto& e : ctx->mt_gen_evs) (void)hipEventDestroy(e.second);
+  for (auto ev : ctx->mt_ev_pool) (void)hipEventDestroy(ev);
+  ctx->mt_gen_evs.clear();
+  ctx->mt_ev_pool.clear();
+  if (ctx->mt_gen_stream) (void)hipStreamDestroy(ctx->mt_gen_stream);
+  if (ctx->mt_ring) (void)hipFree(ctx->mt_ring);
+  if (ctx->mt_gen_raw) (void)hipFree(ctx->mt_gen_raw);
+  if (ctx->mt_done) (void)hipFree(ctx->mt_done);
+  if (ctx->mt_done_host) (void)hipHostFree(ctx->mt_done_host);
+  ctx->mt_gen_stream = nullptr;
+  ctx->mt_ring = ctx->mt_gen_raw = nullptr;
+  ctx->mt_done = ctx->mt_done_host = nullptr;
+}
+
+static void mt_ring_readback(nts_hip_ctx* ctx) {
+  const uint64_t snap = __atomic_load_n(ctx->mt_done_host, __ATOMIC_ACQUIRE);
+  const uint32_t sseq = (uint32_t)(snap >> 40);
+  if (sseq == ctx->mt_seq_done) return;
+  ctx->mt_seq_done = sseq;
+  ctx->mt_pos_done = snap & kMtPosMask;
+  auto& p = ctx->mt_pending;  // layers up to sseq are in mt_pos_done now
+  p.erase(p.begin(), std::find_if(p.begin(), p.end(), [&](const std::pair<uint32_t, uint64_t>& e) {
+            return ((sseq - e.first) & 0xFFFFFFu) >= (1u << 23);  // e.first > sseq (24-bit order)
+          }));
+}
+
+int mt_ring_prepare(nts_hip_ctx* ctx, uint64_t w_bound, hipStream_t st, uint64_t* gen_hi,
+                    uint32_t* seq) {
+  NTS_RET(mt_ring_ensure(ctx));
+  mt_ring_readback(ctx);
+  auto upper_now = [&] {
+    uint64_t u = ctx->mt_pos_done + w_bound;
+    for (auto& e : ctx->mt_pending) u += e.second;
+    return u;
+  };
+  // through the block holding the last word the layer may read, + one block
+  uint64_t need = upper_now() / 624 + 2;
+  auto ring_cap = [&] {  // blocks the generator may reach without overwriting
+    const uint64_t oldest = ctx->mt_pos_done >= 624 ? ctx->mt_pos_done - 624 : 0;
+    return (oldest + kMtRingWords) / 624;
+  };
+  if (need > ring_cap()) {  // too far ahead of what has been read back: wait for the layers
+    NTS_HIP_TRY(hipStreamSynchronize(st));
+    mt_ring_readback(ctx);
+    need = upper_now() / 624 + 2;
+    NTS_CHECK_ARG(need <= ring_cap(), "MT19937: a layer's word bound exceeds the stream ring");
+  }
+  ctx->mt_seq = (ctx->mt_seq + 1) & 0xFFFFFFu;
+  if (ctx->mt_seq == 0) ctx->mt_seq = 1;  // (0: nothing done yet)
+  *seq = ctx->mt_seq;
+  ctx->mt_pending.push_back({ctx->mt_seq, w_bound});
+  const uint64_t target = std::min(need + 2 * (w_bound / 624 + 1), ring_cap());
+  while (ctx->mt_gen_blocks < target) {
+    const uint32_t n = (uint32_t)std::min<uint64_t>(target - ctx->mt_gen_blocks, kMtGenChunk);
+    hipLaunchKernelGGL(k_mt_ring_gen, dim3(1), dim3(kGenThreads), 0, ctx->mt_gen_stream,
+                       ctx->mt_gen_raw, ctx->mt_ring, ctx->mt_gen_blocks, n);
+    NTS_LAUNCH_CHECK();
+    ctx->mt_gen_blocks += n;
+    hipEvent_t ev;
+    if (!ctx->mt_ev_pool.empty()) {
+      ev = ctx->mt_ev_pool.back();
+      ctx->mt_ev_pool.pop_back();
+    } else {
+      NTS_HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    NTS_HIP_TRY(hipEventRecord(ev, ctx->mt_gen_stream));
+    ctx->mt_gen_evs.push_back({ctx->mt_gen_blocks, ev});
+  }
+  // wait for the first launch that covers the layer's words; launches before
+  // it are complete then too (one stream), so their events go back to the pool
+  auto& evs = ctx->mt_gen_evs;
+  size_t i = 0;
+  while (i + 1 < evs.size() && evs[i].first < need) ++i;
+  NTS_HIP_TRY(hipStreamWaitEvent(st, evs[i].second, 0));
+  *gen_hi = evs[i].first * 624;
+  for (size_t k = 0; k < i; ++k) ctx->mt_ev_pool.push_back(evs[k].second);
+  evs.erase(evs.begin(), evs.begin() + i);
+  return NTS_OK;
+}
+
+// after a layer's last MT kernel: its end position back to the host (pinned)
+int mt_ring_finish(nts_hip_ctx* ctx, hipStream_t st) {
+  NTS_HIP_TRY(hipMemcpyAsync(ctx->mt_done_host, ctx->mt_done, sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, st));
+  return NTS_OK;
+}
+
+}  // namespace nts_hip
+
 using namespace nts_hip;
 
 extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, int fanout,
@@ -1552,14 +1652,12 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t mt_info_n = rng_mode != NTS_RNG_PHILOX ? al((uint64_t)o->v_cap * 4) : 0;
   const uint64_t mt_base_n = mt_chunked ? al((uint64_t)o->v_cap + 1) : 0;
   const uint64_t mt_stat_n = mt_chunked ? al(2 * nch_cap) : 0;
-  const uint64_t mt_w_n = mt_chunked ? al(w_cap + 256) : 0;  // + the walks' look-ahead
-  const uint64_t mt_rb_n = mt_chunked ? al((w_cap / 624 + 3) * 624) : 0;
   const uint64_t mt_win_n = mt_chunked ? al(2 * nch_cap) : 0;
   const uint64_t mt_tab_n = mt_chunked ? al(nch_cap * kMtWmax) : 0;
   const uint64_t mt_ent_n = mt_chunked ? al(nch_cap + 1) : 0;
   const uint64_t mt_misc_n = mt_chunked ? 64 : 0;
-  const uint64_t mt_n = mt_info_n + mt_base_n + mt_stat_n + mt_w_n + mt_rb_n + mt_win_n +
-                        mt_tab_n + mt_ent_n + mt_misc_n;
+  const uint64_t mt_n = mt_info_n + mt_base_n + mt_stat_n + mt_win_n + mt_tab_n + mt_ent_n +
+                        mt_misc_n;
   const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n) *
                           sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
@@ -1630,64 +1728,72 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
     const int lem = rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0;
     static const int mt_dbg = getenv("NTS_MT_DEBUG") ? 1 : 0;
     uint4* info = reinterpret_cast<uint4*>(t_mt);
+    // the stream words this layer may read are generated (ahead, on the
+    // ring's side stream) before its kernels run
+    uint64_t gen_hi = 0;
+    uint32_t seq = 0;
+    NTS_RET(mt_ring_prepare(ctx, w_cap, st, &gen_hi, &seq));
     if (mt_chunked) {
       uint32_t* base = t_mt + mt_info_n;
       float2* cstat = reinterpret_cast<float2*>(base + mt_base_n);
-      uint32_t* W = base + mt_base_n + mt_stat_n;
-      uint32_t* rb = W + mt_w_n;
-      uint2* win = reinterpret_cast<uint2*>(rb + mt_rb_n);
-      uint32_t* tabs = rb + mt_rb_n + mt_win_n;
+      uint2* win = reinterpret_cast<uint2*>(base + mt_base_n + mt_stat_n);
+      uint32_t* tabs = base + mt_base_n + mt_stat_n + mt_win_n;
       uint32_t* entries = tabs + mt_tab_n;
-      uint32_t* misc = entries + mt_ent_n;  // [0] words generated, [1] fallbacks
+      uint32_t* misc = entries + mt_ent_n;  // [1] fallbacks, [2..3] the layer's first stream word
+      uint64_t* a0p = reinterpret_cast<uint64_t*>(misc + 2);
       NTS_HIP_TRY(hipMemsetAsync(cstat, 0, mt_stat_n * sizeof(uint32_t), st));
       hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                         o->column_offset, o->sizes, o->e_cap, lem, info, base, cstat);
+                         o->column_offset, o->sizes, o->e_cap, lem, info, base, cstat,
+                         (const uint64_t*)ctx->mt_done, a0p);
       NTS_LAUNCH_CHECK();
       NTS_RET(scan1_exclusive(ctx, base, base, o->sizes, o->v_cap, st));
-      hipLaunchKernelGGL(k_mtp_gen, dim3(1), dim3(kGenThreads), 0, st, ctx->mt_state, base,
-                         o->sizes, cstat, (uint32_t)w_cap, W, rb, misc);
-      NTS_LAUNCH_CHECK();
       const dim3 tgrid(kMtWmax / 256, (uint32_t)nch_cap);
-      const MtChunked chunked{W, base, entries};
+      const MtChunked chunked{ctx->mt_ring, a0p, gen_hi, base, entries, nullptr, 0u, nullptr};
       if (fanout <= 16) {
         hipLaunchKernelGGL(k_mtp_tables<16>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
-                           W, misc, lem, win, tabs);
+                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs);
         NTS_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_mtp_resolve<16>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes, W,
-                           misc, lem, win, tabs, entries, rb, ctx->mt_state, o->sizes + 3, misc + 1);
+        hipLaunchKernelGGL(k_mtp_resolve<16>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
+                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs, entries, ctx->mt_done, seq,
+                           ctx->mt_state, o->sizes + 3, misc + 1);
         NTS_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_mt_serial<16, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
                            info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
       } else {
         hipLaunchKernelGGL(k_mtp_tables<32>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
-                           W, misc, lem, win, tabs);
+                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs);
         NTS_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_mtp_resolve<32>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes, W,
-                           misc, lem, win, tabs, entries, rb, ctx->mt_state, o->sizes + 3, misc + 1);
+        hipLaunchKernelGGL(k_mtp_resolve<32>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
+                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs, entries, ctx->mt_done, seq,
+                           ctx->mt_state, o->sizes + 3, misc + 1);
         NTS_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_mt_serial<32, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
                            info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
       }
       NTS_LAUNCH_CHECK();
+      NTS_RET(mt_ring_finish(ctx, st));
       const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
       hipLaunchKernelGGL(k_mt_rows, dim3(gs), dim3(kSelThreads), 0, st, a);
       NTS_LAUNCH_CHECK();
       goto frontier;
     }
     hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                       o->column_offset, o->sizes, o->e_cap, lem, info, nullptr, nullptr);
+                       o->column_offset, o->sizes, o->e_cap, lem, info, nullptr, nullptr,
+                       nullptr, nullptr);
     NTS_LAUNCH_CHECK();
-    const MtChunked none{nullptr, nullptr, nullptr};
+    const MtChunked whole{ctx->mt_ring, nullptr, gen_hi, nullptr, nullptr, ctx->mt_done, seq,
+                          o->sizes + 3};
     if (fanout >= 0 && fanout <= 16)
       hipLaunchKernelGGL((k_mt_serial<16, false>), dim3(1), dim3(kWave), 0, st, info, o->sizes,
-                         o->sample_ans, ctx->mt_state, lem, mt_dbg, none);
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg, whole);
     else if (fanout >= 0 && fanout <= 32)
       hipLaunchKernelGGL((k_mt_serial<32, false>), dim3(1), dim3(kWave), 0, st, info, o->sizes,
-                         o->sample_ans, ctx->mt_state, lem, mt_dbg, none);
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg, whole);
     else
       hipLaunchKernelGGL((k_mt_serial<64, false>), dim3(1), dim3(kWave), 0, st, info, o->sizes,
-                         o->sample_ans, ctx->mt_state, lem, mt_dbg, none);
+                         o->sample_ans, ctx->mt_state, lem, mt_dbg, whole);
     NTS_LAUNCH_CHECK();
+    NTS_RET(mt_ring_finish(ctx, st));
     const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));
     hipLaunchKernelGGL(k_mt_rows, dim3(gs), dim3(kSelThreads), 0, st, a);
   }
