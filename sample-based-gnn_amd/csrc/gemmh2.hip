@@ -1154,10 +1154,6 @@ constexpr int kH2Nn3KS = 20;  // k-steps held in registers (Kp <= 640)
 // TR (no epilogue activation, NKS > 0): the MFMA operands swapped so that
 // each lane holds four consecutive columns of one row — one 16-byte store per
 // lane and tile instead of four 4-byte stores
-#ifndef NTS_NN3_ACC2
-#define NTS_NN3_ACC2 0  // compile-time A/B (make variant VFLAGS=-DNTS_NN3_ACC2=1)
-#endif
-constexpr bool kNn3Acc2 = NTS_NN3_ACC2 != 0;
 template <bool EPI, bool AMAP, int NKS = 0, int DIAG = 0, bool RP = false, bool TR = false>
 __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const char* __restrict__ Q,
                                                   uint64_t ldq, int pitch, int plane_bytes,
@@ -1254,16 +1250,8 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
     if (!(DIAG & 2)) NTS_NN3_ISSUE(r + 2);
     const char* xs = sx + (r % 3) * xstage + i * pitch;
     f32x4h acc = f32x4h{0.f, 0.f, 0.f, 0.f};
-    // kNn3Acc2: odd k-steps into a second accumulator (two independent MFMA
-    // chains per wave), summed after the step loop
-    f32x4h acc_o = f32x4h{0.f, 0.f, 0.f, 0.f};
     auto step = [&](int s, const f16x8& a1, const f16x8& a0) {
-      if constexpr (kNn3Acc2 && !(DIAG & 1) && !TR) {
-        f32x4h& ac = (s & 1) ? acc_o : acc;
-        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, wf[s][0], ac, 0, 0, 0);
-        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][1], ac, 0, 0, 0);
-        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, wf[s][0], ac, 0, 0, 0);
-      } else if constexpr (DIAG & 1) {
+      if constexpr (DIAG & 1) {
         acc[0] += (float)a1[0] + (float)a0[0] + (float)wf[s][0][0] + (float)wf[s][1][0];
       } else if constexpr (TR) {  // D^T: rows of W^T (columns) x columns of X^T (rows)
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[s][0], a1, acc, 0, 0, 0);
@@ -1299,10 +1287,6 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 #pragma unroll
       for (int s = 0; s < kH2Nn3KS; ++s)
         if (s < nks) step(s, ld1(s), ld0(s));
-    }
-    if constexpr (kNn3Acc2 && !(DIAG & 1) && !TR) {
-#pragma unroll
-      for (int v = 0; v < 4; ++v) acc[v] += acc_o[v];
     }
     if constexpr (TR) {  // acc[v] = H[16 (t0 + r) + i][n0 + 16 wv + 4 g + v]
       const int64_t row = (int64_t)(t0 + r) * 16 + i;
