@@ -928,6 +928,26 @@ __device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint
   return used;
 }
 
+// regs_consume on words already applied (the accepted position, or
+// 0xFFFFFFFF for a rejected word) in an LDS window: word t at u[t]
+template <int NW>
+__device__ __forceinline__ uint32_t window_consume(const uint32_t* u, uint32_t n) {
+  constexpr uint32_t kRej = 0xFFFFFFFFu;
+  uint32_t val[NW];
+  uint32_t cnt = 0, used = 0;
+#pragma unroll
+  for (int t = 0; t < NW; ++t) {
+    if ((uint32_t)t >= n && __ballot(used == 0) == 0) break;
+    val[t] = u[t];
+    bool dup = val[t] == kRej;
+#pragma unroll
+    for (int b = 0; b < t; ++b) dup |= val[b] == val[t];
+    cnt += dup ? 0u : 1u;
+    used = (used == 0 && cnt == n) ? (uint32_t)t + 1u : used;
+  }
+  return used;
+}
+
 // The stream ring's generator: nblk more 624-word blocks of the stream after
 // the raw block in `raw` (block blk0 - 1), tempered into the ring at words
 // 624 blk0 ...; `raw` is left holding the last one.  One workgroup (a twist is
@@ -987,6 +1007,7 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   __shared__ uint32_t bs[kMtChunk];
   __shared__ uint32_t lst[NMAX * 256];
   __shared__ float red[2][4];
+  __shared__ uint32_t uu[4][2][192];  // per wave: the union windows of two dsts
   const int t = threadIdx.x;
   const uint32_t k = blockIdx.y, v = sizes[0];
   const uint32_t i0 = k * kMtChunk;
@@ -1023,39 +1044,70 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   const MtWords W{ring, a0, (uint32_t)(gen_hi - a0)};
   const bool lemire = lemire_i != 0;
   uint32_t dl = lo + slot;
-  // software pipeline: the words of the next drawing dst are fetched while
-  // this one is checked, at the start it would have if this one is clean
-  // (the common case); a lane whose Delta moved fetches again
+  // The wave's lanes walk the dst with nearby starts (consecutive Deltas,
+  // drifting apart by their extra words): the union of their words, kU from
+  // the smallest start, is fetched once per wave (three words a lane) and
+  // accepted / mapped to positions once, into LDS; each lane reads its window
+  // from there.  The next drawing dst's union is fetched while this one is
+  // checked, based at this step's smallest Delta (Deltas only grow).  A wave
+  // whose starts spread wider than the union reads its own words.
+  constexpr int NW = NMAX + 8;
+  constexpr int kU = 192;
+  const int wvi = t >> 6, ln = t & 63;
+  auto wmin = [](uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, kWave));
+    return x;
+  };
+  auto wmax = [](uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, kWave));
+    return x;
+  };
+  uint32_t rw[kU / kWave];
+  auto load_union = [&](uint32_t P) {
+#pragma unroll
+    for (int q = 0; q < kU / kWave; ++q) rw[q] = W[P + ln + kWave * q];
+  };
+  auto store_union = [&](int buf, const uint4& f) {
+#pragma unroll
+    for (int q = 0; q < kU / kWave; ++q) {
+      uint32_t x;
+      uu[wvi][buf][ln + kWave * q] = mt_apply(rw[q], f.z, f.w, lemire, x) ? x : 0xFFFFFFFFu;
+    }
+  };
   const uint32_t cnt = i1 - i0;
   auto next_draw = [&](uint32_t j) {
     while (j < cnt && inf[j].y == 0) ++j;
     return j;
   };
-  // NW words per dst in registers: the n-th distinct draw is found there
-  // unless it needs more than NW - n extra words
-  constexpr int NW = NMAX + 8;
   uint32_t j = next_draw(0);
-  uint32_t wv[NW];
-  uint32_t pf = j < cnt ? bs[j] + dl : 0u;
-#pragma unroll
-  for (int q = 0; q < NW; ++q) wv[q] = W[pf + q];
+  int buf = 0;
+  uint32_t P0 = j < cnt ? bs[j] + wmin(dl) : 0u;
+  if (j < cnt) {
+    load_union(P0);
+    store_union(0, inf[j]);
+  }
   while (j < cnt) {
     const uint4 f = inf[j];
     const uint32_t p = bs[j] + dl;
-    uint32_t cur[NW];
-#pragma unroll
-    for (int q = 0; q < NW; ++q) cur[q] = wv[q];
-    if (p != pf) {  // (the previous dst consumed extra words)
+    const uint32_t jn = next_draw(j + 1);
+    const uint32_t P0n = jn < cnt ? bs[jn] + wmin(dl) : 0u;
+    if (jn < cnt) load_union(P0n);
+    uint32_t used;
+    if (wmax(p) + NW - P0 <= (uint32_t)kU) {  // (p >= P0: Deltas only grow)
+      used = window_consume<NW>(&uu[wvi][buf][p - P0], f.y);
+    } else {
+      uint32_t cur[NW];
 #pragma unroll
       for (int q = 0; q < NW; ++q) cur[q] = W[p + q];
+      used = regs_consume<NW>(cur, f.y, f.z, f.w, lemire);
     }
-    const uint32_t jn = next_draw(j + 1);
-    pf = jn < cnt ? bs[jn] + dl : 0u;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) wv[q] = W[pf + q];
-    uint32_t used = regs_consume<NW>(cur, f.y, f.z, f.w, lemire);
     if (used == 0) used = lane_consume<NMAX>(W, p, f.y, f.z, f.w, lemire, lst + t, 256);
     dl += used - f.y;
+    if (jn < cnt) store_union(buf ^ 1, inf[jn]);
+    P0 = P0n;
+    buf ^= 1;
     j = jn;
   }
   if (slot < wn) tabs[(uint64_t)k * kMtWmax + slot] = dl;
