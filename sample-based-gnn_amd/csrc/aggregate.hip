@@ -952,15 +952,12 @@ static int pick_vec(uint32_t F, uint64_t ld1, uint64_t ld2, const void* p1, cons
 struct Shape {
   int lpd, nch;
 };
-// NTS_AGG_LPD16 (compile-time A/B, `make variant`): 128-float rows on
-// 16-lane groups of two float4 per lane (four rows per wave instead of two)
-#ifndef NTS_AGG_LPD16
-#define NTS_AGG_LPD16 0
-#endif
+// (128-float rows on 16-lane groups of two float4 per lane — four rows per
+// wave instead of two — measured: hop-0 backward 42.5 vs 44.8 us, the bottom
+// CSR backward 125-127 vs 122, C2 0.824 vs 0.807 ms/step; not kept)
 static Shape pick_shape(uint32_t nv) {
   if (nv <= 8) return {8, 1};
   if (nv <= 16) return {16, 1};
-  if (NTS_AGG_LPD16 && nv > 16 && nv <= 32) return {16, 2};
   if (nv <= 32) return {32, 1};
   if (nv <= 64) return {64, 1};
   uint32_t nch = (nv + 63) / 64;
@@ -1012,7 +1009,6 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
                          nv, y, ldy, last_valid, tier, ax);                                 \
   } while (0)
   if (s.lpd == 8) NTS_G(8, 1);
-  else if (s.lpd == 16 && s.nch == 2) NTS_G(16, 2);
   else if (s.lpd == 16) NTS_G(16, 1);
   else if (s.lpd == 32) NTS_G(32, 1);
   else switch (s.nch) {
