@@ -217,6 +217,9 @@ def parse():
                    help="PD cache: batches per super-batch (PIPELINE_NUM)")
     p.add_argument("--no-fuse-act", action="store_true",
                    help="relu/dropout as torch ops instead of the GEMM epilogue")
+    p.add_argument("--sampler-gate", type=int, default=0, choices=[0, 1, 2],
+                   help="pipelined sampler behind the bottom forward GEMM (1), and the backward "
+                        "GEMM behind the sampler (2)")
     p.add_argument("--sampler-cus", type=int, default=0,
                    help="CUs reserved for the pipelined sampler stream (0: no partition)")
     p.add_argument("--no-pad-features", action="store_true",
@@ -355,6 +358,7 @@ def main():
                                             0 if args.no_priority else 1),
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
+                          sampler_gate=args.sampler_gate,
                           pad_features=not args.no_pad_features, cache_rate=args.cache_rate,
                           deterministic_backward=not args.atomic_backward,
                           gat=args.model == "gat", gemm=args.gemm, pair_table=args.pair_table, pd_cache=args.pd_cache,

@@ -37,7 +37,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
                seed=2000, hip_gemm=True, pipeline=True, transform_first=-1,
                early_aggregate=True, sampler_priority=1, fuse_activation=True,
-               fuse_loss=True, sampler_cus=0, pad_features=True, cache_rate=-1.0,
+               fuse_loss=True, sampler_cus=0, sampler_gate=0, pad_features=True, cache_rate=-1.0,
                up_degree=False, gat=False, pd_cache=False, pd_rate=0.2, pd_super_batch=4,
                gemm="split3", overlap_allreduce=-1, pair_table=3, sample_gpu=False):
     E = ext()
@@ -67,6 +67,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
     c.fuse_activation = bool(fuse_activation)
     c.fuse_loss = bool(fuse_loss)
     c.sampler_cus = int(sampler_cus)
+    c.sampler_gate = int(sampler_gate)
     c.pad_features = bool(pad_features)
     c.cache_rate = float(cache_rate)
     c.up_degree = bool(up_degree)

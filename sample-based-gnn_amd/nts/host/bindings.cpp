@@ -192,6 +192,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("sampler_priority", &GCNConfig::sampler_priority)
       .def_readwrite("fuse_loss", &GCNConfig::fuse_loss)
       .def_readwrite("sampler_cus", &GCNConfig::sampler_cus)
+      .def_readwrite("sampler_gate", &GCNConfig::sampler_gate)
       .def_readwrite("pad_features", &GCNConfig::pad_features)
       .def_readwrite("cache_rate", &GCNConfig::cache_rate)
       .def_readwrite("up_degree", &GCNConfig::up_degree)

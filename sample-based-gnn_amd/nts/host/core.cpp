@@ -769,6 +769,8 @@ struct HipLinearActFn : public torch::autograd::Function<HipLinearActFn> {
 // backward: dH = A^T (dX1 ⊙ [X1 > 0] / (1-p)) over the CSR, dW = X[source]^T dH.
 // Recorded as one NN op whose input is the feature table (the bottom graph
 // op has no backward, core/ntsContext.hpp:443-444).
+std::function<void()> g_after_fwd_gemm, g_before_bwd_gemm;  // set_bottom_gemm_hooks
+
 struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
   static NtsVar forward(AutogradContext* ctx, NtsVar table, NtsVar W, int64_t sg_ptr,
                         int64_t cs_ptr, double p, int64_t seed, int64_t offset, int64_t prof_ptr,
@@ -806,6 +808,7 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                                         Wc.data_ptr<float>(), (uint64_t)N, hp, (uint64_t)N),
                 "nts_hip_gemm_gather_f32");
     if (prof) prof->end(KernelProfiler::GATHER_GEMM, st, 2.0 * (double)s * F * N);
+    if (g_after_fwd_gemm) g_after_fwd_gemm();
     NtsVar X1 = torch::empty({v, N}, f32_opts(dev));
     if (prof) prof->begin(KernelProfiler::BOTTOM_AGG, st);
     hip_check(nts_hip_spmm_csc_fwd_act(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
@@ -895,6 +898,7 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                   4.0 * N * v + 8.0 * sg->e_size + 4.0 * (s + 1) + 4.0 * N * s);
     }
     NtsVar dW = torch::empty({F, N}, W.options());
+    if (g_before_bwd_gemm) g_before_bwd_gemm();
     if (prof) prof->begin(KernelProfiler::GATHER_GEMM_TN, st);
     if (pairs_q && colmax.defined())
       hip_check(nts_hip_gemm_h2p_tn_gather_cm(cs->ctx(), (int)F, (int)N, (int)s,
@@ -1035,6 +1039,12 @@ struct HipActFn : public torch::autograd::Function<HipActFn> {
 
 NtsVar hip_relu_dropout(const NtsVar& x, double p, uint64_t seed, uint64_t offset, NtsStream* cs) {
   return HipActFn::apply(x, p, (int64_t)seed, (int64_t)offset, reinterpret_cast<int64_t>(cs));
+}
+
+void set_bottom_gemm_hooks(std::function<void()> after_fwd_gemm,
+                           std::function<void()> before_bwd_gemm) {
+  g_after_fwd_gemm = std::move(after_fwd_gemm);
+  g_before_bwd_gemm = std::move(before_bwd_gemm);
 }
 
 NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,

@@ -571,19 +571,36 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
       reuse_slot_ = slot;
     } else if (ss) {
       next_slot_ = (slot + 1) % nslots_;
-      if (!pass_done_ && sampler->sample_not_finished()) {
-        issue(next_slot_, *ss);  // prefetch the next batch behind this one
-        prefetched_ = next_slot_;
-      } else if (!pass_done_) {
-        // last batch of the pass: sample the first batch of the next pass now
-        // (same seeds, same stream position as after restart()), so the
-        // pipeline does not drain at every pass boundary
-        sampler->restart();
-        issue(next_slot_, *ss);
-        carry_ = next_slot_;
-        pass_done_ = true;
+      if (cfg.sampler_gate > 0 && tf_) {
+        // issued from the bottom layer's forward GEMM hook (below), behind it
+        deferred_issue_ = [this] { prefetch_next(); };
+      } else {
+        prefetch_next();
       }
     }
+  }
+  if (deferred_issue_) {
+    if (!gate_ev_)
+      TORCH_CHECK(hipEventCreateWithFlags(&gate_ev_, hipEventDisableTiming) == hipSuccess,
+                  "hipEventCreate");
+    set_bottom_gemm_hooks(
+        [this] {
+          if (!deferred_issue_) return;
+          TORCH_CHECK(hipEventRecord(gate_ev_, (hipStream_t)cs->stream()) == hipSuccess &&
+                          hipStreamWaitEvent((hipStream_t)ss->stream(), gate_ev_, 0) == hipSuccess,
+                      "hipEventRecord/hipStreamWaitEvent");
+          auto f = std::move(deferred_issue_);
+          deferred_issue_ = nullptr;
+          f();
+        },
+        cfg.sampler_gate >= 2
+            ? std::function<void()>([this] {
+                if (gated_slot_ >= 0)
+                  TORCH_CHECK(hipStreamWaitEvent((hipStream_t)cs->stream(), ready_[gated_slot_], 0) ==
+                                  hipSuccess,
+                              "hipStreamWaitEvent");
+              })
+            : std::function<void()>());
   }
   fresh_pass_ = false;
   last_sg = sg;
@@ -618,6 +635,13 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
     ctx.self_backward(false);
   }
   pd_active_ = false;
+  if (deferred_issue_) {  // (the hook did not run: issue behind the step's kernels so far)
+    auto f = std::move(deferred_issue_);
+    deferred_issue_ = nullptr;
+    f();
+  }
+  set_bottom_gemm_hooks(nullptr, nullptr);
+  gated_slot_ = -1;
   Update();
   for (auto* p : P) p->zero_grad();
   TORCH_CHECK(hipEventRecord(sg->consumed, (hipStream_t)cs->stream()) == hipSuccess,
@@ -629,6 +653,24 @@ float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   for (int l = 0; l < sg->layers; ++l) batch_edges += sg->sampled_sgs[l]->e_size;
   ++batches;
   return 0.f;  // the loss stays on the device (no per-step host sync)
+}
+
+// the pipelined sampler's next batch (issued behind the batch being trained)
+void GCN_SAMPLE_ALLGPU_impl::prefetch_next() {
+  if (!pass_done_ && sampler->sample_not_finished()) {
+    issue(next_slot_, *ss);  // prefetch the next batch behind this one
+    prefetched_ = next_slot_;
+    gated_slot_ = next_slot_;
+  } else if (!pass_done_) {
+    // last batch of the pass: sample the first batch of the next pass now
+    // (same seeds, same stream position as after restart()), so the
+    // pipeline does not drain at every pass boundary
+    sampler->restart();
+    issue(next_slot_, *ss);
+    carry_ = next_slot_;
+    gated_slot_ = next_slot_;
+    pass_done_ = true;
+  }
 }
 
 void GCN_SAMPLE_ALLGPU_impl::restart() {

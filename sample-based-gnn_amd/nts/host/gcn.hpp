@@ -32,6 +32,11 @@ struct GCNConfig {
   // after the training stream's)
   int sampler_priority = 1;
   int sampler_cus = 0;
+  // pipelined sampler, transform-first bottom layer: 0 = the next batch's
+  // sampling is issued ahead of the training step; 1 = behind the forward
+  // gather GEMM (it starts once that GEMM ends); 2 = also the backward gather
+  // GEMM waits for it (neither GEMM shares CUs with the sampler)
+  int sampler_gate = 0;
   bool pad_features = true;           // copy wide feature tables to a 128-byte row pitch
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   // bottom layer order: 1 = transform first, A (X W) (rows narrowed before the
@@ -212,6 +217,12 @@ class GCN_SAMPLE_ALLGPU_impl {
   int carry_ = -1;
   bool pass_done_ = false;
   bool fresh_pass_ = true;
+  // cfg.sampler_gate: the next batch's issue, deferred to the bottom layer's
+  // forward GEMM hook, and the event it waits on
+  std::function<void()> deferred_issue_;
+  hipEvent_t gate_ev_ = nullptr;
+  int gated_slot_ = -1;
+  void prefetch_next();
 };
 
 }  // namespace nts

@@ -446,6 +446,11 @@ struct PairTable {
   bool tn = true;
   NtsVar Q;   // int16 [V, 2 Kp] planar form (defined: the weight gradient on k_h2_tn3)
 };
+// Stream-phase hooks of the transform-first bottom layer (the driver's
+// sampler gating, GCNConfig::sampler_gate): called on the host right after
+// the forward gather GEMM is enqueued, and right before the backward one.
+void set_bottom_gemm_hooks(std::function<void()> after_fwd_gemm,
+                           std::function<void()> before_bwd_gemm);
 NtsVar hip_bottom_transform(const NtsVar& table, const NtsVar& W, sampCSC* sg, double p,
                             uint64_t seed, uint64_t offset, NtsStream* cs, KernelProfiler* prof,
                             float* h_out = nullptr, const PairTable* pairs = nullptr);
