@@ -358,6 +358,27 @@ def test_pipeline_carries_batches_across_passes(E, graph):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize("gate", [1, 2])
+def test_sampler_gate_trains_identically(E, graph, gate):
+    """--sampler-gate only moves where the next batch's sampling is issued
+    (behind the transform-first bottom forward GEMM; with 2 the backward GEMM
+    also waits for it): weights bit-identical to the ungated pipeline across
+    pass boundaries."""
+    a, *_ = _driver(E, graph, 602, 7, [602, 32, 7], [10, 5], 300, drop=0.5, pipeline=True,
+                    transform_first=1, sampler_gate=gate)
+    b, *_ = _driver(E, graph, 602, 7, [602, 32, 7], [10, 5], 300, drop=0.5, pipeline=True,
+                    transform_first=1)
+    for d in (a, b):
+        d.run_epoch()
+        for _ in range(3):
+            if not d.sample_not_finished():
+                d.restart()
+            d.train_batch()
+        d.synchronize()
+    for x, y in zip(a.weights(), b.weights()):
+        assert torch.equal(x, y)
+
+
 def _gat_layer_ref(X, W, att, ly):
     """GAT_SAMPLE_ALL_GPU layer (toolkits/GAT_SAMPLE_ALL_GPU.hpp:322-388), fp64,
     materialised messages, on an oracle-sampled merged layer."""
