@@ -928,21 +928,25 @@ __device__ __forceinline__ uint32_t regs_consume(const uint32_t (&cur)[NW], uint
   return used;
 }
 
-// regs_consume on an LDS window of words already applied: u[t] = the
-// accepted position (0xFFFFFFFF: rejected) and dd[t] = the distance back to
-// the previous word of the union with the same position (0: none within NW).
-// Word t of a window starting at u is new iff accepted and that previous word
-// lies before the window (dd == 0 or dd > t) — no pairwise compares per lane.
+// regs_consume on words already applied (the accepted position, or
+// 0xFFFFFFFF for a rejected word) in an LDS window: word t at u[t].  (Each
+// union word's distance back to its previous equal, computed once per wave
+// and read by the lanes instead of their pairwise compares, measured slower:
+// 6.0 vs 2.3 ms for the C2 bottom layer's tables — a chain of LDS reads per
+// word.)
 template <int NW>
-__device__ __forceinline__ uint32_t window_consume(const uint32_t* u, const uint8_t* dd,
-                                                   uint32_t n) {
+__device__ __forceinline__ uint32_t window_consume(const uint32_t* u, uint32_t n) {
+  constexpr uint32_t kRej = 0xFFFFFFFFu;
+  uint32_t val[NW];
   uint32_t cnt = 0, used = 0;
 #pragma unroll
   for (int t = 0; t < NW; ++t) {
     if ((uint32_t)t >= n && __ballot(used == 0) == 0) break;
-    const uint32_t d = dd[t];
-    const bool fresh = u[t] != 0xFFFFFFFFu && (d == 0 || d > (uint32_t)t);
-    cnt += fresh ? 1u : 0u;
+    val[t] = u[t];
+    bool dup = val[t] == kRej;
+#pragma unroll
+    for (int b = 0; b < t; ++b) dup |= val[b] == val[t];
+    cnt += dup ? 0u : 1u;
     used = (used == 0 && cnt == n) ? (uint32_t)t + 1u : used;
   }
   return used;
@@ -1008,7 +1012,6 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   __shared__ uint32_t lst[NMAX * 256];
   __shared__ float red[2][4];
   __shared__ uint32_t uu[4][2][192];  // per wave: the union windows of two dsts
-  __shared__ uint8_t ud[4][2][192];   // ... and each word's distance to its previous equal
   const int t = threadIdx.x;
   const uint32_t k = blockIdx.y, v = sizes[0];
   const uint32_t i0 = k * kMtChunk;
@@ -1071,26 +1074,10 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
     for (int q = 0; q < kU / kWave; ++q) rw[q] = W[P + ln + kWave * q];
   };
   auto store_union = [&](int buf, const uint4& f) {
-    uint32_t mv[kU / kWave];
 #pragma unroll
     for (int q = 0; q < kU / kWave; ++q) {
       uint32_t x;
-      mv[q] = mt_apply(rw[q], f.z, f.w, lemire, x) ? x : 0xFFFFFFFFu;
-      uu[wvi][buf][ln + kWave * q] = mv[q];
-    }
-    __builtin_amdgcn_wave_barrier();  // (one wave: its LDS writes land before its reads)
-    // the distance back to the previous word with the same position (within
-    // NW - 1 words: no window reaches further back)
-#pragma unroll
-    for (int q = 0; q < kU / kWave; ++q) {
-      const int jj = ln + kWave * q;
-      uint32_t d = 0;
-      if (mv[q] != 0xFFFFFFFFu) {
-#pragma unroll
-        for (int b = 1; b < NW; ++b)
-          if (d == 0 && jj - b >= 0 && uu[wvi][buf][jj - b] == mv[q]) d = (uint32_t)b;
-      }
-      ud[wvi][buf][jj] = (uint8_t)d;
+      uu[wvi][buf][ln + kWave * q] = mt_apply(rw[q], f.z, f.w, lemire, x) ? x : 0xFFFFFFFFu;
     }
   };
   const uint32_t cnt = i1 - i0;
@@ -1113,7 +1100,7 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
     if (jn < cnt) load_union(P0n);
     uint32_t used;
     if (wmax(p) + NW - P0 <= (uint32_t)kU) {  // (p >= P0: Deltas only grow)
-      used = window_consume<NW>(&uu[wvi][buf][p - P0], &ud[wvi][buf][p - P0], f.y);
+      used = window_consume<NW>(&uu[wvi][buf][p - P0], f.y);
     } else {
       uint32_t cur[NW];
 #pragma unroll
