@@ -17,3 +17,7 @@ print("gate", sys.argv[2], round(d["ms_per_step"], 4), "ms/step; alone", round(a
 PY
   done
 done
+timeout -k 10 400 python -u -m pytest tests/test_hip_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -k "mt19937 or fanout_above" > $O/mt_tests.log 2>&1 || { echo "mt tests failed"; tail -30 $O/mt_tests.log; exit 1; }
+tail -1 $O/mt_tests.log
+timeout -k 10 300 python -u bench.py --rng mt --steps 20 --warmup 3 $B --no-interference-probe > $O/mt.json 2> $O/mt.err || { echo "mt failed"; tail -5 $O/mt.err; exit 1; }
+python3 -c "import json; d=json.loads(open('$O/mt.json').read().strip().splitlines()[-1]); print('MT', round(d['ms_per_step'],3), 'ms/step', '%.3g' % d['value'])"
