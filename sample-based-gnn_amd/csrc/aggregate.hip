@@ -983,6 +983,12 @@ static int gather_u_env() {
   }();
   return u;
 }
+// rows in flight for the post-mask CSR gather (the hop above a transform-first
+// bottom layer: ~2 edges per row at C2); 0: gather_u's (compile-time A/B)
+#ifndef NTS_AGG_PM_U
+#define NTS_AGG_PM_U 0
+#endif
+constexpr int kAggPmU = NTS_AGG_PM_U;
 constexpr int gather_u(int floats_per_lane) {
   return floats_per_lane <= 4 ? 8 : floats_per_lane <= 12 ? 5 : 4;
 }
@@ -998,7 +1004,7 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
 // widest (register budget); NTS_GATHER_U=4 forces 4 for the mid-width rows
 #define NTS_G(LPD, NCH)                                                                     \
   do {                                                                                      \
-    constexpr int u = gather_u(VEC * NCH);                                                  \
+    constexpr int u = (MODE == kAggPostMask && kAggPmU > 0) ? kAggPmU : gather_u(VEC * NCH); \
     if (u == 5 && gather_u_env() == 4)                                                      \
       hipLaunchKernelGGL((k_spmm_gather<VEC, LPD, NCH, MAP, 4, TIER, MODE, COOP>), dim3(grid), \
                          dim3(kAggThreads), 0, st, off, idx, w, n_dev, n_cap, x, ldx, map, \
