@@ -6,10 +6,15 @@ TAG=${1:-chk}
 K=${2:-}
 O=gpurun_out/$TAG
 mkdir -p $O
+# heartbeat under gpurun_out/ (some full-size tests run minutes without
+# printing; each test still has its own --timeout)
+( while true; do date +%T >> $O/heartbeat.txt; sleep 50; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 if [ -n "$K" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$K" > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
 else
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=12 > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread --durations=12 > $O/tests.log 2>&1 || { echo "tests failed"; tail -30 $O/tests.log; exit 1; }
 fi
 grep -E "passed|failed|s call" $O/tests.log | head -16
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
