@@ -163,12 +163,36 @@ uint32_t scan_next_epoch(nts_hip_ctx* ctx);
 int mt_ring_reset(nts_hip_ctx* ctx);
 void mt_ring_free(nts_hip_ctx* ctx);
 
+// The tile a look-back workgroup works on: its ticket in dispatch order, not
+// blockIdx.x.  Workgroups are not placed in index order across the XCDs, so
+// once a grid exceeds what is resident at once (about 2K workgroups) a tile
+// could wait on a lower-indexed one that never gets a slot: the frontier
+// compaction of a 111 M-vertex graph (27 K tiles) hung that way.  With tickets
+// every lower tile already runs.  The workgroup that draws the last ticket
+// resets the counter (no other draw is left in the launch) for the stream's
+// next one.  Every thread of the workgroup calls it.
+__device__ __forceinline__ uint32_t lb_ticket(uint32_t* ctr, uint32_t nblk) {
+  __shared__ uint32_t s_tile;
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == nblk - 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
+  __syncthreads();
+  return s_tile;
+}
+// the ticket counter: the last word of the zeroed state array (past every
+// tile's word)
+inline uint32_t* scan_ticket(nts_hip_ctx* ctx) {
+  return reinterpret_cast<uint32_t*>(ctx->scan_state + ctx->scan_state_elems - 1);
+}
+
 // Decoupled look-back (one wave, every lane calls): tile `tile` publishes its
 // aggregate, sums its predecessors' states (RELAXED agent-scope atomics: each
 // 64-bit word {epoch:30 | kind:2 | value:32} carries its own value) up to the
 // first inclusive one, publishes its inclusive prefix and returns the
-// exclusive one.  Tiles only wait on lower-numbered tiles, which the
-// dispatcher places first, so the chain completes.
+// exclusive one.  Tiles only wait on lower tiles, which already run when
+// tiles are tickets (lb_ticket), so the chain completes.
 __device__ __forceinline__ uint64_t lb_word(uint32_t epoch, uint64_t kind, uint32_t v) {
   return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | (kind << 32) | v;
 }

@@ -46,7 +46,7 @@ int ensure_scratch(nts_hip_ctx* ctx, size_t bytes) {
 
 // Tile states of the single-pass scan: zeroed once (epoch 0 is never issued).
 int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems) {
-  if (elems <= ctx->scan_state_elems) return NTS_OK;
+  if (elems < ctx->scan_state_elems) return NTS_OK;  // the last word: the ticket counter
   NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (ctx->scan_state) NTS_HIP_TRY(hipFree(ctx->scan_state));
   ctx->scan_state = nullptr;

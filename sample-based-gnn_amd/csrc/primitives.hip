@@ -249,21 +249,23 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
                                                         uint32_t* __restrict__ out,
                                                         const uint32_t* n_dev, uint64_t n_cap,
                                                         uint64_t* __restrict__ state,
-                                                        uint32_t epoch, CountArgs ca) {
+                                                        uint32_t epoch, uint32_t* ticket,
+                                                        CountArgs ca) {
   __shared__ uint32_t tile[kScanTile + kScanTile / 16];
   __shared__ uint32_t wsum[kScanThreads / kWave];
   __shared__ uint32_t s_prefix;
+  const uint32_t ti = lb_ticket(ticket, gridDim.x);
   const int t = threadIdx.x, lane = t & 63;
   uint64_t n;
   uint32_t v_req = 0;
   if (COUNT) {
     v_req = *ca.v_in;
     n = min(v_req, ca.v_cap);
-    if (blockIdx.x == 0 && t == 0) ca.sizes[0] = (uint32_t)n;
+    if (ti == 0 && t == 0) ca.sizes[0] = (uint32_t)n;
   } else {
     n = n_dev ? (uint64_t)*n_dev : n_cap;
   }
-  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  const uint64_t base = (uint64_t)ti * kScanTile;
   if (base > n) return;  // every tile up to the one holding out[n] runs the chain
   if constexpr (COUNT) {
     uint32_t x[kScanItems];
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   const uint32_t ex = block_excl_scan(s, wsum, &agg);
   // publish, look back (wave 0, lanes over 64 predecessors at a time)
   if (t < kWave) {
-    if (blockIdx.x == 0) {
+    if (ti == 0) {
       if (t == 0) {
         __hip_atomic_store(state, tile_word(epoch, kTileIncl, agg), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
@@ -298,10 +300,10 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
       }
     } else {
       if (t == 0)
-        __hip_atomic_store(state + blockIdx.x, tile_word(epoch, kTileAgg, agg), __ATOMIC_RELAXED,
+        __hip_atomic_store(state + ti, tile_word(epoch, kTileAgg, agg), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       uint32_t prefix = 0;
-      int64_t top = (int64_t)blockIdx.x - 1;  // highest tile not yet folded in
+      int64_t top = (int64_t)ti - 1;  // highest tile not yet folded in
       for (;;) {
         const int64_t p = top - lane;
         uint64_t w = 0;
@@ -325,7 +327,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
         top -= kWave;
       }
       if (t == 0) {
-        __hip_atomic_store(state + blockIdx.x, tile_word(epoch, kTileIncl, prefix + agg),
+        __hip_atomic_store(state + ti, tile_word(epoch, kTileIncl, prefix + agg),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_prefix = prefix;
       }
@@ -375,7 +377,7 @@ int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const u
   const uint64_t nb = n_cap / kScanTile + 1;
   NTS_RET(ensure_scan_state(ctx, scan1_state_elems(n_cap)));
   hipLaunchKernelGGL(k_scan1<false>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, in, out,
-                     n_dev, n_cap, ctx->scan_state, next_epoch(ctx), CountArgs{});
+                     n_dev, n_cap, ctx->scan_state, next_epoch(ctx), scan_ticket(ctx), CountArgs{});
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }
@@ -453,7 +455,7 @@ int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t 
   const uint64_t nb = (uint64_t)ca.v_cap / kScanTile + 1;
   NTS_RET(ensure_scan_state(ctx, scan1_state_elems(ca.v_cap)));
   hipLaunchKernelGGL(k_scan1<true>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, nullptr,
-                     co, nullptr, (uint64_t)ca.v_cap, ctx->scan_state, next_epoch(ctx), ca);
+                     co, nullptr, (uint64_t)ca.v_cap, ctx->scan_state, next_epoch(ctx), scan_ticket(ctx), ca);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }

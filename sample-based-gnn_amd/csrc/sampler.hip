@@ -1275,8 +1275,9 @@ __global__ __launch_bounds__(kMarkThreads) void k_mark_count(const uint8_t* __re
 __global__ __launch_bounds__(kMarkThreads) void k_mark_fused(
     uint8_t* __restrict__ marks, uint32_t nblk, uint64_t n_vertices, uint32_t s_cap,
     uint32_t* __restrict__ source, uint32_t* __restrict__ src_index, uint32_t* sizes,
-    uint64_t* __restrict__ state, uint32_t epoch) {
-  const uint64_t tid = (uint64_t)blockIdx.x * kMarkThreads + threadIdx.x;
+    uint64_t* __restrict__ state, uint32_t epoch, uint32_t* ticket) {
+  const uint32_t tile = lb_ticket(ticket, nblk);
+  const uint64_t tid = (uint64_t)tile * kMarkThreads + threadIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __shared__ uint32_t ws[kMarkThreads / kWave];
   __shared__ uint32_t s_prefix;
@@ -1297,12 +1298,12 @@ __global__ __launch_bounds__(kMarkThreads) void k_mark_fused(
     agg += ws[i];
   }
   if (w == 0) {
-    const uint32_t pre = lookback_exclusive(state, blockIdx.x, epoch, agg);
+    const uint32_t pre = lookback_exclusive(state, tile, epoch, agg);
     if (lane == 0) s_prefix = pre;
   }
   __syncthreads();
   uint32_t pos = s_prefix + off + inc - c;
-  if (blockIdx.x == nblk - 1 && threadIdx.x == 0) {
+  if (tile == nblk - 1 && threadIdx.x == 0) {
     const uint32_t total = s_prefix + agg;
     sizes[2] = min(total, s_cap);
     if (total > s_cap) atomicOr(&sizes[3], 2u);
@@ -1869,7 +1870,7 @@ frontier:
     NTS_RET(ensure_scan_state(ctx, scan1_state_elems((uint64_t)nblk_marks * 4096)));
     hipLaunchKernelGGL(k_mark_fused, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
                        nblk_marks, V, o->s_cap, o->source, ctx->src_index, o->sizes,
-                       ctx->scan_state, scan_next_epoch(ctx));
+                       ctx->scan_state, scan_next_epoch(ctx), scan_ticket(ctx));
     NTS_LAUNCH_CHECK();
   } else {
     hipLaunchKernelGGL(k_mark_count, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
