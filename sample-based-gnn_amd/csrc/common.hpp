@@ -17,6 +17,10 @@ namespace nts_hip {
 
 // ---- error plumbing (thread-local message, status codes) -----------------
 void set_error(const char* fmt, ...);
+// NTS_LAUNCH_TRACE=1 (debugging a hang): every launch check prints its site,
+// waits for the device and prints it again
+bool launch_trace();
+void launch_trace_sync(const char* file, int line);
 
 #define NTS_HIP_TRY(expr)                                                        \
   do {                                                                           \
@@ -44,6 +48,7 @@ void set_error(const char* fmt, ...);
                            hipGetErrorString(_e));                               \
       return NTS_ERR_HIP;                                                        \
     }                                                                            \
+    if (::nts_hip::launch_trace()) ::nts_hip::launch_trace_sync(__FILE__, __LINE__); \
   } while (0)
 
 #define NTS_RET(expr)                                                            \

@@ -19,6 +19,7 @@ void set_error(const char* fmt, ...) {
 
 int ensure_vertices(nts_hip_ctx* ctx, uint64_t n_vertices) {
   if (n_vertices <= ctx->v_cap) return NTS_OK;
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (ctx->marks) NTS_HIP_TRY(hipFree(ctx->marks));
   if (ctx->src_index) NTS_HIP_TRY(hipFree(ctx->src_index));
   ctx->marks = nullptr;
@@ -26,7 +27,10 @@ int ensure_vertices(nts_hip_ctx* ctx, uint64_t n_vertices) {
   // marks are scanned 16 bytes per lane: pad to a multiple of 4096.
   uint64_t padded = (n_vertices + 4095) / 4096 * 4096;
   NTS_HIP_TRY(hipMalloc(&ctx->marks, padded));
-  NTS_HIP_TRY(hipMemset(ctx->marks, 0, padded));
+  // zeroed on the context's stream (a plain hipMemset goes to the NULL
+  // stream, which a non-blocking stream does not wait for) and waited for
+  NTS_HIP_TRY(hipMemsetAsync(ctx->marks, 0, padded, ctx->stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
   NTS_HIP_TRY(hipMalloc(&ctx->src_index, n_vertices * sizeof(uint32_t)));
   ctx->v_cap = n_vertices;
   return NTS_OK;
@@ -44,6 +48,21 @@ int ensure_scratch(nts_hip_ctx* ctx, size_t bytes) {
   return NTS_OK;
 }
 
+bool launch_trace() {
+  static const bool on = [] {
+    const char* e = getenv("NTS_LAUNCH_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+void launch_trace_sync(const char* file, int line) {
+  fprintf(stderr, "[launch] %s:%d\n", file, line);
+  fflush(stderr);
+  (void)hipDeviceSynchronize();
+  fprintf(stderr, "[done] %s:%d\n", file, line);
+  fflush(stderr);
+}
+
 // Tile states of the single-pass scan: zeroed once (epoch 0 is never issued).
 int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems) {
   if (elems < ctx->scan_state_elems) return NTS_OK;  // the last word: the ticket counter
@@ -52,7 +71,13 @@ int ensure_scan_state(nts_hip_ctx* ctx, uint64_t elems) {
   ctx->scan_state = nullptr;
   const uint64_t n = elems + elems / 4 + 64;
   NTS_HIP_TRY(hipMalloc(&ctx->scan_state, n * sizeof(uint64_t)));
-  NTS_HIP_TRY(hipMemset(ctx->scan_state, 0, n * sizeof(uint64_t)));
+  // zeroed on the context's stream and waited for: the NULL stream's
+  // hipMemset is not ordered before the next kernel on a non-blocking stream,
+  // and a tile word or the ticket counter still holding the old allocation's
+  // bytes when the first look-back kernel runs hangs it (a stale ticket count
+  // sends tiles past the grid)
+  NTS_HIP_TRY(hipMemsetAsync(ctx->scan_state, 0, n * sizeof(uint64_t), ctx->stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->scan_state_elems = n;
   return NTS_OK;
 }

@@ -1547,9 +1547,10 @@ int mt_ring_reset(nts_hip_ctx* ctx) {
   if (!ctx->mt_ring) return NTS_OK;
   NTS_HIP_TRY(hipStreamSynchronize(ctx->mt_gen_stream));
   NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
-  NTS_HIP_TRY(hipMemcpy(ctx->mt_gen_raw, ctx->mt_state, 624 * sizeof(uint32_t),
-                        hipMemcpyDeviceToDevice));
-  NTS_HIP_TRY(hipMemset(ctx->mt_done, 0, sizeof(uint64_t)));
+  NTS_HIP_TRY(hipMemcpyAsync(ctx->mt_gen_raw, ctx->mt_state, 624 * sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, ctx->stream));
+  NTS_HIP_TRY(hipMemsetAsync(ctx->mt_done, 0, sizeof(uint64_t), ctx->stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
   *ctx->mt_done_host = 0;
   ctx->mt_gen_blocks = 0;
   ctx->mt_seq = 0;
