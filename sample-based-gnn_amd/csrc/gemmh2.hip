@@ -1962,14 +1962,7 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
   // blocks, each with fewer tiles (large bottom frontiers, e.g. C5)
   const int tile_cap = (160 * 1024 - 3 * 16 * pitch) / (2 * 4 * 16);
   NTS_CHECK_ARG(tile_cap >= 1, "row pitch too large for the NN stage");
-  // NTS_NN3_WAVES=k (A/B): k rounds of blocks over the CUs, so a CU that a
-  // pipelined sampler block holds delays a k-times smaller share of the rows
-  static const int rounds = [] {
-    const char* e = getenv("NTS_NN3_WAVES");
-    const int v = e ? atoi(e) : 1;
-    return v >= 1 && v <= 8 ? v : 1;
-  }();
-  int gx = std::max({1, std::min(rounds * gemm_cus() / ncb, T), (T + tile_cap - 1) / tile_cap});
+  int gx = std::max({1, std::min(gemm_cus() / ncb, T), (T + tile_cap - 1) / tile_cap});
   const int max_tiles = (T + gx - 1) / gx;
   const int lds = 3 * 16 * pitch + 2 * 4 * 16 * max_tiles;
   NTS_CHECK_ARG(lds <= 160 * 1024, "row-id stage");
