@@ -875,7 +875,13 @@ constexpr int kH2Tn3Threads = 512;
 constexpr int kH2Tn3BRaw = 16 * 512;  // one step of fp32 dH rows (N = 128)
 constexpr int kH2Tn3BPl = 16 * 256;   // one plane of the split step
 
-__device__ __forceinline__ uint32_t h2_swz(int row) { return (uint32_t)(2 * (row & 7)); }
+// The X stage's 16-byte chunk swizzle.  Rows sit 2,560 B apart (0 mod the 64
+// banks), and a 32-lane group of the A^T reads (ds_read_b64_tr_b16) takes
+// four rows (8h + tq, tq < 4) x four consecutive chunks from a 4-aligned
+// chunk c: XOR by 4 (row & 3) puts the four rows on disjoint 4-chunk groups,
+// 64 distinct banks.  (2 (row & 7), the earlier form, left rows tq = 0, 1
+// and tq = 2, 3 on the same four chunks: every A^T read 2-way conflicted.)
+__device__ __forceinline__ uint32_t h2_swz(int row) { return (uint32_t)(4 * (row & 3)); }
 
 // TN v4: the structure above on v_mfma_f32_32x32x16_f16 (full-rate f16 MFMA
 // at K = 16; the 16x16x16 form issues at the 16x16x32 form's cycles for half
