@@ -221,7 +221,8 @@ def parse():
                    help="pipelined sampler behind the bottom forward GEMM (1), and the backward "
                         "GEMM behind the sampler (2)")
     p.add_argument("--sampler-cus", type=int, default=0,
-                   help="CUs reserved for the pipelined sampler stream (0: no partition)")
+                   help="CUs of the pipelined sampler stream: n > 0 reserved for it (training on the "
+                        "rest), n < 0 the sampler confined to |n| (training on all); 0: no masks")
     p.add_argument("--no-pad-features", action="store_true",
                    help="gather from the feature table as given (no 128-byte row pitch copy)")
     p.add_argument("--no-fuse-loss", action="store_true",

@@ -37,6 +37,8 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                 "GCN_SAMPLE_GPU samples with the reference's mt19937 stream (rng_mode MT19937)");
     cfg.deterministic_backward = true;  // the CSR exists for every graph-op backward
   }
+  // sampler_cus n > 0: the sampler's stream on n CUs, the training stream on
+  // the others; n < 0: the sampler on |n| CUs, the training stream on all
   if (cfg.pipeline && cfg.sampler_cus > 0)
     cs = std::make_unique<NtsStream>(graph->device,
                                      cu_mask_spread(graph->device, cfg.sampler_cus, true),
@@ -133,9 +135,9 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                           cfg.gat);
   sampler->rng_mode = cfg.rng_mode;
   sampler->up_degree = cfg.up_degree;
-  if (cfg.pipeline && cfg.sampler_cus > 0)
+  if (cfg.pipeline && cfg.sampler_cus != 0)
     ss = std::make_unique<NtsStream>(graph->device,
-                                     cu_mask_spread(graph->device, cfg.sampler_cus, false),
+                                     cu_mask_spread(graph->device, std::abs(cfg.sampler_cus), false),
                                      (uint64_t)cfg.seed);
   else if (cfg.pipeline)
     ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed,

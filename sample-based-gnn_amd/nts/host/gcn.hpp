@@ -31,6 +31,9 @@ struct GCNConfig {
   // normal, -1 = the training stream high (the sampler's blocks dispatched
   // after the training stream's)
   int sampler_priority = 1;
+  // CUs of the pipelined sampler's stream: n > 0 reserves n CUs for it (the
+  // training stream on the rest), n < 0 confines it to |n| CUs and leaves the
+  // training stream on all; 0: no CU masks
   int sampler_cus = 0;
   // pipelined sampler, transform-first bottom layer: 0 = the next batch's
   // sampling is issued ahead of the training step; 1 = behind the forward
