@@ -151,6 +151,36 @@ def test_c2_reddit_shaped_full_batch(E):
     _free()
 
 
+def test_fresh_context_frontier_past_resident_tiles(E):
+    """Regression for the C5 hang: a fresh sampler context whose
+    first layer grows the look-back tile states right before a frontier
+    compaction of more tiles than the chip holds at once (V = 24 M: 5,860
+    tiles of 4,096 vertices).  The states were zeroed on the NULL stream,
+    unordered with the sampler's stream.  Three batches, every array
+    bit-exact vs the oracle's PHILOX restatement of sample_fast
+    (core/ntsFastSampler.hpp:962-1140)."""
+    V, Ecount, B, fan = 24_000_000, 48_000_000, 4096, [10, 5]
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    src = torch.randint(0, V, (Ecount,), device=DEV, generator=gen, dtype=torch.int32)
+    dst = torch.randint(0, V, (Ecount,), device=DEV, generator=gen, dtype=torch.int32)
+    G = E.FullyRepGraph.from_edges(src, dst, V)
+    del src, dst
+    _free()
+    seeds = torch.from_numpy(np.random.default_rng(7).choice(V, 3 * B, replace=False).astype(np.int32))
+    fs = E.FastSampler(G, seeds, 2, B, fan)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    o = orc.Sampler(col, rows, _np(G.in_degree), _np(G.out_degree), fan, rng_mode=orc.RNG_PHILOX,
+                    order_mode=orc.ORDER_DRAW)
+    for b in range(3):
+        got = fs.sample_gpu_fast(B)
+        assert got[1]["src_size"] > 10_000  # random ids: the frontier spans the whole vertex range
+        ref = o.sample(seeds.numpy()[b * B:(b + 1) * B].astype(np.uint32), b)
+        _compare_oracle(got, ref)
+    del fs, got, G, o
+    _free()
+
+
 def _sets_equal(got_layer, ref_layer):
     """Per-dst neighbour multisets equal (the reference emits std::unordered_map
     order inside a dst, core/ntsFastSampler.hpp:1026-1038)."""
