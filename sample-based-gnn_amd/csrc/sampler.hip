@@ -446,15 +446,15 @@ struct MtInfo {
 };
 
 // nn / cstat (chunked resolver, may be null): the draws per dst, and per
-// chunk of kMtChunkP dsts the expected extra words (repeats) and their
+// chunk of csz dsts the expected extra words (repeats) and their
 // variance: drawing the k-th distinct of `deg` positions takes a geometric
 // number of words with success (deg - k) / deg — mean extra k / (deg - k),
 // variance k deg / (deg - k)^2 (rejections, p < deg / 2^32, neglected).
-constexpr uint32_t kMtChunkP = 256;
 __global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __restrict__ dst,
                           const uint32_t* __restrict__ co, uint32_t* sizes, uint32_t e_cap,
                           int lemire, uint4* __restrict__ info, uint32_t* __restrict__ nn,
-                          float2* __restrict__ cstat, const uint64_t* done, uint64_t* a0p) {
+                          float2* __restrict__ cstat, uint32_t csz, const uint64_t* done,
+                          uint64_t* a0p) {
   const uint32_t v = sizes[0];
   // the layer's first stream word, for the kernels after this one (the
   // resolver moves mt_done on)
@@ -478,8 +478,8 @@ __global__ void k_mt_prep(const uint64_t* __restrict__ goff, const uint32_t* __r
           m += (float)k / r;
           var += (float)k * fd / (r * r);
         }
-        atomicAdd(&cstat[i / kMtChunkP].x, m);
-        atomicAdd(&cstat[i / kMtChunkP].y, var);
+        atomicAdd(&cstat[i / csz].x, m);
+        atomicAdd(&cstat[i / csz].y, var);
       }
     }
   }
@@ -639,8 +639,13 @@ __device__ void mt_exact_hashed(MtStream& s, uint32_t* tab, uint32_t* out, uint3
 
 constexpr uint32_t kMtInfo = 2048;  // per-dst info staged in LDS
 constexpr uint32_t kMtPos = 8192;   // kept positions staged in LDS before the flush
-// chunked resolver (fanout <= 32): dsts per chunk, words staged per chunk
+// chunked resolver (fanout <= 32): dsts per chunk (at most; a layer of up to
+// kMtSmallV dsts is cut into kMtChunkSmall-dst chunks: its window tables'
+// lanes walk a quarter of the dsts each and four times as many chunks fill
+// the CUs), words staged per chunk
 constexpr uint32_t kMtChunk = 256;
+constexpr uint32_t kMtChunkSmall = 64;
+constexpr uint32_t kMtSmallV = 32768;
 constexpr uint32_t kMtStage = 12288;
 
 // The hot loop issues no vector-memory instruction: on gfx9 one vmcnt counter
@@ -661,6 +666,7 @@ struct MtChunked {
   uint64_t* done;           // !FLAT: mt_done (the layer starts at its position, ends there)
   uint32_t seq;             // !FLAT: the layer's sequence number
   uint32_t* ovf;            // !FLAT: sizes[3] (bit 2: the generated stream fell short)
+  uint32_t csz = kMtChunk;  // FLAT: dsts per chunk (<= kMtChunk)
 };
 
 template <int G, bool FLAT>
@@ -687,9 +693,9 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
   MtStream s{nullptr, 0u};
   uint64_t a0 = 0;
   if constexpr (FLAT) {
-    i0 = blockIdx.x * kMtChunk;
+    i0 = blockIdx.x * ch.csz;
     if (i0 >= vv) return;
-    vv = min(vv, i0 + kMtChunk);
+    vv = min(vv, i0 + ch.csz);
     a0 = *ch.a0p;
     const MtWords W{ch.ring, a0, (uint32_t)(ch.gen_hi - a0)};
     const uint32_t e0 = ch.base[i0] + ch.entries[blockIdx.x];
@@ -1005,7 +1011,8 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
                                                    const uint32_t* sizes, const float2* cstat,
                                                    const uint32_t* __restrict__ ring,
                                                    const uint64_t* a0p, uint64_t gen_hi,
-                                                   int lemire_i, uint2* __restrict__ win,
+                                                   int lemire_i, uint32_t csz,
+                                                   uint2* __restrict__ win,
                                                    uint32_t* __restrict__ tabs) {
   __shared__ uint4 inf[kMtChunk];
   __shared__ uint32_t bs[kMtChunk];
@@ -1014,9 +1021,9 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   __shared__ uint32_t uu[4][2][192];  // per wave: the union windows of two dsts
   const int t = threadIdx.x;
   const uint32_t k = blockIdx.y, v = sizes[0];
-  const uint32_t i0 = k * kMtChunk;
+  const uint32_t i0 = k * csz;
   if (i0 >= v) return;
-  const uint32_t i1 = min(v, i0 + kMtChunk);
+  const uint32_t i1 = min(v, i0 + csz);
   float m = 0.f, var = 0.f;
   for (uint32_t j = t; j < k; j += 256) {
     m += cstat[j].x;
@@ -1123,7 +1130,7 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
 // the hand-counted vmcnt below is exact).  A Delta outside its chunk's window
 // is walked out by lane 0.  Also leaves the generator state after the layer.
 constexpr int kRing = 5;
-constexpr uint32_t kMtMaxChunks = 4096;  // the host keeps v_cap <= kMtMaxChunks * kMtChunk
+constexpr uint32_t kMtMaxChunks = 4096;  // the host keeps v_cap <= kMtMaxChunks * csz
 constexpr int kRingOps = kMtWmax * 4 / (16 * kWave);  // LDS-DMA instructions per window
 
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
@@ -1142,7 +1149,7 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
                                                       const uint32_t* sizes,
                                                       const uint32_t* __restrict__ sring,
                                                       const uint64_t* a0p, uint64_t gen_hi,
-                                                      int lemire_i,
+                                                      int lemire_i, uint32_t csz,
                                                       const uint2* __restrict__ win,
                                                       const uint32_t* __restrict__ tabs,
                                                       uint32_t* __restrict__ entries,
@@ -1156,7 +1163,7 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
   __shared__ uint32_t lst[NMAX];
   const int lane = threadIdx.x;
   const uint32_t v = sizes[0];
-  const uint32_t nch = min((v + kMtChunk - 1) / kMtChunk, kMtMaxChunks);
+  const uint32_t nch = min((v + csz - 1) / csz, kMtMaxChunks);
   for (uint32_t k = lane; k < nch; k += kWave) wins[k] = win[k];  // before any LDS DMA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1184,7 +1191,7 @@ __global__ __launch_bounds__(kWave) void k_mtp_resolve(const uint4* __restrict__
       ++fallbacks;
       uint32_t d2 = dl;
       if (lane == 0) {
-        const uint32_t i0 = k * kMtChunk, i1 = min(v, i0 + kMtChunk);
+        const uint32_t i0 = k * csz, i1 = min(v, i0 + csz);
         for (uint32_t j = i0; j < i1; ++j) {
           const uint4 f = info[j];
           if (f.y == 0) continue;
@@ -1703,10 +1710,11 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   // C2 seed layer (10,000 dsts, fanout 25) is chunked: 8.9 vs 11.4 ms/step
   // with every layer chunked vs the walker for it, r04)
   const bool mt_chunked_env = getenv("NTS_MT_CHUNKED") != nullptr;
+  const uint32_t mt_csz = o->v_cap <= kMtSmallV ? kMtChunkSmall : kMtChunk;
   const bool mt_chunked = rng_mode != NTS_RNG_PHILOX && !mt_serial_env && fanout >= 1 &&
-                          fanout <= 32 && (uint64_t)o->v_cap <= (uint64_t)kMtMaxChunks * kMtChunk &&
+                          fanout <= 32 && (uint64_t)o->v_cap <= (uint64_t)kMtMaxChunks * mt_csz &&
                           (mt_chunked_env || o->v_cap >= kMtChunkedMinV);
-  const uint64_t nch_cap = (uint64_t)o->v_cap / kMtChunk + 1;
+  const uint64_t nch_cap = (uint64_t)o->v_cap / mt_csz + 1;
   const uint64_t w_cap = (uint64_t)o->e_cap + o->e_cap / 4 + 131072;
   const uint64_t mt_info_n = rng_mode != NTS_RNG_PHILOX ? al((uint64_t)o->v_cap * 4) : 0;
   const uint64_t mt_base_n = mt_chunked ? al((uint64_t)o->v_cap + 1) : 0;
@@ -1802,28 +1810,29 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
       uint64_t* a0p = reinterpret_cast<uint64_t*>(misc + 2);
       NTS_HIP_TRY(hipMemsetAsync(cstat, 0, mt_stat_n * sizeof(uint32_t), st));
       hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                         o->column_offset, o->sizes, o->e_cap, lem, info, base, cstat,
+                         o->column_offset, o->sizes, o->e_cap, lem, info, base, cstat, mt_csz,
                          (const uint64_t*)ctx->mt_done, a0p);
       NTS_LAUNCH_CHECK();
       NTS_RET(scan1_exclusive(ctx, base, base, o->sizes, o->v_cap, st));
       const dim3 tgrid(kMtWmax / 256, (uint32_t)nch_cap);
-      const MtChunked chunked{ctx->mt_ring, a0p, gen_hi, base, entries, nullptr, 0u, nullptr};
+      const MtChunked chunked{ctx->mt_ring, a0p, gen_hi, base, entries, nullptr, 0u, nullptr,
+                              mt_csz};
       if (fanout <= 16) {
         hipLaunchKernelGGL(k_mtp_tables<16>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
-                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs);
+                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs);
         NTS_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_mtp_resolve<16>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
-                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs, entries, ctx->mt_done, seq,
+                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs, entries, ctx->mt_done, seq,
                            ctx->mt_state, o->sizes + 3, misc + 1);
         NTS_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_mt_serial<16, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
                            info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
       } else {
         hipLaunchKernelGGL(k_mtp_tables<32>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
-                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs);
+                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs);
         NTS_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_mtp_resolve<32>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
-                           ctx->mt_ring, a0p, gen_hi, lem, win, tabs, entries, ctx->mt_done, seq,
+                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs, entries, ctx->mt_done, seq,
                            ctx->mt_state, o->sizes + 3, misc + 1);
         NTS_LAUNCH_CHECK();
         hipLaunchKernelGGL((k_mt_serial<32, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
@@ -1837,7 +1846,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
       goto frontier;
     }
     hipLaunchKernelGGL(k_mt_prep, dim3(gv), dim3(256), 0, st, g->column_offset, o->destination,
-                       o->column_offset, o->sizes, o->e_cap, lem, info, nullptr, nullptr,
+                       o->column_offset, o->sizes, o->e_cap, lem, info, nullptr, nullptr, 1u,
                        nullptr, nullptr);
     NTS_LAUNCH_CHECK();
     const MtChunked whole{ctx->mt_ring, nullptr, gen_hi, nullptr, nullptr, ctx->mt_done, seq,
