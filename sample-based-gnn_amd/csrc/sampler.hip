@@ -639,12 +639,16 @@ __device__ void mt_exact_hashed(MtStream& s, uint32_t* tab, uint32_t* out, uint3
 
 constexpr uint32_t kMtInfo = 2048;  // per-dst info staged in LDS
 constexpr uint32_t kMtPos = 8192;   // kept positions staged in LDS before the flush
-// chunked resolver (fanout <= 32): dsts per chunk (at most; a layer of up to
-// kMtSmallV dsts is cut into kMtChunkSmall-dst chunks: its window tables'
-// lanes walk a quarter of the dsts each and four times as many chunks fill
-// the CUs), words staged per chunk
+// chunked resolver (fanout <= 32): dsts per chunk, at most kMtChunk — a
+// layer of up to kMtSmallV dsts is cut into kMtChunkSmall-dst chunks, one of
+// up to kMtMaxChunks x kMtChunkMid into kMtChunkMid-dst chunks: a window
+// table's lanes walk fewer dsts each and more chunks fill the CUs (C2 with
+// --rng mt, scripts/r04_n.sh: 4.60 ms/step at 64 / 256, 4.50 at 32 / 128,
+// 4.80 at 64 / 64 — the resolver's chain over the chunks grows; 5.29 with
+// 256 everywhere); words staged per chunk
 constexpr uint32_t kMtChunk = 256;
-constexpr uint32_t kMtChunkSmall = 64;
+constexpr uint32_t kMtChunkMid = 128;
+constexpr uint32_t kMtChunkSmall = 32;
 constexpr uint32_t kMtSmallV = 32768;
 constexpr uint32_t kMtStage = 12288;
 
@@ -1710,7 +1714,9 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   // C2 seed layer (10,000 dsts, fanout 25) is chunked: 8.9 vs 11.4 ms/step
   // with every layer chunked vs the walker for it, r04)
   const bool mt_chunked_env = getenv("NTS_MT_CHUNKED") != nullptr;
-  const uint32_t mt_csz = o->v_cap <= kMtSmallV ? kMtChunkSmall : kMtChunk;
+  const uint32_t mt_csz = o->v_cap <= kMtSmallV                            ? kMtChunkSmall
+                          : o->v_cap <= (uint64_t)kMtMaxChunks * kMtChunkMid ? kMtChunkMid
+                                                                             : kMtChunk;
   const bool mt_chunked = rng_mode != NTS_RNG_PHILOX && !mt_serial_env && fanout >= 1 &&
                           fanout <= 32 && (uint64_t)o->v_cap <= (uint64_t)kMtMaxChunks * mt_csz &&
                           (mt_chunked_env || o->v_cap >= kMtChunkedMinV);
