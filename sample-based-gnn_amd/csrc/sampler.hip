@@ -23,6 +23,8 @@
 //     the reference's serial fill order (ascending dst), atomic-free.
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace nts_hip {
 
 constexpr int kSelThreads = 256;
@@ -1823,27 +1825,30 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
       const dim3 tgrid(kMtWmax / 256, (uint32_t)nch_cap);
       const MtChunked chunked{ctx->mt_ring, a0p, gen_hi, base, entries, nullptr, 0u, nullptr,
                               mt_csz};
-      if (fanout <= 16) {
-        hipLaunchKernelGGL(k_mtp_tables<16>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
+      // the tables' and resolver's draw bound NMAX at the layer's fanout
+      // class: each lane's window holds NMAX + 8 words in registers (C2 with
+      // --rng mt: 4.49 ms/step with 16 / 32 for fanouts 10 / 25, 4.17 with 12 /
+      // 32, 3.91 with 10 / 25)
+      auto run = [&](auto nmax, auto g) -> int {
+        constexpr int NM = decltype(nmax)::value, G = decltype(g)::value;
+        hipLaunchKernelGGL(k_mtp_tables<NM>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
                            ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs);
         NTS_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_mtp_resolve<16>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
-                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs, entries, ctx->mt_done, seq,
-                           ctx->mt_state, o->sizes + 3, misc + 1);
+        hipLaunchKernelGGL(k_mtp_resolve<NM>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
+                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs, entries, ctx->mt_done,
+                           seq, ctx->mt_state, o->sizes + 3, misc + 1);
         NTS_LAUNCH_CHECK();
-        hipLaunchKernelGGL((k_mt_serial<16, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
-                           info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
-      } else {
-        hipLaunchKernelGGL(k_mtp_tables<32>, tgrid, dim3(256), 0, st, info, base, o->sizes, cstat,
-                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs);
-        NTS_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_mtp_resolve<32>, dim3(1), dim3(kWave), 0, st, info, base, o->sizes,
-                           ctx->mt_ring, a0p, gen_hi, lem, mt_csz, win, tabs, entries, ctx->mt_done, seq,
-                           ctx->mt_state, o->sizes + 3, misc + 1);
-        NTS_LAUNCH_CHECK();
-        hipLaunchKernelGGL((k_mt_serial<32, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st,
-                           info, o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
-      }
+        hipLaunchKernelGGL((k_mt_serial<G, true>), dim3((uint32_t)nch_cap), dim3(kWave), 0, st, info,
+                           o->sizes, o->sample_ans, nullptr, lem, mt_dbg, chunked);
+        return NTS_OK;
+      };
+      using I16 = std::integral_constant<int, 16>;
+      using I32 = std::integral_constant<int, 32>;
+      if (fanout <= 10) NTS_RET(run(std::integral_constant<int, 10>{}, I16{}));
+      else if (fanout <= 12) NTS_RET(run(std::integral_constant<int, 12>{}, I16{}));
+      else if (fanout <= 16) NTS_RET(run(I16{}, I16{}));
+      else if (fanout <= 25) NTS_RET(run(std::integral_constant<int, 25>{}, I32{}));
+      else NTS_RET(run(I32{}, I32{}));
       NTS_LAUNCH_CHECK();
       NTS_RET(mt_ring_finish(ctx, st));
       const uint32_t gs = std::max(1u, std::min(ceil_div(o->v_cap, kSelWaves * kGrpPerWave), 4096u));

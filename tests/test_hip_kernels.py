@@ -127,7 +127,7 @@ def _assert_layers_equal(gl, ol):
 
 
 @pytest.mark.parametrize("walker", ["serial", "chunked"])
-@pytest.mark.parametrize("fanouts", [(25, 10), (3, 2), (-1, 4), (5, 5, 5)])
+@pytest.mark.parametrize("fanouts", [(25, 10), (3, 2), (-1, 4), (5, 5, 5), (15, 11), (30, 12)])
 def test_sampler_mt19937_is_reference_stream(hip, cora, fanouts, walker, monkeypatch):
     """MT19937 mode reproduces the reference generator: identical arrays to the
     oracle in draw order, identical per-dst sets to the reference's
