@@ -1068,7 +1068,10 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   // from there.  The next drawing dst's union is fetched while this one is
   // checked, based at this step's smallest Delta (Deltas only grow).  A wave
   // whose starts spread wider than the union reads its own words.
-  constexpr int NW = NMAX + 8;
+#ifndef NTS_MT_NWX
+#define NTS_MT_NWX 8  // words past the n-th a lane's window holds (compile-time A/B)
+#endif
+  constexpr int NW = NMAX + NTS_MT_NWX;
   constexpr int kU = 192;
   const int wvi = t >> 6, ln = t & 63;
   auto wmin = [](uint32_t x) {
