@@ -1555,7 +1555,11 @@ static int mt_ring_ensure(nts_hip_ctx* ctx) {
   NTS_HIP_TRY(hipMalloc(&ctx->mt_done, sizeof(uint64_t)));
   NTS_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->mt_done_host), sizeof(uint64_t),
                             hipHostMallocDefault));
-  NTS_HIP_TRY(hipStreamCreateWithFlags(&ctx->mt_gen_stream, hipStreamNonBlocking));
+  // the generator (one workgroup per launch) on a high-priority stream: its
+  // launches are dispatched ahead of queued table / training blocks
+  int lo_prio = 0, hi_prio = 0;
+  NTS_HIP_TRY(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+  NTS_HIP_TRY(hipStreamCreateWithPriority(&ctx->mt_gen_stream, hipStreamNonBlocking, hi_prio));
   return mt_ring_reset(ctx);
 }
 
