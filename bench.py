@@ -245,6 +245,9 @@ def parse():
     p.add_argument("--no-secondary-exact", action="store_true",
                    help="skip the secondary measurement of the headline order with fp32-exact "
                         "GEMM inputs (split-bf16 on the gathered rows instead of the pair tables)")
+    p.add_argument("--no-secondary-mt", action="store_true",
+                   help="skip the secondary measurement with the reference's std::mt19937 stream "
+                        "(one rank only)")
     p.add_argument("--no-secondary-af", action="store_true",
                    help="skip the secondary measurement of the reference's bottom-layer order "
                         "(aggregate-first, fp32 aggregation) beside a transform-first headline")
@@ -529,6 +532,21 @@ def main():
                     pipeline=not args.no_pipeline, transform_first=1, gemm="split3", pair_table=0,
                     deterministic_backward=not args.atomic_backward))}
 
+    # the same workload on the reference's own generator stream (std::mt19937
+    # + Lemire, every sampled array bit-exact vs the reference's serial order;
+    # one rank: the SCALE runs keep to the headline)
+    mt_ref = None
+    if (args.model == "gcn" and args.rng == "philox" and world == 1 and args.steps > 0
+            and not args.no_secondary_mt):
+        mt_ref = {
+            "rng": "std::mt19937(2000) + Lemire, the reference's stream (FastSampler::sample_fast)",
+            **time_secondary(host.gcn_config(
+                layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
+                rng_mode=RNG_MODES["mt"], weight=args.weight, fused_gather=not args.no_fused_gather,
+                pipeline=not args.no_pipeline, transform_first=args.transform_first,
+                gemm=args.gemm, pair_table=args.pair_table,
+                deterministic_backward=not args.atomic_backward))}
+
     value = edges / elapsed
     rl = roofline(prof, args, layers, world)
     result = {
@@ -573,6 +591,7 @@ def main():
             "layer_sizes_top_down": layer_sizes,
             "reference_order_secondary": secondary,
             "fp32_exact_inputs_secondary": exact_tf,
+            "reference_stream_secondary": mt_ref,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
                              "nts_env": nts_env(),
                              "workload": pmc_workload(args, layers, world)},
