@@ -25,7 +25,6 @@ from __future__ import annotations
 
 import argparse
 import hashlib
-import gc
 import json
 import os
 import pathlib
@@ -510,27 +509,6 @@ def main():
         del drv2
         return out
 
-    # the same workload on the reference's own generator stream (std::mt19937
-    # + Lemire, every sampled array bit-exact vs the reference's serial order;
-    # one rank: the SCALE runs keep to the headline)
-    mt_ref = None
-    if (args.model == "gcn" and args.rng == "philox" and world == 1 and args.steps > 0
-            and not args.no_secondary_mt):
-        # (first, with the headline driver gone: beside its streams and the
-        # other secondaries' the MT chain measured 5.1 ms/step against 3.9 alone)
-        del drv
-        gc.collect()
-        torch.cuda.synchronize()
-        mt_ref = {
-            "rng": "std::mt19937(2000) + Lemire, the reference's stream (FastSampler::sample_fast)",
-            **time_secondary(host.gcn_config(
-                layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
-                rng_mode=RNG_MODES["mt"], weight=args.weight, fused_gather=not args.no_fused_gather,
-                pipeline=not args.no_pipeline, transform_first=args.transform_first,
-                gemm=args.gemm, pair_table=args.pair_table,
-                deterministic_backward=not args.atomic_backward))}
-
-
     secondary = None  # the reference's bottom-layer order
     exact_tf = None   # the headline order with fp32-exact GEMM inputs
     if tf and args.model == "gcn" and args.steps > 0:
@@ -553,6 +531,23 @@ def main():
                     rng_mode=RNG_MODES[args.rng], weight=args.weight,
                     pipeline=not args.no_pipeline, transform_first=1, gemm="split3", pair_table=0,
                     deterministic_backward=not args.atomic_backward))}
+
+    # the same workload on the reference's own generator stream (std::mt19937
+    # + Lemire, every sampled array bit-exact vs the reference's serial order;
+    # one rank: the SCALE runs keep to the headline).  Measured beside the
+    # headline and secondary drivers' streams: 5.1 ms/step, against 3.8-3.9
+    # for `bench.py --rng mt` on its own
+    mt_ref = None
+    if (args.model == "gcn" and args.rng == "philox" and world == 1 and args.steps > 0
+            and not args.no_secondary_mt):
+        mt_ref = {
+            "rng": "std::mt19937(2000) + Lemire, the reference's stream (FastSampler::sample_fast)",
+            **time_secondary(host.gcn_config(
+                layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
+                rng_mode=RNG_MODES["mt"], weight=args.weight, fused_gather=not args.no_fused_gather,
+                pipeline=not args.no_pipeline, transform_first=args.transform_first,
+                gemm=args.gemm, pair_table=args.pair_table,
+                deterministic_backward=not args.atomic_backward))}
 
     value = edges / elapsed
     rl = roofline(prof, args, layers, world)
