@@ -287,4 +287,13 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
 int gemm3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda,
              const uint32_t* amap, const float* B, uint64_t ldb, const float* X, uint64_t ldx,
              float bscale, float* C, uint64_t ldc);
+// the same arithmetic over whole gathered feature rows streamed into LDS
+// (gemmx3.hip): the transform-first bottom layer's GEMMs
+bool x3_tn_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb);
+int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, const uint32_t* amap,
+          const float* B, uint64_t ldb, float* C, uint64_t ldc);
+bool x3_nn_ok(int M, int N, int K, const float* A, uint64_t lda);
+int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,
+          const uint32_t* amap, const char* bimg, float* C, uint64_t ldc, uint32_t keep_threshold,
+          float scale, uint64_t seed, uint64_t offset);
 }  // namespace nts_hip

@@ -749,6 +749,10 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
   hipLaunchKernelGGL(k_split3_b, dim3((total + 255) / 256), dim3(256), 0, ctx->stream, B, ldb, K,
                      N, total, ncb, bimg);
   NTS_LAUNCH_CHECK();
+#ifndef NTS_NO_X3  // (variant builds: -DNTS_NO_X3 keeps k_gemm3_nn for A/B)
+  if (amap && x3_nn_ok(M, N, K, A, lda))
+    return x3_nn(ctx, epi, M, N, K, A, lda, amap, bimg, C, ldc, keep_threshold, scale, seed, offset);
+#endif
   // one 8-wave block per CU over all column blocks (row blocks a multiple of 8:
   // XCD pairing), no more blocks than 16-tile rounds
   const int T = (M + 15) / 16;
@@ -790,6 +794,10 @@ int gemm3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda
   ex.bx = X;
   ex.ldbx = ldx;
   ex.bscale = bscale;
+#ifndef NTS_NO_X3  // (variant builds: -DNTS_NO_X3 keeps k_s3_tn for A/B)
+  if (amap && !X && x3_tn_ok(M, N, K, A, lda, B, ldb))
+    return x3_tn(ctx, M, N, K, A, lda, amap, B, ldb, C, ldc);
+#endif
   const bool v2_ok = ldb % 4 == 0 && (uintptr_t)B % 16 == 0 &&
                      (!X || (ldx % 4 == 0 && (uintptr_t)X % 16 == 0)) &&
                      (!amap || (uintptr_t)amap % 16 == 0);

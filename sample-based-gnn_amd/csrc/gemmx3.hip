@@ -1,0 +1,636 @@
+// fp32-exact row-gathered GEMMs of the transform-first bottom layer on the
+// bf16 matrix cores (the headline's arithmetic, NTS_GEMM_SPLIT3).
+//
+// The operands are the fp32 feature table itself (no pair table): every fp32
+// value x is split exactly into three bf16 pieces inside the kernel,
+//     x0 = bf16(x),  x1 = bf16(x - x0),  x2 = bf16(x - x0 - x1)   (RNE each)
+// so x0 + x1 + x2 == x for every finite fp32 (24 significant bits, the
+// exponent range of fp32), and a product a b is the six bf16 products
+//     a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0
+// (dropped: a1 b2, a2 b1, a2 b2, each <= 2^-24 |a b|), exact in the fp32
+// accumulator — the split of gemm3.hip, i.e. the reference's fp32
+// `x.matmul(W)` (core/NtsScheduler.hpp:859-862) to fp32 accuracy.
+//
+// What these kernels change against gemm3.hip's k_gemm3_nn / k_s3_tn is the
+// access pattern: WHOLE gathered feature rows (2,432 B of 602 floats) are
+// streamed into LDS by global_load_lds, row-aligned 1-KiB pieces, three
+// stages (two steps in flight), the row ids staged in LDS — the pattern that
+// measured 5.9 TB/s for the pair tables (scripts/probe/stream_probe.hip) —
+// instead of 128-byte slices of 16 rows per k-step (k_gemm3_nn) or dword
+// column gathers (k_s3_tn).
+//
+//   k_x3_tn  dW = X[amap]^T dH: one block per chunk of the gathered rows
+//            covers EVERY output row (the structure of gemmh2.hip's k_h2_tn4):
+//            per 16-row step, each wave reads its X^T fragments with
+//            ds_read_b32 (32 consecutive columns per half-wave: conflict-free)
+//            and its dH fragments likewise, splits them in registers, and runs
+//            v_mfma_f32_32x32x16_bf16 x 6 per 32x32 tile; the chunks'
+//            partials are summed in a fixed order (sum_splits): deterministic.
+#include "common.hpp"
+#include <type_traits>
+
+namespace nts_hip {
+
+typedef __bf16 x3bf8 __attribute__((ext_vector_type(8)));
+typedef float x3f16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* x3_lds_ptr;
+
+__device__ __forceinline__ uint32_t x3_lds(const void* p) { return (uint32_t)(uintptr_t)(x3_lds_ptr)p; }
+// 16 bytes per lane from `src` to LDS (wave-uniform base `lds`) + 16 * lane;
+// inline asm: a compiler-visible LDS DMA makes hipcc drain every stage (see
+// gemm3.hip), so completion is counted by hand with s_waitcnt vmcnt
+__device__ __forceinline__ void x3_glds16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+__device__ __forceinline__ void x3_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// x -> (x0, x1, x2), element-wise over one lane's 8 fragment values
+__device__ __forceinline__ void x3_split(const float (&x)[8], x3bf8 (&h)[3]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 a0 = (__bf16)x[j];
+    const float r1 = x[j] - (float)a0;
+    const __bf16 a1 = (__bf16)r1;
+    h[0][j] = a0;
+    h[1][j] = a1;
+    h[2][j] = (__bf16)(r1 - (float)a1);
+  }
+}
+
+// acc += a b over one 16-deep k-slice of a 32x32 tile (small products first)
+__device__ __forceinline__ x3f16 x3_mfma6(const x3bf8 (&a)[3], const x3bf8 (&b)[3], x3f16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+// ---------------------------------------------------------------------------
+// TN: C[M x N] = X[amap[k]][0..M)^T B[k][0..N) over the gathered rows k of
+// [kbeg, kend) (one chunk per block; N in 128-column blocks).  M <= 608: an
+// X row of Kp = 32 ceil(M / 32) floats is RB = 4 Kp bytes, PR = ceil(RB /
+// 1024) row-aligned DMA pieces per row.
+// LDS: X stages [3][16][RB]; raw dH stages [2][16][128 floats]; dH's three
+// bf16 planes [2 buffers][3][16][128] (256-byte rows, 16-byte chunks
+// XOR-swizzled for ds_read_b64_tr_b16, the layout of gemmh2.hip's TN); row ids.
+// Wave wv: wn = wv & 1 takes columns 64 wn .. +63 (two 32-column tiles), wm =
+// wv >> 1 a quarter of the 32-row output tiles (at most TPW).
+// Per 16-row step s, after the wait (this wave's X(s) and dH(s+1) pieces; the
+// 2 PR pieces of X(s+1) may stay in flight) and the barrier:
+//   issue dH(s+2) into the raw stage dH(s) left, X(s+2) into the stage X(s-1)
+//     left (row ids read one step ahead);
+//   split dH(s+1) (rows past the chunk zeroed) into the other plane buffer,
+//     one float4 per thread (visible to every wave after the next barrier);
+//   B fragments of step s from the planes written during step s-1 (tr reads);
+//   A fragments of tile t: lane (c, h) reads X[16 s + 8 h + j][32 (m_lo + t) +
+//     c], j = 0..7 (ds_read_b32, 32 consecutive dwords per half-wave) for tile
+//     t+1 while tile t's 12 MFMAs run, and splits them (rows past the chunk
+//     are duplicates of its last row, multiplied by zeroed dH rows; the
+//     table's pad columns only reach output rows >= M, never stored).
+constexpr int kX3Threads = 512;
+constexpr int kX3BRaw = 16 * 512;   // one step of fp32 dH rows (128 columns)
+constexpr int kX3BPl = 16 * 256;    // one bf16 plane of a step
+
+__device__ __forceinline__ int x3_tr_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef short x3s4 __attribute__((ext_vector_type(4)));
+typedef short x3s8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) x3s4 x3_lds_s4;
+
+// exact split of two fp32 values into three packed bf16 pairs (RNE each; the
+// per-pair form of x3_split, so the pieces can be scheduled pair by pair)
+typedef __bf16 x3bf2 __attribute__((ext_vector_type(2)));
+typedef float x3f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t x3u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void x3_split2(float x0, float x1, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  const x3bf2 h = __builtin_convertvector((x3f2){x0, x1}, x3bf2);
+  const x3f2 hf = __builtin_convertvector(h, x3f2);
+  const float r0 = x0 - hf[0], r1 = x1 - hf[1];
+  const x3bf2 m = __builtin_convertvector((x3f2){r0, r1}, x3bf2);
+  const x3f2 mf = __builtin_convertvector(m, x3f2);
+  const x3bf2 l = __builtin_convertvector((x3f2){r0 - mf[0], r1 - mf[1]}, x3bf2);
+  p0 = __builtin_bit_cast(uint32_t, h);
+  p1 = __builtin_bit_cast(uint32_t, m);
+  p2 = __builtin_bit_cast(uint32_t, l);
+}
+
+// DIAG (timing probes, NTS_X3_DIAG in the probe build only; results are
+// garbage): 1 no MFMAs, 2 no A splits, 4 no DMA after the prologue, 8 no A
+// fragment reads, 16 no wait for the DMA, 32 no slab stores
+//
+// Instruction schedule of a step (one wave): the head (the wait, the
+// barrier, dH(s+2)'s DMA, the B fragments, tile 0's A fragment split) and
+// then, per 32-row tile t, TWELVE slots, each one MFMA of tile t (the two
+// n-tiles' chains alternate) followed by a fixed share of the other work:
+// tile t+2's eight A reads, one of tile t+1's four split pairs, and —
+// spread over tiles 0..2 — X(s+2)'s six DMA pieces, the block's split of
+// dH(s+1) into the planes, and the row ids of step s+3.  sched_barrier(0)
+// between slots keeps that order: the wave issues its VALU and LDS work in
+// the shadow of its own MFMAs (in-order issue would otherwise run a tile's
+// twelve MFMAs, then its VALU, then its reads, none overlapping).
+template <int TPW, int PR, int DIAG = 0>
+__global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const float* __restrict__ X,
+                                                        uint64_t ldx, const uint32_t* __restrict__ amap,
+                                                        const float* __restrict__ B, uint64_t ldb,
+                                                        float* __restrict__ C, uint64_t ldc, int kchunk,
+                                                        uint64_t split_stride, int nnb) {
+  static_assert(2 * PR <= 6, "X DMA pieces per wave and step");
+  extern __shared__ __attribute__((aligned(16))) char x3tn[];
+  const int Kp = (M + 31) / 32 * 32, RB = 4 * Kp, RW = Kp;  // LDS row: bytes, floats
+  const int xstage = 16 * RB;
+  char* const sx = x3tn;                         // [3][16][RB]
+  char* const sbr = sx + 3 * xstage;             // [2][kX3BRaw]
+  char* const sbp = sbr + 2 * kX3BRaw;           // [2][3][kX3BPl]
+  uint32_t* const sid = reinterpret_cast<uint32_t*>(sbp + 6 * kX3BPl);  // [16 (nsteps + 3)]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nb = blockIdx.x % nnb, split = blockIdx.x / nnb;
+  const int n0 = nb * 128;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk), klast = kend - kbeg - 1;
+  if (klast < 0) return;  // (block-uniform)
+  const int nsteps = (kend - kbeg + 15) / 16;
+  // ids past the chunk: its last row again (every step's DMA, real or not,
+  // reads valid rows, so the per-wave piece counts stay uniform)
+  for (int k = tid; k < 16 * (nsteps + 3); k += kX3Threads)
+    sid[k] = amap ? amap[kbeg + min(k, klast)] : (uint32_t)(kbeg + min(k, klast));
+  __syncthreads();
+  const uint32_t lsx = x3_lds(sx), lsbr = x3_lds(sbr);
+  // this wave's DMA rows of a step: 2 wv, 2 wv + 1
+  auto ids_read = [&](int s) { return *reinterpret_cast<const uint2*>(sid + 16 * s + 2 * wv); };
+  auto ids_uni = [&](uint2 u) {
+    return make_uint2(__builtin_amdgcn_readfirstlane(u.x), __builtin_amdgcn_readfirstlane(u.y));
+  };
+  auto issue_x1 = [&](int s, uint2 id, int q) {  // piece q of this wave's X(s) pieces
+    if ((DIAG & 4) && s >= 2) return;
+    const int row = 2 * wv + q / PR, part = q % PR;
+    const int off = 1024 * part + 16 * lane;
+    const char* src = reinterpret_cast<const char*>(X + (uint64_t)(q < PR ? id.x : id.y) * ldx) + off;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lsx + (s % 3) * xstage + row * RB + 1024 * part);
+    if (off < RB) x3_glds16(src, dst);  // lane 0 always issues: the wave's count is exact
+  };
+  auto issue_b = [&](int s) {
+    if ((DIAG & 4) && s >= 2) return;
+    const int row = 2 * wv + (lane >> 5);
+    const int k = kbeg + min(16 * s + row, klast);
+    x3_glds16(B + (uint64_t)k * ldb + n0 + 4 * (lane & 31), lsbr + (s & 1) * kX3BRaw + 1024 * wv);
+  };
+  // dH(s) raw -> three bf16 planes (buffer s & 1): row sr, columns sc .. sc+3
+  const int sr = tid >> 5, sc = 4 * (tid & 31);
+  const int soff = x3_tr_off(sr, sc / 8) + 8 * ((sc / 4) & 1);
+  auto splitb_read = [&](int s) {
+    return *reinterpret_cast<const float4*>(sbr + (s & 1) * kX3BRaw + 512 * sr + 4 * sc);
+  };
+  auto splitb_write = [&](int s, float4 v) {
+    const bool ok = 16 * s + sr <= klast;
+    uint32_t q0[2], q1[2], q2[2];
+    x3_split2(ok ? v.x : 0.f, ok ? v.y : 0.f, q0[0], q1[0], q2[0]);
+    x3_split2(ok ? v.z : 0.f, ok ? v.w : 0.f, q0[1], q1[1], q2[1]);
+    char* dst = sbp + (s & 1) * 3 * kX3BPl + soff;
+    *reinterpret_cast<uint2*>(dst) = make_uint2(q0[0], q0[1]);
+    *reinterpret_cast<uint2*>(dst + kX3BPl) = make_uint2(q1[0], q1[1]);
+    *reinterpret_cast<uint2*>(dst + 2 * kX3BPl) = make_uint2(q2[0], q2[1]);
+  };
+  const int wn = wv & 1, wm = wv >> 1;
+  const int T32 = (M + 31) / 32;
+  const int m_lo = wm * T32 / 4, nmt = (wm + 1) * T32 / 4 - m_lo;
+  const int c = lane & 31, h = lane >> 5;
+  // 32x32x16 B fragments from the planes: lane (c, h) holds rows 8h .. 8h+7 of
+  // column c, read as two transposed 4-row halves by its 16-lane group
+  const int half = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+  int boff[2][2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int ch = (2 * (64 * wn + 32 * nt + 16 * half + 4 * tp)) / 16;
+    boff[nt][0] = x3_tr_off(8 * h + tq, ch) + 8 * (tp & 1);
+    boff[nt][1] = x3_tr_off(8 * h + tq + 4, ch) + 8 * (tp & 1);
+  }
+  // the A^T fragment column of each tile slot (tiles past nmt repeat the
+  // wave's last one: computed, never stored)
+  int xcol[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) xcol[t] = 32 * max(0, min(m_lo + min(t, nmt - 1), T32 - 1)) + 8 * h * RW + c;
+  x3f16 acc[TPW][2];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[t][nt][v] = 0.f;
+  // prologue: dH(0) split into planes 0; then dH(1), X(0), X(1) in flight
+  issue_b(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  x3_barrier();
+  splitb_write(0, splitb_read(0));
+  issue_b(1);
+  {
+    const uint2 i0 = ids_uni(ids_read(0)), i1 = ids_uni(ids_read(1));
+#pragma unroll
+    for (int q = 0; q < 2 * PR; ++q) issue_x1(0, i0, q);
+#pragma unroll
+    for (int q = 0; q < 2 * PR; ++q) issue_x1(1, i1, q);
+  }
+  uint2 idn = ids_uni(ids_read(2));
+  for (int s = 0; s < nsteps; ++s) {
+    if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (!(DIAG & 16)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PR) : "memory");
+    x3_barrier();
+    issue_b(s + 2);
+    const char* pl = sbp + (s & 1) * 3 * kX3BPl;
+    x3bf8 bq[2][3];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const x3s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((x3_lds_s4*)(pl + p * kX3BPl + boff[nt][0]));
+        const x3s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((x3_lds_s4*)(pl + p * kX3BPl + boff[nt][1]));
+        const x3s8 w = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        bq[nt][p] = __builtin_bit_cast(x3bf8, w);
+      }
+    const float* xs = reinterpret_cast<const float*>(sx + (s % 3) * xstage);
+    float xr[2][8];      // raw A^T fragments, tile t in slot t & 1
+    uint32_t ap[2][3][4];  // split pieces, tile t in slot t & 1: [piece][pair]
+    auto rd = [&](int t, int j) {
+      if constexpr (DIAG & 8) return (float)(t + j) * (float)lane;
+      else return xs[xcol[t] + j * RW];
+    };
+    auto sp = [&](int t, int jp) {  // pair jp of tile t's split
+      if constexpr (DIAG & 2) {
+        ap[t & 1][0][jp] = ap[t & 1][1][jp] = ap[t & 1][2][jp] = __float_as_uint(xr[t & 1][2 * jp]);
+      } else {
+        x3_split2(xr[t & 1][2 * jp], xr[t & 1][2 * jp + 1], ap[t & 1][0][jp], ap[t & 1][1][jp],
+                  ap[t & 1][2][jp]);
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xr[0][j] = rd(0, j);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xr[1][j] = rd(1, j);
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) sp(0, jp);
+    const uint2 idx = idn;  // X(s+2)'s rows
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint2 idr = make_uint2(0u, 0u);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      x3bf8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[p] = __builtin_bit_cast(x3bf8, (x3u4){ap[t & 1][p][0], ap[t & 1][p][1], ap[t & 1][p][2], ap[t & 1][p][3]});
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        __builtin_amdgcn_sched_barrier(0);
+        {  // slot k: product k / 2 (small first) of n-tile k & 1
+          const int nt = k & 1, pr = k >> 1;
+          const int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
+          const int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
+          if constexpr (DIAG & 1) acc[t][nt][0] += (float)a[pa][0] + (float)bq[nt][pb][3];
+          else acc[t][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], bq[nt][pb], acc[t][nt], 0, 0, 0);
+        }
+        if (t + 2 < TPW && k < 8) xr[t & 1][k] = rd(t + 2, k);
+        if (t + 1 < TPW && (k == 3 || k == 5 || k == 7 || k == 9)) sp(t + 1, (k - 3) / 2);
+        if (t == 0 && (k & 1) && k / 2 < 2 * PR) issue_x1(s + 2, idx, k / 2);
+        if (t == 1 && k == 1) bv = splitb_read(s + 1);
+        if (t == 1 && k == 8) splitb_write(s + 1, bv);  // (past the last step: never read)
+        if (t == 2 && k == 1) idr = ids_read(s + 3);
+        if (t == 2 && k == 10) idn = ids_uni(idr);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+  x3_barrier();
+  // acc[t][nt][v] = C[32 (m_lo + t) + 8 (v / 4) + 4 h + v % 4][n0 + 64 wn + 32 nt + c]
+  float* Cb = C + (uint64_t)split * split_stride;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int col = n0 + 64 * wn + 32 * nt + c;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if (t >= nmt) continue;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = 32 * (m_lo + t) + 8 * (v / 4) + 4 * h + (v % 4);
+        if (row < M && (!(DIAG & 32) || acc[t][nt][v] == 1234.5f)) Cb[(uint64_t)row * ldc + col] = acc[t][nt][v];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// NN: C[M x N] = X[amap[m]][0..K) W (+ relu/dropout): 8-wave blocks, one
+// 128-column block per grid.y; the M rows cut into 16-row tiles, wave gw of
+// the grid owning the contiguous tiles [gw T / W, (gw+1) T / W), two at a time
+// in `rounds` rounds (one count for the grid: a block's waves stay in step
+// over the shared W image).  Per 32-deep k-step g of the (round, k-step)
+// sequence, every operand comes from compiler-visible loads TWO steps ahead:
+//   A: lane (i, q) of row tile rt loads X[id][32 s + 8 q .. +7] (two
+//      dwordx4) into a register ring, splits it one step ahead — late in the
+//      step before its MFMAs, beside them;
+//   W: the pre-split fragment image of step s (k_split3_b: 24 KB, three
+//      dwordx4 per thread) into a register ring, written to the LDS stage
+//      late in the step before (two stages, one barrier per step);
+// and per step each wave runs 8 column tiles x 2 row tiles x 6 MFMAs with the
+// B fragments of column tile ct+1 read while those of ct run.  Each output
+// element's sum is k_gemm3_nn's (same split, same piece order, same k order,
+// same MFMA): the results are bit-identical to gemm3.hip's NN.
+constexpr int kX3NnImg = 8 * 3 * 1024;  // one (step, column block) W image
+struct X3Epi {
+  uint32_t keep_threshold = 0;  // EPI: relu + inverted dropout (common.hpp dropout_*)
+  float scale = 1.f;
+  uint64_t seed = 0, offset = 0;
+};
+
+typedef float x3f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ x3f4 x3_mfma6s(const x3bf8 (&a)[3], const x3bf8 (&b)[3], x3f4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+template <bool EPI>
+__global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, const float* __restrict__ X,
+                                                        uint64_t ldx, const uint32_t* __restrict__ amap,
+                                                        const char* __restrict__ bimg,
+                                                        float* __restrict__ C, uint64_t ldc, int rounds,
+                                                        X3Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char x3nn[];  // [2][kX3NnImg]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, q = lane >> 4;
+  const int nb = blockIdx.y, n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int64_t Wn = (int64_t)gridDim.x * 8, gw = (int64_t)blockIdx.x * 8 + wv;
+  const int t_lo = (int)(gw * T / Wn), t_hi = (int)((gw + 1) * T / Wn);
+  const int nks = (K + 31) / 32;
+  const int G = rounds * nks;
+  const size_t bstep = (size_t)gridDim.y * kX3NnImg;
+  const char* bsrc = bimg + (size_t)nb * kX3NnImg + 16 * tid;
+  // this lane's two rows of round r (clamped: a missing tile repeats the
+  // wave's last one and is never stored)
+  auto row_ids = [&](int r, uint32_t (&id)[2]) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int t = min(t_lo + 2 * r + rt, max(t_hi - 1, t_lo));
+      const int64_t row = min((int64_t)t * 16 + i, (int64_t)M - 1);
+      id[rt] = amap ? amap[row] : (uint32_t)row;
+    }
+  };
+  float araw[2][2][8];  // [slot][rt][j]: A(g) in slot g & 1
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 wraw[2][3];     // [slot][piece]: W image of step g, 16 B per thread and piece
+  x3bf8 apc[2][2][3];   // [slot][rt][piece]: split A of step g in slot g & 1
+  uint32_t idc[2], idn[2];  // row ids of the current / next round
+  auto load = [&](int g, const uint32_t (&id)[2], auto slot) {
+    constexpr int sl = decltype(slot)::value;  // g & 1
+    const int s = g % nks;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const float* p = X + (uint64_t)id[rt] * ldx + 32 * s + 8 * q;
+      typedef float f32x4v __attribute__((ext_vector_type(4)));
+      const f32x4v u = *reinterpret_cast<const f32x4v*>(p);
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(p + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        araw[sl][rt][j] = u[j];
+        araw[sl][rt][4 + j] = v[j];
+      }
+    }
+    const char* b = bsrc + (size_t)s * bstep;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) wraw[sl][p] = *reinterpret_cast<const u32x4*>(b + 8192 * p);
+  };
+  auto split_a = [&](int g, auto slot) {
+    constexpr int sl = decltype(slot)::value;  // g & 1
+    const int s = g % nks;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = 32 * s + 8 * q + j < K ? araw[sl][rt][j] : 0.f;  // the pad past K
+      x3_split(x, apc[sl][rt]);
+    }
+  };
+  auto put_w = [&](auto slot) {
+    constexpr int sl = decltype(slot)::value;  // g & 1
+    char* dst = x3nn + sl * kX3NnImg + 16 * tid;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(dst + 8192 * p) = wraw[sl][p];
+  };
+  x3f4 acc[2][8];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+  // prologue: W(0) staged, A(0) split, A(1) / W(1) loaded
+  row_ids(0, idc);
+  row_ids(min(1, rounds - 1), idn);
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  load(0, idc, S0());
+  if (G > 1) load(1, nks > 1 ? idc : idn, S1());
+  split_a(0, S0());
+  put_w(S0());
+  // one step: MFMAs of g on the B fragments of stage g & 1 and the pieces of
+  // slot g & 1; loads of g + 2; the split of A(g+1) and the staging of W(g+1)
+  // beside the second half of the MFMAs; the epilogue after a round's last step
+  auto step = [&](int g, auto par) {
+    constexpr int P = decltype(par)::value;  // g & 1
+    const int s = g % nks, r = g / nks;
+    x3_barrier();  // W(g) staged by every wave; stage (g+1) & 1 free
+    if (g + 2 < G) {
+      const int g2 = g + 2, r2 = g2 / nks;
+      if (r2 == r) load(g2, idc, par);
+      else load(g2, idn, par);
+    }
+    const char* img = x3nn + P * kX3NnImg;
+    auto getb = [&](int ct, x3bf8 (&b)[3]) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
+    };
+    x3bf8 bf[2][3];
+    getb(0, bf[0]);
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      if (ct + 1 < 8) getb(ct + 1, bf[(ct + 1) & 1]);
+      if (ct == 4 && g + 1 < G) {
+        split_a(g + 1, std::integral_constant<int, 1 - P>());
+        put_w(std::integral_constant<int, 1 - P>());
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      acc[0][ct] = x3_mfma6s(apc[P][0], bf[ct & 1], acc[0][ct]);
+      acc[1][ct] = x3_mfma6s(apc[P][1], bf[ct & 1], acc[1][ct]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (s == nks - 1) {  // round r done: store its tiles, start the next round
+      const int nt = min(2, max(0, t_hi - (t_lo + 2 * r)));
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        if (rt < nt) {
+          const int64_t r4 = (int64_t)(t_lo + 2 * r + rt) * 16 + 4 * q;
+#pragma unroll
+          for (int ct = 0; ct < 8; ++ct) {
+            const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+            float o[4] = {acc[rt][ct][0], acc[rt][ct][1], acc[rt][ct][2], acc[rt][ct][3]};
+            if constexpr (EPI) {
+              const uint4 rnd = dropout_words((uint64_t)r4, col, ep.seed, ep.offset);
+              const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+              for (int v = 0; v < 4; ++v)
+                o[v] = (dropout_bits(wd[v], col) >= ep.keep_threshold && o[v] > 0.f) ? o[v] * ep.scale : 0.f;
+            }
+            if ((int)col < N) {
+#pragma unroll
+              for (int v = 0; v < 4; ++v)
+                if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+            }
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+      }
+      idc[0] = idn[0];
+      idc[1] = idn[1];
+      if (r + 2 < rounds) row_ids(r + 2, idn);
+    }
+  };
+  for (int g = 0; g < G; g += 2) {
+    step(g, std::integral_constant<int, 0>());
+    if (g + 1 < G) step(g + 1, std::integral_constant<int, 1>());
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers (gemm3.hip's gemm3_tn / gemm3_nn try these first)
+
+// whole rows of at most 608 floats (Kp), 16-byte aligned, read as Kp floats
+// (so the table's row pitch must cover Kp); 128-column blocks
+bool x3_tn_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb) {
+  const int Kp = (M + 31) / 32 * 32;
+  // the X stages, dH stages and planes leave room for >= 256 row ids (Kp <= 608)
+  const int lds = 3 * 16 * 4 * Kp + 2 * kX3BRaw + 6 * kX3BPl + 4 * 16 * 3 + 4 * 256;
+  return M >= 32 && lds <= 160 * 1024 && N % 128 == 0 && K >= 256 && lda >= (uint64_t)Kp && lda % 4 == 0 &&
+         (uintptr_t)A % 16 == 0 && ldb % 4 == 0 && (uintptr_t)B % 16 == 0;
+}
+
+int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, const uint32_t* amap,
+          const float* B, uint64_t ldb, float* C, uint64_t ldc) {
+  constexpr int TPW = 5;  // ceil(20 tiles / 4)
+  const int Kp = (M + 31) / 32 * 32, RB = 4 * Kp;
+  const int nnb = N / 128;
+  const int ksteps = (K + 15) / 16;
+  int splits = std::max(1, std::min(256 / nnb, ksteps / 8));
+  int kchunk = ((ksteps + splits - 1) / splits) * 16;
+  const int fixed = 3 * 16 * RB + 2 * kX3BRaw + 6 * kX3BPl + 4 * 16 * 3;
+  kchunk = std::min(kchunk, (160 * 1024 - fixed) / 4 / 16 * 16);
+  splits = (K + kchunk - 1) / kchunk;
+  const int lds = fixed + 4 * kchunk;
+  const uint64_t stride = (uint64_t)M * N;
+  float* out = C;
+  uint64_t ldo = ldc;
+  if (splits > 1) {
+    NTS_RET(ensure_scratch(ctx, stride * splits * sizeof(float) + 256));
+    out = (float*)ctx->scratch;
+    ldo = N;
+  }
+  const int pr = (RB + 1023) / 1024;
+#define NTS_X3TN(P, D)                                                                           \
+  do {                                                                                           \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_tn<TPW, P, D>),          \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));           \
+    hipLaunchKernelGGL((k_x3_tn<TPW, P, D>), dim3(nnb * splits), dim3(kX3Threads), lds,          \
+                       ctx->stream, M, K, A, lda, amap, B, ldb, out, ldo, kchunk,                \
+                       splits > 1 ? stride : (uint64_t)0, nnb);                                  \
+  } while (0)
+#ifdef NTS_PROBE_BUILD
+  static const int diag = [] {
+    const char* e = getenv("NTS_X3_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  if (pr == 3 && diag) {
+    switch (diag) {
+      case 1: NTS_X3TN(3, 1); break;
+      case 2: NTS_X3TN(3, 2); break;
+      case 4: NTS_X3TN(3, 4); break;
+      case 5: NTS_X3TN(3, 5); break;
+      case 6: NTS_X3TN(3, 6); break;
+      case 8: NTS_X3TN(3, 8); break;
+      case 10: NTS_X3TN(3, 10); break;
+      case 12: NTS_X3TN(3, 12); break;
+      case 14: NTS_X3TN(3, 14); break;
+      case 16: NTS_X3TN(3, 16); break;
+      case 32: NTS_X3TN(3, 32); break;
+      case 36: NTS_X3TN(3, 36); break;
+      default: NTS_X3TN(3, 15); break;
+    }
+  } else
+#endif
+  if (pr == 1) NTS_X3TN(1, 0);
+  else if (pr == 2) NTS_X3TN(2, 0);
+  else NTS_X3TN(3, 0);
+#undef NTS_X3TN
+  NTS_LAUNCH_CHECK();
+  if (splits == 1) return NTS_OK;
+  return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+}
+
+// NN over gathered rows (or dense, amap null): rows read as Kp = 32 ceil(K /
+// 32) floats (the row pitch must cover them), 16-byte aligned
+bool x3_nn_ok(int M, int N, int K, const float* A, uint64_t lda) {
+  const int Kp = (K + 31) / 32 * 32;
+  return M >= 256 && K >= 1 && N % 16 == 0 && lda >= (uint64_t)Kp && lda % 4 == 0 &&
+         (uintptr_t)A % 16 == 0;
+}
+
+int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,
+          const uint32_t* amap, const char* bimg, float* C, uint64_t ldc, uint32_t keep_threshold,
+          float scale, uint64_t seed, uint64_t offset) {
+  X3Epi ep;
+  ep.keep_threshold = keep_threshold;
+  ep.scale = scale;
+  ep.seed = seed;
+  ep.offset = offset;
+  const int ncb = (N + 127) / 128;
+  const int T = (M + 15) / 16;
+  int gx = std::max(1, 256 / ncb);
+  gx = std::min(gx, (T + 15) / 16);
+  const int64_t Wn = (int64_t)gx * 8;
+  const int max_tiles = (int)((T + Wn - 1) / Wn);
+  const int rounds = (max_tiles + 1) / 2;
+  const dim3 grid(gx, ncb);
+  const int lds = 2 * kX3NnImg;
+  if (epi) {
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL(k_x3_nn<true>, grid, dim3(kX3Threads), lds, ctx->stream, M, N, K, A, lda, amap,
+                       bimg, C, ldc, rounds, ep);
+  } else {
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    hipLaunchKernelGGL(k_x3_nn<false>, grid, dim3(kX3Threads), lds, ctx->stream, M, N, K, A, lda, amap,
+                       bimg, C, ldc, rounds, ep);
+  }
+  NTS_LAUNCH_CHECK();
+  return NTS_OK;
+}
+
+}  // namespace nts_hip

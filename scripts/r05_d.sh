@@ -1,0 +1,16 @@
+#!/bin/bash
+# k_x3_tn / k_x3_nn: parity, then timing against the gemm3.hip kernels (nox3
+# variant) and the TN timing probes (probe build)
+set -o pipefail
+cd "$(dirname "$0")/.."
+O=gpurun_out/r05d; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+    tests/test_gemm_x3.py tests/test_gemm_split3.py > $O/tests.log 2>&1 || exit 1
+timeout -k 10 60 python -u scripts/micro_x3.py --iters 50 --tag product > $O/micro.jsonl 2>&1 || exit 1
+NTS_HIP_LIB=scripts/probe/lib_nox3/libnts_hip.so timeout -k 10 60 \
+    python -u scripts/micro_x3.py --iters 50 --tag nox3 >> $O/micro.jsonl 2>&1 || exit 1
+for D in 0 1 2 4 8 3 10 11 15; do
+  NTS_HIP_LIB=scripts/probe/lib/libnts_hip.so NTS_X3_DIAG=$D timeout -k 10 60 \
+      python -u scripts/micro_x3.py --iters 50 --tag diag$D >> $O/micro.jsonl 2>&1 || exit 1
+done

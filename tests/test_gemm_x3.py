@@ -1,0 +1,93 @@
+"""fp32-exact row-gathered GEMMs over whole feature rows (csrc/gemmx3.hip):
+the transform-first bottom layer's H = X[src] W and dW = X[src]^T dH in the
+headline's arithmetic (every fp32 operand split exactly into three bf16
+pieces in the kernel, six products, fp32 accumulate).
+
+Bar (as tests/test_gemm_split3.py): error against an fp64 GEMM of the same
+fp32 operands at most 1.25x the fp32-input MFMA path's (plus 1e-7 of the
+operand scale) on every shape the kernels take — the reference's fp32
+`x.matmul(W)` precision class (core/NtsScheduler.hpp:859-862); NaN in the
+table's pad columns never reaches a stored element; deterministic.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    from nts import _abi
+    from nts.hip import HipContext
+    f32 = HipContext(0, seed=2000)
+    s3 = HipContext(0, seed=2000)
+    s3.set_gemm_mode(_abi.NTS_GEMM_SPLIT3)
+    return f32, s3
+
+
+def _table(V, K, g, pitch=None):
+    """[V, K] view of a table whose pad columns hold NaN (row pitch: 640 floats
+    for K = 602, the padded feature table's)"""
+    ld = pitch or ((K + 31) // 32 * 32 + 32)
+    big = torch.full((V, ld), float("nan"), device=DEV)
+    big[:, :K] = torch.randn(V, K, device=DEV, generator=g)
+    return big[:, :K]
+
+
+def _check(got32, got3, ref, scale):
+    e32 = ((got32.double() - ref).abs() / scale).max().item()
+    e3 = ((got3.double() - ref).abs() / scale).max().item()
+    assert e3 <= 1.25 * e32 + 1e-7, (e3, e32)
+    assert e3 < 5e-7, e3
+
+
+@pytest.mark.parametrize("M,N,K", [(602, 128, 228656), (602, 128, 4099), (640, 128, 3001),
+                                   (100, 256, 3000), (128, 128, 70001), (41, 128, 300),
+                                   (602, 128, 257)])
+def test_x3_tn_gather(ctxs, M, N, K):
+    f32, s3 = ctxs
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + N + K)
+    V = K + K // 2 + 5
+    table = _table(V, M, g)
+    rows = torch.randint(0, V, (K,), device=DEV, generator=g).to(torch.int32)
+    rows, _ = torch.sort(rows)  # the sampler's src lists are ascending
+    G = torch.randn(K, N, device=DEV, generator=g) * torch.rand(K, 1, device=DEV, generator=g)
+    C32 = torch.empty(M, N, device=DEV)
+    C3 = torch.full((M, N), float("nan"), device=DEV)
+    f32.gemm_tn_gather(table, rows, G, C32)
+    s3.gemm_tn_gather(table, rows, G, C3)
+    Xg = table[rows.long()].double()
+    ref = Xg.t() @ G.double()
+    scale = Xg.abs().t() @ G.double().abs() + 1e-30
+    torch.cuda.synchronize()
+    assert not torch.isnan(C3).any()
+    _check(C32, C3, ref, scale)
+    C3b = torch.empty_like(C3)
+    s3.gemm_tn_gather(table, rows, G, C3b)
+    torch.cuda.synchronize()
+    assert torch.equal(C3, C3b)
+
+
+def test_x3_tn_wide_range(ctxs):
+    """rows spanning many decades and tiny gradients: exact three-piece inputs
+    keep every element's relative precision (no per-row scale)"""
+    f32, s3 = ctxs
+    g = torch.Generator(device=DEV).manual_seed(11)
+    M, N, K = 602, 128, 20000
+    V = 30000
+    table = _table(V, M, g)
+    with torch.no_grad():
+        table.mul_(torch.pow(10.0, torch.randint(-12, 12, (V, M), device=DEV, generator=g).float()))
+    rows = torch.sort(torch.randperm(V, device=DEV, generator=g)[:K])[0].to(torch.int32)
+    G = torch.randn(K, N, device=DEV, generator=g) * 1e-7
+    C32 = torch.empty(M, N, device=DEV)
+    C3 = torch.empty(M, N, device=DEV)
+    f32.gemm_tn_gather(table, rows, G, C32)
+    s3.gemm_tn_gather(table, rows, G, C3)
+    Xg = table[rows.long()].double()
+    ref = Xg.t() @ G.double()
+    scale = Xg.abs().t() @ G.double().abs() + 1e-300
+    torch.cuda.synchronize()
+    _check(C32, C3, ref, scale)
