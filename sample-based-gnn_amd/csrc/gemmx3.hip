@@ -332,23 +332,23 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
 }
 
 // ---------------------------------------------------------------------------
-// NN: C[M x N] = X[amap[m]][0..K) W (+ relu/dropout): 8-wave blocks, one
-// 128-column block per grid.y; the M rows cut into 16-row tiles, wave gw of
-// the grid owning the contiguous tiles [gw T / W, (gw+1) T / W), two at a time
-// in `rounds` rounds (one count for the grid: a block's waves stay in step
-// over the shared W image).  Per 32-deep k-step g of the (round, k-step)
-// sequence, every operand comes from compiler-visible loads TWO steps ahead:
-//   A: lane (i, q) of row tile rt loads X[id][32 s + 8 q .. +7] (two
-//      dwordx4) into a register ring, splits it one step ahead — late in the
-//      step before its MFMAs, beside them;
-//   W: the pre-split fragment image of step s (k_split3_b: 24 KB, three
-//      dwordx4 per thread) into a register ring, written to the LDS stage
-//      late in the step before (two stages, one barrier per step);
-// and per step each wave runs 8 column tiles x 2 row tiles x 6 MFMAs with the
-// B fragments of column tile ct+1 read while those of ct run.  Each output
-// element's sum is k_gemm3_nn's (same split, same piece order, same k order,
-// same MFMA): the results are bit-identical to gemm3.hip's NN.
-constexpr int kX3NnImg = 8 * 3 * 1024;  // one (step, column block) W image
+// NN: C[M x N] = X[amap[m]][0..K) W (+ relu/dropout): the work split and LDS
+// plan of gemm3.hip's k_gemm3_nn — 8-wave blocks, one 128-column block per
+// grid.y, 16-row tiles, wave gw of the grid owning the contiguous tiles [gw T
+// / W, (gw+1) T / W) two at a time in `rounds` rounds; per 32-deep k-step
+// the W fragment image (k_split3_b, 24 KB: 2 stages) and each wave's 2 x (16
+// rows x 32 floats) A slab (3 stages) by LDS DMA, counted vmcnt, one raw
+// barrier — with every k-step read as a whole (the rows' pad past K is
+// zeroed at the split, so the table's row pitch must cover Kp) and the MFMA
+// loop scheduled slot by slot: per column tile 12 MFMAs (the two row tiles'
+// chains alternating), the next column tile's three B fragment reads in the
+// shadow of the first three.  Each output element's sum is k_gemm3_nn's
+// (same split, same piece order, same k order, same instruction): the
+// results are bit-identical.
+constexpr int kX3NnImg = 8 * 3 * 1024;       // one (step, column block) W image
+constexpr int kX3NnAWave = 2 * 2048;         // one wave's A slab of a step
+constexpr int kX3NnA = 8 * kX3NnAWave;       // one A stage
+constexpr int kX3NnLds = 2 * kX3NnImg + 3 * kX3NnA;  // 48 + 96 KB
 struct X3Epi {
   uint32_t keep_threshold = 0;  // EPI: relu + inverted dropout (common.hpp dropout_*)
   float scale = 1.f;
@@ -357,23 +357,15 @@ struct X3Epi {
 
 typedef float x3f4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ x3f4 x3_mfma6s(const x3bf8 (&a)[3], const x3bf8 (&b)[3], x3f4 acc) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
-  return acc;
-}
-
 template <bool EPI>
 __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, const float* __restrict__ X,
                                                         uint64_t ldx, const uint32_t* __restrict__ amap,
                                                         const char* __restrict__ bimg,
                                                         float* __restrict__ C, uint64_t ldc, int rounds,
                                                         X3Epi ep) {
-  extern __shared__ __attribute__((aligned(16))) char x3nn[];  // [2][kX3NnImg]
+  extern __shared__ __attribute__((aligned(16))) char x3nn[];
+  char* const sb = x3nn;                 // [2][kX3NnImg]
+  char* const sa = x3nn + 2 * kX3NnImg;  // [3][8 waves][2 tiles][2048]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, q = lane >> 4;
@@ -381,141 +373,112 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
   const int T = (M + 15) / 16;
   const int64_t Wn = (int64_t)gridDim.x * 8, gw = (int64_t)blockIdx.x * 8 + wv;
   const int t_lo = (int)(gw * T / Wn), t_hi = (int)((gw + 1) * T / Wn);
-  const int nks = (K + 31) / 32;
-  const int G = rounds * nks;
-  const size_t bstep = (size_t)gridDim.y * kX3NnImg;
-  const char* bsrc = bimg + (size_t)nb * kX3NnImg + 16 * tid;
-  // this lane's two rows of round r (clamped: a missing tile repeats the
-  // wave's last one and is never stored)
-  auto row_ids = [&](int r, uint32_t (&id)[2]) {
+  const int nsteps = (K + 31) / 32;
+  const size_t bstride = (size_t)gridDim.y * kX3NnImg;
+  const uint32_t lsb = x3_lds(sb), lsa = x3_lds(sa);
+  const char* bsrc = bimg + (size_t)nb * kX3NnImg + wv * 1024 + 16 * lane;
+  // A DMA role: lane l loads row (l >> 1) & 15, floats 8 (l >> 5) + 4 (l & 1) (+ 16 h)
+  const int gr = (lane >> 1) & 15, gpo = 8 * (lane >> 5) + 4 * (lane & 1);
+  const float* arow[2];
+  auto set_rows = [&](int rd) {
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
-      const int t = min(t_lo + 2 * r + rt, max(t_hi - 1, t_lo));
-      const int64_t row = min((int64_t)t * 16 + i, (int64_t)M - 1);
-      id[rt] = amap ? amap[row] : (uint32_t)row;
+      const int t = min(t_lo + 2 * rd + rt, T - 1);
+      const int64_t row = (int64_t)t * 16 + gr;
+      const uint64_t rr = (uint64_t)(row < M ? row : M - 1);
+      arow[rt] = X + (amap ? (uint64_t)amap[rr] : rr) * ldx + gpo;
     }
   };
-  float araw[2][2][8];  // [slot][rt][j]: A(g) in slot g & 1
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 wraw[2][3];     // [slot][piece]: W image of step g, 16 B per thread and piece
-  x3bf8 apc[2][2][3];   // [slot][rt][piece]: split A of step g in slot g & 1
-  uint32_t idc[2], idn[2];  // row ids of the current / next round
-  auto load = [&](int g, const uint32_t (&id)[2], auto slot) {
-    constexpr int sl = decltype(slot)::value;  // g & 1
-    const int s = g % nks;
+  auto issue_b = [&](int s) {
+    const uint32_t dst = lsb + (s & 1) * kX3NnImg + wv * 1024;
+    const char* src = bsrc + (size_t)s * bstride;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      const float* p = X + (uint64_t)id[rt] * ldx + 32 * s + 8 * q;
-      typedef float f32x4v __attribute__((ext_vector_type(4)));
-      const f32x4v u = *reinterpret_cast<const f32x4v*>(p);
-      const f32x4v v = *reinterpret_cast<const f32x4v*>(p + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        araw[sl][rt][j] = u[j];
-        araw[sl][rt][4 + j] = v[j];
-      }
-    }
-    const char* b = bsrc + (size_t)s * bstep;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) wraw[sl][p] = *reinterpret_cast<const u32x4*>(b + 8192 * p);
+    for (int p = 0; p < 3; ++p) x3_glds16(src + 8192 * p, dst + 8192 * p);
   };
-  auto split_a = [&](int g, auto slot) {
-    constexpr int sl = decltype(slot)::value;  // g & 1
-    const int s = g % nks;
+  auto issue_a = [&](int s) {
+    const uint32_t dst = lsa + (s % 3) * kX3NnA + wv * kX3NnAWave;
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      float x[8];
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = 32 * s + 8 * q + j < K ? araw[sl][rt][j] : 0.f;  // the pad past K
-      x3_split(x, apc[sl][rt]);
-    }
-  };
-  auto put_w = [&](auto slot) {
-    constexpr int sl = decltype(slot)::value;  // g & 1
-    char* dst = x3nn + sl * kX3NnImg + 16 * tid;
-#pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(dst + 8192 * p) = wraw[sl][p];
+      for (int h = 0; h < 2; ++h) x3_glds16(arow[rt] + 32 * s + 16 * h, dst + rt * 2048 + h * 1024);
   };
   x3f4 acc[2][8];
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));  // this wave's tiles this round
+    set_rows(rd);
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
-  // prologue: W(0) staged, A(0) split, A(1) / W(1) loaded
-  row_ids(0, idc);
-  row_ids(min(1, rounds - 1), idn);
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  load(0, idc, S0());
-  if (G > 1) load(1, nks > 1 ? idc : idn, S1());
-  split_a(0, S0());
-  put_w(S0());
-  // one step: MFMAs of g on the B fragments of stage g & 1 and the pieces of
-  // slot g & 1; loads of g + 2; the split of A(g+1) and the staging of W(g+1)
-  // beside the second half of the MFMAs; the epilogue after a round's last step
-  auto step = [&](int g, auto par) {
-    constexpr int P = decltype(par)::value;  // g & 1
-    const int s = g % nks, r = g / nks;
-    x3_barrier();  // W(g) staged by every wave; stage (g+1) & 1 free
-    if (g + 2 < G) {
-      const int g2 = g + 2, r2 = g2 / nks;
-      if (r2 == r) load(g2, idc, par);
-      else load(g2, idn, par);
-    }
-    const char* img = x3nn + P * kX3NnImg;
-    auto getb = [&](int ct, x3bf8 (&b)[3]) {
+      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+    issue_b(0);
+    issue_a(0);
+    if (nsteps > 1) issue_a(1);
+    for (int s = 0; s < nsteps; ++s) {
+      // B(s) and A(s) landed (A(s+1), issued before B(s)... see the order below)
+      if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      x3_barrier();
+      if (s + 1 < nsteps) issue_b(s + 1);
+      if (s + 2 < nsteps) issue_a(s + 2);
+      // A fragments: lane (i, q) of tile rt holds A[row i][32 s + 8 q .. +7]
+      const char* as = sa + (s % 3) * kX3NnA + wv * kX3NnAWave + 32 * (i + 16 * q);
+      const char* img = sb + (s & 1) * kX3NnImg;
+      auto getb = [&](int ct, int p) {
+        return *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
+      };
+      x3bf8 bf[2][3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
-    };
-    x3bf8 bf[2][3];
-    getb(0, bf[0]);
-#pragma unroll
-    for (int ct = 0; ct < 8; ++ct) {
-      if (ct + 1 < 8) getb(ct + 1, bf[(ct + 1) & 1]);
-      if (ct == 4 && g + 1 < G) {
-        split_a(g + 1, std::integral_constant<int, 1 - P>());
-        put_w(std::integral_constant<int, 1 - P>());
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      acc[0][ct] = x3_mfma6s(apc[P][0], bf[ct & 1], acc[0][ct]);
-      acc[1][ct] = x3_mfma6s(apc[P][1], bf[ct & 1], acc[1][ct]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (s == nks - 1) {  // round r done: store its tiles, start the next round
-      const int nt = min(2, max(0, t_hi - (t_lo + 2 * r)));
+      for (int p = 0; p < 3; ++p) bf[0][p] = getb(0, p);
+      x3bf8 a[2][3];
 #pragma unroll
       for (int rt = 0; rt < 2; ++rt) {
-        if (rt < nt) {
-          const int64_t r4 = (int64_t)(t_lo + 2 * r + rt) * 16 + 4 * q;
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v u = *reinterpret_cast<const f4v*>(as + rt * 2048);
+        const f4v v = *reinterpret_cast<const f4v*>(as + rt * 2048 + 16);
+        float x[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
 #pragma unroll
-          for (int ct = 0; ct < 8; ++ct) {
-            const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
-            float o[4] = {acc[rt][ct][0], acc[rt][ct][1], acc[rt][ct][2], acc[rt][ct][3]};
-            if constexpr (EPI) {
-              const uint4 rnd = dropout_words((uint64_t)r4, col, ep.seed, ep.offset);
-              const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+        for (int j = 0; j < 8; ++j) x[j] = 32 * s + 8 * q + j < K ? x[j] : 0.f;  // the pad past K
+        x3_split(x, a[rt]);
+      }
 #pragma unroll
-              for (int v = 0; v < 4; ++v)
-                o[v] = (dropout_bits(wd[v], col) >= ep.keep_threshold && o[v] > 0.f) ? o[v] * ep.scale : 0.f;
-            }
-            if ((int)col < N) {
+      for (int ct = 0; ct < 8; ++ct) {
 #pragma unroll
-              for (int v = 0; v < 4; ++v)
-                if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
-            }
+        for (int k = 0; k < 12; ++k) {
+          __builtin_amdgcn_sched_barrier(0);
+          {  // slot k: product k / 2 (small first) of row tile k & 1
+            const int rt = k & 1, pr = k >> 1;
+            const int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
+            const int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][pa], bf[ct & 1][pb], acc[rt][ct], 0, 0, 0);
           }
+          if (ct + 1 < 8 && (k == 0 || k == 2 || k == 4)) bf[(ct + 1) & 1][k / 2] = getb(ct + 1, k / 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    x3_barrier();  // every wave is done with the B stages before the next round's
+    // epilogue: acc[rt][ct][v] = C[16 t + 4 q + v][n0 + 16 ct + i]
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      if (rt >= nt) continue;
+      const int64_t r4 = (int64_t)(t_lo + 2 * rd + rt) * 16 + 4 * q;
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) {
+        const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+        if ((int)col >= N) continue;
+        float o[4] = {acc[rt][ct][0], acc[rt][ct][1], acc[rt][ct][2], acc[rt][ct][3]};
+        if constexpr (EPI) {
+          const uint4 rnd = dropout_words((uint64_t)r4, col, ep.seed, ep.offset);
+          const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            o[v] = (dropout_bits(wd[v], col) >= ep.keep_threshold && o[v] > 0.f) ? o[v] * ep.scale : 0.f;
         }
 #pragma unroll
-        for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+        for (int v = 0; v < 4; ++v)
+          if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
       }
-      idc[0] = idn[0];
-      idc[1] = idn[1];
-      if (r + 2 < rounds) row_ids(r + 2, idn);
     }
-  };
-  for (int g = 0; g < G; g += 2) {
-    step(g, std::integral_constant<int, 0>());
-    if (g + 1 < G) step(g + 1, std::integral_constant<int, 1>());
   }
 }
 
@@ -609,25 +572,27 @@ int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint6
   ep.scale = scale;
   ep.seed = seed;
   ep.offset = offset;
+  // one 8-wave block per CU over all column blocks (row blocks a multiple of
+  // 8: the column blocks of the same rows share an XCD), no more blocks than
+  // 16-tile rounds (gemm3.hip's grid)
   const int ncb = (N + 127) / 128;
   const int T = (M + 15) / 16;
-  int gx = std::max(1, 256 / ncb);
-  gx = std::min(gx, (T + 15) / 16);
+  int gx = std::max(8, (256 / ncb) / 8 * 8);
+  gx = std::min(gx, std::max(8, ((T + 15) / 16 + 7) / 8 * 8));
   const int64_t Wn = (int64_t)gx * 8;
   const int max_tiles = (int)((T + Wn - 1) / Wn);
   const int rounds = (max_tiles + 1) / 2;
   const dim3 grid(gx, ncb);
-  const int lds = 2 * kX3NnImg;
   if (epi) {
     NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL(k_x3_nn<true>, grid, dim3(kX3Threads), lds, ctx->stream, M, N, K, A, lda, amap,
-                       bimg, C, ldc, rounds, ep);
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kX3NnLds));
+    hipLaunchKernelGGL(k_x3_nn<true>, grid, dim3(kX3Threads), kX3NnLds, ctx->stream, M, N, K, A, lda,
+                       amap, bimg, C, ldc, rounds, ep);
   } else {
     NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<false>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    hipLaunchKernelGGL(k_x3_nn<false>, grid, dim3(kX3Threads), lds, ctx->stream, M, N, K, A, lda, amap,
-                       bimg, C, ldc, rounds, ep);
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kX3NnLds));
+    hipLaunchKernelGGL(k_x3_nn<false>, grid, dim3(kX3Threads), kX3NnLds, ctx->stream, M, N, K, A, lda,
+                       amap, bimg, C, ldc, rounds, ep);
   }
   NTS_LAUNCH_CHECK();
   return NTS_OK;
