@@ -188,10 +188,12 @@ def parse():
                    help="layer GEMM arithmetic: f32 = fp32-input MFMA; split3 = fp32 operands "
                         "split exactly into three bf16 pieces, six piece products on the bf16 "
                         "MFMA (fp32-accurate, csrc/gemm3.hip)")
-    p.add_argument("--pair-table", type=int, default=3, choices=[0, 1, 2, 3],
+    p.add_argument("--pair-table", type=int, default=0, choices=[0, 1, 2, 3],
                    help="transform-first GEMMs on the feature table's f16 pair table "
-                        "(csrc/gemmh2.hip): 0 off, 1 forward GEMM, 2 forward + weight gradient, "
-                        "3 = 2 with the weight gradient on the whole-row planar kernel")
+                        "(csrc/gemmh2.hip; 22-bit significand inputs, narrower than fp32): 0 off "
+                        "(the fp32-exact split-bf16 kernels, csrc/gemmx3.hip), 1 forward GEMM, "
+                        "2 forward + weight gradient, 3 = 2 with the weight gradient on the "
+                        "whole-row planar kernel")
     p.add_argument("--no-fused-gather", action="store_true")
     p.add_argument("--no-pipeline", action="store_true", help="sample on the training stream")
     p.add_argument("--no-hip-gemm", action="store_true", help="layer GEMMs through torch.matmul")
@@ -242,9 +244,12 @@ def parse():
                    help="train on the first N seeds of this rank's shard only (0: all).  PD "
                         "cache on papers100M-shaped graphs: preSample keeps every "
                         "super-batch's hot ids (~0.7 M per super-batch there)")
+    p.add_argument("--secondary", action="store_true",
+                   help="a secondary measurement's child run (no CPU baseline, epochs, sampler-alone "
+                        "rate, interference probe or secondaries of its own)")
     p.add_argument("--no-secondary-exact", action="store_true",
-                   help="skip the secondary measurement of the headline order with fp32-exact "
-                        "GEMM inputs (split-bf16 on the gathered rows instead of the pair tables)")
+                   help="skip the secondary measurement of the headline order on the f16 pair "
+                        "tables (22-bit inputs) instead of the fp32-exact kernels")
     p.add_argument("--no-secondary-mt", action="store_true",
                    help="skip the secondary measurement with the reference's std::mt19937 stream "
                         "(one rank only)")
@@ -332,7 +337,7 @@ def main():
     if args.train_limit > 0:
         train = train[:args.train_limit]
     log(f"[bench] graph {args.shape}: V={V} E={En} F={F_dim} C={C}  ready in {time.time()-t0:.1f}s")
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline and not args.secondary
     src_host = g.src.cpu().numpy().view(np.uint32) if want_cpu else None
     dst_host = g.dst.cpu().numpy().view(np.uint32) if want_cpu else None
     del g
@@ -425,7 +430,7 @@ def main():
                    for l in drv.last_layers]
     # ---- epoch time (mean of epochs 2..N) ----------------------------
     epoch_times = []
-    for _ in range(max(args.epochs, 0)):
+    for _ in range(0 if args.secondary else max(args.epochs, 0)):
         drv.restart()
         barrier()
         te = time.perf_counter()
@@ -447,6 +452,7 @@ def main():
     # ---- diagnostic: the training stream without the sampler beside it -----------
     alone = None
     if (args.model == "gcn" and not args.no_interference_probe and args.steps > 0
+            and not args.secondary
             and not args.no_pipeline):
         drv.set_diag_reuse_sample(True)
         for _ in range(args.warmup):
@@ -473,7 +479,7 @@ def main():
 
     # ---- GPU sampler alone (SURVEY §8d sampler-only rate) -------------------------
     sampler_only = None
-    if args.sampler_batches > 0 and args.model == "gcn":
+    if args.sampler_batches > 0 and args.model == "gcn" and not args.secondary:
         L = len(fan)
         csr = [not args.atomic_backward] * (L - 1) + [tf]
         wt = {"sum": E.WeightType.Sum, "mean": E.WeightType.Mean,
@@ -485,69 +491,71 @@ def main():
                         "note": "GPU sampler alone on its stream (3 batches in flight), all ranks"}
 
     # ---- secondary orders / arithmetic on the same workload ----------------------
-    def time_secondary(cfg2):
-        drv2 = E.GCN_SAMPLE_ALLGPU_impl(G, feat, labels, train, cfg2, comm)
-
-        def step2():
-            if not drv2.sample_not_finished():
-                drv2.restart()
-            drv2.train_batch()
-
-        for _ in range(args.warmup):
-            step2()
-        drv2.synchronize()
-        drv2.reset_stats()
-        barrier()
-        ta = time.perf_counter()
-        for _ in range(args.steps):
-            step2()
-        drv2.synchronize()
-        barrier()
-        el2 = max_over_ranks(time.perf_counter() - ta)
-        out = {"value": sum_over_ranks(float(drv2.batch_edges)) / el2, "unit": "sampled-edges/s",
-               "ms_per_step": el2 / args.steps * 1e3, "steps": args.steps, "warmup": args.warmup}
-        del drv2
-        return out
+    # Each secondary runs as a fresh CHILD process (`bench.py ... --secondary`,
+    # one rank, nothing else on the GPU: this process is idle and holds no
+    # stream of its own in flight), so that no driver, stream or sampler of
+    # the headline run sits beside it (measured in round 4: the MT secondary
+    # read 5.1 ms/step beside them against 3.9 alone).
+    def child_secondary(extra: list, note: str):
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--secondary",
+               "--shape", args.shape, "--batch", str(args.batch), "--fanout", args.fanout,
+               "--hidden", str(args.hidden), "--weight", args.weight, "--scale", str(args.scale),
+               "--train-limit", str(args.train_limit), "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--gemm", args.gemm, *extra]
+        if args.layers:
+            cmd += ["--layers", args.layers]
+        if args.no_pipeline:
+            cmd.append("--no-pipeline")
+        if args.atomic_backward:
+            cmd.append("--atomic-backward")
+        log(f"[bench] secondary ({note}): {' '.join(cmd[2:])}")
+        t0 = time.time()
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
+        line = None
+        for out in r.stdout.splitlines():
+            try:
+                obj = json.loads(out)
+            except ValueError:
+                continue
+            if isinstance(obj, dict) and "metric" in obj:
+                line = obj
+        if r.returncode != 0 or line is None:
+            return {"error": f"child exited {r.returncode}", "argv": " ".join(cmd[2:])}
+        rl = line.get("roofline") or {}
+        return {"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+                "steps": line["steps"], "warmup": line["warmup"], "dtype": line["dtype"],
+                "bottom_layer": line["config"].get("bottom_layer"),
+                "roofline": {k: rl.get(k) for k in ("kernel", "bound", "achieved", "peak", "unit",
+                                                      "frac", "avg_launch_ms")},
+                "argv": " ".join(cmd[2:]), "child_wall_s": round(time.time() - t0, 1),
+                "measured": "fresh child process, the headline run idle"}
 
     secondary = None  # the reference's bottom-layer order
-    exact_tf = None   # the headline order with fp32-exact GEMM inputs
-    if tf and args.model == "gcn" and args.steps > 0:
+    pair_tf = None    # the headline order on the f16 pair tables (22-bit inputs)
+    mt_ref = None     # the reference's generator stream
+    if (tf and args.model == "gcn" and args.steps > 0 and world == 1 and not args.secondary):
         if not args.no_secondary_af:
             secondary = {
                 "bottom_layer": "aggregate-first (A X) W, the reference's order: fp32 aggregation "
                                 "bit-exact vs MiniBatchFuseOp, split-bf16 GEMMs (fp32-accurate)",
-                **time_secondary(host.gcn_config(
-                    layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
-                    rng_mode=RNG_MODES[args.rng], weight=args.weight,
-                    pipeline=not args.no_pipeline, transform_first=0, gemm=args.gemm,
-                    deterministic_backward=not args.atomic_backward))}
-        if args.pair_table > 0 and not args.no_secondary_exact:
-            exact_tf = {
-                "bottom_layer": "transform-first A (X W) with fp32-exact GEMM inputs: the gathered "
-                                "fp32 feature rows split in the kernel into three bf16 pieces, six "
-                                "products, fp32 accumulate (no pair table)",
-                **time_secondary(host.gcn_config(
-                    layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
-                    rng_mode=RNG_MODES[args.rng], weight=args.weight,
-                    pipeline=not args.no_pipeline, transform_first=1, gemm="split3", pair_table=0,
-                    deterministic_backward=not args.atomic_backward))}
-
+                **child_secondary(["--transform-first", "0", "--pair-table", "0"],
+                                  "the reference's bottom-layer order")}
+        if args.pair_table == 0 and not args.no_secondary_exact:
+            pair_tf = {
+                "bottom_layer": "transform-first A (X W) with the bottom-layer GEMMs on the feature "
+                                "table's f16 pair tables: 22-bit significand inputs (NARROWER than "
+                                "fp32), 3 f16 MFMA products, fp32 accumulate",
+                **child_secondary(["--transform-first", "1", "--pair-table", "3"],
+                                  "f16 pair tables")}
     # the same workload on the reference's own generator stream (std::mt19937
-    # + Lemire, every sampled array bit-exact vs the reference's serial order;
-    # one rank: the SCALE runs keep to the headline).  Measured beside the
-    # headline and secondary drivers' streams: 5.1 ms/step, against 3.8-3.9
-    # for `bench.py --rng mt` on its own
-    mt_ref = None
+    # + Lemire, every sampled array bit-exact vs the reference's serial order)
     if (args.model == "gcn" and args.rng == "philox" and world == 1 and args.steps > 0
-            and not args.no_secondary_mt):
+            and not args.no_secondary_mt and not args.secondary):
         mt_ref = {
             "rng": "std::mt19937(2000) + Lemire, the reference's stream (FastSampler::sample_fast)",
-            **time_secondary(host.gcn_config(
-                layers, fan, args.batch, learn_rate=0.001, weight_decay=1e-4, drop_rate=0.5,
-                rng_mode=RNG_MODES["mt"], weight=args.weight, fused_gather=not args.no_fused_gather,
-                pipeline=not args.no_pipeline, transform_first=args.transform_first,
-                gemm=args.gemm, pair_table=args.pair_table,
-                deterministic_backward=not args.atomic_backward))}
+            **child_secondary(["--rng", "mt", "--transform-first", str(args.transform_first),
+                               "--pair-table", str(args.pair_table)],
+                              "the reference's MT19937 stream")}
 
     value = edges / elapsed
     rl = roofline(prof, args, layers, world)
@@ -563,9 +571,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("fp32 (bottom-layer GEMMs on the feature table's f16 pair tables: 22-bit "
-                  "significand inputs, 3 f16 MFMA products, fp32 accumulate)"
-                  if tf and args.pair_table >= 1 else "fp32"),
+        "dtype": dtype_name(args, tf),
         "data": "synthetic Chung-Lu power-law graph (seed 2024), N(0,1) fp32 features (seed 7), uniform labels",
         "config": {
             "workload": workload_name(args, layers, V, En, tf),
@@ -592,7 +598,7 @@ def main():
                        if tf and args.pair_table >= 1 else ""),
             "layer_sizes_top_down": layer_sizes,
             "reference_order_secondary": secondary,
-            "fp32_exact_inputs_secondary": exact_tf,
+            "pair_table_secondary": pair_tf,
             "reference_stream_secondary": mt_ref,
             "profile_meta": {"argv": " ".join(sys.argv[1:]), "lib_sha256": lib_sha256(),
                              "nts_env": nts_env(),
@@ -610,6 +616,16 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def dtype_name(args, tf) -> str:
+    if tf and args.pair_table >= 1:
+        return ("f16-pair (bottom-layer GEMMs on the feature table's f16 pair tables: 22-bit "
+                "significand inputs, narrower than fp32; 3 f16 MFMA products, fp32 accumulate)")
+    if args.gemm == "split3":
+        return ("fp32 (GEMM inputs fp32, split exactly into three bf16 pieces in the kernels, "
+                "6 bf16 MFMA products, fp32 accumulate; aggregation fp32)")
+    return "fp32"
 
 
 def workload_name(args, layers, V, En, tf) -> str:
@@ -673,6 +689,28 @@ def roofline(prof: dict, args, layers, world) -> dict:
                       "f16_mfma_flops_per_launch": 3.0 * per, "algorithmic_bytes_per_launch": byt,
                       "mfma_frac": k_m["frac"], "hbm_frac": k_h["frac"],
                       "arithmetic": "f16 pair table (3 f16 MFMAs per fp32 product)",
+                      "calls": st["calls"], "share_of_timed_ms": st["ms"]})
+            kernels[name] = k
+            continue
+        if gemm and args.gemm == "split3" and not args.no_hip_gemm:
+            # fp32-exact row-gathered GEMM (csrc/gemmx3.hip): six bf16 MFMA
+            # products per fp32 product against the dense bf16 peak; and its
+            # algorithmic bytes (each gathered fp32 row of Kp floats once, the
+            # other operand's / the output's rows once, W once) against HBM —
+            # the binding roof is reported
+            rows = per / (2.0 * F * N)
+            byt = rows * (4.0 * Kp + 4.0 * N) + 4.0 * Kp * N
+            mf = 6.0 * per / avg_s / 1e12
+            hb = byt / avg_s / 1e9
+            k_m = {"bound": "mfma", "unit": "TFLOP/s", "achieved": mf, "peak": F16_MFMA_PEAK_TF,
+                   "frac": mf / F16_MFMA_PEAK_TF}
+            k_h = {"bound": "hbm", "unit": "GB/s", "achieved": hb, "peak": HBM_PEAK_GBS,
+                   "frac": hb / HBM_PEAK_GBS}
+            k = dict(max(k_m, k_h, key=lambda d: d["frac"]))
+            k.update({"avg_launch_ms": avg_s * 1e3, "flops_per_launch": per,
+                      "bf16_mfma_flops_per_launch": 6.0 * per, "algorithmic_bytes_per_launch": byt,
+                      "mfma_frac": k_m["frac"], "hbm_frac": k_h["frac"],
+                      "arithmetic": "fp32 split into 3 bf16 pieces (6 bf16 MFMAs per fp32 product)",
                       "calls": st["calls"], "share_of_timed_ms": st["ms"]})
             kernels[name] = k
             continue

@@ -591,6 +591,7 @@ __global__ void k_adam(float* __restrict__ W, const float* __restrict__ G, float
   }
 }
 
+#ifdef NTS_WITH_AGG_LDS  // negative result (2.5 TB/s of rows vs 6.7 in registers): variant builds only
 // ---------------------------------------------------------------------------
 // LDS-staged aggregation of 128- and 256-float rows (k_agg_lds): the same sums as
 // k_spmm_gather (per output row, its edges in edge order, acc + x * w with
@@ -938,6 +939,7 @@ __global__ __launch_bounds__(kLdsThreads) void k_agg_lds(
       __hip_atomic_fetch_add(&sh.freed[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 }
+#endif  // NTS_WITH_AGG_LDS
 
 // ---------------------------------------------------------------------------
 // dispatch
@@ -976,13 +978,12 @@ static int plain_vec(uint32_t F, uint64_t ldx, uint64_t ldy, const void* x, cons
   return vec;
 }
 
-static int gather_u_env() {
-  static const int u = [] {
-    const char* e = getenv("NTS_GATHER_U");
-    return e ? atoi(e) : 0;
-  }();
-  return u;
-}
+// compile-time A/B (make variant VFLAGS=-DNTS_GATHER_U=4): 4 rows in flight
+// for the mid-width rows instead of 5
+#ifndef NTS_GATHER_U
+#define NTS_GATHER_U 0
+#endif
+constexpr int gather_u_env() { return NTS_GATHER_U; }
 // rows in flight for the post-mask CSR gather (the hop above a transform-first
 // bottom layer: ~2 edges per row at C2); 0: gather_u's (compile-time A/B)
 #ifndef NTS_AGG_PM_U
@@ -1001,7 +1002,7 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
                              uint32_t nv, float* y, uint64_t ldy, Tier tier, const AggExtra& ax) {
 // rows in flight per lane group: 8 for narrow rows, 5 for mid-width rows
 // (F ~ 600: 3 float4 per lane; fanout 10/25 -> full batches), 4 for the
-// widest (register budget); NTS_GATHER_U=4 forces 4 for the mid-width rows
+// widest (register budget); -DNTS_GATHER_U=4 forces 4 for the mid-width rows
 #define NTS_G(LPD, NCH)                                                                     \
   do {                                                                                      \
     constexpr int u = (MODE == kAggPostMask && kAggPmU > 0) ? kAggPmU : gather_u(VEC * NCH); \
@@ -1033,20 +1034,15 @@ static int launch_gather_vec(hipStream_t st, uint32_t grid, uint32_t last_valid,
 }
 
 // the LDS-staged gather (k_agg_lds) takes 128-float rows gathered by local id
-// (no row map, no host tier, no per-edge mask rows) in 16-byte vectors;
-// opt-in (NTS_AGG_LDS=1) until measured faster than k_spmm_gather
-static bool agg_lds_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("NTS_AGG_LDS");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+// (no row map, no host tier, no per-edge mask rows) in 16-byte vectors; it
+// exists only in variant builds (make variant V=agglds VFLAGS=-DNTS_WITH_AGG_LDS)
+#ifdef NTS_WITH_AGG_LDS
 template <bool MAP, bool TIER, int MODE>
 static bool agg_lds_applies(int vec, uint32_t F) {
-  return !MAP && !TIER && MODE != kAggMask && vec == 4 && agg_lds_enabled() &&
+  return !MAP && !TIER && MODE != kAggMask && vec == 4 &&
          (F == (uint32_t)kLdsF || (F == 2u * kLdsF && MODE != kAggColmax));
 }
+#endif
 
 template <bool MAP, bool TIER = false, int MODE = kAggPlain, bool COOP = false>
 static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* idx,
@@ -1067,6 +1063,7 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
     vec = 4;
   const uint32_t nv = (F + vec - 1) / vec;
   const uint32_t last_valid = F - (nv - 1) * vec;
+#ifdef NTS_WITH_AGG_LDS
   if (agg_lds_applies<MAP, TIER, MODE>(vec, F)) {
     // 128-float rows: the LDS-staged gather (k_agg_lds)
     // rows per part: kLdsR for the column maxima (the parts the TN GEMM reads,
@@ -1090,17 +1087,18 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
+#endif
   const Shape s = pick_shape(nv);
   const uint32_t gpb = kAggThreads / s.lpd;
   // one destination per lane group: every row's dependent loads (offsets ->
   // ids -> rows) are in flight at once; a grid-stride cap (NTS_AGG_GRID)
   // serialises rows per group and measured slower (C2: 1.069 vs 1.097 ms per
-  // step at a 4096-block cap; the narrow CSR backward 50 -> ~25 us)
-  static const uint32_t cap = [] {
-    const char* e = getenv("NTS_AGG_GRID");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (uint32_t)v : (1u << 24);
-  }();
+  // step at a 4096-block cap; the narrow CSR backward 50 -> ~25 us;
+  // compile-time A/B: -DNTS_AGG_GRID=<blocks>)
+#ifndef NTS_AGG_GRID
+#define NTS_AGG_GRID (1u << 24)
+#endif
+  constexpr uint32_t cap = NTS_AGG_GRID;
   // COOP needs one row per lane group
   const uint32_t grid = std::max(1u, COOP ? ceil_div(n_cap, gpb) : std::min(ceil_div(n_cap, gpb), cap));
   // kAggColmax: the per-block buffer was sized for this grid
@@ -1155,7 +1153,9 @@ int nts_hip_spmm_csr_bwd(nts_hip_ctx* ctx, const uint32_t* row_offset,
 uint32_t nts_hip_csr_bwd_colmax_rows_per_part(uint32_t feature_size) {
   if (feature_size == 0) return 0;
   // (the colmax gather always runs on float4 rows: vec 4)
+#ifdef NTS_WITH_AGG_LDS
   if (agg_lds_applies<false, false, kAggColmax>(4, feature_size)) return (uint32_t)kLdsR;
+#endif
   return (uint32_t)(kAggThreads / pick_shape((feature_size + 3) / 4).lpd);
 }
 

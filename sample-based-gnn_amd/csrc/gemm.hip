@@ -928,10 +928,11 @@ int sum_splits(hipStream_t st, const float* part, int splits, uint64_t stride, i
 }
 
 static bool tn_big_ok(int M, int N, const float* B, uint64_t ldb, const GemmExtra& ex, bool bmask) {
-  static const bool narrow = [] {  // RT = 1 for <= 128 output rows (A/B: NTS_TN_NARROW=0)
-    const char* e = getenv("NTS_TN_NARROW");
-    return !(e && e[0] == '0');
-  }();
+  // RT = 1 for <= 128 output rows (compile-time A/B: -DNTS_TN_NARROW=0)
+#ifndef NTS_TN_NARROW
+#define NTS_TN_NARROW 1
+#endif
+  constexpr bool narrow = NTS_TN_NARROW != 0;
   if (!(M >= 320 || (narrow && M <= 128)) || N % 128 != 0 || ldb % 4 != 0 || (uintptr_t)B % 16 != 0)
     return false;
   if (bmask && (ex.ldbx % 4 != 0 || (uintptr_t)ex.bx % 16 != 0)) return false;
@@ -947,20 +948,20 @@ static int launch_tn_big(nts_hip_ctx* ctx, int M, int N, int K, const float* A, 
   const int nrg = (M + (rt1 ? tb_rows<1>() : tb_rows<5>()) - 1) / (rt1 ? tb_rows<1>() : tb_rows<5>());
   const int ncb = N / 128;
   // narrow tiles hold ~55 KB of LDS and ~70 VGPRs: two blocks fit a CU, and
-  // the second doubles the gathered rows in flight (A/B: NTS_TN_NARROW_BLOCKS)
-  static const int narrow_blocks = [] {
-    const char* e = getenv("NTS_TN_NARROW_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 512;
-  }();
+  // the second doubles the gathered rows in flight (A/B: -DNTS_TN_NARROW_BLOCKS=n)
+#ifndef NTS_TN_NARROW_BLOCKS
+#define NTS_TN_NARROW_BLOCKS 512
+#endif
+  constexpr int narrow_blocks = NTS_TN_NARROW_BLOCKS;
   const int target = rt1 ? narrow_blocks : 256;
   int splits = std::max(1, std::min(target / (nrg * ncb), (K + 4 * kTbKS - 1) / (4 * kTbKS)));
   const int kchunk = ((K + splits - 1) / splits + kTbKS - 1) / kTbKS * kTbKS;
   splits = (K + kchunk - 1) / kchunk;
   const dim3 grid(nrg * ncb * splits);
-  static const bool stagger = [] {
-    const char* e = getenv("NTS_TN_STAGGER");
-    return !(e && e[0] == '0');
-  }();
+#ifndef NTS_TN_STAGGER  // compile-time A/B: -DNTS_TN_STAGGER=0
+#define NTS_TN_STAGGER 1
+#endif
+  constexpr bool stagger = NTS_TN_STAGGER != 0;
   const size_t lds = rt1 ? (stagger ? sizeof(TbSmem<3, 1>) : sizeof(TbSmem<2, 1>))
                         : (stagger ? sizeof(TbSmem<3, 5>) : sizeof(TbSmem<2, 5>));
   const bool a4 = lda % 4 == 0 && lda >= (uint64_t)(M + 3) / 4 * 4 && (uintptr_t)A % 16 == 0;
@@ -1046,14 +1047,14 @@ static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const floa
   if (lda % 4 == 0 && (uintptr_t)A % 16 == 0) avec = 4;
   else if (lda % 2 == 0 && (uintptr_t)A % 8 == 0) avec = 2;
   const int vs = (ldc % 4 == 0 && (uintptr_t)C % 16 == 0) ? 1 : 0;
-  static const int depth = [] {
-    const char* e = getenv("NTS_WRES_DEPTH");
-    return e ? std::max(2, std::min(3, atoi(e))) : 2;
-  }();
-  static const bool xtask = [] {
-    const char* e = getenv("NTS_WRES_XT");
-    return !(e && e[0] == '0');
-  }();
+#ifndef NTS_WRES_DEPTH  // compile-time A/B: -DNTS_WRES_DEPTH=3, -DNTS_WRES_XT=0
+#define NTS_WRES_DEPTH 2
+#endif
+#ifndef NTS_WRES_XT
+#define NTS_WRES_XT 1
+#endif
+  constexpr int depth = NTS_WRES_DEPTH;
+  constexpr bool xtask = NTS_WRES_XT != 0;
 #define NTS_WRES_D(NC, AV, D, X)                                                                \
   do {                                                                                          \
     NTS_HIP_TRY(hipFuncSetAttribute(                                                            \
@@ -1083,12 +1084,12 @@ static int launch_wres(hipStream_t st, int ncol, int M, int N, int K, const floa
 
 // Kernel selection (NTS_GEMM_TILED=1 forces the LDS-tiled kernel everywhere,
 // for A/B comparisons).
-static bool force_tiled() {
-  static const bool f = [] {
-    const char* e = getenv("NTS_GEMM_TILED");
-    return e && e[0] == '1';
-  }();
-  return f;
+static bool force_tiled() {  // compile-time A/B: -DNTS_GEMM_TILED=1
+#ifdef NTS_GEMM_TILED
+  return NTS_GEMM_TILED != 0;
+#else
+  return false;
+#endif
 }
 
 // One GEMM: split the reduction when the output grid alone cannot fill the

@@ -715,12 +715,12 @@ bool gemm3_tn_ok(int M, int N, int K) { return M >= 1 && K >= 256 && N % 16 == 0
 // second-generation NN kernel with the same register pipeline as k_s3_tn
 // measured equal to k_gemm3_nn on the gathered shape and slower on the dense
 // one — DESIGN §3 — so NN keeps k_gemm3_nn.)
-static bool use_v1() {
-  static const bool v = [] {
-    const char* e = getenv("NTS_S3_V1");
-    return e && e[0] == '1';
-  }();
-  return v;
+static bool use_v1() {  // compile-time A/B: -DNTS_S3_V1=1
+#ifdef NTS_S3_V1
+  return NTS_S3_V1 != 0;
+#else
+  return false;
+#endif
 }
 
 int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,

@@ -299,13 +299,12 @@ __device__ __forceinline__ void raw_barrier_h() {
 // tiles, k_h2_tn4 k-chunks, k_h2_nnd tiles): 256, or NTS_GEMM_CUS (A/B: a grid
 // below the CU count leaves CUs to the pipelined sampler's blocks instead of
 // waiting for them)
-static int gemm_cus() {
-  static const int n = [] {
-    const char* e = getenv("NTS_GEMM_CUS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 && v <= 256 ? v : 256;
-  }();
-  return n;
+static int gemm_cus() {  // compile-time A/B: -DNTS_GEMM_CUS=n
+#ifdef NTS_GEMM_CUS
+  return NTS_GEMM_CUS > 0 && NTS_GEMM_CUS <= 256 ? NTS_GEMM_CUS : 256;
+#else
+  return 256;
+#endif
 }
 
 struct H2Extra {
@@ -1325,6 +1324,7 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn3(int M, int N, int Kp, const c
 }
 
 
+#ifdef NTS_WITH_H2_NN4
 // NN v4 (k_h2_nn4): k_h2_nn3 with FOUR LDS stages, three 16-row tiles in
 // flight per block instead of two (the 160 KB of LDS hold exactly four
 // 16 x 2560-byte stages; Kp = 608, 19 k-steps): the row ids move to registers (lane t of each wave
@@ -1444,6 +1444,8 @@ __global__ __launch_bounds__(512, 1) void k_h2_nn4(int M, int N, const char* __r
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
   raw_barrier_h();
 }
+
+#endif  // NTS_WITH_H2_NN4
 
 // ---------------------------------------------------------------------------
 // NN with a DYNAMIC fp32 A of at most 128 columns (the aggregate-first layer
@@ -1886,10 +1888,10 @@ static int h2p_tn_gather(nts_hip_ctx* ctx, int M, int N, int K, const uint16_t* 
     return e ? atoi(e) : 0;
   }();
 #endif
-  static const bool rp = [] {  // row-aligned DMA pieces (A/B: NTS_TN4_RP=0)
-    const char* e = getenv("NTS_TN4_RP");
-    return !(e && e[0] == '0');
-  }();
+#ifndef NTS_TN4_RP  // row-aligned DMA pieces (compile-time A/B: -DNTS_TN4_RP=0)
+#define NTS_TN4_RP 1
+#endif
+  constexpr bool rp = NTS_TN4_RP != 0;
 #define NTS_TN4(D, ...)                                                                            \
   do {                                                                                             \
     NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_tn4<TPW, D, ##__VA_ARGS__>), \
@@ -1989,35 +1991,37 @@ extern "C" int nts_hip_gemm_h2p_gather(nts_hip_ctx* ctx, int relu_dropout, int M
 #else
   constexpr int diag = 0;
 #endif
-  // row-aligned LDS-DMA pieces (A/B: NTS_NN3_RP=0 keeps the row-straddling ones)
-  static const bool rp = [] {
-    const char* e = getenv("NTS_NN3_RP");
-    return !(e && e[0] == '0');
-  }();
-  // 16-byte row stores from swapped MFMA operands (NTS_NN3_TR=1; measured:
+  // row-aligned LDS-DMA pieces (compile-time A/B: -DNTS_NN3_RP=0 keeps the
+  // row-straddling ones)
+#ifndef NTS_NN3_RP
+#define NTS_NN3_RP 1
+#endif
+  constexpr bool rp = NTS_NN3_RP != 0;
+  // 16-byte row stores from swapped MFMA operands (-DNTS_NN3_TR=1; measured:
   // alone 174-178 -> 168-170 us, in the C2 bench no gain — off by default)
-  static const bool tr = [] {
-    const char* e = getenv("NTS_NN3_TR");
-    return e && e[0] == '1';
-  }();
+#ifndef NTS_NN3_TR
+#define NTS_NN3_TR 0
+#endif
+  constexpr bool tr = NTS_NN3_TR != 0;
   const bool tr_ok = tr && ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+#ifdef NTS_WITH_H2_NN4
   // four stages (k_h2_nn4) where the table rows carry their scales in a tail
   // (ldq >= 2 Kp + 8 halves: 2560-byte rows) and the step count is compiled
-  // in.  Opt-in (NTS_H2_NN4=1): measured no faster than k_h2_nn3 in the C2
-  // bench (r04d: 152.6 vs ~158 us alone, 164.9 vs 170.9 us pipelined)
-  static const bool nn4 = [] {
-    const char* e = getenv("NTS_H2_NN4");
-    return e && e[0] == '1';
-  }();
-  if (nn4 && !relu_dropout && a_rows && pitch == 2560 && ldq >= 2 * (uint64_t)Kp + 8 && nsteps == 19) {
+  // in.  Variant builds only (make variant V=nn4 VFLAGS=-DNTS_WITH_H2_NN4):
+  // measured no faster than k_h2_nn3 in the C2 bench (r04d: 152.6 vs ~158 us
+  // alone, 164.9 vs 170.9 us pipelined)
+  if (!relu_dropout && a_rows && pitch == 2560 && ldq >= 2 * (uint64_t)Kp + 8 && nsteps == 19) {
     gx = std::max(gx, (T + 63) / 64);  // <= 64 tiles per block (lane-held row ids)
     constexpr int lds4 = 4 * 16 * 2560;
-#define NTS_H2NN4(NK)                                                                                 do {                                                                                                  NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn4<NK>),                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds4));                 hipLaunchKernelGGL((k_h2_nn4<NK>), dim3(gx, ncb), dim3(512), lds4, ctx->stream, M, N,                                    reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), 2 * Kp, bimg, C, ldc, ex);   } while (0)
-    NTS_H2NN4(19);
-#undef NTS_H2NN4
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_h2_nn4<19>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds4));
+    hipLaunchKernelGGL((k_h2_nn4<19>), dim3(gx, ncb), dim3(512), lds4, ctx->stream, M, N,
+                       reinterpret_cast<const char*>(Q), ldq * sizeof(uint16_t), 2 * Kp, bimg, C,
+                       ldc, ex);
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
+#endif
   // compile-time step counts for the feature widths the driver meets
   // (C2: 602 -> Kp 608); NTS_NN3_DIAG=4 forces the runtime-count loop
   if (relu_dropout) {

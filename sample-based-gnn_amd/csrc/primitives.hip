@@ -190,9 +190,10 @@ int scan_exclusive(const T* in, T* out, const uint32_t* n_dev, uint64_t n_cap, T
 // would add an L2 invalidate / write-back per access — buffer_inv sc1 and
 // buffer_wbl2 sc1 — which cost the whole XCD its L2, measured 34 us a call).  The epoch (a per-call
 // sequence number) makes states of earlier calls invalid, so nothing is reset
-// between calls.  A tile only waits on lower-numbered tiles; workgroups are
-// dispatched in index order on each XCD, so the lowest unfinished tile is
-// always resident and the chain completes.
+// between calls.  A workgroup's tile is its dispatch-order ticket (lb_ticket,
+// common.hpp), not blockIdx.x: a tile only waits on lower tiles, and every
+// lower ticket was drawn by a workgroup that is already running, so the chain
+// completes whatever order the dispatcher places workgroups in.
 // COUNT: the input is not read from memory but computed per item as the
 // sampler's per-dst count min(deg(dst[i]), fanout) (init_co_only,
 // core/FullyRepGraph.hpp:530-539), with the omit map of sample_gpu_fast_omit
@@ -418,14 +419,14 @@ __global__ __launch_bounds__(kScanThreads) void k_count_reduce(CountArgs ca,
 
 size_t count_scan_tmp_elems(uint64_t v_cap) { return scan_tmp_elems<uint32_t>(v_cap) + 64; }
 
-// NTS_SCAN1=0: the two-kernel scans for count_scan and the radix histograms
+// -DNTS_SCAN1=0: the two-kernel scans for count_scan and the radix histograms
 // (A/B); default the single-pass look-back scans
-bool scan1_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("NTS_SCAN1");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+bool scan1_enabled() {  // compile-time A/B: -DNTS_SCAN1=0
+#ifdef NTS_SCAN1
+  return NTS_SCAN1 != 0;
+#else
+  return true;
+#endif
 }
 
 int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t stream,

@@ -1808,7 +1808,11 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
     }
   } else {
     const int lem = rng_mode == NTS_RNG_MT19937_LEMIRE ? 1 : 0;
-    static const int mt_dbg = getenv("NTS_MT_DEBUG") ? 1 : 0;
+#ifdef NTS_MT_DEBUG  // (debug builds: -DNTS_MT_DEBUG=1)
+    constexpr int mt_dbg = NTS_MT_DEBUG;
+#else
+    constexpr int mt_dbg = 0;
+#endif
     uint4* info = reinterpret_cast<uint4*>(t_mt);
     // the stream words this layer may read are generated (ahead, on the
     // ring's side stream) before its kernels run

@@ -718,12 +718,12 @@ __global__ __launch_bounds__(256) void k_top_finish(const float* __restrict__ pa
   (void)K;
 }
 
-static bool top_ksplit() {  // A/B: NTS_TOP_KSPLIT=0 runs the per-wave form
-  static const bool on = [] {
-    const char* e = getenv("NTS_TOP_KSPLIT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+static bool top_ksplit() {  // compile-time A/B: -DNTS_TOP_KSPLIT=0 runs the per-wave form
+#ifdef NTS_TOP_KSPLIT
+  return NTS_TOP_KSPLIT != 0;
+#else
+  return true;
+#endif
 }
 
 template <int NCT, bool LOSS, bool GRAD>

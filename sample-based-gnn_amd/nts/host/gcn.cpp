@@ -81,10 +81,12 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
     TORCH_CHECK(tf_ok, "transform_first needs >= 2 layers, the MFMA GEMMs with the fused "
                        "activation, no GAT and no feature cache");
   // auto (-1): transform first where the first layer narrows the rows at
-  // least 4x and its GEMMs run on the f16 pair tables (C2: 602 -> 128,
-  // 0.87 vs 0.99 ms/step); the reference's order elsewhere
+  // least 4x and its GEMMs run on the whole-row fp32-exact kernels
+  // (csrc/gemmx3.hip, split-bf16) or the f16 pair tables (C2: 602 -> 128,
+  // 0.93 vs 1.04 ms/step fp32-exact); the reference's order elsewhere
   tf_ = tf_ok && (cfg.transform_first == 1 ||
-                  (cfg.transform_first < 0 && cfg.pair_table >= 3 &&
+                  (cfg.transform_first < 0 &&
+                   (cfg.pair_table >= 3 || cfg.gemm_mode == NTS_GEMM_SPLIT3) &&
                    cfg.layer_size[0] >= 4 * cfg.layer_size[1]));
   if (tf_ && cfg.pair_table > 0) {
     // the feature table is static: its rows are split into f16 pairs once,

@@ -44,17 +44,19 @@ struct GCNConfig {
   bool early_aggregate = true;        // bottom aggregation issued with the sampling (see issue())
   // bottom layer order: 1 = transform first, A (X W) (rows narrowed before the
   // aggregation), 0 = aggregate first, (A X) W (the reference's order),
-  // -1 = auto: transform first where F_in >= 4 F_out and the pair-table
-  // GEMMs apply (pair_table >= 3), aggregate first elsewhere
+  // -1 = auto: transform first where F_in >= 4 F_out and the split-bf16
+  // (fp32-exact) or pair-table GEMMs apply, aggregate first elsewhere
   int transform_first = -1;
   // layer GEMM arithmetic (nts_hip_ctx_set_gemm_mode): NTS_GEMM_F32 (fp32-input
   // MFMA) or NTS_GEMM_SPLIT3 (fp32-accurate three-piece bf16 split)
   int gemm_mode = NTS_GEMM_SPLIT3;
   // transform-first GEMMs on the feature table's f16 pair table (csrc/gemmh2.hip,
-  // built once at construction): 0 = off (gemm_mode), 1 = the forward GEMM,
-  // 2 = the forward and the weight-gradient GEMMs, 3 = 2 with the weight
-  // gradient on the planar table's whole-row kernel where the shape allows
-  int pair_table = 3;
+  // built once at construction; 22-bit significand inputs, narrower than
+  // fp32: opt-in): 0 = off (gemm_mode: fp32-exact split-bf16), 1 = the
+  // forward GEMM, 2 = the forward and the weight-gradient GEMMs, 3 = 2 with
+  // the weight gradient on the planar table's whole-row kernel where the
+  // shape allows
+  int pair_table = 0;
   // data parallel: the gradient all-reduce of step k runs on a stream of its
   // own and the optimizer step waits for it only where step k+1 first reads
   // W (after its bottom aggregation, which does not depend on W): -1 = on with

@@ -4,7 +4,7 @@ and the backward A^T dZ with rs-scaled column maxima (spmm_csr_bwd_colmax),
 plus the hop-0 forward / post-mask backward — time per call and the rate of
 the gathered rows (every edge's 512-byte row) and of the algorithmic bytes.
 
-  NTS_AGG_LDS=0|1 python scripts/micro_agg.py [--iters 20]
+  python scripts/micro_agg.py [--iters 20]   (NTS_HIP_LIB=scripts/probe/lib_agglds/libnts_hip.so: the k_agg_lds variant, make variant V=agglds VFLAGS=-DNTS_WITH_AGG_LDS)
 """
 import argparse
 import json

@@ -51,6 +51,24 @@ def test_roofline_dominant_kernel_and_units(bench, monkeypatch):
     assert g["bound"] == "hbm" and g["frac"] == pytest.approx(max(g["mfma_frac"], g["hbm_frac"]))
 
 
+def test_roofline_split3_gather_gemm_dual_roof(bench, monkeypatch):
+    """fp32-exact gathered GEMM (csrc/gemmx3.hip): six bf16 MFMA products per
+    fp32 product against the dense bf16 peak, its algorithmic bytes against
+    HBM; the larger fraction is the reported bound; the dtype says fp32."""
+    monkeypatch.setattr(bench, "attach_pmc", lambda *a, **k: None)
+    prof = {"gather_gemm_tn": {"ms": 4.0, "calls": 20, "units": 20 * 35e9}}
+    rl = bench.roofline(prof, _args(), [602, 128, 41], 1)
+    g = rl["kernels"]["gather_gemm_tn"]
+    rows = 35e9 / (2 * 602 * 128)
+    assert g["bf16_mfma_flops_per_launch"] == pytest.approx(6 * 35e9)
+    assert g["algorithmic_bytes_per_launch"] == pytest.approx(rows * (4 * 608 + 4 * 128) + 4 * 608 * 128)
+    assert g["mfma_frac"] == pytest.approx(6 * 35e9 / 0.2e-3 / 1e12 / bench.F16_MFMA_PEAK_TF)
+    assert g["frac"] == pytest.approx(max(g["mfma_frac"], g["hbm_frac"]))
+    assert rl["kernel"] == "gather_gemm_tn"
+    assert bench.dtype_name(_args(), True).startswith("fp32 ")
+    assert "narrower than fp32" in bench.dtype_name(_args(pair_table=3), True)
+
+
 def test_pmc_attached_only_for_the_same_build_and_workload(bench, monkeypatch, tmp_path):
     (tmp_path / "profiles").mkdir()
     monkeypatch.setattr(bench, "ROOT", tmp_path)
@@ -127,3 +145,17 @@ def test_nts_env_is_recorded(bench, monkeypatch):
     monkeypatch.setenv("NTS_SCAN1", "0")
     assert bench.nts_env()["NTS_SCAN1"] == "0"
     assert bench.diag_env() == []
+
+
+def test_product_library_env_knobs():
+    """The product library reads at most these environment variables (the
+    A/B variants are compile-time flags of `make variant`, the timing probes
+    exist only in `make probe`): a debugging aid for hangs and the two
+    MT19937 walker selections the kernel tests A/B."""
+    import re
+    lib = ROOT / "sample-based-gnn_amd" / "nts" / "lib" / "libnts_hip.so"
+    if not lib.exists():
+        pytest.skip("libnts_hip.so not built")
+    names = set(m.group(1).decode() for m in re.finditer(rb"\x00(NTS_[A-Z0-9_]+)\x00", lib.read_bytes()))
+    assert names <= {"NTS_LAUNCH_TRACE", "NTS_MT_SERIAL", "NTS_MT_CHUNKED"}, names
+    assert len(names) <= 10
