@@ -357,7 +357,10 @@ struct X3Epi {
 
 typedef float x3f4 __attribute__((ext_vector_type(4)));
 
-template <bool EPI>
+// DIAG (timing probes, NTS_X3_DIAG in the probe build only; results are
+// garbage): 1 no MFMAs, 2 no A splits, 4 no DMA after each round's first
+// steps, 8 no B fragment reads
+template <bool EPI, int DIAG = 0>
 __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, const float* __restrict__ X,
                                                         uint64_t ldx, const uint32_t* __restrict__ amap,
                                                         const char* __restrict__ bimg,
@@ -390,12 +393,14 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     }
   };
   auto issue_b = [&](int s) {
+    if ((DIAG & 4) && s >= 2) return;
     const uint32_t dst = lsb + (s & 1) * kX3NnImg + wv * 1024;
     const char* src = bsrc + (size_t)s * bstride;
 #pragma unroll
     for (int p = 0; p < 3; ++p) x3_glds16(src + 8192 * p, dst + 8192 * p);
   };
   auto issue_a = [&](int s) {
+    if ((DIAG & 4) && s >= 2) return;
     const uint32_t dst = lsa + (s % 3) * kX3NnA + wv * kX3NnAWave;
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
@@ -415,7 +420,7 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     if (nsteps > 1) issue_a(1);
     for (int s = 0; s < nsteps; ++s) {
       // B(s) and A(s) landed (A(s+1), issued before B(s)... see the order below)
-      if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (s + 1 < nsteps && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       x3_barrier();
       if (s + 1 < nsteps) issue_b(s + 1);
@@ -424,7 +429,8 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
       const char* as = sa + (s % 3) * kX3NnA + wv * kX3NnAWave + 32 * (i + 16 * q);
       const char* img = sb + (s & 1) * kX3NnImg;
       auto getb = [&](int ct, int p) {
-        return *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
+        if constexpr (DIAG & 8) return x3bf8{};
+        else return *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
       };
       x3bf8 bf[2][3];
 #pragma unroll
@@ -438,7 +444,14 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
         float x[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = 32 * s + 8 * q + j < K ? x[j] : 0.f;  // the pad past K
-        x3_split(x, a[rt]);
+        if constexpr (DIAG & 2) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[rt][p][j] = __builtin_bit_cast(__bf16, (short)__float_as_uint(x[j]));
+        } else {
+          x3_split(x, a[rt]);
+        }
       }
 #pragma unroll
       for (int ct = 0; ct < 8; ++ct) {
@@ -449,7 +462,11 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
             const int rt = k & 1, pr = k >> 1;
             const int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
             const int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
-            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][pa], bf[ct & 1][pb], acc[rt][ct], 0, 0, 0);
+            if constexpr (DIAG & 1) acc[rt][ct][0] += (float)a[rt][pa][0] + (float)bf[ct & 1][pb][1];
+            else if constexpr (EPI)
+              acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][pa], bf[ct & 1][pb], acc[rt][ct], 0, 0, 0);
+            else  // C^T = W^T X^T: the same fragments, operands swapped
+              acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ct & 1][pb], a[rt][pa], acc[rt][ct], 0, 0, 0);
           }
           if (ct + 1 < 8 && (k == 0 || k == 2 || k == 4)) bf[(ct + 1) & 1][k / 2] = getb(ct + 1, k / 2);
         }
@@ -457,6 +474,28 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
       }
     }
     x3_barrier();  // every wave is done with the B stages before the next round's
+    if constexpr (!EPI) {
+      // transposed accumulators: acc[rt][ct][v] = C[16 t + i][n0 + 16 ct + 4 q + v],
+      // one 16-byte store per tile and lane
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        if (rt >= nt) continue;
+        const int64_t row = (int64_t)(t_lo + 2 * rd + rt) * 16 + i;
+        if (row >= M) continue;
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) {
+          const int col = n0 + 16 * ct + 4 * q;
+          if (col >= N) continue;
+          float* dst = C + (uint64_t)row * ldc + col;
+          if (ldc % 4 == 0 && (uintptr_t)C % 16 == 0)
+            *reinterpret_cast<x3f4*>(dst) = acc[rt][ct];
+          else
+#pragma unroll
+            for (int v = 0; v < 4; ++v) dst[v] = acc[rt][ct][v];
+        }
+      }
+      continue;
+    }
     // epilogue: acc[rt][ct][v] = C[16 t + 4 q + v][n0 + 16 ct + i]
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt) {
@@ -583,17 +622,34 @@ int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint6
   const int max_tiles = (int)((T + Wn - 1) / Wn);
   const int rounds = (max_tiles + 1) / 2;
   const dim3 grid(gx, ncb);
-  if (epi) {
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kX3NnLds));
-    hipLaunchKernelGGL(k_x3_nn<true>, grid, dim3(kX3Threads), kX3NnLds, ctx->stream, M, N, K, A, lda,
-                       amap, bimg, C, ldc, rounds, ep);
-  } else {
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<false>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, kX3NnLds));
-    hipLaunchKernelGGL(k_x3_nn<false>, grid, dim3(kX3Threads), kX3NnLds, ctx->stream, M, N, K, A, lda,
-                       amap, bimg, C, ldc, rounds, ep);
-  }
+#define NTS_X3NN(E, D)                                                                            \
+  do {                                                                                            \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn<E, D>),                \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kX3NnLds));       \
+    hipLaunchKernelGGL((k_x3_nn<E, D>), grid, dim3(kX3Threads), kX3NnLds, ctx->stream, M, N, K, A, \
+                       lda, amap, bimg, C, ldc, rounds, ep);                                      \
+  } while (0)
+#ifdef NTS_PROBE_BUILD
+  static const int diag = [] {
+    const char* e = getenv("NTS_X3_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  if (!epi && diag) {
+    switch (diag) {
+      case 1: NTS_X3NN(false, 1); break;
+      case 2: NTS_X3NN(false, 2); break;
+      case 4: NTS_X3NN(false, 4); break;
+      case 6: NTS_X3NN(false, 6); break;
+      case 8: NTS_X3NN(false, 8); break;
+      case 12: NTS_X3NN(false, 12); break;
+      case 14: NTS_X3NN(false, 14); break;
+      default: NTS_X3NN(false, 5); break;
+    }
+  } else
+#endif
+  if (epi) NTS_X3NN(true, 0);
+  else NTS_X3NN(false, 0);
+#undef NTS_X3NN
   NTS_LAUNCH_CHECK();
   return NTS_OK;
 }
