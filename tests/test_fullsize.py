@@ -264,6 +264,34 @@ def test_c3_products_shaped_three_layers_mean(E):
     _free()
 
 
+def test_c3_mt19937_three_layers(E):
+    """C3's sampling (products-shaped, 15-10-5, batch 1,024) on the
+    reference's own generator stream: every array of the three layers
+    bit-exact vs the oracle's std::mt19937(2000) walk in draw order and the
+    generator state identical after each of two batches."""
+    from nts import synthetic
+    g, F, C = synthetic.shaped("products", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    fan, B = [15, 10, 5], 1024
+    perm = np.random.default_rng(16).permutation(V).astype(np.int32)[:2 * B]
+    fs = E.FastSampler(G, torch.from_numpy(perm), 3, B, fan, rng_mode=1, seed=2000)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    od, idg = _np(G.out_degree), _np(G.in_degree)
+    o = orc.Sampler(col, rows, idg, od, fan, seed=2000, rng_mode=orc.RNG_MT_LEMIRE,
+                    order_mode=orc.ORDER_DRAW)
+    for b in range(2):
+        got = fs.sample_gpu_fast(B, E.WeightType.Mean)
+        _properties(G, got, fan, V)
+        ref = o.sample(perm[b * B:(b + 1) * B].view(np.uint32), b, orc.W_MEAN)
+        _compare_oracle(got, ref)
+        assert np.array_equal(_np(fs.rng_state()), o.mt_state()), f"generator state, batch {b}"
+    del fs, got, G
+    _free()
+
+
 def test_c4_products_shaped_two_layer_gcn(E):
     """C4's per-GPU workload (GCN_SAMPLE_ALL_MULTI, products-shaped, 100-256-47,
     fanout 25-10, B=1,024 per GPU): the sampled batch bit-exact vs the

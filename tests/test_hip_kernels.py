@@ -158,6 +158,38 @@ def test_sampler_mt19937_is_reference_stream(hip, cora, fanouts, walker, monkeyp
     assert np.array_equal(hip.rng_state().numpy().view(np.uint32), o_draw.mt_state())
 
 
+def _regular_graph(V, d, seed):
+    """Every vertex with exactly d distinct in-neighbours."""
+    rng = np.random.default_rng(seed)
+    src = np.concatenate([rng.choice(V, d, replace=False) for _ in range(V)]).astype(np.uint32)
+    dst = np.repeat(np.arange(V, dtype=np.uint32), d)
+    return V, src, dst
+
+
+@pytest.mark.parametrize("walker", ["serial", "chunked"])
+@pytest.mark.parametrize("deg,fanouts", [(26, (25, 25)), (11, (10, 10))])
+def test_sampler_mt19937_coupon_collector(hip, deg, fanouts, walker, monkeypatch):
+    """Every degree = fanout + 1, the worst case of the rejection draws (about
+    3x the words of the sampled edges at fanout 25: the coupon collector):
+    the stream generated for each layer covers it — arrays bit-exact vs the
+    oracle's std::mt19937(2000) walk and the generator state identical after
+    every batch (core/ntsFastSampler.hpp:200-205,1020-1054)."""
+    monkeypatch.setenv("NTS_MT_SERIAL" if walker == "serial" else "NTS_MT_CHUNKED", "1")
+    V, src, dst = _regular_graph(30_000, deg, 4)
+    g = _graph(hip, V, src, dst)
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    rng = np.random.default_rng(2)
+    hip.rng_seed(2000)
+    o = orc.Sampler(col, rows, in_d, out_d, list(fanouts), seed=2000,
+                    rng_mode=orc.RNG_MT_LEMIRE, order_mode=orc.ORDER_DRAW)
+    for bs in range(2):
+        seeds = rng.choice(V, 2048, replace=False).astype(np.uint32)
+        gl = [_gpu_layer_np(l) for l in _sample_gpu(hip, g, seeds, list(fanouts), 1, bs)]
+        _assert_layers_equal(gl, o.sample(seeds, bs))
+        assert np.array_equal(hip.rng_state().numpy().view(np.uint32), o.mt_state()), bs
+
+
 def test_sampler_mt19937_div_mode(hip, cora):
     V, src, dst = cora
     g = _graph(hip, V, src, dst)
