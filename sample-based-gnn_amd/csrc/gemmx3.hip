@@ -342,7 +342,10 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
 // zeroed at the split, so the table's row pitch must cover Kp) and the MFMA
 // loop scheduled slot by slot: per column tile 12 MFMAs (the two row tiles'
 // chains alternating), the next column tile's three B fragment reads in the
-// shadow of the first three.  Each output element's sum is k_gemm3_nn's
+// shadow of the first three.  The A slab is wave-private, so the next step's
+// fragments are read and split during the current step (a mid-step wait for
+// its 4 pieces at column tile 4, split pairs in tiles 5-6, two register sets
+// by step parity): 267 vs 273 us at C2 on one box (scripts/r05_q.sh).  Each output element's sum is k_gemm3_nn's
 // (same split, same piece order, same k order, same instruction): the
 // results are bit-identical.
 constexpr int kX3NnImg = 8 * 3 * 1024;       // one (step, column block) W image
@@ -408,6 +411,89 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
       for (int h = 0; h < 2; ++h) x3_glds16(arow[rt] + 32 * s + 16 * h, dst + rt * 2048 + h * 1024);
   };
   x3f4 acc[2][8];
+  float xr[2][8];           // raw A fragments (one step, per row tile)
+  uint32_t ap[2][2][3][4];  // split A pieces: [step parity][row tile][piece][pair]
+  // A(s) fragments: lane (i, q) of tile rt holds A[row i][32 s + 8 q .. +7]
+  // (this wave's own slab: only its own DMA count guards it, no barrier)
+  auto read_a = [&](int s, int rt) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const char* as = sa + (s % 3) * kX3NnA + wv * kX3NnAWave + 32 * (i + 16 * q) + rt * 2048;
+    const f4v u = *reinterpret_cast<const f4v*>(as);
+    const f4v v = *reinterpret_cast<const f4v*>(as + 16);
+    const float x[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xr[rt][j] = x[j];
+    if (32 * s + 32 > K) {  // the pad past K (the last step only: a uniform branch)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xr[rt][j] = 32 * s + 8 * q + j < K ? x[j] : 0.f;
+    }
+  };
+  auto split_a = [&](auto par, int rt, int jp) {
+    constexpr int P = decltype(par)::value;
+    if constexpr (DIAG & 2) {
+      ap[P][rt][0][jp] = ap[P][rt][1][jp] = ap[P][rt][2][jp] = __float_as_uint(xr[rt][2 * jp]);
+    } else {
+      x3_split2(xr[rt][2 * jp], xr[rt][2 * jp + 1], ap[P][rt][0][jp], ap[P][rt][1][jp], ap[P][rt][2][jp]);
+    }
+  };
+  // one k-step on the split A(s) in ap[P]; A(s+1) is read and split into
+  // ap[1-P] in the second half of the column tiles, after a mid-step wait for
+  // its 4 pieces (younger in flight: B(s+1)'s 3 and A(s+2)'s 4)
+  auto step = [&](int s, auto par) {
+    constexpr int P = decltype(par)::value;
+    if (s > 0) {
+      // B(s) landed (A(s) was waited for in step s-1; A(s+1)'s 4 pieces may stay in flight)
+      if (s + 1 < nsteps && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      x3_barrier();
+      if (s + 1 < nsteps) issue_b(s + 1);
+      if (s + 2 < nsteps) issue_a(s + 2);
+    }
+    const bool nxt2 = s + 2 < nsteps;
+    const char* img = sb + (s & 1) * kX3NnImg;
+    auto getb = [&](int ct, int p) {
+      if constexpr (DIAG & 8) return x3bf8{};
+      else return *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
+    };
+    x3bf8 bf[2][3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) bf[0][p] = getb(0, p);
+    x3bf8 a[2][3];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[rt][p] = __builtin_bit_cast(x3bf8, (x3u4){ap[P][rt][p][0], ap[P][rt][p][1], ap[P][rt][p][2], ap[P][rt][p][3]});
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        __builtin_amdgcn_sched_barrier(0);
+        {  // slot k: product k / 2 (small first) of row tile k & 1
+          const int rt = k & 1, pr = k >> 1;
+          const int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
+          const int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
+          if constexpr (DIAG & 1) acc[rt][ct][0] += (float)a[rt][pa][0] + (float)bf[ct & 1][pb][1];
+          else if constexpr (EPI)
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][pa], bf[ct & 1][pb], acc[rt][ct], 0, 0, 0);
+          else  // C^T = W^T X^T: the same fragments, operands swapped
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ct & 1][pb], a[rt][pa], acc[rt][ct], 0, 0, 0);
+        }
+        if (ct + 1 < 8 && (k == 0 || k == 2 || k == 4)) bf[(ct + 1) & 1][k / 2] = getb(ct + 1, k / 2);
+        // (unconditional: past the round's last step this reads and splits a
+        // stale stage nobody uses, cheaper than branching every slot)
+        if (ct == 4 && k == 0) {
+          if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          else if (nxt2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        }
+        if (ct == 4 && k == 1) read_a(s + 1, 0);
+        if (ct == 4 && k == 3) read_a(s + 1, 1);
+        if ((ct == 5 || ct == 6) && k % 3 == 1) split_a(std::integral_constant<int, 1 - P>{}, ct - 5, k / 3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   for (int rd = 0; rd < rounds; ++rd) {
     const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));  // this wave's tiles this round
     set_rows(rd);
@@ -418,60 +504,21 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     issue_b(0);
     issue_a(0);
     if (nsteps > 1) issue_a(1);
-    for (int s = 0; s < nsteps; ++s) {
-      // B(s) and A(s) landed (A(s+1), issued before B(s)... see the order below)
-      if (s + 1 < nsteps && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      x3_barrier();
-      if (s + 1 < nsteps) issue_b(s + 1);
-      if (s + 2 < nsteps) issue_a(s + 2);
-      // A fragments: lane (i, q) of tile rt holds A[row i][32 s + 8 q .. +7]
-      const char* as = sa + (s % 3) * kX3NnA + wv * kX3NnAWave + 32 * (i + 16 * q);
-      const char* img = sb + (s & 1) * kX3NnImg;
-      auto getb = [&](int ct, int p) {
-        if constexpr (DIAG & 8) return x3bf8{};
-        else return *reinterpret_cast<const x3bf8*>(img + ct * 3072 + p * 1024 + 16 * lane);
-      };
-      x3bf8 bf[2][3];
+    // B(0) and A(0) landed (the 4 pieces of A(1) may stay in flight)
+    if (nsteps > 1 && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    x3_barrier();
+    if (nsteps > 1) issue_b(1);
+    if (nsteps > 2) issue_a(2);
+    read_a(0, 0);
+    read_a(0, 1);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bf[0][p] = getb(0, p);
-      x3bf8 a[2][3];
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v u = *reinterpret_cast<const f4v*>(as + rt * 2048);
-        const f4v v = *reinterpret_cast<const f4v*>(as + rt * 2048 + 16);
-        float x[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = 32 * s + 8 * q + j < K ? x[j] : 0.f;  // the pad past K
-        if constexpr (DIAG & 2) {
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) a[rt][p][j] = __builtin_bit_cast(__bf16, (short)__float_as_uint(x[j]));
-        } else {
-          x3_split(x, a[rt]);
-        }
-      }
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-          __builtin_amdgcn_sched_barrier(0);
-          {  // slot k: product k / 2 (small first) of row tile k & 1
-            const int rt = k & 1, pr = k >> 1;
-            const int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
-            const int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
-            if constexpr (DIAG & 1) acc[rt][ct][0] += (float)a[rt][pa][0] + (float)bf[ct & 1][pb][1];
-            else if constexpr (EPI)
-              acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rt][pa], bf[ct & 1][pb], acc[rt][ct], 0, 0, 0);
-            else  // C^T = W^T X^T: the same fragments, operands swapped
-              acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[ct & 1][pb], a[rt][pa], acc[rt][ct], 0, 0, 0);
-          }
-          if (ct + 1 < 8 && (k == 0 || k == 2 || k == 4)) bf[(ct + 1) & 1][k / 2] = getb(ct + 1, k / 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      for (int jp = 0; jp < 4; ++jp) split_a(std::integral_constant<int, 0>{}, rt, jp);
+    for (int s = 0; s < nsteps; s += 2) {
+      step(s, std::integral_constant<int, 0>{});
+      if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
     }
     x3_barrier();  // every wave is done with the B stages before the next round's
     if constexpr (!EPI) {
