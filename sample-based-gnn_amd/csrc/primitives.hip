@@ -470,8 +470,11 @@ template size_t scan_tmp_elems<uint64_t>(uint64_t);
 
 // ============================================================================
 // stable LSD radix sort: D-bit digits (D <= 9, passes = ceil(bits / 9)),
-// 4096-item tiles.  Per pass: per-tile digit counts (digit-major), one
-// exclusive scan over them, then a scatter in which each wave ranks its 1,024
+// 4096-item tiles.  Per pass: per-tile digit counts (digit-major, row stride
+// nb = the capacity's tile count), a scan of each digit's row over the live
+// tiles (one workgroup per digit, the row totals to `totals`), then a scatter
+// that adds the digits' exclusive prefix over the totals (scanned per
+// workgroup in LDS) and in which each wave ranks its 1,024
 // contiguous items against a running per-wave digit count in LDS (match-any by
 // ballots, no barrier inside the item loop), the tile is reordered by digit in
 // LDS and written out in runs (coalesced stores).
@@ -489,29 +492,75 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
   __syncthreads();
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
-  if (base < n) {
+  if (base >= n) return;  // past the end: k_radix_rowscan reads only the tiles below n
 #pragma unroll
-    for (int k = 0; k < kRadixItems; ++k) {
-      const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
-      if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
-    }
+  for (int k = 0; k < kRadixItems; ++k) {
+    const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
   }
   __syncthreads();
   for (uint32_t d = t; d < bins; d += kRadixThreads) hist[(uint64_t)d * nb + blockIdx.x] = h[d];
+}
+
+// digit d = blockIdx.x: exclusive scan of hist[d nb .. d nb + live tiles) in
+// place, its total to totals[d].  Replaces a device-wide scan of the whole
+// bins x nb array (sized by the capacity, most of it zeros past n): no tile
+// waits on another, and the grid is the digit count, not the capacity.
+__global__ __launch_bounds__(kRadixThreads) void k_radix_rowscan(uint32_t* __restrict__ hist,
+                                                                 const uint32_t* n_dev, uint64_t n_cap,
+                                                                 uint32_t nb, uint32_t* __restrict__ totals) {
+  __shared__ uint32_t wsum[kRadixThreads / kWave];
+  const int t = threadIdx.x;
+  const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
+  const uint32_t live = (uint32_t)((n + kRadixTile - 1) / kRadixTile);  // <= nb
+  uint32_t* row = hist + (uint64_t)blockIdx.x * nb;
+  constexpr int kPer = 4;  // consecutive entries per thread
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < live; c0 += kRadixThreads * kPer) {
+    uint32_t v[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t j = c0 + t * kPer + k;
+      v[k] = j < live ? row[j] : 0u;
+      sum += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = carry + block_excl_scan(sum, wsum, &tot);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t j = c0 + t * kPer + k;
+      if (j < live) row[j] = run;
+      run += v[k];
+    }
+    carry += tot;
+    __syncthreads();  // wsum is reused by the next chunk
+  }
+  if (t == 0) totals[blockIdx.x] = carry;
 }
 
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* n_dev,
     uint64_t n_cap, uint32_t shift, uint32_t dbits, const uint32_t* __restrict__ hist,
-    uint32_t nb) {
+    uint32_t nb, const uint32_t* __restrict__ totals) {
   __shared__ RadixTileLds sm;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   if ((uint64_t)blockIdx.x * kRadixTile >= n) return;  // whole tile past the end
   const uint32_t bins = 1u << dbits;
+  {  // the digits' starts: exclusive scan of the row totals (thread t: digits 2t, 2t + 1)
+    static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");
+    const int t = threadIdx.x;
+    const uint32_t c0 = 2u * t < bins ? totals[2 * t] : 0u;
+    const uint32_t c1 = 2u * t + 1 < bins ? totals[2 * t + 1] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(c0 + c1, sm.wsum, &tot);
+    if (2u * t < bins) sm.gstart[2 * t] = ex;
+    if (2u * t + 1 < bins) sm.gstart[2 * t + 1] = ex + c0;
+    // (radix_tile_order's first barrier orders these before the reads below)
+  }
   radix_tile_order(sm, keys_in, vals_in, n, shift, dbits, [](uint32_t, uint32_t) {}, [&] {
     for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
-      sm.gstart[d] = hist[(uint64_t)d * nb + blockIdx.x];
+      sm.gstart[d] += hist[(uint64_t)d * nb + blockIdx.x];
   });
   const uint32_t cnt = radix_tile_count(n), mask = (1u << dbits) - 1u;
   for (uint32_t i = threadIdx.x; i < cnt; i += kRadixThreads) {
@@ -525,14 +574,14 @@ size_t radix_tmp_bytes(uint64_t n_cap) {
   uint64_t nb = (n_cap + kRadixTile - 1) / kRadixTile;
   if (nb == 0) nb = 1;
   size_t hist = (size_t)kRadixMaxBins * nb + 1;
-  size_t elems = 2 * ((n_cap + 63) / 64 * 64) + (hist + 63) / 64 * 64 +
-                 scan_tmp_elems<uint32_t>(kRadixMaxBins * nb) + 64;
+  size_t elems = 2 * ((n_cap + 63) / 64 * 64) + (hist + 63) / 64 * 64 + kRadixMaxBins + 64;
   return elems * sizeof(uint32_t);
 }
 
 int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t bits,
                      void* tmp, hipStream_t stream, nts_hip_ctx* ctx) {
+  (void)ctx;  // (the device-wide look-back scan's state lived there)
   if (n_cap == 0) return NTS_OK;
   uint32_t nb = ceil_div(n_cap, kRadixTile);
   uint64_t n_al = (n_cap + 63) / 64 * 64;
@@ -543,8 +592,7 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
   const int npass = (int)((bits + kRadixMaxBits - 1) / kRadixMaxBits);
   const uint32_t dbits = (bits + npass - 1) / npass;
   const uint32_t mask = (1u << dbits) - 1u;
-  const uint64_t hist_n = (uint64_t)(mask + 1) * nb;
-  uint32_t* stmp = hist + ((uint64_t)kRadixMaxBins * nb + 1 + 63) / 64 * 64;
+  uint32_t* totals = hist + ((uint64_t)kRadixMaxBins * nb + 1 + 63) / 64 * 64;
   const uint32_t* ksrc = keys_in;
   const uint32_t* vsrc = vals_in;
   for (int p = 0; p < npass; ++p) {
@@ -555,12 +603,12 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
     hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev,
                        n_cap, shift, mask, hist, nb);
     NTS_LAUNCH_CHECK();
-    if (ctx && scan1_enabled())  // one kernel (single-pass look-back scan)
-      NTS_RET(scan1_exclusive(ctx, hist, hist, nullptr, hist_n, stream));
-    else
-      NTS_RET(scan_exclusive<uint32_t>(hist, hist, nullptr, hist_n, stmp, stream));
+    hipLaunchKernelGGL(k_radix_rowscan, dim3(mask + 1), dim3(kRadixThreads), 0, stream, hist, n_dev,
+                       n_cap, nb, totals);
+    NTS_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc,
-                       kdst, vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb);
+                       kdst, vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb,
+                       (const uint32_t*)totals);
     NTS_LAUNCH_CHECK();
     ksrc = kdst;
     vsrc = vdst;
