@@ -728,7 +728,9 @@ def roofline(prof: dict, args, layers, world) -> dict:
     k = kernels[dom]
     rl = {"bound": k["bound"], "kernel": dom, "achieved": k["achieved"], "peak": k["peak"],
           "unit": k["unit"], "frac": k["frac"], "traffic": None,
-          "avg_launch_ms": k["avg_launch_ms"], "kernels": kernels}
+          "avg_launch_ms": k["avg_launch_ms"], "kernels": kernels,
+          "timing": ("HIP events on the launching stream over the timed steps, one kernel "
+                     "class per step in rotation (KernelProfiler, nts_host.hpp)")}
     attach_pmc(rl, dom, args, layers, world)
     return rl
 

@@ -552,6 +552,7 @@ void GCN_SAMPLE_ALLGPU_impl::flush_update() {
 float GCN_SAMPLE_ALLGPU_impl::train_batch() {
   auto guard = cs->guard();
   double t0 = now_s();
+  if (cfg.profile) prof.next_step();  // (one kernel class timed per step)
   NtsStream& sst = ss ? *ss : *cs;
   // set_diag_reuse_sample (diagnostic only, not a valid measurement): sample
   // once and train every step on that batch — the training stream's time

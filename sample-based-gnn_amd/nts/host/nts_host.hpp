@@ -400,6 +400,10 @@ NtsVar hip_linear_act(const NtsVar& x, const NtsVar& W, double p, uint64_t seed,
 // Device time of selected kernels on the stream that launches them (HIP
 // events; resolve() synchronises — call outside timed regions).  `units` are
 // the algorithmic bytes (aggregations) or flops (GEMMs) of one launch.
+// One kernel class per step is timed, rotating over the classes the driver
+// has launched (next_step() per training step): each event pair costs the
+// training stream ~4-5 us of gap, so timing every class every step added ~36
+// us to a 0.9 ms step; a quarter of the launches of each class is the sample.
 class KernelProfiler {
  public:
   enum Id { BOTTOM_AGG = 0, GATHER_GEMM, GATHER_GEMM_TN, BOTTOM_BWD, GAT_FWD, kCount };
@@ -415,11 +419,23 @@ class KernelProfiler {
   void end(Id id, hipStream_t st, double units);
   void resolve();
   void reset();
-  void add_units(Id id, double units) { stat[id].units += units; }
+  void add_units(Id id, double units) {
+    if (active(id)) stat[id].units += units;
+  }
+  void next_step() { ++step_; }
   static const char* name(int id);
   Stat stat[kCount];
 
  private:
+  // this step's timed class: the (step % #seen)-th of the classes seen so far
+  bool active(Id id) {
+    seen_ |= 1u << id;
+    uint32_t m = seen_;
+    for (int k = (int)(step_ % (uint64_t)__builtin_popcount(seen_)); k > 0; --k) m &= m - 1;
+    return (m & (~m + 1)) == (1u << id);
+  }
+  uint32_t seen_ = 0;
+  uint64_t step_ = 0;
   struct Slot {
     Id id = BOTTOM_AGG;
     hipEvent_t a = nullptr, b = nullptr;
