@@ -211,30 +211,31 @@ __device__ __forceinline__ uint64_t tile_word(uint32_t epoch, uint64_t kind, uin
 // 711-915), whose cache row is recorded in omit_row.  Three rounds of
 // independent loads (dst ids, their offsets, the omit map) instead of one
 // dependent chain per item.
+template <int IT>
 __device__ __forceinline__ void count_items(const CountArgs& ca, uint64_t base, uint64_t n,
-                                            uint32_t (&x)[kScanItems]) {
+                                            uint32_t (&x)[IT]) {
   const int t = threadIdx.x;
-  uint32_t d[kScanItems];
-  uint64_t lo[kScanItems], hi[kScanItems];
+  uint32_t d[IT];
+  uint64_t lo[IT], hi[IT];
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const uint64_t i = base + (uint64_t)k * kScanThreads + t;
     d[k] = i < n ? ca.dst[i] : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const uint64_t i = base + (uint64_t)k * kScanThreads + t;
     lo[k] = i < n ? ca.goff[d[k]] : 0u;
     hi[k] = i < n ? ca.goff[d[k] + 1] : 0u;
   }
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const uint32_t deg = (uint32_t)(hi[k] - lo[k]);
     x[k] = ca.fanout < 0 ? deg : min(deg, (uint32_t)ca.fanout);
   }
   if (ca.omit_map) {
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
       const uint64_t i = base + (uint64_t)k * kScanThreads + t;
       if (i < n) {
         const bool om = ca.omit_map[d[k]] == ca.omit_key;
@@ -245,14 +246,19 @@ __device__ __forceinline__ void count_items(const CountArgs& ca, uint64_t base, 
   }
 }
 
-template <bool COUNT>
+// IT items per thread: 16 for the radix-free generic scans; 4 for the count
+// scan, whose items are three dependent random loads each — 1,024-item tiles
+// put 4x the workgroups on the chip (57 -> 228 at C2's second layer) and keep
+// the tile's LDS (4.4 KB) within what a CU has left beside the 144 KB GEMMs.
+template <bool COUNT, int IT>
 __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restrict__ in,
                                                         uint32_t* __restrict__ out,
                                                         const uint32_t* n_dev, uint64_t n_cap,
                                                         uint64_t* __restrict__ state,
                                                         uint32_t epoch, uint32_t* ticket,
                                                         CountArgs ca) {
-  __shared__ uint32_t tile[kScanTile + kScanTile / 16];
+  constexpr int kTile = kScanThreads * IT;
+  __shared__ uint32_t tile[kTile + kTile / 16];
   __shared__ uint32_t wsum[kScanThreads / kWave];
   __shared__ uint32_t s_prefix;
   const uint32_t ti = lb_ticket(ticket, gridDim.x);
@@ -266,27 +272,27 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   } else {
     n = n_dev ? (uint64_t)*n_dev : n_cap;
   }
-  const uint64_t base = (uint64_t)ti * kScanTile;
+  const uint64_t base = (uint64_t)ti * kTile;
   if (base > n) return;  // every tile up to the one holding out[n] runs the chain
   if constexpr (COUNT) {
-    uint32_t x[kScanItems];
+    uint32_t x[IT];
     count_items(ca, base, n, x);
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) tile[pad_idx(k * kScanThreads + t)] = x[k];
+    for (int k = 0; k < IT; ++k) tile[pad_idx(k * kScanThreads + t)] = x[k];
   } else {
 #pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
       const uint32_t j = k * kScanThreads + t;
       const uint64_t i = base + j;
       tile[pad_idx(j)] = i < n ? in[i] : 0u;
     }
   }
   __syncthreads();
-  uint32_t v[kScanItems];
+  uint32_t v[IT];
   uint32_t s = 0;
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    v[k] = tile[pad_idx(t * kScanItems + k)];
+  for (int k = 0; k < IT; ++k) {
+    v[k] = tile[pad_idx(t * IT + k)];
     s += v[k];
   }
   uint32_t agg;
@@ -338,8 +344,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   uint32_t run = ex + s_prefix;
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    tile[pad_idx(t * kScanItems + k)] = run;
+  for (int k = 0; k < IT; ++k) {
+    tile[pad_idx(t * IT + k)] = run;
     // COUNT: the dst whose edges cross the edge capacity truncates the layer
     // at its first edge — the selection skips a dst that does not fit whole,
     // so e_size never covers unwritten edge slots (their ids are garbage)
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan1(const uint32_t* __restri
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const uint32_t j = k * kScanThreads + t;
     const uint64_t i = base + j;
     if (i <= n) out[i] = tile[pad_idx(j)];
@@ -377,7 +383,7 @@ int scan1_exclusive(nts_hip_ctx* ctx, const uint32_t* in, uint32_t* out, const u
                     uint64_t n_cap, hipStream_t stream) {
   const uint64_t nb = n_cap / kScanTile + 1;
   NTS_RET(ensure_scan_state(ctx, scan1_state_elems(n_cap)));
-  hipLaunchKernelGGL(k_scan1<false>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, in, out,
+  hipLaunchKernelGGL((k_scan1<false, kScanItems>), dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, in, out,
                      n_dev, n_cap, ctx->scan_state, next_epoch(ctx), scan_ticket(ctx), CountArgs{});
   NTS_LAUNCH_CHECK();
   return NTS_OK;
@@ -453,9 +459,10 @@ int count_scan(nts_hip_ctx* ctx, const CountArgs& ca, uint32_t* co, hipStream_t 
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }
-  const uint64_t nb = (uint64_t)ca.v_cap / kScanTile + 1;
-  NTS_RET(ensure_scan_state(ctx, scan1_state_elems(ca.v_cap)));
-  hipLaunchKernelGGL(k_scan1<true>, dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, nullptr,
+  constexpr int kCountItems = 4;
+  const uint64_t nb = (uint64_t)ca.v_cap / (kScanThreads * kCountItems) + 1;
+  NTS_RET(ensure_scan_state(ctx, (nb + 63) / 64 * 64));
+  hipLaunchKernelGGL((k_scan1<true, kCountItems>), dim3((uint32_t)nb), dim3(kScanThreads), 0, stream, nullptr,
                      co, nullptr, (uint64_t)ca.v_cap, ctx->scan_state, next_epoch(ctx), scan_ticket(ctx), ca);
   NTS_LAUNCH_CHECK();
   return NTS_OK;
