@@ -40,7 +40,7 @@ def profiler_kernel(name: str):
         return "gather_gemm"                     # X[src] W0 (no epilogue)
     if k == "k_gemm3_nn" and targs == ["false", "true"]:
         return "gather_gemm"                     # split-bf16 X[src] W0
-    if k == "k_x3_nn" and targs == ["false"]:
+    if k == "k_x3_nn" and targs[0] == "false":
         return "gather_gemm"                     # split-bf16 X[src] W0, whole rows (gemmx3.hip)
     if k == "k_x3_tn":
         return "gather_gemm_tn"                  # split-bf16 X[src]^T dH, whole rows (gemmx3.hip)
