@@ -1920,9 +1920,12 @@ frontier:
     NTS_LAUNCH_CHECK();
   }
 
-  // 3) frontier: ascending compaction of the byte map (single pass; the
-  // two-kernel form with the two-kernel scans, NTS_SCAN1=0)
-  if (scan1_enabled()) {
+  // 3) frontier: ascending compaction of the byte map — single pass up to
+  // kMarkFusedMaxTiles tiles (C2's 57), else (and with the two-kernel scans,
+  // NTS_SCAN1=0) count + write: at products' 598 tiles the look-back chain
+  // took 23 us a layer against 5 + 9 for the pair (scripts/r05_c3tr.sh)
+  constexpr uint32_t kMarkFusedMaxTiles = 256;
+  if (scan1_enabled() && nblk_marks <= kMarkFusedMaxTiles) {
     NTS_RET(ensure_scan_state(ctx, scan1_state_elems((uint64_t)nblk_marks * 4096)));
     hipLaunchKernelGGL(k_mark_fused, dim3(nblk_marks), dim3(kMarkThreads), 0, st, ctx->marks,
                        nblk_marks, V, o->s_cap, o->source, ctx->src_index, o->sizes,
