@@ -232,6 +232,41 @@ def test_c2_mt19937_reference_stream_full_batch(E):
     _free()
 
 
+def test_c2_mt19937_stream_ring_wraps(E):
+    """The MT19937 stream ring (2^25 tempered words on the device, generated
+    ahead of the layers that read them) wrapping around: 24 consecutive C2
+    batches (B = 10,000, 25-10) consume more than 2^25 words, so the later
+    layers read words stored at ring index (stream word mod 2^25) and the
+    generator refills slots that earlier layers read — the host-side
+    bookkeeping (read-back position, pending bounds, the ring-capacity wait in
+    mt_ring_prepare) included.  Every batch bit-exact vs the oracle's
+    std::mt19937(2000) walk in draw order (core/ntsFastSampler.hpp:200-205,
+    962-1140), the generator state identical after the last."""
+    from nts import synthetic
+    g, F, C = synthetic.shaped("reddit", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    fan, B, nb = [25, 10], 10_000, 24
+    rng = np.random.default_rng(17)
+    perm = np.concatenate([rng.permutation(V), rng.permutation(V)]).astype(np.int32)[:nb * B]
+    fs = E.FastSampler(G, torch.from_numpy(perm), 2, B, fan, rng_mode=1, seed=2000)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    o = orc.Sampler(col, rows, _np(G.in_degree), _np(G.out_degree), fan, seed=2000,
+                    rng_mode=orc.RNG_MT_LEMIRE, order_mode=orc.ORDER_DRAW)
+    edges = 0
+    for b in range(nb):
+        got = fs.sample_gpu_fast(B)
+        edges += sum(int(l["e_size"]) for l in got)
+        ref = o.sample(perm[b * B:(b + 1) * B].view(np.uint32), b)
+        _compare_oracle(got, ref)
+    assert edges > (1 << 25), edges  # at least one accepted word per edge: the ring wrapped
+    assert np.array_equal(_np(fs.rng_state()), o.mt_state())
+    del fs, got, G
+    _free()
+
+
 def test_c3_products_shaped_three_layers_mean(E):
     from nts import synthetic
     g, F, C = synthetic.shaped("products", device=DEV)
