@@ -439,8 +439,11 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
   // one k-step on the split A(s) in ap[P]; A(s+1) is read and split into
   // ap[1-P] in the second half of the column tiles, after a mid-step wait for
   // its 4 pieces (younger in flight: B(s+1)'s 3 and A(s+2)'s 4)
-  auto step = [&](int s, auto par) {
-    constexpr int P = decltype(par)::value;
+  // NT: the row tiles this wave computes this round (2, or 1 in a round with
+  // one tile left: the MFMAs, A reads and splits of the idle tile skipped —
+  // its DMA still runs, so the counted waits are the same)
+  auto step = [&](int s, auto par, auto ntc) {
+    constexpr int P = decltype(par)::value, NT = decltype(ntc)::value;
     if (s > 0) {
       // B(s) landed (A(s) was waited for in step s-1; A(s+1)'s 4 pieces may stay in flight)
       if (s + 1 < nsteps && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -460,17 +463,17 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     for (int p = 0; p < 3; ++p) bf[0][p] = getb(0, p);
     x3bf8 a[2][3];
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < NT; ++rt)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
         a[rt][p] = __builtin_bit_cast(x3bf8, (x3u4){ap[P][rt][p][0], ap[P][rt][p][1], ap[P][rt][p][2], ap[P][rt][p][3]});
 #pragma unroll
     for (int ct = 0; ct < 8; ++ct) {
 #pragma unroll
-      for (int k = 0; k < 12; ++k) {
+      for (int k = 0; k < 6 * NT; ++k) {
         __builtin_amdgcn_sched_barrier(0);
-        {  // slot k: product k / 2 (small first) of row tile k & 1
-          const int rt = k & 1, pr = k >> 1;
+        {  // slot k: product k / NT (small first) of row tile k % NT
+          const int rt = NT == 2 ? (k & 1) : 0, pr = NT == 2 ? (k >> 1) : k;
           const int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
           const int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
           if constexpr (DIAG & 1) acc[rt][ct][0] += (float)a[rt][pa][0] + (float)bf[ct & 1][pb][1];
@@ -488,19 +491,19 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
           else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
         }
         if (ct == 4 && k == 1) read_a(s + 1, 0);
-        if (ct == 4 && k == 3) read_a(s + 1, 1);
-        if ((ct == 5 || ct == 6) && k % 3 == 1) split_a(std::integral_constant<int, 1 - P>{}, ct - 5, k / 3);
+        if constexpr (NT == 2) {
+          if (ct == 4 && k == 3) read_a(s + 1, 1);
+          if ((ct == 5 || ct == 6) && k % 3 == 1) split_a(std::integral_constant<int, 1 - P>{}, ct - 5, k / 3);
+        } else {
+          if (ct == 5 && (k & 1)) split_a(std::integral_constant<int, 1 - P>{}, 0, k >> 1);
+          if (ct == 6 && k == 1) split_a(std::integral_constant<int, 1 - P>{}, 0, 3);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  for (int rd = 0; rd < rounds; ++rd) {
-    const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));  // this wave's tiles this round
-    set_rows(rd);
-#pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+  auto round_steps = [&](auto ntc) {
+    constexpr int NT = decltype(ntc)::value;
     issue_b(0);
     issue_a(0);
     if (nsteps > 1) issue_a(1);
@@ -510,16 +513,32 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     x3_barrier();
     if (nsteps > 1) issue_b(1);
     if (nsteps > 2) issue_a(2);
-    read_a(0, 0);
-    read_a(0, 1);
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < NT; ++rt) read_a(0, rt);
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt)
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) split_a(std::integral_constant<int, 0>{}, rt, jp);
     for (int s = 0; s < nsteps; s += 2) {
-      step(s, std::integral_constant<int, 0>{});
-      if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{});
+      step(s, std::integral_constant<int, 0>{}, ntc);
+      if (s + 1 < nsteps) step(s + 1, std::integral_constant<int, 1>{}, ntc);
     }
+  };
+  for (int rd = 0; rd < rounds; ++rd) {
+    const int nt = min(2, max(0, t_hi - (t_lo + 2 * rd)));  // this wave's tiles this round
+    set_rows(rd);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+    // (a round with one tile left — at C2 the last of every wave's four —
+    // runs half the MFMAs; the block's waves still meet at every barrier)
+#ifdef NTS_X3_NO_NT1  // (A/B build: every round on both tiles)
+    round_steps(std::integral_constant<int, 2>{});
+#else
+    if (nt == 2) round_steps(std::integral_constant<int, 2>{});
+    else round_steps(std::integral_constant<int, 1>{});
+#endif
     x3_barrier();  // every wave is done with the B stages before the next round's
     if constexpr (!EPI) {
       // transposed accumulators: acc[rt][ct][v] = C[16 t + i][n0 + 16 ct + 4 q + v],
