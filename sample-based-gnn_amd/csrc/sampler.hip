@@ -1031,7 +1031,9 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
                                                    uint32_t* __restrict__ tabs) {
   __shared__ uint4 inf[kMtChunk];
   __shared__ uint32_t bs[kMtChunk];
+#ifdef NTS_MT_LDS_LST  // (A/B build: the fallback walk's list in LDS, NMAX words a lane)
   __shared__ uint32_t lst[NMAX * 256];
+#endif
   __shared__ float red[2][4];
   __shared__ uint32_t uu[4][2][192];  // per wave: the union windows of two dsts
   const int t = threadIdx.x;
@@ -1132,7 +1134,18 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
       for (int q = 0; q < NW; ++q) cur[q] = W[p + q];
       used = regs_consume<NW>(cur, f.y, f.z, f.w, lemire);
     }
-    if (used == 0) used = lane_consume<NMAX>(W, p, f.y, f.z, f.w, lemire, lst + t, 256);
+    if (used == 0) {
+#ifdef NTS_MT_LDS_LST
+      used = lane_consume<NMAX>(W, p, f.y, f.z, f.w, lemire, lst + t, 256);
+#else
+      // the rare sequential walk keeps its list in private memory (scratch):
+      // in LDS it cost NMAX KiB a block and capped the kernel at 7 (NMAX 10)
+      // or 4 (NMAX 25) waves per SIMD
+      uint32_t plst[NMAX];
+      asm volatile("" ::"v"(plst) : "memory");  // (its address escapes: scratch, not registers)
+      used = lane_consume<NMAX>(W, p, f.y, f.z, f.w, lemire, plst, 1);
+#endif
+    }
     dl += used - f.y;
     if (jn < cnt) store_union(buf ^ 1, inf[jn]);
     P0 = P0n;
