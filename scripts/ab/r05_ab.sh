@@ -1,0 +1,10 @@
+#!/bin/bash
+# MT19937 mode: banded resolver — bit-exact tests, the --rng mt step, its trace
+set -o pipefail
+cd "$(dirname "$0")/../.."
+O=gpurun_out/r05ab; mkdir -p $O
+export TMPDIR=/tmp
+A="--secondary --rng mt --steps 20 --warmup 5 --no-pipeline"
+timeout -k 10 300 python -u bench.py $A > $O/mt.json 2> $O/mt.log || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- \
+  python3 bench.py $A > $O/trace.log 2>&1

@@ -1,0 +1,12 @@
+#!/bin/bash
+# r05b: k_x3_tn parity + timing; the piece-size probe for the NN design
+set -o pipefail
+cd "$(dirname "$0")/../.."
+O=gpurun_out/r05b; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 120 ./scripts/probe/piece_probe 10 > $O/piece.jsonl 2>&1 &&
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+    tests/test_gemm_x3.py tests/test_gemm_split3.py > $O/tests.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --pair-table 0 --transform-first 1 --steps 20 --warmup 5 \
+    --no-cpu-baseline --no-secondary-af --no-secondary-mt --epochs 0 --sampler-batches 0 \
+    > $O/exact.json 2> $O/exact.log
