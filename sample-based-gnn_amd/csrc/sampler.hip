@@ -654,12 +654,20 @@ constexpr uint32_t kMtPos = 8192;   // kept positions staged in LDS before the f
 // layer of up to kMtSmallV dsts is cut into kMtChunkSmall-dst chunks, one of
 // up to kMtMaxChunks x kMtChunkMid into kMtChunkMid-dst chunks: a window
 // table's lanes walk fewer dsts each and more chunks fill the CUs (C2 with
-// --rng mt, scripts/r04_n.sh: 4.60 ms/step at 64 / 256, 4.50 at 32 / 128,
+// --rng mt, scripts/ab/r04_n.sh: 4.60 ms/step at 64 / 256, 4.50 at 32 / 128,
 // 4.80 at 64 / 64 — the resolver's chain over the chunks grows; 5.29 with
-// 256 everywhere); words staged per chunk
+// 256 everywhere; round 5, with the tables at 8 / 6 waves per SIMD,
+// scripts/ab/r05_aj.sh: mid 96 / 128 / 192 -> 3.63 / 3.59-3.61 / 3.57,
+// small 24 / 32 / 48 -> 3.56-3.58 / 3.59-3.61 / 3.60); words staged per chunk
+#ifndef NTS_MT_CHUNK_MID  // (A/B builds)
+#define NTS_MT_CHUNK_MID 192
+#endif
+#ifndef NTS_MT_CHUNK_SMALL
+#define NTS_MT_CHUNK_SMALL 32
+#endif
 constexpr uint32_t kMtChunk = 256;
-constexpr uint32_t kMtChunkMid = 128;
-constexpr uint32_t kMtChunkSmall = 32;
+constexpr uint32_t kMtChunkMid = NTS_MT_CHUNK_MID;
+constexpr uint32_t kMtChunkSmall = NTS_MT_CHUNK_SMALL;
 constexpr uint32_t kMtSmallV = 32768;
 constexpr uint32_t kMtStage = 12288;
 
