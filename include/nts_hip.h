@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 8  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 9  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
                                      accuracy counts in the fused loss;
                                   4: PD cache entry points + omit fields, GEMM mode;
@@ -43,7 +43,8 @@ extern "C" {
                                   7: the column maxima per part of rows (no row scales in
                                      the backward), nts_hip_csr_bwd_colmax_rows_per_part;
                                   8: nts_hip_comm_count; the CSR-backward column maxima scaled by
-                                     the pair table's row scales (exact TN operand maxima) */
+                                     the pair table's row scales (exact TN operand maxima);
+                                  9: nts_sampcsc_dev::sizes_host */
 
 /* status codes */
 #define NTS_OK 0
@@ -139,6 +140,12 @@ typedef struct {
   uint32_t *omit_row;              /* [v_cap] with omit_map: omit_loc[dst[i]]
                                       for an omitted dst i, else NTS_NOT_CACHED
                                       (the batch's own snapshot of the cache) */
+  uint32_t *sizes_host;            /* NULL, or a device-visible pointer to host
+                                      memory (hipHostMalloc mapped + coherent):
+                                      the layer's last kernel also stores the 4
+                                      sizes words there, so the host reads them
+                                      after the stream's event without a D2H
+                                      copy of its own                          */
 } nts_sampcsc_dev;
 
 /* ---- context ------------------------------------------------------------ */

@@ -1479,7 +1479,15 @@ struct RelabelArgs {
   uint32_t* ri;
   float* wf;
   uint32_t* up_cnt;
+  uint32_t* pub;  // the layer's last kernel: nts_sampcsc_dev::sizes_host, else NULL
 };
+
+// the layer's sizes words into the caller's host-mapped copy, from the layer's
+// last kernel (every sizes word is final by then): replaces a per-batch D2H
+// copy, a blit kernel of its own on the sampler stream
+__device__ __forceinline__ void publish_sizes(const uint32_t* sizes, uint32_t* pub) {
+  if (pub && blockIdx.x == 0 && threadIdx.x < 4) pub[threadIdx.x] = sizes[threadIdx.x];
+}
 
 __device__ __forceinline__ uint32_t relabel_one(const RelabelArgs& a, uint32_t k) {
   const uint32_t g = a.ans[k];
@@ -1499,6 +1507,7 @@ __device__ __forceinline__ uint32_t relabel_one(const RelabelArgs& a, uint32_t k
 }
 
 __global__ void k_relabel(RelabelArgs a) {
+  publish_sizes(a.sizes, a.pub);
   const uint32_t e = a.sizes[1];
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x)
     relabel_one(a, k);
@@ -1508,7 +1517,9 @@ __global__ void k_relabel(RelabelArgs a) {
 // in = sampled edges of the dst (its CSC segment)
 __global__ void k_up_weight(const uint32_t* __restrict__ ri, const uint32_t* __restrict__ edst,
                             const uint32_t* __restrict__ co, const uint32_t* __restrict__ cnt,
-                            const uint32_t* sizes, int weight_type, float* __restrict__ wf) {
+                            const uint32_t* sizes, int weight_type, float* __restrict__ wf,
+                            uint32_t* pub) {
+  publish_sizes(sizes, pub);
   const uint32_t e = sizes[1];
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e; k += gridDim.x * blockDim.x) {
     const uint32_t d = edst[k];
@@ -1539,7 +1550,8 @@ __global__ void k_csr_finalize(const uint32_t* __restrict__ skey, const uint32_t
                                const uint32_t* __restrict__ edst, const float* __restrict__ wf,
                                const uint32_t* sizes, uint32_t* __restrict__ ro,
                                uint32_t* __restrict__ ci, float* __restrict__ wb,
-                               uint32_t* __restrict__ ceid) {
+                               uint32_t* __restrict__ ceid, uint32_t* pub) {
+  publish_sizes(sizes, pub);
   const uint32_t e = sizes[1];
   const uint32_t s = sizes[2];
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < e; j += gridDim.x * blockDim.x) {
@@ -1979,13 +1991,14 @@ frontier:
   RelabelArgs ra{o->sample_ans,      o->edge_dst, o->destination, ctx->src_index,
                  g->out_degree,      g->in_degree, o->column_offset, o->sizes,
                  weight_type,        o->row_indices, o->edge_weight_forward,
-                 up ? t_up : nullptr};
+                 up ? t_up : nullptr, (up || csr) ? nullptr : o->sizes_host};
   if (up) NTS_HIP_TRY(hipMemsetAsync(t_up, 0, up_n * sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_relabel, dim3(ge), dim3(256), 0, st, ra);
   NTS_LAUNCH_CHECK();
   if (up) {
     hipLaunchKernelGGL(k_up_weight, dim3(ge), dim3(256), 0, st, o->row_indices, o->edge_dst,
-                       o->column_offset, t_up, o->sizes, weight_type, o->edge_weight_forward);
+                       o->column_offset, t_up, o->sizes, weight_type, o->edge_weight_forward,
+                       csr ? nullptr : o->sizes_host);
     NTS_LAUNCH_CHECK();
   }
 
@@ -2002,7 +2015,7 @@ frontier:
     hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
                        weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
                        o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
-                       o->csr_edge_id);
+                       o->csr_edge_id, o->sizes_host);
     NTS_LAUNCH_CHECK();
   }
   return NTS_OK;

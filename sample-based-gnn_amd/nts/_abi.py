@@ -18,7 +18,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ["NTS_HIP_LIB"]) if os.environ.get("NTS_HIP_LIB") else _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 8  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 9  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
@@ -78,6 +78,7 @@ class SampCSCDev(C.Structure):
         ("sizes", C.c_void_p), ("dst_local_id", C.c_void_p), ("csr_edge_id", C.c_void_p),
         ("omit_map", C.c_void_p), ("omit_key", C.c_uint32), ("omit_loc", C.c_void_p),
         ("omit_row", C.c_void_p),
+        ("sizes_host", C.c_void_p),
     ]
 
 

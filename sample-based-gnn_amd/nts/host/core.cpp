@@ -218,13 +218,21 @@ SampledSubgraph::SampledSubgraph(int device, int layers_, const std::vector<int>
   // every layer's sizes[4] as a view of one device array: one D2H per batch
   dev_sizes = torch::zeros({std::max(layers, 1) * 4}, u32_opts(device));
   for (int l = 0; l < layers; ++l) sampled_sgs[l]->sizes = dev_sizes.narrow(0, 4 * l, 4);
-  host_sizes = torch::empty({layers * 4}, torch::TensorOptions().dtype(torch::kInt32).pinned_memory(true));
+  void* hs = nullptr;
+  hip_rt(hipHostMalloc(&hs, 16 * (size_t)std::max(layers, 1), hipHostMallocMapped | hipHostMallocCoherent),
+         "hipHostMalloc(sizes)");
+  host_sizes = static_cast<int32_t*>(hs);
+  std::fill(host_sizes, host_sizes + 4 * std::max(layers, 1), 0);
+  void* hd = nullptr;
+  hip_rt(hipHostGetDevicePointer(&hd, hs, 0), "hipHostGetDevicePointer(sizes)");
+  host_sizes_dev = static_cast<uint32_t*>(hd);
   hip_rt(hipEventCreateWithFlags(&sampled, hipEventDisableTiming), "hipEventCreate");
   hip_rt(hipEventCreateWithFlags(&consumed, hipEventDisableTiming), "hipEventCreate");
 }
 
 SampledSubgraph::~SampledSubgraph() {
   for (auto* s : sampled_sgs) delete s;
+  (void)hipHostFree(host_sizes);
   (void)hipEventDestroy(sampled);
   (void)hipEventDestroy(consumed);
 }
@@ -315,6 +323,7 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
     o.sizes = dptr<uint32_t>(s->sizes);
     o.dst_local_id = dptr<uint32_t>(s->dst_local_id);  // undefined (NULL) unless merged
     o.csr_edge_id = dptr<uint32_t>(s->csr_edge_id);
+    o.sizes_host = ssg->host_sizes_dev + 4 * l;
     if (l == layer - 1 && omit_map) {
       if (!s->omit_row.defined())
         s->omit_row = torch::empty({std::max<int64_t>(s->v_cap, 1)}, u32_opts(whole_graph->device));
@@ -335,11 +344,8 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
     dst = o.source;
     vsz = o.sizes + 2;
   }
-  // one D2H of all layer sizes per batch (the reference syncs twice per layer)
-  int32_t* hs = ssg->host_sizes.data_ptr<int32_t>();
-  hip_rt(hipMemcpyAsync(hs, dptr<uint32_t>(ssg->dev_sizes), 16 * (size_t)layer,
-                        hipMemcpyDeviceToHost, st),
-         "hipMemcpyAsync(sizes)");
+  // the layers' sizes reach host_sizes from their last kernels (the reference
+  // syncs twice per layer; a D2H copy here cost a blit kernel per batch)
   hip_rt(hipEventRecord(ssg->sampled, st), "hipEventRecord");
   if (host_profile()) fprintf(stderr, "[host] issue total: %.1f us\n", (now_s() - t0) * 1e6);
   ssg->pending_batch = (int)actual;
@@ -355,7 +361,7 @@ SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
   hip_rt(hipEventSynchronize(ssg->sampled), "hipEventSynchronize");
   if (host_profile()) fprintf(stderr, "[host] finish wait: %.1f us\n", (now_s() - t0) * 1e6);
   ssg->pending_batch = 0;
-  const int32_t* hs = ssg->host_sizes.data_ptr<int32_t>();
+  const volatile int32_t* hs = ssg->host_sizes;
   for (int l = 0; l < layer; ++l) {
     sampCSC* s = ssg->sampled_sgs[l];
     s->v_size = (VertexId)hs[4 * l];

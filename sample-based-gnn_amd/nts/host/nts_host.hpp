@@ -158,8 +158,11 @@ class SampledSubgraph {
   int layers = 0;
   std::vector<int> fanout;
   torch::Tensor dev_sizes;   // device u32 [layers*4]: the layers' sizes (views)
-  torch::Tensor host_sizes;  // pinned int32 [layers*4]
-  hipEvent_t sampled = nullptr;   // recorded after the sizes copy of the last issue
+  // int32 [layers*4] in mapped, coherent host memory: each layer's last
+  // kernel stores its sizes words there (nts_sampcsc_dev::sizes_host)
+  int32_t* host_sizes = nullptr;
+  uint32_t* host_sizes_dev = nullptr;  // its device-visible address
+  hipEvent_t sampled = nullptr;   // recorded after the last issue's kernels
   hipEvent_t consumed = nullptr;  // recorded by the trainer once it is done with the slot
   int pending_batch = 0;          // seeds of the issued, not yet finished batch
   SampledSubgraph(int device, int layers, const std::vector<int>& fanout, VertexId batch,
@@ -167,6 +170,8 @@ class SampledSubgraph {
                   bool weights,
                   bool merge = false);
   ~SampledSubgraph();
+  SampledSubgraph(const SampledSubgraph&) = delete;
+  SampledSubgraph& operator=(const SampledSubgraph&) = delete;
 };
 
 // ---------------------------------------------------------------------------
