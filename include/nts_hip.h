@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 9  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 10  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
                                      accuracy counts in the fused loss;
                                   4: PD cache entry points + omit fields, GEMM mode;
@@ -44,7 +44,10 @@ extern "C" {
                                      the backward), nts_hip_csr_bwd_colmax_rows_per_part;
                                   8: nts_hip_comm_count; the CSR-backward column maxima scaled by
                                      the pair table's row scales (exact TN operand maxima);
-                                  9: nts_sampcsc_dev::sizes_host */
+                                  9: nts_sampcsc_dev::sizes_host;
+                                  10: the activation's keep mask as bits (nts_hip_act_bits_words,
+                                      nts_hip_spmm_csc_fwd_act_bits,
+                                      nts_hip_spmm_csr_bwd_postmask_bits) */
 
 /* status codes */
 #define NTS_OK 0
@@ -350,6 +353,27 @@ int nts_hip_spmm_csr_bwd_postmask(nts_hip_ctx *ctx, const uint32_t *row_offset,
                                   const uint32_t *s, uint32_t s_cap, const float *g_out,
                                   uint64_t ld_gout, const float *x_act, uint64_t ld_act, float scale,
                                   uint32_t feature_size, float *g_in, uint64_t ld_gin);
+/* The same pair with the activation's keep mask [X_act > 0] carried as bits
+ * instead of re-read from X_act's rows (16 bytes a 128-float row instead of
+ * 512): nts_hip_act_bits_words(F) words per row (0: F unsupported — F must be
+ * a multiple of 4 from 68 to 2048; the caller then uses the float forms),
+ * 16-byte aligned.
+ * nts_hip_spmm_csc_fwd_act_bits = nts_hip_spmm_csc_fwd_act that also writes
+ * mask_bits[v_cap rows]; nts_hip_spmm_csr_bwd_postmask_bits =
+ * nts_hip_spmm_csr_bwd_postmask reading those bits (X_act's rows = g_in's
+ * rows).  Results identical to the float forms. */
+uint32_t nts_hip_act_bits_words(uint32_t feature_size);
+int nts_hip_spmm_csc_fwd_act_bits(nts_hip_ctx *ctx, const uint32_t *column_offset,
+                                  const uint32_t *row_indices, const float *weight,
+                                  const uint32_t *v, uint32_t v_cap, const float *x, uint64_t ldx,
+                                  uint32_t feature_size, float *y, uint64_t ldy, float p,
+                                  uint64_t seed, uint64_t offset, uint32_t *mask_bits);
+int nts_hip_spmm_csr_bwd_postmask_bits(nts_hip_ctx *ctx, const uint32_t *row_offset,
+                                       const uint32_t *column_indices,
+                                       const float *weight_backward, const uint32_t *s,
+                                       uint32_t s_cap, const float *g_out, uint64_t ld_gout,
+                                       const uint32_t *mask_bits, float scale,
+                                       uint32_t feature_size, float *g_in, uint64_t ld_gin);
 /* The activation's backward alone: out = g ⊙ [x_act > 0] * scale ([rows x
  * feature_size], each with its leading dimension) — what libtorch's relu and
  * dropout backward compute for vertexForward (toolkits/GCN_SAMPLE_GPU.hpp:252-266),

@@ -118,7 +118,18 @@ struct AggExtra {
   uint32_t* cm_out = nullptr;
   const float* cm_rs = nullptr;
   const uint32_t* cm_map = nullptr;
+  // the activation's keep mask as bits (nts_hip_act_bits_words): kAggAct
+  // writes them beside its output (bits_out), kAggPostMask reads them instead
+  // of the output's rows (bits_in); ldb words per row
+  uint32_t* bits_out = nullptr;
+  const uint32_t* bits_in = nullptr;
+  uint64_t ldb = 0;
 };
+
+// Mask bits of a float4 row on LPD >= 32 lanes (one chunk of NCH float4 a
+// lane): word (h NCH + c) 4 + q of a row holds, at bit b, whether component q
+// of chunk c of lane 32 h + b is > 0 (h = 0 for 32-lane groups)
+// (nts_hip_act_bits_words: (LPD / 32) NCH 4 words a row)
 
 template <int VEC>
 __device__ __forceinline__ float& vcomp(typename VT<VEC>::T& v, int q) {
@@ -238,18 +249,53 @@ __device__ __forceinline__ void store_row(typename VT<VEC>::T (&acc)[NCH], uint3
         }
       }
     }
+    if constexpr (VEC == 4 && LPD >= 32) {
+      if (ax.bits_out) {  // (uniform) the row's keep mask, one ballot per component
+        const int hw = (threadIdx.x & 63) >> 5;
+        uint32_t* brow = ax.bits_out + (uint64_t)d * ax.ldb + (LPD == 64 ? hw : 0) * NCH * 4;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          uint32_t wq[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            wq[q] = (uint32_t)(__ballot(vcomp<VEC>(acc[c], q) > 0.f) >> (32 * hw));
+          if ((threadIdx.x & 31) == 0)
+            *reinterpret_cast<uint4*>(brow + 4 * c) = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+        }
+      }
+    }
   }
   if constexpr (MODE == kAggPostMask) {  // dZ = dX ⊙ [X > 0] · scale, X row d
-    const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)d * ax.ldm);
+    bool bits = false;
+    if constexpr (VEC == 4 && LPD >= 32) {
+      if (ax.bits_in) {  // (uniform) the keep mask as bits
+        bits = true;
+        const uint4* brow = reinterpret_cast<const uint4*>(ax.bits_in + (uint64_t)d * ax.ldb) +
+                            (LPD == 64 ? (sl >> 5) : 0) * NCH;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const uint32_t col = c0 + sl + c * LPD;
-      if (col < nv) {
-        const T m = mrow[col];
+        for (int c = 0; c < NCH; ++c) {
+          const uint4 b4 = brow[c];
+          const uint32_t wq[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) {
-          float& v = vcomp<VEC>(acc[c], q);
-          v = vcomp<VEC>(m, q) > 0.f ? v * ax.scale : 0.f;
+          for (int q = 0; q < 4; ++q) {
+            float& v = vcomp<VEC>(acc[c], q);
+            v = ((wq[q] >> (sl & 31)) & 1u) ? v * ax.scale : 0.f;
+          }
+        }
+      }
+    }
+    if (!bits) {
+      const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)d * ax.ldm);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const uint32_t col = c0 + sl + c * LPD;
+        if (col < nv) {
+          const T m = mrow[col];
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            float& v = vcomp<VEC>(acc[c], q);
+            v = vcomp<VEC>(m, q) > 0.f ? v * ax.scale : 0.f;
+          }
         }
       }
     }
@@ -274,9 +320,11 @@ __device__ __forceinline__ void store_row(typename VT<VEC>::T (&acc)[NCH], uint3
 // edges (in edge order) and the partial sums are added in group order through
 // LDS.  Deterministic; rows up to kLongRow edges keep the serial edge order
 // (bit-identical to MiniBatchFuseOp::backward's), longer rows are summed as
-// GPB in-order pieces.  Needs one row per group (grid = ceil(n_cap / GPB)).
+// GPB in-order pieces.  A group takes at most kCoopRows rows (grid >=
+// ceil(n_cap / (GPB kCoopRows))): the block's long rows fit its list.
 template <int U>
 constexpr uint32_t kLongRow() { return 4 * U; }
+constexpr uint32_t kCoopRows = 16;
 
 // Row software pipeline of k_spmm_gather (compile-time A/B builds, `make
 // variant`): 0 none, 1 the next row's offsets, 2 the offsets two rows ahead
@@ -311,7 +359,7 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(NCH
   const uint32_t n = n_dev ? min(*n_dev, n_cap) : n_cap;
   constexpr int GPB = kAggThreads / LPD;
   const int grp = threadIdx.x / LPD, sl = threadIdx.x % LPD;
-  __shared__ uint32_t long_rows[COOP ? GPB : 1];
+  __shared__ uint32_t long_rows[COOP ? GPB * kCoopRows : 1];
   __shared__ uint32_t n_long;
   if (COOP) {
     if (threadIdx.x == 0) n_long = 0;
@@ -405,24 +453,54 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(NCH
       // kAggPostMask: the output row's mask is known before the edges are —
       // load it first, so its latency overlaps the gather instead of following it
       T pm[MODE == kAggPostMask ? NCH : 1];
+      uint4 pb[MODE == kAggPostMask && VEC == 4 && LPD >= 32 ? NCH : 1];
       if constexpr (MODE == kAggPostMask) {
-        const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)d * ax.ldm);
+        bool bits = false;
+        if constexpr (VEC == 4 && LPD >= 32) {
+          if (ax.bits_in) {  // (uniform) the keep mask as bits
+            bits = true;
+            const uint4* brow = reinterpret_cast<const uint4*>(ax.bits_in + (uint64_t)d * ax.ldb) +
+                                (LPD == 64 ? (sl >> 5) : 0) * NCH;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-          const uint32_t col = c0 + sl + c * LPD;
-          pm[c] = col < nv ? mrow[col] : V::zero();
+            for (int c = 0; c < NCH; ++c) pb[c] = brow[c];
+          }
+        }
+        if (!bits) {
+          const T* mrow = reinterpret_cast<const T*>(ax.mx + (uint64_t)d * ax.ldm);
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            const uint32_t col = c0 + sl + c * LPD;
+            pm[c] = col < nv ? mrow[col] : V::zero();
+          }
         }
       }
       gather_edges<VEC, LPD, NCH, MAP, U, TIER, EM>(acc, cbeg, cend, c0, sl, idx, w, x, ldx, map,
                                                       nv, tier, ax, kAggPf >= 2, cpr, cpw);
       if constexpr (MODE == kAggPostMask) {  // same arithmetic as store_row's
+        bool bits = false;
+        if constexpr (VEC == 4 && LPD >= 32) {
+          if (ax.bits_in) {
+            bits = true;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c)
+            for (int c = 0; c < NCH; ++c) {
+              const uint32_t wq[4] = {pb[c].x, pb[c].y, pb[c].z, pb[c].w};
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) {
-            float& v = vcomp<VEC>(acc[c], q);
-            v = vcomp<VEC>(pm[c], q) > 0.f ? v * ax.scale : 0.f;
+              for (int q = 0; q < 4; ++q) {
+                float& v = vcomp<VEC>(acc[c], q);
+                v = ((wq[q] >> (sl & 31)) & 1u) ? v * ax.scale : 0.f;
+              }
+            }
           }
+        }
+        if (!bits) {
+#pragma unroll
+          for (int c = 0; c < NCH; ++c)
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+              float& v = vcomp<VEC>(acc[c], q);
+              v = vcomp<VEC>(pm[c], q) > 0.f ? v * ax.scale : 0.f;
+            }
+        }
       }
       store_row<VEC, LPD, NCH, MODE == kAggPostMask ? kAggPlain : EM>(acc, d, c0, sl, nv,
                                                                       last_valid, y, ldy, ax);
@@ -1052,7 +1130,8 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
                          uint32_t expect_grid = 0) {
   int vec = pick_vec(F, ldx, ldy, x, y);
   if (TIER) vec = std::min(vec, pick_vec(F, tier.ldh, ldx, tier.host, x));
-  if (MODE == kAggMask || MODE == kAggPostMask) vec = std::min(vec, pick_vec(F, ax.ldm, ldx, ax.mx, x));
+  if (MODE == kAggMask || (MODE == kAggPostMask && !ax.bits_in))
+    vec = std::min(vec, pick_vec(F, ax.ldm, ldx, ax.mx, x));
   // rows padded to a 16-byte multiple (the 128-byte feature / output pitch):
   // float4 loads, the partial last vector reads pitch padding and stores only
   // its valid floats
@@ -1099,8 +1178,19 @@ static int launch_gather(hipStream_t st, const uint32_t* off, const uint32_t* id
 #define NTS_AGG_GRID (1u << 24)
 #endif
   constexpr uint32_t cap = NTS_AGG_GRID;
-  // COOP needs one row per lane group
-  const uint32_t grid = std::max(1u, COOP ? ceil_div(n_cap, gpb) : std::min(ceil_div(n_cap, gpb), cap));
+  // the post-mask CSR gather (the hop above a transform-first bottom layer,
+  // ~2 edges per row at C2) with a few rows per group instead of one
+  // (compile-time A/B, -DNTS_AGG_PM_GRID=<blocks>): 44.7 / 44.6 / 51.7 us at
+  // 4096 / 8192 / 2048 blocks against 44.9 at one row per group
+  // (scripts/ab/r05_au.sh) — bound by its bytes, not by block lifetimes
+#ifndef NTS_AGG_PM_GRID
+#define NTS_AGG_PM_GRID (1u << 24)
+#endif
+  constexpr uint32_t pm_cap = MODE == kAggPostMask ? NTS_AGG_PM_GRID : (1u << 24);
+  // COOP: at most kCoopRows rows per lane group (the colmax parts: one)
+  const uint32_t grid =
+      std::max(1u, COOP ? std::max(ceil_div(n_cap, gpb * kCoopRows), std::min(ceil_div(n_cap, gpb), pm_cap))
+                        : std::min(ceil_div(n_cap, gpb), cap));
   // kAggColmax: the per-block buffer was sized for this grid
   NTS_CHECK_ARG(expect_grid == 0 || expect_grid == grid, "aggregation grid != the sized one");
   if (vec == 4)
@@ -1240,6 +1330,66 @@ int nts_hip_spmm_csr_bwd_postmask(nts_hip_ctx* ctx, const uint32_t* row_offset,
   AggExtra ax;
   ax.mx = x_act;
   ax.ldm = ld_act;
+  ax.scale = scale;
+  return launch_gather<false, false, kAggPostMask, true>(ctx->stream, row_offset, column_indices,
+                                                         weight_backward, s, s_cap, g_out, ld_gout,
+                                                         nullptr, feature_size, g_in, ld_gin,
+                                                         Tier{nullptr, nullptr, 0, 0}, ax);
+}
+
+uint32_t nts_hip_act_bits_words(uint32_t feature_size) {
+  if (feature_size == 0 || feature_size % 4) return 0;
+  const uint32_t nv = feature_size / 4;
+  const Shape s = pick_shape(nv);
+  if (s.lpd < 32 || nv > (uint32_t)(s.lpd * s.nch)) return 0;  // float4 rows of one chunk
+  return (uint32_t)(s.lpd / 32) * (uint32_t)s.nch * 4u;  // act_bits_words<LPD, NCH>()
+}
+
+int nts_hip_spmm_csc_fwd_act_bits(nts_hip_ctx* ctx, const uint32_t* column_offset,
+                                  const uint32_t* row_indices, const float* weight,
+                                  const uint32_t* v, uint32_t v_cap, const float* x, uint64_t ldx,
+                                  uint32_t feature_size, float* y, uint64_t ldy, float p,
+                                  uint64_t seed, uint64_t offset, uint32_t* mask_bits) {
+  NTS_CHECK_ARG(ctx && column_offset && row_indices && x && y && mask_bits, "NULL argument");
+  NTS_CHECK_ARG(ldx >= feature_size && ldy >= feature_size, "leading dimension < feature_size");
+  NTS_CHECK_ARG(p >= 0.f && p <= 1.f, "dropout probability must be in [0, 1]");
+  const uint32_t words = nts_hip_act_bits_words(feature_size);
+  if (words == 0) return NTS_ERR_UNSUPPORTED;
+  NTS_CHECK_ARG(pick_vec(feature_size, ldx, ldy, x, y) == 4 && (uintptr_t)mask_bits % 16 == 0,
+                "mask bits: 16-byte aligned rows with ld % 4 == 0");
+  if (v_cap == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  AggExtra ax;
+  ax.keep_threshold = dropout_threshold(p);
+  ax.scale = p >= 1.f ? 0.f : 1.0f / (1.0f - p);
+  ax.seed = seed;
+  ax.offset = offset;
+  ax.bits_out = mask_bits;
+  ax.ldb = words;
+  return launch_gather<false, false, kAggAct>(ctx->stream, column_offset, row_indices, weight, v,
+                                              v_cap, x, ldx, nullptr, feature_size, y, ldy,
+                                              Tier{nullptr, nullptr, 0, 0}, ax);
+}
+
+int nts_hip_spmm_csr_bwd_postmask_bits(nts_hip_ctx* ctx, const uint32_t* row_offset,
+                                       const uint32_t* column_indices,
+                                       const float* weight_backward, const uint32_t* s,
+                                       uint32_t s_cap, const float* g_out, uint64_t ld_gout,
+                                       const uint32_t* mask_bits, float scale,
+                                       uint32_t feature_size, float* g_in, uint64_t ld_gin) {
+  NTS_CHECK_ARG(ctx && row_offset && column_indices && g_out && mask_bits && g_in, "NULL argument");
+  NTS_CHECK_ARG(ld_gout >= feature_size && ld_gin >= feature_size,
+                "leading dimension < feature_size");
+  const uint32_t words = nts_hip_act_bits_words(feature_size);
+  if (words == 0) return NTS_ERR_UNSUPPORTED;
+  NTS_CHECK_ARG(pick_vec(feature_size, ld_gout, ld_gin, g_out, g_in) == 4 &&
+                    (uintptr_t)mask_bits % 16 == 0,
+                "mask bits: 16-byte aligned rows with ld % 4 == 0");
+  if (s_cap == 0) return NTS_OK;
+  NTS_HIP_TRY(hipSetDevice(ctx->device));
+  AggExtra ax;
+  ax.bits_in = mask_bits;
+  ax.ldb = words;
   ax.scale = scale;
   return launch_gather<false, false, kAggPostMask, true>(ctx->stream, row_offset, column_indices,
                                                          weight_backward, s, s_cap, g_out, ld_gout,

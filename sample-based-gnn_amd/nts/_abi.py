@@ -18,7 +18,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ["NTS_HIP_LIB"]) if os.environ.get("NTS_HIP_LIB") else _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 9  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 10  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
@@ -53,6 +53,7 @@ EXPORTED = (
     "nts_hip_h2_split_rows_planar", "nts_hip_gemm_h2p_tn_gather", "nts_hip_gemm_h2p_gather",
     "nts_hip_spmm_csr_bwd_postmask", "nts_hip_spmm_csr_bwd_colmax", "nts_hip_gemm_h2p_tn_gather_cm",
     "nts_hip_csr_bwd_colmax_rows_per_part", "nts_hip_gemm_h2d_act",
+    "nts_hip_act_bits_words", "nts_hip_spmm_csc_fwd_act_bits", "nts_hip_spmm_csr_bwd_postmask_bits",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -117,6 +118,9 @@ def lib() -> C.CDLL:
         "nts_hip_spmm_csc_fwd_act": ([P, P, P, P, P, U32, P, U64, U32, P, U64, F, U64, U64], I),
         "nts_hip_spmm_csr_bwd_masked": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
         "nts_hip_spmm_csr_bwd_postmask": ([P, P, P, P, P, U32, P, U64, P, U64, F, U32, P, U64], I),
+        "nts_hip_act_bits_words": ([U32], U32),
+        "nts_hip_spmm_csc_fwd_act_bits": ([P, P, P, P, P, U32, P, U64, U32, P, U64, F, U64, U64, P], I),
+        "nts_hip_spmm_csr_bwd_postmask_bits": ([P, P, P, P, P, U32, P, U64, P, F, U32, P, U64], I),
         "nts_hip_act_backward": ([P, U32, U32, P, U64, P, U64, F, P, U64], I),
         "nts_hip_presample_counts": ([P, C.POINTER(GraphDev), P, U32, I, P, P], I),
         "nts_hip_presample_select": ([P, P, U64, F, P, P], I),

@@ -146,6 +146,26 @@ class HipContext:
                                                 ptr(x), x.stride(0), F, ptr(y), y.stride(0),
                                                 float(p), int(seed), int(offset)))
 
+    def act_bits_words(self, F):
+        return int(self.lib.nts_hip_act_bits_words(F))
+
+    def spmm_csc_fwd_act_bits(self, co, ri, w, v_dev, v_cap, x, y, bits, p=0.0, seed=0, offset=0):
+        """spmm_csc_fwd_act that also writes the keep mask [y > 0] as bits
+        (act_bits_words(F) int32 words per row)."""
+        F = x.shape[1]
+        check(self.lib.nts_hip_spmm_csc_fwd_act_bits(self.h, ptr(co), ptr(ri), ptr(w), ptr(v_dev),
+                                                     v_cap, ptr(x), x.stride(0), F, ptr(y),
+                                                     y.stride(0), float(p), int(seed), int(offset),
+                                                     ptr(bits)))
+
+    def spmm_csr_bwd_postmask_bits(self, ro, ci, wb, s_dev, s_cap, g_out, bits, g_in, scale=1.0):
+        """spmm_csr_bwd_postmask with the mask from spmm_csc_fwd_act_bits."""
+        F = g_out.shape[1]
+        check(self.lib.nts_hip_spmm_csr_bwd_postmask_bits(self.h, ptr(ro), ptr(ci), ptr(wb),
+                                                          ptr(s_dev), s_cap, ptr(g_out),
+                                                          g_out.stride(0), ptr(bits), float(scale), F,
+                                                          ptr(g_in), g_in.stride(0)))
+
     def spmm_csr_bwd_postmask(self, ro, ci, wb, s_dev, s_cap, g_out, x_act, g_in, scale=1.0):
         """g_in = (A^T g_out) ⊙ (x_act > 0) * scale, x_act indexed by g_in's rows."""
         F = g_out.shape[1]

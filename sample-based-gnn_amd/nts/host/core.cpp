@@ -517,7 +517,13 @@ NtsVar SingleGPUAllSampleGraphOp::backward(NtsVar& g) {
   TORCH_CHECK(go.size(0) == (int64_t)sg->v_size, "output grad rows != v_size");
   if (sg->has_csr) {
     NtsVar gi = torch::empty({(int64_t)sg->src_size, F}, f32_opts(cuda_stream->device()));
-    if (sg->post_mask)  // the transform-first bottom layer's activation backward fused
+    if (sg->post_mask_bits)  // the same, the mask read as bits
+      hip_check(nts_hip_spmm_csr_bwd_postmask_bits(
+                    cuda_stream->ctx(), sg->dev_r_o(), sg->dev_c_i(), sg->dev_e_w_b(), nullptr,
+                    sg->src_size, go.data_ptr<float>(), (uint64_t)F, sg->post_mask_bits,
+                    sg->post_mask_scale, (uint32_t)F, gi.data_ptr<float>(), (uint64_t)F),
+                "nts_hip_spmm_csr_bwd_postmask_bits");
+    else if (sg->post_mask)  // the transform-first bottom layer's activation backward fused
       hip_check(nts_hip_spmm_csr_bwd_postmask(cuda_stream->ctx(), sg->dev_r_o(), sg->dev_c_i(),
                                               sg->dev_e_w_b(), nullptr, sg->src_size,
                                               go.data_ptr<float>(), (uint64_t)F, sg->post_mask,
@@ -817,11 +823,27 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     if (g_after_fwd_gemm) g_after_fwd_gemm();
     NtsVar X1 = torch::empty({v, N}, f32_opts(dev));
     if (prof) prof->begin(KernelProfiler::BOTTOM_AGG, st);
-    hip_check(nts_hip_spmm_csc_fwd_act(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
-                                       nullptr, (uint32_t)v, hp, (uint64_t)N, (uint32_t)N,
-                                       X1.data_ptr<float>(), (uint64_t)N, (float)p, (uint64_t)seed,
-                                       (uint64_t)offset),
-              "nts_hip_spmm_csc_fwd_act");
+    // the keep mask [X1 > 0] also as bits (16 B a 128-float row), which the
+    // graph op above reads in its fused activation backward instead of X1
+    const uint32_t words = nts_hip_act_bits_words((uint32_t)N);
+    if (words) {
+      const int64_t need = std::max<int64_t>((int64_t)sg->v_cap, 1) * words;
+      if (!sg->act_bits.defined() || sg->act_bits.numel() < need)
+        sg->act_bits = torch::empty({need}, torch::TensorOptions().dtype(torch::kInt32).device(
+                                                torch::kCUDA, dev));
+      hip_check(nts_hip_spmm_csc_fwd_act_bits(
+                    cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(), nullptr, (uint32_t)v,
+                    hp, (uint64_t)N, (uint32_t)N, X1.data_ptr<float>(), (uint64_t)N, (float)p,
+                    (uint64_t)seed, (uint64_t)offset,
+                    reinterpret_cast<uint32_t*>(sg->act_bits.data_ptr<int32_t>())),
+                "nts_hip_spmm_csc_fwd_act_bits");
+    } else {
+      hip_check(nts_hip_spmm_csc_fwd_act(cs->ctx(), sg->dev_c_o(), sg->dev_r_i(), sg->dev_e_w_f(),
+                                         nullptr, (uint32_t)v, hp, (uint64_t)N, (uint32_t)N,
+                                         X1.data_ptr<float>(), (uint64_t)N, (float)p,
+                                         (uint64_t)seed, (uint64_t)offset),
+                "nts_hip_spmm_csc_fwd_act");
+    }
     // compulsory bytes: each H row once, index + weight per edge, offsets, output
     if (prof)
       prof->end(KernelProfiler::BOTTOM_AGG, st,

@@ -395,6 +395,12 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
       if (hop >= 1) {
         sampCSC* up = sg->sampled_sgs[hop - 1];
         up->post_mask = fuse ? X.data_ptr<float>() : nullptr;
+        // (NTS_TF_MASK_FLOAT=1: the mask read from X1's rows, for A/B)
+        static const bool mask_float_env = getenv("NTS_TF_MASK_FLOAT") != nullptr;
+        up->post_mask_bits = fuse && !mask_float_env && s->act_bits.defined() &&
+                                     nts_hip_act_bits_words((uint32_t)X.size(1))
+                                 ? reinterpret_cast<const uint32_t*>(s->act_bits.data_ptr<int32_t>())
+                                 : nullptr;
         up->post_mask_ld = (uint64_t)X.stride(0);
         up->post_mask_scale = p < 1.0 ? 1.0f / (1.0f - (float)p) : 0.f;
       }

@@ -130,6 +130,8 @@ class sampCSC {
   const float* post_mask = nullptr;
   uint64_t post_mask_ld = 0;
   float post_mask_scale = 1.f;
+  const uint32_t* post_mask_bits = nullptr;  // that mask as bits (act_bits of the layer below)
+  torch::Tensor act_bits;  // transform-first bottom layer: its output's keep mask as bits
   bool grad_premasked = false;
 
   sampCSC(int device, VertexId v_cap, VertexId e_cap, VertexId s_cap, bool csr, bool weights);

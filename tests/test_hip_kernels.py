@@ -560,6 +560,151 @@ def test_spmm_csr_bwd_postmask(hip, cora, F):
     assert torch.isnan(got[s:]).all()
 
 
+@pytest.mark.gpu
+def test_spmm_csr_bwd_postmask_many_rows(hip):
+    """The post-mask CSR gather at hop-0 scale (200,000 rows of ~2 edges, empty
+    rows, and hub rows of 33-3,000 edges scattered over the blocks): a lane
+    group may take several rows (capped grid) — bit-identical to the plain CSR
+    backward (one row per group) followed by act_backward."""
+    g = torch.Generator(device=DEV).manual_seed(11)
+    s, v, F = 200_000, 10_000, 128
+    ln = torch.poisson(torch.full((s,), 1.8, device=DEV), generator=g).to(torch.int64)
+    hubs = torch.randint(0, s, (300,), device=DEV, generator=g)
+    ln[hubs] = torch.randint(33, 3000, (300,), device=DEV, generator=g)
+    ln[hubs[:40] // 64 * 64] = 40  # several long rows in one block
+    ro = torch.zeros(s + 1, dtype=torch.int64, device=DEV)
+    ro[1:] = torch.cumsum(ln, 0)
+    e = int(ro[-1])
+    ci = torch.randint(0, v, (e,), device=DEV, generator=g).to(torch.int32)
+    wb = torch.rand(e, device=DEV, generator=g)
+    ro = ro.to(torch.int32)
+    G = torch.randn(v, F, device=DEV, generator=g)
+    Xa = torch.relu(torch.randn(s, F, device=DEV, generator=g)) * 2
+    sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
+    plain = torch.empty(s, F, device=DEV)
+    hip.spmm_csr_bwd(ro, ci, wb, sdev, s, G, plain)
+    ref = torch.empty(s, F, device=DEV)
+    hip.act_backward(plain, Xa, ref, scale=2.0)
+    got = torch.full((s + 5, F), float("nan"), device=DEV)
+    hip.spmm_csr_bwd_postmask(ro, ci, wb, sdev, s + 5, G, Xa, got, scale=2.0)
+    torch.cuda.synchronize()
+    assert torch.equal(got[:s], ref)
+    assert torch.isnan(got[s:]).all()
+
+
+def _pack_act_bits(y, words):
+    """The keep mask [y > 0] in nts_hip_act_bits_words' layout: column j is
+    float4 f = j // 4, component q = j % 4, on lane l = f % LPD of chunk
+    c = f // LPD (LPD 32 up to 32 float4, else 64), word (h NCH + c) 4 + q with
+    h = l // 32, bit l % 32."""
+    rows, F = y.shape
+    nv = F // 4
+    lpd = 32 if nv <= 32 else 64
+    nch = 1 if lpd == 32 else (nv + 63) // 64
+    assert words == (lpd // 32) * nch * 4
+    j = np.arange(F)
+    f4, q = j // 4, j % 4
+    c, l = f4 // lpd, f4 % lpd
+    word = ((l // 32) * nch + c) * 4 + q
+    out = np.zeros((rows, words), dtype=np.uint64)
+    keep = (y > 0).astype(np.uint64)
+    for k in range(F):
+        out[:, word[k]] |= keep[:, k] << np.uint64(l[k] % 32)
+    return out.astype(np.uint32)
+
+
+def test_act_bits_words(hip):
+    assert [hip.act_bits_words(F) for F in (68, 128, 132, 256, 512, 1024, 2048)] == [4, 4, 8, 8, 16, 32, 64]
+    assert [hip.act_bits_words(F) for F in (0, 4, 41, 64, 130, 602, 2052)] == [0] * 7
+
+
+@pytest.mark.parametrize("F", [68, 128, 256, 512])
+def test_spmm_csc_fwd_act_bits(hip, cora, F):
+    """The forward that also writes its keep mask as bits: the output equal to
+    spmm_csc_fwd_act's, the bits equal to [y > 0] in the documented layout."""
+    V, src, dst = cora
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    _, l1 = o.sample(np.arange(2, V, 13, dtype=np.uint32))
+    rng = np.random.default_rng(F)
+    v, s = l1["v_size"], l1["src_size"]
+    X = _t(rng.standard_normal((s, F)).astype(np.float32))
+    vdev = torch.tensor([v], dtype=torch.int32, device=DEV)
+    args = (_t(l1["column_offset"]), _t(l1["row_indices"]), _t(l1["edge_weight_forward"]), vdev, v + 3, X)
+    ref = torch.empty(v + 3, F, device=DEV)
+    hip.spmm_csc_fwd_act(*args, ref, p=0.5, seed=9, offset=2)
+    W = hip.act_bits_words(F)
+    y = torch.empty(v + 3, F, device=DEV)
+    bits = torch.full(((v + 3) * W,), -1, dtype=torch.int32, device=DEV)
+    hip.spmm_csc_fwd_act_bits(*args, y, bits, p=0.5, seed=9, offset=2)
+    torch.cuda.synchronize()
+    assert torch.equal(y[:v], ref[:v])
+    got = bits.view(v + 3, W)[:v].cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, _pack_act_bits(y[:v].cpu().numpy(), W))
+    assert (bits.view(v + 3, W)[v:] == -1).all()  # rows past v untouched
+
+
+@pytest.mark.parametrize("F", [68, 128, 256, 512])
+def test_spmm_csr_bwd_postmask_bits(hip, cora, F):
+    """The post-mask CSR backward reading the forward's mask bits == the same
+    backward reading the forward's output rows, bit for bit."""
+    V, src, dst = cora
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    o = orc.Sampler(col, rows, in_d, out_d, [25, 10], rng_mode=orc.RNG_PHILOX, order_mode=orc.ORDER_DRAW)
+    l0, l1 = o.sample(np.arange(4, V, 11, dtype=np.uint32))
+    rng = np.random.default_rng(F + 5)
+    # the bottom layer l1 (dsts = l0's srcs) makes the activation, l0 backward reads it
+    v1, s1 = l1["v_size"], l1["src_size"]
+    X = _t(rng.standard_normal((s1, F)).astype(np.float32))
+    W = hip.act_bits_words(F)
+    Xa = torch.empty(v1, F, device=DEV)
+    bits = torch.empty(v1 * W, dtype=torch.int32, device=DEV)
+    hip.spmm_csc_fwd_act_bits(_t(l1["column_offset"]), _t(l1["row_indices"]), _t(l1["edge_weight_forward"]),
+                              torch.tensor([v1], dtype=torch.int32, device=DEV), v1, X, Xa, bits,
+                              p=0.3, seed=4, offset=1)
+    v, s = l0["v_size"], l0["src_size"]
+    assert s == v1
+    G = _t(rng.standard_normal((v, F)).astype(np.float32))
+    sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
+    ro, ci, wb = _t(l0["row_offset"]), _t(l0["column_indices"]), _t(l0["edge_weight_backward"])
+    ref = torch.empty(s, F, device=DEV)
+    hip.spmm_csr_bwd_postmask(ro, ci, wb, sdev, s, G, Xa, ref, scale=1.0 / 0.7)
+    got = torch.full((s + 2, F), float("nan"), device=DEV)
+    hip.spmm_csr_bwd_postmask_bits(ro, ci, wb, sdev, s + 2, G, bits, got, scale=1.0 / 0.7)
+    torch.cuda.synchronize()
+    assert torch.equal(got[:s], ref)
+    assert torch.isnan(got[s:]).all()
+
+
+@pytest.mark.gpu
+def test_spmm_csr_bwd_postmask_bits_many_rows(hip):
+    """The bits form at hop-0 scale with hub rows (block-cooperative sums)."""
+    g = torch.Generator(device=DEV).manual_seed(12)
+    s, v, F = 200_000, 10_000, 128
+    ln = torch.poisson(torch.full((s,), 1.8, device=DEV), generator=g).to(torch.int64)
+    hubs = torch.randint(0, s, (300,), device=DEV, generator=g)
+    ln[hubs] = torch.randint(33, 3000, (300,), device=DEV, generator=g)
+    ro = torch.zeros(s + 1, dtype=torch.int64, device=DEV)
+    ro[1:] = torch.cumsum(ln, 0)
+    e = int(ro[-1])
+    ci = torch.randint(0, v, (e,), device=DEV, generator=g).to(torch.int32)
+    wb = torch.rand(e, device=DEV, generator=g)
+    ro = ro.to(torch.int32)
+    G = torch.randn(v, F, device=DEV, generator=g)
+    Xa = torch.relu(torch.randn(s, F, device=DEV, generator=g))
+    W = hip.act_bits_words(F)
+    bits = torch.from_numpy(_pack_act_bits(Xa.cpu().numpy(), W).view(np.int32)).to(DEV).reshape(-1)
+    sdev = torch.tensor([s], dtype=torch.int32, device=DEV)
+    ref = torch.empty(s, F, device=DEV)
+    hip.spmm_csr_bwd_postmask(ro, ci, wb, sdev, s, G, Xa, ref, scale=2.0)
+    got = torch.empty(s, F, device=DEV)
+    hip.spmm_csr_bwd_postmask_bits(ro, ci, wb, sdev, s, G, bits, got, scale=2.0)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("F", [4, 40, 128, 512])
 def test_spmm_csr_bwd_colmax(hip, cora, F):
     """The CSR backward that also emits its output's column maxima per part of
