@@ -1070,11 +1070,24 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   __syncthreads();
   const float mm = red[0][0] + red[0][1] + red[0][2] + red[0][3];
   const float vv = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-  const float h = ceilf(4.f * sqrtf(vv)) + 8.f;
+// the window's half-width in sigmas (compile-time A/B; a Delta outside its
+// window, ~0.3 % of the chunks at 3, is walked out by the resolver): C2 --rng
+// mt 3.57-3.59 / 3.57-3.58 / 3.52-3.55 ms/step at 4 / 3.5 / 3 (r05_ax.sh)
+#ifndef NTS_MT_SIGMA
+#define NTS_MT_SIGMA 3.f
+#endif
+  const float h = ceilf(NTS_MT_SIGMA * sqrtf(vv)) + 8.f;
   const uint32_t lo = (uint32_t)fmaxf(0.f, floorf(mm - h));
   const uint32_t wn = min(kMtWmax, (uint32_t)(mm + h - (float)lo) + 1u);
   if (blockIdx.x == 0 && t == 0) win[k] = make_uint2(lo, wn);
+  // waves whose entries all lie past the window leave (no block barrier
+  // below): the last block of a window is ~half idle otherwise (3.60-3.62 ->
+  // 3.57-3.59 ms/step, r05_ax.sh)
+#ifdef NTS_MT_BLOCK_EXIT  // (A/B build: whole blocks only)
   if (blockIdx.x * 256u >= wn) return;
+#else
+  if (blockIdx.x * 256u + (uint32_t)(t & ~63) >= wn) return;
+#endif
   const uint32_t slot = blockIdx.x * 256u + t;
   const uint64_t a0 = *a0p;
   const MtWords W{ring, a0, (uint32_t)(gen_hi - a0)};
