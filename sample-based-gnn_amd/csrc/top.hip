@@ -55,15 +55,47 @@ struct TopArgs {
   uint32_t* cpart;    // LOSS with accuracy: [blocks] rows whose argmax is the label
 };
 
-__device__ __forceinline__ float grp_max(float v) {  // over the 16 lanes of a group
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
+// Reductions over the 16 lanes of a group (a DPP row) by DPP moves: the
+// partner of each step is lane ^ 1, lane ^ 2 (quad permutes), then the other
+// quad of the 8-lane half (half mirror) and the other half (row mirror) — the
+// pairing tree of an xor butterfly 1, 2, 4, 8, so every lane ends with the
+// same sum as that butterfly's.  (The butterfly by __shfl_xor is a chain of
+// ds_bpermute round trips: 4-8 us of each block's softmax phase,
+// NTS_TOP_TIMING.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kDppX1 = 0xB1, kDppX2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+__device__ __forceinline__ float grp_max(float v) {
+  v = fmaxf(v, dpp_f<kDppX1>(v));
+  v = fmaxf(v, dpp_f<kDppX2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  return fmaxf(v, dpp_f<kDppMirror>(v));
 }
 __device__ __forceinline__ float grp_sum(float v) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+  v += dpp_f<kDppX1>(v);
+  v += dpp_f<kDppX2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  return v + dpp_f<kDppMirror>(v);
+}
+// argmax over the group (first index among equal values)
+__device__ __forceinline__ void grp_argmax_step(float& best, int& bi, float ob, int oi) {
+  if (ob > best || (ob == best && oi < bi)) {
+    best = ob;
+    bi = oi;
+  }
+}
+__device__ __forceinline__ int grp_argmax(float best, int bi) {
+  grp_argmax_step(best, bi, dpp_f<kDppX1>(best), dpp_i<kDppX1>(bi));
+  grp_argmax_step(best, bi, dpp_f<kDppX2>(best), dpp_i<kDppX2>(bi));
+  grp_argmax_step(best, bi, dpp_f<kDppHalfMirror>(best), dpp_i<kDppHalfMirror>(bi));
+  grp_argmax_step(best, bi, dpp_f<kDppMirror>(best), dpp_i<kDppMirror>(bi));
+  return bi;
 }
 
 // Stage W into LDS as sW[k][Cp] (zero columns >= C): coalesced loads of the
@@ -277,15 +309,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent(TopArgs a) {
             best = lp[ct][v];
             bi = 16 * ct + i;
           }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          const float ob = __shfl_xor(best, o, kWave);
-          const int oi = __shfl_xor(bi, o, kWave);
-          if (ob > best || (ob == best && oi < bi)) {
-            best = ob;
-            bi = oi;
-          }
-        }
+        bi = grp_argmax(best, bi);
         ok += (i == 0 && tgt[v] >= 0 && bi == tgt[v]) ? 1u : 0u;
       }
 #pragma unroll
@@ -430,8 +454,8 @@ template <int NCT, bool LOSS, bool GRAD, bool VEC4>
 __global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
   constexpr int CP = 16 * NCT, NW = kTopWaves;
   extern __shared__ float smem[];
-  __shared__ float wl;
-  __shared__ uint32_t wc;
+  __shared__ float wl[NW];
+  __shared__ uint32_t wc[NW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int K = a.K, P = K + 4, nkt = K / 16;
@@ -440,6 +464,26 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
   float* zp = sY + 16 * P;         // [NW][16][CP] partial logits
   float* dz = zp + NW * 16 * CP;   // [16][CP]
   const int r0 = blockIdx.x * 16;
+#ifdef NTS_TOP_TIMING  // (probe builds: phase times of two blocks, printf)
+  uint64_t tt[8];
+  int nt_ = 0;
+  auto mark = [&] { tt[nt_++] = wall_clock64(); };
+#else
+  auto mark = [] {};
+#endif
+  mark();
+  // the rows' labels and the upstream gradient first: their global loads
+  // then overlap the staging instead of following the logits (a dependent
+  // memory latency of 4-6 us per block there, NTS_TOP_TIMING)
+  constexpr int VPW = 4 / NW;  // rows 4 g + v per lane group finished by this wave
+  static_assert(4 % NW == 0, "kTopWaves must divide 4");
+  int tgt[VPW];
+#pragma unroll
+  for (int vv = 0; vv < VPW; ++vv) {
+    const int r = r0 + 4 * g + w + vv * NW;
+    tgt[vv] = r < a.n ? (int)a.labels[r] : -1;
+  }
+  const float gl = GRAD ? (a.grad ? *a.grad : 1.0f) / (float)a.n : 0.f;
   {  // the tile's 16 rows, all threads (rows >= n are zero)
     constexpr int B = 8;
     if (VEC4) {
@@ -477,6 +521,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
   }
   stage_w<CP>(a, sW);
   __syncthreads();
+  mark();
   f32x4 z[NCT];
 #pragma unroll
   for (int ct = 0; ct < NCT; ++ct) z[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -497,90 +542,107 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) zp[(w * 16 + 4 * g + v) * CP + 16 * ct + i] = z[ct][v];
   __syncthreads();
+  mark();
+  // each wave finishes the rows 4 g + v of its own v (v = w, w + NW, ...): the
+  // logits' sum over the waves' k-splits, log_softmax twice (log_softmax2's
+  // arithmetic per row), the loss and accuracy terms and dZ — a quarter of the
+  // tile each (the whole tile on wave 0 was 4-6 us of every block, NTS_TOP_TIMING)
+  float lw = 0.f;
+  uint32_t okw = 0;
 #pragma unroll
-  for (int ct = 0; ct < NCT; ++ct)
+  for (int vv = 0; vv < VPW; ++vv) {
+    const int v = w + vv * NW;
+    float zv[NCT];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
+    for (int ct = 0; ct < NCT; ++ct) {
       float t = zp[(4 * g + v) * CP + 16 * ct + i];
 #pragma unroll
       for (int q = 1; q < NW; ++q) t += zp[(q * 16 + 4 * g + v) * CP + 16 * ct + i];
-      z[ct][v] = t;
+      zv[ct] = t;
     }
-  float lp[NCT][4], lp2[NCT][4];
-  log_softmax2<NCT>(z, a.C, i, lp, lp2);
-  int tgt[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int r = r0 + 4 * g + v;
-    tgt[v] = r < a.n ? (int)a.labels[r] : -1;
-  }
-  if (LOSS && w == 0) {
-    float l = 0.f;
-#pragma unroll
-    for (int v = 0; v < 4; ++v)
+    float lp[NCT], lp2[NCT];
+    {
+      float m = -INFINITY;
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
-        if (16 * ct + i == tgt[v]) l -= lp2[ct][v];
+        if (16 * ct + i < a.C) m = fmaxf(m, zv[ct]);
+      m = grp_max(m);
+      float sm = 0.f;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, kWave);
-    if (lane == 0) wl = l;
-    if (a.cpart) {  // getCorrect (toolkits/GCN_SAMPLE_ALLGPU.hpp:166-172), as k_top_xent
-      uint32_t ok = 0;
+      for (int ct = 0; ct < NCT; ++ct)
+        if (16 * ct + i < a.C) sm += expf(zv[ct] - m);
+      sm = grp_sum(sm);
+      const float lse = m + logf(sm);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
+      for (int ct = 0; ct < NCT; ++ct) lp[ct] = zv[ct] - lse;
+      float m2 = -INFINITY;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (16 * ct + i < a.C) m2 = fmaxf(m2, lp[ct]);
+      m2 = grp_max(m2);
+      float s2 = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (16 * ct + i < a.C) s2 += expf(lp[ct] - m2);
+      s2 = grp_sum(s2);
+      const float lse2 = m2 + logf(s2);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) lp2[ct] = lp[ct] - lse2;
+    }
+    if (LOSS) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+        if (16 * ct + i == tgt[vv]) lw -= lp2[ct];
+      if (a.cpart) {  // getCorrect (toolkits/GCN_SAMPLE_ALLGPU.hpp:166-172), as k_top_xent
         float best = -INFINITY;
         int bi = 0x7fffffff;
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct)
-          if (16 * ct + i < a.C && lp[ct][v] > best) {
-            best = lp[ct][v];
+          if (16 * ct + i < a.C && lp[ct] > best) {
+            best = lp[ct];
             bi = 16 * ct + i;
           }
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          const float ob = __shfl_xor(best, o, kWave);
-          const int oi = __shfl_xor(bi, o, kWave);
-          if (ob > best || (ob == best && oi < bi)) {
-            best = ob;
-            bi = oi;
-          }
-        }
-        ok += (i == 0 && tgt[v] >= 0 && bi == tgt[v]) ? 1u : 0u;
+        bi = grp_argmax(best, bi);
+        okw += (i == 0 && tgt[vv] >= 0 && bi == tgt[vv]) ? 1u : 0u;
       }
+    }
+    if (GRAD) {
+      const int r = r0 + 4 * g + v;
+      float d2[NCT], s2 = 0.f;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) ok += __shfl_down(ok, o, kWave);
-      if (lane == 0) wc = ok;
+      for (int ct = 0; ct < NCT; ++ct) {
+        d2[ct] = (16 * ct + i == tgt[vv]) ? -gl : 0.f;
+        s2 += d2[ct];
+      }
+      s2 = grp_sum(s2);
+      float d1[NCT], s1 = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const bool on = 16 * ct + i < a.C;
+        d1[ct] = on ? d2[ct] - expf(lp2[ct]) * s2 : 0.f;
+        s1 += d1[ct];
+      }
+      s1 = grp_sum(s1);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        const bool on = 16 * ct + i < a.C && r < a.n;
+        dz[(4 * g + v) * CP + 16 * ct + i] = on ? d1[ct] - expf(lp[ct]) * s1 : 0.f;
+      }
+    }
+  }
+  if (LOSS) {  // the wave's terms, then the block's in wave order (below)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lw += __shfl_down(lw, o, kWave);
+    if (lane == 0) wl[w] = lw;
+    if (a.cpart) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) okw += __shfl_down(okw, o, kWave);
+      if (lane == 0) wc[w] = okw;
     }
   }
   if (GRAD) {
-    if (w == 0) {
-      const float gl = (a.grad ? *a.grad : 1.0f) / (float)a.n;
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int r = r0 + 4 * g + v;
-        float d2[NCT], s2 = 0.f;
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-          d2[ct] = (16 * ct + i == tgt[v]) ? -gl : 0.f;
-          s2 += d2[ct];
-        }
-        s2 = grp_sum(s2);
-        float d1[NCT], s1 = 0.f;
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-          const bool on = 16 * ct + i < a.C;
-          d1[ct] = on ? d2[ct] - expf(lp2[ct][v]) * s2 : 0.f;
-          s1 += d1[ct];
-        }
-        s1 = grp_sum(s1);
-#pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-          const bool on = 16 * ct + i < a.C && r < a.n;
-          dz[(4 * g + v) * CP + 16 * ct + i] = on ? d1[ct] - expf(lp[ct][v]) * s1 : 0.f;
-        }
-      }
-    }
     __syncthreads();
+    mark();
     // dY [16 x K] = dZ W^T on this wave's k tiles, two at a time
     constexpr int KT = 2;
     for (int j0 = w; j0 < nkt; j0 += KT * NW) {
@@ -610,6 +672,7 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
         }
       }
     }
+    mark();
     // dW slab of this block [K x CP] = Y^T dZ, rows of this wave's k tiles
     const uint64_t nslab = gridDim.x, slab = blockIdx.x;
     for (int j0 = w; j0 < nkt; j0 += KT * NW) {
@@ -648,17 +711,32 @@ __global__ __launch_bounds__(kTopThreads) void k_top_xent_ks(TopArgs a) {
       }
     }
   }
+  mark();
   if (LOSS) {
     __syncthreads();
     if (threadIdx.x == 0) {
-      a.lpart[blockIdx.x] = wl;
-      if (a.cpart) a.cpart[blockIdx.x] = wc;
+      float l = 0.f;
+      uint32_t c = 0;
+      for (int q = 0; q < NW; ++q) {
+        l += wl[q];
+        c += wc[q];
+      }
+      a.lpart[blockIdx.x] = l;
+      if (a.cpart) a.cpart[blockIdx.x] = c;
     }
   }
+#ifdef NTS_TOP_TIMING
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  mark();
+  if ((blockIdx.x == 3 || blockIdx.x == gridDim.x - 5) && threadIdx.x == 64 && nt_ == 7)
+    printf("top blk %d: stage %d logits %d softmax %d dY %d dW %d tail %d (x10ns)\n", blockIdx.x,
+           (int)(tt[1] - tt[0]), (int)(tt[2] - tt[1]), (int)(tt[3] - tt[2]), (int)(tt[4] - tt[3]),
+           (int)(tt[5] - tt[4]), (int)(tt[6] - tt[5]));
+#endif
 }
 
 // Blocks [0, K*NCT): dW chunk (k, ct) = sum over the wave slabs — thread
-// (sg, i) sums slabs sg, sg+16, ... in order (8 loads in flight), then a fixed
+// (sg, i) sums slabs sg, sg+16, ... in order (40 loads in flight), then a fixed
 // pairwise tree over the 16 slab groups.  Block K*NCT (or 0 without GRAD):
 // loss = (sum of block partials, fixed tree) / n.
 template <int NCT>
@@ -674,7 +752,9 @@ __global__ __launch_bounds__(256) void k_top_finish(const float* __restrict__ pa
   if ((int)blockIdx.x < nchunks) {
     const int q = blockIdx.x, sg = t >> 4, i = t & 15;
     const float* p = part + (uint64_t)q * nslab * 16 + i;
-    constexpr int B = 8;
+    // every load of a thread in flight at once up to 640 slabs (C2: 625; the
+    // sum order is unchanged: z ascending)
+    constexpr int B = 40;
     for (int z = sg; z < nslab; z += 16 * B) {
       float v[B];
 #pragma unroll
