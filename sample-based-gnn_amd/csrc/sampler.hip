@@ -300,6 +300,23 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox(SelectArgs a) {
 constexpr int kGrp = 16;
 constexpr int kGrpPerWave = kWave / kGrp;
 
+// dup |= an earlier accepted lane J of the 16-lane group drew val (J < gl):
+// lane J of each 16-lane row by a DPP row broadcast (row_newbcast) instead of
+// __shfl's ds_bpermute — sampler alone 5.98-6.02 -> 6.04-6.07 G edges/s,
+// bit-identical (scripts/ab/r05_ba.sh)
+template <int J>
+struct GrpDupScan {
+  static __device__ __forceinline__ void run(bool& dup, uint32_t val, int gl, uint32_t okm) {
+    const uint32_t vj = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)val, 0x150 + J, 0xF, 0xF, false);
+    dup |= (J < gl) && ((okm >> J) & 1u) && (vj == val);
+    GrpDupScan<J + 1>::run(dup, val, gl, okm);
+  }
+};
+template <>
+struct GrpDupScan<kGrp> {
+  static __device__ __forceinline__ void run(bool&, uint32_t, int, uint32_t) {}
+};
+
 __global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a) {
   __shared__ uint32_t sets[kSelWaves * kGrpPerWave][kGrp];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -337,11 +354,7 @@ __global__ __launch_bounds__(kSelThreads) void k_select_philox_g16(SelectArgs a)
       bool dup = false;
       for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
       const uint32_t okm = (uint32_t)(__ballot(ok) >> gshift) & 0xFFFFu;
-#pragma unroll
-      for (int j = 0; j < kGrp; ++j) {
-        const uint32_t vj = (uint32_t)__shfl((int)val, j, kGrp);
-        dup |= (j < gl) && ((okm >> j) & 1u) && (vj == val);
-      }
+      GrpDupScan<0>::run(dup, val, gl, okm);
       const bool isnew = ok && !dup;
       const uint32_t newm = (uint32_t)(__ballot(isnew) >> gshift) & 0xFFFFu;
       uint32_t take = newm;
