@@ -119,8 +119,10 @@ __device__ __forceinline__ uint32_t select_distinct(const SelectArgs& a, uint32_
     bool dup = false;
     for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);  // LDS broadcast reads
     const uint64_t okmask = __ballot(ok);
+    // lane j's draw by v_readlane (a scalar broadcast), not __shfl's
+    // ds_bpermute round trip per j
     for (int j = 0; j < R; ++j) {
-      uint32_t vj = __shfl(val, j, kWave);
+      uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)val, j);
       dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
     }
     const bool isnew = ok && !dup;
@@ -204,7 +206,7 @@ __device__ uint32_t select_distinct_hashed(uint32_t need, uint32_t* hset, uint32
     bool dup = ok && hset_has(hset, mask, val);
     const uint64_t okmask = __ballot(ok);
     for (int j = 0; j < kWave; ++j) {
-      const uint32_t vj = __shfl(val, j, kWave);
+      const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)val, j);
       dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
     }
     const uint64_t newmask = __ballot(ok && !dup);
@@ -544,7 +546,7 @@ __device__ void mt_exact(MtStream& s, uint32_t* set, uint32_t* ans, uint32_t c, 
     for (uint32_t j = 0; j < count; ++j) dup |= (set[j] == val);
     const uint64_t okmask = __ballot(ok);
     for (int j = 0; j < R; ++j) {
-      const uint32_t vj = __shfl(val, j, kWave);
+      const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)val, j);
       dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
     }
     const bool isnew = ok && !dup;
@@ -636,7 +638,7 @@ __device__ void mt_exact_hashed(MtStream& s, uint32_t* tab, uint32_t* out, uint3
     bool dup = ok && hset_has(tab, mask, val);
     const uint64_t okmask = __ballot(ok);
     for (int j = 0; j < kWave; ++j) {
-      const uint32_t vj = __shfl(val, j, kWave);
+      const uint32_t vj = (uint32_t)__builtin_amdgcn_readlane((int)val, j);
       dup |= (j < lane) && ((okmask >> j) & 1ull) && (vj == val);
     }
     const uint64_t newmask = __ballot(ok && !dup);
