@@ -1121,16 +1121,23 @@ __global__ __launch_bounds__(256) void k_mtp_tables(const uint4* __restrict__ in
   constexpr int NW = NMAX + NTS_MT_NWX;
   constexpr int kU = 192;
   const int wvi = t >> 6, ln = t & 63;
-  auto wmin = [](uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, kWave));
-    return x;
+  // wave minimum / maximum (every lane active here): DPP moves within each
+  // 16-lane row, then the four rows' values by v_readlane — a few VALU
+  // cycles instead of six dependent ds_bpermute round trips per call (two
+  // calls per dst step)
+  auto row16 = [](uint32_t x, auto op) {
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false));
+    x = op(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false));
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0);
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32);
+    const uint32_t r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return op(op(r0, r1), op(r2, r3));
   };
-  auto wmax = [](uint32_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, kWave));
-    return x;
-  };
+  auto wmin = [&](uint32_t x) { return row16(x, [](uint32_t p, uint32_t q) { return min(p, q); }); };
+  auto wmax = [&](uint32_t x) { return row16(x, [](uint32_t p, uint32_t q) { return max(p, q); }); };
   uint32_t rw[kU / kWave];
   auto load_union = [&](uint32_t P) {
 #pragma unroll
