@@ -91,9 +91,23 @@ def default_cpu_threads() -> int:
     return max(1, n)
 
 
+# the NTS_* variables something on the measured path still reads: the
+# library (a launch-trace debug aid and the two MT19937 walker selections),
+# the host extension (two host-side timing aids), this script (an A/B library
+# path and the shared-GPU rehearsal); every other knob is a compile-time flag
+READ_ENV = ("NTS_LAUNCH_TRACE", "NTS_MT_SERIAL", "NTS_MT_CHUNKED", "NTS_HOST_PROFILE", "NTS_TIMELINE",
+            "NTS_HIP_LIB", "NTS_BENCH_SHARE_GPU")
+
+
 def nts_env() -> dict:
-    """Every NTS_* variable of this run (recorded in profile_meta)."""
-    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("NTS_")}
+    """The NTS_* variables of this run that are read (recorded in
+    profile_meta), and under "ignored" the names of any set that nothing reads
+    any more (former A/B knobs, now `make variant` flags)."""
+    env = {k: v for k, v in sorted(os.environ.items()) if k in READ_ENV}
+    ignored = sorted(k for k in os.environ if k.startswith("NTS_") and k not in READ_ENV)
+    if ignored:
+        env["ignored"] = ignored
+    return env
 
 
 def diag_env() -> list:
@@ -155,17 +169,65 @@ def launch_selftest(world: int, rank: int) -> None:
     """--launch-selftest: the launcher's control flow without a GPU — every
     rank joins a gloo group and rank 0 prints a line with the ranks that
     answered (tests/test_bench.py)."""
+    import torch
     import torch.distributed as dist
+    ar_us = None
     if world > 1:
         dist.init_process_group("gloo")
         ranks = [None] * world
         dist.all_gather_object(ranks, rank)
+        # the line's gradient-exchange fields, as the real run reports them:
+        # one SUM all-reduce of the C2 bucket (602*128 + 128*41 floats) per
+        # step, host wall time, max over ranks
+        bucket = torch.ones(602 * 128 + 128 * 41)
+        t = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            dist.all_reduce(bucket)
+            t.append(time.perf_counter() - t0)
+        m = torch.tensor([1e6 * sum(t) / len(t)], dtype=torch.float64)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        ar_us = float(m[0])
         dist.destroy_process_group()
     else:
         ranks = [0]
     if rank == 0:
         print(json.dumps({"metric": "launch-selftest", "value": 0.0, "n_gpus": world,
-                          "ranks": ranks}), flush=True)
+                          "ranks": ranks, "rccl_ranks": None,
+                          "config": {"allreduce_us_per_step": ar_us,
+                                     "allreduce_timing": {"how": "host wall time (gloo, CPU)"}}}),
+              flush=True)
+
+
+# flags of the parent run that a secondary child must not inherit: the
+# secondary machinery itself, the launcher, the CPU baseline and the extra
+# measurements only the headline run makes (value-taking flags map to True)
+_CHILD_DROP = {"--secondary": False, "--no-secondary-exact": False, "--no-secondary-mt": False,
+               "--no-secondary-af": False, "--gpus": True, "--no-cpu-baseline": False,
+               "--cpu-threads": True, "--cpu-max-steps": True, "--cpu-o0-steps": True,
+               "--epochs": True, "--sampler-batches": True, "--no-interference-probe": False,
+               "--launch-selftest": False}
+
+
+def child_argv(argv: list, overrides: dict) -> list:
+    """A secondary child's argv: the parent's own workload flags (argv, as
+    given on the command line) minus `_CHILD_DROP`, with every flag in
+    `overrides` ({"--rng": "mt", ...}) replaced, then `--secondary`."""
+    out, i = [], 0
+    while i < len(argv):
+        a = argv[i]
+        key, has_eq = (a.split("=", 1)[0], True) if a.startswith("--") and "=" in a else (a, False)
+        takes = _CHILD_DROP.get(key)
+        if key in overrides:
+            takes = True
+        if takes is None:
+            out.append(a)
+        elif takes and not has_eq:
+            i += 1  # drop the flag's value too
+        i += 1
+    for k, v in overrides.items():
+        out += [k, str(v)]
+    return out + ["--secondary"]
 
 
 def parse():
@@ -410,6 +472,9 @@ def main():
         step()
     drv.synchronize()
     drv.reset_stats()
+    if comm is not None:  # the gradient exchange's own time per step (below)
+        comm.timing_reset()
+        comm.set_timing(True)
 
     barrier()
     t0 = time.perf_counter()
@@ -419,6 +484,15 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     prof = drv.resolve_profile()
+    allreduce = None
+    if comm is not None:
+        comm.set_timing(False)
+        ar = comm.timing_stats()
+        allreduce = {"us_per_step": max_over_ranks(float(ar["us_per_call"])) if ar["calls"] else None,
+                     "calls": int(ar["calls"]),
+                     "how": ("HIP events around the RCCL call on the stream it runs on (max over ranks)"
+                             if ar["how"] == "hip-events" else
+                             "host wall time of the blocking host-transport call (max over ranks)")}
     edges_local = float(drv.batch_edges)
     sample_s = float(drv.sample_time)
     train_host_s = float(drv.train_time)
@@ -496,18 +570,10 @@ def main():
     # stream of its own in flight), so that no driver, stream or sampler of
     # the headline run sits beside it (measured in round 4: the MT secondary
     # read 5.1 ms/step beside them against 3.9 alone).
-    def child_secondary(extra: list, note: str):
-        cmd = [sys.executable, str(ROOT / "bench.py"), "--secondary",
-               "--shape", args.shape, "--batch", str(args.batch), "--fanout", args.fanout,
-               "--hidden", str(args.hidden), "--weight", args.weight, "--scale", str(args.scale),
-               "--train-limit", str(args.train_limit), "--steps", str(args.steps),
-               "--warmup", str(args.warmup), "--gemm", args.gemm, *extra]
-        if args.layers:
-            cmd += ["--layers", args.layers]
-        if args.no_pipeline:
-            cmd.append("--no-pipeline")
-        if args.atomic_backward:
-            cmd.append("--atomic-backward")
+    def child_secondary(overrides: dict, note: str):
+        # the parent's own workload flags (every flag the headline
+        # was run with, --rng / --no-pad-features / --cache-rate ... included)
+        cmd = [sys.executable, str(ROOT / "bench.py"), *child_argv(sys.argv[1:], overrides)]
         log(f"[bench] secondary ({note}): {' '.join(cmd[2:])}")
         t0 = time.time()
         r = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
@@ -538,14 +604,14 @@ def main():
             secondary = {
                 "bottom_layer": "aggregate-first (A X) W, the reference's order: fp32 aggregation "
                                 "bit-exact vs MiniBatchFuseOp, split-bf16 GEMMs (fp32-accurate)",
-                **child_secondary(["--transform-first", "0", "--pair-table", "0"],
+                **child_secondary({"--transform-first": 0, "--pair-table": 0},
                                   "the reference's bottom-layer order")}
         if args.pair_table == 0 and not args.no_secondary_exact:
             pair_tf = {
                 "bottom_layer": "transform-first A (X W) with the bottom-layer GEMMs on the feature "
                                 "table's f16 pair tables: 22-bit significand inputs (NARROWER than "
                                 "fp32), 3 f16 MFMA products, fp32 accumulate",
-                **child_secondary(["--transform-first", "1", "--pair-table", "3"],
+                **child_secondary({"--transform-first": 1, "--pair-table": 3},
                                   "f16 pair tables")}
     # the same workload on the reference's own generator stream (std::mt19937
     # + Lemire, every sampled array bit-exact vs the reference's serial order)
@@ -553,8 +619,7 @@ def main():
             and not args.no_secondary_mt and not args.secondary):
         mt_ref = {
             "rng": "std::mt19937(2000) + Lemire, the reference's stream (FastSampler::sample_fast)",
-            **child_secondary(["--rng", "mt", "--transform-first", str(args.transform_first),
-                               "--pair-table", str(args.pair_table)],
+            **child_secondary({"--rng": "mt"},
                               "the reference's MT19937 stream")}
 
     value = edges / elapsed
@@ -580,6 +645,8 @@ def main():
             "gradient_exchange": ("none (one rank)" if comm is None else
                                   "gloo host transport" if comm.host_transport else
                                   f"RCCL all-reduce, {rccl_ranks} ranks"),
+            "allreduce_us_per_step": allreduce["us_per_step"] if allreduce else None,
+            "allreduce_timing": allreduce,
             "training_stream_alone": alone,
             "fanout": args.fanout,
             "epoch_time_s": epoch_s,

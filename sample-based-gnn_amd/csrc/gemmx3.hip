@@ -170,6 +170,9 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
     sid[k] = amap ? amap[kbeg + min(k, klast)] : (uint32_t)(kbeg + min(k, klast));
   __syncthreads();
   const uint32_t lsx = x3_lds(sx), lsbr = x3_lds(sbr);
+#ifdef NTS_X3_PRIO
+  if (wv >= 4) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for the younger half
+#endif
   // this wave's DMA rows of a step: 2 wv, 2 wv + 1
   auto ids_read = [&](int s) { return *reinterpret_cast<const uint2*>(sid + 16 * s + 2 * wv); };
   auto ids_uni = [&](uint2 u) {
@@ -382,6 +385,9 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
   const int nsteps = (K + 31) / 32;
   const size_t bstride = (size_t)gridDim.y * kX3NnImg;
   const uint32_t lsb = x3_lds(sb), lsa = x3_lds(sa);
+#ifdef NTS_X3_PRIO
+  if (wv >= 4) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for the younger half
+#endif
   const char* bsrc = bimg + (size_t)nb * kX3NnImg + wv * 1024 + 16 * lane;
   // A DMA role: lane l loads row (l >> 1) & 15, floats 8 (l >> 5) + 4 (l & 1) (+ 16 h)
   const int gr = (lane >> 1) & 15, gpo = 8 * (lane >> 5) + 4 * (lane & 1);
@@ -588,6 +594,314 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
 }
 
 // ---------------------------------------------------------------------------
+// NN, round 6: k_x3_nn7 — the product of k_x3_nn (same fragments, same piece
+// order, same k order: bit-identical), reorganised so that the W image is
+// streamed once per 7 x 16 = 112 rows of every wave instead of once per 32,
+// and the gathered rows skip LDS:
+//   * 4-wave blocks, one wave per SIMD (up to 512 registers a lane); each
+//     wave owns the contiguous 16-row tiles [gw T / W, (gw+1) T / W), in
+//     rounds of RT = 7 tiles x 128 columns (224 accumulator registers); the
+//     MFMAs of a step are row-tile major (tile t's 48, then tile t+1's);
+//   * per 32-deep k-step the block shares one 24 KB W image in LDS (three
+//     buffers, 6 LDS-DMA pieces per wave and step, one barrier per step); the
+//     B fragments of column tile c+1 are read while column tile c's six MFMAs
+//     run (two register sets);
+//   * each wave's own A rows are loaded straight to registers (two 16-byte
+//     loads per lane, tile and step) one step ahead, and split into the three
+//     bf16 pieces one tile ahead of their MFMAs, one split instruction per
+//     MFMA slot;
+//   * the loads run on across rounds (the next round's first rows are in
+//     flight during a round's last step); the accumulators are stored at each
+//     round's end.
+// VMEM order per step g (W(g) in LDS buffer g % 3): tile t < RT-1 issues
+// kX3N7Wp[t] pieces of W(g+1), then the A loads of tile t+1 for step g+1;
+// tile RT-1 issues the A loads of tile 0 for step g+2 and, at its start,
+// waits for its own W(g+1) pieces (counted by hand: hipcc does not see the
+// LDS DMA) and meets the block's barrier — after which W(g+1) is visible and
+// every wave is done with step g-1, so buffer (g+2) % 3 (= W(g-1)'s) is free
+// for the next step's pieces.  hipcc's own waits for the A registers count
+// only its own loads (over-waiting by the W pieces: still >= 4 tiles of
+// slack).
+constexpr int kX3N7Threads = 256;
+constexpr int kX3N7RT = 7;
+constexpr int kX3N7Lds = 3 * kX3NnImg;  // 72 KB
+// W(g+1) pieces issued per tile (6 per wave and step: 24 KB / 4 waves)
+__device__ constexpr int kX3N7Wp[kX3N7RT] = {2, 2, 2, 0, 0, 0, 0};
+// after the last W piece (tile 2): tile 2's own A loads and tiles 3..5's
+constexpr int kX3N7WWait = 2 * (kX3N7RT - 1 - 2);
+// the piece set of each tile (consecutive tiles, the last tile and the next
+// step's first included, never share a set)
+__device__ constexpr int kX3N7Pb[kX3N7RT] = {0, 1, 2, 0, 1, 2, 1};
+
+// compile-time loop: f(integral_constant<int, I>) for I in [B, E)
+template <int B, int E, class F>
+__device__ __forceinline__ void x3_sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    x3_sfor<B + 1, E>(f);
+  }
+}
+
+// one of the 44 instructions of the exact split of 8 fp32 values x (one
+// lane's A fragment) into three packed bf16 pieces p[0..2][0..3]: the
+// instruction sequence of x3_split2 for four pairs in lock step, so that each
+// instruction's operands were produced at least four slots earlier
+template <int O>
+__device__ __forceinline__ void x3_split_op(const float (&x)[8], float (&r)[8], float (&f)[8],
+                                            uint32_t (&p)[3][4]) {
+  auto pk = [](float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((x3f2){a, b}, x3bf2));
+  };
+  if constexpr (O < 4) {  // x0 = bf16(x)
+    p[0][O] = pk(x[2 * O], x[2 * O + 1]);
+  } else if constexpr (O < 12) {  // back to fp32
+    constexpr int e = O - 4;
+    f[e] = __uint_as_float((e & 1) ? (p[0][e / 2] & 0xffff0000u) : (p[0][e / 2] << 16));
+  } else if constexpr (O < 20) {  // r = x - x0 (exact)
+    r[O - 12] = x[O - 12] - f[O - 12];
+  } else if constexpr (O < 24) {  // x1 = bf16(r)
+    p[1][O - 20] = pk(r[2 * (O - 20)], r[2 * (O - 20) + 1]);
+  } else if constexpr (O < 32) {
+    constexpr int e = O - 24;
+    f[e] = __uint_as_float((e & 1) ? (p[1][e / 2] & 0xffff0000u) : (p[1][e / 2] << 16));
+  } else if constexpr (O < 40) {  // r - x1 (exact)
+    r[O - 32] = r[O - 32] - f[O - 32];
+  } else if constexpr (O < 44) {  // x2 = bf16(r - x1) (exact)
+    p[2][O - 40] = pk(r[2 * (O - 40)], r[2 * (O - 40) + 1]);
+  }
+}
+
+// B fragments read this many column tiles ahead (NTS_X3N7_BQ: 1 or 2)
+#ifndef NTS_X3N7_BQ
+#define NTS_X3N7_BQ 1
+#endif
+// DIAG (timing probes, NTS_X3_DIAG in the probe build only; results are
+// garbage): 1 no MFMAs, 2 no splits, 4 no A loads after the prologue, 8 no B
+// fragment reads, 16 no W DMA after the prologue (and no wait for it), 32 no
+// barrier
+template <int RT, int DIAG = 0>
+__global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K, const float* __restrict__ X,
+                                                           uint64_t ldx, const uint32_t* __restrict__ amap,
+                                                           const char* __restrict__ bimg, float* __restrict__ C,
+                                                           uint64_t ldc, int rounds) {
+  static_assert(RT == kX3N7RT, "the W piece schedule is written for 7 tiles");
+  extern __shared__ __attribute__((aligned(16))) char x3n7[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, q = lane >> 4;
+  const int nb = blockIdx.y, n0 = nb * 128;
+  const int T = (M + 15) / 16;
+  const int64_t Wn = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + wv;
+  const int t_lo = (int)(gw * T / Wn), t_hi = (int)((gw + 1) * T / Wn);
+  const int nsteps = (K + 31) / 32;
+  const uint64_t bstride = (uint64_t)gridDim.y * kX3NnImg;
+  const uint32_t lsw = x3_lds(x3n7) + 6144 * wv;  // this wave's 6 KB share of a W buffer
+  const char* bsrc = bimg + (size_t)nb * kX3NnImg + 6144 * wv + 16 * lane;
+  // the lane's row id in tile slot rt of round rd (slots past the wave's
+  // tiles repeat its last tile: computed, never stored)
+  auto row_id = [&](int rd, int rt) -> uint32_t {
+    int t = min(t_lo + RT * rd + rt, max(t_hi, t_lo + 1) - 1);
+    t = min(t, T - 1);
+    int64_t r = (int64_t)t * 16 + i;
+    if (r >= M) r = M - 1;
+    const uint32_t id = amap ? amap[r] : (uint32_t)r;
+    return (DIAG & 64) ? (id & 1023u) : id;  // (probe: an L2-resident working set)
+  };
+  const float* ptr[RT];  // slot rt's rows (+ 8 q), in the round of its next load
+  uint32_t nid[RT];      // the next round's row ids
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) ptr[rt] = X + (uint64_t)row_id(0, rt) * ldx + 8 * q;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) nid[rt] = row_id(1, rt);
+#ifndef NTS_X3N7_WREG  // (A/B build -DNTS_X3N7_WREG: the W image staged through registers)
+  auto issue_w = [&](int s, int buf, int piece) {  // piece of W(k-step s) into buffer buf
+    x3_glds16(bsrc + (size_t)s * bstride + 1024 * piece, lsw + buf * kX3NnImg + 1024 * piece);
+  };
+#else
+  // the W image staged through registers: hipcc counts these loads with the
+  // A loads, so its waits for the A registers are exact (an LDS DMA it cannot
+  // see made every such wait cover six more loads)
+  // (all six pieces of W(g+1) loaded at the start of step g, before the A
+  // loads of step g: their wait at the step's last tile then forces no A
+  // load of this step — the VMEM counter is in order)
+  x3f4 wst[6];
+  char* const wdst = x3n7 + 6144 * wv + 16 * lane;
+  auto load_w = [&](int s, auto pc) {
+    constexpr int piece = decltype(pc)::value;
+    wst[piece] = *reinterpret_cast<const x3f4*>(bsrc + (size_t)s * bstride + 1024 * piece);
+  };
+  // (inline asm: a plain LDS store was hoisted to its load, waiting for it)
+  const uint32_t wdst_l = x3_lds(wdst);
+  auto store_w = [&](int buf, auto pc) {
+    constexpr int piece = decltype(pc)::value;
+    const uint32_t addr = wdst_l + buf * kX3NnImg;
+    const x3f4 v = wst[piece];
+    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "n"(1024 * piece) : "memory");
+  };
+#endif
+  float4 raw[RT][2];  // A fragments of one step (tile 0: the next step's)
+  auto load_a = [&](int rt, int s) {
+    const float* p = ptr[rt] + 32 * s;
+    raw[rt][0] = *reinterpret_cast<const float4*>(p);
+    raw[rt][1] = *reinterpret_cast<const float4*>(p + 4);
+  };
+  x3f4 acc[RT][8];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+  uint32_t pcs[3][3][4];  // split A pieces, tile t in pcs[kX3N7Pb[t]]
+  constexpr int NB = NTS_X3N7_BQ + 1;
+  x3bf8 bq[NB][3];        // B fragments, column tile c in bq[c % NB]
+  float sr[8], sf[8];     // split temporaries
+  auto read_b = [&](int buf, int ct, int p) {
+    return *reinterpret_cast<const x3bf8*>(x3n7 + buf * kX3NnImg + ct * 3072 + p * 1024 + 16 * lane);
+  };
+  // the pad past K (a step past it only, wave-uniform): zero the raw values
+  auto mask_k = [&](float (&x)[8], int s) {
+    if (32 * s + 32 > K) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = 32 * s + 8 * q + j < K ? x[j] : 0.f;
+    }
+  };
+  auto raw8 = [&](int rt, float (&x)[8]) {
+    x[0] = raw[rt][0].x; x[1] = raw[rt][0].y; x[2] = raw[rt][0].z; x[3] = raw[rt][0].w;
+    x[4] = raw[rt][1].x; x[5] = raw[rt][1].y; x[6] = raw[rt][1].z; x[7] = raw[rt][1].w;
+  };
+  // ---- prologue: W(0) -> buffer 0, A(0) of every tile; split tile 0; A(1)
+  // of tile 0; W(1) -> buffer 1 (ordered as one step's tile 6 -> tile 0)
+#ifndef NTS_X3N7_WREG
+#pragma unroll
+  for (int p = 0; p < 6; ++p) issue_w(0, 0, p);
+#else
+  x3_sfor<0, 6>([&](auto pc) {
+    load_w(0, pc);
+    store_w(0, pc);
+  });
+#endif
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) load_a(rt, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  x3_barrier();
+  {
+    float x[8];
+    raw8(0, x);
+    mask_k(x, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x3_split2(x[2 * j], x[2 * j + 1], pcs[0][0][j], pcs[0][1][j], pcs[0][2][j]);
+  }
+  load_a(0, 1);  // (nsteps >= 4)
+#pragma unroll
+  for (int c = 0; c < NTS_X3N7_BQ; ++c)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) bq[c][p] = read_b(0, c, p);
+  // ---- the steps of every round
+  int wb = 0;  // W(g)'s buffer
+  for (int rd = 0; rd < rounds; ++rd) {
+  for (int s = 0; s < nsteps; ++s) {
+    int s1 = s + 1, rd1 = rd;
+    if (s1 == nsteps) { s1 = 0; ++rd1; }
+    int s2 = s1 + 1, rd2 = rd1;
+    if (s2 == nsteps) { s2 = 0; ++rd2; }
+    const int wb1 = wb == 2 ? 0 : wb + 1;  // W(g+1)'s buffer
+    x3_sfor<0, RT>([&](auto rtc) {
+      constexpr int rt = decltype(rtc)::value;
+      constexpr int cur = kX3N7Pb[rt], nxt = kX3N7Pb[rt + 1 < RT ? rt + 1 : 0];
+      x3bf8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        a[p] = __builtin_bit_cast(x3bf8, (x3u4){pcs[cur][p][0], pcs[cur][p][1], pcs[cur][p][2], pcs[cur][p][3]});
+      // the raw values this tile splits: tile rt+1 of this step, or (last
+      // tile) tile 0 of the next step
+      constexpr int srt = rt + 1 < RT ? rt + 1 : 0;
+      const int ss = rt + 1 < RT ? s : s1;
+      float x[8];
+      if constexpr (rt + 1 == RT) {  // W(g+1) landed (own pieces), then the block's
+#ifndef NTS_X3N7_WREG
+        if constexpr (!(DIAG & 16)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kX3N7WWait) : "memory");
+#else
+        if constexpr (!(DIAG & 16)) x3_sfor<0, 6>([&](auto pc) { store_w(wb1, pc); });
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's W(g+1) stores
+#endif
+        if constexpr (!(DIAG & 32)) x3_barrier();  // and every wave's
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      raw8(srt, x);
+      mask_k(x, ss);
+      x3_sfor<0, 48>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int ct = k / 6, pr = k % 6;
+        __builtin_amdgcn_sched_barrier(0);
+        {  // slot k: product pr (small first) of column tile ct
+          constexpr int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
+          constexpr int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
+          if constexpr (DIAG & 1) acc[rt][ct][0] += (float)a[pa][0] + (float)bq[ct % NB][pb][1];
+          else acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ct % NB][pb], a[pa], acc[rt][ct], 0, 0, 0);
+        }
+        // the next column tile's B fragments (slots 6 ct .. 6 ct + 2): W(g)'s,
+        // or after the last column tile of the last tile W(g+1)'s column tile 0
+        if constexpr (pr < 3) {
+          constexpr int cn = ct + NTS_X3N7_BQ;  // the column tile read (8, 9: the next tile's 0, 1)
+          if constexpr (DIAG & 8) {
+          } else if constexpr (cn < 8) bq[cn % NB][pr] = read_b(wb, cn, pr);
+          else if constexpr (rt + 1 < RT) bq[(cn - 8) % NB][pr] = read_b(wb, cn - 8, pr);
+          else bq[(cn - 8) % NB][pr] = read_b(wb1, cn - 8, pr);
+        }
+        // one split instruction per slot (slots 1..44)
+        if constexpr (DIAG & 2) {
+          if constexpr (k >= 1 && k <= 12) pcs[nxt][(k - 1) / 4][(k - 1) % 4] = __float_as_uint(x[(k - 1) % 8]);
+        } else if constexpr (k >= 1 && k <= 44) x3_split_op<k - 1>(x, sr, sf, pcs[nxt]);
+        if constexpr (rt + 1 < RT) {
+          // W(g+1) pieces (buffer (g+1) % 3 held W(g-2): free since every
+          // wave passed step g-1's barrier)
+#ifndef NTS_X3N7_WREG
+          if constexpr (!(DIAG & 16) && kX3N7Wp[rt] > 0 && (k == 4 || k == 28)) issue_w(s1, wb1, 2 * rt + (k == 28));
+#else
+          // W(g+1) (tile 0, slots 2..7), stored into buffer (g+1) % 3 at tile RT-1
+          if constexpr (!(DIAG & 16) && rt == 0 && k >= 2 && k < 8)
+            load_w(s1, std::integral_constant<int, (k >= 2 && k < 8 ? k - 2 : 0)>{});
+#endif
+        }
+        // the split's r = x - x0 ran (slot 20): the raw registers are free
+        if constexpr (k == 22 && !(DIAG & 4)) {
+          if constexpr (rt + 1 < RT) {
+            if (s1 == 0 && rd1 < rounds) ptr[srt] = X + (uint64_t)nid[srt] * ldx + 8 * q;
+            load_a(srt, s1);
+          } else {
+            if (s2 == 0 && rd2 < rounds) ptr[0] = X + (uint64_t)nid[0] * ldx + 8 * q;
+            load_a(0, s2);
+          }
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    wb = wb1;
+  }
+    // round end: store the round's tiles, zero the accumulators, fetch the
+    // row ids of the round after next
+    {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int t = t_lo + RT * rd + rt;
+        const int64_t row = (int64_t)t * 16 + i;
+        if (t < t_hi && row < M) {
+#pragma unroll
+          for (int ct = 0; ct < 8; ++ct) {
+            const int col = n0 + 16 * ct + 4 * q;
+            if (col < N) *reinterpret_cast<x3f4*>(C + (uint64_t)row * ldc + col) = acc[rt][ct];
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) nid[rt] = row_id(rd + 2, rt);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the block
+}
+
+// ---------------------------------------------------------------------------
 // launchers (gemm3.hip's gemm3_tn / gemm3_nn try these first)
 
 // whole rows of at most 608 floats (Kp), 16-byte aligned, read as Kp floats
@@ -695,6 +1009,50 @@ int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint6
     hipLaunchKernelGGL((k_x3_nn<E, D>), grid, dim3(kX3Threads), kX3NnLds, ctx->stream, M, N, K, A, \
                        lda, amap, bimg, C, ldc, rounds, ep);                                      \
   } while (0)
+#ifndef NTS_X3_NN_V1  // (A/B builds: -DNTS_X3_NN_V1 keeps k_x3_nn for every call)
+  if (!epi && (K + 31) / 32 >= 4) {
+    // k_x3_nn7: 4-wave blocks, at most one per CU and column block, each wave
+    // kX3N7RT tiles a round
+    const int T7 = (M + 15) / 16;
+    const int gx7 = std::max(1, std::min(std::max(1, 256 / ncb), (T7 + 4 * kX3N7RT - 1) / (4 * kX3N7RT)));
+    const int64_t W7 = (int64_t)gx7 * 4;
+    const int tiles7 = (int)((T7 + W7 - 1) / W7);
+    const int rounds7 = (tiles7 + kX3N7RT - 1) / kX3N7RT;
+#define NTS_X3N7(D)                                                                              \
+  do {                                                                                           \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn7<kX3N7RT, D>),        \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kX3N7Lds));      \
+    hipLaunchKernelGGL((k_x3_nn7<kX3N7RT, D>), dim3(gx7, ncb), dim3(kX3N7Threads), kX3N7Lds,     \
+                       ctx->stream, M, N, K, A, lda, amap, bimg, C, ldc, rounds7);               \
+  } while (0)
+#ifdef NTS_PROBE_BUILD
+    static const int diag7 = [] {
+      const char* e = getenv("NTS_X3_DIAG");
+      return e ? atoi(e) : 0;
+    }();
+    switch (diag7) {
+      case 0: NTS_X3N7(0); break;
+      case 1: NTS_X3N7(1); break;
+      case 2: NTS_X3N7(2); break;
+      case 4: NTS_X3N7(4); break;
+      case 8: NTS_X3N7(8); break;
+      case 16: NTS_X3N7(16); break;
+      case 32: NTS_X3N7(32); break;
+      case 6: NTS_X3N7(6); break;
+      case 14: NTS_X3N7(14); break;
+      case 62: NTS_X3N7(62); break;
+      case 64: NTS_X3N7(64); break;
+      case 68: NTS_X3N7(68); break;
+      default: NTS_X3N7(63); break;
+    }
+#else
+    NTS_X3N7(0);
+#endif
+#undef NTS_X3N7
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
+#endif
 #ifdef NTS_PROBE_BUILD
   static const int diag = [] {
     const char* e = getenv("NTS_X3_DIAG");

@@ -159,6 +159,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              c.allreduce_sum(t.data_ptr<float>(), (uint64_t)t.numel(), (void*)stream);
            },
            py::arg("tensor"), py::arg("stream"))
+      .def("set_timing", &Communicator::set_timing, py::arg("on"))
+      .def("timing_reset", &Communicator::timing_reset)
+      .def("timing_stats",
+           [](Communicator& c) {
+             auto t = c.timing_stats();
+             py::dict d;
+             d["us_per_call"] = std::get<0>(t);
+             d["calls"] = std::get<1>(t);
+             d["how"] = std::get<2>(t);
+             return d;
+           })
       .def_readonly("nranks", &Communicator::nranks)
       .def_readonly("rank", &Communicator::rank);
 

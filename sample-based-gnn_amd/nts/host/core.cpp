@@ -875,9 +875,13 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
     uint32_t rpp = 0;
     // dZ = dX1 ⊙ mask once per dst row, then the plain CSR gather (measured
     // faster than applying the mask to every gathered row:
-    // nts_hip_spmm_csr_bwd_masked reads two rows per edge); NTS_TF_MASKED_BWD=1
-    // selects the fused form
-    static const bool fused_mask = getenv("NTS_TF_MASKED_BWD") != nullptr;
+    // nts_hip_spmm_csr_bwd_masked reads two rows per edge); the A/B build
+    // -DNTS_TF_MASKED_BWD selects the fused form
+#ifdef NTS_TF_MASKED_BWD
+    constexpr bool fused_mask = true;
+#else
+    constexpr bool fused_mask = false;
+#endif
     if (fused_mask && !sg->grad_premasked) {
       if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
       hip_check(nts_hip_spmm_csr_bwd_masked(cs->ctx(), sg->dev_r_o(), sg->dev_c_i(),
@@ -899,9 +903,13 @@ struct HipBottomTFFn : public torch::autograd::Function<HipBottomTFFn> {
                   "nts_hip_act_backward");
       if (prof) prof->begin(KernelProfiler::BOTTOM_BWD, st);
       // the planar-table TN GEMM takes dH's column maxima per part of rows
-      // from this gather's epilogue (one read of dH instead of two);
-      // NTS_TN_CHUNK_SCALES=1 keeps its own per-chunk pre-pass
-      static const bool chunk_scales = getenv("NTS_TN_CHUNK_SCALES") != nullptr;
+      // from this gather's epilogue (one read of dH instead of two); the A/B
+      // build -DNTS_TN_CHUNK_SCALES keeps its own per-chunk pre-pass
+#ifdef NTS_TN_CHUNK_SCALES
+      constexpr bool chunk_scales = true;
+#else
+      constexpr bool chunk_scales = false;
+#endif
       // (its float4 rows need 16-byte aligned dZ / dH rows: else the plain gather)
       const bool cm_rows = N <= 512 && N % 4 == 0 && (uintptr_t)dZ.data_ptr<float>() % 16 == 0 &&
                            (uintptr_t)dH.data_ptr<float>() % 16 == 0;
@@ -1317,7 +1325,29 @@ Communicator::Communicator(int n, int r, HostCollective host)
   TORCH_CHECK(host_ && n >= 1 && r >= 0 && r < n, "host collective: ranks");
 }
 Communicator::~Communicator() {
+  for (auto& e : tev_) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
   if (comm_) nts_hip_comm_destroy(comm_);
+}
+void Communicator::timing_reset() {
+  if (tused_) TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+  tused_ = 0;
+  host_us_ = 0;
+  host_calls_ = 0;
+}
+std::tuple<double, uint64_t, std::string> Communicator::timing_stats() {
+  if (host_) return {host_calls_ ? host_us_ / (double)host_calls_ : 0.0, host_calls_, "host-wall"};
+  double us = 0;
+  for (size_t i = 0; i < tused_; ++i) {
+    TORCH_CHECK(hipEventSynchronize(tev_[i].second) == hipSuccess, "hipEventSynchronize");
+    float ms = 0;
+    TORCH_CHECK(hipEventElapsedTime(&ms, tev_[i].first, tev_[i].second) == hipSuccess,
+                "hipEventElapsedTime");
+    us += 1e3 * ms;
+  }
+  return {tused_ ? us / (double)tused_ : 0.0, (uint64_t)tused_, "hip-events"};
 }
 void Communicator::host_call(float* buf, uint64_t n, void* stream, int op, int root) {
   TORCH_CHECK(hipStreamSynchronize((hipStream_t)stream) == hipSuccess, "hipStreamSynchronize");
@@ -1327,8 +1357,30 @@ void Communicator::host_call(float* buf, uint64_t n, void* stream, int op, int r
   TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
 }
 void Communicator::allreduce_sum(float* buf, uint64_t n, void* stream) {
-  if (host_) return host_call(buf, n, stream, 0, 0);
+  if (host_) {
+    const double t0 = now_s();
+    host_call(buf, n, stream, 0, 0);
+    if (timing_) {
+      host_us_ += 1e6 * (now_s() - t0);
+      ++host_calls_;
+    }
+    return;
+  }
+  if (timing_) {
+    if (tused_ == tev_.size()) {
+      hipEvent_t a, b;
+      TORCH_CHECK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence) == hipSuccess &&
+                      hipEventCreateWithFlags(&b, hipEventDisableSystemFence) == hipSuccess,
+                  "hipEventCreateWithFlags");
+      tev_.push_back({a, b});
+    }
+    TORCH_CHECK(hipEventRecord(tev_[tused_].first, (hipStream_t)stream) == hipSuccess, "hipEventRecord");
+  }
   hip_check(nts_hip_allreduce_sum_f32(comm_, buf, n, stream), "nts_hip_allreduce_sum_f32");
+  if (timing_) {
+    TORCH_CHECK(hipEventRecord(tev_[tused_].second, (hipStream_t)stream) == hipSuccess, "hipEventRecord");
+    ++tused_;
+  }
 }
 void Communicator::broadcast(float* buf, uint64_t n, int root, void* stream) {
   if (host_) return host_call(buf, n, stream, 1, root);

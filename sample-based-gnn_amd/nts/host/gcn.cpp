@@ -385,18 +385,26 @@ std::vector<NtsVar> GCN_SAMPLE_ALLGPU_impl::forward(SampledSubgraph* sg, bool ke
           F);
       // training: the graph op above applies this layer's relu/dropout
       // backward to its own backward output (one CSR pass instead of the CSR
-      // gather + nts_hip_act_backward; same arithmetic); NTS_TF_MASKED_BWD=1
-      // keeps the unfused masked gather for A/B
+      // gather + nts_hip_act_backward; same arithmetic); the A/B build
+      // -DNTS_TF_MASKED_BWD keeps the unfused masked gather
       // (only over a CSR: with the atomic CSC backward the layer above has
       // none, and this layer then runs nts_hip_act_backward itself)
-      static const bool masked_env = getenv("NTS_TF_MASKED_BWD") != nullptr;
+#ifdef NTS_TF_MASKED_BWD
+      constexpr bool masked_env = true;
+#else
+      constexpr bool masked_env = false;
+#endif
       const bool fuse = ctx.is_train() && !masked_env && hop >= 1 &&
                         sg->sampled_sgs[hop - 1]->has_csr;
       if (hop >= 1) {
         sampCSC* up = sg->sampled_sgs[hop - 1];
         up->post_mask = fuse ? X.data_ptr<float>() : nullptr;
-        // (NTS_TF_MASK_FLOAT=1: the mask read from X1's rows, for A/B)
-        static const bool mask_float_env = getenv("NTS_TF_MASK_FLOAT") != nullptr;
+        // (A/B build -DNTS_TF_MASK_FLOAT: the mask read from X1's rows)
+#ifdef NTS_TF_MASK_FLOAT
+        constexpr bool mask_float_env = true;
+#else
+        constexpr bool mask_float_env = false;
+#endif
         up->post_mask_bits = fuse && !mask_float_env && s->act_bits.defined() &&
                                      nts_hip_act_bits_words((uint32_t)X.size(1))
                                  ? reinterpret_cast<const uint32_t*>(s->act_bits.data_ptr<int32_t>())

@@ -519,11 +519,24 @@ class Communicator {
   // (-1, -1) for the host transport
   std::pair<int, int> rccl_count() const;
   int nranks, rank;
+  // Per-call timing of allreduce_sum (bench.py's allreduce_us_per_step):
+  // RCCL — a HIP event pair (no system fence) around the call on the stream it
+  // is enqueued on; host transport — the host wall time of the blocking call.
+  // timing_stats() synchronises the events: call outside timed regions.
+  void set_timing(bool on) { timing_ = on; }
+  void timing_reset();
+  // (mean microseconds per call, calls, "hip-events" | "host-wall")
+  std::tuple<double, uint64_t, std::string> timing_stats();
 
  private:
   void host_call(float* buf, uint64_t n, void* stream, int op, int root);
   nts_hip_comm* comm_ = nullptr;
   HostCollective host_;
+  bool timing_ = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> tev_;
+  size_t tused_ = 0;
+  double host_us_ = 0;
+  uint64_t host_calls_ = 0;
 };
 
 }  // namespace nts

@@ -127,6 +127,9 @@ def test_gpus_n_launches_n_ranks_itself():
     obj = json.loads(lines[0])
     assert obj["n_gpus"] == 2 and sorted(obj["ranks"]) == [0, 1]
     assert "torch.distributed.run" in obj["config"]["launcher"]
+    # an N-rank line carries the communicator's rank count and the
+    # gradient exchange's own time per step
+    assert "rccl_ranks" in obj and obj["config"]["allreduce_us_per_step"] > 0
 
 
 def test_world_size_must_match_gpus():
@@ -142,9 +145,31 @@ def test_diagnostic_knobs_are_refused():
 
 
 def test_nts_env_is_recorded(bench, monkeypatch):
-    monkeypatch.setenv("NTS_SCAN1", "0")
-    assert bench.nts_env()["NTS_SCAN1"] == "0"
+    monkeypatch.setenv("NTS_MT_SERIAL", "1")
+    monkeypatch.setenv("NTS_SCAN1", "0")  # a former knob, now a compile-time flag
+    env = bench.nts_env()
+    assert env["NTS_MT_SERIAL"] == "1" and "NTS_SCAN1" not in env
+    assert env["ignored"] == ["NTS_SCAN1"]
     assert bench.diag_env() == []
+
+
+def test_child_argv_keeps_the_workload(bench):
+    """A secondary child runs the parent's own workload: every
+    workload flag given to the parent (--rng, --no-pad-features, --cache-rate
+    ...) reaches the child, the secondary controls do not, and the overrides
+    replace the parent's value of the same flag."""
+    argv = ["--rng", "mt", "--no-pad-features", "--cache-rate", "0.3", "--steps", "7",
+            "--transform-first=1", "--no-secondary-mt", "--gpus", "1", "--cpu-threads", "4",
+            "--epochs", "2", "--sampler-gate", "1"]
+    out = bench.child_argv(argv, {"--transform-first": 0, "--pair-table": 0})
+    assert out[:7] == ["--rng", "mt", "--no-pad-features", "--cache-rate", "0.3", "--steps", "7"]
+    assert "--transform-first=1" not in out and out.count("--transform-first") == 1
+    assert out[out.index("--transform-first") + 1] == "0" and out[out.index("--pair-table") + 1] == "0"
+    for gone in ("--no-secondary-mt", "--gpus", "--cpu-threads", "--epochs"):
+        assert gone not in out
+    assert out[-1] == "--secondary" and out[out.index("--sampler-gate") + 1] == "1"
+    mt = bench.child_argv(["--rng", "philox", "--no-pad-features"], {"--rng": "mt"})
+    assert mt == ["--no-pad-features", "--rng", "mt", "--secondary"]
 
 
 def test_product_library_env_knobs():
@@ -159,3 +184,14 @@ def test_product_library_env_knobs():
     names = set(m.group(1).decode() for m in re.finditer(rb"\x00(NTS_[A-Z0-9_]+)\x00", lib.read_bytes()))
     assert names <= {"NTS_LAUNCH_TRACE", "NTS_MT_SERIAL", "NTS_MT_CHUNKED"}, names
     assert len(names) <= 10
+
+
+def test_host_extension_env_knobs():
+    """The C++ host layer reads only two timing aids (NTS_TF_* /
+    NTS_TN_CHUNK_SCALES are compile-time A/B flags since round 6)."""
+    import re
+    ext = ROOT / "sample-based-gnn_amd" / "nts" / "lib" / "host_build" / "nts_host_ext.so"
+    if not ext.exists():
+        pytest.skip("nts_host_ext.so not built")
+    names = set(m.group(1).decode() for m in re.finditer(rb"\x00(NTS_[A-Z0-9_]+)\x00", ext.read_bytes()))
+    assert names <= {"NTS_HOST_PROFILE", "NTS_TIMELINE"}, names

@@ -195,4 +195,6 @@ def test_bench_gpus_2_launches_two_ranks_on_one_gpu():
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["rccl_ranks"] is None
     assert line["config"]["gradient_exchange"] == "gloo host transport"
+    assert line["config"]["allreduce_us_per_step"] > 0
+    assert line["config"]["allreduce_timing"]["calls"] == 3
     assert line["config"]["global_batch"] == 256 and line["value"] > 0

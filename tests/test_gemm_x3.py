@@ -91,3 +91,37 @@ def test_x3_tn_wide_range(ctxs):
     scale = Xg.abs().t() @ G.double().abs() + 1e-300
     torch.cuda.synchronize()
     _check(C32, C3, ref, scale)
+
+
+@pytest.mark.parametrize("M,N,K,V", [(228656, 128, 602, 232965), (7 * 16 * 1024 * 3 + 37, 128, 602, 400000),
+                                     (257, 128, 602, 300), (5000, 64, 602, 6000), (2500, 256, 100, 4000),
+                                     (4000, 128, 97, 4100), (1000, 48, 129, 1200)])
+def test_x3_nn_gather_bitexact(ctxs, M, N, K, V):
+    """k_x3_nn7 (4-wave blocks, 7 row tiles a wave, A straight to registers,
+    rounds chained; the default for the un-fused gathered NN): the gathered
+    product equals the split GEMM of the gathered copy bit for bit (same
+    pieces, same piece and k order), over tile counts that leave the last
+    round short, several rounds, N below / above one 128-column block, K
+    with a pad step; NaN in the table's pad columns never reaches an output."""
+    f32, s3 = ctxs
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * K + N)
+    table = _table(V, K, g)
+    rows = torch.randint(0, V, (M,), device=DEV, generator=g).to(torch.int32)
+    rows, _ = torch.sort(rows)
+    W = torch.randn(K, N, device=DEV, generator=g)
+    C3 = torch.full((M, N), float("nan"), device=DEV)
+    s3.gemm_gather(table, rows, W, C3)
+    Xg = torch.empty(M, (K + 31) // 32 * 32, device=DEV)[:, :K]
+    Xg.copy_(table[rows.long()])
+    C3c = torch.empty(M, N, device=DEV)
+    s3.gemm(Xg, W, C3c)
+    torch.cuda.synchronize()
+    assert not torch.isnan(C3).any()
+    assert torch.equal(C3, C3c)
+    if M <= 300000:
+        C32 = torch.empty(M, N, device=DEV)
+        f32.gemm_gather(table, rows, W, C32)
+        ref = Xg.double() @ W.double()
+        scale = Xg.double().abs() @ W.double().abs() + 1e-30
+        torch.cuda.synchronize()
+        _check(C32, C3, ref, scale)
