@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define NTS_HIP_ABI_VERSION 10  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
+#define NTS_HIP_ABI_VERSION 11  /* 2: nts_sampcsc_dev gained dst_local_id, csr_edge_id;
                                   3: transform-first entry points, fused agg+GEMM removed,
                                      accuracy counts in the fused loss;
                                   4: PD cache entry points + omit fields, GEMM mode;
@@ -47,7 +47,9 @@ extern "C" {
                                   9: nts_sampcsc_dev::sizes_host;
                                   10: the activation's keep mask as bits (nts_hip_act_bits_words,
                                       nts_hip_spmm_csc_fwd_act_bits,
-                                      nts_hip_spmm_csr_bwd_postmask_bits) */
+                                      nts_hip_spmm_csr_bwd_postmask_bits);
+                                  11: MT19937 re-run of a short stream (nts_hip_mt_budget_scale,
+                                      nts_hip_mt_checkpoint, nts_hip_mt_rewind) */
 
 /* status codes */
 #define NTS_OK 0
@@ -185,6 +187,23 @@ int nts_hip_ctx_get_gemm_mode(nts_hip_ctx *ctx);
 int nts_hip_rng_seed(nts_hip_ctx *ctx, uint64_t seed);
 /* Copy the MT19937 state (624 words + position) to host; synchronises. */
 int nts_hip_rng_state(nts_hip_ctx *ctx, uint32_t *host_state625);
+/* MT19937 modes, recovery from a short stream (no reference counterpart: the
+ * reference's CPU generator, core/ntsFastSampler.hpp:200-205, is unbounded;
+ * the device replay generates each layer's words ahead up to a bound).
+ * A layer whose draws pass its bound reports it (sizes[3] bit 2) and leaves
+ * the generator where the layer began; the caller rewinds to the batch's
+ * checkpoint, scales the bound up and samples the batch again — bit-exact,
+ * the stream is the same.
+ *   nts_hip_mt_budget_scale: multiply every later layer's word bound by
+ *     `scale` (> 0; 1 = the coupon-collector mean x 1.05 + 131,072 words).
+ *   nts_hip_mt_checkpoint: enqueue (on the context's stream) a copy of the
+ *     generator state (625 u32: 624 words + position) into the DEVICE buffer
+ *     `dev_state625` — taken before a batch's first layer.
+ *   nts_hip_mt_rewind: synchronise the context's streams, make
+ *     `dev_state625` the generator state and restart the word ring from it. */
+int nts_hip_mt_budget_scale(nts_hip_ctx *ctx, double scale);
+int nts_hip_mt_checkpoint(nts_hip_ctx *ctx, uint32_t *dev_state625);
+int nts_hip_mt_rewind(nts_hip_ctx *ctx, const uint32_t *dev_state625);
 
 /* ---- graph preprocessing ----------------------------------------------- */
 /* Degrees from an edge list, clamped to >= 1:

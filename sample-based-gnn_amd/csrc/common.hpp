@@ -139,6 +139,7 @@ struct nts_hip_ctx {
   std::vector<std::pair<uint32_t, uint64_t>> mt_pending;    // (layer seq, word bound) not yet read back
   std::vector<std::pair<uint64_t, hipEvent_t>> mt_gen_evs;  // (blocks after, event) of generation launches
   std::vector<hipEvent_t> mt_ev_pool;
+  double mt_budget_scale = 1.0;        // x every layer's word bound (nts_hip_mt_budget_scale)
 };
 
 namespace nts_hip {
@@ -166,6 +167,7 @@ size_t scan1_state_elems(uint64_t n_cap);
 uint32_t scan_next_epoch(nts_hip_ctx* ctx);
 // MT19937 stream ring (sampler.hip): forget the generated stream (seeding)
 int mt_ring_reset(nts_hip_ctx* ctx);
+int mt_ring_rebase(nts_hip_ctx* ctx);
 void mt_ring_free(nts_hip_ctx* ctx);
 
 // The tile a look-back workgroup works on: its ticket in dispatch order, not

@@ -1741,12 +1741,50 @@ int mt_ring_prepare(nts_hip_ctx* ctx, uint64_t w_bound, hipStream_t st, uint64_t
   return NTS_OK;
 }
 
-uint64_t mt_word_bound(uint64_t e_cap, int fanout) {
+uint64_t mt_word_bound(uint64_t e_cap, int fanout, double scale) {
   if (fanout <= 0) return 131072;  // (no draws: every neighbour taken)
   double h = 0.0;  // H_{f+1} - 1
   for (int k = 2; k <= fanout + 1; ++k) h += 1.0 / k;
   const double per_edge = (double)(fanout + 1) * h / fanout;
-  return (uint64_t)std::ceil((double)e_cap * per_edge * 1.05) + 131072;
+  const double w = ((double)e_cap * per_edge * 1.05 + 131072.0) * scale;
+  return std::max<uint64_t>((uint64_t)std::ceil(w), 1024);
+}
+
+// The ring restarted from the generator state in ctx->mt_state (raw block B
+// holding the last word consumed, _M_p = p): ring block 0 = B tempered (word
+// p is the next to read), the generator continues from B (block 1 = twist(B)).
+__global__ __launch_bounds__(256) void k_mt_rebase(const uint32_t* __restrict__ st,
+                                                  uint32_t* __restrict__ ring,
+                                                  uint32_t* __restrict__ raw,
+                                                  uint64_t* __restrict__ done) {
+  for (int k = threadIdx.x; k < 624; k += 256) {
+    ring[k] = mt_temper(st[k]);
+    raw[k] = st[k];
+  }
+  if (threadIdx.x == 0) *done = (uint64_t)st[624];  // position p, layer seq 0
+}
+
+int mt_ring_rebase(nts_hip_ctx* ctx) {
+  NTS_RET(mt_ring_ensure(ctx));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->mt_gen_stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  hipLaunchKernelGGL(k_mt_rebase, dim3(1), dim3(256), 0, ctx->stream, ctx->mt_state, ctx->mt_ring,
+                     ctx->mt_gen_raw, ctx->mt_done);
+  NTS_LAUNCH_CHECK();
+  uint32_t p = 624;
+  NTS_HIP_TRY(hipMemcpyAsync(&p, ctx->mt_state + 624, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             ctx->stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  NTS_CHECK_ARG(p >= 1 && p <= 624, "MT19937 state: position out of range");
+  *ctx->mt_done_host = p;
+  ctx->mt_gen_blocks = 1;
+  ctx->mt_seq = 0;
+  ctx->mt_pos_done = p;
+  ctx->mt_seq_done = 0;
+  ctx->mt_pending.clear();
+  for (auto& e : ctx->mt_gen_evs) ctx->mt_ev_pool.push_back(e.second);
+  ctx->mt_gen_evs.clear();
+  return NTS_OK;
 }
 
 // after a layer's last MT kernel: its end position back to the host (pinned)
@@ -1822,7 +1860,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   // (H_{f+1} - 1) / f (f = 10: 2.22, 25: 2.97, 32: 3.18), so the bound
   // covers every degree profile's mean with 5 % and 131,072 words to spare
   // (the per-dst spread is ~sqrt(f) draws: invisible past a few dsts)
-  const uint64_t w_cap = mt_word_bound(o->e_cap, fanout);
+  const uint64_t w_cap = mt_word_bound(o->e_cap, fanout, ctx->mt_budget_scale);
   const uint64_t mt_info_n = rng_mode != NTS_RNG_PHILOX ? al((uint64_t)o->v_cap * 4) : 0;
   const uint64_t mt_base_n = mt_chunked ? al((uint64_t)o->v_cap + 1) : 0;
   const uint64_t mt_stat_n = mt_chunked ? al(2 * nch_cap) : 0;
@@ -2054,4 +2092,27 @@ frontier:
     NTS_LAUNCH_CHECK();
   }
   return NTS_OK;
+}
+
+extern "C" int nts_hip_mt_budget_scale(nts_hip_ctx* ctx, double scale) {
+  NTS_CHECK_ARG(ctx, "ctx is NULL");
+  NTS_CHECK_ARG(scale > 0.0 && scale < 1e6, "scale must be > 0");
+  ctx->mt_budget_scale = scale;
+  return NTS_OK;
+}
+
+extern "C" int nts_hip_mt_checkpoint(nts_hip_ctx* ctx, uint32_t* dev_state625) {
+  NTS_CHECK_ARG(ctx && dev_state625, "NULL argument");
+  NTS_HIP_TRY(hipMemcpyAsync(dev_state625, ctx->mt_state, 625 * sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, ctx->stream));
+  return NTS_OK;
+}
+
+extern "C" int nts_hip_mt_rewind(nts_hip_ctx* ctx, const uint32_t* dev_state625) {
+  NTS_CHECK_ARG(ctx && dev_state625, "NULL argument");
+  if (ctx->mt_gen_stream) NTS_HIP_TRY(hipStreamSynchronize(ctx->mt_gen_stream));
+  NTS_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  NTS_HIP_TRY(hipMemcpyAsync(ctx->mt_state, dev_state625, 625 * sizeof(uint32_t),
+                             hipMemcpyDeviceToDevice, ctx->stream));
+  return mt_ring_rebase(ctx);
 }

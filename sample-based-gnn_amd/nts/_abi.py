@@ -18,7 +18,7 @@ _HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = pathlib.Path(os.environ["NTS_HIP_LIB"]) if os.environ.get("NTS_HIP_LIB") else _HERE / "lib" / "libnts_hip.so"
 
 NTS_OK = 0
-ABI_VERSION = 10  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
+ABI_VERSION = 11  # NTS_HIP_ABI_VERSION of the header these ctypes structs mirror
 NTS_RNG_PHILOX = 0
 NTS_RNG_MT19937_LEMIRE = 1
 NTS_RNG_MT19937_DIV = 2
@@ -54,6 +54,7 @@ EXPORTED = (
     "nts_hip_spmm_csr_bwd_postmask", "nts_hip_spmm_csr_bwd_colmax", "nts_hip_gemm_h2p_tn_gather_cm",
     "nts_hip_csr_bwd_colmax_rows_per_part", "nts_hip_gemm_h2d_act",
     "nts_hip_act_bits_words", "nts_hip_spmm_csc_fwd_act_bits", "nts_hip_spmm_csr_bwd_postmask_bits",
+    "nts_hip_mt_budget_scale", "nts_hip_mt_checkpoint", "nts_hip_mt_rewind",
 )
 NTS_NOT_CACHED = 0xFFFFFFFF
 
@@ -108,6 +109,9 @@ def lib() -> C.CDLL:
         "nts_hip_ctx_get_gemm_mode": ([P], I),
         "nts_hip_ctx_reserve": ([P, U64, U64], I),
         "nts_hip_rng_seed": ([P, U64], I),
+        "nts_hip_mt_budget_scale": ([P, C.c_double], I),
+        "nts_hip_mt_checkpoint": ([P, P], I),
+        "nts_hip_mt_rewind": ([P, P], I),
         "nts_hip_rng_state": ([P, P], I),
         "nts_hip_degrees": ([P, P, P, U64, U64, P, P], I),
         "nts_hip_build_csc": ([P, P, P, U64, U64, P, P], I),

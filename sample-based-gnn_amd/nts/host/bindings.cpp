@@ -73,19 +73,41 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<PySampler>(m, "FastSampler")
       .def(py::init([](std::shared_ptr<FullyRepGraph> g, const torch::Tensor& seeds, int layers,
                        int batch, std::vector<int> fanout, int rng_mode, uint64_t seed,
-                       bool csr) {
+                       bool csr, int pipeline) {
              auto p = new PySampler();
              TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
              p->cs = std::make_unique<NtsStream>(g->device, nullptr, seed);
              auto guard = p->cs->guard();
              std::vector<bool> c(layers, csr);
-             p->s = std::make_unique<FastSampler>(g, to_ids(seeds), layers, batch, fanout, 1, c, true);
+             p->s = std::make_unique<FastSampler>(g, to_ids(seeds), layers, batch, fanout, pipeline,
+                                                  c, true);
              p->s->rng_mode = rng_mode;
              return p;
            }),
            py::arg("graph"), py::arg("seeds"), py::arg("layers"), py::arg("batch_size"),
            py::arg("fanout"), py::arg("rng_mode") = (int)NTS_RNG_PHILOX, py::arg("seed") = 2000,
-           py::arg("csr") = true)
+           py::arg("csr") = true, py::arg("pipeline") = 1)
+      // the split form (several slots in flight, finished in issue order)
+      .def("issue",
+           [](PySampler& p, int batch, int slot, WeightType w) {
+             auto guard = p.cs->guard();
+             p.s->issue_gpu_sample(batch, slot, *p.cs, w);
+           },
+           py::arg("batch_size"), py::arg("slot"), py::arg("weight_type") = WeightType::Sum)
+      .def("finish",
+           [](PySampler& p, int slot) {
+             auto guard = p.cs->guard();
+             auto out = layers_of(p.s->finish_gpu_sample(slot));
+             p.cs->synchronize();
+             return out;
+           },
+           py::arg("slot"))
+      // MT19937 modes: scale every later layer's word bound (tests force a
+      // short stream with a small scale; a re-run multiplies it by 4)
+      .def("set_mt_budget_scale",
+           [](PySampler& p, double scale) { p.s->set_mt_budget_scale(*p.cs, scale); })
+      .def_property_readonly("mt_budget_scale", [](PySampler& p) { return p.s->mt_budget_scale(); })
+      .def_property_readonly("mt_reruns", [](PySampler& p) { return p.s->mt_reruns; })
       .def("sample_gpu_fast",
            [](PySampler& p, int batch, WeightType w) {
              auto guard = p.cs->guard();

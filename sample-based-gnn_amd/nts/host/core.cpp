@@ -249,6 +249,7 @@ FastSampler::FastSampler(std::shared_ptr<FullyRepGraph> g, const std::vector<Ver
     ssgs.push_back(new SampledSubgraph(g->device, layers, fanout, batch_cap_, g->global_vertices,
                                        g->global_edges, csr_layers, weights, merge_src_dst));
   ssg = ssgs[0];
+  recs_.resize(ssgs.size());
   set_sample_nids(index);
   dev_iota_ = torch::arange((int64_t)batch_cap_ + 1, u32_opts(g->device));
 }
@@ -290,13 +291,46 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   // the whole issue loop; the event is normally complete already.
   if (ssgs.size() > 1) hip_rt(hipEventSynchronize(ssg->consumed), "hipEventSynchronize");
   hip_rt(hipStreamWaitEvent(st, ssg->consumed, 0), "hipStreamWaitEvent");
-  const nts_graph_dev g = whole_graph->dev();
   int wt = w == WeightType::Sum           ? NTS_WEIGHT_SUM
            : w == WeightType::Mean        ? NTS_WEIGHT_MEAN
            : w == WeightType::MeanSampled ? NTS_WEIGHT_MEAN_SAMPLED
                                           : NTS_WEIGHT_NONE;
   if (up_degree && wt != NTS_WEIGHT_NONE) wt |= NTS_WEIGHT_UP_DEGREE;
-  const VertexId* dst = dptr<VertexId>(dev_nids_) + work_offset;
+  // what a re-run of this batch needs (MT19937 modes: a short word stream)
+  IssueRec& r = recs_[ssg_id];
+  r.offset = work_offset;
+  r.actual = actual;
+  r.batch_seq = batch_seq;
+  r.wt = wt;
+  r.omit_map = omit_map;
+  r.omit_key = omit_key;
+  r.omit_loc = omit_loc;
+  r.cs = &cs;
+  if (rng_mode != NTS_RNG_PHILOX) {
+    if (!r.mt_ckpt.defined())
+      r.mt_ckpt = torch::empty({625}, u32_opts(whole_graph->device));
+    // the generator state before the batch's first layer (stream order)
+    hip_check(nts_hip_mt_checkpoint(cs.ctx(), dptr<uint32_t>(r.mt_ckpt)), "nts_hip_mt_checkpoint");
+  }
+  issued_.push_back(ssg_id);
+  enqueue_layers(ssg_id, r);
+  if (host_profile()) fprintf(stderr, "[host] issue total: %.1f us\n", (now_s() - t0) * 1e6);
+  ssg->pending_batch = (int)actual;
+  work_offset += actual;
+  ++batch_seq;
+  all_time += now_s() - t0;
+}
+
+// the batch's sampling kernels (every layer) on the record's stream
+void FastSampler::enqueue_layers(int ssg_id, const IssueRec& r) {
+  ssg = ssgs[ssg_id];
+  NtsStream& cs = *r.cs;
+  hipStream_t st = (hipStream_t)cs.stream();
+  const nts_graph_dev g = whole_graph->dev();
+  const int wt = r.wt;
+  const VertexId actual = r.actual;
+  const uint64_t bseq = r.batch_seq;
+  const VertexId* dst = dptr<VertexId>(dev_nids_) + r.offset;
   sampCSC* s0 = ssg->sampled_sgs[0];
   // layer-0 v_size as a device scalar without a per-batch memset: entry
   // `actual` of the device table 0..batch_cap
@@ -324,21 +358,21 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
     o.dst_local_id = dptr<uint32_t>(s->dst_local_id);  // undefined (NULL) unless merged
     o.csr_edge_id = dptr<uint32_t>(s->csr_edge_id);
     o.sizes_host = ssg->host_sizes_dev + 4 * l;
-    if (l == layer - 1 && omit_map) {
+    if (l == layer - 1 && r.omit_map) {
       if (!s->omit_row.defined())
         s->omit_row = torch::empty({std::max<int64_t>(s->v_cap, 1)}, u32_opts(whole_graph->device));
-      o.omit_map = omit_map;
-      o.omit_key = omit_key;
-      o.omit_loc = omit_loc;
+      o.omit_map = r.omit_map;
+      o.omit_key = r.omit_key;
+      o.omit_loc = r.omit_loc;
       o.omit_row = dptr<uint32_t>(s->omit_row);
     }
     const double tl = now_s();
-    hip_check(nts_hip_sample_layer(cs.ctx(), &g, fanout[l], l, batch_seq, rng_mode, wt, &o),
+    hip_check(nts_hip_sample_layer(cs.ctx(), &g, fanout[l], l, bseq, rng_mode, wt, &o),
               "nts_hip_sample_layer");
     if (host_profile()) fprintf(stderr, "[host] sample_layer %d: %.1f us\n", l, (now_s() - tl) * 1e6);
     // the reference keeps the destination as a view of the previous source
     if (l == 0)
-      s->destination = dev_nids_.narrow(0, work_offset, std::max<int64_t>(actual, 0));
+      s->destination = dev_nids_.narrow(0, r.offset, std::max<int64_t>(actual, 0));
     else
       s->destination = ssg->sampled_sgs[l - 1]->source;
     dst = o.source;
@@ -347,11 +381,38 @@ void FastSampler::issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, We
   // the layers' sizes reach host_sizes from their last kernels (the reference
   // syncs twice per layer; a D2H copy here cost a blit kernel per batch)
   hip_rt(hipEventRecord(ssg->sampled, st), "hipEventRecord");
-  if (host_profile()) fprintf(stderr, "[host] issue total: %.1f us\n", (now_s() - t0) * 1e6);
-  ssg->pending_batch = (int)actual;
-  work_offset += actual;
-  ++batch_seq;
-  all_time += now_s() - t0;
+}
+
+void FastSampler::set_mt_budget_scale(NtsStream& cs, double scale) {
+  mt_budget_ = scale;
+  hip_check(nts_hip_mt_budget_scale(cs.ctx(), scale), "nts_hip_mt_budget_scale");
+}
+
+// MT19937 modes: a layer's draws passed the words generated for it (its
+// bound, nts_hip_mt_budget_scale).  That layer left the generator where it
+// began, so every layer after it — of this batch and of the batches issued
+// behind it — read the stream from the wrong word.  Re-run from the batch's
+// checkpoint with every bound scaled up: the batch and each one issued after
+// it, in order (the same stream, so the same, reference-exact sets).
+void FastSampler::rerun_from(int ssg_id) {
+  TORCH_CHECK(rng_mode != NTS_RNG_PHILOX, "only the MT19937 modes can fall short");
+  TORCH_CHECK(rerun_ok, "a short MT19937 stream with work chained to the sampled batches "
+              "(early aggregation): cannot re-run");
+  auto it = std::find(issued_.begin(), issued_.end(), ssg_id);
+  TORCH_CHECK(it != issued_.end(), "re-run of a batch that is not pending");
+  IssueRec& r0 = recs_[ssg_id];
+  NtsStream& cs = *r0.cs;
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
+  mt_budget_ = std::min(mt_budget_ * 4.0, 1e4);
+  hip_check(nts_hip_mt_budget_scale(cs.ctx(), mt_budget_), "nts_hip_mt_budget_scale");
+  hip_check(nts_hip_mt_rewind(cs.ctx(), dptr<uint32_t>(r0.mt_ckpt)), "nts_hip_mt_rewind");
+  ++mt_reruns;
+  for (auto j = it; j != issued_.end(); ++j) {
+    IssueRec& r = recs_[*j];
+    hip_check(nts_hip_mt_checkpoint(r.cs->ctx(), dptr<uint32_t>(r.mt_ckpt)), "nts_hip_mt_checkpoint");
+    enqueue_layers(*j, r);
+  }
+  TORCH_CHECK(hipDeviceSynchronize() == hipSuccess, "hipDeviceSynchronize");
 }
 
 SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
@@ -360,16 +421,22 @@ SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
   TORCH_CHECK(ssg->pending_batch > 0, "finish_gpu_sample without a pending issue");
   hip_rt(hipEventSynchronize(ssg->sampled), "hipEventSynchronize");
   if (host_profile()) fprintf(stderr, "[host] finish wait: %.1f us\n", (now_s() - t0) * 1e6);
-  ssg->pending_batch = 0;
   const volatile int32_t* hs = ssg->host_sizes;
+  for (int attempt = 0;; ++attempt) {
+    bool short_stream = false;
+    for (int l = 0; l < layer; ++l) short_stream |= (hs[4 * l + 3] & 4) != 0;
+    if (!short_stream) break;
+    TORCH_CHECK(attempt < 8, "the MT19937 word stream fell short ", attempt + 1,
+                " times for one batch (bound scale ", mt_budget_, ")");
+    rerun_from(ssg_id);  // synchronises
+  }
+  ssg->pending_batch = 0;
+  issued_.erase(std::find(issued_.begin(), issued_.end(), ssg_id));
   for (int l = 0; l < layer; ++l) {
     sampCSC* s = ssg->sampled_sgs[l];
     s->v_size = (VertexId)hs[4 * l];
     s->e_size = (VertexId)hs[4 * l + 1];
     s->src_size = (VertexId)hs[4 * l + 2];
-    TORCH_CHECK((hs[4 * l + 3] & 4) == 0, "sampled layer ", l,
-                ": the MT19937 word stream generated for the layer fell short of the words "
-                "its rejection draws consumed (the generator state is not advanced)");
     TORCH_CHECK(hs[4 * l + 3] == 0, "sampled layer ", l, " exceeded its capacity");
     sampled_edges += s->e_size;
   }

@@ -157,6 +157,7 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
   // sampling, on the sampling stream: with the pipeline it runs while the
   // previous batch trains (HBM-bound gather next to MFMA-bound GEMMs).
   early_ = cfg.early_aggregate && cfg.fused_gather && !cfg.gat && !tf_ && !cfg.pd_cache;
+  sampler->rerun_ok = !early_;  // (an MT re-run would leave the early aggregation stale)
   if (cfg.pd_cache) {
     TORCH_CHECK(!cfg.gat && L >= 2 && cfg.hip_gemm && cfg.pd_super_batch >= 1 &&
                     cfg.pd_rate >= 0.0,

@@ -21,6 +21,7 @@
 #include <memory>
 #include <stack>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include "nts_hip.h"
@@ -250,6 +251,13 @@ class FastSampler {
   // event (recorded by the trainer) — issue makes `cs` wait for it.
   void issue_gpu_sample(int batch_size, int ssg_id, NtsStream& cs, WeightType w);
   SampledSubgraph* finish_gpu_sample(int ssg_id);
+  // MT19937 modes: a batch whose word stream fell short is sampled again
+  // from its checkpoint with larger bounds (finish_gpu_sample does it; the
+  // batches issued behind it are re-run too).  rerun_ok = false when work
+  // chained to the sampled batches on the sampler stream (the driver's early
+  // aggregation) would have to be re-done as well: then a short stream throws.
+  bool rerun_ok = true;
+  uint64_t mt_reruns = 0;  // batches re-run so far (tests)
   bool sample_not_finished() const { return work_offset < work_range[1]; }
   void restart() { work_offset = work_range[0]; }
   void set_sample_nids(const std::vector<VertexId>& ids);
@@ -263,8 +271,27 @@ class FastSampler {
   // HBM, the rest zero-copy from the pinned host table, in one kernel
   void load_feature_gpu_cache(NtsStream& cs, SampledSubgraph* sg, NtsVar& local_feature,
                               const FeatureCache& cache);
+  // MT19937 modes: every later layer's word bound x scale (tests force a short
+  // first stream with a small one; each re-run multiplies it by 4)
+  void set_mt_budget_scale(NtsStream& cs, double scale);
+  double mt_budget_scale() const { return mt_budget_; }
 
  private:
+  struct IssueRec {  // one pending batch per slot: what a re-run needs
+    VertexId offset = 0, actual = 0;
+    uint64_t batch_seq = 0;
+    int wt = 0;
+    const uint32_t* omit_map = nullptr;
+    uint32_t omit_key = 0;
+    const uint32_t* omit_loc = nullptr;
+    NtsStream* cs = nullptr;
+    torch::Tensor mt_ckpt;  // device u32 [625]: the generator before the batch
+  };
+  std::vector<IssueRec> recs_;
+  std::deque<int> issued_;  // slots issued and not yet finished, in issue order
+  double mt_budget_ = 1.0;
+  void enqueue_layers(int ssg_id, const IssueRec& r);
+  void rerun_from(int ssg_id);
   torch::Tensor dev_nids_;  // device copy of sample_nids
   torch::Tensor dev_iota_;  // 0, 1, ..., batch_cap: device scalars for the layer-0 v_size
   VertexId batch_cap_ = 0;

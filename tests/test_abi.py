@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
                          text=True, check=True).stdout
     exported = set(re.findall(r"\bT (nts_hip_\w+)", out))
     assert set(header_symbols()) <= exported
-    assert lib.nts_hip_abi_version() == _abi.ABI_VERSION == 10
+    assert lib.nts_hip_abi_version() == _abi.ABI_VERSION == 11
 
 
 def test_library_is_gfx950_code_object():

@@ -232,6 +232,47 @@ def test_c2_mt19937_reference_stream_full_batch(E):
     _free()
 
 
+def test_c2_mt19937_short_stream_reruns(E):
+    """A layer whose MT19937 draws outrun the words generated for it is not
+    fatal: the first bounds are forced 20x too small
+    (nts_hip_mt_budget_scale), three C2 batches (B = 10,000, 25-10) are issued
+    into three slots ahead of the first finish — the pipelined driver's order
+    — and finishing the first one rewinds the generator to its checkpoint,
+    raises the bounds and samples it and the two behind it again.  Every batch
+    (and two more, sampled synchronously) bit-exact vs the oracle's
+    std::mt19937(2000) walk, and the generator state identical after the
+    last: the re-runs read the same stream (core/ntsFastSampler.hpp:200-205,
+    962-1140)."""
+    from nts import synthetic
+    g, F, C = synthetic.shaped("reddit", device=DEV)
+    V = g.n_vertices
+    G = E.FullyRepGraph.from_edges(g.src, g.dst, V)
+    del g
+    fan, B, nb = [25, 10], 10_000, 5
+    rng = np.random.default_rng(21)
+    perm = rng.permutation(V).astype(np.int32)[:nb * B]
+    fs = E.FastSampler(G, torch.from_numpy(perm), 2, B, fan, rng_mode=1, seed=2000, pipeline=3)
+    fs.set_mt_budget_scale(0.05)
+    col = G.column_offset.cpu().numpy().view(np.uint64)
+    rows = G.row_indices.cpu().numpy().view(np.uint32)
+    o = orc.Sampler(col, rows, _np(G.in_degree), _np(G.out_degree), fan, seed=2000,
+                    rng_mode=orc.RNG_MT_LEMIRE, order_mode=orc.ORDER_DRAW)
+    for slot in range(3):
+        fs.issue(B, slot)
+    for b in range(nb):
+        if b < 3:
+            got = fs.finish(b)
+        else:
+            fs.issue(B, b % 3)
+            got = fs.finish(b % 3)
+        _compare_oracle(got, o.sample(perm[b * B:(b + 1) * B].view(np.uint32), b))
+        if b == 0:
+            assert fs.mt_reruns >= 1 and fs.mt_budget_scale > 0.05, (fs.mt_reruns, fs.mt_budget_scale)
+    assert np.array_equal(_np(fs.rng_state()), o.mt_state())
+    del fs, got, G
+    _free()
+
+
 def test_c2_mt19937_stream_ring_wraps(E):
     """The MT19937 stream ring (2^25 tempered words on the device, generated
     ahead of the layers that read them) wrapping around: 24 consecutive C2
