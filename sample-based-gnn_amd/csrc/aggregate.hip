@@ -398,7 +398,19 @@ __global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(NCH
       wt = w ? __builtin_nontemporal_load(w + b + sl) : 1.0f;
     }
   };
+#ifdef NTS_AGG_XCD
+  // (A/B build: XCD-aware block order — the blocks one XCD runs, b % 8 under
+  // round-robin placement, take one contiguous eighth of the dsts, so each
+  // XCD's L2 sees one dst range's sources; bijective for any grid)
+  uint32_t bid = blockIdx.x;
+  if constexpr (!CM) {
+    const uint32_t q8 = gridDim.x / 8, r8 = gridDim.x % 8, x8 = blockIdx.x % 8;
+    bid = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + blockIdx.x / 8;
+  }
+  uint32_t d = bid * GPB + grp;
+#else
   uint32_t d = blockIdx.x * GPB + grp;
+#endif
   uint32_t beg = 0, end = 0, beg1 = 0, end1 = 0, pr = 0;
   float pw = 0.f;
   if (kAggPf >= 1 && d < n) {

@@ -741,6 +741,10 @@ __global__ __launch_bounds__(kWave) void k_mt_serial(const uint4* __restrict__ i
     if (nw <= kMtStage) {
       for (uint32_t k = lane; k < nw; k += kWave) wl[k] = W[e0 + k];
       s.tw = wl;
+      // the chunk consumes exactly its nw words when the layer's stream is
+      // whole; when it fell short the walks stop there (past wl a walk read
+      // LDS garbage and, through the flat pointer, left the LDS aperture)
+      s.fnw = nw;
     } else {  // (rare) read the chunk's words in place
       s.tw = ch.ring;
       s.fa = a0 + e0;
@@ -924,6 +928,10 @@ __device__ __forceinline__ uint32_t lane_consume(const MtWords& W, uint32_t p, u
   // per 16 words, not per word: a dst whose degree is close to n needs many)
   uint32_t cnt = 0, q = p, end = p;
   while (cnt < n) {
+    // past the words generated for the layer (a short stream, which the
+    // layer reports): stop — past nw every word reads 0, and a walk there
+    // would run to the 2^20 guard for every dst behind it
+    if (q >= W.nw) break;
     uint32_t buf[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) buf[j] = W[q + j];
@@ -942,7 +950,8 @@ __device__ __forceinline__ uint32_t lane_consume(const MtWords& W, uint32_t p, u
     q += 16;
     if (q - p > 1u << 20) break;  // (unreachable for deg > n) keep every lane finite
   }
-  return (cnt >= n ? end : q) - p;
+  // (a walk cut short ends at or past nw, so the layer's end does too)
+  return (cnt >= n ? end : max(q, p + n)) - p;
 }
 
 // words consumed by one dst whose draws start at the first of the NW words in
@@ -1311,7 +1320,10 @@ __global__ __launch_bounds__(kSelThreads) void k_mt_rows(SelectArgs a) {
     if ((uint64_t)c + n > a.e_cap) continue;
     const bool copy = n == deg;
     for (uint32_t k = gl; k < n; k += kGrp) {
-      const uint32_t g = a.grows[beg + (copy ? k : a.ans[c + k])];
+      // (positions are < deg; the clamp only keeps the reads inside the
+      // graph when a short stream left stale words in ans — that layer is
+      // reported short and sampled again)
+      const uint32_t g = a.grows[beg + (copy ? k : min(a.ans[c + k], deg - 1))];
       a.ans[c + k] = g;
       a.edst[c + k] = i;
       a.marks[g] = 1;

@@ -428,7 +428,8 @@ SampledSubgraph* FastSampler::finish_gpu_sample(int ssg_id) {
     if (!short_stream) break;
     TORCH_CHECK(attempt < 8, "the MT19937 word stream fell short ", attempt + 1,
                 " times for one batch (bound scale ", mt_budget_, ")");
-    rerun_from(ssg_id);  // synchronises
+    rerun_from(ssg_id);  // synchronises (and moves `ssg` to the last slot it re-ran)
+    ssg = ssgs[ssg_id];
   }
   ssg->pending_batch = 0;
   issued_.erase(std::find(issued_.begin(), issued_.end(), ssg_id));

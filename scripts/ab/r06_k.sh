@@ -1,9 +1,8 @@
 #!/bin/bash
-# MT19937 short-stream re-run (ABI 11): the MT tests, incl. the forced
-# short first bounds at C2 size with three slots in flight
+# the MT19937 tests (forced short first bounds included)
 set -o pipefail
 cd "$(dirname "$0")/../.."
-O=gpurun_out/r06h; mkdir -p $O
+O=gpurun_out/r06k; mkdir -p $O
 export TMPDIR=/tmp
 ( for i in $(seq 1 40); do sleep 30; date >> $O/heartbeat.txt; done ) &
 HB=$!
