@@ -167,8 +167,11 @@ int nts_hip_ctx_reserve(nts_hip_ctx* ctx, uint64_t n_vertices, uint64_t max_item
   size_t need = radix_tmp_bytes(items);
   size_t s64 = scan_tmp_elems<uint64_t>(items + 1) * sizeof(uint64_t) + 256;
   if (s64 > need) need = s64;
-  // the radix sort's histogram scan is the largest single-pass scan
-  NTS_RET(ensure_scan_state(ctx, scan1_state_elems(512 * (items / 4096 + 1))));
+  // look-back state: the largest single-pass scan is the count scan (1,024-item
+  // tiles over a layer's dsts, count_scan); the frontier compaction uses at
+  // most 256 tiles and scan1_exclusive 4,096-item tiles (the
+  // radix sort's digit scans need no state since round 5)
+  NTS_RET(ensure_scan_state(ctx, (items / 1024 + 2 + 63) / 64 * 64));
   return ensure_scratch(ctx, need);
 }
 

@@ -425,8 +425,8 @@ __global__ __launch_bounds__(kScanThreads) void k_count_reduce(CountArgs ca,
 
 size_t count_scan_tmp_elems(uint64_t v_cap) { return scan_tmp_elems<uint32_t>(v_cap) + 64; }
 
-// -DNTS_SCAN1=0: the two-kernel scans for count_scan and the radix histograms
-// (A/B); default the single-pass look-back scans
+// -DNTS_SCAN1=0: the two-kernel scans for count_scan and the frontier
+// compaction (A/B); default the single-pass look-back scans
 bool scan1_enabled() {  // compile-time A/B: -DNTS_SCAN1=0
 #ifdef NTS_SCAN1
   return NTS_SCAN1 != 0;

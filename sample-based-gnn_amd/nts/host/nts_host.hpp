@@ -456,20 +456,31 @@ class KernelProfiler {
   void add_units(Id id, double units) {
     if (active(id)) stat[id].units += units;
   }
-  void next_step() { ++step_; }
+  // a new step: its timed class is the (step % #seen)-th of the classes seen
+  // in the steps before it, frozen for the whole step (a class
+  // first seen mid-step no longer changes the choice between begin, add_units
+  // and end of one step); before any class was seen, the step's first caller
+  void next_step() {
+    ++step_;
+    sel_ = -1;
+    if (seen_) {
+      uint32_t m = seen_;
+      for (int k = (int)(step_ % (uint64_t)__builtin_popcount(seen_)); k > 0; --k) m &= m - 1;
+      sel_ = __builtin_ctz(m);
+    }
+  }
   static const char* name(int id);
   Stat stat[kCount];
 
  private:
-  // this step's timed class: the (step % #seen)-th of the classes seen so far
   bool active(Id id) {
     seen_ |= 1u << id;
-    uint32_t m = seen_;
-    for (int k = (int)(step_ % (uint64_t)__builtin_popcount(seen_)); k > 0; --k) m &= m - 1;
-    return (m & (~m + 1)) == (1u << id);
+    if (sel_ < 0) sel_ = (int)id;
+    return sel_ == (int)id;
   }
   uint32_t seen_ = 0;
   uint64_t step_ = 0;
+  int sel_ = -1;  // this step's timed class
   struct Slot {
     Id id = BOTTOM_AGG;
     hipEvent_t a = nullptr, b = nullptr;
