@@ -750,7 +750,11 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
                      N, total, ncb, bimg);
   NTS_LAUNCH_CHECK();
 #ifndef NTS_NO_X3  // (variant builds: -DNTS_NO_X3 keeps k_gemm3_nn for A/B)
-  if (amap && x3_nn_ok(M, N, K, A, lda))
+  // the row-gathered NN (k_x3_nn / k_x3_nn7); dense rows reach k_x3_nn7 (and
+  // its relu/dropout epilogue) only under NTS_GEMM_SPLIT3_ALL: on C3's dense
+  // 100-wide bottom layer it measured 124 us vs 60 us on k_h2_nnd (round 6)
+  if ((amap && x3_nn_ok(M, N, K, A, lda)) ||
+      (ctx->gemm_mode == NTS_GEMM_SPLIT3_ALL && x3_nn7_ok(M, N, K, A, lda)))
     return x3_nn(ctx, epi, M, N, K, A, lda, amap, bimg, C, ldc, keep_threshold, scale, seed, offset);
 #endif
   // one 8-wave block per CU over all column blocks (row blocks a multiple of 8:

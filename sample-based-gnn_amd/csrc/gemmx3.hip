@@ -679,11 +679,13 @@ __device__ __forceinline__ void x3_split_op(const float (&x)[8], float (&r)[8], 
 // garbage): 1 no MFMAs, 2 no splits, 4 no A loads after the prologue, 8 no B
 // fragment reads, 16 no W DMA after the prologue (and no wait for it), 32 no
 // barrier
-template <int RT, int DIAG = 0>
+// EPI: relu + inverted dropout epilogue (the non-swapped product, k_x3_nn<true>'s
+// accumulator layout and mask keys: bit-identical to it)
+template <int RT, int DIAG = 0, bool EPI = false>
 __global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K, const float* __restrict__ X,
                                                            uint64_t ldx, const uint32_t* __restrict__ amap,
                                                            const char* __restrict__ bimg, float* __restrict__ C,
-                                                           uint64_t ldc, int rounds) {
+                                                           uint64_t ldc, int rounds, X3Epi ep) {
   static_assert(RT == kX3N7RT, "the W piece schedule is written for 7 tiles");
   extern __shared__ __attribute__((aligned(16))) char x3n7[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -836,7 +838,10 @@ __global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K,
           constexpr int pa = pr == 0 ? 2 : pr == 1 ? 1 : pr == 2 ? 0 : pr == 3 ? 1 : 0;
           constexpr int pb = pr == 0 ? 0 : pr == 1 ? 1 : pr == 2 ? 2 : pr == 3 ? 0 : pr == 4 ? 1 : 0;
           if constexpr (DIAG & 1) acc[rt][ct][0] += (float)a[pa][0] + (float)bq[ct % NB][pb][1];
-          else acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ct % NB][pb], a[pa], acc[rt][ct], 0, 0, 0);
+          else if constexpr (EPI)
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[pa], bq[ct % NB][pb], acc[rt][ct], 0, 0, 0);
+          else  // C^T = W^T X^T: the same fragments, operands swapped (16-byte row stores)
+            acc[rt][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[ct % NB][pb], a[pa], acc[rt][ct], 0, 0, 0);
         }
         // the next column tile's B fragments (slots 6 ct .. 6 ct + 2): W(g)'s,
         // or after the last column tile of the last tile W(g+1)'s column tile 0
@@ -880,20 +885,43 @@ __global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K,
     // round end: store the round's tiles, zero the accumulators, fetch the
     // row ids of the round after next
     {
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
+      x3_sfor<0, RT>([&](auto rtc) {
+        constexpr int rt = decltype(rtc)::value;
         const int t = t_lo + RT * rd + rt;
-        const int64_t row = (int64_t)t * 16 + i;
-        if (t < t_hi && row < M) {
+        if constexpr (!EPI) {
+          // acc[rt][ct][v] = C[16 t + i][n0 + 16 ct + 4 q + v]
+          const int64_t row = (int64_t)t * 16 + i;
+          if (t < t_hi && row < M) {
 #pragma unroll
-          for (int ct = 0; ct < 8; ++ct) {
-            const int col = n0 + 16 * ct + 4 * q;
-            if (col < N) *reinterpret_cast<x3f4*>(C + (uint64_t)row * ldc + col) = acc[rt][ct];
+            for (int ct = 0; ct < 8; ++ct) {
+              const int col = n0 + 16 * ct + 4 * q;
+              if (col < N) *reinterpret_cast<x3f4*>(C + (uint64_t)row * ldc + col) = acc[rt][ct];
+            }
           }
+        } else if (t < t_hi) {
+          // acc[rt][ct][v] = C[16 t + 4 q + v][n0 + 16 ct + i], relu + dropout
+          // (compile-time indices throughout: a runtime-indexed accumulator
+          // array goes to scratch)
+          const int64_t r4 = (int64_t)t * 16 + 4 * q;
+          x3_sfor<0, 8>([&](auto ctc) {
+            constexpr int ct = decltype(ctc)::value;
+            const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+            if ((int)col < N) {
+              const uint4 rnd = dropout_words((uint64_t)r4, col, ep.seed, ep.offset);
+              const uint32_t wd[4] = {rnd.x, rnd.y, rnd.z, rnd.w};
+              x3_sfor<0, 4>([&](auto vc) {
+                constexpr int v = decltype(vc)::value;
+                const float o = acc[rt][ct][v];
+                if (r4 + v < M)
+                  C[(uint64_t)(r4 + v) * ldc + col] =
+                      (dropout_bits(wd[v], col) >= ep.keep_threshold && o > 0.f) ? o * ep.scale : 0.f;
+              });
+            }
+          });
         }
 #pragma unroll
         for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = x3f4{0.f, 0.f, 0.f, 0.f};
-      }
+      });
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) nid[rt] = row_id(rd + 2, rt);
     }
@@ -982,6 +1010,12 @@ bool x3_nn_ok(int M, int N, int K, const float* A, uint64_t lda) {
   return M >= 256 && K >= 1 && N % 16 == 0 && lda >= (uint64_t)Kp && lda % 4 == 0 &&
          (uintptr_t)A % 16 == 0;
 }
+// k_x3_nn7's shapes: >= 4 k-steps (its rounds chain the next round's loads
+// over the last two) and enough rows for its 4-wave blocks to fill the chip
+// (2,048 16-row tiles: one round of 7 per wave over 256 blocks... and more)
+bool x3_nn7_ok(int M, int N, int K, const float* A, uint64_t lda) {
+  return x3_nn_ok(M, N, K, A, lda) && (K + 31) / 32 >= 4 && M >= 32768;
+}
 
 int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,
           const uint32_t* amap, const char* bimg, float* C, uint64_t ldc, uint32_t keep_threshold,
@@ -1010,7 +1044,7 @@ int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint6
                        lda, amap, bimg, C, ldc, rounds, ep);                                      \
   } while (0)
 #ifndef NTS_X3_NN_V1  // (A/B builds: -DNTS_X3_NN_V1 keeps k_x3_nn for every call)
-  if (!epi && (K + 31) / 32 >= 4) {
+  if (x3_nn7_ok(M, N, K, A, lda)) {
     // k_x3_nn7: 4-wave blocks, at most one per CU and column block, each wave
     // kX3N7RT tiles a round
     const int T7 = (M + 15) / 16;
@@ -1018,19 +1052,21 @@ int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint6
     const int64_t W7 = (int64_t)gx7 * 4;
     const int tiles7 = (int)((T7 + W7 - 1) / W7);
     const int rounds7 = (tiles7 + kX3N7RT - 1) / kX3N7RT;
-#define NTS_X3N7(D)                                                                              \
+#define NTS_X3N7E(D, E)                                                                          \
   do {                                                                                           \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn7<kX3N7RT, D>),        \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nn7<kX3N7RT, D, E>),     \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, kX3N7Lds));      \
-    hipLaunchKernelGGL((k_x3_nn7<kX3N7RT, D>), dim3(gx7, ncb), dim3(kX3N7Threads), kX3N7Lds,     \
-                       ctx->stream, M, N, K, A, lda, amap, bimg, C, ldc, rounds7);               \
+    hipLaunchKernelGGL((k_x3_nn7<kX3N7RT, D, E>), dim3(gx7, ncb), dim3(kX3N7Threads), kX3N7Lds,  \
+                       ctx->stream, M, N, K, A, lda, amap, bimg, C, ldc, rounds7, ep);           \
   } while (0)
+#define NTS_X3N7(D) NTS_X3N7E(D, false)
 #ifdef NTS_PROBE_BUILD
     static const int diag7 = [] {
       const char* e = getenv("NTS_X3_DIAG");
       return e ? atoi(e) : 0;
     }();
-    switch (diag7) {
+    if (epi) NTS_X3N7E(0, true);
+    else switch (diag7) {
       case 0: NTS_X3N7(0); break;
       case 1: NTS_X3N7(1); break;
       case 2: NTS_X3N7(2); break;
@@ -1046,9 +1082,11 @@ int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint6
       default: NTS_X3N7(63); break;
     }
 #else
-    NTS_X3N7(0);
+    if (epi) NTS_X3N7E(0, true);
+    else NTS_X3N7(0);
 #endif
 #undef NTS_X3N7
+#undef NTS_X3N7E
     NTS_LAUNCH_CHECK();
     return NTS_OK;
   }

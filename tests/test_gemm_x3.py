@@ -125,3 +125,46 @@ def test_x3_nn_gather_bitexact(ctxs, M, N, K, V):
         scale = Xg.double().abs() @ W.double().abs() + 1e-30
         torch.cuda.synchronize()
         _check(C32, C3, ref, scale)
+
+
+@pytest.mark.parametrize("M,N,K,p", [(140000, 256, 100, 0.5), (60000, 128, 602, 0.3),
+                                     (40000, 256, 128, 0.0)])
+def test_x3_nn7_relu_dropout_dense(ctxs, M, N, K, p):
+    """k_x3_nn7's relu/dropout epilogue on dense rows (reached under
+    NTS_GEMM_SPLIT3_ALL when the row pitch covers whole k-steps; the default
+    split mode keeps the narrow aggregate-first layers of C3 / C4 on the fp32
+    MFMA kernels, which measured faster): bit-identical to
+    k_gemm3_nn<relu/dropout> on the same rows at a pitch k_x3_nn7 does not take
+    (same pieces, piece and k order, accumulator layout and Philox keep mask),
+    and within the split path's bound of an fp64 product."""
+    from nts import _abi
+    from nts.hip import HipContext
+    f32, s3 = ctxs
+    s3all = HipContext(0, seed=2000)
+    s3all.set_gemm_mode(_abi.NTS_GEMM_SPLIT3_ALL)
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    Kp = (K + 31) // 32 * 32
+    Apad = torch.full((M, Kp + 32), float("nan"), device=DEV)[:, :K]  # k_x3_nn7's pitch
+    Apad.copy_(torch.randn(M, K, device=DEV, generator=g))
+    A4 = torch.empty(M, (K + 3) // 4 * 4 + (4 if K % 32 == 0 else 0), device=DEV)[:, :K]
+    A4.copy_(Apad)  # a 16-byte pitch below Kp: k_gemm3_nn
+    B = torch.randn(K, N, device=DEV, generator=g)
+    seed, offset = 0x1234_5678_9ABC, 77
+    C7 = torch.full((M, N), float("nan"), device=DEV)
+    Cr = torch.empty(M, N, device=DEV)
+    C32 = torch.empty(M, N, device=DEV)
+    s3all.gemm_relu_dropout(Apad, B, C7, p=p, seed=seed, offset=offset)
+    s3all.gemm_relu_dropout(A4, B, Cr, p=p, seed=seed, offset=offset)
+    f32.gemm_relu_dropout(A4, B, C32, p=p, seed=seed, offset=offset)
+    torch.cuda.synchronize()
+    assert not torch.isnan(C7).any()
+    assert torch.equal(C7, Cr)
+    Z = Apad.double() @ B.double()
+    scale = Apad.double().abs() @ B.double().abs() + 1e-30
+    clear = Z.abs() > 1e-5 * scale
+    assert torch.equal((C32 != 0) & clear, (C7 != 0) & clear)
+    s = 1.0 / (1.0 - p)
+    ref = torch.where(C32 != 0, torch.relu(Z) * s, torch.zeros_like(Z))
+    e32 = ((C32.double() - ref).abs() / (scale * s))[clear].max().item()
+    e7 = ((C7.double() - ref).abs() / (scale * s))[clear].max().item()
+    assert e7 <= 1.25 * e32 + 1e-7, (e7, e32)
