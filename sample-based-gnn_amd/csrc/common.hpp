@@ -274,6 +274,12 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap,
                      uint32_t bits, void* tmp, hipStream_t stream, nts_hip_ctx* ctx = nullptr);
 size_t radix_tmp_bytes(uint64_t n_cap);
+// One stable pass of that sort on digit (key >> shift) & (2^dbits - 1), dbits
+// <= 9: keys_in/vals_in -> keys_out/vals_out.  *totals (in tmp) receives the
+// per-digit item counts (2^dbits words), valid on the stream after the pass.
+int radix_pass_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
+                     uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t shift,
+                     uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals);
 
 // C[M x N] = sum of `splits` partial slabs [M x N] (ld N, `stride` floats
 // apart) in a fixed order (deterministic; gemm.hip).

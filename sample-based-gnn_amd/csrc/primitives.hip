@@ -585,41 +585,63 @@ size_t radix_tmp_bytes(uint64_t n_cap) {
   return elems * sizeof(uint32_t);
 }
 
+static uint32_t* radix_totals(void* tmp, uint64_t n_cap) {
+  const uint32_t nb = ceil_div(n_cap, kRadixTile);
+  const uint64_t n_al = (n_cap + 63) / 64 * 64;
+  return (uint32_t*)tmp + 2 * n_al + ((uint64_t)kRadixMaxBins * nb + 1 + 63) / 64 * 64;
+}
+
+// one pass: digit counts per tile, their per-digit scan, the stable scatter
+static void radix_pass(const uint32_t* ksrc, const uint32_t* vsrc, uint32_t* kdst, uint32_t* vdst,
+                       const uint32_t* n_dev, uint64_t n_cap, uint32_t shift, uint32_t dbits,
+                       void* tmp, hipStream_t stream) {
+  const uint32_t nb = ceil_div(n_cap, kRadixTile);
+  const uint64_t n_al = (n_cap + 63) / 64 * 64;
+  uint32_t* hist = (uint32_t*)tmp + 2 * n_al;
+  uint32_t* totals = radix_totals(tmp, n_cap);
+  const uint32_t mask = (1u << dbits) - 1u;
+  hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev, n_cap,
+                     shift, mask, hist, nb);
+  hipLaunchKernelGGL(k_radix_rowscan, dim3(mask + 1), dim3(kRadixThreads), 0, stream, hist, n_dev,
+                     n_cap, nb, totals);
+  hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc, kdst,
+                     vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb,
+                     (const uint32_t*)totals);
+}
+
 int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t bits,
                      void* tmp, hipStream_t stream, nts_hip_ctx* ctx) {
   (void)ctx;  // (the device-wide look-back scan's state lived there)
   if (n_cap == 0) return NTS_OK;
-  uint32_t nb = ceil_div(n_cap, kRadixTile);
-  uint64_t n_al = (n_cap + 63) / 64 * 64;
+  const uint64_t n_al = (n_cap + 63) / 64 * 64;
   uint32_t* ktmp = (uint32_t*)tmp;
   uint32_t* vtmp = ktmp + n_al;
-  uint32_t* hist = vtmp + n_al;
   if (bits < 1) bits = 1;
   const int npass = (int)((bits + kRadixMaxBits - 1) / kRadixMaxBits);
   const uint32_t dbits = (bits + npass - 1) / npass;
-  const uint32_t mask = (1u << dbits) - 1u;
-  uint32_t* totals = hist + ((uint64_t)kRadixMaxBins * nb + 1 + 63) / 64 * 64;
   const uint32_t* ksrc = keys_in;
   const uint32_t* vsrc = vals_in;
   for (int p = 0; p < npass; ++p) {
     bool to_out = ((npass - 1 - p) % 2) == 0;
     uint32_t* kdst = to_out ? keys_out : ktmp;
     uint32_t* vdst = to_out ? vals_out : vtmp;
-    const uint32_t shift = dbits * p;
-    hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev,
-                       n_cap, shift, mask, hist, nb);
-    NTS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_radix_rowscan, dim3(mask + 1), dim3(kRadixThreads), 0, stream, hist, n_dev,
-                       n_cap, nb, totals);
-    NTS_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc,
-                       kdst, vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb,
-                       (const uint32_t*)totals);
+    radix_pass(ksrc, vsrc, kdst, vdst, n_dev, n_cap, dbits * p, dbits, tmp, stream);
     NTS_LAUNCH_CHECK();
     ksrc = kdst;
     vsrc = vdst;
   }
+  return NTS_OK;
+}
+
+int radix_pass_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
+                     uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t shift,
+                     uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals) {
+  NTS_CHECK_ARG(dbits >= 1 && dbits <= (uint32_t)kRadixMaxBits, "radix digit of 1..9 bits");
+  NTS_CHECK_ARG(n_cap > 0, "empty capacity");
+  radix_pass(keys_in, vals_in, keys_out, vals_out, n_dev, n_cap, shift, dbits, tmp, stream);
+  NTS_LAUNCH_CHECK();
+  *totals = radix_totals(tmp, n_cap);
   return NTS_OK;
 }
 

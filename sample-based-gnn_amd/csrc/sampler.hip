@@ -1592,6 +1592,139 @@ __global__ void k_dst_local(const uint32_t* __restrict__ dst, const uint32_t* __
     dl[d] = src_index[dst[d]];
 }
 
+// ---- CSR transpose in two halves -------------------------------------------
+// First half (radix_pass_pairs): ONE stable radix pass on the high H bits of
+// the local src, so each bucket of 2^L consecutive sources holds its edges
+// contiguously, in edge order.  Second half, k_csr_bucket: one workgroup per
+// bucket finishes the transpose in LDS — per-wave counts of the low L bits
+// (the bucket's row counts: the row offsets come out of their scan), then each
+// wave re-reads its quarter of the bucket in order and ranks every edge
+// against a running per-(wave, row) position (match-any by ballots), so a
+// row's edges land in edge order: the stable order of the reference's serial
+// fill (core/coocsc.hpp:82-111), as the two-pass radix sort + k_csr_finalize
+// gave.  Replaces the second radix pass (its counts, digit scans and 8-byte
+// scatter) and the finalize's separate read of the sorted pairs.
+constexpr int kCsrBucketThreads = 256;
+constexpr int kCsrBucketWaves = kCsrBucketThreads / kWave;
+constexpr int kCsrBucketIt = 4;  // 64-edge groups per lane in flight
+
+template <int L>
+__global__ __launch_bounds__(kCsrBucketThreads) void k_csr_bucket(
+    const uint32_t* __restrict__ skey, const uint32_t* __restrict__ seid,
+    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ edst,
+    const float* __restrict__ wf, const uint32_t* sizes, uint32_t* __restrict__ ro,
+    uint32_t* __restrict__ ci, float* __restrict__ wb, uint32_t* __restrict__ ceid, uint32_t* pub) {
+  constexpr uint32_t R = 1u << L, RPT = R > kCsrBucketThreads ? R / kCsrBucketThreads : 1;
+  __shared__ uint32_t wh[kCsrBucketWaves][R];  // per-wave row counts -> running positions
+  __shared__ uint32_t wsum[kCsrBucketWaves];
+  publish_sizes(sizes, pub);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t b = blockIdx.x, s = sizes[2], r0 = b << L;
+  if (r0 > s) return;  // (block-uniform) no row of this bucket, nor ro[s]
+  // the bucket's start: the items of the buckets before it
+  uint32_t part = 0;
+  for (uint32_t i = t; i < b; i += kCsrBucketThreads) part += totals[i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, kWave);
+  if (lane == 0) wsum[w] = part;
+  for (uint32_t d = t; d < R; d += kCsrBucketThreads)
+#pragma unroll
+    for (int ww = 0; ww < kCsrBucketWaves; ++ww) wh[ww][d] = 0;
+  __syncthreads();
+  uint32_t bstart = 0;
+#pragma unroll
+  for (int ww = 0; ww < kCsrBucketWaves; ++ww) bstart += wsum[ww];
+  const uint32_t cnt = totals[b];
+  const uint32_t q0 = (uint32_t)((uint64_t)cnt * w / kCsrBucketWaves);
+  const uint32_t q1 = (uint32_t)((uint64_t)cnt * (w + 1) / kCsrBucketWaves);
+  const uint32_t* kb = skey + bstart;
+  const uint32_t* eb = seid + bstart;
+  // (1) wave w counts the rows of its quarter
+  for (uint32_t i = q0 + lane; i < q1; i += kWave) atomicAdd(&wh[w][kb[i] & (R - 1)], 1u);
+  __syncthreads();  // (also: every wave has read wsum)
+  // (2) thread t owns rows t RPT .. +RPT-1: per-wave exclusive offsets, the
+  // rows' counts scanned over the block -> row offsets and absolute positions
+  uint32_t rc[RPT], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < RPT; ++k) {
+    const uint32_t d = t * RPT + k;
+    uint32_t run = 0;
+    if (d < R) {
+#pragma unroll
+      for (int ww = 0; ww < kCsrBucketWaves; ++ww) {
+        const uint32_t c = wh[ww][d];
+        wh[ww][d] = run;
+        run += c;
+      }
+    }
+    rc[k] = run;
+    sum += run;
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();  // wsum reused
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = bstart + inc - sum;
+#pragma unroll
+  for (int ww = 0; ww < kCsrBucketWaves; ++ww) base += ww < w ? wsum[ww] : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < RPT; ++k) {
+    const uint32_t d = t * RPT + k;
+    if (d < R) {
+      if (r0 + d <= s) ro[r0 + d] = base;
+#pragma unroll
+      for (int ww = 0; ww < kCsrBucketWaves; ++ww) wh[ww][d] += base;
+    }
+    base += rc[k];
+  }
+  __syncthreads();
+  // (3) each wave walks its quarter in order, kCsrBucketIt groups of 64 at a
+  // time (loads and gathers first, then the ranks in group order)
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (uint32_t i0 = q0; i0 < q1; i0 += kCsrBucketIt * kWave) {
+    uint32_t key[kCsrBucketIt], eid[kCsrBucketIt], dv[kCsrBucketIt];
+    float fv[kCsrBucketIt];
+#pragma unroll
+    for (int g = 0; g < kCsrBucketIt; ++g) {
+      const uint32_t i = i0 + g * kWave + lane;
+      key[g] = i < q1 ? kb[i] : 0u;
+      eid[g] = i < q1 ? eb[i] : 0u;
+    }
+#pragma unroll
+    for (int g = 0; g < kCsrBucketIt; ++g) {
+      const bool ok = i0 + g * kWave + lane < q1;
+      dv[g] = ok ? edst[eid[g]] : 0u;
+      fv[g] = ok && wb && wf ? wf[eid[g]] : 0.f;
+    }
+#pragma unroll
+    for (int g = 0; g < kCsrBucketIt; ++g) {
+      const bool ok = i0 + g * kWave + lane < q1;
+      const uint32_t d = key[g] & (R - 1);
+      uint64_t peers = __ballot(ok);
+#pragma unroll
+      for (int bb = 0; bb < L; ++bb) {
+        const bool bit = (d >> bb) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      const uint32_t prev = wh[w][d];
+      const uint32_t before = (uint32_t)__popcll(peers & lt);
+      if (ok && before == 0) wh[w][d] = prev + (uint32_t)__popcll(peers);
+      if (ok) {
+        const uint32_t pos = prev + before;
+        ci[pos] = dv[g];
+        if (ceid) ceid[pos] = eid[g];
+        if (wb) wb[pos] = fv[g];
+      }
+    }
+  }
+}
+
 // ---- CSR from sorted (local src, edge id) ----------------------------------
 __global__ void k_csr_finalize(const uint32_t* __restrict__ skey, const uint32_t* __restrict__ seid,
                                const uint32_t* __restrict__ edst, const float* __restrict__ wf,
@@ -2095,8 +2228,33 @@ frontier:
   // later passes' tile offsets by a per-digit decoupled look-back (48-91 us)
   // or counted by the pass before with atomics (65 vs 16 us).
   if (csr) {
+    const uint32_t bits = ceil_log2((uint64_t)o->s_cap + 1);
+#ifndef NTS_CSR_RADIX2  // (A/B build: the two-pass radix sort + k_csr_finalize)
+    if (bits >= 11 && bits <= 19) {
+      // one radix pass on the high H bits, then k_csr_bucket per 2^L sources
+      const uint32_t H = std::min(9u, bits - 6), L = bits - H;
+      const uint32_t* totals = nullptr;
+      NTS_RET(radix_pass_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap, L,
+                               H, t_sort, st, &totals));
+      const float* wf = weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward;
+#define NTS_CSR_BUCKET(LL)                                                                        \
+  hipLaunchKernelGGL(k_csr_bucket<LL>, dim3(1u << H), dim3(kCsrBucketThreads), 0, st, t_skey,   \
+                     t_seid, totals, o->edge_dst, wf, o->sizes, o->row_offset, o->column_indices, \
+                     o->edge_weight_backward, o->csr_edge_id, o->sizes_host)
+      switch (L) {
+        case 6: NTS_CSR_BUCKET(6); break;
+        case 7: NTS_CSR_BUCKET(7); break;
+        case 8: NTS_CSR_BUCKET(8); break;
+        case 9: NTS_CSR_BUCKET(9); break;
+        default: NTS_CSR_BUCKET(10); break;
+      }
+#undef NTS_CSR_BUCKET
+      NTS_LAUNCH_CHECK();
+      return NTS_OK;
+    }
+#endif
     NTS_RET(radix_sort_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap,
-                             ceil_log2((uint64_t)o->s_cap + 1), t_sort, st, ctx));
+                             bits, t_sort, st, ctx));
     hipLaunchKernelGGL(k_csr_finalize, dim3(ge), dim3(256), 0, st, t_skey, t_seid, o->edge_dst,
                        weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward,
                        o->sizes, o->row_offset, o->column_indices, o->edge_weight_backward,
