@@ -277,9 +277,18 @@ size_t radix_tmp_bytes(uint64_t n_cap);
 // One stable pass of that sort on digit (key >> shift) & (2^dbits - 1), dbits
 // <= 9: keys_in/vals_in -> keys_out/vals_out.  *totals (in tmp) receives the
 // per-digit item counts (2^dbits words), valid on the stream after the pass.
+// Payloads (optional, vals_in NULL only): pN_out[pos] = pN_in[i] for the
+// item i that lands at pos.
+struct RadixPayload {
+  const uint32_t* p1_in = nullptr;
+  uint32_t* p1_out = nullptr;
+  const uint32_t* p2_in = nullptr;
+  uint32_t* p2_out = nullptr;
+};
 int radix_pass_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t shift,
-                     uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals);
+                     uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals,
+                     const RadixPayload& pl = RadixPayload{});
 
 // C[M x N] = sum of `splits` partial slabs [M x N] (ld N, `stride` floats
 // apart) in a fixed order (deterministic; gemm.hip).

@@ -549,7 +549,8 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* n_dev,
     uint64_t n_cap, uint32_t shift, uint32_t dbits, const uint32_t* __restrict__ hist,
-    uint32_t nb, const uint32_t* __restrict__ totals) {
+    uint32_t nb, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ p1_in,
+    uint32_t* __restrict__ p1_out, const uint32_t* __restrict__ p2_in, uint32_t* __restrict__ p2_out) {
   __shared__ RadixTileLds sm;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
   if ((uint64_t)blockIdx.x * kRadixTile >= n) return;  // whole tile past the end
@@ -565,16 +566,39 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     if (2u * t + 1 < bins) sm.gstart[2 * t + 1] = ex + c0;
     // (radix_tile_order's first barrier orders these before the reads below)
   }
+  uint32_t loc[kRadixItems];
   radix_tile_order(sm, keys_in, vals_in, n, shift, dbits, [](uint32_t, uint32_t) {}, [&] {
     for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
       sm.gstart[d] += hist[(uint64_t)d * nb + blockIdx.x];
-  });
+  }, loc);
   const uint32_t cnt = radix_tile_count(n), mask = (1u << dbits) - 1u;
   for (uint32_t i = threadIdx.x; i < cnt; i += kRadixThreads) {
     const uint32_t k = sm.sk[i], pos = radix_tile_pos(sm, i, k, shift, mask);
     keys_out[pos] = k;
     vals_out[pos] = sm.sv[i];
   }
+  // payloads (vals_in NULL: the values are the items' indices): read in index
+  // order (coalesced), moved into the digit order through sm.sv, written in
+  // the keys' runs
+  auto payload = [&](const uint32_t* __restrict__ pin, uint32_t* __restrict__ pout) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t wbase = (uint64_t)blockIdx.x * kRadixTile + (uint64_t)w * (kRadixItems * kWave);
+    uint32_t pv[kRadixItems];
+#pragma unroll
+    for (int k = 0; k < kRadixItems; ++k) {
+      const uint64_t i = wbase + (uint64_t)k * kWave + lane;
+      pv[k] = i < n ? pin[i] : 0u;
+    }
+    __syncthreads();  // every read of sm.sv above is done
+#pragma unroll
+    for (int k = 0; k < kRadixItems; ++k)
+      if (wbase + (uint64_t)k * kWave + lane < n) sm.sv[loc[k]] = pv[k];
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += kRadixThreads)
+      pout[radix_tile_pos(sm, i, sm.sk[i], shift, mask)] = sm.sv[i];
+  };
+  if (p1_out) payload(p1_in, p1_out);
+  if (p2_out) payload(p2_in, p2_out);
 }
 
 size_t radix_tmp_bytes(uint64_t n_cap) {
@@ -594,7 +618,7 @@ static uint32_t* radix_totals(void* tmp, uint64_t n_cap) {
 // one pass: digit counts per tile, their per-digit scan, the stable scatter
 static void radix_pass(const uint32_t* ksrc, const uint32_t* vsrc, uint32_t* kdst, uint32_t* vdst,
                        const uint32_t* n_dev, uint64_t n_cap, uint32_t shift, uint32_t dbits,
-                       void* tmp, hipStream_t stream) {
+                       void* tmp, hipStream_t stream, const RadixPayload& pl = RadixPayload{}) {
   const uint32_t nb = ceil_div(n_cap, kRadixTile);
   const uint64_t n_al = (n_cap + 63) / 64 * 64;
   uint32_t* hist = (uint32_t*)tmp + 2 * n_al;
@@ -606,7 +630,7 @@ static void radix_pass(const uint32_t* ksrc, const uint32_t* vsrc, uint32_t* kds
                      n_cap, nb, totals);
   hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc, kdst,
                      vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb,
-                     (const uint32_t*)totals);
+                     (const uint32_t*)totals, pl.p1_in, pl.p1_out, pl.p2_in, pl.p2_out);
 }
 
 int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
@@ -636,10 +660,12 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
 
 int radix_pass_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_out,
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t shift,
-                     uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals) {
+                     uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals,
+                     const RadixPayload& pl) {
   NTS_CHECK_ARG(dbits >= 1 && dbits <= (uint32_t)kRadixMaxBits, "radix digit of 1..9 bits");
   NTS_CHECK_ARG(n_cap > 0, "empty capacity");
-  radix_pass(keys_in, vals_in, keys_out, vals_out, n_dev, n_cap, shift, dbits, tmp, stream);
+  NTS_CHECK_ARG(!(pl.p1_out || pl.p2_out) || !vals_in, "payloads need index values (vals_in NULL)");
+  radix_pass(keys_in, vals_in, keys_out, vals_out, n_dev, n_cap, shift, dbits, tmp, stream, pl);
   NTS_LAUNCH_CHECK();
   *totals = radix_totals(tmp, n_cap);
   return NTS_OK;

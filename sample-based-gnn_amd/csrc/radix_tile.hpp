@@ -31,11 +31,13 @@ struct RadixTileLds {
 // sm.gstart[d] — where the tile's run of digit d starts in the output — for
 // its digits d = t, t + 256 (< bins), their counts in sm.lstart[d].
 // vals_in == nullptr: values are the item indices.
+// loc[k]: where this thread's item k (index base + 1024 w + 64 k + lane) went
+// in the digit order (so payloads read later in index order can follow it).
 template <class Pub, class GS>
 __device__ __forceinline__ void radix_tile_order(RadixTileLds& sm, const uint32_t* __restrict__ keys_in,
                                                  const uint32_t* __restrict__ vals_in, uint64_t n,
                                                  uint32_t shift, uint32_t dbits, Pub&& publish,
-                                                 GS&& gstart) {
+                                                 GS&& gstart, uint32_t (&loc)[kRadixItems]) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
   const uint32_t mask = (1u << dbits) - 1u, bins = mask + 1;
@@ -113,9 +115,9 @@ __device__ __forceinline__ void radix_tile_order(RadixTileLds& sm, const uint32_
   for (int k = 0; k < kRadixItems; ++k) {
     if (wbase + (uint64_t)k * kWave + lane < n) {
       const uint32_t d = (key[k] >> shift) & mask;
-      const uint32_t loc = sm.lstart[d] + sm.wh[w][d] + rank[k];
-      sm.sk[loc] = key[k];
-      sm.sv[loc] = val[k];
+      loc[k] = sm.lstart[d] + sm.wh[w][d] + rank[k];
+      sm.sk[loc[k]] = key[k];
+      sm.sv[loc[k]] = val[k];
     }
   }
   __syncthreads();

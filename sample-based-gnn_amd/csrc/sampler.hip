@@ -1604,15 +1604,15 @@ __global__ void k_dst_local(const uint32_t* __restrict__ dst, const uint32_t* __
 // fill (core/coocsc.hpp:82-111), as the two-pass radix sort + k_csr_finalize
 // gave.  Replaces the second radix pass (its counts, digit scans and 8-byte
 // scatter) and the finalize's separate read of the sorted pairs.
-constexpr int kCsrBucketThreads = 256;
+constexpr int kCsrBucketThreads = 1024;  // 16 waves: short in-order chains per bucket
 constexpr int kCsrBucketWaves = kCsrBucketThreads / kWave;
 constexpr int kCsrBucketIt = 4;  // 64-edge groups per lane in flight
 
 template <int L>
 __global__ __launch_bounds__(kCsrBucketThreads) void k_csr_bucket(
     const uint32_t* __restrict__ skey, const uint32_t* __restrict__ seid,
-    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ edst,
-    const float* __restrict__ wf, const uint32_t* sizes, uint32_t* __restrict__ ro,
+    const uint32_t* __restrict__ totals, const uint32_t* __restrict__ sdst,
+    const uint32_t* __restrict__ swf, const uint32_t* sizes, uint32_t* __restrict__ ro,
     uint32_t* __restrict__ ci, float* __restrict__ wb, uint32_t* __restrict__ ceid, uint32_t* pub) {
   constexpr uint32_t R = 1u << L, RPT = R > kCsrBucketThreads ? R / kCsrBucketThreads : 1;
   __shared__ uint32_t wh[kCsrBucketWaves][R];  // per-wave row counts -> running positions
@@ -1639,6 +1639,8 @@ __global__ __launch_bounds__(kCsrBucketThreads) void k_csr_bucket(
   const uint32_t q1 = (uint32_t)((uint64_t)cnt * (w + 1) / kCsrBucketWaves);
   const uint32_t* kb = skey + bstart;
   const uint32_t* eb = seid + bstart;
+  const uint32_t* db = sdst + bstart;
+  const uint32_t* fb = swf ? swf + bstart : nullptr;
   // (1) wave w counts the rows of its quarter
   for (uint32_t i = q0 + lane; i < q1; i += kWave) atomicAdd(&wh[w][kb[i] & (R - 1)], 1u);
   __syncthreads();  // (also: every wave has read wsum)
@@ -1683,8 +1685,11 @@ __global__ __launch_bounds__(kCsrBucketThreads) void k_csr_bucket(
     base += rc[k];
   }
   __syncthreads();
-  // (3) each wave walks its quarter in order, kCsrBucketIt groups of 64 at a
-  // time (loads and gathers first, then the ranks in group order)
+  // (3) each wave walks its share in order, kCsrBucketIt groups of 64 at a
+  // time (the loads first, then the ranks in group order); the dst ids and
+  // forward weights came through the radix pass beside the edge ids
+  // (payloads gathered within each 4096-edge tile), so every read here is
+  // sequential
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (uint32_t i0 = q0; i0 < q1; i0 += kCsrBucketIt * kWave) {
     uint32_t key[kCsrBucketIt], eid[kCsrBucketIt], dv[kCsrBucketIt];
@@ -1692,14 +1697,11 @@ __global__ __launch_bounds__(kCsrBucketThreads) void k_csr_bucket(
 #pragma unroll
     for (int g = 0; g < kCsrBucketIt; ++g) {
       const uint32_t i = i0 + g * kWave + lane;
-      key[g] = i < q1 ? kb[i] : 0u;
-      eid[g] = i < q1 ? eb[i] : 0u;
-    }
-#pragma unroll
-    for (int g = 0; g < kCsrBucketIt; ++g) {
-      const bool ok = i0 + g * kWave + lane < q1;
-      dv[g] = ok ? edst[eid[g]] : 0u;
-      fv[g] = ok && wb && wf ? wf[eid[g]] : 0.f;
+      const bool ok = i < q1;
+      key[g] = ok ? kb[i] : 0u;
+      eid[g] = ok && ceid ? eb[i] : 0u;
+      dv[g] = ok ? db[i] : 0u;
+      fv[g] = ok && wb && fb ? __uint_as_float(fb[i]) : 0.f;
     }
 #pragma unroll
     for (int g = 0; g < kCsrBucketIt; ++g) {
@@ -1980,6 +1982,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t blk = al(nblk_marks + 1);
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
+  const uint64_t sort_p = csr ? 2 * al(o->e_cap) : 0;  // k_csr_bucket's payloads
   const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
   // MT19937 modes: per-dst info; the chunked resolver (fanout 1..32) adds the
@@ -2015,7 +2018,7 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t mt_misc_n = mt_chunked ? 64 : 0;
   const uint64_t mt_n = mt_info_n + mt_base_n + mt_stat_n + mt_win_n + mt_tab_n + mt_ent_n +
                         mt_misc_n;
-  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + up_n + mt_n) *
+  const size_t need = (scan_co + blk + scan_blk + sort_k + sort_v + sort_p + up_n + mt_n) *
                           sizeof(uint32_t) + sort_tmp + 256;
   NTS_RET(ensure_scratch(ctx, need));
   uint32_t* w0 = (uint32_t*)ctx->scratch;
@@ -2024,7 +2027,9 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   uint32_t* t_scan_blk = t_blk + blk;
   uint32_t* t_skey = t_scan_blk + scan_blk;
   uint32_t* t_seid = t_skey + sort_k;
-  uint32_t* t_up = t_seid + sort_v;
+  uint32_t* t_sdst = t_seid + sort_v;
+  uint32_t* t_swf = t_sdst + sort_p / 2;
+  uint32_t* t_up = t_sdst + sort_p;
   uint32_t* t_mt = t_up + up_n;  // MT19937 modes: per-dst MtInfo (16-byte aligned)
   void* t_sort = (void*)(t_mt + mt_n);
 
@@ -2234,12 +2239,20 @@ frontier:
       // one radix pass on the high H bits, then k_csr_bucket per 2^L sources
       const uint32_t H = std::min(9u, bits - 6), L = bits - H;
       const uint32_t* totals = nullptr;
+      const bool wpl = weight_type != NTS_WEIGHT_NONE && o->edge_weight_backward;
+      RadixPayload pl;
+      pl.p1_in = o->edge_dst;
+      pl.p1_out = t_sdst;
+      if (wpl) {
+        pl.p2_in = reinterpret_cast<const uint32_t*>(o->edge_weight_forward);
+        pl.p2_out = t_swf;
+      }
       NTS_RET(radix_pass_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap, L,
-                               H, t_sort, st, &totals));
-      const float* wf = weight_type == NTS_WEIGHT_NONE ? nullptr : o->edge_weight_forward;
+                               H, t_sort, st, &totals, pl));
+      const uint32_t* swf = wpl ? t_swf : nullptr;
 #define NTS_CSR_BUCKET(LL)                                                                        \
   hipLaunchKernelGGL(k_csr_bucket<LL>, dim3(1u << H), dim3(kCsrBucketThreads), 0, st, t_skey,   \
-                     t_seid, totals, o->edge_dst, wf, o->sizes, o->row_offset, o->column_indices, \
+                     t_seid, totals, t_sdst, swf, o->sizes, o->row_offset, o->column_indices,   \
                      o->edge_weight_backward, o->csr_edge_id, o->sizes_host)
       switch (L) {
         case 6: NTS_CSR_BUCKET(6); break;
