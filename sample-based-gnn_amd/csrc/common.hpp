@@ -277,6 +277,8 @@ size_t radix_tmp_bytes(uint64_t n_cap);
 // One stable pass of that sort on digit (key >> shift) & (2^dbits - 1), dbits
 // <= 9: keys_in/vals_in -> keys_out/vals_out.  *totals (in tmp) receives the
 // per-digit item counts (2^dbits words), valid on the stream after the pass.
+// Tiles of 1,024 items (the generic sort: 4,096); tmp: radix_pass_tmp_bytes.
+// vals_out may be NULL (keys and payloads only).
 // Payloads (optional, vals_in NULL only): pN_out[pos] = pN_in[i] for the
 // item i that lands at pos.
 struct RadixPayload {
@@ -289,6 +291,7 @@ int radix_pass_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
                      uint32_t* vals_out, const uint32_t* n_dev, uint64_t n_cap, uint32_t shift,
                      uint32_t dbits, void* tmp, hipStream_t stream, const uint32_t** totals,
                      const RadixPayload& pl = RadixPayload{});
+size_t radix_pass_tmp_bytes(uint64_t n_cap);
 
 // C[M x N] = sum of `splits` partial slabs [M x N] (ld N, `stride` floats
 // apart) in a fixed order (deterministic; gemm.hip).

@@ -487,6 +487,7 @@ template size_t scan_tmp_elems<uint64_t>(uint64_t);
 // LDS and written out in runs (coalesced stores).
 // Tiles past the device-side count n exit at once.
 // ============================================================================
+template <int IT>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __restrict__ keys,
                                                               const uint32_t* n_dev,
                                                               uint64_t n_cap, uint32_t shift,
@@ -498,10 +499,10 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
   for (uint32_t d = t; d < bins; d += kRadixThreads) h[d] = 0;
   __syncthreads();
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
-  const uint64_t base = (uint64_t)blockIdx.x * kRadixTile;
+  const uint64_t base = (uint64_t)blockIdx.x * (kRadixThreads * IT);
   if (base >= n) return;  // past the end: k_radix_rowscan reads only the tiles below n
 #pragma unroll
-  for (int k = 0; k < kRadixItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     const uint64_t i = base + (uint64_t)k * kRadixThreads + t;
     if (i < n) atomicAdd(&h[(keys[i] >> shift) & mask], 1u);
   }
@@ -515,11 +516,12 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_hist(const uint32_t* __
 // waits on another, and the grid is the digit count, not the capacity.
 __global__ __launch_bounds__(kRadixThreads) void k_radix_rowscan(uint32_t* __restrict__ hist,
                                                                  const uint32_t* n_dev, uint64_t n_cap,
-                                                                 uint32_t nb, uint32_t* __restrict__ totals) {
+                                                                 uint32_t nb, uint32_t tile,
+                                                                 uint32_t* __restrict__ totals) {
   __shared__ uint32_t wsum[kRadixThreads / kWave];
   const int t = threadIdx.x;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
-  const uint32_t live = (uint32_t)((n + kRadixTile - 1) / kRadixTile);  // <= nb
+  const uint32_t live = (uint32_t)((n + tile - 1) / tile);  // <= nb
   uint32_t* row = hist + (uint64_t)blockIdx.x * nb;
   constexpr int kPer = 4;  // consecutive entries per thread
   uint32_t carry = 0;
@@ -545,15 +547,16 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_rowscan(uint32_t* __res
   if (t == 0) totals[blockIdx.x] = carry;
 }
 
+template <int IT>
 __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out, const uint32_t* n_dev,
     uint64_t n_cap, uint32_t shift, uint32_t dbits, const uint32_t* __restrict__ hist,
     uint32_t nb, const uint32_t* __restrict__ totals, const uint32_t* __restrict__ p1_in,
     uint32_t* __restrict__ p1_out, const uint32_t* __restrict__ p2_in, uint32_t* __restrict__ p2_out) {
-  __shared__ RadixTileLds sm;
+  __shared__ RadixTileLds<IT> sm;
   const uint64_t n = n_dev ? (uint64_t)*n_dev : n_cap;
-  if ((uint64_t)blockIdx.x * kRadixTile >= n) return;  // whole tile past the end
+  if ((uint64_t)blockIdx.x * (kRadixThreads * IT) >= n) return;  // whole tile past the end
   const uint32_t bins = 1u << dbits;
   {  // the digits' starts: exclusive scan of the row totals (thread t: digits 2t, 2t + 1)
     static_assert(2 * kRadixThreads == kRadixMaxBins, "two digits per thread");
@@ -566,32 +569,32 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
     if (2u * t + 1 < bins) sm.gstart[2 * t + 1] = ex + c0;
     // (radix_tile_order's first barrier orders these before the reads below)
   }
-  uint32_t loc[kRadixItems];
+  uint32_t loc[IT];
   radix_tile_order(sm, keys_in, vals_in, n, shift, dbits, [](uint32_t, uint32_t) {}, [&] {
     for (uint32_t d = threadIdx.x; d < bins; d += kRadixThreads)
       sm.gstart[d] += hist[(uint64_t)d * nb + blockIdx.x];
   }, loc);
-  const uint32_t cnt = radix_tile_count(n), mask = (1u << dbits) - 1u;
+  const uint32_t cnt = radix_tile_count<IT>(n), mask = (1u << dbits) - 1u;
   for (uint32_t i = threadIdx.x; i < cnt; i += kRadixThreads) {
     const uint32_t k = sm.sk[i], pos = radix_tile_pos(sm, i, k, shift, mask);
     keys_out[pos] = k;
-    vals_out[pos] = sm.sv[i];
+    if (vals_out) vals_out[pos] = sm.sv[i];
   }
   // payloads (vals_in NULL: the values are the items' indices): read in index
   // order (coalesced), moved into the digit order through sm.sv, written in
   // the keys' runs
   auto payload = [&](const uint32_t* __restrict__ pin, uint32_t* __restrict__ pout) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint64_t wbase = (uint64_t)blockIdx.x * kRadixTile + (uint64_t)w * (kRadixItems * kWave);
-    uint32_t pv[kRadixItems];
+    const uint64_t wbase = (uint64_t)blockIdx.x * (kRadixThreads * IT) + (uint64_t)w * (IT * kWave);
+    uint32_t pv[IT];
 #pragma unroll
-    for (int k = 0; k < kRadixItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
       const uint64_t i = wbase + (uint64_t)k * kWave + lane;
       pv[k] = i < n ? pin[i] : 0u;
     }
     __syncthreads();  // every read of sm.sv above is done
 #pragma unroll
-    for (int k = 0; k < kRadixItems; ++k)
+    for (int k = 0; k < IT; ++k)
       if (wbase + (uint64_t)k * kWave + lane < n) sm.sv[loc[k]] = pv[k];
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += kRadixThreads)
@@ -601,34 +604,39 @@ __global__ __launch_bounds__(kRadixThreads) void k_radix_scatter(
   if (p2_out) payload(p2_in, p2_out);
 }
 
-size_t radix_tmp_bytes(uint64_t n_cap) {
-  uint64_t nb = (n_cap + kRadixTile - 1) / kRadixTile;
+static size_t radix_tmp_bytes_t(uint64_t n_cap, uint32_t tile) {
+  uint64_t nb = (n_cap + tile - 1) / tile;
   if (nb == 0) nb = 1;
   size_t hist = (size_t)kRadixMaxBins * nb + 1;
   size_t elems = 2 * ((n_cap + 63) / 64 * 64) + (hist + 63) / 64 * 64 + kRadixMaxBins + 64;
   return elems * sizeof(uint32_t);
 }
 
-static uint32_t* radix_totals(void* tmp, uint64_t n_cap) {
-  const uint32_t nb = ceil_div(n_cap, kRadixTile);
+size_t radix_tmp_bytes(uint64_t n_cap) { return radix_tmp_bytes_t(n_cap, kRadixTile); }
+size_t radix_pass_tmp_bytes(uint64_t n_cap) { return radix_tmp_bytes_t(n_cap, kRadixThreads * kRadixPassItems); }
+
+static uint32_t* radix_totals(void* tmp, uint64_t n_cap, uint32_t tile) {
+  const uint32_t nb = ceil_div(n_cap, tile);
   const uint64_t n_al = (n_cap + 63) / 64 * 64;
   return (uint32_t*)tmp + 2 * n_al + ((uint64_t)kRadixMaxBins * nb + 1 + 63) / 64 * 64;
 }
 
 // one pass: digit counts per tile, their per-digit scan, the stable scatter
+template <int IT>
 static void radix_pass(const uint32_t* ksrc, const uint32_t* vsrc, uint32_t* kdst, uint32_t* vdst,
                        const uint32_t* n_dev, uint64_t n_cap, uint32_t shift, uint32_t dbits,
                        void* tmp, hipStream_t stream, const RadixPayload& pl = RadixPayload{}) {
-  const uint32_t nb = ceil_div(n_cap, kRadixTile);
+  constexpr uint32_t tile = kRadixThreads * IT;
+  const uint32_t nb = ceil_div(n_cap, tile);
   const uint64_t n_al = (n_cap + 63) / 64 * 64;
   uint32_t* hist = (uint32_t*)tmp + 2 * n_al;
-  uint32_t* totals = radix_totals(tmp, n_cap);
+  uint32_t* totals = radix_totals(tmp, n_cap, tile);
   const uint32_t mask = (1u << dbits) - 1u;
-  hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev, n_cap,
+  hipLaunchKernelGGL(k_radix_hist<IT>, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, n_dev, n_cap,
                      shift, mask, hist, nb);
   hipLaunchKernelGGL(k_radix_rowscan, dim3(mask + 1), dim3(kRadixThreads), 0, stream, hist, n_dev,
-                     n_cap, nb, totals);
-  hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc, kdst,
+                     n_cap, nb, tile, totals);
+  hipLaunchKernelGGL(k_radix_scatter<IT>, dim3(nb), dim3(kRadixThreads), 0, stream, ksrc, vsrc, kdst,
                      vdst, n_dev, n_cap, shift, dbits, (const uint32_t*)hist, nb,
                      (const uint32_t*)totals, pl.p1_in, pl.p1_out, pl.p2_in, pl.p2_out);
 }
@@ -650,7 +658,7 @@ int radix_sort_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
     bool to_out = ((npass - 1 - p) % 2) == 0;
     uint32_t* kdst = to_out ? keys_out : ktmp;
     uint32_t* vdst = to_out ? vals_out : vtmp;
-    radix_pass(ksrc, vsrc, kdst, vdst, n_dev, n_cap, dbits * p, dbits, tmp, stream);
+    radix_pass<kRadixItems>(ksrc, vsrc, kdst, vdst, n_dev, n_cap, dbits * p, dbits, tmp, stream);
     NTS_LAUNCH_CHECK();
     ksrc = kdst;
     vsrc = vdst;
@@ -665,9 +673,10 @@ int radix_pass_pairs(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t*
   NTS_CHECK_ARG(dbits >= 1 && dbits <= (uint32_t)kRadixMaxBits, "radix digit of 1..9 bits");
   NTS_CHECK_ARG(n_cap > 0, "empty capacity");
   NTS_CHECK_ARG(!(pl.p1_out || pl.p2_out) || !vals_in, "payloads need index values (vals_in NULL)");
-  radix_pass(keys_in, vals_in, keys_out, vals_out, n_dev, n_cap, shift, dbits, tmp, stream, pl);
+  radix_pass<kRadixPassItems>(keys_in, vals_in, keys_out, vals_out, n_dev, n_cap, shift, dbits, tmp,
+                              stream, pl);
   NTS_LAUNCH_CHECK();
-  *totals = radix_totals(tmp, n_cap);
+  *totals = radix_totals(tmp, n_cap, kRadixThreads * kRadixPassItems);
   return NTS_OK;
 }
 

@@ -1983,7 +1983,8 @@ extern "C" int nts_hip_sample_layer(nts_hip_ctx* ctx, const nts_graph_dev* g, in
   const uint64_t scan_blk = al(scan_tmp_elems<uint32_t>(nblk_marks) + 1);
   const uint64_t sort_k = csr ? al(o->e_cap) : 0, sort_v = sort_k;
   const uint64_t sort_p = csr ? 2 * al(o->e_cap) : 0;  // k_csr_bucket's payloads
-  const size_t sort_tmp = csr ? radix_tmp_bytes(o->e_cap) : 0;
+  const size_t sort_tmp =
+      csr ? std::max(radix_tmp_bytes(o->e_cap), radix_pass_tmp_bytes(o->e_cap)) : 0;
   const uint64_t up_n = up ? al(o->s_cap) : 0;
   // MT19937 modes: per-dst info; the chunked resolver (fanout 1..32) adds the
   // draws' scan, chunk stats, the bulk word stream + raw blocks, the window
@@ -2247,8 +2248,9 @@ frontier:
         pl.p2_in = reinterpret_cast<const uint32_t*>(o->edge_weight_forward);
         pl.p2_out = t_swf;
       }
-      NTS_RET(radix_pass_pairs(o->row_indices, nullptr, t_skey, t_seid, o->sizes + 1, o->e_cap, L,
-                               H, t_sort, st, &totals, pl));
+      // (the edge ids only where the CSR's edge-id map is asked for: GAT)
+      NTS_RET(radix_pass_pairs(o->row_indices, nullptr, t_skey, o->csr_edge_id ? t_seid : nullptr,
+                               o->sizes + 1, o->e_cap, L, H, t_sort, st, &totals, pl));
       const uint32_t* swf = wpl ? t_swf : nullptr;
 #define NTS_CSR_BUCKET(LL)                                                                        \
   hipLaunchKernelGGL(k_csr_bucket<LL>, dim3(1u << H), dim3(kCsrBucketThreads), 0, st, t_skey,   \
