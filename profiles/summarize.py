@@ -42,6 +42,8 @@ def profiler_kernel(name: str):
         return "gather_gemm"                     # split-bf16 X[src] W0
     if k == "k_x3_nn" and targs[0] == "false":
         return "gather_gemm"                     # split-bf16 X[src] W0, whole rows (gemmx3.hip)
+    if k == "k_x3_nn7" and len(targs) > 2 and targs[2] == "false":
+        return "gather_gemm"                     # round 6: 4-wave blocks, 7 row tiles a wave
     if k == "k_x3_tn":
         return "gather_gemm_tn"                  # split-bf16 X[src]^T dH, whole rows (gemmx3.hip)
     if k == "k_gemm_tn_big" and targs[0] == "false":
