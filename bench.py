@@ -262,6 +262,8 @@ def parse():
     p.add_argument("--early-agg", action="store_true",
                    help="aggregate-first: issue the bottom aggregation behind the sampler")
     p.add_argument("--no-priority", action="store_true", help="sampler stream at normal priority")
+    p.add_argument("--sampler-high-priority", action="store_true",
+                   help="sampler stream at high priority (default: high for --rng mt only)")
     p.add_argument("--training-priority", action="store_true",
                    help="the training stream at high priority, the sampler's at normal")
     p.add_argument("--model", default="gcn", choices=["gcn", "gat"],
@@ -426,7 +428,8 @@ def main():
                           pipeline=not args.no_pipeline, hip_gemm=not args.no_hip_gemm,
                           transform_first=args.transform_first, early_aggregate=args.early_agg,
                           sampler_priority=(-1 if args.training_priority else
-                                            0 if args.no_priority else 1),
+                                            0 if args.no_priority else
+                                            1 if args.sampler_high_priority else 2),
                           fuse_activation=not args.no_fuse_act,
                           fuse_loss=not args.no_fuse_loss, sampler_cus=args.sampler_cus,
                           sampler_gate=args.sampler_gate,

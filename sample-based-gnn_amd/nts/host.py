@@ -36,7 +36,7 @@ def gcn_config(layers, fanout, batch_size, learn_rate=0.01, weight_decay=1e-4, d
                rng_mode=_abi.NTS_RNG_PHILOX, weight="sum", fused_gather=True,
                bias_correction=False, deterministic_backward=True, shuffle=True, profile=False,
                seed=2000, hip_gemm=True, pipeline=True, transform_first=-1,
-               early_aggregate=True, sampler_priority=1, fuse_activation=True,
+               early_aggregate=True, sampler_priority=2, fuse_activation=True,
                fuse_loss=True, sampler_cus=0, sampler_gate=0, pad_features=True, cache_rate=-1.0,
                up_degree=False, gat=False, pd_cache=False, pd_rate=0.2, pd_super_batch=4,
                gemm="split3", overlap_allreduce=-1, pair_table=0, sample_gpu=False):

@@ -143,7 +143,8 @@ GCN_SAMPLE_ALLGPU_impl::GCN_SAMPLE_ALLGPU_impl(std::shared_ptr<FullyRepGraph> g,
                                      (uint64_t)cfg.seed);
   else if (cfg.pipeline)
     ss = std::make_unique<NtsStream>(graph->device, nullptr, (uint64_t)cfg.seed,
-                                     cfg.sampler_priority > 0);
+                                     cfg.sampler_priority == 1 ||
+                                         (cfg.sampler_priority == 2 && cfg.rng_mode != NTS_RNG_PHILOX));
   // size the scratch arenas once so the training loop never allocates
   uint64_t items = graph->global_vertices;
   for (auto* s : sampler->ssg->sampled_sgs) items = std::max<uint64_t>({items, s->e_cap, s->v_cap});

@@ -29,8 +29,11 @@ struct GCNConfig {
   bool fuse_loss = true;              // training: output layer + log_softmax x2 + nll in 2 kernels
   // pipelined sampler's stream priority: 1 = sampler stream high, 0 = both
   // normal, -1 = the training stream high (the sampler's blocks dispatched
-  // after the training stream's)
-  int sampler_priority = 1;
+  // after the training stream's), 2 = auto: high for the MT19937 stream (its
+  // chain is the step's critical path), normal for Philox (its ~0.2 ms of
+  // kernels a batch fit beside the training step: C2 0.819-0.823 vs
+  // 0.830-0.832 ms/step with the sampler high, scripts/ab/r06_u.sh)
+  int sampler_priority = 2;
   // CUs of the pipelined sampler's stream: n > 0 reserves n CUs for it (the
   // training stream on the rest), n < 0 confines it to |n| CUs and leaves the
   // training stream on all; 0: no CU masks
