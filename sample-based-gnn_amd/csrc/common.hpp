@@ -314,6 +314,7 @@ int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, c
           const float* B, uint64_t ldb, float* C, uint64_t ldc);
 bool x3_nn_ok(int M, int N, int K, const float* A, uint64_t lda);
 bool x3_nn7_ok(int M, int N, int K, const float* A, uint64_t lda);
+bool x3_nnk_ok(int M, int N, int K, const float* A, uint64_t lda);  // gemm3.hip: K <= 128, dense
 int x3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, uint64_t lda,
           const uint32_t* amap, const char* bimg, float* C, uint64_t ldc, uint32_t keep_threshold,
           float scale, uint64_t seed, uint64_t offset);

@@ -1106,8 +1106,15 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
   // The split kernels pay off on wide reductions / wide outputs (the C2
   // bottom layer, K = M = 602); narrow ones (products-shaped F = 100) run
   // faster on the fp32-input MFMA kernels (C3: 0.716 vs 0.740 ms/step).
+  // Round 6: short dense reductions (K <= 128) on k_x3_nnk, which keeps the
+  // whole W image in LDS.
+#ifndef NTS_NO_X3K  // (A/B build: -DNTS_NO_X3K keeps these on the fp32-input kernels)
+  const bool nnk = !trans_a && !BMASK && !ex.amap && x3_nnk_ok(M, N, K, A, lda);
+#else
+  const bool nnk = false;
+#endif
   if (ctx->gemm_mode == NTS_GEMM_SPLIT3_ALL ||
-      (ctx->gemm_mode == NTS_GEMM_SPLIT3 && (trans_a ? M : K) >= 256)) {
+      (ctx->gemm_mode == NTS_GEMM_SPLIT3 && ((trans_a ? M : K) >= 256 || nnk))) {
     if (!trans_a && !BMASK && gemm3_nn_ok(M, N, K, A, lda))
       return gemm3_nn(ctx, EPI, M, N, K, A, lda, ex.amap, B, ldb, C, ldc, ex.keep_threshold,
                       ex.scale, ex.seed, ex.offset);

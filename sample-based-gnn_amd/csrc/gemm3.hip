@@ -328,6 +328,146 @@ __global__ __launch_bounds__(kS3NnThreads, 1) void k_gemm3_nn(int M, int N, int 
 }
 
 // ---------------------------------------------------------------------------
+// NN for short reductions (K <= 128, dense rows: the aggregate-first bottom
+// layers of the products-shaped C3 / C4, Z = relu/dropout(Y W0) with Y
+// [~140 K x 100]).  k_gemm3_nn streams the W image step by step and pipelines
+// A through LDS over the k-loop; with <= 4 k-steps a round that is all
+// prologue (110 us for C3's layer, no faster than the fp32-input kernel).
+// Here each block keeps its column block's WHOLE image (nsteps x 24 KB) in
+// LDS for its lifetime and each wave loops over 32-row tiles (grid-strided),
+// A loaded straight to registers:
+// per k-step the two row tiles' fragments split in registers, 8 column tiles
+// x 6 MFMAs each (the pieces, products, k order and instruction of
+// k_gemm3_nn: bit-identical), relu/dropout in the epilogue.
+// two waves per SIMD (<= 256 registers each: no next-tile A in registers; the
+// other wave covers the loads) so one wave's epilogue VALU — the dropout
+// Philox rounds, as many cycles as the tile's MFMAs — overlaps the other's
+// MFMAs
+constexpr int kX3KThreads = 512;
+constexpr int kX3KSteps = 4;  // K <= 128
+
+// lane i and its neighbour i ^ 1 hold the two columns of one Philox column
+// pair (dropout_words keys (row / 4, col / 2)): each computes one of two
+// column tiles' words and takes the other's from its neighbour (DPP swap)
+__device__ __forceinline__ uint32_t x3k_swap(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+}
+
+template <bool EPI>
+__global__ __launch_bounds__(kX3KThreads, 1) void k_x3_nnk(int M, int N, int K,
+                                                          const float* __restrict__ A, uint64_t lda,
+                                                          const char* __restrict__ bimg,
+                                                          float* __restrict__ C, uint64_t ldc,
+                                                          Gemm3Extra ex) {
+  extern __shared__ __attribute__((aligned(16))) char x3k[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int cb = blockIdx.y, ncb = gridDim.y, n0 = cb * 128;
+  const int nsteps = (K + 31) / 32;
+  // the column block's image of every step: [s][ct][piece][lane], by LDS DMA
+  // (1 KB a wave instruction, no registers; inline asm, so the wait is ours)
+  {
+    const int wu = __builtin_amdgcn_readfirstlane(wv);
+    const uint32_t lds0 = lds_addr(x3k);
+    for (int c = wu; c < nsteps * (kS3Img / 1024); c += kX3KThreads / 64) {
+      const int o = c * 1024, s = o / kS3Img, r = o - s * kS3Img;
+      glds16(bimg + ((size_t)s * ncb + cb) * kS3Img + r + 16 * lane, lds0 + (uint32_t)o);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int T = (M + 31) / 32;
+  const int W = gridDim.x * (kX3KThreads / 64), gw = blockIdx.x * (kX3KThreads / 64) + wv;
+  // lane (i, g)'s fragments of a tile: rows 32 t + 16 rt + i, k = 32 s + 8 g + j
+  auto load = [&](int t, float (&x)[2][kX3KSteps][8]) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int64_t row = (int64_t)t * 32 + 16 * rt + i;
+      const float* pr = A + (uint64_t)(row < M ? row : M - 1) * lda;
+#pragma unroll
+      for (int s = 0; s < kX3KSteps; ++s) {
+        const int k0 = 32 * s + 8 * g;
+        if (k0 + 8 <= K) {
+          const float4 u = *reinterpret_cast<const float4*>(pr + k0);
+          const float4 v = *reinterpret_cast<const float4*>(pr + k0 + 4);
+          x[rt][s][0] = u.x; x[rt][s][1] = u.y; x[rt][s][2] = u.z; x[rt][s][3] = u.w;
+          x[rt][s][4] = v.x; x[rt][s][5] = v.y; x[rt][s][6] = v.z; x[rt][s][7] = v.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float val = pr[min(k0 + j, K - 1)];
+            x[rt][s][j] = k0 + j < K ? val : 0.f;
+          }
+        }
+      }
+    }
+  };
+  for (int t = gw; t < T; t += W) {
+    float cur[2][kX3KSteps][8];
+    load(t, cur);
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < 8; ++ct) acc[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < kX3KSteps; ++s) {
+      if (s < nsteps) {
+        bf16x8 a[2][3];
+        split3(cur[0][s], a[0][0], a[0][1], a[0][2]);
+        split3(cur[1][s], a[1][0], a[1][1], a[1][2]);
+        const char* img = x3k + s * kS3Img;
+#pragma unroll
+        for (int ct = 0; ct < 8; ++ct) {
+          bf16x8 b[3];
+          get3(img + ct * 3 * kS3Frag, kS3Frag, lane, b);
+          acc[0][ct] = mfma6(a[0], b, acc[0][ct]);
+          acc[1][ct] = mfma6(a[1], b, acc[1][ct]);
+        }
+      }
+    }
+    // epilogue: acc[rt][ct][v] = C[32 t + 16 rt + 4 g + v][n0 + 16 ct + i];
+    // per column-tile pair one Philox call a lane, shared with the neighbour
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      const int64_t r4 = (int64_t)t * 32 + 16 * rt + 4 * g;
+#pragma unroll
+      for (int cp = 0; cp < 4; ++cp) {
+        uint4 wd[2];
+        if constexpr (EPI) {
+          const int ctm = 2 * cp + (i & 1);  // the tile this lane's call serves
+          const uint4 w = dropout_words((uint64_t)r4, (uint32_t)(n0 + 16 * ctm + i), ex.seed, ex.offset);
+          const uint4 o = make_uint4(x3k_swap(w.x), x3k_swap(w.y), x3k_swap(w.z), x3k_swap(w.w));
+          wd[0] = (i & 1) ? o : w;
+          wd[1] = (i & 1) ? w : o;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ct = 2 * cp + h;
+          const uint32_t col = (uint32_t)(n0 + 16 * ct + i);
+          if ((int)col >= N) continue;
+          float o[4] = {acc[rt][ct][0], acc[rt][ct][1], acc[rt][ct][2], acc[rt][ct][3]};
+          if constexpr (EPI) {
+            const uint32_t wv4[4] = {wd[h].x, wd[h].y, wd[h].z, wd[h].w};
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              o[v] = (dropout_bits(wv4[v], col) >= ex.keep_threshold && o[v] > 0.f) ? o[v] * ex.scale : 0.f;
+          }
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (r4 + v < M) C[(uint64_t)(r4 + v) * ldc + col] = o[v];
+        }
+      }
+    }
+  }
+}
+
+bool x3_nnk_ok(int M, int N, int K, const float* A, uint64_t lda) {
+  return K >= 1 && K <= 32 * kX3KSteps && M >= 4096 && N >= 1 && lda >= (uint64_t)K && lda % 4 == 0 &&
+         (uintptr_t)A % 16 == 0;
+}
+
+// ---------------------------------------------------------------------------
 // TN: C[M x N] = A[K x M]^T op(B)[K x N].  Block = 8 waves, output tile 160
 // rows (10 row tiles) x 128 columns; wave (wm, wn) = (wv & 1, wv >> 1) owns
 // row tiles 5 wm .. 5 wm + 4 and column tiles 2 wn, 2 wn + 1 (40
@@ -757,6 +897,21 @@ int gemm3_nn(nts_hip_ctx* ctx, bool epi, int M, int N, int K, const float* A, ui
       (ctx->gemm_mode == NTS_GEMM_SPLIT3_ALL && x3_nn7_ok(M, N, K, A, lda)))
     return x3_nn(ctx, epi, M, N, K, A, lda, amap, bimg, C, ldc, keep_threshold, scale, seed, offset);
 #endif
+  if (!amap && x3_nnk_ok(M, N, K, A, lda)) {  // short reductions, dense rows
+    const int G = std::max(1, std::min(256 / ncb, ((M + 31) / 32 + 7) / 8));
+    const int lds = nsteps * kS3Img;
+#define NTS_X3K(E)                                                                                 \
+  do {                                                                                             \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_nnk<E>),                  \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));             \
+    hipLaunchKernelGGL((k_x3_nnk<E>), dim3(G, ncb), dim3(kX3KThreads), lds, ctx->stream, M, N, K, A, \
+                       lda, bimg, C, ldc, ex);                                                     \
+  } while (0)
+    if (epi) NTS_X3K(true); else NTS_X3K(false);
+#undef NTS_X3K
+    NTS_LAUNCH_CHECK();
+    return NTS_OK;
+  }
   // one 8-wave block per CU over all column blocks (row blocks a multiple of 8:
   // XCD pairing), no more blocks than 16-tile rounds
   const int T = (M + 15) / 16;

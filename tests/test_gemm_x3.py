@@ -168,3 +168,42 @@ def test_x3_nn7_relu_dropout_dense(ctxs, M, N, K, p):
     e32 = ((C32.double() - ref).abs() / (scale * s))[clear].max().item()
     e7 = ((C7.double() - ref).abs() / (scale * s))[clear].max().item()
     assert e7 <= 1.25 * e32 + 1e-7, (e7, e32)
+
+
+@pytest.mark.parametrize("M,N,K,pitch,p", [(140390, 256, 100, 100, 0.5), (20000, 128, 128, 128, 0.3),
+                                           (9000, 48, 37, 40, 0.0)])
+def test_x3_nnk_short_reduction(ctxs, M, N, K, pitch, p):
+    """k_x3_nnk (round 6: dense rows, K <= 128, the whole W image in LDS; the
+    default for C3 / C4's aggregate-first bottom layer): every row
+    bit-identical to k_gemm3_nn's on the same rows (its first 4,000, below
+    k_x3_nnk's 4,096-row floor: same pieces, products, k order and keep mask),
+    and within the split path's bound of an fp64 product."""
+    f32, s3 = ctxs
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    A = torch.empty(M, pitch, device=DEV)[:, :K]
+    A.copy_(torch.randn(M, K, device=DEV, generator=g))
+    B = torch.randn(K, N, device=DEV, generator=g)
+    seed, offset = 0x0DDB_1A5E_5BAD_5EED, 5
+    Ck = torch.full((M, N), float("nan"), device=DEV)
+    C32 = torch.empty(M, N, device=DEV)
+    s3.gemm_relu_dropout(A, B, Ck, p=p, seed=seed, offset=offset)
+    f32.gemm_relu_dropout(A, B, C32, p=p, seed=seed, offset=offset)
+    from nts import _abi
+    from nts.hip import HipContext
+    s3all = HipContext(0, seed=2000)
+    s3all.set_gemm_mode(_abi.NTS_GEMM_SPLIT3_ALL)
+    m = 4000
+    Cg = torch.empty(m, N, device=DEV)
+    s3all.gemm_relu_dropout(A[:m], B, Cg, p=p, seed=seed, offset=offset)
+    torch.cuda.synchronize()
+    assert not torch.isnan(Ck).any()
+    assert torch.equal(Ck[:m], Cg)
+    Z = A.double() @ B.double()
+    scale = A.double().abs() @ B.double().abs() + 1e-30
+    clear = Z.abs() > 1e-5 * scale
+    assert torch.equal((C32 != 0) & clear, (Ck != 0) & clear)
+    s = 1.0 / (1.0 - p)
+    ref = torch.where(C32 != 0, torch.relu(Z) * s, torch.zeros_like(Z))
+    e32 = ((C32.double() - ref).abs() / (scale * s))[clear].max().item()
+    ek = ((Ck.double() - ref).abs() / (scale * s))[clear].max().item()
+    assert ek <= 1.25 * e32 + 1e-7, (ek, e32)
