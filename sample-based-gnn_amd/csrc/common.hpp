@@ -309,9 +309,14 @@ int gemm3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda
              float bscale, float* C, uint64_t ldc);
 // the same arithmetic over whole gathered feature rows streamed into LDS
 // (gemmx3.hip): the transform-first bottom layer's GEMMs
-bool x3_tn_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb);
+bool x3_tn_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb,
+              const float* Xm = nullptr, uint64_t ldxm = 0);
+bool x3_tn_bm_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb,
+                 const float* Xm, uint64_t ldxm);
+// Xm != NULL: B = B ⊙ [Xm > 0] · bscale (dense rows, M <= 128)
 int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, const uint32_t* amap,
-          const float* B, uint64_t ldb, float* C, uint64_t ldc);
+          const float* B, uint64_t ldb, float* C, uint64_t ldc, const float* Xm = nullptr,
+          uint64_t ldxm = 0, float bscale = 1.f);
 bool x3_nn_ok(int M, int N, int K, const float* A, uint64_t lda);
 bool x3_nn7_ok(int M, int N, int K, const float* A, uint64_t lda);
 bool x3_nnk_ok(int M, int N, int K, const float* A, uint64_t lda);  // gemm3.hip: K <= 128, dense

@@ -143,12 +143,18 @@ __device__ __forceinline__ void x3_split2(float x0, float x1, uint32_t& p0, uint
 // between slots keeps that order: the wave issues its VALU and LDS work in
 // the shadow of its own MFMAs (in-order issue would otherwise run a tile's
 // twelve MFMAs, then its VALU, then its reads, none overlapping).
-template <int TPW, int PR, int DIAG = 0>
+// BM (round 6, dense rows): B = dH ⊙ [Xm > 0] · bscale — the relu/dropout
+// backward of an aggregate-first bottom layer (C3 / C4, M = 100) fused: the
+// Xm rows of each step ride beside dH's (one more DMA per wave, issued before
+// the X pieces, so the counted waits are unchanged) and mask it at the split.
+template <int TPW, int PR, int DIAG = 0, bool BM = false>
 __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const float* __restrict__ X,
                                                         uint64_t ldx, const uint32_t* __restrict__ amap,
                                                         const float* __restrict__ B, uint64_t ldb,
                                                         float* __restrict__ C, uint64_t ldc, int kchunk,
-                                                        uint64_t split_stride, int nnb) {
+                                                        uint64_t split_stride, int nnb,
+                                                        const float* __restrict__ Xm, uint64_t ldxm,
+                                                        float bscale) {
   static_assert(2 * PR <= 6, "X DMA pieces per wave and step");
   extern __shared__ __attribute__((aligned(16))) char x3tn[];
   const int Kp = (M + 31) / 32 * 32, RB = 4 * Kp, RW = Kp;  // LDS row: bytes, floats
@@ -156,7 +162,8 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
   char* const sx = x3tn;                         // [3][16][RB]
   char* const sbr = sx + 3 * xstage;             // [2][kX3BRaw]
   char* const sbp = sbr + 2 * kX3BRaw;           // [2][3][kX3BPl]
-  uint32_t* const sid = reinterpret_cast<uint32_t*>(sbp + 6 * kX3BPl);  // [16 (nsteps + 3)]
+  char* const sbm = sbp + 6 * kX3BPl;            // BM: [2][kX3BRaw] raw Xm rows
+  uint32_t* const sid = reinterpret_cast<uint32_t*>(sbm + (BM ? 2 * kX3BRaw : 0));  // [16 (nsteps + 3)]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nb = blockIdx.x % nnb, split = blockIdx.x / nnb;
@@ -169,7 +176,7 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
   for (int k = tid; k < 16 * (nsteps + 3); k += kX3Threads)
     sid[k] = amap ? amap[kbeg + min(k, klast)] : (uint32_t)(kbeg + min(k, klast));
   __syncthreads();
-  const uint32_t lsx = x3_lds(sx), lsbr = x3_lds(sbr);
+  const uint32_t lsx = x3_lds(sx), lsbr = x3_lds(sbr), lsbm = x3_lds(sbm);
 #ifdef NTS_X3_PRIO
   if (wv >= 4) __builtin_amdgcn_s_setprio(1);  // A/B: static priority for the younger half
 #endif
@@ -191,12 +198,22 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
     const int row = 2 * wv + (lane >> 5);
     const int k = kbeg + min(16 * s + row, klast);
     x3_glds16(B + (uint64_t)k * ldb + n0 + 4 * (lane & 31), lsbr + (s & 1) * kX3BRaw + 1024 * wv);
+    if constexpr (BM)
+      x3_glds16(Xm + (uint64_t)k * ldxm + n0 + 4 * (lane & 31), lsbm + (s & 1) * kX3BRaw + 1024 * wv);
   };
   // dH(s) raw -> three bf16 planes (buffer s & 1): row sr, columns sc .. sc+3
   const int sr = tid >> 5, sc = 4 * (tid & 31);
   const int soff = x3_tr_off(sr, sc / 8) + 8 * ((sc / 4) & 1);
   auto splitb_read = [&](int s) {
-    return *reinterpret_cast<const float4*>(sbr + (s & 1) * kX3BRaw + 512 * sr + 4 * sc);
+    float4 v = *reinterpret_cast<const float4*>(sbr + (s & 1) * kX3BRaw + 512 * sr + 4 * sc);
+    if constexpr (BM) {
+      const float4 m = *reinterpret_cast<const float4*>(sbm + (s & 1) * kX3BRaw + 512 * sr + 4 * sc);
+      v.x = m.x > 0.f ? v.x * bscale : 0.f;
+      v.y = m.y > 0.f ? v.y * bscale : 0.f;
+      v.z = m.z > 0.f ? v.z * bscale : 0.f;
+      v.w = m.w > 0.f ? v.w * bscale : 0.f;
+    }
+    return v;
   };
   auto splitb_write = [&](int s, float4 v) {
     const bool ok = 16 * s + sr <= klast;
@@ -281,8 +298,10 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
     };
 #pragma unroll
     for (int j = 0; j < 8; ++j) xr[0][j] = rd(0, j);
+    if constexpr (TPW > 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) xr[1][j] = rd(1, j);
+      for (int j = 0; j < 8; ++j) xr[1][j] = rd(1, j);
+    }
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) sp(0, jp);
     const uint2 idx = idn;  // X(s+2)'s rows
@@ -307,10 +326,13 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
         if (t + 2 < TPW && k < 8) xr[t & 1][k] = rd(t + 2, k);
         if (t + 1 < TPW && (k == 3 || k == 5 || k == 7 || k == 9)) sp(t + 1, (k - 3) / 2);
         if (t == 0 && (k & 1) && k / 2 < 2 * PR) issue_x1(s + 2, idx, k / 2);
-        if (t == 1 && k == 1) bv = splitb_read(s + 1);
-        if (t == 1 && k == 8) splitb_write(s + 1, bv);  // (past the last step: never read)
-        if (t == 2 && k == 1) idr = ids_read(s + 3);
-        if (t == 2 && k == 10) idn = ids_uni(idr);
+        // (fewer than three tiles: these slots move into tile 0 / 1)
+        constexpr int tB = TPW >= 2 ? 1 : 0, kBr = TPW >= 2 ? 1 : 5, kBw = TPW >= 2 ? 8 : 9;
+        constexpr int tI = TPW >= 3 ? 2 : 0, kIr = TPW >= 3 ? 1 : 6, kIw = TPW >= 3 ? 10 : 11;
+        if (t == tB && k == kBr) bv = splitb_read(s + 1);
+        if (t == tB && k == kBw) splitb_write(s + 1, bv);  // (past the last step: never read)
+        if (t == tI && k == kIr) idr = ids_read(s + 3);
+        if (t == tI && k == kIw) idn = ids_uni(idr);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -934,23 +956,27 @@ __global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K,
 
 // whole rows of at most 608 floats (Kp), 16-byte aligned, read as Kp floats
 // (so the table's row pitch must cover Kp); 128-column blocks
-bool x3_tn_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb) {
+bool x3_tn_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb,
+              const float* Xm, uint64_t ldxm) {
   const int Kp = (M + 31) / 32 * 32;
-  // the X stages, dH stages and planes leave room for >= 256 row ids (Kp <= 608)
-  const int lds = 3 * 16 * 4 * Kp + 2 * kX3BRaw + 6 * kX3BPl + 4 * 16 * 3 + 4 * 256;
+  // the X stages, dH stages (+ the mask rows) and planes leave room for >= 256
+  // row ids (Kp <= 608)
+  const int lds = 3 * 16 * 4 * Kp + 2 * kX3BRaw + 6 * kX3BPl + (Xm ? 2 * kX3BRaw : 0) + 4 * 16 * 3 +
+                  4 * 256;
   return M >= 32 && lds <= 160 * 1024 && N % 128 == 0 && K >= 256 && lda >= (uint64_t)Kp && lda % 4 == 0 &&
-         (uintptr_t)A % 16 == 0 && ldb % 4 == 0 && (uintptr_t)B % 16 == 0;
+         (uintptr_t)A % 16 == 0 && ldb % 4 == 0 && (uintptr_t)B % 16 == 0 &&
+         (!Xm || (ldxm % 4 == 0 && (uintptr_t)Xm % 16 == 0));
 }
 
 int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, const uint32_t* amap,
-          const float* B, uint64_t ldb, float* C, uint64_t ldc) {
-  constexpr int TPW = 5;  // ceil(20 tiles / 4)
+          const float* B, uint64_t ldb, float* C, uint64_t ldc, const float* Xm, uint64_t ldxm,
+          float bscale) {
   const int Kp = (M + 31) / 32 * 32, RB = 4 * Kp;
   const int nnb = N / 128;
   const int ksteps = (K + 15) / 16;
   int splits = std::max(1, std::min(256 / nnb, ksteps / 8));
   int kchunk = ((ksteps + splits - 1) / splits) * 16;
-  const int fixed = 3 * 16 * RB + 2 * kX3BRaw + 6 * kX3BPl + 4 * 16 * 3;
+  const int fixed = 3 * 16 * RB + 2 * kX3BRaw + 6 * kX3BPl + (Xm ? 2 * kX3BRaw : 0) + 4 * 16 * 3;
   kchunk = std::min(kchunk, (160 * 1024 - fixed) / 4 / 16 * 16);
   splits = (K + kchunk - 1) / kchunk;
   const int lds = fixed + 4 * kchunk;
@@ -963,44 +989,60 @@ int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, c
     ldo = N;
   }
   const int pr = (RB + 1023) / 1024;
-#define NTS_X3TN(P, D)                                                                           \
+  // tiles a wave: the 32-row tiles of M over 4 row groups (5 for C2's 602;
+  // 1 for C3 / C4's 100 — tiles past a wave's own repeat its last one, so a
+  // TPW above its count is pure waste)
+  const int tpw = ((M + 31) / 32 + 3) / 4;
+#define NTS_X3TN(T, P, D, BMK)                                                                   \
   do {                                                                                           \
-    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_tn<TPW, P, D>),          \
+    NTS_HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_x3_tn<T, P, D, BMK>),      \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds));           \
-    hipLaunchKernelGGL((k_x3_tn<TPW, P, D>), dim3(nnb * splits), dim3(kX3Threads), lds,          \
+    hipLaunchKernelGGL((k_x3_tn<T, P, D, BMK>), dim3(nnb * splits), dim3(kX3Threads), lds,      \
                        ctx->stream, M, K, A, lda, amap, B, ldb, out, ldo, kchunk,                \
-                       splits > 1 ? stride : (uint64_t)0, nnb);                                  \
+                       splits > 1 ? stride : (uint64_t)0, nnb, Xm, ldxm, bscale);                \
   } while (0)
 #ifdef NTS_PROBE_BUILD
   static const int diag = [] {
     const char* e = getenv("NTS_X3_DIAG");
     return e ? atoi(e) : 0;
   }();
-  if (pr == 3 && diag) {
+  if (pr == 3 && diag && !Xm) {
     switch (diag) {
-      case 1: NTS_X3TN(3, 1); break;
-      case 2: NTS_X3TN(3, 2); break;
-      case 4: NTS_X3TN(3, 4); break;
-      case 5: NTS_X3TN(3, 5); break;
-      case 6: NTS_X3TN(3, 6); break;
-      case 8: NTS_X3TN(3, 8); break;
-      case 10: NTS_X3TN(3, 10); break;
-      case 12: NTS_X3TN(3, 12); break;
-      case 14: NTS_X3TN(3, 14); break;
-      case 16: NTS_X3TN(3, 16); break;
-      case 32: NTS_X3TN(3, 32); break;
-      case 36: NTS_X3TN(3, 36); break;
-      default: NTS_X3TN(3, 15); break;
+      case 1: NTS_X3TN(5, 3, 1, false); break;
+      case 2: NTS_X3TN(5, 3, 2, false); break;
+      case 4: NTS_X3TN(5, 3, 4, false); break;
+      case 5: NTS_X3TN(5, 3, 5, false); break;
+      case 6: NTS_X3TN(5, 3, 6, false); break;
+      case 8: NTS_X3TN(5, 3, 8, false); break;
+      case 10: NTS_X3TN(5, 3, 10, false); break;
+      case 12: NTS_X3TN(5, 3, 12, false); break;
+      case 14: NTS_X3TN(5, 3, 14, false); break;
+      case 16: NTS_X3TN(5, 3, 16, false); break;
+      case 32: NTS_X3TN(5, 3, 32, false); break;
+      case 36: NTS_X3TN(5, 3, 36, false); break;
+      default: NTS_X3TN(5, 3, 15, false); break;
     }
   } else
 #endif
-  if (pr == 1) NTS_X3TN(1, 0);
-  else if (pr == 2) NTS_X3TN(2, 0);
-  else NTS_X3TN(3, 0);
+  // (the one-tile form only for the masked A/B path: the product keeps TPW 5
+  // for every unmasked shape, see gemm.hip NTS_X3_TN_BM)
+  if (Xm && tpw <= 1 && pr == 1) {
+    NTS_X3TN(1, 1, 0, true);
+  } else if (Xm) {
+    return NTS_ERR_INVALID;  // (x3_tn_bm_ok keeps masked calls to one-tile shapes)
+  } else if (pr == 1) NTS_X3TN(5, 1, 0, false);
+  else if (pr == 2) NTS_X3TN(5, 2, 0, false);
+  else NTS_X3TN(5, 3, 0, false);
 #undef NTS_X3TN
   NTS_LAUNCH_CHECK();
   if (splits == 1) return NTS_OK;
   return sum_splits(ctx->stream, out, splits, stride, M, N, C, ldc);
+}
+
+// the masked (BM) form is instantiated for one-tile shapes only: M <= 128
+bool x3_tn_bm_ok(int M, int N, int K, const float* A, uint64_t lda, const float* B, uint64_t ldb,
+                 const float* Xm, uint64_t ldxm) {
+  return M <= 128 && x3_tn_ok(M, N, K, A, lda, B, ldb, Xm, ldxm);
 }
 
 // NN over gathered rows (or dense, amap null): rows read as Kp = 32 ceil(K /
