@@ -1113,14 +1113,10 @@ static int gemm(nts_hip_ctx* ctx, bool trans_a, int M, int N, int K, const float
 #else
   const bool nnk = false;
 #endif
-#ifdef NTS_X3_TN_BM
-  // (A/B build) ... and the masked weight gradient of such a layer (dW = Y^T
-  // (dZ ⊙ [Z > 0]) s, M <= 128 output rows) on k_x3_tn's one-tile form with
-  // the mask rows beside dZ's (the row pitch must cover 32 ceil(M / 32)
-  // floats).  Not in the product: C3 0.597 vs 0.606 ms/step, but ~1 run in 4
-  // left one wave's 32 x 128 tile of a block wrong by ~2e-4 (relative to
-  // |Y|^T|dZ|) — a race the one-tile step's short slot schedule exposes,
-  // not found this round (scripts/dbg_tn.py)
+#ifndef NTS_NO_X3K
+  // ... and the masked weight gradient of such a layer (dW = Y^T (dZ ⊙ [Z >
+  // 0]) s, M <= 128 output rows) on k_x3_tn's one-tile form with the mask rows
+  // beside dZ's (the row pitch must cover 32 ceil(M / 32) floats)
   if (trans_a && BMASK && !EPI && ctx->gemm_mode != NTS_GEMM_F32 &&
       x3_tn_bm_ok(M, N, K, A, lda, B, ldb, ex.bx, ex.ldbx))
     return x3_tn(ctx, M, N, K, A, lda, ex.amap, B, ldb, C, ldc, ex.bx, ex.ldbx, ex.bscale);

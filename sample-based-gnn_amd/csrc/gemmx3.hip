@@ -266,8 +266,18 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_tn(int M, int K, const flo
   }
   uint2 idn = ids_uni(ids_read(2));
   for (int s = 0; s < nsteps; ++s) {
+    // every DMA of this wave drained (vmcnt(0)), not just the ones this step
+    // reads (vmcnt(2 PR), which leaves X(s+1)'s pieces in flight): with the
+    // counted wait the one-tile form (its dH split 5 slots after the wait)
+    // read a stale step about one run in four — 6 of 23 vs 0 of 23 drained
+    // (scripts/dbg_tn.py) — so the count is not safe to rely on; C2 pays
+    // nothing for the drain (0.828-0.831 vs 0.829-0.832 ms/step, r06_y.sh)
+#ifdef NTS_X3TN_COUNTED  // (A/B build: the counted wait)
     if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (!(DIAG & 16)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PR) : "memory");
+#else
+    if constexpr (!(DIAG & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     x3_barrier();
     issue_b(s + 2);
     const char* pl = sbp + (s & 1) * 3 * kX3BPl;
@@ -1024,8 +1034,7 @@ int x3_tn(nts_hip_ctx* ctx, int M, int N, int K, const float* A, uint64_t lda, c
     }
   } else
 #endif
-  // (the one-tile form only for the masked A/B path: the product keeps TPW 5
-  // for every unmasked shape, see gemm.hip NTS_X3_TN_BM)
+  // (the one-tile form for the masked short shapes; unmasked shapes keep TPW 5)
   if (Xm && tpw <= 1 && pr == 1) {
     NTS_X3TN(1, 1, 0, true);
   } else if (Xm) {

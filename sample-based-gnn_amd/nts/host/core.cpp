@@ -731,7 +731,8 @@ NtsVar row_major(const NtsVar& x) {
 // bottom aggregation output: aligned row writes, 16-byte A loads in the
 // GEMMs that consume it).
 NtsVar row_padded_empty(int64_t rows, int64_t F, int device) {
-  const int64_t ld = F >= 256 ? (F + 31) / 32 * 32 : F;
+  // (F >= 64: whole 32-float k-steps for k_x3_tn's row reads, C3 / C4's F = 100)
+  const int64_t ld = F >= 64 ? (F + 31) / 32 * 32 : F;
   if (ld == F) return torch::empty({rows, F}, f32_opts(device));
   return torch::empty_strided({rows, F}, {ld, 1}, f32_opts(device));
 }

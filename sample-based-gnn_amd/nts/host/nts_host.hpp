@@ -422,7 +422,7 @@ NtsVar hip_linear_xent(const NtsVar& y, const NtsVar& W, const NtsVar& target, N
                        uint32_t* correct = nullptr);
 // row-major fp32 views the HIP GEMMs take without a copy (unit column stride)
 NtsVar row_major(const NtsVar& x);
-// [rows, F] with 128-byte aligned rows when F >= 256 (padded leading dimension)
+// [rows, F] with 128-byte aligned rows when F >= 64 (padded leading dimension)
 NtsVar row_padded_empty(int64_t rows, int64_t F, int device);
 // dropout(relu(x W), p) in one MFMA GEMM (activation in the epilogue, Philox
 // mask of (seed, offset)); autograd: dW = x^T (dX ⊙ [X > 0] / (1-p)) fused.

@@ -207,3 +207,36 @@ def test_x3_nnk_short_reduction(ctxs, M, N, K, pitch, p):
     e32 = ((C32.double() - ref).abs() / (scale * s))[clear].max().item()
     ek = ((Ck.double() - ref).abs() / (scale * s))[clear].max().item()
     assert ek <= 1.25 * e32 + 1e-7, (ek, e32)
+
+
+@pytest.mark.parametrize("K,M,N,pitch", [(140390, 100, 256, 128), (30000, 64, 128, 64),
+                                         (5000, 100, 128, 104)])
+def test_x3_tn_masked_short(ctxs, K, M, N, pitch):
+    """k_x3_tn's masked one-tile form (round 6: dW = Y^T (dZ ⊙ [Z > 0]) s for
+    C3 / C4's aggregate-first bottom layer, M <= 128 feature rows, dense Y
+    rows whose pitch covers 32 ceil(M / 32) floats — the last case's 104 does
+    not and stays on the fp32-input kernel; NaN pad columns only reach output
+    rows >= M, never stored): within the split path's bound of an fp64
+    product, three runs each (its counted step wait once left a stale step
+    about one run in four; the drained wait must not)."""
+    f32, s3 = ctxs
+    g = torch.Generator(device=DEV).manual_seed(K + M)
+    Y = torch.full((K, pitch), float("nan"), device=DEV)[:, :M]
+    Y.copy_(torch.randn(K, M, device=DEV, generator=g))
+    G = torch.randn(K, N, device=DEV, generator=g)
+    Z = torch.relu(torch.randn(K, N, device=DEV, generator=g))
+    s = 2.0
+    C32 = torch.empty(M, N, device=DEV)
+    f32.gemm_tn_masked(Y, G, Z, C32, scale=s)
+    Gm = torch.where(Z > 0, G.double() * s, torch.zeros_like(G, dtype=torch.float64))
+    ref = Y.double().T @ Gm
+    scale = Y.double().abs().T @ Gm.abs() + 1e-30
+    torch.cuda.synchronize()
+    e32 = ((C32.double() - ref).abs() / scale).max().item()
+    for _ in range(3):
+        C3 = torch.full((M, N), float("nan"), device=DEV)
+        s3.gemm_tn_masked(Y, G, Z, C3, scale=s)
+        torch.cuda.synchronize()
+        assert not torch.isnan(C3).any()
+        e3 = ((C3.double() - ref).abs() / scale).max().item()
+        assert e3 <= 1.25 * e32 + 1e-7, (e3, e32)
