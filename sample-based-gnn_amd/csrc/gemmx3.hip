@@ -852,7 +852,11 @@ __global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K,
       float x[8];
       if constexpr (rt + 1 == RT) {  // W(g+1) landed (own pieces), then the block's
 #ifndef NTS_X3N7_WREG
+#ifdef NTS_X3N7_WAIT0  // (A/B build: drain every load at the W wait)
+        if constexpr (!(DIAG & 16)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
         if constexpr (!(DIAG & 16)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kX3N7WWait) : "memory");
+#endif
 #else
         if constexpr (!(DIAG & 16)) x3_sfor<0, 6>([&](auto pc) { store_w(wb1, pc); });
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's W(g+1) stores
