@@ -269,8 +269,12 @@ __global__ __launch_bounds__(kS3NnThreads, 1) void k_gemm3_nn(int M, int N, int 
     if (nfull > 1) issue_a(1);
     for (int s = 0; s < nsteps; ++s) {
       // B(s) and A(s) landed (A(s+1), issued after B(s), may stay in flight)
+#ifdef NTS_S3NN_COUNTED  // (A/B build: the counted wait)
       if (s + 1 < nfull) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else  // drained: the LDS-DMA loads need not retire in issue order (k_x3_tn, round 6)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
       if (!(ex.diag & 4)) raw_barrier();
       if (s + 1 < nsteps) issue_b(s + 1);
       if (s + 2 < nfull) issue_a(s + 2);

@@ -484,13 +484,14 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     constexpr int P = decltype(par)::value, NT = decltype(ntc)::value;
     if (s > 0) {
       // B(s) landed (A(s) was waited for in step s-1; A(s+1)'s 4 pieces may stay in flight)
-      if (s + 1 < nsteps && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // (drained, not counted: k_x3_tn showed the LDS-DMA loads need not
+      // retire in issue order; this kernel serves the gathered NN below
+      // k_x3_nn7's 32,768 rows, where the drain costs little)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       x3_barrier();
       if (s + 1 < nsteps) issue_b(s + 1);
       if (s + 2 < nsteps) issue_a(s + 2);
     }
-    const bool nxt2 = s + 2 < nsteps;
     const char* img = sb + (s & 1) * kX3NnImg;
     auto getb = [&](int ct, int p) {
       if constexpr (DIAG & 8) return x3bf8{};
@@ -523,11 +524,7 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
         if (ct + 1 < 8 && (k == 0 || k == 2 || k == 4)) bf[(ct + 1) & 1][k / 2] = getb(ct + 1, k / 2);
         // (unconditional: past the round's last step this reads and splits a
         // stale stage nobody uses, cheaper than branching every slot)
-        if (ct == 4 && k == 0) {
-          if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          else if (nxt2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        }
+        if (ct == 4 && k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A(s+1) (drained)
         if (ct == 4 && k == 1) read_a(s + 1, 0);
         if constexpr (NT == 2) {
           if (ct == 4 && k == 3) read_a(s + 1, 1);
@@ -545,9 +542,8 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_x3_nn(int M, int N, int K, co
     issue_b(0);
     issue_a(0);
     if (nsteps > 1) issue_a(1);
-    // B(0) and A(0) landed (the 4 pieces of A(1) may stay in flight)
-    if (nsteps > 1 && !(DIAG & 4)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // B(0) and A(0) landed (drained)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     x3_barrier();
     if (nsteps > 1) issue_b(1);
     if (nsteps > 2) issue_a(2);
