@@ -699,6 +699,14 @@ __device__ __forceinline__ void x3_split_op(const float (&x)[8], float (&r)[8], 
   }
 }
 
+// The W image reaches LDS through registers (normal loads, whose waits hipcc
+// counts exactly) — not by LDS DMA with a hand-counted wait: k_x3_tn showed
+// the DMA counter need not retire in issue order, and the DMA form's counted
+// W wait once left a C2-size product not bit-identical to k_gemm3_nn's (round
+// 6, r06final).  -DNTS_X3N7_WDMA keeps the DMA form for A/B.
+#ifndef NTS_X3N7_WDMA
+#define NTS_X3N7_WREG 1
+#endif
 // B fragments read this many column tiles ahead (NTS_X3N7_BQ: 1 or 2)
 #ifndef NTS_X3N7_BQ
 #define NTS_X3N7_BQ 1
@@ -743,7 +751,7 @@ __global__ __launch_bounds__(kX3N7Threads, 1) void k_x3_nn7(int M, int N, int K,
   for (int rt = 0; rt < RT; ++rt) ptr[rt] = X + (uint64_t)row_id(0, rt) * ldx + 8 * q;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) nid[rt] = row_id(1, rt);
-#ifndef NTS_X3N7_WREG  // (A/B build -DNTS_X3N7_WREG: the W image staged through registers)
+#ifndef NTS_X3N7_WREG  // (A/B build -DNTS_X3N7_WDMA: the W image by LDS DMA)
   auto issue_w = [&](int s, int buf, int piece) {  // piece of W(k-step s) into buffer buf
     x3_glds16(bsrc + (size_t)s * bstride + 1024 * piece, lsw + buf * kX3NnImg + 1024 * piece);
   };
