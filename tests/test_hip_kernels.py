@@ -1186,3 +1186,27 @@ def test_capacity_overflow_flag_survives_multi_tile_scan(hip, rng_mode):
         hip.sample_layer(g, lay, 10, 0, rep, rng_mode, 0)
         torch.cuda.synchronize()
         assert lay.sizes_host()[3] == 0
+
+
+@pytest.mark.parametrize("V", [1500, 100_000, 400_000, 600_000])
+def test_csr_transpose_bucket_geometries(hip, V):
+    """The CSR transpose (round 6: one radix pass on the high H source bits +
+    k_csr_bucket per 2^L sources) at every bucket geometry — 11-bit source
+    ids (H = 5, L = 6), 17 (9, 8), 19 (9, 10: 1,024-row buckets) and 20 bits
+    (past the bucket form: the two-pass sort + k_csr_finalize) — on a graph
+    with a hub source every dst links to (one CSR row spread over every wave
+    of its bucket): all arrays bit-exact vs the oracle's serial fill."""
+    src, dst = _random_graph(V, 8 * V, V)[1:]
+    hub = np.arange(1, V, dtype=np.uint32)
+    src = np.concatenate([src, np.zeros(V - 1, np.uint32)])
+    dst = np.concatenate([dst, hub])
+    g = _graph(hip, V, src, dst)
+    col, rows = orc.build_csc(V, src, dst)
+    out_d, in_d = orc.degrees(V, src, dst)
+    seeds = np.random.default_rng(V).choice(V, V // 10, replace=False).astype(np.uint32)
+    o = orc.Sampler(col, rows, in_d, out_d, [10], seed=2000, rng_mode=orc.RNG_PHILOX,
+                    order_mode=orc.ORDER_DRAW)
+    gl = [_gpu_layer_np(l) for l in _sample_gpu(hip, g, seeds, [10], 0, 1, 1)]
+    ol = o.sample(seeds, 1, 1)
+    assert ol[0]["src_size"] > 100
+    _assert_layers_equal(gl, ol)
