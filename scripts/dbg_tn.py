@@ -1,5 +1,8 @@
-"""Repro of the masked one-tile k_x3_tn race (NTS_X3_TN_BM builds via NTS_HIP_LIB):
-the masked weight gradient at C3's shape against fp64, repeated."""
+"""Repro of the masked one-tile k_x3_tn race: the masked weight gradient at
+C3's shape against fp64, repeated (argv[1] times).  The product drains each
+step's DMA wait; `make variant V=cnt VFLAGS=-DNTS_X3TN_COUNTED` and
+NTS_HIP_LIB=scripts/probe/lib_cnt/libnts_hip.so bring back the counted wait
+that read a stale step ~1 run in 4."""
 import sys, torch
 sys.path.insert(0, "sample-based-gnn_amd")
 from nts import _abi
